@@ -1,0 +1,57 @@
+"""Build libasr.so (the HIP/gfx950 hot path + C ABI) in-tree with hipcc.
+
+The shared library is written next to this file so it travels with the
+repository snapshot to the GPU box; nothing is installed anywhere.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libasr.so")
+SOURCES = ["asr_theta.hip", "asr_conv_mfma.hip", "asr_conv_f32.hip", "asr_api.hip"]
+HEADERS = ["asr_common.h", os.path.join("..", "..", "include", "asr.h")]
+ARCH = "gfx950"
+
+
+def hipcc() -> str:
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the HIP toolchain (ROCm) is required to build libasr.so")
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile every HIP source for gfx950 into one shared library."""
+    if not force and not _stale():
+        return LIB
+    objs = []
+    cc = hipcc()
+    flags = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-unused-function",
+             "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
+    tmp = LIB + ".tmp"
+    cmd = [cc] + flags + ["-shared", "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError("hipcc failed building libasr.so:\n" + res.stdout + res.stderr)
+    os.replace(tmp, LIB)
+    del objs
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

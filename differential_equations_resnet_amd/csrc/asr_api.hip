@@ -1,0 +1,517 @@
+// C ABI entry points (include/asr.h): conv forward/backward dispatch and the
+// native single-block-network executor (stem, L Euler blocks, head, loss,
+// backward, Adam).
+//
+// Reference call stack replaced: Training.train's
+// sess.run(train_step) (training/training.py:578-597) over the graph built by
+// get_single_block_resnet_build_function (models/tfkeras_resnets.py:547-602)
+// and Training._build_optimizer (training/training.py:283-304).
+#include <math.h>
+
+#include <vector>
+
+#include "asr_common.h"
+
+namespace asr {
+// asr_theta.hip
+long theta_count(int C, int kind, int antisymmetric);
+int param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta_dst);
+int reduce_and_project(const float* slabs, int P, long E, const float* db_slabs, int PB, int Cb,
+                       const int32_t* theta_dst, long n_theta, float* dtheta, float* dbias, float* dw_out, float* ws,
+                       hipStream_t s);
+size_t reduce_ws_bytes(int P, long E);
+// asr_conv_mfma.hip
+bool mfma_supported(int C, int W);
+int conv_mfma(int mode, const void* xin, void* out, uint64_t* mask, const void* w, const float* bias, float h,
+              float two_gamma, int N, int H, int W, int C, hipStream_t s);
+int wgrad_mfma(int mode, const void* x, const void* dy, const uint64_t* mask, float h, int N, int H, int W, int C,
+               float* slabs, float* db_slabs, int* nslabs, hipStream_t s);
+// asr_conv_f32.hip
+int conv_f32(int fmode, const void* xin, void* out, uint64_t* mask, const float* w, const float* bias, float h,
+             float two_gamma, const float* dy, int N, int H, int W, int Ci, int Co, int out_bf16, hipStream_t s);
+int make_dz(int fmode, const void* dy, const uint64_t* mask, const void* relu_src, float h, int N, int H, int W, int C,
+            int src_bf16, float* dz, hipStream_t s);
+int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, int Ci, int Co, float* slabs,
+              float* db_slabs, int* nslabs, hipStream_t s);
+int wgrad_f32_chunks(int N, int H);
+
+constexpr int kMaxSlabsApi = 512;  // matches asr_conv_mfma.hip kMaxSlabs
+enum { F_EULER = 0, F_CONV = 1, F_RELU = 2, B_EULER = 3, B_CONV = 4 };
+
+static int check_shape(int N, int H, int W, int C) {
+  if (N < 1 || H < 1 || W < 1 || C < 1) return fail(ASR_E_ARG, "bad shape N=%d H=%d W=%d C=%d", N, H, W, C);
+  if ((long)N * H * W * C > (1L << 40)) return fail(ASR_E_ARG, "shape too large");
+  return ASR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// conv backward workspace
+// ---------------------------------------------------------------------------
+struct BwdWs {
+  size_t dz, slabs, db, red, total;
+};
+
+static BwdWs bwd_ws_layout(int N, int H, int W, int C, int dtype) {
+  BwdWs b{};
+  const long E = 9L * C * C;
+  const long P = (long)N * H * W * C;
+  const int nsl = kMaxSlabsApi;
+  size_t off = 0;
+  b.dz = off;
+  if (dtype == ASR_F32) off += align_up((size_t)P * 4, 256);
+  b.slabs = off;
+  off += align_up((size_t)nsl * E * 4, 256);
+  b.db = off;
+  off += align_up((size_t)nsl * C * 4, 256);
+  b.red = off;
+  off += align_up(reduce_ws_bytes(nsl, E), 256);
+  b.total = off;
+  return b;
+}
+
+static int conv_backward_impl(int mode, const void* dy, const void* x, const uint64_t* mask, const void* w,
+                              const int32_t* theta_dst, long n_theta, float h, float gamma, int N, int H, int W,
+                              int C, int dtype, void* dx, float* dtheta, float* dbias, float* dw_hwio, void* ws,
+                              hipStream_t s) {
+  const BwdWs L = bwd_ws_layout(N, H, W, C, dtype);
+  unsigned char* base = (unsigned char*)ws;
+  float* slabs = (float*)(base + L.slabs);
+  float* dbs = (float*)(base + L.db);
+  float* red = (float*)(base + L.red);
+  const bool need_w = dtheta || dbias || dw_hwio;
+  const int cm = (mode == ASR_MODE_EULER) ? 2 : 3;  // BWD_EULER / BWD_CONV
+  int nsl = 0;
+  if (dtype == ASR_BF16) {
+    if (dx) ASR_TRY(conv_mfma(cm, dy, dx, (uint64_t*)mask, w, nullptr, h, 2.f * gamma, N, H, W, C, s));
+    if (need_w) ASR_TRY(wgrad_mfma(cm, x, dy, mask, h, N, H, W, C, slabs, dbs, &nsl, s));
+  } else {
+    float* dz = (float*)(base + L.dz);
+    ASR_TRY(make_dz(mode == ASR_MODE_EULER ? F_EULER : F_CONV, dy, mask, nullptr, h, N, H, W, C, 0, dz, s));
+    if (dx)
+      ASR_TRY(conv_f32(mode == ASR_MODE_EULER ? B_EULER : B_CONV, dz, dx, nullptr, (const float*)w, nullptr, h,
+                       2.f * gamma, (const float*)dy, N, H, W, C, C, 0, s));
+    if (need_w) ASR_TRY(wgrad_f32(x, 0, dz, N, H, W, C, C, slabs, dbs, &nsl, s));
+  }
+  if (need_w)
+    ASR_TRY(reduce_and_project(slabs, nsl, 9L * C * C, dbs, nsl, C, dtheta ? theta_dst : nullptr, n_theta, dtheta,
+                               dbias, dw_hwio, red, s));
+  return ASR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// stem / head / optimizer kernels
+// ---------------------------------------------------------------------------
+template <typename Tin>
+__global__ void k_normalize(const Tin* __restrict__ img, long n, float mean, float inv_std, int use_norm,
+                            float* __restrict__ out) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float v = (float)img[i];
+    if (use_norm) v = (v - mean) * inv_std;
+    out[i] = v;
+  }
+}
+
+// GAP -> Dense(K) -> softmax [-> Keras CE loss and its gradient] per image.
+// models/tfkeras_resnets.py:595-597; loss training.py:295 (TF 1.12
+// keras.backend.categorical_crossentropy: renormalise, clip [1e-7, 1-1e-7],
+// -sum t*log q; clip gradient passes on the closed interval).
+template <typename T>
+__global__ __launch_bounds__(256) void k_head(const T* __restrict__ xL, const float* __restrict__ fck,
+                                              const float* __restrict__ fcb, const float* __restrict__ targets,
+                                              int HW, int C, int K, float inv_n, float* __restrict__ probs,
+                                              float* __restrict__ loss_per, float* __restrict__ dlogits,
+                                              float* __restrict__ gap, T* __restrict__ dxL) {
+  __shared__ float red[256];
+  __shared__ float gs[256];
+  __shared__ float lg[256];
+  __shared__ float dl[256];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const int PL = C <= 256 ? max(1, 256 / C) : 1;
+  float s = 0.f;
+  if (tid < PL * C) {
+    const int c = tid % C, pl = tid / C;
+    const T* base = xL + (long)n * HW * C;
+    for (int p = pl; p < HW; p += PL) s += to_f32(base[(long)p * C + c]);
+  }
+  red[tid] = s;
+  __syncthreads();
+  if (tid < C) {
+    float t = 0.f;
+    for (int pl = 0; pl < PL; ++pl) t += red[pl * C + tid];
+    t /= (float)HW;
+    gs[tid] = t;
+    if (gap) gap[(long)n * C + tid] = t;
+  }
+  __syncthreads();
+  if (tid < K) {
+    float a = fcb ? fcb[tid] : 0.f;
+    for (int c = 0; c < C; ++c) a = fmaf(gs[c], fck[(long)c * K + tid], a);
+    lg[tid] = a;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float m = -INFINITY;
+    for (int k = 0; k < K; ++k) m = fmaxf(m, lg[k]);
+    float S = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float e = expf(lg[k] - m);
+      lg[k] = e;
+      S += e;
+    }
+    float s2 = 0.f;
+    for (int k = 0; k < K; ++k) {
+      lg[k] /= S;  // probabilities
+      s2 += lg[k];
+      if (probs) probs[(long)n * K + k] = lg[k];
+    }
+    if (targets) {
+      const float eps = 1e-7f;
+      float loss = 0.f, sdq_p = 0.f;
+      for (int k = 0; k < K; ++k) {
+        const float q = lg[k] / s2;
+        const float qc = fminf(fmaxf(q, eps), 1.f - eps);
+        const float t = targets[(long)n * K + k];
+        loss -= t * logf(qc);
+        const float dq = (q >= eps && q <= 1.f - eps) ? -t / qc * inv_n : 0.f;
+        dl[k] = dq;
+        sdq_p += dq * lg[k];
+      }
+      if (loss_per) loss_per[n] = loss;
+      float sp_dp = 0.f;
+      for (int k = 0; k < K; ++k) {
+        const float dp = dl[k] / s2 - sdq_p / (s2 * s2);
+        dl[k] = dp;
+        sp_dp += lg[k] * dp;
+      }
+      for (int k = 0; k < K; ++k) {
+        const float d = lg[k] * (dl[k] - sp_dp);
+        dl[k] = d;
+        if (dlogits) dlogits[(long)n * K + k] = d;
+      }
+    }
+  }
+  __syncthreads();
+  if (targets && dxL) {
+    if (tid < C) {
+      float a = 0.f;
+      for (int k = 0; k < K; ++k) a = fmaf(dl[k], fck[(long)tid * K + k], a);
+      gs[tid] = a / (float)HW;
+    }
+    __syncthreads();
+    T* o = dxL + (long)n * HW * C;
+    for (long i = tid; i < (long)HW * C; i += 256) o[i] = from_f32<T>(gs[i % C]);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_head_param_grads(const float* __restrict__ gap,
+                                                          const float* __restrict__ dlogits, int N, int C, int K,
+                                                          float* __restrict__ dfck, float* __restrict__ dfcb,
+                                                          const float* __restrict__ loss_per,
+                                                          float* __restrict__ loss_out) {
+  __shared__ float red[256];
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < C * K + K; idx += 256) {
+    float a = 0.f;
+    if (idx < C * K) {
+      const int c = idx / K, k = idx % K;
+      for (int n = 0; n < N; ++n) a = fmaf(gap[(long)n * C + c], dlogits[(long)n * K + k], a);
+      dfck[idx] = a;
+    } else {
+      const int k = idx - C * K;
+      for (int n = 0; n < N; ++n) a += dlogits[(long)n * K + k];
+      dfcb[k] = a;
+    }
+  }
+  float s = 0.f;
+  for (int n = tid; n < N; n += 256) s += loss_per[n];
+  red[tid] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (tid < w) red[tid] += red[tid + w];
+    __syncthreads();
+  }
+  if (tid == 0) *loss_out = red[0] / (float)N;
+}
+
+__global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                       float* __restrict__ v, long n, float lr_t, float b1, float b2, float eps, float gscale) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float gi = g[i] * gscale;
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] -= lr_t * mi / (sqrtf(vi) + eps);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// network layout
+// ---------------------------------------------------------------------------
+struct NetLayout {
+  long ntheta, P, E, wstride;  // wstride in elements of the W dtype
+  long off_c1k, off_c1b, off_blk, blk_stride, off_fck, off_fcb, nparams;
+  size_t w_src, theta_dst, wbuf, x0, acts, masks, dxa, dxb, dz, slabs, dbs, red, probs, loss_per, dlogits, gap, loss,
+      total;
+  long mask_words;
+  int act_bytes;
+};
+
+static int net_check(const asr_net_config* c) {
+  if (!c) return fail(ASR_E_ARG, "null config");
+  ASR_TRY(check_shape(c->N, c->H, c->W, c->C));
+  if (c->L < 1 || c->Cin < 1 || c->num_classes < 1 || c->num_classes > 256 || c->C > 256)
+    return fail(ASR_E_ARG, "bad net config (L=%d Cin=%d K=%d C=%d)", c->L, c->Cin, c->num_classes, c->C);
+  if (c->dtype != ASR_F32 && c->dtype != ASR_BF16) return fail(ASR_E_ARG, "bad dtype");
+  if (c->dtype == ASR_BF16 && !mfma_supported(c->C, c->W))
+    return fail(ASR_E_UNSUPPORTED, "bf16 network needs C in {16,32,64} and W == 32 (C=%d W=%d)", c->C, c->W);
+  return ASR_OK;
+}
+
+static NetLayout net_layout(const asr_net_config* c) {
+  NetLayout L{};
+  const int C = c->C, K = c->num_classes;
+  L.ntheta = theta_count(C, ASR_PARAM_3BY3, 1);
+  L.P = (long)c->N * c->H * c->W * C;
+  L.E = 9L * C * C;
+  L.act_bytes = c->dtype == ASR_BF16 ? 2 : 4;
+  L.wstride = c->dtype == ASR_BF16 ? (long)(C / 16) * ((9 * C + 31) / 32) * 512 : L.E;
+  L.off_c1k = 0;
+  L.off_c1b = 9L * c->Cin * C;
+  L.off_blk = L.off_c1b + C;
+  L.blk_stride = L.ntheta + C;
+  L.off_fck = L.off_blk + (long)c->L * L.blk_stride;
+  L.off_fcb = L.off_fck + (long)C * K;
+  L.nparams = L.off_fcb + K;
+  L.mask_words = (long)c->N * c->H * ((c->W + 15) / 16) * ((C + 15) / 16) * 4;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += align_up(bytes, 256);
+    return o;
+  };
+  L.w_src = take((size_t)L.E * 4);
+  L.theta_dst = take((size_t)L.ntheta * 2 * 4);
+  L.wbuf = take((size_t)c->L * L.wstride * L.act_bytes);
+  L.x0 = take((size_t)c->N * c->H * c->W * c->Cin * 4);
+  L.acts = take((size_t)(c->L + 1) * L.P * L.act_bytes);
+  L.masks = take((size_t)c->L * L.mask_words * 8);
+  L.dxa = take((size_t)L.P * L.act_bytes);
+  L.dxb = take((size_t)L.P * L.act_bytes);
+  L.dz = take((size_t)L.P * 4);
+  const long Emax = std::max(L.E, 9L * c->Cin * C);
+  L.slabs = take((size_t)kMaxSlabsApi * Emax * 4);
+  L.dbs = take((size_t)kMaxSlabsApi * C * 4);
+  L.red = take(reduce_ws_bytes(kMaxSlabsApi, Emax));
+  L.probs = take((size_t)c->N * K * 4);
+  L.loss_per = take((size_t)c->N * 4);
+  L.dlogits = take((size_t)c->N * K * 4);
+  L.gap = take((size_t)c->N * C * 4);
+  L.loss = take(4);
+  L.total = off;
+  return L;
+}
+
+static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const float* params, const void* images,
+                            bool training, unsigned char* ws, hipStream_t s) {
+  const int C = c->C, N = c->N, H = c->H, W = c->W;
+  const bool bf = c->dtype == ASR_BF16;
+  // 1. materialise W for all L blocks (one launch)
+  ASR_TRY(asr_theta_to_w(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src), c->gamma,
+                         ws + L.wbuf, L.wstride, c->dtype, s));
+  // 2. input normalisation (tfkeras_resnets.py:555-559)
+  const long nin = (long)N * H * W * c->Cin;
+  float* x0 = (float*)(ws + L.x0);
+  const unsigned gn = (unsigned)std::min<long>((nin + 255) / 256, 4096);
+  const float inv_std = c->use_norm ? 1.f / c->divide_by_stddev : 1.f;
+  if (c->input_u8)
+    hipLaunchKernelGGL(k_normalize<uint8_t>, dim3(gn), dim3(256), 0, s, (const uint8_t*)images, nin,
+                       c->subtract_mean, inv_std, c->use_norm, x0);
+  else
+    hipLaunchKernelGGL(k_normalize<float>, dim3(gn), dim3(256), 0, s, (const float*)images, nin, c->subtract_mean,
+                       inv_std, c->use_norm, x0);
+  ASR_LAUNCH_CHECK("k_normalize");
+  // 3. stem conv1 + relu (tfkeras_resnets.py:563-572)
+  unsigned char* acts = ws + L.acts;
+  auto act = [&](int i) -> unsigned char* {
+    const int slot = training ? i : (i & 1);
+    return acts + (size_t)slot * L.P * L.act_bytes;
+  };
+  ASR_TRY(conv_f32(F_RELU, x0, act(0), nullptr, params + L.off_c1k, params + L.off_c1b, 1.f, 0.f, nullptr, N, H, W,
+                   c->Cin, C, bf ? 1 : 0, s));
+  // 4. L Euler blocks (tfkeras_resnets.py:579-582 -> :28-94)
+  for (int l = 0; l < c->L; ++l) {
+    const float* bias = params + L.off_blk + (long)l * L.blk_stride + L.ntheta;
+    const unsigned char* wl = ws + L.wbuf + (size_t)l * L.wstride * L.act_bytes;
+    uint64_t* mask = training ? (uint64_t*)(ws + L.masks) + (size_t)l * L.mask_words : nullptr;
+    if (bf)
+      ASR_TRY(conv_mfma(0, act(l), act(l + 1), mask, wl, bias, c->h, 0.f, N, H, W, C, s));
+    else
+      ASR_TRY(conv_f32(F_EULER, act(l), act(l + 1), mask, (const float*)wl, bias, c->h, 0.f, nullptr, N, H, W, C, C,
+                       0, s));
+  }
+  return ASR_OK;
+}
+
+}  // namespace asr
+
+using namespace asr;
+
+extern "C" {
+
+long asr_mask_words(int N, int H, int W, int C) {
+  if (N < 1 || H < 1 || W < 1 || C < 1) return -1;
+  return (long)N * H * ((W + 15) / 16) * ((C + 15) / 16) * 4;
+}
+
+int asr_conv_forward(int mode, const void* x, void* y, uint64_t* mask, const void* w, const float* bias, float h,
+                     int N, int H, int W, int C, int dtype, asr_stream_t stream) {
+  ASR_TRY(check_shape(N, H, W, C));
+  if (!x || !y || !w) return fail(ASR_E_ARG, "asr_conv_forward: null pointer");
+  if (mode != ASR_MODE_EULER && mode != ASR_MODE_CONV) return fail(ASR_E_ARG, "asr_conv_forward: bad mode %d", mode);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == ASR_BF16) {
+    if (!mfma_supported(C, W))
+      return fail(ASR_E_UNSUPPORTED, "bf16 conv needs C in {16,32,64} and W == 32 (C=%d W=%d)", C, W);
+    return conv_mfma(mode == ASR_MODE_EULER ? 0 : 1, x, y, mask, w, bias, h, 0.f, N, H, W, C, s);
+  }
+  if (dtype == ASR_F32)
+    return conv_f32(mode == ASR_MODE_EULER ? F_EULER : F_CONV, x, y, mask, (const float*)w, bias, h, 0.f, nullptr, N,
+                    H, W, C, C, 0, s);
+  return fail(ASR_E_ARG, "asr_conv_forward: bad dtype %d", dtype);
+}
+
+size_t asr_conv_backward_workspace_bytes(int N, int H, int W, int C, int dtype) {
+  if (check_shape(N, H, W, C) != ASR_OK) return 0;
+  return bwd_ws_layout(N, H, W, C, dtype).total;
+}
+
+int asr_conv_backward(int mode, const void* dy, const void* x, const uint64_t* mask, const void* w,
+                      const int32_t* theta_dst, long n_theta, float h, float gamma, int N, int H, int W, int C,
+                      int dtype, void* dx, float* dtheta, float* dbias, float* dw_hwio, void* ws, size_t ws_bytes,
+                      asr_stream_t stream) {
+  ASR_TRY(check_shape(N, H, W, C));
+  if (mode != ASR_MODE_EULER && mode != ASR_MODE_CONV) return fail(ASR_E_ARG, "asr_conv_backward: bad mode %d", mode);
+  if (!dy || !w || (mode == ASR_MODE_EULER && !mask)) return fail(ASR_E_ARG, "asr_conv_backward: null pointer");
+  if ((dtheta || dbias || dw_hwio) && !x) return fail(ASR_E_ARG, "asr_conv_backward: x needed for weight gradients");
+  if (dtheta && !theta_dst) return fail(ASR_E_ARG, "asr_conv_backward: theta_dst needed for dtheta");
+  if (dtype != ASR_F32 && dtype != ASR_BF16) return fail(ASR_E_ARG, "asr_conv_backward: bad dtype");
+  if (dtype == ASR_BF16 && !mfma_supported(C, W))
+    return fail(ASR_E_UNSUPPORTED, "bf16 conv needs C in {16,32,64} and W == 32 (C=%d W=%d)", C, W);
+  if (!ws || ws_bytes < bwd_ws_layout(N, H, W, C, dtype).total)
+    return fail(ASR_E_WORKSPACE, "asr_conv_backward: workspace too small");
+  return conv_backward_impl(mode, dy, x, mask, w, theta_dst, n_theta, h, gamma, N, H, W, C, dtype, dx, dtheta, dbias,
+                            dw_hwio, ws, (hipStream_t)stream);
+}
+
+long asr_net_param_count(const asr_net_config* cfg) {
+  if (net_check(cfg) != ASR_OK) return -1;
+  return net_layout(cfg).nparams;
+}
+
+size_t asr_net_workspace_bytes(const asr_net_config* cfg) {
+  if (net_check(cfg) != ASR_OK) return 0;
+  return net_layout(cfg).total;
+}
+
+int asr_net_prepare(const asr_net_config* cfg, void* ws, size_t ws_bytes) {
+  ASR_TRY(net_check(cfg));
+  const NetLayout L = net_layout(cfg);
+  if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_net_prepare: workspace too small");
+  std::vector<int32_t> w_src((size_t)L.E), theta_dst((size_t)L.ntheta * 2);
+  ASR_TRY(param_map(cfg->C, ASR_PARAM_3BY3, 1, w_src.data(), theta_dst.data()));
+  unsigned char* b = (unsigned char*)ws;
+  ASR_TRY(hip_check(hipMemcpy(b + L.w_src, w_src.data(), w_src.size() * 4, hipMemcpyHostToDevice), "hipMemcpy"));
+  ASR_TRY(hip_check(hipMemcpy(b + L.theta_dst, theta_dst.data(), theta_dst.size() * 4, hipMemcpyHostToDevice),
+                    "hipMemcpy"));
+  return ASR_OK;
+}
+
+int asr_net_forward(const asr_net_config* cfg, const float* params, const void* images, float* probs, void* ws,
+                    size_t ws_bytes, asr_stream_t stream) {
+  ASR_TRY(net_check(cfg));
+  const NetLayout L = net_layout(cfg);
+  if (!params || !images || !probs) return fail(ASR_E_ARG, "asr_net_forward: null pointer");
+  if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_net_forward: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  unsigned char* b = (unsigned char*)ws;
+  ASR_TRY(net_forward_impl(cfg, L, params, images, false, b, s));
+  const unsigned char* xL = b + L.acts + (size_t)(cfg->L & 1) * L.P * L.act_bytes;
+  const int HW = cfg->H * cfg->W;
+  if (cfg->dtype == ASR_BF16)
+    hipLaunchKernelGGL(k_head<bf16>, dim3(cfg->N), dim3(256), 0, s, (const bf16*)xL, params + L.off_fck,
+                       params + L.off_fcb, nullptr, HW, cfg->C, cfg->num_classes, 0.f, probs, nullptr, nullptr,
+                       nullptr, nullptr);
+  else
+    hipLaunchKernelGGL(k_head<float>, dim3(cfg->N), dim3(256), 0, s, (const float*)xL, params + L.off_fck,
+                       params + L.off_fcb, nullptr, HW, cfg->C, cfg->num_classes, 0.f, probs, nullptr, nullptr,
+                       nullptr, nullptr);
+  ASR_LAUNCH_CHECK("k_head");
+  return ASR_OK;
+}
+
+int asr_net_forward_backward(const asr_net_config* cfg, const float* params, const void* images, const float* targets,
+                             float* grads, float* loss, float* probs, void* ws, size_t ws_bytes,
+                             asr_stream_t stream) {
+  ASR_TRY(net_check(cfg));
+  const NetLayout L = net_layout(cfg);
+  if (!params || !images || !targets || !grads || !loss) return fail(ASR_E_ARG, "asr_net_forward_backward: null");
+  if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_net_forward_backward: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  unsigned char* b = (unsigned char*)ws;
+  const int C = cfg->C, N = cfg->N, H = cfg->H, W = cfg->W, K = cfg->num_classes;
+  const bool bf = cfg->dtype == ASR_BF16;
+  ASR_TRY(net_forward_impl(cfg, L, params, images, true, b, s));
+  auto act = [&](int i) { return b + L.acts + (size_t)i * L.P * L.act_bytes; };
+  // head: probabilities, per-image loss, dlogits, dL/dx_L
+  unsigned char* dcur = b + L.dxa;
+  unsigned char* dnext = b + L.dxb;
+  float* probs_ws = probs ? probs : (float*)(b + L.probs);
+  const int HW = H * W;
+  if (bf)
+    hipLaunchKernelGGL(k_head<bf16>, dim3(N), dim3(256), 0, s, (const bf16*)act(cfg->L), params + L.off_fck,
+                       params + L.off_fcb, targets, HW, C, K, 1.f / N, probs_ws, (float*)(b + L.loss_per),
+                       (float*)(b + L.dlogits), (float*)(b + L.gap), (bf16*)dcur);
+  else
+    hipLaunchKernelGGL(k_head<float>, dim3(N), dim3(256), 0, s, (const float*)act(cfg->L), params + L.off_fck,
+                       params + L.off_fcb, targets, HW, C, K, 1.f / N, probs_ws, (float*)(b + L.loss_per),
+                       (float*)(b + L.dlogits), (float*)(b + L.gap), (float*)dcur);
+  ASR_LAUNCH_CHECK("k_head");
+  hipLaunchKernelGGL(k_head_param_grads, dim3(1), dim3(256), 0, s, (const float*)(b + L.gap),
+                     (const float*)(b + L.dlogits), N, C, K, grads + L.off_fck, grads + L.off_fcb,
+                     (const float*)(b + L.loss_per), loss);
+  ASR_LAUNCH_CHECK("k_head_param_grads");
+  // Euler blocks, last to first
+  const int32_t* theta_dst = (const int32_t*)(b + L.theta_dst);
+  for (int l = cfg->L - 1; l >= 0; --l) {
+    const unsigned char* wl = b + L.wbuf + (size_t)l * L.wstride * L.act_bytes;
+    const uint64_t* mask = (const uint64_t*)(b + L.masks) + (size_t)l * L.mask_words;
+    float* dth = grads + L.off_blk + (long)l * L.blk_stride;
+    ASR_TRY(conv_backward_impl(ASR_MODE_EULER, dcur, act(l), mask, wl, theta_dst, L.ntheta, cfg->h, cfg->gamma, N, H,
+                               W, C, cfg->dtype, dnext, dth, dth + L.ntheta, nullptr, b + L.dz, s));
+    std::swap(dcur, dnext);
+  }
+  // stem: dz1 = dx1 * [x1 > 0]; conv1 weight gradient from the normalised input
+  float* dz = (float*)(b + L.dz);
+  ASR_TRY(make_dz(F_RELU, dcur, nullptr, act(0), 1.f, N, H, W, C, bf ? 1 : 0, dz, s));
+  int nsl = 0;
+  float* slabs = (float*)(b + L.slabs);
+  float* dbs = (float*)(b + L.dbs);
+  ASR_TRY(wgrad_f32(b + L.x0, 0, dz, N, H, W, cfg->Cin, C, slabs, dbs, &nsl, s));
+  ASR_TRY(reduce_and_project(slabs, nsl, 9L * cfg->Cin * C, dbs, nsl, C, nullptr, 0, nullptr, grads + L.off_c1b,
+                             grads + L.off_c1k, (float*)(b + L.red), s));
+  return ASR_OK;
+}
+
+int asr_adam_update(float* params, const float* grads, float* m, float* v, long n, float lr, float beta1, float beta2,
+                    float eps, long step, float grad_scale, asr_stream_t stream) {
+  if (!params || !grads || !m || !v || n < 0 || step < 1) return fail(ASR_E_ARG, "asr_adam_update: bad arguments");
+  const double lr_t = (double)lr * sqrt(1.0 - pow((double)beta2, (double)step)) / (1.0 - pow((double)beta1, (double)step));
+  const unsigned grid = (unsigned)std::max<long>(1, std::min<long>((n + 255) / 256, 4096));
+  hipLaunchKernelGGL(k_adam, dim3(grid), dim3(256), 0, (hipStream_t)stream, params, grads, m, v, n, (float)lr_t,
+                     beta1, beta2, eps, grad_scale);
+  ASR_LAUNCH_CHECK("k_adam");
+  return ASR_OK;
+}
+
+}  // extern "C"

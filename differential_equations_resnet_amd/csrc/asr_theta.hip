@@ -1,0 +1,338 @@
+// Parametrisation of the antisymmetric kernel: theta -> W materialisation and
+// the dW -> dtheta pull-back.
+//
+// Reference: layers/tfkeras_layer_Conv2DAntisymmetric3By3.py:104-141 (assembly
+// loop, one slice/neg/concat graph per output channel) and :210-293 (diagonal
+// block [[a,b,c],[d,gamma,-d],[-c,-b,-a]], off-diagonal -rot180 transpose);
+// layers/tfkeras_layer_Conv2DAntisymmetric.py:109-145, :216-270 (general layer).
+//
+// Instead of ~24(C-1)+1.5C(C-1) graph ops per layer per step, the whole
+// assembly is a precomputed element map (asr_param_map, built once on the
+// host) and one gather launch for all L layers of a network (asr_theta_to_w).
+// The map's transpose gives the exact autodiff of the assembly: every theta
+// entry feeds at most two W entries with signs +-1, so dtheta is a two-term
+// gather from the reduced dW (k_project).
+#include <stdarg.h>
+#include <stdio.h>
+
+#include <vector>
+
+#include "asr_common.h"
+
+namespace asr {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int cu_count() {
+  static thread_local int dev_cached = -1, cus = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (dev != dev_cached) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    dev_cached = dev;
+    cus = v;
+  }
+  return cus;
+}
+
+// ---------------------------------------------------------------------------
+// host: element maps
+// ---------------------------------------------------------------------------
+
+// Free positions of the general layer's diagonal block in variable-creation
+// order (…Conv2DAntisymmetric.py:231-264), for kernel_size 3.
+static void general_free_positions(int antisymmetric, std::vector<std::pair<int, int>>& out) {
+  const int k = 3;
+  for (int i = 0; i < k; ++i)
+    for (int j = i; j < k; ++j) {
+      if (j > i || (j == i && i <= k / 2 - 1))
+        out.push_back({i, j});
+      else if (j == i && i == k / 2 && (k % 2) == 1 && !antisymmetric)
+        out.push_back({i, j});
+    }
+}
+
+long theta_count(int C, int kind, int antisymmetric) {
+  if (C < 1) return -1;
+  if (kind == ASR_PARAM_3BY3) return 4L * C + 9L * C * (C - 1) / 2;
+  if (kind == ASR_PARAM_GENERAL) {
+    std::vector<std::pair<int, int>> fp;
+    general_free_positions(antisymmetric, fp);
+    return (long)fp.size() * C + 9L * C * (C - 1) / 2;
+  }
+  return -1;
+}
+
+int param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta_dst) {
+  if (C < 1 || !w_src) return fail(ASR_E_ARG, "asr_param_map: bad arguments");
+  if (kind == ASR_PARAM_3BY3 && !antisymmetric)
+    return fail(ASR_E_ARG, "asr_param_map: the 3by3 layer is always antisymmetric");
+  const long E = 9L * C * C;
+  auto idx = [C](int ky, int kx, int i, int o) { return ((long)(ky * 3 + kx) * C + i) * C + o; };
+  for (long e = 0; e < E; ++e) w_src[e] = -1;  // gamma unless set below
+  if (kind == ASR_PARAM_3BY3) {
+    // diagonal: a (0,0) b (0,1) c (0,2) d (1,0); mirrors negated (…3By3.py:261-275)
+    const int pos[8][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 0}, {2, 2}, {2, 1}, {2, 0}, {1, 2}};
+    const int var[8] = {0, 1, 2, 3, 0, 1, 2, 3};
+    const int neg[8] = {0, 0, 0, 0, 1, 1, 1, 1};
+    for (int o = 0; o < C; ++o)
+      for (int q = 0; q < 8; ++q)
+        w_src[idx(pos[q][0], pos[q][1], o, o)] = (int32_t)(((long)(var[q] * C + o) << 1) | neg[q]);
+    long base = 4L * C;
+    for (int o = 0; o < C - 1; ++o) {
+      const int nind = C - o - 1;
+      for (int i = o + 1; i < C; ++i) {
+        const int m = i - o - 1;
+        for (int ky = 0; ky < 3; ++ky)
+          for (int kx = 0; kx < 3; ++kx) {
+            const long j = base + (long)(ky * 3 + kx) * nind + m;
+            w_src[idx(ky, kx, i, o)] = (int32_t)(j << 1);                  // W[:,:,i,o] = indep_o
+            w_src[idx(2 - ky, 2 - kx, o, i)] = (int32_t)((j << 1) | 1);    // W[:,:,o,i] = -rot180
+          }
+      }
+      base += 9L * nind;
+    }
+  } else if (kind == ASR_PARAM_GENERAL) {
+    std::vector<std::pair<int, int>> fp;
+    general_free_positions(antisymmetric, fp);
+    long off = 0;
+    for (int o = 0; o < C; ++o) {
+      for (size_t n = 0; n < fp.size(); ++n) {
+        const int i = fp[n].first, j = fp[n].second;
+        const long t = off + (long)n;
+        w_src[idx(i, j, o, o)] = (int32_t)(t << 1);
+        const int mi = 2 - i, mj = 2 - j;
+        if (mi != i || mj != j) w_src[idx(mi, mj, o, o)] = (int32_t)((t << 1) | (antisymmetric ? 1 : 0));
+      }
+      off += (long)fp.size();
+      const int nind = C - o - 1;
+      if (nind > 0) {
+        for (int i = o + 1; i < C; ++i) {
+          const int m = i - o - 1;
+          for (int ky = 0; ky < 3; ++ky)
+            for (int kx = 0; kx < 3; ++kx) {
+              const long j = off + (long)(ky * 3 + kx) * nind + m;  // [k,k,nind,1]
+              w_src[idx(ky, kx, i, o)] = (int32_t)(j << 1);
+              w_src[idx(2 - ky, 2 - kx, o, i)] = (int32_t)((j << 1) | 1);
+            }
+        }
+        off += 9L * nind;
+      }
+    }
+  } else {
+    return fail(ASR_E_ARG, "asr_param_map: unknown kind %d", kind);
+  }
+  if (theta_dst) {
+    const long nt = theta_count(C, kind, antisymmetric);
+    for (long j = 0; j < 2 * nt; ++j) theta_dst[j] = -1;
+    for (long e = 0; e < E; ++e) {
+      const int32_t v = w_src[e];
+      if (v < 0) continue;
+      const long j = v >> 1;
+      const int32_t enc = (int32_t)((e << 1) | (v & 1));
+      if (theta_dst[2 * j] < 0)
+        theta_dst[2 * j] = enc;
+      else if (theta_dst[2 * j + 1] < 0)
+        theta_dst[2 * j + 1] = enc;
+      else
+        return fail(ASR_E_ARG, "asr_param_map: theta %ld feeds more than two W entries", j);
+    }
+  }
+  return ASR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// device: materialisation
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ float w_value(const float* theta, const int32_t* w_src, long e, float gamma) {
+  const int32_t v = w_src[e];
+  if (v < 0) return gamma;
+  const float t = theta[v >> 1];
+  return (v & 1) ? -t : t;
+}
+
+// plain HWIO float: one thread per element, blockIdx.y = layer
+__global__ void k_theta_to_w_hwio(const float* __restrict__ theta, long theta_stride, int C,
+                                  const int32_t* __restrict__ w_src, float gamma, float* __restrict__ w,
+                                  long w_stride) {
+  const long E = 9L * C * C;
+  const int l = blockIdx.y;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < E; e += (long)gridDim.x * blockDim.x)
+    w[l * w_stride + e] = w_value(theta + l * theta_stride, w_src, e, gamma);
+}
+
+// MFMA fragment-packed bf16 (see asr_conv_mfma.hip, "W pack"):
+//   pack[((ot*KS + ks)*64 + lane)*8 + j] = W^T[o = 16*ot + (lane&15)][kappa = 32*ks + 8*(lane>>4) + j]
+//   with kappa = tap*C + i (tap = ky*3+kx), zero for kappa >= 9C.
+// One 64-lane wave per (ot, ks) fragment: each lane builds its 8 elements and
+// writes 16 contiguous bytes.
+__global__ void k_theta_to_w_pack(const float* __restrict__ theta, long theta_stride, int C,
+                                  const int32_t* __restrict__ w_src, float gamma, bf16* __restrict__ w,
+                                  long w_stride) {
+  const int KS = (9 * C + 31) / 32;
+  const int OT = C / 16;
+  const int l = blockIdx.y;
+  const int frag = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  if (frag >= OT * KS) return;
+  const int lane = threadIdx.x & 63;
+  const int ot = frag / KS, ks = frag % KS;
+  const int o = 16 * ot + (lane & 15);
+  const float* th = theta + l * theta_stride;
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int kappa = 32 * ks + 8 * (lane >> 4) + j;
+    float x = 0.f;
+    if (kappa < 9 * C) {
+      const int tap = kappa / C, i = kappa % C;
+      x = w_value(th, w_src, ((long)tap * C + i) * C + o, gamma);
+    }
+    v[j] = (bf16)x;
+  }
+  *(bf16x8*)(w + l * w_stride + ((long)frag * 64 + lane) * 8) = v;
+}
+
+// ---------------------------------------------------------------------------
+// device: split-K reduction of fp32 slabs and the theta projection
+// ---------------------------------------------------------------------------
+
+// out[g][e] = sum_{p in [g*per, min((g+1)*per, P))} in[p][e]   (deterministic)
+__global__ void k_reduce_slabs(const float* __restrict__ in, long E, int P, int per, float* __restrict__ out) {
+  const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int g = blockIdx.y;
+  if (e >= E) return;
+  const int p0 = g * per, p1 = min(P, p0 + per);
+  float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+  int p = p0;
+  for (; p + 3 < p1; p += 4) {
+    acc0 += in[(long)p * E + e];
+    acc1 += in[(long)(p + 1) * E + e];
+    acc2 += in[(long)(p + 2) * E + e];
+    acc3 += in[(long)(p + 3) * E + e];
+  }
+  for (; p < p1; ++p) acc0 += in[(long)p * E + e];
+  out[(long)g * E + e] = (acc0 + acc1) + (acc2 + acc3);
+}
+
+// dtheta[j] = sum over the (<=2) W entries theta j feeds of sign * dW[e];
+// dW = sum of G group slabs of E floats (G small).  Also optional dW copy and
+// db = sum of GB slabs of Cb floats.
+__global__ void k_project(const float* __restrict__ dw_groups, int G, long E, const int32_t* __restrict__ theta_dst,
+                          long n_theta, float* __restrict__ dtheta, float* __restrict__ dw_out,
+                          const float* __restrict__ db_groups, int GB, int Cb, float* __restrict__ dbias) {
+  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  auto dw = [&](long e) {
+    float s = 0.f;
+    for (int g = 0; g < G; ++g) s += dw_groups[(long)g * E + e];
+    return s;
+  };
+  if (dtheta && t < n_theta) {
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int32_t v = theta_dst[2 * t + q];
+      if (v >= 0) {
+        const float d = dw(v >> 1);
+        acc += (v & 1) ? -d : d;
+      }
+    }
+    dtheta[t] = acc;
+  }
+  if (dw_out && t < E) dw_out[t] = dw(t);
+  if (dbias && t < Cb) {
+    float s = 0.f;
+    for (int g = 0; g < GB; ++g) s += db_groups[(long)g * Cb + t];
+    dbias[t] = s;
+  }
+}
+
+}  // namespace asr
+
+using namespace asr;
+
+extern "C" {
+
+const char* asr_last_error(void) { return g_err; }
+int asr_abi_version(void) { return 1; }
+int asr_device_cu_count(void) { return cu_count(); }
+
+long asr_theta_count(int C, int kind, int antisymmetric) { return theta_count(C, kind, antisymmetric); }
+
+int asr_param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta_dst) {
+  return param_map(C, kind, antisymmetric, w_src, theta_dst);
+}
+
+long asr_wpack_elems(int C) {
+  if (C % 16 != 0) return -1;
+  return (long)(C / 16) * ((9 * C + 31) / 32) * 64 * 8;
+}
+
+int asr_theta_to_w(const float* theta, long theta_stride, int L, int C, const int32_t* w_src, float gamma,
+                   void* w_out, long w_stride, int dtype, asr_stream_t stream) {
+  if (!theta || !w_src || !w_out || L < 1 || C < 1 || L > 65535)
+    return fail(ASR_E_ARG, "asr_theta_to_w: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == ASR_F32) {
+    const long E = 9L * C * C;
+    if (w_stride < E) return fail(ASR_E_ARG, "asr_theta_to_w: w_stride too small");
+    dim3 grid((unsigned)std::min<long>((E + 255) / 256, 1024), L);
+    hipLaunchKernelGGL(k_theta_to_w_hwio, grid, dim3(256), 0, s, theta, theta_stride, C, w_src, gamma,
+                       (float*)w_out, w_stride);
+    ASR_LAUNCH_CHECK("k_theta_to_w_hwio");
+  } else if (dtype == ASR_BF16) {
+    if (C % 16 != 0) return fail(ASR_E_UNSUPPORTED, "asr_theta_to_w: bf16 pack needs C %% 16 == 0 (C=%d)", C);
+    if (w_stride < asr_wpack_elems(C)) return fail(ASR_E_ARG, "asr_theta_to_w: w_stride too small");
+    const int frags = (C / 16) * ((9 * C + 31) / 32);
+    dim3 grid((frags + 3) / 4, L);
+    hipLaunchKernelGGL(k_theta_to_w_pack, grid, dim3(256), 0, s, theta, theta_stride, C, w_src, gamma,
+                       (bf16*)w_out, w_stride);
+    ASR_LAUNCH_CHECK("k_theta_to_w_pack");
+  } else {
+    return fail(ASR_E_ARG, "asr_theta_to_w: bad dtype %d", dtype);
+  }
+  return ASR_OK;
+}
+
+}  // extern "C"
+
+namespace asr {
+
+// Reduce P slabs of E floats (dW partials) and PB slabs of Cb floats (db
+// partials); project dW onto theta (if theta_dst) and/or copy it out.
+// ws must hold reduce_ws_bytes(P, E) bytes.
+int reduce_and_project(const float* slabs, int P, long E, const float* db_slabs, int PB, int Cb,
+                       const int32_t* theta_dst, long n_theta, float* dtheta, float* dbias, float* dw_out, float* ws,
+                       hipStream_t s) {
+  const int per = 32;
+  const int G = (P + per - 1) / per;
+  float* grp = ws;
+  dim3 g1((unsigned)((E + 255) / 256), G);
+  hipLaunchKernelGGL(k_reduce_slabs, g1, dim3(256), 0, s, slabs, E, P, per, grp);
+  ASR_LAUNCH_CHECK("k_reduce_slabs");
+  const long n = std::max(std::max(dtheta ? n_theta : 0L, dw_out ? E : 0L), (long)Cb);
+  hipLaunchKernelGGL(k_project, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, grp, G, E, theta_dst,
+                     dtheta ? n_theta : 0L, dtheta, dw_out, db_slabs, PB, Cb, dbias);
+  ASR_LAUNCH_CHECK("k_project");
+  return ASR_OK;
+}
+
+size_t reduce_ws_bytes(int P, long E) { return (size_t)((P + 31) / 32) * E * sizeof(float); }
+
+}  // namespace asr

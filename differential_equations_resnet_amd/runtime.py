@@ -1,0 +1,206 @@
+"""Typed Python wrappers over the C ABI, with PyTorch-ROCm tensors used only as
+device-memory containers (data_ptr) and for the current HIP stream.
+
+Every function here launches libasr kernels; none computes anything in torch.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import ASR_BF16, ASR_F32, ASR_MODE_CONV, ASR_MODE_EULER, ASR_PARAM_3BY3, ASR_PARAM_GENERAL, NetConfig
+
+__all__ = [
+    "require_gpu", "dtype_code", "torch_dtype", "ParamMap", "param_map", "theta_count", "theta_to_w",
+    "conv_forward", "conv_backward", "NetExecutor", "adam_update",
+]
+
+
+def require_gpu() -> torch.device:
+    if not torch.cuda.is_available():
+        raise _lib.AsrError("a gfx950 (MI355X) HIP device is required: libasr has no CPU path")
+    _lib.load()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def dtype_code(dtype) -> int:
+    if dtype in (torch.float32, "float32", np.float32, ASR_F32):
+        return ASR_F32
+    if dtype in (torch.bfloat16, "bfloat16", "bf16", ASR_BF16):
+        return ASR_BF16
+    raise ValueError(f"unsupported activation dtype {dtype!r} (float32 or bfloat16)")
+
+
+def torch_dtype(code: int):
+    return torch.float32 if code == ASR_F32 else torch.bfloat16
+
+
+def theta_count(C: int, kind: int = ASR_PARAM_3BY3, antisymmetric: bool = True) -> int:
+    n = _lib.load().asr_theta_count(C, kind, int(antisymmetric))
+    if n < 0:
+        raise ValueError(f"bad theta_count arguments C={C} kind={kind}")
+    return int(n)
+
+
+@dataclass
+class ParamMap:
+    C: int
+    kind: int
+    antisymmetric: bool
+    w_src: np.ndarray      # int32 [9*C*C]
+    theta_dst: np.ndarray  # int32 [2*n_theta]
+    _dev: dict
+
+    @property
+    def n_theta(self) -> int:
+        return self.theta_dst.size // 2
+
+    def device(self, device) -> tuple:
+        key = str(device)
+        if key not in self._dev:
+            self._dev[key] = (torch.from_numpy(self.w_src).to(device), torch.from_numpy(self.theta_dst).to(device))
+        return self._dev[key]
+
+
+_MAPS: dict = {}
+
+
+def param_map(C: int, kind: int = ASR_PARAM_3BY3, antisymmetric: bool = True) -> ParamMap:
+    """Element map of W(theta) and its pull-back (asr_param_map, host)."""
+    key = (C, kind, bool(antisymmetric))
+    if key not in _MAPS:
+        nt = theta_count(C, kind, antisymmetric)
+        w_src = np.empty(9 * C * C, dtype=np.int32)
+        dst = np.empty(2 * nt, dtype=np.int32)
+        _lib.call("asr_param_map", C, kind, int(antisymmetric), w_src.ctypes.data, dst.ctypes.data)
+        _MAPS[key] = ParamMap(C, kind, bool(antisymmetric), w_src, dst, {})
+    return _MAPS[key]
+
+
+def wpack_elems(C: int) -> int:
+    n = _lib.load().asr_wpack_elems(C)
+    if n < 0:
+        raise _lib.AsrUnsupported(f"bf16 packed W needs C % 16 == 0 (C={C})")
+    return int(n)
+
+
+def theta_to_w(theta: torch.Tensor, C: int, pmap: ParamMap, gamma: float, dtype: int, layers: int = 1,
+               theta_stride: int | None = None) -> torch.Tensor:
+    """Materialise W for `layers` layers whose thetas are theta_stride floats
+    apart.  bf16 -> MFMA-packed layout, f32 -> HWIO [layers, 3, 3, C, C]."""
+    dev = theta.device
+    w_src, _ = pmap.device(dev)
+    stride = pmap.n_theta if theta_stride is None else theta_stride
+    if dtype == ASR_BF16:
+        per = wpack_elems(C)
+        out = torch.empty(layers * per, dtype=torch.bfloat16, device=dev)
+    else:
+        per = 9 * C * C
+        out = torch.empty(layers * per, dtype=torch.float32, device=dev)
+    _lib.call("asr_theta_to_w", _p(theta), stride, layers, C, _p(w_src), float(gamma), _p(out), per, dtype, _stream())
+    if dtype == ASR_F32:
+        return out.view(layers, 3, 3, C, C)
+    return out.view(layers, per)
+
+
+def conv_forward(mode: int, x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, h: float = 1.0,
+                 mask: torch.Tensor | None = None) -> torch.Tensor:
+    N, H, W, C = x.shape
+    dt = dtype_code(x.dtype)
+    if not x.is_contiguous():
+        raise ValueError("x must be contiguous NHWC")
+    y = torch.empty_like(x)
+    _lib.call("asr_conv_forward", mode, _p(x), _p(y), _p(mask), _p(w), _p(bias), float(h), N, H, W, C, dt, _stream())
+    return y
+
+
+def mask_words(N: int, H: int, W: int, C: int) -> int:
+    return int(_lib.load().asr_mask_words(N, H, W, C))
+
+
+def conv_backward(mode: int, dy: torch.Tensor, x: torch.Tensor, mask: torch.Tensor | None, w: torch.Tensor,
+                  pmap: ParamMap, h: float, gamma: float, want_dx=True, want_dtheta=True, want_dbias=True,
+                  want_dw=False):
+    N, H, W, C = dy.shape
+    dt = dtype_code(dy.dtype)
+    dev = dy.device
+    ws_bytes = int(_lib.load().asr_conv_backward_workspace_bytes(N, H, W, C, dt))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    dx = torch.empty_like(dy) if want_dx else None
+    dth = torch.empty(pmap.n_theta, dtype=torch.float32, device=dev) if want_dtheta else None
+    db = torch.empty(C, dtype=torch.float32, device=dev) if want_dbias else None
+    dw = torch.empty(3, 3, C, C, dtype=torch.float32, device=dev) if want_dw else None
+    _, theta_dst = pmap.device(dev)
+    _lib.call("asr_conv_backward", mode, _p(dy), _p(x), _p(mask), _p(w), _p(theta_dst), pmap.n_theta, float(h),
+              float(gamma), N, H, W, C, dt, _p(dx), _p(dth), _p(db), _p(dw), _p(ws), ws_bytes, _stream())
+    return dx, dth, db, dw
+
+
+def adam_update(params, grads, m, v, lr, beta1, beta2, eps, step, grad_scale=1.0):
+    _lib.call("asr_adam_update", _p(params), _p(grads), _p(m), _p(v), params.numel(), float(lr), float(beta1),
+              float(beta2), float(eps), int(step), float(grad_scale), _stream())
+
+
+class NetExecutor:
+    """Native executor of the single-block antisymmetric ResNet
+    (asr_net_* in include/asr.h).  Owns the device workspace; parameters,
+    gradients and Adam moments are flat float32 buffers in Keras
+    get_weights() order."""
+
+    def __init__(self, N, H, W, Cin, C, L, num_classes, h, gamma=0.0, subtract_mean=None, divide_by_stddev=None,
+                 dtype="bfloat16", input_u8=True, device=None):
+        self.device = device or require_gpu()
+        use_norm = subtract_mean is not None or divide_by_stddev is not None
+        self.cfg = NetConfig(int(N), int(H), int(W), int(Cin), int(C), int(L), int(num_classes), float(h),
+                             float(gamma), float(subtract_mean or 0.0),
+                             float(divide_by_stddev if divide_by_stddev is not None else 1.0), int(use_norm),
+                             dtype_code(dtype), int(bool(input_u8)))
+        lib = _lib.load()
+        self.n_params = int(lib.asr_net_param_count(ct.byref(self.cfg)))
+        if self.n_params < 0:
+            _lib.check(_lib.ASR_E_ARG, "asr_net_param_count")
+        self.ws_bytes = int(lib.asr_net_workspace_bytes(ct.byref(self.cfg)))
+        if self.ws_bytes == 0:
+            _lib.check(_lib.ASR_E_ARG, "asr_net_workspace_bytes")
+        self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
+        _lib.call("asr_net_prepare", ct.byref(self.cfg), _p(self.ws), self.ws_bytes)
+        self.grads = torch.zeros(self.n_params, dtype=torch.float32, device=self.device)
+        self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.probs = torch.zeros(N, num_classes, dtype=torch.float32, device=self.device)
+
+    def _check_inputs(self, params, images):
+        c = self.cfg
+        if params.numel() != self.n_params or params.dtype != torch.float32 or not params.is_cuda:
+            raise ValueError(f"params must be a float32 device buffer of {self.n_params} elements")
+        want = torch.uint8 if c.input_u8 else torch.float32
+        if tuple(images.shape) != (c.N, c.H, c.W, c.Cin) or images.dtype != want or not images.is_contiguous():
+            raise ValueError(f"images must be contiguous {want} [{c.N},{c.H},{c.W},{c.Cin}] (NHWC)")
+
+    def forward(self, params, images) -> torch.Tensor:
+        self._check_inputs(params, images)
+        _lib.call("asr_net_forward", ct.byref(self.cfg), _p(params), _p(images), _p(self.probs), _p(self.ws),
+                  self.ws_bytes, _stream())
+        return self.probs
+
+    def forward_backward(self, params, images, targets, want_probs=False):
+        self._check_inputs(params, images)
+        if tuple(targets.shape) != (self.cfg.N, self.cfg.num_classes) or targets.dtype != torch.float32:
+            raise ValueError("targets must be float32 one-hot [N, num_classes]")
+        _lib.call("asr_net_forward_backward", ct.byref(self.cfg), _p(params), _p(images), _p(targets),
+                  _p(self.grads), _p(self.loss), _p(self.probs) if want_probs else None, _p(self.ws),
+                  self.ws_bytes, _stream())
+        return self.loss, self.grads

@@ -1,0 +1,177 @@
+/*
+ * asr.h — C ABI of libasr.so, the MI355X-native hot path of the
+ * antisymmetric-ResNet (pierluigiferrari/differential_equations_resnet).
+ *
+ * One Euler block of the reference is
+ *     x_{n+1} = x_n + h * relu(conv3x3(x_n, W(theta)) + b)
+ * (models/tfkeras_resnets.py:69-92) where W(theta) is re-materialised from the
+ * layer's free parameters on every step
+ * (layers/tfkeras_layer_Conv2DAntisymmetric3By3.py:85-171).
+ *
+ * Conventions
+ *   - plain pointers and sizes only; every pointer is a device pointer unless
+ *     the comment says "host";
+ *   - activations NHWC, kernels HWIO [3][3][C_in][C_out] (reference layout);
+ *   - every call is a stateless launch on the caller's stream; nothing here
+ *     allocates device memory: workspaces are caller-owned, sized by the
+ *     *_workspace_bytes queries;
+ *   - every entry point returns 0 on success and a negative ASR_E* code on
+ *     failure; asr_last_error() returns a thread-local message.  Nothing
+ *     throws across the ABI.
+ *
+ * Each declaration cites the reference interface it replaces.
+ */
+#ifndef ASR_H_
+#define ASR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* asr_stream_t; /* a hipStream_t (0 = null stream) */
+
+/* error codes */
+#define ASR_OK 0
+#define ASR_E_ARG (-1)         /* invalid argument (shape, dtype, null)       */
+#define ASR_E_UNSUPPORTED (-2) /* valid but not implemented on this device    */
+#define ASR_E_WORKSPACE (-3)   /* workspace too small                          */
+#define ASR_E_HIP (-4)         /* HIP runtime error (see asr_last_error)       */
+#define ASR_E_DEVICE (-5)      /* no usable gfx950 device                      */
+
+/* activation dtypes */
+#define ASR_F32 0
+#define ASR_BF16 1
+
+/* parametrisations of the antisymmetric kernel (what theta means) */
+#define ASR_PARAM_3BY3 0    /* Conv2DAntisymmetric3By3: a,b,c,d then
+                               input_kernels_for_output_kernel_{o}[3,3,C-o-1]
+                               (…3By3.py:104-141, :219-245)                   */
+#define ASR_PARAM_GENERAL 1 /* Conv2DAntisymmetric (kernel_size 3): per o the
+                               centro_sym_{i}_{j} scalars then
+                               input_kernels_for_output_kernel_{o}[3,3,C-o-1,1]
+                               (…Conv2DAntisymmetric.py:109-145)              */
+
+/* conv modes */
+#define ASR_MODE_EULER 0 /* y = x + h*relu(conv(x)+b); mask = [conv(x)+b > 0]
+                            (tfkeras_resnets.py:69-92)                        */
+#define ASR_MODE_CONV 1  /* y = conv(x) + b  (the layer's call(),
+                            …3By3.py:157-171)                                 */
+
+const char* asr_last_error(void);
+int asr_abi_version(void);
+
+/* Number of gfx950 compute units of the current device (0 on failure). */
+int asr_device_cu_count(void);
+
+/* ------------------------------------------------------------------------
+ * Parametrisation (host-side, pure arithmetic)
+ * --------------------------------------------------------------------- */
+
+/* Number of free kernel parameters (no bias).  3BY3: 4C + 9C(C-1)/2.
+ * Replaces the add_weight calls of …3By3.py:119-124, :219-245 and
+ * …Conv2DAntisymmetric.py:123-128, :234-239. */
+long asr_theta_count(int C, int kind, int antisymmetric);
+
+/* Host: fill the element map of W(theta).
+ *   w_src[e] for every HWIO element e = ((ky*3+kx)*C+i)*C+o:
+ *      (j<<1)|neg  => W[e] = (neg ? -1 : +1) * theta[j]
+ *      -1          => W[e] = gamma (non-trainable centre, …3By3.py:248-250)
+ *   theta_dst[2*j+0], theta_dst[2*j+1]: the (<=2) W elements theta[j] feeds,
+ *      encoded (e<<1)|neg, -1 if unused.  This is the pull-back used for the
+ *      weight-gradient projection (autodiff of …3By3.py:115-141).
+ * w_src: 9*C*C int32, theta_dst: 2*asr_theta_count int32 (host memory). */
+int asr_param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta_dst);
+
+/* Elements of the packed bf16 W consumed by the MFMA kernels. */
+long asr_wpack_elems(int C);
+
+/* Materialise W for L layers in one launch (replaces the per-step
+ * slice/neg/concat/stack graph of …3By3.py:113-141).
+ *   theta:  layer l's theta at theta + l*theta_stride (float32)
+ *   w_src:  device copy of asr_param_map's w_src
+ *   dtype == ASR_BF16: w_out (bf16) gets the MFMA fragment-packed layout,
+ *                      layer l at l*w_stride elements;
+ *   dtype == ASR_F32:  w_out (float) gets plain HWIO [3][3][C][C]. */
+int asr_theta_to_w(const float* theta, long theta_stride, int L, int C, const int32_t* w_src,
+                   float gamma, void* w_out, long w_stride, int dtype, asr_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Fused antisymmetric 3x3 conv / Euler block
+ * --------------------------------------------------------------------- */
+
+/* Forward.  mode ASR_MODE_EULER: y = x + h*relu(conv(x,W)+b), mask written;
+ * ASR_MODE_CONV: y = conv(x,W)+b (mask may be NULL).
+ *   x, y: [N,H,W,C] in dtype;  w: output of asr_theta_to_w for dtype;
+ *   bias: C floats or NULL;  mask: asr_mask_words(N,H,W,C) uint64 words.
+ * Replaces Conv2DAntisymmetric3By3.call (…3By3.py:157-171) and
+ * single_layer_identity_block's relu/scale/add (tfkeras_resnets.py:89-92). */
+int asr_conv_forward(int mode, const void* x, void* y, uint64_t* mask, const void* w,
+                     const float* bias, float h, int N, int H, int W, int C, int dtype,
+                     asr_stream_t stream);
+
+long asr_mask_words(int N, int H, int W, int C);
+
+/* Backward of asr_conv_forward (the autodiff of training.py:300 through the
+ * block).  Given dy = dL/dy:
+ *   EULER: dz = h*dy*mask;  dx = dy + A^T dz = dy - conv(dz,W) + 2*gamma*dz
+ *   CONV:  dz = dy;         dx = A^T dz      =    - conv(dz,W) + 2*gamma*dz
+ *   dW = sum_p patch(x) (x) dz, projected onto theta through theta_dst
+ *   (device copy of asr_param_map's theta_dst); db = sum_p dz.
+ * dtheta / dbias / dx may be NULL to skip that output; dw_hwio (float
+ * [3][3][C][C], may be NULL) receives the unprojected dW.
+ * ws: caller workspace of asr_conv_backward_workspace_bytes bytes. */
+size_t asr_conv_backward_workspace_bytes(int N, int H, int W, int C, int dtype);
+int asr_conv_backward(int mode, const void* dy, const void* x, const uint64_t* mask,
+                      const void* w, const int32_t* theta_dst, long n_theta, float h,
+                      float gamma, int N, int H, int W, int C, int dtype, void* dx,
+                      float* dtheta, float* dbias, float* dw_hwio, void* ws, size_t ws_bytes,
+                      asr_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Whole single-block network (get_single_block_resnet_build_function,
+ * tfkeras_resnets.py:511-604, antisymmetric, num_stages=2, strides (1,1),
+ * no BN/pooling):  normalise -> conv1+relu -> L Euler blocks -> GAP ->
+ * Dense(num_classes, softmax); loss = mean Keras categorical cross-entropy
+ * on the probabilities (training.py:295).
+ * Parameters are ONE float32 buffer in Keras get_weights() order:
+ *   conv1 kernel [3,3,Cin,C], conv1 bias [C],
+ *   L x (theta_3by3 [asr_theta_count(C)], bias [C]),
+ *   fc kernel [C,K], fc bias [K].
+ * --------------------------------------------------------------------- */
+typedef struct asr_net_config {
+  int N, H, W, Cin, C, L, num_classes;
+  float h, gamma;
+  float subtract_mean, divide_by_stddev; /* applied when use_norm != 0   */
+  int use_norm;
+  int dtype;    /* activation dtype: ASR_F32 or ASR_BF16                */
+  int input_u8; /* images are uint8 (1) or float32 (0), NHWC            */
+} asr_net_config;
+
+long asr_net_param_count(const asr_net_config* cfg);
+size_t asr_net_workspace_bytes(const asr_net_config* cfg);
+/* One-time setup of a workspace (uploads the parameter maps; blocking). */
+int asr_net_prepare(const asr_net_config* cfg, void* ws, size_t ws_bytes);
+/* probs: [N, K] float (softmax outputs, the Model's output). */
+int asr_net_forward(const asr_net_config* cfg, const float* params, const void* images,
+                    float* probs, void* ws, size_t ws_bytes, asr_stream_t stream);
+/* One training forward+backward: targets [N,K] float (one-hot);
+ * grads: same layout as params (overwritten); loss: 1 float (batch mean);
+ * probs may be NULL. */
+int asr_net_forward_backward(const asr_net_config* cfg, const float* params, const void* images,
+                             const float* targets, float* grads, float* loss, float* probs,
+                             void* ws, size_t ws_bytes, asr_stream_t stream);
+
+/* tf.train.AdamOptimizer.apply_gradients (training.py:300-301), TF1
+ * epsilon-hat form; step is the 1-based update count; g is multiplied by
+ * grad_scale first (1/world for data-parallel mean). */
+int asr_adam_update(float* params, const float* grads, float* m, float* v, long n, float lr,
+                    float beta1, float beta2, float eps, long step, float grad_scale,
+                    asr_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ASR_H_ */

@@ -1,0 +1,191 @@
+"""GPU parity of the HIP kernels (through the C ABI) against the numpy oracle.
+
+Tolerances (stated per north_star's "within a stated fp32 tolerance"):
+  fp32 path  : |gpu - oracle| <= 2e-5 * max|oracle| + 1e-5 * |oracle|  (fp32 FMA chains of
+               length 9C vs fp64)
+  bf16 path  : the oracle is fed the SAME bf16-rounded inputs and W; the GPU
+               accumulates in fp32 and rounds the output once, so
+               |gpu - oracle| <= 2^-8 * |oracle| + 4e-3 * max|oracle| per element;
+               weight gradients (fp32 outputs) within 1e-3 of max|oracle|.
+Masks must agree exactly wherever |z| > 1e-4 * max|z| (fp32) / 2e-2 * max|z| (bf16).
+"""
+import numpy as np
+import pytest
+
+from helpers import assert_close, bf16_round, decode_mask
+from oracle import asr_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def rt():
+    from differential_equations_resnet_amd import runtime
+    runtime.require_gpu()
+    return runtime
+
+
+def _theta(C, seed, scale=1.0):
+    rng = np.random.default_rng(seed)
+    th = O.init_theta_3by3(C, rng, np.float64)
+    return (O.flatten(th) * scale).astype(np.float32)
+
+
+@pytest.mark.parametrize("C", [4, 16, 64])
+@pytest.mark.parametrize("gamma", [0.0, -0.1])
+def test_theta_to_w_f32_exact(rt, C, gamma):
+    th = _theta(C, C)
+    pm = rt.param_map(C)
+    dev = torch.device("cuda")
+    W = rt.theta_to_w(torch.from_numpy(th).to(dev), C, pm, gamma, rt.ASR_F32)[0].cpu().numpy()
+    want = O.assemble_3by3_literal(O.unflatten(th.astype(np.float64), O.theta_shapes_3by3(C)), gamma)
+    np.testing.assert_array_equal(W, want.astype(np.float32))
+
+
+def test_theta_to_w_multi_layer(rt):
+    C, L = 16, 3
+    n = O.theta_count_3by3(C)
+    stride = n + C
+    flat = np.random.default_rng(5).standard_normal(L * stride).astype(np.float32)
+    pm = rt.param_map(C)
+    W = rt.theta_to_w(torch.from_numpy(flat).cuda(), C, pm, 0.0, rt.ASR_F32, layers=L, theta_stride=stride)
+    W = W.cpu().numpy()
+    src, sign = O.param_map(C)
+    for l in range(L):
+        want = O.assemble_from_map(flat[l * stride:l * stride + n].astype(np.float64), C, src, sign, 0.0)
+        np.testing.assert_array_equal(W[l], want.astype(np.float32))
+
+
+def _run_forward(rt, mode, x_np, th, b, C, gamma, h, dtype):
+    dev = torch.device("cuda")
+    pm = rt.param_map(C)
+    tdt = rt.torch_dtype(dtype)
+    x = torch.from_numpy(x_np).to(dev).to(tdt).contiguous()
+    w = rt.theta_to_w(torch.from_numpy(th).to(dev), C, pm, gamma, dtype)
+    N, H, W_, _ = x_np.shape
+    mask = torch.zeros(rt.mask_words(N, H, W_, C), dtype=torch.int64, device=dev)
+    bias = torch.from_numpy(b).to(dev)
+    y = rt.conv_forward(mode, x, w, bias, h, mask if mode == rt.ASR_MODE_EULER else None)
+    return x, w, y, mask, pm
+
+
+def _oracle_W(th, C, gamma, bf):
+    src, sign = O.param_map(C)
+    W = O.assemble_from_map(th.astype(np.float64), C, src, sign, gamma)
+    return bf16_round(W).astype(np.float64) if bf else W
+
+
+SHAPES_BF16 = [(2, 32, 32, 16), (2, 32, 32, 32), (2, 32, 32, 64), (1, 11, 32, 64), (3, 5, 32, 16)]
+SHAPES_F32 = [(2, 32, 32, 16), (1, 7, 13, 5), (2, 9, 32, 64), (1, 3, 3, 1)]
+
+
+@pytest.mark.parametrize("dtype_name,shape", [("f32", s) for s in SHAPES_F32] + [("bf16", s) for s in SHAPES_BF16])
+@pytest.mark.parametrize("mode_name", ["euler", "conv"])
+@pytest.mark.parametrize("gamma,h", [(0.0, 0.25), (-0.1, 1.0)])
+def test_forward_parity(rt, dtype_name, shape, mode_name, gamma, h):
+    N, H, W_, C = shape
+    bf = dtype_name == "bf16"
+    dtype = rt.ASR_BF16 if bf else rt.ASR_F32
+    mode = rt.ASR_MODE_EULER if mode_name == "euler" else rt.ASR_MODE_CONV
+    rng = np.random.default_rng(hash((shape, mode_name, gamma)) % 2**32)
+    x_np = rng.standard_normal(shape).astype(np.float32)
+    th = _theta(C, 7, scale=1.0)
+    b = (rng.standard_normal(C) * 0.1).astype(np.float32)
+    x, w, y, mask, _ = _run_forward(rt, mode, x_np, th, b, C, gamma, h, dtype)
+    xo = bf16_round(x_np).astype(np.float64) if bf else x_np.astype(np.float64)
+    Wo = _oracle_W(th, C, gamma, bf)
+    z = O.conv2d_same(xo, Wo) + b
+    if mode == rt.ASR_MODE_EULER:
+        want = xo + h * np.maximum(z, 0)
+    else:
+        want = z
+    got = y.float().cpu().numpy()
+    scale = np.abs(want).max()
+    if bf:
+        assert_close(got, want, rtol=2 ** -8, atol=4e-3 * scale, what="bf16 forward")
+    else:
+        assert_close(got, want, rtol=1e-5, atol=2e-5 * scale, what="f32 forward")
+    if mode == rt.ASR_MODE_EULER:
+        m = decode_mask(mask.cpu().numpy(), N, H, W_, C)
+        sure = np.abs(z) > (2e-2 if bf else 1e-4) * np.abs(z).max()
+        assert np.array_equal(m[sure], (z > 0)[sure]), "relu mask mismatch"
+
+
+@pytest.mark.parametrize("dtype_name,shape", [("f32", s) for s in SHAPES_F32] + [("bf16", s) for s in SHAPES_BF16])
+@pytest.mark.parametrize("mode_name", ["euler", "conv"])
+@pytest.mark.parametrize("gamma,h", [(0.0, 0.25), (-0.1, 1.0)])
+def test_backward_parity(rt, dtype_name, shape, mode_name, gamma, h):
+    N, H, W_, C = shape
+    bf = dtype_name == "bf16"
+    dtype = rt.ASR_BF16 if bf else rt.ASR_F32
+    mode = rt.ASR_MODE_EULER if mode_name == "euler" else rt.ASR_MODE_CONV
+    rng = np.random.default_rng(hash((shape, mode_name, gamma, 1)) % 2**32)
+    x_np = rng.standard_normal(shape).astype(np.float32)
+    dy_np = rng.standard_normal(shape).astype(np.float32)
+    th = _theta(C, 11)
+    b = (rng.standard_normal(C) * 0.1).astype(np.float32)
+    x, w, y, mask, pm = _run_forward(rt, rt.ASR_MODE_EULER, x_np, th, b, C, gamma, h, dtype)
+    dev = torch.device("cuda")
+    dy = torch.from_numpy(dy_np).to(dev).to(rt.torch_dtype(dtype)).contiguous()
+    dx, dth, db, dw = rt.conv_backward(mode, dy, x, mask if mode == rt.ASR_MODE_EULER else None, w, pm, h, gamma,
+                                       want_dw=True)
+    # oracle, fed the GPU's mask (the mask itself is checked in test_forward_parity)
+    xo = bf16_round(x_np).astype(np.float64) if bf else x_np.astype(np.float64)
+    dyo = bf16_round(dy_np).astype(np.float64) if bf else dy_np.astype(np.float64)
+    Wo = _oracle_W(th, C, gamma, bf)
+    if mode == rt.ASR_MODE_EULER:
+        m = decode_mask(mask.cpu().numpy(), N, H, W_, C)
+        dz_f = h * dyo * m
+    else:
+        dz_f = dyo
+    dz_q = bf16_round(dz_f).astype(np.float64) if bf else dz_f
+    dx_want = (dyo if mode == rt.ASR_MODE_EULER else 0.0) - O.conv2d_same(dz_q, Wo) + 2 * gamma * dz_q
+    dW_want = O.conv2d_backprop_filter(xo, dz_q)
+    db_want = dz_f.sum(axis=(0, 1, 2))
+    src, sign = O.param_map(C)
+    dth_want = O.project_dW(dW_want, src, sign, pm.n_theta)
+    sc = np.abs(dx_want).max()
+    if bf:
+        assert_close(dx.float().cpu().numpy(), dx_want, rtol=2 ** -8, atol=4e-3 * sc, what="bf16 dx")
+        tol = 1e-3
+    else:
+        assert_close(dx.cpu().numpy(), dx_want, rtol=1e-5, atol=2e-5 * sc, what="f32 dx")
+        tol = 2e-5
+    assert_close(dw.cpu().numpy(), dW_want, rtol=0, atol=tol * np.abs(dW_want).max(), what="dW")
+    assert_close(dth.cpu().numpy(), dth_want, rtol=0, atol=tol * np.abs(dth_want).max(), what="dtheta")
+    assert_close(db.cpu().numpy(), db_want, rtol=0, atol=2e-5 * max(np.abs(db_want).max(), 1), what="dbias")
+
+
+def test_dgrad_identity_transpose(rt):
+    """The kernel's dgrad (-A + 2 gamma I applied with the SAME W) equals the
+    generic Conv2DBackpropInput of the oracle (no antisymmetry assumed)."""
+    N, H, W_, C = 2, 32, 32, 16
+    rng = np.random.default_rng(3)
+    th = _theta(C, 3)
+    x_np = rng.standard_normal((N, H, W_, C)).astype(np.float32)
+    dz_np = rng.standard_normal((N, H, W_, C)).astype(np.float32)
+    x, w, y, mask, pm = _run_forward(rt, rt.ASR_MODE_CONV, x_np, th, np.zeros(C, np.float32), C, -0.3, 1.0,
+                                     rt.ASR_F32)
+    dz = torch.from_numpy(dz_np).cuda()
+    dx, *_ = rt.conv_backward(rt.ASR_MODE_CONV, dz, x, None, w, pm, 1.0, -0.3, want_dtheta=False, want_dbias=False)
+    Wo = _oracle_W(th, C, -0.3, False)
+    want = O.conv2d_backprop_input(dz_np.astype(np.float64), Wo, x_np.shape)
+    assert_close(dx.cpu().numpy(), want, rtol=1e-5, atol=2e-5 * np.abs(want).max(), what="dgrad")
+
+
+def test_adam_matches_tf1(rt):
+    rng = np.random.default_rng(0)
+    n = 1000
+    p = rng.standard_normal(n).astype(np.float32)
+    ps = [p.astype(np.float64).copy()]
+    ms, vs = [np.zeros(n)], [np.zeros(n)]
+    P = torch.from_numpy(p).cuda()
+    M = torch.zeros(n, device="cuda")
+    V = torch.zeros(n, device="cuda")
+    for t in range(1, 4):
+        g = rng.standard_normal(n).astype(np.float32)
+        rt.adam_update(P, torch.from_numpy(g).cuda(), M, V, 1e-3, 0.9, 0.999, 1e-7, t, 1.0)
+        O.adam_tf1(ps, [g.astype(np.float64)], ms, vs, t, 1e-3, 0.9, 0.999, 1e-7)
+    assert_close(P.cpu().numpy(), ps[0], rtol=1e-6, atol=1e-7, what="adam")

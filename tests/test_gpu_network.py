@@ -1,0 +1,93 @@
+"""GPU parity of the native network executor (asr_net_*) against the oracle's
+restatement of get_single_block_resnet_build_function + Keras CE + TF1 Adam.
+
+Tolerances: fp32 — probabilities and loss within 1e-5 relative, every
+gradient within 1e-4 of its tensor's max |oracle| value; bf16 — probabilities
+within 2e-2 absolute, loss within 1% relative, gradients: cosine similarity
+with the fp64 oracle >= 0.99 per parameter tensor.
+"""
+import numpy as np
+import pytest
+
+from helpers import assert_close
+from oracle import asr_oracle as O
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def _setup(C=16, L=3, N=4, H=32, W=32, h=0.5, gamma=0.0, seed=0):
+    spec = O.NetSpec(C=C, L=L, h=h, gamma=gamma, H=H, W=W)
+    rng = np.random.default_rng(seed)
+    params = O.init_params(spec, rng, np.float64, bias_std=0.05)
+    params = [p.astype(np.float32).astype(np.float64) for p in params]
+    imgs = rng.integers(0, 256, (N, H, W, 3)).astype(np.uint8)
+    labels = rng.integers(0, 10, N)
+    onehot = np.eye(10)[labels]
+    return spec, params, imgs, onehot
+
+
+def _executor(spec, N, dtype):
+    from differential_equations_resnet_amd.runtime import NetExecutor
+    return NetExecutor(N, spec.H, spec.W, 3, spec.C, spec.L, spec.num_classes, spec.h, spec.gamma,
+                       subtract_mean=127.5, divide_by_stddev=127.5, dtype=dtype, input_u8=True)
+
+
+@pytest.mark.parametrize("gamma", [0.0, -0.05])
+def test_network_fp32_parity(gamma):
+    spec, params, imgs, onehot = _setup(gamma=gamma)
+    N = imgs.shape[0]
+    ex = _executor(spec, N, "float32")
+    flat = torch.from_numpy(O.flatten(params).astype(np.float32)).cuda()
+    assert flat.numel() == ex.n_params == spec.n_params()
+    probs_gpu = ex.forward(flat, torch.from_numpy(imgs).cuda()).cpu().numpy()
+    probs, cache = O.net_forward(spec, params, imgs)
+    assert_close(probs_gpu, probs, rtol=1e-5, atol=1e-6, what="probs")
+    loss, grads = ex.forward_backward(flat, torch.from_numpy(imgs).cuda(),
+                                      torch.from_numpy(onehot.astype(np.float32)).cuda(), want_probs=True)
+    want_loss = O.net_loss(probs, onehot)
+    assert abs(loss.item() - want_loss) <= 1e-5 * abs(want_loss)
+    g_want = O.net_backward(spec, params, cache, onehot)
+    g_got = O.unflatten(grads.cpu().numpy().astype(np.float64), [p.shape for p in params])
+    for i, (a, b) in enumerate(zip(g_got, g_want)):
+        assert_close(a, b, rtol=0, atol=1e-4 * max(np.abs(b).max(), 1e-12), what=f"grad[{i}] {b.shape}")
+
+
+def test_network_bf16_close():
+    spec, params, imgs, onehot = _setup(C=16, L=4, N=8, h=0.25)
+    N = imgs.shape[0]
+    ex = _executor(spec, N, "bfloat16")
+    flat = torch.from_numpy(O.flatten(params).astype(np.float32)).cuda()
+    probs_gpu = ex.forward(flat, torch.from_numpy(imgs).cuda()).cpu().numpy()
+    probs, cache = O.net_forward(spec, params, imgs)
+    assert np.abs(probs_gpu - probs).max() < 2e-2
+    loss, grads = ex.forward_backward(flat, torch.from_numpy(imgs).cuda(),
+                                      torch.from_numpy(onehot.astype(np.float32)).cuda())
+    want_loss = O.net_loss(probs, onehot)
+    assert abs(loss.item() - want_loss) <= 1e-2 * abs(want_loss)
+    g_want = O.net_backward(spec, params, cache, onehot)
+    g_got = O.unflatten(grads.cpu().numpy().astype(np.float64), [p.shape for p in params])
+    for i, (a, b) in enumerate(zip(g_got, g_want)):
+        if np.abs(b).max() == 0:
+            continue
+        cos = (a * b).sum() / (np.linalg.norm(a) * np.linalg.norm(b) + 1e-30)
+        assert cos >= 0.99, f"grad[{i}] {b.shape}: cosine {cos}"
+
+
+def test_network_train_steps_decrease_loss():
+    """A few Adam steps on one fixed batch must reduce the loss (plumbing of
+    forward_backward + asr_adam_update)."""
+    from differential_equations_resnet_amd import runtime
+    spec, params, imgs, onehot = _setup(C=16, L=3, N=16, h=0.5, seed=3)
+    ex = _executor(spec, 16, "bfloat16")
+    flat = torch.from_numpy(O.flatten(params).astype(np.float32)).cuda()
+    m = torch.zeros_like(flat)
+    v = torch.zeros_like(flat)
+    x = torch.from_numpy(imgs).cuda()
+    t = torch.from_numpy(onehot.astype(np.float32)).cuda()
+    losses = []
+    for step in range(1, 21):
+        loss, grads = ex.forward_backward(flat, x, t)
+        losses.append(loss.item())
+        runtime.adam_update(flat, grads, m, v, 1e-3, 0.9, 0.999, 1e-7, step)
+    assert losses[-1] < 0.7 * losses[0], losses
