@@ -16,24 +16,33 @@ namespace asr {
 // asr_theta.hip
 long theta_count(int C, int kind, int antisymmetric);
 int param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta_dst);
-int reduce_and_project(const float* slabs, int P, long E, const float* db_slabs, int PB, int Cb,
-                       const int32_t* theta_dst, long n_theta, float* dtheta, float* dbias, float* dw_out, float* ws,
-                       hipStream_t s);
-size_t reduce_ws_bytes(int P, long E);
+int reduce_and_project(const float* slabs, int P, long E, int Cb, const int32_t* theta_dst, long n_theta,
+                       float* dtheta, float* dbias, float* dw_out, float* ws, hipStream_t s);
+size_t reduce_ws_bytes(int P, long ES);
 // asr_conv_mfma.hip
 bool mfma_supported(int C, int W);
 int conv_mfma(int mode, const void* xin, void* out, uint64_t* mask, const void* w, const float* bias, float h,
               float two_gamma, int N, int H, int W, int C, hipStream_t s);
 int wgrad_mfma(int mode, const void* x, const void* dy, const uint64_t* mask, float h, int N, int H, int W, int C,
-               float* slabs, float* db_slabs, int* nslabs, hipStream_t s);
+               float* slabs, int* nslabs, hipStream_t s);
 // asr_conv_f32.hip
 int conv_f32(int fmode, const void* xin, void* out, uint64_t* mask, const float* w, const float* bias, float h,
              float two_gamma, const float* dy, int N, int H, int W, int Ci, int Co, int out_bf16, hipStream_t s);
 int make_dz(int fmode, const void* dy, const uint64_t* mask, const void* relu_src, float h, int N, int H, int W, int C,
             int src_bf16, float* dz, hipStream_t s);
 int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, int Ci, int Co, float* slabs,
-              float* db_slabs, int* nslabs, hipStream_t s);
+              int* nslabs, hipStream_t s);
 int wgrad_f32_chunks(int N, int H);
+// asr_stem_head.hip
+bool stem_supported(int Cin, int H, int W, int C);
+int stem_forward(const void* img, int input_u8, const float* w1, const float* b1, int N, int H, int W, int Cin, int C,
+                 float mean, float inv_std, int use_norm, void* out, int out_bf16, hipStream_t s);
+int stem_wgrad(const void* img, int input_u8, const void* dx1, const void* x1, int act_bf16, int N, int H, int W,
+               int Cin, int C, float mean, float inv_std, int use_norm, float* slabs, int* nslabs, hipStream_t s);
+int head(const void* xL, int act_bf16, const float* fck, const float* fcb, const float* targets, int N, int HW, int C,
+         int K, float* probs, float* loss_per, float* dlogits, float* gap, void* dxL, hipStream_t s);
+int head_param_grads(const float* gap, const float* dlogits, int N, int C, int K, float* dfck, float* dfcb,
+                     const float* loss_per, float* loss_out, hipStream_t s);
 
 constexpr int kMaxSlabsApi = 512;  // matches asr_conv_mfma.hip kMaxSlabs
 enum { F_EULER = 0, F_CONV = 1, F_RELU = 2, B_EULER = 3, B_CONV = 4 };
@@ -48,7 +57,7 @@ static int check_shape(int N, int H, int W, int C) {
 // conv backward workspace
 // ---------------------------------------------------------------------------
 struct BwdWs {
-  size_t dz, slabs, db, red, total;
+  size_t dz, slabs, red, total;
 };
 
 static BwdWs bwd_ws_layout(int N, int H, int W, int C, int dtype) {
@@ -60,11 +69,9 @@ static BwdWs bwd_ws_layout(int N, int H, int W, int C, int dtype) {
   b.dz = off;
   if (dtype == ASR_F32) off += align_up((size_t)P * 4, 256);
   b.slabs = off;
-  off += align_up((size_t)nsl * E * 4, 256);
-  b.db = off;
-  off += align_up((size_t)nsl * C * 4, 256);
+  off += align_up((size_t)nsl * (E + C) * 4, 256);
   b.red = off;
-  off += align_up(reduce_ws_bytes(nsl, E), 256);
+  off += align_up(reduce_ws_bytes(nsl, E + C), 256);
   b.total = off;
   return b;
 }
@@ -76,163 +83,30 @@ static int conv_backward_impl(int mode, const void* dy, const void* x, const uin
   const BwdWs L = bwd_ws_layout(N, H, W, C, dtype);
   unsigned char* base = (unsigned char*)ws;
   float* slabs = (float*)(base + L.slabs);
-  float* dbs = (float*)(base + L.db);
   float* red = (float*)(base + L.red);
   const bool need_w = dtheta || dbias || dw_hwio;
   const int cm = (mode == ASR_MODE_EULER) ? 2 : 3;  // BWD_EULER / BWD_CONV
   int nsl = 0;
   if (dtype == ASR_BF16) {
     if (dx) ASR_TRY(conv_mfma(cm, dy, dx, (uint64_t*)mask, w, nullptr, h, 2.f * gamma, N, H, W, C, s));
-    if (need_w) ASR_TRY(wgrad_mfma(cm, x, dy, mask, h, N, H, W, C, slabs, dbs, &nsl, s));
+    if (need_w) ASR_TRY(wgrad_mfma(cm, x, dy, mask, h, N, H, W, C, slabs, &nsl, s));
   } else {
     float* dz = (float*)(base + L.dz);
     ASR_TRY(make_dz(mode == ASR_MODE_EULER ? F_EULER : F_CONV, dy, mask, nullptr, h, N, H, W, C, 0, dz, s));
     if (dx)
       ASR_TRY(conv_f32(mode == ASR_MODE_EULER ? B_EULER : B_CONV, dz, dx, nullptr, (const float*)w, nullptr, h,
                        2.f * gamma, (const float*)dy, N, H, W, C, C, 0, s));
-    if (need_w) ASR_TRY(wgrad_f32(x, 0, dz, N, H, W, C, C, slabs, dbs, &nsl, s));
+    if (need_w) ASR_TRY(wgrad_f32(x, 0, dz, N, H, W, C, C, slabs, &nsl, s));
   }
   if (need_w)
-    ASR_TRY(reduce_and_project(slabs, nsl, 9L * C * C, dbs, nsl, C, dtheta ? theta_dst : nullptr, n_theta, dtheta,
-                               dbias, dw_hwio, red, s));
+    ASR_TRY(reduce_and_project(slabs, nsl, 9L * C * C, C, dtheta ? theta_dst : nullptr, n_theta, dtheta, dbias,
+                               dw_hwio, red, s));
   return ASR_OK;
 }
 
 // ---------------------------------------------------------------------------
-// stem / head / optimizer kernels
+// optimizer
 // ---------------------------------------------------------------------------
-template <typename Tin>
-__global__ void k_normalize(const Tin* __restrict__ img, long n, float mean, float inv_std, int use_norm,
-                            float* __restrict__ out) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    float v = (float)img[i];
-    if (use_norm) v = (v - mean) * inv_std;
-    out[i] = v;
-  }
-}
-
-// GAP -> Dense(K) -> softmax [-> Keras CE loss and its gradient] per image.
-// models/tfkeras_resnets.py:595-597; loss training.py:295 (TF 1.12
-// keras.backend.categorical_crossentropy: renormalise, clip [1e-7, 1-1e-7],
-// -sum t*log q; clip gradient passes on the closed interval).
-template <typename T>
-__global__ __launch_bounds__(256) void k_head(const T* __restrict__ xL, const float* __restrict__ fck,
-                                              const float* __restrict__ fcb, const float* __restrict__ targets,
-                                              int HW, int C, int K, float inv_n, float* __restrict__ probs,
-                                              float* __restrict__ loss_per, float* __restrict__ dlogits,
-                                              float* __restrict__ gap, T* __restrict__ dxL) {
-  __shared__ float red[256];
-  __shared__ float gs[256];
-  __shared__ float lg[256];
-  __shared__ float dl[256];
-  const int n = blockIdx.x, tid = threadIdx.x;
-  const int PL = C <= 256 ? max(1, 256 / C) : 1;
-  float s = 0.f;
-  if (tid < PL * C) {
-    const int c = tid % C, pl = tid / C;
-    const T* base = xL + (long)n * HW * C;
-    for (int p = pl; p < HW; p += PL) s += to_f32(base[(long)p * C + c]);
-  }
-  red[tid] = s;
-  __syncthreads();
-  if (tid < C) {
-    float t = 0.f;
-    for (int pl = 0; pl < PL; ++pl) t += red[pl * C + tid];
-    t /= (float)HW;
-    gs[tid] = t;
-    if (gap) gap[(long)n * C + tid] = t;
-  }
-  __syncthreads();
-  if (tid < K) {
-    float a = fcb ? fcb[tid] : 0.f;
-    for (int c = 0; c < C; ++c) a = fmaf(gs[c], fck[(long)c * K + tid], a);
-    lg[tid] = a;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    float m = -INFINITY;
-    for (int k = 0; k < K; ++k) m = fmaxf(m, lg[k]);
-    float S = 0.f;
-    for (int k = 0; k < K; ++k) {
-      const float e = expf(lg[k] - m);
-      lg[k] = e;
-      S += e;
-    }
-    float s2 = 0.f;
-    for (int k = 0; k < K; ++k) {
-      lg[k] /= S;  // probabilities
-      s2 += lg[k];
-      if (probs) probs[(long)n * K + k] = lg[k];
-    }
-    if (targets) {
-      const float eps = 1e-7f;
-      float loss = 0.f, sdq_p = 0.f;
-      for (int k = 0; k < K; ++k) {
-        const float q = lg[k] / s2;
-        const float qc = fminf(fmaxf(q, eps), 1.f - eps);
-        const float t = targets[(long)n * K + k];
-        loss -= t * logf(qc);
-        const float dq = (q >= eps && q <= 1.f - eps) ? -t / qc * inv_n : 0.f;
-        dl[k] = dq;
-        sdq_p += dq * lg[k];
-      }
-      if (loss_per) loss_per[n] = loss;
-      float sp_dp = 0.f;
-      for (int k = 0; k < K; ++k) {
-        const float dp = dl[k] / s2 - sdq_p / (s2 * s2);
-        dl[k] = dp;
-        sp_dp += lg[k] * dp;
-      }
-      for (int k = 0; k < K; ++k) {
-        const float d = lg[k] * (dl[k] - sp_dp);
-        dl[k] = d;
-        if (dlogits) dlogits[(long)n * K + k] = d;
-      }
-    }
-  }
-  __syncthreads();
-  if (targets && dxL) {
-    if (tid < C) {
-      float a = 0.f;
-      for (int k = 0; k < K; ++k) a = fmaf(dl[k], fck[(long)tid * K + k], a);
-      gs[tid] = a / (float)HW;
-    }
-    __syncthreads();
-    T* o = dxL + (long)n * HW * C;
-    for (long i = tid; i < (long)HW * C; i += 256) o[i] = from_f32<T>(gs[i % C]);
-  }
-}
-
-__global__ __launch_bounds__(256) void k_head_param_grads(const float* __restrict__ gap,
-                                                          const float* __restrict__ dlogits, int N, int C, int K,
-                                                          float* __restrict__ dfck, float* __restrict__ dfcb,
-                                                          const float* __restrict__ loss_per,
-                                                          float* __restrict__ loss_out) {
-  __shared__ float red[256];
-  const int tid = threadIdx.x;
-  for (int idx = tid; idx < C * K + K; idx += 256) {
-    float a = 0.f;
-    if (idx < C * K) {
-      const int c = idx / K, k = idx % K;
-      for (int n = 0; n < N; ++n) a = fmaf(gap[(long)n * C + c], dlogits[(long)n * K + k], a);
-      dfck[idx] = a;
-    } else {
-      const int k = idx - C * K;
-      for (int n = 0; n < N; ++n) a += dlogits[(long)n * K + k];
-      dfcb[k] = a;
-    }
-  }
-  float s = 0.f;
-  for (int n = tid; n < N; n += 256) s += loss_per[n];
-  red[tid] = s;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (tid < w) red[tid] += red[tid + w];
-    __syncthreads();
-  }
-  if (tid == 0) *loss_out = red[0] / (float)N;
-}
-
 __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                        float* __restrict__ v, long n, float lr_t, float b1, float b2, float eps, float gscale) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -248,13 +122,23 @@ __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float
 // ---------------------------------------------------------------------------
 // network layout
 // ---------------------------------------------------------------------------
+template <typename Tin>
+__global__ void k_normalize(const Tin* __restrict__ img, long n, float mean, float inv_std, int use_norm,
+                            float* __restrict__ out) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float v = (float)img[i];
+    if (use_norm) v = (v - mean) * inv_std;
+    out[i] = v;
+  }
+}
+
 struct NetLayout {
   long ntheta, P, E, wstride;  // wstride in elements of the W dtype
   long off_c1k, off_c1b, off_blk, blk_stride, off_fck, off_fcb, nparams;
-  size_t w_src, theta_dst, wbuf, x0, acts, masks, dxa, dxb, dz, slabs, dbs, red, probs, loss_per, dlogits, gap, loss,
-      total;
+  size_t w_src, theta_dst, wbuf, x0, acts, masks, dxa, dxb, bwdws, slabs, red, probs, loss_per, dlogits, gap, total;
   long mask_words;
   int act_bytes;
+  bool fast_stem;
 };
 
 static int net_check(const asr_net_config* c) {
@@ -284,6 +168,7 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.off_fcb = L.off_fck + (long)C * K;
   L.nparams = L.off_fcb + K;
   L.mask_words = (long)c->N * c->H * ((c->W + 15) / 16) * ((C + 15) / 16) * 4;
+  L.fast_stem = stem_supported(c->Cin, c->H, c->W, C);
   size_t off = 0;
   auto take = [&](size_t bytes) {
     size_t o = off;
@@ -293,21 +178,21 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.w_src = take((size_t)L.E * 4);
   L.theta_dst = take((size_t)L.ntheta * 2 * 4);
   L.wbuf = take((size_t)c->L * L.wstride * L.act_bytes);
-  L.x0 = take((size_t)c->N * c->H * c->W * c->Cin * 4);
+  L.x0 = take(L.fast_stem ? 0 : (size_t)c->N * c->H * c->W * c->Cin * 4);
   L.acts = take((size_t)(c->L + 1) * L.P * L.act_bytes);
   L.masks = take((size_t)c->L * L.mask_words * 8);
   L.dxa = take((size_t)L.P * L.act_bytes);
   L.dxb = take((size_t)L.P * L.act_bytes);
-  L.dz = take((size_t)L.P * 4);
-  const long Emax = std::max(L.E, 9L * c->Cin * C);
-  L.slabs = take((size_t)kMaxSlabsApi * Emax * 4);
-  L.dbs = take((size_t)kMaxSlabsApi * C * 4);
-  L.red = take(reduce_ws_bytes(kMaxSlabsApi, Emax));
+  // per-block backward workspace (asr_conv_backward layout), reused by the stem
+  const BwdWs bw = bwd_ws_layout(c->N, c->H, c->W, C, c->dtype);
+  const long E1 = 9L * c->Cin * C;
+  const size_t stem_ws = align_up((size_t)L.P * 4, 256) + align_up((size_t)kMaxSlabsApi * (E1 + C) * 4, 256) +
+                         align_up(reduce_ws_bytes(kMaxSlabsApi, E1 + C), 256);
+  L.bwdws = take(std::max(bw.total, stem_ws));
   L.probs = take((size_t)c->N * K * 4);
   L.loss_per = take((size_t)c->N * 4);
   L.dlogits = take((size_t)c->N * K * 4);
   L.gap = take((size_t)c->N * C * 4);
-  L.loss = take(4);
   L.total = off;
   return L;
 }
@@ -316,30 +201,34 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
                             bool training, unsigned char* ws, hipStream_t s) {
   const int C = c->C, N = c->N, H = c->H, W = c->W;
   const bool bf = c->dtype == ASR_BF16;
+  const float inv_std = c->use_norm ? 1.f / c->divide_by_stddev : 1.f;
   // 1. materialise W for all L blocks (one launch)
   ASR_TRY(asr_theta_to_w(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src), c->gamma,
                          ws + L.wbuf, L.wstride, c->dtype, s));
-  // 2. input normalisation (tfkeras_resnets.py:555-559)
-  const long nin = (long)N * H * W * c->Cin;
-  float* x0 = (float*)(ws + L.x0);
-  const unsigned gn = (unsigned)std::min<long>((nin + 255) / 256, 4096);
-  const float inv_std = c->use_norm ? 1.f / c->divide_by_stddev : 1.f;
-  if (c->input_u8)
-    hipLaunchKernelGGL(k_normalize<uint8_t>, dim3(gn), dim3(256), 0, s, (const uint8_t*)images, nin,
-                       c->subtract_mean, inv_std, c->use_norm, x0);
-  else
-    hipLaunchKernelGGL(k_normalize<float>, dim3(gn), dim3(256), 0, s, (const float*)images, nin, c->subtract_mean,
-                       inv_std, c->use_norm, x0);
-  ASR_LAUNCH_CHECK("k_normalize");
-  // 3. stem conv1 + relu (tfkeras_resnets.py:563-572)
   unsigned char* acts = ws + L.acts;
   auto act = [&](int i) -> unsigned char* {
     const int slot = training ? i : (i & 1);
     return acts + (size_t)slot * L.P * L.act_bytes;
   };
-  ASR_TRY(conv_f32(F_RELU, x0, act(0), nullptr, params + L.off_c1k, params + L.off_c1b, 1.f, 0.f, nullptr, N, H, W,
-                   c->Cin, C, bf ? 1 : 0, s));
-  // 4. L Euler blocks (tfkeras_resnets.py:579-582 -> :28-94)
+  // 2. normalisation + conv1 + relu (tfkeras_resnets.py:555-572)
+  if (L.fast_stem) {
+    ASR_TRY(stem_forward(images, c->input_u8, params + L.off_c1k, params + L.off_c1b, N, H, W, c->Cin, C,
+                         c->subtract_mean, inv_std, c->use_norm, act(0), bf ? 1 : 0, s));
+  } else {
+    const long nin = (long)N * H * W * c->Cin;
+    float* x0 = (float*)(ws + L.x0);
+    const unsigned gn = (unsigned)std::min<long>((nin + 255) / 256, 4096);
+    if (c->input_u8)
+      hipLaunchKernelGGL(k_normalize<uint8_t>, dim3(gn), dim3(256), 0, s, (const uint8_t*)images, nin,
+                         c->subtract_mean, inv_std, c->use_norm, x0);
+    else
+      hipLaunchKernelGGL(k_normalize<float>, dim3(gn), dim3(256), 0, s, (const float*)images, nin,
+                         c->subtract_mean, inv_std, c->use_norm, x0);
+    ASR_LAUNCH_CHECK("k_normalize");
+    ASR_TRY(conv_f32(F_RELU, x0, act(0), nullptr, params + L.off_c1k, params + L.off_c1b, 1.f, 0.f, nullptr, N, H,
+                     W, c->Cin, C, bf ? 1 : 0, s));
+  }
+  // 3. L Euler blocks (tfkeras_resnets.py:579-582 -> :28-94)
   for (int l = 0; l < c->L; ++l) {
     const float* bias = params + L.off_blk + (long)l * L.blk_stride + L.ntheta;
     const unsigned char* wl = ws + L.wbuf + (size_t)l * L.wstride * L.act_bytes;
@@ -437,16 +326,8 @@ int asr_net_forward(const asr_net_config* cfg, const float* params, const void* 
   unsigned char* b = (unsigned char*)ws;
   ASR_TRY(net_forward_impl(cfg, L, params, images, false, b, s));
   const unsigned char* xL = b + L.acts + (size_t)(cfg->L & 1) * L.P * L.act_bytes;
-  const int HW = cfg->H * cfg->W;
-  if (cfg->dtype == ASR_BF16)
-    hipLaunchKernelGGL(k_head<bf16>, dim3(cfg->N), dim3(256), 0, s, (const bf16*)xL, params + L.off_fck,
-                       params + L.off_fcb, nullptr, HW, cfg->C, cfg->num_classes, 0.f, probs, nullptr, nullptr,
-                       nullptr, nullptr);
-  else
-    hipLaunchKernelGGL(k_head<float>, dim3(cfg->N), dim3(256), 0, s, (const float*)xL, params + L.off_fck,
-                       params + L.off_fcb, nullptr, HW, cfg->C, cfg->num_classes, 0.f, probs, nullptr, nullptr,
-                       nullptr, nullptr);
-  ASR_LAUNCH_CHECK("k_head");
+  ASR_TRY(head(xL, cfg->dtype == ASR_BF16, params + L.off_fck, params + L.off_fcb, nullptr, cfg->N, cfg->H * cfg->W,
+               cfg->C, cfg->num_classes, probs, nullptr, nullptr, nullptr, nullptr, s));
   return ASR_OK;
 }
 
@@ -467,20 +348,10 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   unsigned char* dcur = b + L.dxa;
   unsigned char* dnext = b + L.dxb;
   float* probs_ws = probs ? probs : (float*)(b + L.probs);
-  const int HW = H * W;
-  if (bf)
-    hipLaunchKernelGGL(k_head<bf16>, dim3(N), dim3(256), 0, s, (const bf16*)act(cfg->L), params + L.off_fck,
-                       params + L.off_fcb, targets, HW, C, K, 1.f / N, probs_ws, (float*)(b + L.loss_per),
-                       (float*)(b + L.dlogits), (float*)(b + L.gap), (bf16*)dcur);
-  else
-    hipLaunchKernelGGL(k_head<float>, dim3(N), dim3(256), 0, s, (const float*)act(cfg->L), params + L.off_fck,
-                       params + L.off_fcb, targets, HW, C, K, 1.f / N, probs_ws, (float*)(b + L.loss_per),
-                       (float*)(b + L.dlogits), (float*)(b + L.gap), (float*)dcur);
-  ASR_LAUNCH_CHECK("k_head");
-  hipLaunchKernelGGL(k_head_param_grads, dim3(1), dim3(256), 0, s, (const float*)(b + L.gap),
-                     (const float*)(b + L.dlogits), N, C, K, grads + L.off_fck, grads + L.off_fcb,
-                     (const float*)(b + L.loss_per), loss);
-  ASR_LAUNCH_CHECK("k_head_param_grads");
+  ASR_TRY(head(act(cfg->L), bf, params + L.off_fck, params + L.off_fcb, targets, N, H * W, C, K, probs_ws,
+               (float*)(b + L.loss_per), (float*)(b + L.dlogits), (float*)(b + L.gap), dcur, s));
+  ASR_TRY(head_param_grads((const float*)(b + L.gap), (const float*)(b + L.dlogits), N, C, K, grads + L.off_fck,
+                           grads + L.off_fcb, (const float*)(b + L.loss_per), loss, s));
   // Euler blocks, last to first
   const int32_t* theta_dst = (const int32_t*)(b + L.theta_dst);
   for (int l = cfg->L - 1; l >= 0; --l) {
@@ -488,18 +359,25 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
     const uint64_t* mask = (const uint64_t*)(b + L.masks) + (size_t)l * L.mask_words;
     float* dth = grads + L.off_blk + (long)l * L.blk_stride;
     ASR_TRY(conv_backward_impl(ASR_MODE_EULER, dcur, act(l), mask, wl, theta_dst, L.ntheta, cfg->h, cfg->gamma, N, H,
-                               W, C, cfg->dtype, dnext, dth, dth + L.ntheta, nullptr, b + L.dz, s));
+                               W, C, cfg->dtype, dnext, dth, dth + L.ntheta, nullptr, b + L.bwdws, s));
     std::swap(dcur, dnext);
   }
-  // stem: dz1 = dx1 * [x1 > 0]; conv1 weight gradient from the normalised input
-  float* dz = (float*)(b + L.dz);
-  ASR_TRY(make_dz(F_RELU, dcur, nullptr, act(0), 1.f, N, H, W, C, bf ? 1 : 0, dz, s));
+  // stem: dz1 = dx1 * [x1 > 0]; conv1 weight/bias gradient from the normalised input
+  const long E1 = 9L * cfg->Cin * C;
+  unsigned char* sw = b + L.bwdws;
+  float* dz = (float*)sw;
+  float* slabs = (float*)(sw + align_up((size_t)L.P * 4, 256));
+  float* red = (float*)(sw + align_up((size_t)L.P * 4, 256) + align_up((size_t)kMaxSlabsApi * (E1 + C) * 4, 256));
   int nsl = 0;
-  float* slabs = (float*)(b + L.slabs);
-  float* dbs = (float*)(b + L.dbs);
-  ASR_TRY(wgrad_f32(b + L.x0, 0, dz, N, H, W, cfg->Cin, C, slabs, dbs, &nsl, s));
-  ASR_TRY(reduce_and_project(slabs, nsl, 9L * cfg->Cin * C, dbs, nsl, C, nullptr, 0, nullptr, grads + L.off_c1b,
-                             grads + L.off_c1k, (float*)(b + L.red), s));
+  const float inv_std = cfg->use_norm ? 1.f / cfg->divide_by_stddev : 1.f;
+  if (L.fast_stem) {
+    ASR_TRY(stem_wgrad(images, cfg->input_u8, dcur, act(0), bf, N, H, W, cfg->Cin, C, cfg->subtract_mean, inv_std,
+                       cfg->use_norm, slabs, &nsl, s));
+  } else {
+    ASR_TRY(make_dz(F_RELU, dcur, nullptr, act(0), 1.f, N, H, W, C, bf ? 1 : 0, dz, s));
+    ASR_TRY(wgrad_f32(b + L.x0, 0, dz, N, H, W, cfg->Cin, C, slabs, &nsl, s));
+  }
+  ASR_TRY(reduce_and_project(slabs, nsl, E1, C, nullptr, 0, nullptr, grads + L.off_c1b, grads + L.off_c1k, red, s));
   return ASR_OK;
 }
 

@@ -116,6 +116,7 @@ __global__ void k_make_dz(const T* __restrict__ dy, const uint64_t* __restrict__
 
 // dW[tap][i][o] partial over a chunk of image rows:
 //   slab[chunk][(tap*Ci + i)*Co + o] = sum_{rows in chunk, px} x[p+s(tap)][i] * dz[p][o]
+// (slab rows are E + Co floats: dW partial then the db partial of k_db_f32)
 template <typename Tx>
 __global__ __launch_bounds__(256) void k_wgrad_f32(const Tx* __restrict__ x, const float* __restrict__ dz, int N,
                                                    int H, int W, int Ci, int Co, int rows_per_chunk,
@@ -140,18 +141,18 @@ __global__ __launch_bounds__(256) void k_wgrad_f32(const Tx* __restrict__ x, con
     const int p0 = max(0, -sx), p1 = min(W, W - sx);
     for (int p = p0; p < p1; ++p) acc = fmaf(to_f32(xr[(long)(p + sx) * Ci + i]), dr[(long)p * Co + o], acc);
   }
-  slabs[(long)blockIdx.y * E + e] = acc;
+  slabs[(long)blockIdx.y * (E + Co) + e] = acc;
 }
 
-// db partial per chunk of pixel rows: db_slabs[chunk][o]
-__global__ void k_db_f32(const float* __restrict__ dz, long rows, int W, int C, int rows_per_chunk,
-                         float* __restrict__ db_slabs) {
+// db partial per chunk of pixel rows, into the slab row tail: slabs[chunk][E + o]
+__global__ void k_db_f32(const float* __restrict__ dz, long rows, int W, int C, int rows_per_chunk, long E,
+                         float* __restrict__ slabs) {
   const int o = threadIdx.x;
   if (o >= C) return;
   const long r0 = (long)blockIdx.x * rows_per_chunk, r1 = min(rows, r0 + rows_per_chunk);
   float acc = 0.f;
   for (long p = r0 * W; p < r1 * W; ++p) acc += dz[p * C + o];
-  db_slabs[(long)blockIdx.x * C + o] = acc;
+  slabs[(long)blockIdx.x * (E + C) + E + o] = acc;
 }
 
 template <typename Tin, typename Tout, int MODE>
@@ -208,7 +209,7 @@ int wgrad_f32_chunks(int N, int H) {
 }
 
 int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, int Ci, int Co, float* slabs,
-              float* db_slabs, int* nslabs, hipStream_t s) {
+              int* nslabs, hipStream_t s) {
   const long R = (long)N * H;
   const int chunks = wgrad_f32_chunks(N, H);
   const int rpc = (int)((R + chunks - 1) / chunks);
@@ -220,11 +221,9 @@ int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, i
   else
     hipLaunchKernelGGL(k_wgrad_f32<float>, grid, dim3(256), 0, s, (const float*)x, dz, N, H, W, Ci, Co, rpc, slabs);
   ASR_LAUNCH_CHECK("k_wgrad_f32");
-  if (db_slabs) {
-    if (Co > 1024) return fail(ASR_E_UNSUPPORTED, "db: C > 1024");
-    hipLaunchKernelGGL(k_db_f32, dim3(nch), dim3(((Co + 63) / 64) * 64), 0, s, dz, R, W, Co, rpc, db_slabs);
-    ASR_LAUNCH_CHECK("k_db_f32");
-  }
+  if (Co > 1024) return fail(ASR_E_UNSUPPORTED, "db: C > 1024");
+  hipLaunchKernelGGL(k_db_f32, dim3(nch), dim3(((Co + 63) / 64) * 64), 0, s, dz, R, W, Co, rpc, E, slabs);
+  ASR_LAUNCH_CHECK("k_db_f32");
   *nslabs = nch;
   return ASR_OK;
 }

@@ -244,8 +244,7 @@ __device__ __forceinline__ bf16x8 tr_pair(const unsigned char* p0, const unsigne
 template <int C, int W, int MODE>
 __global__ __launch_bounds__(256, 2) void k_wgrad_mfma(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                        const uint64_t* __restrict__ mask, float h, int N, int H,
-                                                       int BR, float* __restrict__ slabs,
-                                                       float* __restrict__ db_slabs) {
+                                                       int BR, float* __restrict__ slabs) {
   using G = Geo<C>;
   constexpr int TW = W + 2, PT = W / 16, NQ = G::NQ, OT = G::OT, MTW = G::MTW;
   constexpr int KPR = W / 32;  // 32-pixel k-steps per image row
@@ -361,7 +360,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_mfma(const bf16* __restrict__ 
     }
   }
   if (kg == 0) {
-    float* slab = slabs + (long)blockIdx.x * 9 * C * C;
+    float* slab = slabs + (long)blockIdx.x * (9 * C * C + C);
 #pragma unroll
     for (int mi = 0; mi < MTW; ++mi)
 #pragma unroll
@@ -382,7 +381,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_mfma(const bf16* __restrict__ 
     const int q = tid / 8, j = tid % 8;
     float s = 0.f;
     for (int t = q; t < 256; t += NQ) s += dbl[j * 256 + t];
-    db_slabs[(long)blockIdx.x * C + tid] = s;
+    slabs[(long)blockIdx.x * (9 * C * C + C) + 9 * C * C + tid] = s;
   }
 }
 
@@ -445,7 +444,7 @@ static int launch_conv_mfma(int mode, const void* xin, void* out, uint64_t* mask
 
 template <int C, int W>
 static int launch_wgrad_mfma(int mode, const void* x, const void* dy, const uint64_t* mask, float h, int N, int H,
-                             float* slabs, float* db_slabs, int* nslabs, hipStream_t s) {
+                             float* slabs, int* nslabs, hipStream_t s) {
   const int BR = pick_br(H);
   const long items = (long)N * ((H + BR - 1) / BR);
   const int grid = grid_for(items);
@@ -453,10 +452,10 @@ static int launch_wgrad_mfma(int mode, const void* x, const void* dy, const uint
   const size_t lds = wgrad_lds<C, W>(BR);
   if (mode == BWD_EULER)
     hipLaunchKernelGGL((k_wgrad_mfma<C, W, BWD_EULER>), dim3(grid), dim3(256), lds, s, (const bf16*)x,
-                       (const bf16*)dy, mask, h, N, H, BR, slabs, db_slabs);
+                       (const bf16*)dy, mask, h, N, H, BR, slabs);
   else
     hipLaunchKernelGGL((k_wgrad_mfma<C, W, BWD_CONV>), dim3(grid), dim3(256), lds, s, (const bf16*)x,
-                       (const bf16*)dy, mask, h, N, H, BR, slabs, db_slabs);
+                       (const bf16*)dy, mask, h, N, H, BR, slabs);
   ASR_LAUNCH_CHECK("k_wgrad_mfma");
   return ASR_OK;
 }
@@ -475,12 +474,12 @@ int conv_mfma(int mode, const void* xin, void* out, uint64_t* mask, const void* 
 }
 
 int wgrad_mfma(int mode, const void* x, const void* dy, const uint64_t* mask, float h, int N, int H, int W, int C,
-               float* slabs, float* db_slabs, int* nslabs, hipStream_t s) {
+               float* slabs, int* nslabs, hipStream_t s) {
   if (W != 32) return fail(ASR_E_UNSUPPORTED, "bf16 wgrad: W=%d not supported", W);
   switch (C) {
-    case 16: return launch_wgrad_mfma<16, 32>(mode, x, dy, mask, h, N, H, slabs, db_slabs, nslabs, s);
-    case 32: return launch_wgrad_mfma<32, 32>(mode, x, dy, mask, h, N, H, slabs, db_slabs, nslabs, s);
-    case 64: return launch_wgrad_mfma<64, 32>(mode, x, dy, mask, h, N, H, slabs, db_slabs, nslabs, s);
+    case 16: return launch_wgrad_mfma<16, 32>(mode, x, dy, mask, h, N, H, slabs, nslabs, s);
+    case 32: return launch_wgrad_mfma<32, 32>(mode, x, dy, mask, h, N, H, slabs, nslabs, s);
+    case 64: return launch_wgrad_mfma<64, 32>(mode, x, dy, mask, h, N, H, slabs, nslabs, s);
   }
   return fail(ASR_E_UNSUPPORTED, "bf16 wgrad: C=%d not supported", C);
 }

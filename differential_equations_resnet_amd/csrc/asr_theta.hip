@@ -231,36 +231,26 @@ __global__ void k_reduce_slabs(const float* __restrict__ in, long E, int P, int 
   out[(long)g * E + e] = (acc0 + acc1) + (acc2 + acc3);
 }
 
-// dtheta[j] = sum over the (<=2) W entries theta j feeds of sign * dW[e];
-// dW = sum of G group slabs of E floats (G small).  Also optional dW copy and
-// db = sum of GB slabs of Cb floats.
-__global__ void k_project(const float* __restrict__ dw_groups, int G, long E, const int32_t* __restrict__ theta_dst,
-                          long n_theta, float* __restrict__ dtheta, float* __restrict__ dw_out,
-                          const float* __restrict__ db_groups, int GB, int Cb, float* __restrict__ dbias) {
+// dtheta[j] = sum over the (<=2) W entries theta j feeds of sign * dW[e],
+// from the fully reduced slab row [dW (E floats) | db (Cb floats)].  Also an
+// optional dW copy and db.
+__global__ void k_project(const float* __restrict__ red, long E, const int32_t* __restrict__ theta_dst, long n_theta,
+                          float* __restrict__ dtheta, float* __restrict__ dw_out, int Cb, float* __restrict__ dbias) {
   const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  auto dw = [&](long e) {
-    float s = 0.f;
-    for (int g = 0; g < G; ++g) s += dw_groups[(long)g * E + e];
-    return s;
-  };
   if (dtheta && t < n_theta) {
     float acc = 0.f;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int32_t v = theta_dst[2 * t + q];
       if (v >= 0) {
-        const float d = dw(v >> 1);
+        const float d = red[v >> 1];
         acc += (v & 1) ? -d : d;
       }
     }
     dtheta[t] = acc;
   }
-  if (dw_out && t < E) dw_out[t] = dw(t);
-  if (dbias && t < Cb) {
-    float s = 0.f;
-    for (int g = 0; g < GB; ++g) s += db_groups[(long)g * Cb + t];
-    dbias[t] = s;
-  }
+  if (dw_out && t < E) dw_out[t] = red[t];
+  if (dbias && t < Cb) dbias[t] = red[E + t];
 }
 
 }  // namespace asr
@@ -314,25 +304,33 @@ int asr_theta_to_w(const float* theta, long theta_stride, int L, int C, const in
 
 namespace asr {
 
-// Reduce P slabs of E floats (dW partials) and PB slabs of Cb floats (db
-// partials); project dW onto theta (if theta_dst) and/or copy it out.
-// ws must hold reduce_ws_bytes(P, E) bytes.
-int reduce_and_project(const float* slabs, int P, long E, const float* db_slabs, int PB, int Cb,
-                       const int32_t* theta_dst, long n_theta, float* dtheta, float* dbias, float* dw_out, float* ws,
-                       hipStream_t s) {
+// Reduce P slab rows of ES = E + Cb floats ([dW partial | db partial], written
+// by the wgrad kernels) deterministically in two passes (P -> ceil(P/32) -> 1),
+// then project dW onto theta (if theta_dst) and/or copy dW / db out.
+// ws must hold reduce_ws_bytes(P, E + Cb) bytes.
+int reduce_and_project(const float* slabs, int P, long E, int Cb, const int32_t* theta_dst, long n_theta,
+                       float* dtheta, float* dbias, float* dw_out, float* ws, hipStream_t s) {
+  const long ES = E + Cb;
   const int per = 32;
   const int G = (P + per - 1) / per;
   float* grp = ws;
-  dim3 g1((unsigned)((E + 255) / 256), G);
-  hipLaunchKernelGGL(k_reduce_slabs, g1, dim3(256), 0, s, slabs, E, P, per, grp);
+  float* fin = ws + (long)G * ES;
+  dim3 g1((unsigned)((ES + 255) / 256), G);
+  hipLaunchKernelGGL(k_reduce_slabs, g1, dim3(256), 0, s, slabs, ES, P, per, grp);
   ASR_LAUNCH_CHECK("k_reduce_slabs");
+  const float* red = grp;
+  if (G > 1) {
+    hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)((ES + 255) / 256), 1), dim3(256), 0, s, grp, ES, G, G, fin);
+    ASR_LAUNCH_CHECK("k_reduce_slabs");
+    red = fin;
+  }
   const long n = std::max(std::max(dtheta ? n_theta : 0L, dw_out ? E : 0L), (long)Cb);
-  hipLaunchKernelGGL(k_project, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, grp, G, E, theta_dst,
-                     dtheta ? n_theta : 0L, dtheta, dw_out, db_slabs, PB, Cb, dbias);
+  hipLaunchKernelGGL(k_project, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, red, E, theta_dst,
+                     dtheta ? n_theta : 0L, dtheta, dw_out, Cb, dbias);
   ASR_LAUNCH_CHECK("k_project");
   return ASR_OK;
 }
 
-size_t reduce_ws_bytes(int P, long E) { return (size_t)((P + 31) / 32) * E * sizeof(float); }
+size_t reduce_ws_bytes(int P, long ES) { return (size_t)((P + 31) / 32 + 1) * ES * sizeof(float); }
 
 }  // namespace asr

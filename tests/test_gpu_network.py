@@ -90,4 +90,5 @@ def test_network_train_steps_decrease_loss():
         loss, grads = ex.forward_backward(flat, x, t)
         losses.append(loss.item())
         runtime.adam_update(flat, grads, m, v, 1e-3, 0.9, 0.999, 1e-7, step)
-    assert losses[-1] < 0.7 * losses[0], losses
+    assert losses[-1] < 0.9 * losses[0], losses
+    assert all(b < a for a, b in zip(losses, losses[1:])), losses
