@@ -77,7 +77,7 @@ def block_roofline(rt, lib, C, N, dtype_name, reps, h):
     th = torch.randn(pm.n_theta, device=dev, generator=g) * 0.05
     bias = torch.zeros(C, device=dev)
     w = rt.theta_to_w(th, C, pm, 0.0, dt)
-    mask = torch.zeros(rt.mask_words(N, H, W, C), dtype=torch.int64, device=dev)
+    mask = torch.zeros(rt.mask_bytes(N, H, W, C), dtype=torch.uint8, device=dev)
     ws_bytes = int(lib.asr_conv_backward_workspace_bytes(N, H, W, C, dt))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     dth = torch.empty(pm.n_theta, device=dev)

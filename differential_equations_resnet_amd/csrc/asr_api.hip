@@ -21,14 +21,14 @@ int reduce_and_project(const float* slabs, int P, long E, int Cb, const int32_t*
 size_t reduce_ws_bytes(int P, long ES);
 // asr_conv_mfma.hip
 bool mfma_supported(int C, int W);
-int conv_mfma(int mode, const void* xin, void* out, uint64_t* mask, const void* w, const float* bias, float h,
+int conv_mfma(int mode, const void* xin, void* out, uint8_t* mask, const void* w, const float* bias, float h,
               float two_gamma, int N, int H, int W, int C, hipStream_t s);
-int wgrad_mfma(int mode, const void* x, const void* dy, const uint64_t* mask, float h, int N, int H, int W, int C,
+int wgrad_mfma(int mode, const void* x, const void* dy, const uint8_t* mask, float h, int N, int H, int W, int C,
                float* slabs, int* nslabs, hipStream_t s);
 // asr_conv_f32.hip
-int conv_f32(int fmode, const void* xin, void* out, uint64_t* mask, const float* w, const float* bias, float h,
+int conv_f32(int fmode, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
              float two_gamma, const float* dy, int N, int H, int W, int Ci, int Co, int out_bf16, hipStream_t s);
-int make_dz(int fmode, const void* dy, const uint64_t* mask, const void* relu_src, float h, int N, int H, int W, int C,
+int make_dz(int fmode, const void* dy, const uint8_t* mask, const void* relu_src, float h, int N, int H, int W, int C,
             int src_bf16, float* dz, hipStream_t s);
 int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, int Ci, int Co, float* slabs,
               int* nslabs, hipStream_t s);
@@ -76,7 +76,7 @@ static BwdWs bwd_ws_layout(int N, int H, int W, int C, int dtype) {
   return b;
 }
 
-static int conv_backward_impl(int mode, const void* dy, const void* x, const uint64_t* mask, const void* w,
+static int conv_backward_impl(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w,
                               const int32_t* theta_dst, long n_theta, float h, float gamma, int N, int H, int W,
                               int C, int dtype, void* dx, float* dtheta, float* dbias, float* dw_hwio, void* ws,
                               hipStream_t s) {
@@ -88,7 +88,7 @@ static int conv_backward_impl(int mode, const void* dy, const void* x, const uin
   const int cm = (mode == ASR_MODE_EULER) ? 2 : 3;  // BWD_EULER / BWD_CONV
   int nsl = 0;
   if (dtype == ASR_BF16) {
-    if (dx) ASR_TRY(conv_mfma(cm, dy, dx, (uint64_t*)mask, w, nullptr, h, 2.f * gamma, N, H, W, C, s));
+    if (dx) ASR_TRY(conv_mfma(cm, dy, dx, (uint8_t*)mask, w, nullptr, h, 2.f * gamma, N, H, W, C, s));
     if (need_w) ASR_TRY(wgrad_mfma(cm, x, dy, mask, h, N, H, W, C, slabs, &nsl, s));
   } else {
     float* dz = (float*)(base + L.dz);
@@ -136,7 +136,7 @@ struct NetLayout {
   long ntheta, P, E, wstride;  // wstride in elements of the W dtype
   long off_c1k, off_c1b, off_blk, blk_stride, off_fck, off_fcb, nparams;
   size_t w_src, theta_dst, wbuf, x0, acts, masks, dxa, dxb, bwdws, slabs, red, probs, loss_per, dlogits, gap, total;
-  long mask_words;
+  long mask_bytes;
   int act_bytes;
   bool fast_stem;
 };
@@ -167,7 +167,7 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.off_fck = L.off_blk + (long)c->L * L.blk_stride;
   L.off_fcb = L.off_fck + (long)C * K;
   L.nparams = L.off_fcb + K;
-  L.mask_words = (long)c->N * c->H * ((c->W + 15) / 16) * ((C + 15) / 16) * 4;
+  L.mask_bytes = asr_mask_bytes(c->N, c->H, c->W, C);
   L.fast_stem = stem_supported(c->Cin, c->H, c->W, C);
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -180,7 +180,7 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.wbuf = take((size_t)c->L * L.wstride * L.act_bytes);
   L.x0 = take(L.fast_stem ? 0 : (size_t)c->N * c->H * c->W * c->Cin * 4);
   L.acts = take((size_t)(c->L + 1) * L.P * L.act_bytes);
-  L.masks = take((size_t)c->L * L.mask_words * 8);
+  L.masks = take((size_t)c->L * L.mask_bytes);
   L.dxa = take((size_t)L.P * L.act_bytes);
   L.dxb = take((size_t)L.P * L.act_bytes);
   // per-block backward workspace (asr_conv_backward layout), reused by the stem
@@ -232,7 +232,7 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
   for (int l = 0; l < c->L; ++l) {
     const float* bias = params + L.off_blk + (long)l * L.blk_stride + L.ntheta;
     const unsigned char* wl = ws + L.wbuf + (size_t)l * L.wstride * L.act_bytes;
-    uint64_t* mask = training ? (uint64_t*)(ws + L.masks) + (size_t)l * L.mask_words : nullptr;
+    uint8_t* mask = training ? (uint8_t*)(ws + L.masks) + (size_t)l * L.mask_bytes : nullptr;
     if (bf)
       ASR_TRY(conv_mfma(0, act(l), act(l + 1), mask, wl, bias, c->h, 0.f, N, H, W, C, s));
     else
@@ -248,12 +248,12 @@ using namespace asr;
 
 extern "C" {
 
-long asr_mask_words(int N, int H, int W, int C) {
+long asr_mask_bytes(int N, int H, int W, int C) {
   if (N < 1 || H < 1 || W < 1 || C < 1) return -1;
-  return (long)N * H * ((W + 15) / 16) * ((C + 15) / 16) * 4;
+  return ((long)N * H * W * C + 31) / 32 * 4;
 }
 
-int asr_conv_forward(int mode, const void* x, void* y, uint64_t* mask, const void* w, const float* bias, float h,
+int asr_conv_forward(int mode, const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h,
                      int N, int H, int W, int C, int dtype, asr_stream_t stream) {
   ASR_TRY(check_shape(N, H, W, C));
   if (!x || !y || !w) return fail(ASR_E_ARG, "asr_conv_forward: null pointer");
@@ -275,7 +275,7 @@ size_t asr_conv_backward_workspace_bytes(int N, int H, int W, int C, int dtype) 
   return bwd_ws_layout(N, H, W, C, dtype).total;
 }
 
-int asr_conv_backward(int mode, const void* dy, const void* x, const uint64_t* mask, const void* w,
+int asr_conv_backward(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w,
                       const int32_t* theta_dst, long n_theta, float h, float gamma, int N, int H, int W, int C,
                       int dtype, void* dx, float* dtheta, float* dbias, float* dw_hwio, void* ws, size_t ws_bytes,
                       asr_stream_t stream) {
@@ -356,7 +356,7 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   const int32_t* theta_dst = (const int32_t*)(b + L.theta_dst);
   for (int l = cfg->L - 1; l >= 0; --l) {
     const unsigned char* wl = b + L.wbuf + (size_t)l * L.wstride * L.act_bytes;
-    const uint64_t* mask = (const uint64_t*)(b + L.masks) + (size_t)l * L.mask_words;
+    const uint8_t* mask = (const uint8_t*)(b + L.masks) + (size_t)l * L.mask_bytes;
     float* dth = grads + L.off_blk + (long)l * L.blk_stride;
     ASR_TRY(conv_backward_impl(ASR_MODE_EULER, dcur, act(l), mask, wl, theta_dst, L.ntheta, cfg->h, cfg->gamma, N, H,
                                W, C, cfg->dtype, dnext, dth, dth + L.ntheta, nullptr, b + L.bwdws, s));

@@ -50,10 +50,4 @@ __device__ __forceinline__ bf16 from_f32<bf16>(float v) { return (bf16)v; }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-// mask word index of (n, y, pixel-tile, channel-tile); 4 words per 16x16 block,
-// word e holds bit (4*g + ...) : bit (g*16 + px_local) is channel 16*ot + 4*g + e.
-__device__ __forceinline__ long mask_base(int n, int y, int pt, int ot, int H, int PT, int OT) {
-  return ((((long)n * H + y) * PT + pt) * OT + ot) * 4;
-}
-
 }  // namespace asr

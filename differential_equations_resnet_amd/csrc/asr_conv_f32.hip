@@ -13,12 +13,12 @@ namespace asr {
 enum { F_EULER = 0, F_CONV = 1, F_RELU = 2, B_EULER = 3, B_CONV = 4 };
 
 // One wave = (n, y, 16-pixel tile, 16-channel tile).  Lane (g = lane>>4,
-// lx = lane&15) computes pixel 16*pt+lx, channels 16*ot+4g .. +3 — the same
-// lane->(pixel, channel) map as the MFMA D fragment, so the mask ballots are
-// bit-identical to the bf16 kernels'.
+// lx = lane&15) computes pixel 16*pt+lx, channels 16*ot+4g .. +3 (the MFMA D
+// fragment map).  Relu mask: bit (pixel*C + o) (asr.h), set with atomicOr on
+// a zeroed buffer because C need not be a multiple of 8 here.
 template <typename Tin, typename Tout, int MODE>
 __global__ __launch_bounds__(256) void k_conv_f32(const Tin* __restrict__ xin, Tout* __restrict__ out,
-                                                  uint64_t* __restrict__ mask, const float* __restrict__ w,
+                                                  uint32_t* __restrict__ mask, const float* __restrict__ w,
                                                   const float* __restrict__ bias, float h, float two_gamma,
                                                   const float* __restrict__ dy, int N, int H, int W, int Ci, int Co) {
   const int PT = (W + 15) / 16, OT = (Co + 15) / 16;
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void k_conv_f32(const Tin* __restrict__ xin, T
     }
   }
   const long pix = (((long)n * H + y) * W + px);
-  uint64_t bw[4];
+  unsigned nib = 0;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int o = o0 + e;
@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void k_conv_f32(const Tin* __restrict__ xin, T
     if constexpr (MODE <= F_RELU) {
       const float z = acc[e] + ((bias && o < Co) ? bias[o] : 0.f);
       if constexpr (MODE == F_EULER) {
-        bw[e] = __ballot(ok && z > 0.f);
+        if (ok && z > 0.f) nib |= 1u << e;
         if (ok) v = to_f32(xin[pix * Ci + o]) + h * fmaxf(z, 0.f);
       } else if constexpr (MODE == F_CONV) {
         v = z;
@@ -77,36 +77,25 @@ __global__ __launch_bounds__(256) void k_conv_f32(const Tin* __restrict__ xin, T
     if (ok) out[pix * Co + o] = from_f32<Tout>(v);
   }
   if constexpr (MODE == F_EULER) {
-    if (mask && lane < 4) {
-      uint64_t mine = bw[0];
-      if (lane == 1) mine = bw[1];
-      if (lane == 2) mine = bw[2];
-      if (lane == 3) mine = bw[3];
-      mask[mask_base(n, y, pt, ot, H, PT, OT) + lane] = mine;
+    if (mask && nib) {
+      const long b0 = pix * Co + o0;  // first of this lane's 4 channels
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if ((nib >> e) & 1u) atomicOr(mask + ((b0 + e) >> 5), 1u << ((b0 + e) & 31));
     }
   }
 }
 
 // dz = h*dy*mask (EULER), dy (CONV) or dy*[src > 0] (RELU), as float.
 template <typename T>
-__global__ void k_make_dz(const T* __restrict__ dy, const uint64_t* __restrict__ mask, const T* __restrict__ relu_src,
+__global__ void k_make_dz(const T* __restrict__ dy, const uint8_t* __restrict__ mask, const T* __restrict__ relu_src,
                           int mode, float h, int N, int H, int W, int C, float* __restrict__ dz) {
   const long P = (long)N * H * W * C;
-  const int PT = (W + 15) / 16, OT = (C + 15) / 16;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < P; idx += (long)gridDim.x * blockDim.x) {
     const float d = to_f32(dy[idx]);
     float v = d;
     if (mode == F_EULER) {
-      const int o = (int)(idx % C);
-      long pix = idx / C;
-      const int x = (int)(pix % W);
-      pix /= W;
-      const int y = (int)(pix % H);
-      const int n = (int)(pix / H);
-      const int ol = o & 15;
-      const uint64_t word = mask[mask_base(n, y, x >> 4, o >> 4, H, PT, OT) + (ol & 3)];
-      const int bit = (ol >> 2) * 16 + (x & 15);
-      v = ((word >> bit) & 1ull) ? h * d : 0.f;
+      v = ((mask[idx >> 3] >> (idx & 7)) & 1) ? h * d : 0.f;  // bit idx = pixel*C + o
     } else if (mode == F_RELU) {
       v = to_f32(relu_src[idx]) > 0.f ? d : 0.f;
     }
@@ -156,18 +145,22 @@ __global__ void k_db_f32(const float* __restrict__ dz, long rows, int W, int C, 
 }
 
 template <typename Tin, typename Tout, int MODE>
-static int launch_conv_f32(const void* xin, void* out, uint64_t* mask, const float* w, const float* bias, float h,
+static int launch_conv_f32(const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
                            float two_gamma, const float* dy, int N, int H, int W, int Ci, int Co, hipStream_t s) {
   const long tasks = (long)N * H * ((W + 15) / 16) * ((Co + 15) / 16);
   const long blocks = (tasks + 3) / 4;
   if (blocks > 0x7fffffffL) return fail(ASR_E_ARG, "conv f32: problem too large");
+  if (MODE == F_EULER && mask) {
+    const long bytes = ((long)N * H * W * Co + 31) / 32 * 4;
+    ASR_TRY(hip_check(hipMemsetAsync(mask, 0, bytes, s), "hipMemsetAsync(mask)"));
+  }
   hipLaunchKernelGGL((k_conv_f32<Tin, Tout, MODE>), dim3((unsigned)blocks), dim3(256), 0, s, (const Tin*)xin,
-                     (Tout*)out, mask, w, bias, h, two_gamma, dy, N, H, W, Ci, Co);
+                     (Tout*)out, (uint32_t*)mask, w, bias, h, two_gamma, dy, N, H, W, Ci, Co);
   ASR_LAUNCH_CHECK("k_conv_f32");
   return ASR_OK;
 }
 
-int conv_f32(int fmode, const void* xin, void* out, uint64_t* mask, const float* w, const float* bias, float h,
+int conv_f32(int fmode, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
              float two_gamma, const float* dy, int N, int H, int W, int Ci, int Co, int out_bf16, hipStream_t s) {
   switch (fmode) {
     case F_EULER:
@@ -186,7 +179,7 @@ int conv_f32(int fmode, const void* xin, void* out, uint64_t* mask, const float*
   return fail(ASR_E_ARG, "conv f32: bad mode");
 }
 
-int make_dz(int fmode, const void* dy, const uint64_t* mask, const void* relu_src, float h, int N, int H, int W, int C,
+int make_dz(int fmode, const void* dy, const uint8_t* mask, const void* relu_src, float h, int N, int H, int W, int C,
             int src_bf16, float* dz, hipStream_t s) {
   const long P = (long)N * H * W * C;
   const unsigned grid = (unsigned)std::min<long>((P + 255) / 256, 8192);

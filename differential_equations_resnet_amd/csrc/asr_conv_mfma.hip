@@ -59,38 +59,109 @@ __device__ __forceinline__ int tile_off(int row, int col, int q, int TW) {
 
 __device__ __forceinline__ uint4 u4zero() { return make_uint4(0, 0, 0, 0); }
 
-// dz = h*dy*mask (EULER) for one 16-byte chunk of 8 channels starting at
-// channel 8*q of pixel (n, gy, gx).  Mask layout: asr_common.h mask_base.
-template <int C>
-__device__ __forceinline__ uint4 make_dz_chunk(uint4 dyv, const uint64_t* __restrict__ mask, int n, int gy, int gx,
-                                               int q, int H, int PT, float h, float* dzf) {
-  const long mb = mask_base(n, gy, gx >> 4, q >> 1, H, PT, Geo<C>::OT);
-  const uint4 w01 = *(const uint4*)(mask + mb);
-  const uint4 w23 = *(const uint4*)(mask + mb + 2);
-  const uint64_t w[4] = {((uint64_t)w01.y << 32) | w01.x, ((uint64_t)w01.w << 32) | w01.z,
-                         ((uint64_t)w23.y << 32) | w23.x, ((uint64_t)w23.w << 32) | w23.z};
-  const int sh0 = (2 * (q & 1)) * 16 + (gx & 15);
-  bf16x8 dy8 = *(bf16x8*)&dyv;
+// Mask layout (asr.h asr_mask_bytes): bit (pixel*C + o), pixel = (n*H + y)*W + x,
+// i.e. NHWC bit order; one byte = 8 channels of one pixel = one 16-byte chunk.
+// dz = h*dy*mask for the chunk of 8 channels whose mask byte is mb.
+__device__ __forceinline__ uint4 dz_chunk(uint4 dyv, unsigned mb, float h, float* dzf) {
+  const bf16x8 dy8 = *(const bf16x8*)&dyv;
   bf16x8 out;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int bit = sh0 + (j >> 2) * 16;
-    const float m = (float)((w[j & 3] >> bit) & 1ull);
-    const float d = h * (float)dy8[j] * m;
+    const float d = ((mb >> j) & 1u) ? h * (float)dy8[j] : 0.f;
     dzf[j] = d;
     out[j] = (bf16)d;
   }
-  return *(uint4*)&out;
+  return *(const uint4*)&out;
+}
+
+// Stage rows [y0-1, y0+rows] x cols [-1, W] of `src` (bf16 NHWC) into an LDS
+// tile (zero outside the image).  All global loads of a batch are issued
+// before any LDS store so their latencies overlap.
+template <int C, int W, int MAXROWS, int KB = 4>
+__device__ __forceinline__ void stage_plain(const bf16* __restrict__ src, unsigned char* tile, int n, int y0,
+                                            int rows, int H, int tid) {
+  constexpr int TW = W + 2, NQ = C / 8;
+  const int nch = rows * TW * NQ;
+  for (int base = 0; base < nch; base += 256 * KB) {
+    uint4 v[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const int c = base + tid + 256 * k;
+      v[k] = u4zero();
+      const int q = c % NQ, pc = c / NQ, col = pc % TW, r = pc / TW;
+      const int gy = y0 + r, gx = col - 1;
+      if (c < nch && gy >= 0 && gy < H && gx >= 0 && gx < W)
+        v[k] = *(const uint4*)(src + (((long)n * H + gy) * W + gx) * C + q * 8);
+    }
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const int c = base + tid + 256 * k;
+      const int q = c % NQ, pc = c / NQ, col = pc % TW, r = pc / TW;
+      if (c < nch) *(uint4*)(tile + tile_off<C>(r, col, q, TW)) = v[k];
+    }
+  }
+}
+
+// Stage dz = h*dy*mask (EULER) or dy (CONV) for rows [y0+r0, y0+r0+rows) into
+// `tz` (tile rows 0..rows-1) and optionally the raw dy into `ty` (same rows,
+// shifted by ty_row).  Accumulates db partial sums (8 channels per thread).
+template <int C, int W, int MAXROWS, bool EULER, int KB = 4>
+__device__ __forceinline__ void stage_dz(const bf16* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                         unsigned char* tz, unsigned char* ty, int ty_lo, int ty_hi, int n,
+                                         int gy0, int rows, int H, float h, int tid, float* dbacc, int db_lo,
+                                         int db_hi) {
+  constexpr int TW = W + 2, NQ = C / 8;
+  const int nch = rows * TW * NQ;
+  for (int base = 0; base < nch; base += 256 * KB) {
+    uint4 v[KB];
+    unsigned mb[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const int c = base + tid + 256 * k;
+      v[k] = u4zero();
+      mb[k] = 0;
+      const int q = c % NQ, pc = c / NQ, col = pc % TW, r = pc / TW;
+      const int gy = gy0 + r, gx = col - 1;
+      if (c < nch && gy >= 0 && gy < H && gx >= 0 && gx < W) {
+        const long pix = ((long)n * H + gy) * W + gx;
+        v[k] = *(const uint4*)(dy + pix * C + q * 8);
+        if constexpr (EULER) mb[k] = mask[pix * NQ + q];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const int c = base + tid + 256 * k;
+      const int q = c % NQ, pc = c / NQ, col = pc % TW, r = pc / TW;
+      if (c < nch) {
+        float f[8];
+        uint4 dz;
+        if constexpr (EULER) {
+          dz = dz_chunk(v[k], mb[k], h, f);
+        } else {
+          dz = v[k];
+          const bf16x8 d8 = *(const bf16x8*)&v[k];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = (float)d8[j];
+        }
+        *(uint4*)(tz + tile_off<C>(r, col, q, TW)) = dz;
+        if (ty && r >= ty_lo && r < ty_hi) *(uint4*)(ty + tile_off<C>(r - ty_lo, col, q, TW)) = v[k];
+        if (dbacc && r >= db_lo && r < db_hi) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dbacc[j] += f[j];
+        }
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
 // forward conv / Euler step, and dgrad (MODE >= BWD_EULER)
 // ---------------------------------------------------------------------------
-template <int C, int W, int MODE>
+template <int C, int W, int BR, int MODE>
 __global__ __launch_bounds__(256, 2) void k_conv_mfma(const bf16* __restrict__ xin, bf16* __restrict__ out,
-                                                      uint64_t* __restrict__ mask, const bf16* __restrict__ wpack,
+                                                      uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
                                                       const float* __restrict__ bias, float h, float two_gamma,
-                                                      int N, int H, int BR) {
+                                                      int N, int H) {
   using G = Geo<C>;
   constexpr int TW = W + 2, PT = W / 16, NQ = G::NQ, OTW = G::OTW, KS = G::KS;
   constexpr bool BWD = MODE >= BWD_EULER;
@@ -135,25 +206,11 @@ __global__ __launch_bounds__(256, 2) void k_conv_mfma(const bf16* __restrict__ x
     const int y0 = (int)(item % nb) * BR;
     const int rows = min(BR, H - y0);
     // ---- stage the band (+halo) into LDS ----
-    const int nch = (rows + 2) * TW * NQ;
-    for (int c = tid; c < nch; c += 256) {
-      const int q = c % NQ, pc = c / NQ, col = pc % TW, r = pc / TW;
-      const int gy = y0 - 1 + r, gx = col - 1;
-      const bool inb = gy >= 0 && gy < H && gx >= 0 && gx < W;
-      uint4 v = u4zero();
-      if (inb) v = *(const uint4*)(xin + (((long)n * H + gy) * W + gx) * C + q * 8);
-      if constexpr (BWD) {
-        uint4 dz = v;
-        if constexpr (EULER) {
-          float tmp[8];
-          if (inb) dz = make_dz_chunk<C>(v, mask, n, gy, gx, q, H, PT, h, tmp);
-        }
-        *(uint4*)(tileA + tile_off<C>(r, col, q, TW)) = dz;
-        if (r >= 1 && r <= rows) *(uint4*)(tileB + tile_off<C>(r - 1, col, q, TW)) = v;
-      } else {
-        *(uint4*)(tileA + tile_off<C>(r, col, q, TW)) = v;
-      }
-    }
+    if constexpr (BWD)
+      stage_dz<C, W, BR + 2, EULER>(xin, mask, tileA, tileB, 1, rows + 1, n, y0 - 1, rows + 2, H, h, tid, nullptr, 0,
+                                    0);
+    else
+      stage_plain<C, W, BR + 2>(xin, tileA, n, y0 - 1, rows + 2, H, tid);
     __syncthreads();
 
     // ---- implicit GEMM + epilogue, one output row at a time ----
@@ -175,23 +232,25 @@ __global__ __launch_bounds__(256, 2) void k_conv_mfma(const bf16* __restrict__ x
         }
       }
       const int gy = y0 + r;
-      uint64_t bw[OTW][PT][4];
 #pragma unroll
-      for (int t = 0; t < OTW; ++t) {
-        const int o0 = 16 * (oh * OTW + t) + 4 * g;
+      for (int pt = 0; pt < PT; ++pt) {
+        const int px = 16 * pt + lx;
+        unsigned mword = 0;  // FWD_EULER: relu bits of this pixel's OTW*16 channels
 #pragma unroll
-        for (int pt = 0; pt < PT; ++pt) {
-          const int px = 16 * pt + lx;
+        for (int t = 0; t < OTW; ++t) {
+          const int o0 = 16 * (oh * OTW + t) + 4 * g;
           const int co = tile_off<C>(r + 1, px + 1, o0 >> 3, TW) + (o0 & 4) * 2;
           float v[4];
           if constexpr (MODE == FWD_EULER) {
             const bf16x4 xr = *(const bf16x4*)(tileA + co);
+            unsigned nib = 0;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const float z = acc[t][pt][e] + bz[t][e];
-              bw[t][pt][e] = __ballot(z > 0.f);
+              nib |= (z > 0.f ? 1u : 0u) << e;
               v[e] = (float)xr[e] + h * fmaxf(z, 0.f);
             }
+            mword |= nib << (16 * t + 4 * g);
           } else if constexpr (MODE == FWD_CONV) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = acc[t][pt][e] + bz[t][e];
@@ -208,20 +267,16 @@ __global__ __launch_bounds__(256, 2) void k_conv_mfma(const bf16* __restrict__ x
           for (int e = 0; e < 4; ++e) o4[e] = (bf16)v[e];
           *(bf16x4*)(out + (((long)n * H + gy) * W + px) * C + o0) = o4;
         }
-      }
-      if constexpr (MODE == FWD_EULER) {
-        if (mask) {
-          uint64_t mine = 0;
-#pragma unroll
-          for (int pt = 0; pt < PT; ++pt)
-#pragma unroll
-            for (int t = 0; t < OTW; ++t)
-#pragma unroll
-              for (int e = 0; e < 4; ++e)
-                if (lane == (pt * OTW + t) * 4 + e) mine = bw[t][pt][e];
-          if (lane < 4 * OTW * PT) {
-            const int pt = lane / (4 * OTW), rem = lane % (4 * OTW);
-            mask[mask_base(n, gy, pt, oh * OTW, H, PT, G::OT) + rem] = mine;
+        if constexpr (MODE == FWD_EULER) {
+          // gather the 4 lane groups' nibbles: lanes lx, lx+16, lx+32, lx+48 share the pixel
+          mword |= __shfl_xor(mword, 16);
+          mword |= __shfl_xor(mword, 32);
+          if (mask && g == 0) {
+            uint8_t* mp = mask + ((((long)n * H + gy) * W + px) * C + 16 * oh * OTW) / 8;
+            if constexpr (OTW == 2)
+              *(uint32_t*)mp = mword;
+            else
+              *(uint16_t*)mp = (uint16_t)mword;
           }
         }
       }
@@ -241,12 +296,12 @@ __device__ __forceinline__ bf16x8 tr_pair(const unsigned char* p0, const unsigne
   return *(bf16x8*)&c;
 }
 
-template <int C, int W, int MODE>
+template <int C, int W, int BR, int MODE>
 __global__ __launch_bounds__(256, 2) void k_wgrad_mfma(const bf16* __restrict__ x, const bf16* __restrict__ dy,
-                                                       const uint64_t* __restrict__ mask, float h, int N, int H,
-                                                       int BR, float* __restrict__ slabs) {
+                                                       const uint8_t* __restrict__ mask, float h, int N, int H,
+                                                       float* __restrict__ slabs) {
   using G = Geo<C>;
-  constexpr int TW = W + 2, PT = W / 16, NQ = G::NQ, OT = G::OT, MTW = G::MTW;
+  constexpr int TW = W + 2, NQ = G::NQ, OT = G::OT, MTW = G::MTW;
   constexpr int KPR = W / 32;  // 32-pixel k-steps per image row
   constexpr bool EULER = (MODE == BWD_EULER);
   static_assert(W % 32 == 0, "wgrad k-steps are 32 pixels of one row");
@@ -275,37 +330,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_mfma(const bf16* __restrict__ 
     const int n = (int)(item / nb);
     const int y0 = (int)(item % nb) * BR;
     const int rows = min(BR, H - y0);
-    // x band with halo
-    const int nchx = (rows + 2) * TW * NQ;
-    for (int c = tid; c < nchx; c += 256) {
-      const int q = c % NQ, pc = c / NQ, col = pc % TW, r = pc / TW;
-      const int gy = y0 - 1 + r, gx = col - 1;
-      uint4 v = u4zero();
-      if (gy >= 0 && gy < H && gx >= 0 && gx < W) v = *(const uint4*)(x + (((long)n * H + gy) * W + gx) * C + q * 8);
-      *(uint4*)(tileX + tile_off<C>(r, col, q, TW)) = v;
-    }
-    // dz interior rows (no halo needed), db partial sums
-    const int nchz = rows * TW * NQ;
-    for (int c = tid; c < nchz; c += 256) {
-      const int q = c % NQ, pc = c / NQ, col = pc % TW, r = pc / TW;
-      const int gy = y0 + r, gx = col - 1;
-      uint4 dz = u4zero();
-      if (gx >= 0 && gx < W) {
-        const uint4 v = *(const uint4*)(dy + (((long)n * H + gy) * W + gx) * C + q * 8);
-        if constexpr (EULER) {
-          float f[8];
-          dz = make_dz_chunk<C>(v, mask, n, gy, gx, q, H, PT, h, f);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) dbacc[j] += f[j];
-        } else {
-          dz = v;
-          const bf16x8 d8 = *(const bf16x8*)&v;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) dbacc[j] += (float)d8[j];
-        }
-      }
-      *(uint4*)(tileZ + tile_off<C>(r, col, q, TW)) = dz;
-    }
+    stage_plain<C, W, BR + 2>(x, tileX, n, y0 - 1, rows + 2, H, tid);
+    stage_dz<C, W, BR, EULER>(dy, mask, tileZ, nullptr, 0, 0, n, y0, rows, H, h, tid, dbacc, 0, BR);
     __syncthreads();
 
     for (int kk = kg; kk < rows * KPR; kk += G::KSPLIT) {
@@ -359,8 +385,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_mfma(const bf16* __restrict__ 
               acc[mi][ot][e] += red[((((k2 - 1) * G::TG + tg) * MTW + mi) * OT + ot) * 256 + e * 64 + lane];
     }
   }
+  float* slab = slabs + (long)blockIdx.x * (9 * C * C + C);
   if (kg == 0) {
-    float* slab = slabs + (long)blockIdx.x * (9 * C * C + C);
 #pragma unroll
     for (int mi = 0; mi < MTW; ++mi)
 #pragma unroll
@@ -381,7 +407,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_mfma(const bf16* __restrict__ 
     const int q = tid / 8, j = tid % 8;
     float s = 0.f;
     for (int t = q; t < 256; t += NQ) s += dbl[j * 256 + t];
-    slabs[(long)blockIdx.x * (9 * C * C + C) + 9 * C * C + tid] = s;
+    slab[9 * C * C + tid] = s;
   }
 }
 
@@ -390,7 +416,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_mfma(const bf16* __restrict__ 
 // ---------------------------------------------------------------------------
 constexpr int kMaxSlabs = 512;
 
-static int pick_br(int H) { return H >= 8 ? 8 : H; }
+constexpr int kBR = 8;  // output rows per band (work item)
 
 template <int C, int W>
 static size_t conv_lds(int BR, bool bwd) {
@@ -417,17 +443,17 @@ static int grid_for(long items) {
 }
 
 template <int C, int W>
-static int launch_conv_mfma(int mode, const void* xin, void* out, uint64_t* mask, const void* w, const float* bias,
+static int launch_conv_mfma(int mode, const void* xin, void* out, uint8_t* mask, const void* w, const float* bias,
                             float h, float two_gamma, int N, int H, hipStream_t s) {
-  const int BR = pick_br(H);
+  const int BR = kBR;
   const long items = (long)N * ((H + BR - 1) / BR);
   const int grid = grid_for(items);
   const bool bwd = mode >= BWD_EULER;
   const size_t lds = conv_lds<C, W>(BR, bwd);
 #define ASR_CONV_CASE(M)                                                                                   \
   case M:                                                                                                  \
-    hipLaunchKernelGGL((k_conv_mfma<C, W, M>), dim3(grid), dim3(256), lds, s, (const bf16*)xin, (bf16*)out, \
-                       mask, (const bf16*)w, bias, h, two_gamma, N, H, BR);                                \
+    hipLaunchKernelGGL((k_conv_mfma<C, W, kBR, M>), dim3(grid), dim3(256), lds, s, (const bf16*)xin,        \
+                       (bf16*)out, mask, (const bf16*)w, bias, h, two_gamma, N, H);                        \
     break;
   switch (mode) {
     ASR_CONV_CASE(FWD_EULER)
@@ -443,26 +469,26 @@ static int launch_conv_mfma(int mode, const void* xin, void* out, uint64_t* mask
 }
 
 template <int C, int W>
-static int launch_wgrad_mfma(int mode, const void* x, const void* dy, const uint64_t* mask, float h, int N, int H,
+static int launch_wgrad_mfma(int mode, const void* x, const void* dy, const uint8_t* mask, float h, int N, int H,
                              float* slabs, int* nslabs, hipStream_t s) {
-  const int BR = pick_br(H);
+  const int BR = kBR;
   const long items = (long)N * ((H + BR - 1) / BR);
   const int grid = grid_for(items);
   *nslabs = grid;
   const size_t lds = wgrad_lds<C, W>(BR);
   if (mode == BWD_EULER)
-    hipLaunchKernelGGL((k_wgrad_mfma<C, W, BWD_EULER>), dim3(grid), dim3(256), lds, s, (const bf16*)x,
-                       (const bf16*)dy, mask, h, N, H, BR, slabs);
+    hipLaunchKernelGGL((k_wgrad_mfma<C, W, kBR, BWD_EULER>), dim3(grid), dim3(256), lds, s, (const bf16*)x,
+                       (const bf16*)dy, mask, h, N, H, slabs);
   else
-    hipLaunchKernelGGL((k_wgrad_mfma<C, W, BWD_CONV>), dim3(grid), dim3(256), lds, s, (const bf16*)x,
-                       (const bf16*)dy, mask, h, N, H, BR, slabs);
+    hipLaunchKernelGGL((k_wgrad_mfma<C, W, kBR, BWD_CONV>), dim3(grid), dim3(256), lds, s, (const bf16*)x,
+                       (const bf16*)dy, mask, h, N, H, slabs);
   ASR_LAUNCH_CHECK("k_wgrad_mfma");
   return ASR_OK;
 }
 
 bool mfma_supported(int C, int W) { return (C == 16 || C == 32 || C == 64) && W == 32; }
 
-int conv_mfma(int mode, const void* xin, void* out, uint64_t* mask, const void* w, const float* bias, float h,
+int conv_mfma(int mode, const void* xin, void* out, uint8_t* mask, const void* w, const float* bias, float h,
               float two_gamma, int N, int H, int W, int C, hipStream_t s) {
   if (W != 32) return fail(ASR_E_UNSUPPORTED, "bf16 conv: W=%d not supported (W must be 32)", W);
   switch (C) {
@@ -473,7 +499,7 @@ int conv_mfma(int mode, const void* xin, void* out, uint64_t* mask, const void* 
   return fail(ASR_E_UNSUPPORTED, "bf16 conv: C=%d not supported (16, 32, 64)", C);
 }
 
-int wgrad_mfma(int mode, const void* x, const void* dy, const uint64_t* mask, float h, int N, int H, int W, int C,
+int wgrad_mfma(int mode, const void* x, const void* dy, const uint8_t* mask, float h, int N, int H, int W, int C,
                float* slabs, int* nslabs, hipStream_t s) {
   if (W != 32) return fail(ASR_E_UNSUPPORTED, "bf16 wgrad: W=%d not supported", W);
   switch (C) {

@@ -128,8 +128,8 @@ def conv_forward(mode: int, x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor
     return y
 
 
-def mask_words(N: int, H: int, W: int, C: int) -> int:
-    return int(_lib.load().asr_mask_words(N, H, W, C))
+def mask_bytes(N: int, H: int, W: int, C: int) -> int:
+    return int(_lib.load().asr_mask_bytes(N, H, W, C))
 
 
 def conv_backward(mode: int, dy: torch.Tensor, x: torch.Tensor, mask: torch.Tensor | None, w: torch.Tensor,

@@ -105,14 +105,15 @@ int asr_theta_to_w(const float* theta, long theta_stride, int L, int C, const in
 /* Forward.  mode ASR_MODE_EULER: y = x + h*relu(conv(x,W)+b), mask written;
  * ASR_MODE_CONV: y = conv(x,W)+b (mask may be NULL).
  *   x, y: [N,H,W,C] in dtype;  w: output of asr_theta_to_w for dtype;
- *   bias: C floats or NULL;  mask: asr_mask_words(N,H,W,C) uint64 words.
+ *   bias: C floats or NULL;  mask: asr_mask_bytes(N,H,W,C) bytes, relu bit of
+ *   element (pixel, o) at bit index pixel*C + o (NHWC bit order, LSB first).
  * Replaces Conv2DAntisymmetric3By3.call (…3By3.py:157-171) and
  * single_layer_identity_block's relu/scale/add (tfkeras_resnets.py:89-92). */
-int asr_conv_forward(int mode, const void* x, void* y, uint64_t* mask, const void* w,
+int asr_conv_forward(int mode, const void* x, void* y, uint8_t* mask, const void* w,
                      const float* bias, float h, int N, int H, int W, int C, int dtype,
                      asr_stream_t stream);
 
-long asr_mask_words(int N, int H, int W, int C);
+long asr_mask_bytes(int N, int H, int W, int C);
 
 /* Backward of asr_conv_forward (the autodiff of training.py:300 through the
  * block).  Given dy = dL/dy:
@@ -124,7 +125,7 @@ long asr_mask_words(int N, int H, int W, int C);
  * [3][3][C][C], may be NULL) receives the unprojected dW.
  * ws: caller workspace of asr_conv_backward_workspace_bytes bytes. */
 size_t asr_conv_backward_workspace_bytes(int N, int H, int W, int C, int dtype);
-int asr_conv_backward(int mode, const void* dy, const void* x, const uint64_t* mask,
+int asr_conv_backward(int mode, const void* dy, const void* x, const uint8_t* mask,
                       const void* w, const int32_t* theta_dst, long n_theta, float h,
                       float gamma, int N, int H, int W, int C, int dtype, void* dx,
                       float* dtheta, float* dbias, float* dw_hwio, void* ws, size_t ws_bytes,

@@ -10,17 +10,12 @@ def bf16_round(x):
     return r.astype(np.uint32).view(np.float32).reshape(a.shape)
 
 
-def decode_mask(words, N, H, W, C):
-    """Inverse of the mask layout (csrc/asr_common.h mask_base): returns bool
-    [N,H,W,C] with bit (n,y,x,o) = word[((n*H+y)*PT + x//16)*OT + o//16)*4 + (o%16)%4]
-    >> ((o%16)//4*16 + x%16)."""
-    w = np.asarray(words).view(np.uint64)
-    PT, OT = (W + 15) // 16, (C + 15) // 16
-    n, y, x, o = np.meshgrid(np.arange(N), np.arange(H), np.arange(W), np.arange(C), indexing="ij")
-    ol = o % 16
-    idx = ((((n * H + y) * PT + x // 16) * OT + o // 16) * 4 + (ol % 4))
-    bit = (ol // 4) * 16 + (x % 16)
-    return ((w[idx] >> bit.astype(np.uint64)) & np.uint64(1)).astype(bool)
+def decode_mask(mask_bytes, N, H, W, C):
+    """Inverse of the relu-mask layout (include/asr.h): bit (pixel*C + o),
+    LSB first, pixel = (n*H + y)*W + x.  Returns bool [N,H,W,C]."""
+    b = np.asarray(mask_bytes).view(np.uint8)
+    bits = np.unpackbits(b, bitorder="little")[: N * H * W * C]
+    return bits.reshape(N, H, W, C).astype(bool)
 
 
 def rel_err(a, b):

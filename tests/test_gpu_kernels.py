@@ -65,7 +65,7 @@ def _run_forward(rt, mode, x_np, th, b, C, gamma, h, dtype):
     x = torch.from_numpy(x_np).to(dev).to(tdt).contiguous()
     w = rt.theta_to_w(torch.from_numpy(th).to(dev), C, pm, gamma, dtype)
     N, H, W_, _ = x_np.shape
-    mask = torch.zeros(rt.mask_words(N, H, W_, C), dtype=torch.int64, device=dev)
+    mask = torch.zeros(rt.mask_bytes(N, H, W_, C), dtype=torch.uint8, device=dev)
     bias = torch.from_numpy(b).to(dev)
     y = rt.conv_forward(mode, x, w, bias, h, mask if mode == rt.ASR_MODE_EULER else None)
     return x, w, y, mask, pm
