@@ -87,7 +87,7 @@ def load(build_if_missing: bool = True):
     global _lib
     if _lib is not None:
         return _lib
-    path = _build.LIB
+    path = os.environ.get("ASR_LIB_OVERRIDE", _build.LIB)  # development: ablation builds
     if not os.path.exists(path):
         if not build_if_missing:
             raise AsrError(f"libasr.so not found at {path}; run differential_equations_resnet_amd._build.build()")

@@ -19,12 +19,12 @@ int param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta
 int reduce_and_project(const float* slabs, int P, long E, int Cb, const int32_t* theta_dst, long n_theta,
                        float* dtheta, float* dbias, float* dw_out, float* ws, hipStream_t s);
 size_t reduce_ws_bytes(int P, long ES);
-// asr_conv_mfma.hip
-bool mfma_supported(int C, int W);
-int conv_mfma(int mode, const void* xin, void* out, uint8_t* mask, const void* w, const float* bias, float h,
-              float two_gamma, int N, int H, int W, int C, hipStream_t s);
-int wgrad_mfma(int mode, const void* x, const void* dy, const uint8_t* mask, float h, int N, int H, int W, int C,
-               float* slabs, int* nslabs, hipStream_t s);
+// asr_block_mfma.hip
+int block_fwd_mfma(int mode, const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h, int N,
+                   int H, int W, int C, hipStream_t s);
+int block_bwd_mfma(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
+                   float two_gamma, int N, int H, int W, int C, void* dx, float* slabs, int* nslabs, hipStream_t s);
+static bool mfma_supported(int C, int W) { return (C == 16 || C == 32 || C == 64) && W == 32; }
 // asr_conv_f32.hip
 int conv_f32(int fmode, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
              float two_gamma, const float* dy, int N, int H, int W, int Ci, int Co, int out_bf16, hipStream_t s);
@@ -88,8 +88,8 @@ static int conv_backward_impl(int mode, const void* dy, const void* x, const uin
   const int cm = (mode == ASR_MODE_EULER) ? 2 : 3;  // BWD_EULER / BWD_CONV
   int nsl = 0;
   if (dtype == ASR_BF16) {
-    if (dx) ASR_TRY(conv_mfma(cm, dy, dx, (uint8_t*)mask, w, nullptr, h, 2.f * gamma, N, H, W, C, s));
-    if (need_w) ASR_TRY(wgrad_mfma(cm, x, dy, mask, h, N, H, W, C, slabs, &nsl, s));
+    if (!dx && !need_w) return ASR_OK;
+    ASR_TRY(block_bwd_mfma(cm, dy, x, mask, w, h, 2.f * gamma, N, H, W, C, dx, slabs, &nsl, s));
   } else {
     float* dz = (float*)(base + L.dz);
     ASR_TRY(make_dz(mode == ASR_MODE_EULER ? F_EULER : F_CONV, dy, mask, nullptr, h, N, H, W, C, 0, dz, s));
@@ -234,7 +234,7 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
     const unsigned char* wl = ws + L.wbuf + (size_t)l * L.wstride * L.act_bytes;
     uint8_t* mask = training ? (uint8_t*)(ws + L.masks) + (size_t)l * L.mask_bytes : nullptr;
     if (bf)
-      ASR_TRY(conv_mfma(0, act(l), act(l + 1), mask, wl, bias, c->h, 0.f, N, H, W, C, s));
+      ASR_TRY(block_fwd_mfma(0, act(l), act(l + 1), mask, wl, bias, c->h, N, H, W, C, s));
     else
       ASR_TRY(conv_f32(F_EULER, act(l), act(l + 1), mask, (const float*)wl, bias, c->h, 0.f, nullptr, N, H, W, C, C,
                        0, s));
@@ -262,7 +262,7 @@ int asr_conv_forward(int mode, const void* x, void* y, uint8_t* mask, const void
   if (dtype == ASR_BF16) {
     if (!mfma_supported(C, W))
       return fail(ASR_E_UNSUPPORTED, "bf16 conv needs C in {16,32,64} and W == 32 (C=%d W=%d)", C, W);
-    return conv_mfma(mode == ASR_MODE_EULER ? 0 : 1, x, y, mask, w, bias, h, 0.f, N, H, W, C, s);
+    return block_fwd_mfma(mode == ASR_MODE_EULER ? 0 : 1, x, y, mask, w, bias, h, N, H, W, C, s);
   }
   if (dtype == ASR_F32)
     return conv_f32(mode == ASR_MODE_EULER ? F_EULER : F_CONV, x, y, mask, (const float*)w, bias, h, 0.f, nullptr, N,

@@ -1,0 +1,753 @@
+// Persistent, LDS-DMA-pipelined bf16 kernels of the antisymmetric Euler block
+// (gfx950): forward, and a FUSED backward (dgrad + wgrad + db in one pass).
+//
+// Reference operator: Conv2DAntisymmetric3By3.call (tf.nn.conv2d SAME NHWC +
+// bias, layers/tfkeras_layer_Conv2DAntisymmetric3By3.py:157-171) inside
+// single_layer_identity_block (relu, h*, +input: models/tfkeras_resnets.py:69-92)
+// and its autodiff (training/training.py:300).
+//
+// Work item = one band of BR output rows of one image.  One 512-thread
+// workgroup per CU walks a contiguous run of items (consecutive bands of the
+// same images, so halo rows are L2 hits).  The input rows of item i+1 are
+// copied HBM -> LDS by global_load_lds (no VGPR staging) while item i is
+// computed; the XOR swizzle of the LDS image is applied on the per-lane
+// SOURCE address (the DMA writes 1 KiB lane-linear), halo columns are zeroed
+// once, rows outside the image come from a zero page.
+//
+// Math (implicit GEMM on v_mfma_f32_16x16x32_bf16, kappa = tap*C + i):
+//   forward  Z^T[o][p]  = sum_kappa W^T[o][kappa] X[p][kappa]      (A = W^T in VGPRs)
+//   dgrad    (A dz)     : the same GEMM on dz = h*dy*mask, because
+//                         A^T = -A + 2*gamma*I for the assembled W:
+//                         dx = dy - A dz + 2*gamma*dz
+//   wgrad    dW[kappa][o] = sum_p X[p + s(tap)][i] dz[p][o]          (K = pixels;
+//                         both operands read with ds_read_b64_tr_b16)
+// In the fused backward, waves 0-3 own the dgrad (W fragments resident in
+// VGPRs) and waves 4-7 own the wgrad (the dW tile set resident in
+// accumulators for the workgroup's whole run); both consume the same LDS
+// images of dz (computed once per item from dy and the relu mask) and x.
+#include <stdlib.h>
+
+#include "asr_common.h"
+
+#ifndef ASR_ABLATE
+#define ASR_ABLATE 0  // development only: fwd 1 no epilogue, 2 no MFMA, 3 no prefetch DMA;
+                      // bwd 4 no convert, 5 no dgrad MFMA, 6 no wgrad MFMA, 7 no dgrad epilogue
+#endif
+
+namespace asr {
+
+namespace blk {
+
+enum { FWD_EULER = 0, FWD_CONV = 1, BWD_EULER = 2, BWD_CONV = 3 };
+
+template <int C>
+struct Geo {
+  static constexpr int NQ = C / 8;              // 16-byte chunks per pixel
+  static constexpr int OT = C / 16;             // 16-channel tiles
+  static constexpr int KS = (9 * C + 31) / 32;  // 32-deep k-steps of the conv GEMM
+  static constexpr int OSPLIT = (C == 64) ? 2 : 1;
+  static constexpr int OTW = OT / OSPLIT;       // o-tiles per conv wave
+  static constexpr int MT = 9 * C / 16;         // wgrad m-tiles
+  static constexpr int MTW = 9;                 // wgrad m-tiles per wave
+  static constexpr int TG = MT / MTW;           // wgrad tile groups
+  static constexpr int KSPLIT = 4 / TG;         // wgrad waves sharing a tile group
+  static constexpr int PPI = 512 / C;           // pixels per 1 KiB DMA instruction
+  __device__ __forceinline__ static int swz(int col) {
+    if constexpr (C == 64) return col & 7;
+    else if constexpr (C == 32) return (col >> 1) & 3;
+    else return 0;
+  }
+};
+
+template <int C>
+__device__ __forceinline__ int toff(int row, int col, int q, int TW) {
+  return ((row * TW + col) * Geo<C>::NQ + (q ^ Geo<C>::swz(col))) * 16;
+}
+
+__device__ __attribute__((aligned(16))) uint4 g_zero_page[64];  // 1 KiB of zeros (DMA source for padding)
+
+typedef const __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+__device__ __forceinline__ void dma16(const void* src, unsigned char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds_wave_base, 16, 0, 0);
+}
+
+// DMA image rows [gy0, gy0+nrows) of image n (rows outside [0,H) -> zeros) into
+// tile rows [0, nrows), interior columns 1..W.  One instruction = PPI pixels.
+// The lane's source offset inside a PPI-pixel segment does not depend on the
+// segment (swz(col) only sees col mod 8 / mod 16, and PPI is a multiple of
+// that), so per instruction only a wave-uniform base changes.
+template <int C, int W>
+__device__ __forceinline__ int dma_lane_off(int lane) {
+  using G = Geo<C>;
+  const int pl = lane / G::NQ, p = lane % G::NQ;
+  return pl * C + (p ^ G::swz(1 + pl)) * 8;  // elements
+}
+
+template <int C, int W>
+__device__ __forceinline__ void dma_rows(const bf16* __restrict__ src, unsigned char* tile, int n, int gy0,
+                                         int nrows, int H, int wave, int nwaves, int lane) {
+  using G = Geo<C>;
+  constexpr int TW = W + 2, NQ = G::NQ, PPI = G::PPI, IPR = W / PPI;
+  static_assert(W % PPI == 0, "image width must be a multiple of the DMA pixel group");
+  static_assert(PPI % 16 == 0 || (PPI % 8 == 0 && C == 64), "segment-invariant swizzle");
+  const int loff = dma_lane_off<C, W>(lane);
+  const bf16* img = src + (long)n * H * W * C;
+  for (int j = wave; j < nrows * IPR; j += nwaves) {
+    const int r = j / IPR, seg = j - r * IPR;  // wave-uniform
+    const int gy = gy0 + r;
+    const void* s = (gy >= 0 && gy < H) ? (const void*)(img + ((long)gy * W + seg * PPI) * C + loff)
+                                        : (const void*)(g_zero_page + lane);
+    dma16(s, tile + ((r * TW + 1 + seg * PPI) * NQ) * 16);
+  }
+}
+
+// DMA the relu-mask bytes of rows [gy0, gy0+nrows) (W*C/8 bytes per row) into
+// a lane-linear LDS array (rows outside the image -> zeros).
+template <int C, int W>
+__device__ __forceinline__ void dma_mask_rows(const uint8_t* __restrict__ mask, unsigned char* mt, int n, int gy0,
+                                              int nrows, int H, int wave, int nwaves, int lane) {
+  constexpr int RB = W * C / 8;  // bytes per image row
+  const int total = nrows * RB;
+  for (int j = wave; j * 1024 < total; j += nwaves) {
+    const int b = j * 1024 + lane * 16;
+    const int r = b / RB, off = b % RB;
+    const int gy = gy0 + r;
+    const void* s = (b < total && gy >= 0 && gy < H) ? (const void*)(mask + ((long)n * H + gy) * RB + off)
+                                                     : (const void*)(g_zero_page + lane);
+    dma16(s, mt + j * 1024);
+  }
+}
+
+// Workgroup barrier that waits only for this wave's vector-memory ops OLDER
+// than its `n` youngest (vmcnt counts loads, stores and LDS-DMA in issue
+// order).  Used so that the barrier guarding an LDS-DMA'd buffer does not
+// also wait for the global stores issued after that DMA.
+__device__ __forceinline__ void barrier_vm(int n) {
+  switch (n) {
+    case 4: asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+  }
+}
+// barrier for LDS data only (in-flight DMA and stores keep flying)
+__device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// zero the halo columns (0 and W+1) of a tile with `rows` rows
+template <int C, int W>
+__device__ __forceinline__ void zero_halo_cols(unsigned char* tile, int rows, int tid, int nthreads) {
+  constexpr int TW = W + 2, NQ = Geo<C>::NQ;
+  for (int i = tid; i < rows * 2 * NQ; i += nthreads) {
+    const int q = i % NQ, side = (i / NQ) & 1, r = i / (2 * NQ);
+    *(uint4*)(tile + toff<C>(r, side ? W + 1 : 0, q, TW)) = make_uint4(0, 0, 0, 0);
+  }
+}
+
+// Per-lane LDS offsets of the conv GEMM's B fragments.  k-step ks covers
+// kappa = 32*ks + 8*g + j (g = lane>>4): for C >= 32 that is tap 32*ks/C and
+// chunk qb + g (qb = (32*ks % C)/8), so only the 3 column shifts x the C/32
+// chunk bases are lane-dependent (3 or 6 VGPRs); the tap row and the pixel
+// tile become ds_read immediates.  For C = 16 the tap itself depends on g,
+// so all KS offsets are lane values.
+template <int C, int W>
+struct Frag {
+  static constexpr int TW = W + 2, NQ = C / 8, KS = Geo<C>::KS;
+  static constexpr int NB = (C >= 32) ? 3 * (C / 32) : KS;
+  int o[NB];
+  __device__ __forceinline__ void init(int g, int lx) {
+    if constexpr (C >= 32) {
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+        for (int cb = 0; cb < C / 32; ++cb) o[kx * (C / 32) + cb] = toff<C>(0, lx + kx, 4 * cb + g, TW);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        int tap = (32 * ks + 8 * g) / C;
+        if (tap > 8) tap = 8;  // C=16 tail k-step: A is zero there
+        o[ks] = toff<C>(tap / 3, lx + tap % 3, (32 * ks + 8 * g) % C / 8, TW);
+      }
+    }
+  }
+  template <int ks>
+  static constexpr int slot() {
+    if constexpr (C >= 32) return ((32 * ks / C) % 3) * (C / 32) + (32 * ks % C) / 32;
+    else return ks;
+  }
+  template <int ks, int pt>
+  static constexpr int imm() {
+    if constexpr (C >= 32) return ((32 * ks / C) / 3) * TW * NQ * 16 + pt * 16 * NQ * 16;
+    else return pt * 16 * NQ * 16;
+  }
+};
+
+__device__ __forceinline__ unsigned lds_u32(const void* p) {
+  return (unsigned)(uintptr_t)((ASR_LDS const unsigned char*)p);
+}
+
+// Hand-scheduled LDS reads (hipcc would otherwise wait lgkmcnt(0) on the
+// just-issued prefetch): "=v" output + explicit counted wait +
+// sched_barrier (cdna_hip_programming.md §5.7, rule 18).
+template <int OFF>
+__device__ __forceinline__ bf16x8 ds_read128(unsigned addr) {
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int C, int W, int ks>
+__device__ __forceinline__ void conv_issue(const unsigned (&ra)[Frag<C, W>::NB], bf16x8 (&B)[W / 16]) {
+  if constexpr (W / 16 >= 1) B[0] = ds_read128<Frag<C, W>::template imm<ks, 0>()>(ra[Frag<C, W>::template slot<ks>()]);
+  if constexpr (W / 16 >= 2) B[1] = ds_read128<Frag<C, W>::template imm<ks, 1>()>(ra[Frag<C, W>::template slot<ks>()]);
+  static_assert(W / 16 <= 2, "conv_issue handles up to two pixel tiles");
+}
+
+// one k-step of the software pipeline: B of step ks lives in buffer ks%3;
+// the reads of step ks+1 are in flight, those of ks+2 are issued after the
+// MFMAs of ks (three buffers: a read never targets registers an MFMA issued
+// in the previous step may still be reading).
+template <int C, int W, int ks>
+__device__ __forceinline__ void conv_step(const unsigned (&ra)[Frag<C, W>::NB],
+                                          const bf16x8 (&A)[Geo<C>::OTW][Geo<C>::KS],
+                                          f32x4 (&acc)[Geo<C>::OTW][W / 16], bf16x8 (&B)[3][W / 16]) {
+  using G = Geo<C>;
+  constexpr int PT = W / 16, KS = G::KS;
+  if constexpr (ks < KS) {
+    lgkm_wait<(ks + 1 < KS) ? PT : 0>();
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt)
+#pragma unroll
+      for (int t = 0; t < G::OTW; ++t)
+        acc[t][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[t][ks], B[ks % 3][pt], acc[t][pt], 0, 0, 0);
+    if constexpr (ks + 2 < KS) conv_issue<C, W, ks + 2>(ra, B[(ks + 2) % 3]);
+    conv_step<C, W, ks + 1>(ra, A, acc, B);
+  }
+}
+
+// conv GEMM of one output row (tile row r is the row above it)
+template <int C, int W>
+__device__ __forceinline__ void conv_row(const unsigned char* tile, int r, const bf16x8 (&A)[Geo<C>::OTW][Geo<C>::KS],
+                                         const Frag<C, W>& f, f32x4 (&acc)[Geo<C>::OTW][W / 16]) {
+  using G = Geo<C>;
+  constexpr int TW = W + 2, PT = W / 16;
+#pragma unroll
+  for (int t = 0; t < G::OTW; ++t)
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt) acc[t][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const unsigned rb = lds_u32(tile + r * TW * G::NQ * 16);
+  unsigned ra[Frag<C, W>::NB];
+#pragma unroll
+  for (int k = 0; k < Frag<C, W>::NB; ++k) ra[k] = rb + (unsigned)f.o[k];
+  bf16x8 B[3][PT];
+  lgkm_wait<0>();  // nothing else of ours outstanding on the LDS counter
+  conv_issue<C, W, 0>(ra, B[0]);
+  if constexpr (G::KS > 1) conv_issue<C, W, 1>(ra, B[1]);
+  conv_step<C, W, 0>(ra, A, acc, B);
+}
+
+template <int C>
+__device__ __forceinline__ void load_A(const bf16* __restrict__ wpack, int oh, int lane,
+                                       bf16x8 (&A)[Geo<C>::OTW][Geo<C>::KS]) {
+  using G = Geo<C>;
+#pragma unroll
+  for (int t = 0; t < G::OTW; ++t)
+#pragma unroll
+    for (int ks = 0; ks < G::KS; ++ks)
+      A[t][ks] = *(const bf16x8*)(wpack + (((long)(oh * G::OTW + t) * G::KS + ks) * 64 + lane) * 8);
+}
+
+// contiguous run of items for this workgroup
+__device__ __forceinline__ void item_range(long items, long* i0, long* i1) {
+  const long per = items / gridDim.x, rem = items % gridDim.x;
+  const long b = blockIdx.x;
+  *i0 = b * per + min(b, rem);
+  *i1 = *i0 + per + (b < rem ? 1 : 0);
+}
+
+// ===========================================================================
+// forward
+// ===========================================================================
+template <int C, int W, int BR, int MODE, int NW>
+__global__ __launch_bounds__(64 * NW) void k_fwd(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                             uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
+                                             const float* __restrict__ bias, float h, int N, int H) {
+  using G = Geo<C>;
+  constexpr int TW = W + 2, PT = W / 16, NQ = G::NQ, OTW = G::OTW;
+  constexpr int TILE = (BR + 2) * TW * NQ * 16;
+  constexpr int RS = NW / G::OSPLIT;  // waves splitting the band's rows
+  constexpr bool EULER = MODE == FWD_EULER;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int oh = wave % G::OSPLIT, rg = wave / G::OSPLIT;
+  const int g = lane >> 4, lx = lane & 15;
+
+  bf16x8 A[OTW][G::KS];
+  load_A<C>(wpack, oh, lane, A);
+  Frag<C, W> boff;
+  boff.init(g, lx);
+  float bz[OTW][4];
+#pragma unroll
+  for (int t = 0; t < OTW; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bz[t][e] = bias ? bias[16 * (oh * OTW + t) + 4 * g + e] : 0.f;
+
+  zero_halo_cols<C, W>(lds, BR + 2, tid, 64 * NW);
+  zero_halo_cols<C, W>(lds + TILE, BR + 2, tid, 64 * NW);
+  const int nb = (H + BR - 1) / BR;
+  long i0, i1;
+  item_range((long)N * nb, &i0, &i1);
+  if (i0 < i1) {
+    const int n = (int)(i0 / nb), y0 = (int)(i0 % nb) * BR;
+    dma_rows<C, W>(x, lds, n, y0 - 1, min(BR, H - y0) + 2, H, wave, NW, lane);
+  }
+  int nst = 0;  // global stores this wave issued after the DMA it must now wait for
+  for (long it = i0; it < i1; ++it) {
+    const int buf = (int)((it - i0) & 1);
+    unsigned char* tile = lds + buf * TILE;
+    barrier_vm(nst);  // this item's DMA has landed; the other buffer is free
+    nst = 0;
+    if (ASR_ABLATE != 3 && it + 1 < i1) {
+      const int n1 = (int)((it + 1) / nb), y1 = (int)((it + 1) % nb) * BR;
+      dma_rows<C, W>(x, lds + (buf ^ 1) * TILE, n1, y1 - 1, min(BR, H - y1) + 2, H, wave, NW, lane);
+    }
+    const int n = (int)(it / nb), y0 = (int)(it % nb) * BR;
+    const int rows = min(BR, H - y0);
+    for (int r = rg; r < rows; r += RS) {
+      f32x4 acc[OTW][PT];
+      if (ASR_ABLATE != 2) {
+        conv_row<C, W>(tile, r, A, boff, acc);
+      } else {
+#pragma unroll
+        for (int t = 0; t < OTW; ++t)
+#pragma unroll
+          for (int pt = 0; pt < PT; ++pt) acc[t][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      if (ASR_ABLATE == 1) {
+#pragma unroll
+        for (int t = 0; t < OTW; ++t)
+#pragma unroll
+          for (int pt = 0; pt < PT; ++pt) asm volatile("" ::"v"(acc[t][pt]));
+        continue;
+      }
+      const int gy = y0 + r;
+      nst += PT * (OTW + ((EULER && mask) ? 1 : 0));
+#pragma unroll
+      for (int pt = 0; pt < PT; ++pt) {
+        const int px = 16 * pt + lx;
+        unsigned mword = 0;
+#pragma unroll
+        for (int t = 0; t < OTW; ++t) {
+          const int o0 = 16 * (oh * OTW + t) + 4 * g;
+          bf16x4 o4;
+          if constexpr (EULER) {
+            const bf16x4 xr = *(const bf16x4*)(tile + toff<C>(r + 1, px + 1, o0 >> 3, TW) + (o0 & 4) * 2);
+            unsigned nib = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float z = acc[t][pt][e] + bz[t][e];
+              nib |= (z > 0.f ? 1u : 0u) << e;
+              o4[e] = (bf16)((float)xr[e] + h * fmaxf(z, 0.f));
+            }
+            mword |= nib << (16 * t + 4 * g);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o4[e] = (bf16)(acc[t][pt][e] + bz[t][e]);
+          }
+          *(bf16x4*)(y + (((long)n * H + gy) * W + px) * C + o0) = o4;
+        }
+        if constexpr (EULER) {
+          mword |= __shfl_xor(mword, 16);
+          mword |= __shfl_xor(mword, 32);
+          if (mask && g == 0) {
+            uint8_t* mp = mask + ((((long)n * H + gy) * W + px) * C + 16 * oh * OTW) / 8;
+            if constexpr (OTW == 2)
+              *(uint32_t*)mp = mword;
+            else
+              *(uint16_t*)mp = (uint16_t)mword;
+          }
+        }
+      }
+    }
+  }
+}
+
+// ===========================================================================
+// fused backward
+// ===========================================================================
+__device__ __forceinline__ bf16x8 tr_pair(const unsigned char* p0, const unsigned char* p1) {
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ASR_LDS s16x4*)p0);
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ASR_LDS s16x4*)p1);
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return *(bf16x8*)&c;
+}
+
+template <int C, int W, int BR>
+struct BwdLds {
+  static constexpr int TW = W + 2;
+  static constexpr int TILE = (BR + 2) * TW * (C / 8) * 16;
+  static constexpr int MTB = (((BR + 2) * W * C / 8) + 1023) / 1024 * 1024;  // mask bytes, 1 KiB-rounded
+  static constexpr int DY = 0;                 // 2 x TILE (dy, halo rows)
+  static constexpr int X = DY + 2 * TILE;      // 2 x TILE (x, halo rows)
+  static constexpr int DZ = X + 2 * TILE;      // 1 x TILE (dz, halo rows)
+  static constexpr int MSK = DZ + TILE;        // 2 x MTB
+  static constexpr int TOTAL = MSK + 2 * MTB;
+};
+
+template <int C, int W, int BR, bool EULER>
+__device__ __forceinline__ void bwd_issue(const bf16* dy, const bf16* x, const uint8_t* mask, unsigned char* lds,
+                                          int buf, long it, int nb, int H, int wave, int lane, int nwaves) {
+  using L = BwdLds<C, W, BR>;
+  const int n = (int)(it / nb), y0 = (int)(it % nb) * BR;
+  const int nr = min(BR, H - y0) + 2;
+  dma_rows<C, W>(dy, lds + L::DY + buf * L::TILE, n, y0 - 1, nr, H, wave, nwaves, lane);
+  dma_rows<C, W>(x, lds + L::X + buf * L::TILE, n, y0 - 1, nr, H, wave, nwaves, lane);
+  if constexpr (EULER) dma_mask_rows<C, W>(mask, lds + L::MSK + buf * L::MTB, n, y0 - 1, nr, H, wave, nwaves, lane);
+}
+
+// dz = h*dy*mask (or dy) for all staged rows, into the DZ tile.
+template <int C, int W, int BR, bool EULER>
+__device__ __forceinline__ void bwd_convert(unsigned char* lds, int buf, int nr, float h, int tid, int nthreads) {
+  using L = BwdLds<C, W, BR>;
+  constexpr int TW = W + 2, NQ = C / 8, KB = 4;
+  const unsigned char* dyt = lds + L::DY + buf * L::TILE;
+  const unsigned char* mt = lds + L::MSK + buf * L::MTB;
+  unsigned char* dzt = lds + L::DZ;
+  const int nch = nr * TW * NQ;
+  for (int c0 = tid; c0 < nch; c0 += KB * nthreads) {
+    uint4 v[KB];
+    unsigned mb[KB];
+    int off[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {  // all LDS reads first (latencies overlap)
+      const int c = c0 + k * nthreads;
+      const int cc = c < nch ? c : 0;
+      const int q = cc % NQ, pc = cc / NQ, col = pc % TW, r = pc / TW;
+      off[k] = toff<C>(r, col, q, TW);
+      v[k] = *(const uint4*)(dyt + off[k]);
+      mb[k] = 0xffu;
+      if constexpr (EULER) mb[k] = (col >= 1 && col <= W) ? mt[(r * W + col - 1) * NQ + q] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      if (c0 + k * nthreads < nch) {
+        const bf16x8 d8 = *(const bf16x8*)&v[k];
+        bf16x8 z8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          z8[j] = (bf16)(((mb[k] >> j) & 1u) ? (EULER ? h * (float)d8[j] : (float)d8[j]) : 0.f);
+        *(bf16x8*)(dzt + off[k]) = z8;
+      }
+    }
+  }
+}
+
+template <int C, int W, int BR, int MODE>
+__global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                             const uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
+                                             float h, float two_gamma, int N, int H, bf16* __restrict__ dx,
+                                             float* __restrict__ slabs) {
+  using G = Geo<C>;
+  using L = BwdLds<C, W, BR>;
+  constexpr int TW = W + 2, PT = W / 16, NQ = G::NQ, OTW = G::OTW, OT = G::OT, MTW = G::MTW;
+  constexpr int KPR = W / 32;
+  constexpr bool EULER = MODE == BWD_EULER;
+  static_assert(W % 32 == 0, "wgrad k-steps are 32 pixels of one row");
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, lx = lane & 15;
+
+  for (int b = 0; b < 2; ++b) {
+    zero_halo_cols<C, W>(lds + L::DY + b * L::TILE, BR + 2, tid, 512);
+    zero_halo_cols<C, W>(lds + L::X + b * L::TILE, BR + 2, tid, 512);
+  }
+  const int nb = (H + BR - 1) / BR;
+  long i0, i1;
+  item_range((long)N * nb, &i0, &i1);
+  if (i0 < i1) bwd_issue<C, W, BR, EULER>(dy, x, mask, lds, 0, i0, nb, H, wave, lane, 8);
+
+  float* slab = slabs + (long)blockIdx.x * (9 * C * C + C);
+  if (wave < 4) {
+    // ---------------- dgrad waves ----------------
+    constexpr int RS = 4 / G::OSPLIT;
+    const int oh = wave % G::OSPLIT, rg = wave / G::OSPLIT;
+    bf16x8 A[OTW][G::KS];
+    load_A<C>(wpack, oh, lane, A);
+    Frag<C, W> boff;
+    boff.init(g, lx);
+    float dbacc[OTW][4];  // db partial for channels 16*(oh*OTW+t) + 4g + e over this lane's pixels
+#pragma unroll
+    for (int t = 0; t < OTW; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dbacc[t][e] = 0.f;
+    int nst = 0;
+    for (long it = i0; it < i1; ++it) {
+      const int buf = (int)((it - i0) & 1);
+      const int n = (int)(it / nb), y0 = (int)(it % nb) * BR;
+      const int rows = min(BR, H - y0);
+      barrier_vm(nst);  // item's DMA landed; previous item fully consumed
+      nst = 0;
+      if (it + 1 < i1) bwd_issue<C, W, BR, EULER>(dy, x, mask, lds, buf ^ 1, it + 1, nb, H, wave, lane, 4);
+      if (ASR_ABLATE != 4) bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, h, tid, 512);
+      barrier_lds();  // dz ready
+      const unsigned char* dzt = lds + L::DZ;
+      const unsigned char* dyt = lds + L::DY + buf * L::TILE;
+      for (int r = rg; r < rows; r += RS) {
+        f32x4 acc[OTW][PT];
+        if (ASR_ABLATE != 5) {
+          conv_row<C, W>(dzt, r, A, boff, acc);
+        } else {
+#pragma unroll
+          for (int t = 0; t < OTW; ++t)
+#pragma unroll
+            for (int pt = 0; pt < PT; ++pt) acc[t][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        if (ASR_ABLATE == 7) {
+#pragma unroll
+          for (int t = 0; t < OTW; ++t)
+#pragma unroll
+            for (int pt = 0; pt < PT; ++pt) asm volatile("" ::"v"(acc[t][pt]));
+          continue;
+        }
+        const int gy = y0 + r;
+        if (dx) nst += PT * OTW;
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt) {
+          const int px = 16 * pt + lx;
+#pragma unroll
+          for (int t = 0; t < OTW; ++t) {
+            const int o0 = 16 * (oh * OTW + t) + 4 * g;
+            const int co = toff<C>(r + 1, px + 1, o0 >> 3, TW) + (o0 & 4) * 2;
+            const bf16x4 dzr = *(const bf16x4*)(dzt + co);
+            const bf16x4 dyr = *(const bf16x4*)(dyt + co);
+            unsigned mb = 0xffu;
+            if constexpr (EULER) mb = (lds + L::MSK + buf * L::MTB)[((r + 1) * W + px) * NQ + (o0 >> 3)] >> (o0 & 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              dbacc[t][e] += ((mb >> e) & 1u) ? (EULER ? h * (float)dyr[e] : (float)dyr[e]) : 0.f;
+            bf16x4 o4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              o4[e] = (bf16)((EULER ? (float)dyr[e] : 0.f) - acc[t][pt][e] + two_gamma * (float)dzr[e]);
+            if (dx) *(bf16x4*)(dx + (((long)n * H + gy) * W + px) * C + o0) = o4;
+          }
+        }
+      }
+    }
+    // reduce db over the 16 pixel lanes, then over the row-group waves (LDS)
+#pragma unroll
+    for (int t = 0; t < OTW; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = dbacc[t][e];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        dbacc[t][e] = v;
+      }
+    barrier_vm(0);  // matches the wgrad waves' end-of-loop barrier
+    float* dbl = (float*)lds + 12288;  // [RS][C], past the K-split scratch
+    if (lx == 0) {
+#pragma unroll
+      for (int t = 0; t < OTW; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dbl[rg * C + 16 * (oh * OTW + t) + 4 * g + e] = dbacc[t][e];
+    }
+    if constexpr (G::KSPLIT > 1) {
+      __syncthreads();
+      __syncthreads();
+    }
+  } else {
+    // ---------------- wgrad waves ----------------
+    const int w4 = wave - 4;
+    const int tg = w4 % G::TG, kg = w4 / G::TG;
+    const int tq = lx >> 2, tp = lx & 3;
+    f32x4 acc[MTW][OT];
+#pragma unroll
+    for (int mi = 0; mi < MTW; ++mi)
+#pragma unroll
+      for (int ot = 0; ot < OT; ++ot) acc[mi][ot] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (long it = i0; it < i1; ++it) {
+      const int buf = (int)((it - i0) & 1);
+      const int y0 = (int)(it % nb) * BR;
+      const int rows = min(BR, H - y0);
+      barrier_vm(0);
+      if (ASR_ABLATE != 4) bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, h, tid, 512);
+      barrier_lds();
+      const unsigned char* dzt = lds + L::DZ;
+      const unsigned char* xt = lds + L::X + buf * L::TILE;
+      for (int kk = kg; kk < (ASR_ABLATE == 6 ? 0 : rows * KPR); kk += G::KSPLIT) {
+        const int r = kk / KPR, kb = kk % KPR;
+        const int pb = 32 * kb + 8 * g + tq;
+        auto loadA = [&](int mi) {
+          const int mt = tg * MTW + mi;
+          const int tap = (16 * mt) / C, itile = ((16 * mt) % C) / 16;
+          const int ky = tap / 3, kx = tap % 3;
+          const int q = 2 * itile + (tp >> 1);
+          return tr_pair(xt + toff<C>(r + ky, pb + kx, q, TW) + 8 * (tp & 1),
+                         xt + toff<C>(r + ky, pb + 4 + kx, q, TW) + 8 * (tp & 1));
+        };
+        bf16x8 Bf[OT];
+#pragma unroll
+        for (int ot = 0; ot < OT; ++ot) {
+          const int q = 2 * ot + (tp >> 1);
+          Bf[ot] = tr_pair(dzt + toff<C>(r + 1, pb + 1, q, TW) + 8 * (tp & 1),
+                           dzt + toff<C>(r + 1, pb + 5, q, TW) + 8 * (tp & 1));
+        }
+        bf16x8 Ac = loadA(0), An;
+#pragma unroll
+        for (int mi = 0; mi < MTW; ++mi) {
+          if (mi + 1 < MTW) An = loadA(mi + 1);
+#pragma unroll
+          for (int ot = 0; ot < OT; ++ot)
+            acc[mi][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ac, Bf[ot], acc[mi][ot], 0, 0, 0);
+          if (mi + 1 < MTW) Ac = An;
+        }
+      }
+    }
+    barrier_vm(0);  // all items consumed: LDS reusable
+    float* red = (float*)lds;
+    if constexpr (G::KSPLIT > 1) {
+      if (kg > 0) {
+#pragma unroll
+        for (int mi = 0; mi < MTW; ++mi)
+#pragma unroll
+          for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              red[((((kg - 1) * G::TG + tg) * MTW + mi) * OT + ot) * 256 + e * 64 + lane] = acc[mi][ot][e];
+      }
+      __syncthreads();
+      if (kg == 0) {
+        for (int k2 = 1; k2 < G::KSPLIT; ++k2)
+#pragma unroll
+          for (int mi = 0; mi < MTW; ++mi)
+#pragma unroll
+            for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                acc[mi][ot][e] += red[((((k2 - 1) * G::TG + tg) * MTW + mi) * OT + ot) * 256 + e * 64 + lane];
+      }
+      __syncthreads();
+    }
+    if (kg == 0) {
+#pragma unroll
+      for (int mi = 0; mi < MTW; ++mi)
+#pragma unroll
+        for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int m = 16 * (tg * MTW + mi) + 4 * g + e;
+            slab[(long)m * C + 16 * ot + lx] = acc[mi][ot][e];
+          }
+    }
+  }
+  __syncthreads();
+  if (tid < C) {
+    const float* dbl = (const float*)lds + 12288;
+    float s = 0.f;
+    for (int q = 0; q < 4 / G::OSPLIT; ++q) s += dbl[q * C + tid];
+    slab[9 * C * C + tid] = s;
+  }
+}
+
+}  // namespace blk
+
+// ---------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------
+constexpr int kFwdBR = 8;
+constexpr int kBwdBR = 4;
+constexpr int kMaxBlockSlabs = 512;
+
+static int persistent_grid(long items) {
+  int cus = cu_count();
+  if (cus <= 0) cus = 256;
+  return (int)std::max<long>(1, std::min<long>({items, (long)cus, (long)kMaxBlockSlabs}));
+}
+
+template <int C, int W, int BR, int NW>
+static int launch_fwd_v(int mode, const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h,
+                        int N, int H, hipStream_t s) {
+  static_assert(NW % blk::Geo<C>::OSPLIT == 0, "waves must cover the o-split");
+  const long items = (long)N * ((H + BR - 1) / BR);
+  int cus = cu_count();
+  if (cus <= 0) cus = 256;
+  const int grid = (int)std::max<long>(1, std::min<long>(items, (long)cus * (8 / NW)));
+  const size_t lds = 2 * (size_t)(BR + 2) * (W + 2) * C * 2;
+  if (mode == blk::FWD_EULER)
+    hipLaunchKernelGGL((blk::k_fwd<C, W, BR, blk::FWD_EULER, NW>), dim3(grid), dim3(64 * NW), lds, s,
+                       (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+  else
+    hipLaunchKernelGGL((blk::k_fwd<C, W, BR, blk::FWD_CONV, NW>), dim3(grid), dim3(64 * NW), lds, s,
+                       (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+  ASR_LAUNCH_CHECK("k_fwd");
+  return ASR_OK;
+}
+
+template <int C, int W>
+static int launch_fwd(int mode, const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h,
+                      int N, int H, hipStream_t s) {
+  static const int variant = [] {
+    const char* e = getenv("ASR_FWD_VARIANT");  // development: A/B of the workgroup geometry
+    return e ? atoi(e) : 1;
+  }();
+  switch (variant) {
+    case 0: return launch_fwd_v<C, W, 8, 8>(mode, x, y, mask, w, bias, h, N, H, s);
+    case 2: return launch_fwd_v<C, W, 2, 2>(mode, x, y, mask, w, bias, h, N, H, s);
+    case 3: return launch_fwd_v<C, W, 8, 4>(mode, x, y, mask, w, bias, h, N, H, s);
+    default: return launch_fwd_v<C, W, 4, 4>(mode, x, y, mask, w, bias, h, N, H, s);
+  }
+}
+
+template <int C, int W>
+static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
+                      float two_gamma, int N, int H, void* dx, float* slabs, int* nslabs, hipStream_t s) {
+  const long items = (long)N * ((H + kBwdBR - 1) / kBwdBR);
+  const int grid = persistent_grid(items);
+  *nslabs = grid;
+  using L = blk::BwdLds<C, W, kBwdBR>;
+  const size_t red = (size_t)(12288 + 4 * 64) * 4;
+  const size_t lds = std::max((size_t)L::TOTAL, red);
+  if (mode == blk::BWD_EULER)
+    hipLaunchKernelGGL((blk::k_bwd<C, W, kBwdBR, blk::BWD_EULER>), dim3(grid), dim3(512), lds, s, (const bf16*)dy,
+                       (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs);
+  else
+    hipLaunchKernelGGL((blk::k_bwd<C, W, kBwdBR, blk::BWD_CONV>), dim3(grid), dim3(512), lds, s, (const bf16*)dy,
+                       (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs);
+  ASR_LAUNCH_CHECK("k_bwd");
+  return ASR_OK;
+}
+
+int block_fwd_mfma(int mode, const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h, int N,
+                   int H, int W, int C, hipStream_t s) {
+  if (W != 32) return fail(ASR_E_UNSUPPORTED, "bf16 block: W=%d not supported (W must be 32)", W);
+  switch (C) {
+    case 16: return launch_fwd<16, 32>(mode, x, y, mask, w, bias, h, N, H, s);
+    case 32: return launch_fwd<32, 32>(mode, x, y, mask, w, bias, h, N, H, s);
+    case 64: return launch_fwd<64, 32>(mode, x, y, mask, w, bias, h, N, H, s);
+  }
+  return fail(ASR_E_UNSUPPORTED, "bf16 block: C=%d not supported (16, 32, 64)", C);
+}
+
+int block_bwd_mfma(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
+                   float two_gamma, int N, int H, int W, int C, void* dx, float* slabs, int* nslabs, hipStream_t s) {
+  if (W != 32) return fail(ASR_E_UNSUPPORTED, "bf16 block: W=%d not supported (W must be 32)", W);
+  switch (C) {
+    case 16: return launch_bwd<16, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, s);
+    case 32: return launch_bwd<32, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, s);
+    case 64: return launch_bwd<64, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, s);
+  }
+  return fail(ASR_E_UNSUPPORTED, "bf16 block: C=%d not supported (16, 32, 64)", C);
+}
+
+}  // namespace asr
