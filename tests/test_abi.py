@@ -1,0 +1,115 @@
+"""CPU tests of the C ABI: libasr.so builds/loads, exports every symbol
+declared in include/asr.h, and its host-side pure functions (parameter maps,
+sizes) agree with the oracle.  No kernel is launched here (no GPU)."""
+import ctypes as ct
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import asr_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from differential_equations_resnet_amd import _lib
+    return _lib.load(build_if_missing=True)
+
+
+def header_functions():
+    text = open(os.path.join(ROOT, "include", "asr.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(asr_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_symbols_exported(lib):
+    names = header_functions()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in include/asr.h but not exported"
+
+
+def test_python_binding_covers_header():
+    from differential_equations_resnet_amd import _lib
+    bound = {n for n, _, _ in _lib.SIGNATURES}
+    assert bound == set(header_functions())
+
+
+def test_abi_version_and_errors(lib):
+    assert lib.asr_abi_version() == 1
+    assert lib.asr_theta_count(0, 0, 1) < 0
+    # a bad-argument call reports through asr_last_error without a GPU
+    rc = lib.asr_param_map(0, 0, 1, None, None)
+    assert rc == -1
+    assert b"asr_param_map" in lib.asr_last_error()
+
+
+@pytest.mark.parametrize("C", [1, 2, 5, 16, 64])
+def test_param_map_3by3_matches_oracle(lib, C):
+    n = lib.asr_theta_count(C, 0, 1)
+    assert n == O.theta_count_3by3(C)
+    w_src = np.empty(9 * C * C, np.int32)
+    dst = np.empty(2 * n, np.int32)
+    assert lib.asr_param_map(C, 0, 1, w_src.ctypes.data, dst.ctypes.data) == 0
+    src, sign = O.param_map(C)
+    want = np.where(src >= 0, (src << 1) | (sign < 0), -1)
+    assert np.array_equal(w_src, want)
+    # theta_dst is the exact inverse: every theta entry feeds 2 W entries with opposite-sign pairs
+    for j in range(n):
+        es = [v >> 1 for v in dst[2 * j:2 * j + 2] if v >= 0]
+        assert len(es) == 2
+        for e in es:
+            assert w_src[e] >> 1 == j
+
+
+@pytest.mark.parametrize("C,anti", [(3, True), (6, True), (4, False)])
+def test_param_map_general_matches_oracle(lib, C, anti):
+    n = lib.asr_theta_count(C, 1, int(anti))
+    assert n == O.theta_count_general(C, 3, anti)
+    w_src = np.empty(9 * C * C, np.int32)
+    dst = np.empty(2 * n, np.int32)
+    assert lib.asr_param_map(C, 1, int(anti), w_src.ctypes.data, dst.ctypes.data) == 0
+    src, sign = O.param_map(C, "general", 3, anti)
+    assert np.array_equal(w_src, np.where(src >= 0, (src << 1) | (sign < 0), -1))
+
+
+def test_projection_through_map_is_autodiff(lib):
+    """dtheta from the ABI's theta_dst pull-back == oracle project_dW."""
+    C = 5
+    n = lib.asr_theta_count(C, 0, 1)
+    w_src = np.empty(9 * C * C, np.int32)
+    dst = np.empty(2 * n, np.int32)
+    lib.asr_param_map(C, 0, 1, w_src.ctypes.data, dst.ctypes.data)
+    dW = np.random.default_rng(0).standard_normal(9 * C * C)
+    got = np.zeros(n)
+    for j in range(n):
+        for v in dst[2 * j:2 * j + 2]:
+            if v >= 0:
+                got[j] += -dW[v >> 1] if v & 1 else dW[v >> 1]
+    src, sign = O.param_map(C)
+    assert np.allclose(got, O.project_dW(dW, src, sign, n))
+
+
+def test_sizes(lib):
+    from differential_equations_resnet_amd import _lib
+    assert lib.asr_wpack_elems(64) == 4 * 18 * 64 * 8
+    assert lib.asr_wpack_elems(16) == 1 * 5 * 64 * 8
+    assert lib.asr_wpack_elems(20) < 0
+    assert lib.asr_mask_bytes(2, 32, 32, 64) == 2 * 32 * 32 * 64 // 8
+    assert lib.asr_conv_backward_workspace_bytes(2, 32, 32, 64, 1) > 0
+    cfg = _lib.NetConfig(512, 32, 32, 3, 64, 30, 10, 8 / 30, 0.0, 127.5, 127.5, 1, 1, 1)
+    assert lib.asr_net_param_count(ct.byref(cfg)) == O.NetSpec(C=64, L=30).n_params()
+    ws = lib.asr_net_workspace_bytes(ct.byref(cfg))
+    assert 2e9 < ws < 8e9  # activations of 31 layers + masks + slabs
+    bad = _lib.NetConfig(512, 32, 24, 3, 64, 30, 10, 0.1, 0.0, 0.0, 1.0, 0, 1, 1)  # bf16 needs W == 32
+    assert lib.asr_net_workspace_bytes(ct.byref(bad)) == 0
+
+
+def test_netparams_layout_matches_oracle():
+    from differential_equations_resnet_amd import netparams
+    assert netparams.net_param_shapes(16, 3) == O.NetSpec(C=16, L=3).param_shapes()
+    flat = netparams.init_net_params(16, 3, seed=1)
+    assert flat.dtype == np.float32 and flat.size == O.NetSpec(C=16, L=3).n_params()
