@@ -226,8 +226,7 @@ def main():
                 traffic = json.load(f).get("hbm_bytes_per_block")
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "Euler block fwd+bwd (k_conv_mfma fwd, k_conv_mfma dgrad, k_wgrad_mfma, k_reduce_slabs, "
-                          "k_project)",
+                "kernel": "Euler block fwd+bwd (blk::k_fwd, blk::k_bwd fused dgrad+wgrad, k_reduce_slabs, k_project)",
                 "algorithmic_bytes": rb["bytes"], "avg_us": round(rb["t"] * 1e6, 2),
                 "avg_us_fwd": round(rb["t_fwd"] * 1e6, 2), "avg_us_bwd": round(rb["t_bwd"] * 1e6, 2),
                 "mfma_tflops": round(tflops, 1), "mfma_frac": round(tflops / peak_tf, 4)}

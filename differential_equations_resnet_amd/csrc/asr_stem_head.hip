@@ -32,44 +32,51 @@ __device__ __forceinline__ void stage_image(const Tin* __restrict__ img, float* 
 }
 
 // conv1 forward: out = relu(conv3x3(norm(img)) + b); one image per block
-// iteration, thread = (pixel, VEC-channel chunk).
+// iteration; thread = (VEC-channel group, pixel lane) with its 9*CIN*VEC
+// weights in registers, the normalised image tile in LDS.
 template <int CIN, typename Tin, typename Tout, int VEC>
 __global__ __launch_bounds__(256) void k_stem_fwd(const Tin* __restrict__ img, const float* __restrict__ w1,
                                                   const float* __restrict__ b1, int N, int H, int W, int C,
                                                   float mean, float inv_std, int use_norm, Tout* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* ws = sm;                           // 9*CIN*C
-  float* bs = ws + 9 * CIN * C;             // C
-  float* tile = bs + ((C + 3) & ~3);        // (H+2)(W+2)CIN
-  for (int i = threadIdx.x; i < 9 * CIN * C; i += blockDim.x) ws[i] = w1[i];
-  for (int i = threadIdx.x; i < C; i += blockDim.x) bs[i] = b1 ? b1[i] : 0.f;
-  const int NQ = C / VEC, TW = W + 2;
+  float* tile = sm;  // (H+2)(W+2)CIN
+  const int NG = C / VEC, PLN = max(1, 256 / NG);
+  const int cg = threadIdx.x % NG, pl = threadIdx.x / NG;
+  const bool active = threadIdx.x < PLN * NG;
+  float wr[9 * CIN][VEC], bz[VEC];
+#pragma unroll
+  for (int k = 0; k < 9 * CIN; ++k)
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) wr[k][v] = active ? w1[k * C + cg * VEC + v] : 0.f;
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) bz[v] = (active && b1) ? b1[cg * VEC + v] : 0.f;
+  const int TW = W + 2;
   for (int n = blockIdx.x; n < N; n += gridDim.x) {
     __syncthreads();
     stage_image<CIN>(img + (long)n * H * W * CIN, tile, H, W, mean, inv_std, use_norm);
     __syncthreads();
-    for (int it = threadIdx.x; it < H * W * NQ; it += blockDim.x) {
-      const int q = it % NQ, p = it / NQ, x = p % W, y = p / W;
+    if (!active) continue;
+    for (int p = pl; p < H * W; p += PLN) {
+      const int x = p % W, y = p / W;
       float acc[VEC];
 #pragma unroll
-      for (int v = 0; v < VEC; ++v) acc[v] = bs[q * VEC + v];
+      for (int v = 0; v < VEC; ++v) acc[v] = bz[v];
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const float* tp = tile + ((y + tap / 3) * TW + x + tap % 3) * CIN;
 #pragma unroll
         for (int ci = 0; ci < CIN; ++ci) {
           const float xv = tp[ci];
-          const float* wr = ws + (tap * CIN + ci) * C + q * VEC;
 #pragma unroll
-          for (int v = 0; v < VEC; ++v) acc[v] = fmaf(xv, wr[v], acc[v]);
+          for (int v = 0; v < VEC; ++v) acc[v] = fmaf(xv, wr[tap * CIN + ci][v], acc[v]);
         }
       }
-      Tout* o = out + ((long)n * H * W + p) * C + q * VEC;
-      if constexpr (VEC == 8 && sizeof(Tout) == 2) {
-        bf16x8 r;
+      Tout* o = out + ((long)n * H * W + p) * C + cg * VEC;
+      if constexpr (VEC == 4 && sizeof(Tout) == 2) {
+        bf16x4 r;
 #pragma unroll
-        for (int v = 0; v < 8; ++v) r[v] = (bf16)fmaxf(acc[v], 0.f);
-        *(bf16x8*)o = r;
+        for (int v = 0; v < 4; ++v) r[v] = (bf16)fmaxf(acc[v], 0.f);
+        *(bf16x4*)o = r;
       } else {
 #pragma unroll
         for (int v = 0; v < VEC; ++v) o[v] = from_f32<Tout>(fmaxf(acc[v], 0.f));
@@ -102,17 +109,30 @@ __global__ __launch_bounds__(256) void k_stem_wgrad(const Tin* __restrict__ img,
     if (active) {
       const T* d = dx1 + (long)n * H * W * C;
       const T* a = x1 + (long)n * H * W * C;
-      for (int p = pl; p < H * W; p += PG) {
-        const float dv = to_f32(d[(long)p * C + o]);
-        const float g = to_f32(a[(long)p * C + o]) > 0.f ? dv : 0.f;
-        const int x = p % W, y = p / W;
+      constexpr int U = 8;  // pixels per batch: all global loads issued before use
+      for (int p0 = pl; p0 < H * W; p0 += U * PG) {
+        float gv[U];
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-          const float* tp = tile + ((y + tap / 3) * TW + x + tap % 3) * CIN;
-#pragma unroll
-          for (int ci = 0; ci < CIN; ++ci) acc[tap * CIN + ci] = fmaf(tp[ci], g, acc[tap * CIN + ci]);
+        for (int u = 0; u < U; ++u) {
+          const int p = p0 + u * PG;
+          const int pc = p < H * W ? p : 0;
+          const float dv = to_f32(d[(long)pc * C + o]);
+          const float av = to_f32(a[(long)pc * C + o]);
+          gv[u] = (p < H * W && av > 0.f) ? dv : 0.f;
         }
-        acc[KC] += g;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int p = p0 + u * PG;
+          const int pc = p < H * W ? p : 0;
+          const int x = pc % W, y = pc / W;
+#pragma unroll
+          for (int tap = 0; tap < 9; ++tap) {
+            const float* tp = tile + ((y + tap / 3) * TW + x + tap % 3) * CIN;
+#pragma unroll
+            for (int ci = 0; ci < CIN; ++ci) acc[tap * CIN + ci] = fmaf(tp[ci], gv[u], acc[tap * CIN + ci]);
+          }
+          acc[KC] += gv[u];
+        }
       }
     }
   }
@@ -312,9 +332,9 @@ static int stem_grid(int N) { return std::max(1, std::min(N, kMaxSlabsStem)); }
 template <int CIN, typename Tin, typename Tout>
 static void launch_stem_fwd(const void* img, const float* w1, const float* b1, int N, int H, int W, int C, float mean,
                             float inv_std, int use_norm, void* out, hipStream_t s) {
-  const size_t lds = ((size_t)9 * CIN * C + ((C + 3) & ~3) + (size_t)(H + 2) * (W + 2) * CIN) * 4;
-  if (C % 8 == 0)
-    hipLaunchKernelGGL((k_stem_fwd<CIN, Tin, Tout, 8>), dim3(stem_grid(N)), dim3(256), lds, s, (const Tin*)img, w1,
+  const size_t lds = (size_t)(H + 2) * (W + 2) * CIN * 4;
+  if (C % 4 == 0)
+    hipLaunchKernelGGL((k_stem_fwd<CIN, Tin, Tout, 4>), dim3(stem_grid(N)), dim3(256), lds, s, (const Tin*)img, w1,
                        b1, N, H, W, C, mean, inv_std, use_norm, (Tout*)out);
   else
     hipLaunchKernelGGL((k_stem_fwd<CIN, Tin, Tout, 1>), dim3(stem_grid(N)), dim3(256), lds, s, (const Tin*)img, w1,

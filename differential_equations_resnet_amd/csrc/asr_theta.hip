@@ -234,23 +234,30 @@ __global__ void k_reduce_slabs(const float* __restrict__ in, long E, int P, int 
 // dtheta[j] = sum over the (<=2) W entries theta j feeds of sign * dW[e],
 // from the fully reduced slab row [dW (E floats) | db (Cb floats)].  Also an
 // optional dW copy and db.
-__global__ void k_project(const float* __restrict__ red, long E, const int32_t* __restrict__ theta_dst, long n_theta,
-                          float* __restrict__ dtheta, float* __restrict__ dw_out, int Cb, float* __restrict__ dbias) {
+__global__ void k_project(const float* __restrict__ red_groups, int G, long E, const int32_t* __restrict__ theta_dst,
+                          long n_theta, float* __restrict__ dtheta, float* __restrict__ dw_out, int Cb,
+                          float* __restrict__ dbias) {
   const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long ES = E + Cb;
+  auto red_at = [&](long e) {  // sum of the G group partials (fixed order: deterministic)
+    float a = 0.f;
+    for (int g = 0; g < G; ++g) a += red_groups[(long)g * ES + e];
+    return a;
+  };
   if (dtheta && t < n_theta) {
     float acc = 0.f;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int32_t v = theta_dst[2 * t + q];
       if (v >= 0) {
-        const float d = red[v >> 1];
+        const float d = red_at(v >> 1);
         acc += (v & 1) ? -d : d;
       }
     }
     dtheta[t] = acc;
   }
-  if (dw_out && t < E) dw_out[t] = red[t];
-  if (dbias && t < Cb) dbias[t] = red[E + t];
+  if (dw_out && t < E) dw_out[t] = red_at(t);
+  if (dbias && t < Cb) dbias[t] = red_at(E + t);
 }
 
 }  // namespace asr
@@ -318,14 +325,9 @@ int reduce_and_project(const float* slabs, int P, long E, int Cb, const int32_t*
   dim3 g1((unsigned)((ES + 255) / 256), G);
   hipLaunchKernelGGL(k_reduce_slabs, g1, dim3(256), 0, s, slabs, ES, P, per, grp);
   ASR_LAUNCH_CHECK("k_reduce_slabs");
-  const float* red = grp;
-  if (G > 1) {
-    hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)((ES + 255) / 256), 1), dim3(256), 0, s, grp, ES, G, G, fin);
-    ASR_LAUNCH_CHECK("k_reduce_slabs");
-    red = fin;
-  }
+  (void)fin;
   const long n = std::max(std::max(dtheta ? n_theta : 0L, dw_out ? E : 0L), (long)Cb);
-  hipLaunchKernelGGL(k_project, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, red, E, theta_dst,
+  hipLaunchKernelGGL(k_project, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, grp, G, E, theta_dst,
                      dtheta ? n_theta : 0L, dtheta, dw_out, Cb, dbias);
   ASR_LAUNCH_CHECK("k_project");
   return ASR_OK;
