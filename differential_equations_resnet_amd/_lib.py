@@ -28,6 +28,8 @@ ASR_F32 = 0
 ASR_BF16 = 1
 ASR_PARAM_3BY3 = 0
 ASR_PARAM_GENERAL = 1
+ASR_PARAM_REGULAR = 2
+ABI_VERSION = 2
 ASR_MODE_EULER = 0
 ASR_MODE_CONV = 1
 
@@ -45,6 +47,7 @@ class NetConfig(ct.Structure):
         ("N", ct.c_int), ("H", ct.c_int), ("W", ct.c_int), ("Cin", ct.c_int), ("C", ct.c_int), ("L", ct.c_int),
         ("num_classes", ct.c_int), ("h", ct.c_float), ("gamma", ct.c_float), ("subtract_mean", ct.c_float),
         ("divide_by_stddev", ct.c_float), ("use_norm", ct.c_int), ("dtype", ct.c_int), ("input_u8", ct.c_int),
+        ("param_kind", ct.c_int), ("antisymmetric", ct.c_int),
     ]
 
 
@@ -61,6 +64,8 @@ SIGNATURES = [
     ("asr_device_cu_count", _I, []),
     ("asr_theta_count", _L, [_I, _I, _I]),
     ("asr_param_map", _I, [_I, _I, _I, _P, _P]),
+    ("asr_param_is_antisymmetric", _I, [_I, _I]),
+    ("asr_param_map_transpose", _I, [_I, _P, _P]),
     ("asr_wpack_elems", _L, [_I]),
     ("asr_theta_to_w", _I, [_P, _L, _I, _I, _P, _F, _P, _L, _I, _P]),
     ("asr_conv_forward", _I, [_I, _P, _P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P]),
@@ -73,6 +78,8 @@ SIGNATURES = [
     ("asr_net_forward", _I, [ct.POINTER(NetConfig), _P, _P, _P, _P, _S, _P]),
     ("asr_net_forward_backward", _I, [ct.POINTER(NetConfig), _P, _P, _P, _P, _P, _P, _P, _S, _P]),
     ("asr_adam_update", _I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _L, _F, _P]),
+    ("asr_segment_sq_norms", _I, [_P, _P, _I, _P, _P]),
+    ("asr_batch_metrics", _I, [_P, _P, _P, _I, _I, _P, _P]),
 ]
 
 _lib = None

@@ -16,6 +16,8 @@ namespace asr {
 // asr_theta.hip
 long theta_count(int C, int kind, int antisymmetric);
 int param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta_dst);
+int param_is_antisymmetric(int kind, int antisymmetric);
+int param_map_transpose(int C, const int32_t* w_src, int32_t* w_bwd);
 int reduce_and_project(const float* slabs, int P, long E, int Cb, const int32_t* theta_dst, long n_theta,
                        float* dtheta, float* dbias, float* dw_out, float* ws, hipStream_t s);
 size_t reduce_ws_bytes(int P, long ES);
@@ -120,6 +122,59 @@ __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float
 }
 
 // ---------------------------------------------------------------------------
+// metrics
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_segment_sq_norms(const float* __restrict__ x, const long* __restrict__ off,
+                                                          float* __restrict__ out) {
+  const long b = off[blockIdx.x], e = off[blockIdx.x + 1];
+  float acc = 0.f;
+  for (long i = b + threadIdx.x; i < e; i += blockDim.x) acc = fmaf(x[i], x[i], acc);
+  for (int d = 32; d >= 1; d >>= 1) acc += __shfl_xor(acc, d, 64);
+  __shared__ float part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = (part[0] + part[1]) + (part[2] + part[3]);
+}
+
+// loss == nullptr: the batch-mean Keras categorical cross-entropy is computed
+// from the probabilities here (evaluation runs forward only).
+__global__ __launch_bounds__(256) void k_batch_metrics(const float* __restrict__ probs, const float* __restrict__ tgt,
+                                                       const float* __restrict__ loss, int N, int K,
+                                                       float* __restrict__ accum) {
+  __shared__ int correct;
+  __shared__ float lsum[4];
+  if (threadIdx.x == 0) correct = 0;
+  __syncthreads();
+  float l = 0.f;
+  for (int n = threadIdx.x; n < N; n += blockDim.x) {
+    const float* p = probs + (long)n * K;
+    const float* t = tgt + (long)n * K;
+    int ap = 0, at = 0;
+    float bp = p[0], bt = t[0], s = 0.f;
+    for (int k = 0; k < K; ++k) {  // first maximum, as tf.argmax
+      if (p[k] > bp) bp = p[k], ap = k;
+      if (t[k] > bt) bt = t[k], at = k;
+      s += p[k];
+    }
+    if (ap == at) atomicAdd(&correct, 1);
+    if (!loss)
+      for (int k = 0; k < K; ++k) {
+        const float q = fminf(fmaxf(p[k] / s, 1e-7f), 1.f - 1e-7f);
+        l -= t[k] * logf(q);
+      }
+  }
+  for (int d = 32; d >= 1; d >>= 1) l += __shfl_xor(l, d, 64);
+  if ((threadIdx.x & 63) == 0) lsum[threadIdx.x >> 6] = l;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    accum[0] += loss ? *loss : ((lsum[0] + lsum[1]) + (lsum[2] + lsum[3])) / (float)N;
+    accum[1] += (float)correct;
+    accum[2] += (float)N;
+    accum[3] += 1.f;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // network layout
 // ---------------------------------------------------------------------------
 template <typename Tin>
@@ -135,7 +190,8 @@ __global__ void k_normalize(const Tin* __restrict__ img, long n, float mean, flo
 struct NetLayout {
   long ntheta, P, E, wstride;  // wstride in elements of the W dtype
   long off_c1k, off_c1b, off_blk, blk_stride, off_fck, off_fcb, nparams;
-  size_t w_src, theta_dst, wbuf, x0, acts, masks, dxa, dxb, bwdws, slabs, red, probs, loss_per, dlogits, gap, total;
+  bool sep_bwd;  // operator not antisymmetric: dgrad uses W_bwd = -flip(W)^T
+  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, x0, acts, masks, dxa, dxb, bwdws, slabs, red, probs, loss_per, dlogits, gap, total;
   long mask_bytes;
   int act_bytes;
   bool fast_stem;
@@ -147,6 +203,9 @@ static int net_check(const asr_net_config* c) {
   if (c->L < 1 || c->Cin < 1 || c->num_classes < 1 || c->num_classes > 256 || c->C > 256)
     return fail(ASR_E_ARG, "bad net config (L=%d Cin=%d K=%d C=%d)", c->L, c->Cin, c->num_classes, c->C);
   if (c->dtype != ASR_F32 && c->dtype != ASR_BF16) return fail(ASR_E_ARG, "bad dtype");
+  if (param_is_antisymmetric(c->param_kind, c->antisymmetric) < 0) return ASR_E_ARG;
+  if (c->param_kind == ASR_PARAM_3BY3 && !c->antisymmetric)
+    return fail(ASR_E_ARG, "the 3by3 parametrisation is always antisymmetric");
   if (c->dtype == ASR_BF16 && !mfma_supported(c->C, c->W))
     return fail(ASR_E_UNSUPPORTED, "bf16 network needs C in {16,32,64} and W == 32 (C=%d W=%d)", c->C, c->W);
   return ASR_OK;
@@ -155,7 +214,8 @@ static int net_check(const asr_net_config* c) {
 static NetLayout net_layout(const asr_net_config* c) {
   NetLayout L{};
   const int C = c->C, K = c->num_classes;
-  L.ntheta = theta_count(C, ASR_PARAM_3BY3, 1);
+  L.ntheta = theta_count(C, c->param_kind, c->antisymmetric);
+  L.sep_bwd = param_is_antisymmetric(c->param_kind, c->antisymmetric) == 0;
   L.P = (long)c->N * c->H * c->W * C;
   L.E = 9L * C * C;
   L.act_bytes = c->dtype == ASR_BF16 ? 2 : 4;
@@ -176,8 +236,10 @@ static NetLayout net_layout(const asr_net_config* c) {
     return o;
   };
   L.w_src = take((size_t)L.E * 4);
+  L.w_src_bwd = take(L.sep_bwd ? (size_t)L.E * 4 : 0);
   L.theta_dst = take((size_t)L.ntheta * 2 * 4);
   L.wbuf = take((size_t)c->L * L.wstride * L.act_bytes);
+  L.wbuf_bwd = take(L.sep_bwd ? (size_t)c->L * L.wstride * L.act_bytes : 0);
   L.x0 = take(L.fast_stem ? 0 : (size_t)c->N * c->H * c->W * c->Cin * 4);
   L.acts = take((size_t)(c->L + 1) * L.P * L.act_bytes);
   L.masks = take((size_t)c->L * L.mask_bytes);
@@ -205,6 +267,9 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
   // 1. materialise W for all L blocks (one launch)
   ASR_TRY(asr_theta_to_w(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src), c->gamma,
                          ws + L.wbuf, L.wstride, c->dtype, s));
+  if (training && L.sep_bwd)
+    ASR_TRY(asr_theta_to_w(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src_bwd), 0.f,
+                           ws + L.wbuf_bwd, L.wstride, c->dtype, s));
   unsigned char* acts = ws + L.acts;
   auto act = [&](int i) -> unsigned char* {
     const int slot = training ? i : (i & 1);
@@ -308,8 +373,13 @@ int asr_net_prepare(const asr_net_config* cfg, void* ws, size_t ws_bytes) {
   const NetLayout L = net_layout(cfg);
   if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_net_prepare: workspace too small");
   std::vector<int32_t> w_src((size_t)L.E), theta_dst((size_t)L.ntheta * 2);
-  ASR_TRY(param_map(cfg->C, ASR_PARAM_3BY3, 1, w_src.data(), theta_dst.data()));
+  ASR_TRY(param_map(cfg->C, cfg->param_kind, cfg->antisymmetric, w_src.data(), theta_dst.data()));
   unsigned char* b = (unsigned char*)ws;
+  if (L.sep_bwd) {
+    std::vector<int32_t> w_bwd((size_t)L.E);
+    ASR_TRY(param_map_transpose(cfg->C, w_src.data(), w_bwd.data()));
+    ASR_TRY(hip_check(hipMemcpy(b + L.w_src_bwd, w_bwd.data(), w_bwd.size() * 4, hipMemcpyHostToDevice), "hipMemcpy"));
+  }
   ASR_TRY(hip_check(hipMemcpy(b + L.w_src, w_src.data(), w_src.size() * 4, hipMemcpyHostToDevice), "hipMemcpy"));
   ASR_TRY(hip_check(hipMemcpy(b + L.theta_dst, theta_dst.data(), theta_dst.size() * 4, hipMemcpyHostToDevice),
                     "hipMemcpy"));
@@ -355,11 +425,12 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   // Euler blocks, last to first
   const int32_t* theta_dst = (const int32_t*)(b + L.theta_dst);
   for (int l = cfg->L - 1; l >= 0; --l) {
-    const unsigned char* wl = b + L.wbuf + (size_t)l * L.wstride * L.act_bytes;
+    const unsigned char* wl = b + (L.sep_bwd ? L.wbuf_bwd : L.wbuf) + (size_t)l * L.wstride * L.act_bytes;
     const uint8_t* mask = (const uint8_t*)(b + L.masks) + (size_t)l * L.mask_bytes;
     float* dth = grads + L.off_blk + (long)l * L.blk_stride;
-    ASR_TRY(conv_backward_impl(ASR_MODE_EULER, dcur, act(l), mask, wl, theta_dst, L.ntheta, cfg->h, cfg->gamma, N, H,
-                               W, C, cfg->dtype, dnext, dth, dth + L.ntheta, nullptr, b + L.bwdws, s));
+    ASR_TRY(conv_backward_impl(ASR_MODE_EULER, dcur, act(l), mask, wl, theta_dst, L.ntheta, cfg->h,
+                               L.sep_bwd ? 0.f : cfg->gamma, N, H, W, C, cfg->dtype, dnext, dth, dth + L.ntheta,
+                               nullptr, b + L.bwdws, s));
     std::swap(dcur, dnext);
   }
   // stem: dz1 = dx1 * [x1 > 0]; conv1 weight/bias gradient from the normalised input
@@ -378,6 +449,22 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
     ASR_TRY(wgrad_f32(b + L.x0, 0, dz, N, H, W, cfg->Cin, C, slabs, &nsl, s));
   }
   ASR_TRY(reduce_and_project(slabs, nsl, E1, C, nullptr, 0, nullptr, grads + L.off_c1b, grads + L.off_c1k, red, s));
+  return ASR_OK;
+}
+
+int asr_segment_sq_norms(const float* x, const long* offsets, int n_segments, float* out, asr_stream_t stream) {
+  if (!x || !offsets || !out || n_segments < 0) return fail(ASR_E_ARG, "asr_segment_sq_norms: bad arguments");
+  if (n_segments == 0) return ASR_OK;
+  hipLaunchKernelGGL(k_segment_sq_norms, dim3(n_segments), dim3(256), 0, (hipStream_t)stream, x, offsets, out);
+  ASR_LAUNCH_CHECK("k_segment_sq_norms");
+  return ASR_OK;
+}
+
+int asr_batch_metrics(const float* probs, const float* targets, const float* loss, int N, int K, float* accum,
+                      asr_stream_t stream) {
+  if (!probs || !targets || !accum || N < 1 || K < 1) return fail(ASR_E_ARG, "asr_batch_metrics: bad args");
+  hipLaunchKernelGGL(k_batch_metrics, dim3(1), dim3(256), 0, (hipStream_t)stream, probs, targets, loss, N, K, accum);
+  ASR_LAUNCH_CHECK("k_batch_metrics");
   return ASR_OK;
 }
 

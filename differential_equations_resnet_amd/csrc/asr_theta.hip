@@ -76,6 +76,7 @@ long theta_count(int C, int kind, int antisymmetric) {
     general_free_positions(antisymmetric, fp);
     return (long)fp.size() * C + 9L * C * (C - 1) / 2;
   }
+  if (kind == ASR_PARAM_REGULAR) return 9L * C * C;
   return -1;
 }
 
@@ -135,6 +136,8 @@ int param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta
         off += 9L * nind;
       }
     }
+  } else if (kind == ASR_PARAM_REGULAR) {
+    for (long e = 0; e < E; ++e) w_src[e] = (int32_t)(e << 1);
   } else {
     return fail(ASR_E_ARG, "asr_param_map: unknown kind %d", kind);
   }
@@ -154,6 +157,29 @@ int param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta
         return fail(ASR_E_ARG, "asr_param_map: theta %ld feeds more than two W entries", j);
     }
   }
+  return ASR_OK;
+}
+
+int param_is_antisymmetric(int kind, int antisymmetric) {
+  if (kind == ASR_PARAM_3BY3) return 1;
+  if (kind == ASR_PARAM_GENERAL) return antisymmetric ? 1 : 0;
+  if (kind == ASR_PARAM_REGULAR) return 0;
+  return fail(ASR_E_ARG, "asr_param_is_antisymmetric: unknown kind %d", kind);
+}
+
+// W_bwd[ky,kx,i,o] = -W[2-ky,2-kx,o,i]: conv(dz, W_bwd) = -A^T dz, so the
+// backward's dx = dy - conv(dz, W_bwd) (+ 2*0*dz) is dy + A^T dz for any W.
+int param_map_transpose(int C, const int32_t* w_src, int32_t* w_bwd) {
+  if (C < 1 || !w_src || !w_bwd) return fail(ASR_E_ARG, "asr_param_map_transpose: bad arguments");
+  auto idx = [C](int ky, int kx, int i, int o) { return ((long)(ky * 3 + kx) * C + i) * C + o; };
+  for (int ky = 0; ky < 3; ++ky)
+    for (int kx = 0; kx < 3; ++kx)
+      for (int i = 0; i < C; ++i)
+        for (int o = 0; o < C; ++o) {
+          const int32_t v = w_src[idx(2 - ky, 2 - kx, o, i)];
+          if (v < 0) return fail(ASR_E_ARG, "asr_param_map_transpose: map has constant (gamma) entries");
+          w_bwd[idx(ky, kx, i, o)] = v ^ 1;
+        }
   return ASR_OK;
 }
 
@@ -267,13 +293,19 @@ using namespace asr;
 extern "C" {
 
 const char* asr_last_error(void) { return g_err; }
-int asr_abi_version(void) { return 1; }
+int asr_abi_version(void) { return 2; }
 int asr_device_cu_count(void) { return cu_count(); }
 
 long asr_theta_count(int C, int kind, int antisymmetric) { return theta_count(C, kind, antisymmetric); }
 
 int asr_param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta_dst) {
   return param_map(C, kind, antisymmetric, w_src, theta_dst);
+}
+
+int asr_param_is_antisymmetric(int kind, int antisymmetric) { return param_is_antisymmetric(kind, antisymmetric); }
+
+int asr_param_map_transpose(int C, const int32_t* w_src, int32_t* w_src_bwd) {
+  return param_map_transpose(C, w_src, w_src_bwd);
 }
 
 long asr_wpack_elems(int C) {

@@ -36,16 +36,35 @@ def he_normal(rng: np.random.Generator, shape) -> np.ndarray:
     return truncated_normal(rng, shape, math.sqrt(2.0 / max(fan_in, 1)) / TRUNC_STD)
 
 
+def _fans(shape):
+    if len(shape) < 2:
+        return int(shape[0]) if shape else 1, int(shape[0]) if shape else 1
+    rf = int(np.prod(shape[:-2])) if len(shape) > 2 else 1
+    return rf * int(shape[-2]), rf * int(shape[-1])
+
+
+def glorot_uniform(rng: np.random.Generator, shape) -> np.ndarray:
+    """Keras default kernel initialiser: U(-l, l), l = sqrt(6/(fan_in+fan_out))."""
+    fi, fo = _fans(shape)
+    lim = math.sqrt(6.0 / max(fi + fo, 1))
+    return rng.uniform(-lim, lim, size=shape).astype(np.float32)
+
+
 def zeros(shape) -> np.ndarray:
     return np.zeros(shape, dtype=np.float32)
 
 
 def get(identifier):
-    """Resolve a Keras-style initializer identifier to fn(rng, shape, **ctx)."""
+    """Resolve a Keras-style initializer identifier to fn(rng, shape, **ctx)
+    (callables are used as such and must accept that signature)."""
     if callable(identifier):
         return identifier
     if identifier in (None, "zeros"):
         return lambda rng, shape, **_: zeros(shape)
+    if identifier == "ones":
+        return lambda rng, shape, **_: np.ones(shape, np.float32)
+    if identifier == "glorot_uniform":
+        return lambda rng, shape, **_: glorot_uniform(rng, shape)
     if identifier == "he_normal":
         return lambda rng, shape, **_: he_normal(rng, shape)
     if identifier == "antisymmetric_he_normal":

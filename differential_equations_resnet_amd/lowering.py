@@ -1,0 +1,290 @@
+"""Lowering of a graph Model onto the native executor (asr_net_*).
+
+The pattern recognised is the reference's single-block ResNet as built by
+get_single_block_resnet_build_function with one stage of identity blocks
+(tfkeras_resnets.py:547-597), which is what every antisymmetric experiment
+runs (_v6.ipynb cells 5-9):
+
+    Input -> Lambda* (elementwise affine: identity / x-mean / x/std)
+          -> Conv2D 3x3 'same' stride 1 (conv1) -> relu
+          -> L x [ conv 3x3 (Conv2DAntisymmetric3By3 | Conv2DAntisymmetric(k=3) | Conv2D)
+                   -> relu -> Lambda(h*x)? -> add(branch, block input) ]
+          -> GlobalAveragePooling2D -> Dense(K, softmax)
+
+Anything else (BN, pooling, stage transitions, strided or non-3x3 convs,
+per-block differing h/gamma) raises AsrUnsupported naming the layer: there
+is no fallback executor.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from .graph import (Activation, Add, Conv2D, Dense, GlobalAveragePooling2D, InputLayer, Lambda, Model,
+                    SymbolicTensor)
+from .layers._antisymmetric import AntisymmetricConvBase
+
+__all__ = ["NetPlan", "analyze", "NativeModel"]
+
+
+@dataclass
+class NetPlan:
+    H: int
+    W: int
+    Cin: int
+    C: int
+    L: int
+    num_classes: int
+    h: float
+    gamma: float
+    subtract_mean: float | None
+    divide_by_stddev: float | None
+    param_kind: int
+    antisymmetric: bool
+    conv1: Conv2D = None
+    blocks: list = field(default_factory=list)
+    fc: Dense = None
+
+    def weight_vars(self):
+        """Variables in the executor's flat order (Keras get_weights order)."""
+        out = [self.conv1.kernel, self.conv1.bias]
+        for conv in self.blocks:
+            out += conv.weights
+        out += [self.fc.kernel, self.fc.bias]
+        return out
+
+    def block_theta_sizes(self):
+        """Per block: number of theta (kernel) floats, excluding the bias."""
+        return [sum(v.value.size for v in conv.weights) - self.C for conv in self.blocks]
+
+
+def _unsupported(layer, why):
+    return _lib.AsrUnsupported(f"cannot lower layer {layer.name} ({type(layer).__name__}): {why}")
+
+
+def _is_relu(t: SymbolicTensor):
+    return isinstance(t.layer, Activation) and t.layer.activation == "relu"
+
+
+def _affine_scalar(layer: Lambda, shape):
+    aff = layer.affine(shape[1:])
+    if aff is None:
+        raise _unsupported(layer, "not an elementwise affine function")
+    s, t = aff
+    if not (np.all(s == s.flat[0]) and np.all(t == t.flat[0])):
+        raise _unsupported(layer, "per-element/per-channel normalisation (the native stem takes scalars)")
+    return float(s.flat[0]), float(t.flat[0])
+
+
+def _conv3x3_same(layer: Conv2D, what):
+    if layer.kernel_size != (3, 3) or layer.strides != (1, 1) or layer.padding != "same" or not layer.use_bias:
+        raise _unsupported(layer, f"{what} must be a 3x3 'same' stride-1 conv with bias")
+    if layer.dilation_rate != (1, 1):
+        raise _unsupported(layer, "dilated conv")
+
+
+def analyze(model: Model) -> NetPlan:
+    if len(model.inputs) != 1 or len(model.outputs) != 1:
+        raise _lib.AsrUnsupported("the native executor runs single-input single-output models")
+    t = model.outputs[0]
+    # head: Dense(K, softmax) <- GAP
+    if not isinstance(t.layer, Dense):
+        raise _unsupported(t.layer, "model output must be the Dense 'fc' layer (include_top=True)")
+    fc = t.layer
+    if fc.activation != "softmax" or not fc.use_bias:
+        raise _unsupported(fc, "the head must be Dense(num_classes, activation='softmax') with bias")
+    t = t.inbound[0]
+    if not isinstance(t.layer, GlobalAveragePooling2D):
+        raise _unsupported(t.layer, "expected GlobalAveragePooling2D before fc")
+    t = t.inbound[0]
+    # identity blocks, last to first
+    blocks, hs = [], []
+    while isinstance(t.layer, Add):
+        if len(t.inbound) != 2:
+            raise _unsupported(t.layer, "add of more than two tensors")
+        branch, skip = t.inbound
+        h = 1.0
+        if isinstance(branch.layer, Lambda):
+            s, off = _affine_scalar(branch.layer, branch.shape)
+            if off != 0.0:
+                raise _unsupported(branch.layer, "block scaling must be h*x")
+            h = s
+            branch = branch.inbound[0]
+        if not _is_relu(branch):
+            raise _unsupported(branch.layer, "expected relu in the block branch (BN is not supported)")
+        conv_t = branch.inbound[0]
+        conv = conv_t.layer
+        if conv_t.inbound[0] is not skip:
+            raise _unsupported(conv, "block branch must start at the block input")
+        if isinstance(conv, AntisymmetricConvBase):
+            if conv.kernel_size != 3 or tuple(conv.strides) != (1, 1) or not conv.use_bias:
+                raise _unsupported(conv, "antisymmetric block conv must be 3x3, stride 1, with bias")
+        elif isinstance(conv, Conv2D):
+            _conv3x3_same(conv, "regular block conv")
+            if conv.activation not in (None, "linear"):
+                raise _unsupported(conv, "conv activation inside an identity block")
+        else:
+            raise _unsupported(conv, "unsupported block conv")
+        blocks.append(conv)
+        hs.append(h)
+        t = skip
+    blocks.reverse()
+    hs.reverse()
+    if not blocks:
+        raise _lib.AsrUnsupported("no identity blocks found")
+    # stem: relu <- conv1 <- Lambda* <- Input
+    if _is_relu(t):
+        t = t.inbound[0]
+        if not isinstance(t.layer, Conv2D) or t.layer.activation not in (None, "linear"):
+            raise _unsupported(t.layer, "expected conv1 before the stem relu (BN is not supported)")
+    elif not (isinstance(t.layer, Conv2D) and t.layer.activation == "relu"):
+        raise _unsupported(t.layer, "expected relu(conv1) before the first block")
+    conv1 = t.layer
+    _conv3x3_same(conv1, "conv1")
+    t = t.inbound[0]
+    scale, shift = 1.0, 0.0
+    while isinstance(t.layer, Lambda):
+        s, off = _affine_scalar(t.layer, t.shape)
+        scale, shift = scale * s, scale * off + shift  # walking backwards: acc o f
+        t = t.inbound[0]
+    if not isinstance(t.layer, InputLayer):
+        raise _unsupported(t.layer, "unsupported stem layer")
+    _, H, W, Cin = t.shape
+    C = conv1.filters
+    if scale == 0.0:
+        raise _lib.AsrUnsupported("input normalisation scales by zero")
+    # executor: (v - mean) * (1/std) == scale*v + shift
+    mean = None if (scale == 1.0 and shift == 0.0) else -shift / scale
+    std = None if mean is None else 1.0 / scale
+    first = blocks[0]
+    kinds = {(type(b), getattr(b, "param_kind", _lib.ASR_PARAM_REGULAR), getattr(b, "antisymmetric", False),
+              float(getattr(b, "gamma", 0.0))) for b in blocks}
+    if len(kinds) != 1 or len(set(hs)) != 1:
+        raise _lib.AsrUnsupported("all identity blocks must share conv type, gamma and h")
+    if isinstance(first, AntisymmetricConvBase):
+        kind, anti, gamma = first.param_kind, bool(first.antisymmetric), float(first.gamma)
+    else:
+        kind, anti, gamma = _lib.ASR_PARAM_REGULAR, False, 0.0
+    plan = NetPlan(H=int(H), W=int(W), Cin=int(Cin), C=int(C), L=len(blocks), num_classes=fc.units, h=float(hs[0]),
+                   gamma=gamma, subtract_mean=mean, divide_by_stddev=std, param_kind=kind, antisymmetric=anti,
+                   conv1=conv1, blocks=blocks, fc=fc)
+    for b in blocks:
+        if b.weights[-1].shape != (C,):
+            raise _unsupported(b, f"block channels must equal conv1 filters ({C})")
+    return plan
+
+
+class NativeModel:
+    """A Model lowered onto the native executor for a fixed per-process batch.
+
+    Holds the flat fp32 device parameters (Keras order), the Adam moments,
+    and one executor per input kind (uint8 or float32 images).  Host-side
+    Variables stay the source of truth between push_weights/pull_weights."""
+
+    def __init__(self, model: Model, batch_size: int, dtype="bfloat16", device=None):
+        from . import runtime
+        import torch
+        self.model = model
+        self.plan = analyze(model)
+        self.batch_size = int(batch_size)
+        self.dtype = dtype
+        self.device = device or runtime.require_gpu()
+        self._torch = torch
+        self._rt = runtime
+        self._executors = {}
+        self.vars = self.plan.weight_vars()
+        self.n_params = int(sum(v.value.size for v in self.vars))
+        self.params = torch.empty(self.n_params, dtype=torch.float32, device=self.device)
+        self.m = None
+        self.v = None
+        self.step = 0
+        self._host_stale = False
+        self.push_weights()
+
+    def matches(self, batch_size, dtype):
+        return self.batch_size == int(batch_size) and self.dtype == dtype
+
+    # -- weights ---------------------------------------------------------------
+    def push_weights(self):
+        flat = np.concatenate([v.value.ravel() for v in self.vars]).astype(np.float32)
+        self.params.copy_(self._torch.from_numpy(flat))
+        self._host_stale = False
+
+    def pull_weights(self):
+        if not self._host_stale:
+            return
+        flat = self.params.detach().cpu().numpy()
+        off = 0
+        for v in self.vars:
+            n = v.value.size
+            v.assign(flat[off:off + n].reshape(v.shape))
+            off += n
+        for layer in self.model.layers:
+            layer._weights_changed()
+        self._host_stale = False
+
+    def mark_updated(self):
+        self._host_stale = True
+
+    # -- execution ---------------------------------------------------------------
+    def executor(self, input_u8: bool):
+        ex = self._executors.get(input_u8)
+        if ex is None:
+            p = self.plan
+            ex = self._rt.NetExecutor(self.batch_size, p.H, p.W, p.Cin, p.C, p.L, p.num_classes, p.h, p.gamma,
+                                      subtract_mean=p.subtract_mean, divide_by_stddev=p.divide_by_stddev,
+                                      dtype=self.dtype, input_u8=input_u8, device=self.device,
+                                      param_kind=p.param_kind, antisymmetric=p.antisymmetric)
+            if ex.n_params != self.n_params:
+                raise _lib.AsrError(f"executor expects {ex.n_params} parameters, model has {self.n_params}")
+            self._executors[input_u8] = ex
+        return ex
+
+    def _images(self, x):
+        torch = self._torch
+        if isinstance(x, np.ndarray):
+            x = torch.from_numpy(np.ascontiguousarray(x))
+        if x.dtype not in (torch.uint8, torch.float32):
+            x = x.float()
+        return x.to(self.device, non_blocking=True).contiguous()
+
+    def predict(self, x):
+        """Softmax outputs [n, K] (numpy) for n images, in batches of
+        batch_size (the last batch is zero-padded)."""
+        torch = self._torch
+        x = self._images(x)
+        n = int(x.shape[0])
+        ex = self.executor(x.dtype == torch.uint8)
+        out = []
+        B = self.batch_size
+        for i in range(0, n, B):
+            chunk = x[i:i + B]
+            if chunk.shape[0] < B:
+                pad = torch.zeros((B,) + tuple(chunk.shape[1:]), dtype=chunk.dtype, device=chunk.device)
+                pad[:chunk.shape[0]] = chunk
+                chunk = pad
+            out.append(ex.forward(self.params, chunk)[: min(B, n - i)].clone())
+        return torch.cat(out).cpu().numpy()
+
+    def forward_backward(self, images, targets, want_probs=False):
+        """(loss, grads, probs): loss [1] and grads [n_params] are views of
+        executor buffers, overwritten by the next call."""
+        torch = self._torch
+        x = self._images(images)
+        if isinstance(targets, np.ndarray):
+            targets = torch.from_numpy(np.ascontiguousarray(targets, dtype=np.float32))
+        targets = targets.to(self.device, non_blocking=True).float().contiguous()
+        ex = self.executor(x.dtype == torch.uint8)
+        loss, grads = ex.forward_backward(self.params, x, targets, want_probs=want_probs)
+        return loss, grads, ex.probs
+
+    def apply_adam(self, grads, lr, beta1=0.9, beta2=0.999, epsilon=1e-7, grad_scale=1.0):
+        torch = self._torch
+        if self.m is None:
+            self.m = torch.zeros_like(self.params)
+            self.v = torch.zeros_like(self.params)
+        self.step += 1
+        self._rt.adam_update(self.params, grads, self.m, self.v, lr, beta1, beta2, epsilon, self.step, grad_scale)
+        self._host_stale = True

@@ -12,7 +12,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import ASR_BF16, ASR_F32, ASR_MODE_CONV, ASR_MODE_EULER, ASR_PARAM_3BY3, ASR_PARAM_GENERAL, NetConfig
+from ._lib import (ASR_BF16, ASR_F32, ASR_MODE_CONV, ASR_MODE_EULER, ASR_PARAM_3BY3, ASR_PARAM_GENERAL,
+                   ASR_PARAM_REGULAR, NetConfig)
 
 __all__ = [
     "require_gpu", "dtype_code", "torch_dtype", "ParamMap", "param_map", "theta_count", "theta_to_w",
@@ -66,6 +67,20 @@ class ParamMap:
     _dev: dict
 
     @property
+    def operator_antisymmetric(self) -> bool:
+        return bool(_lib.load().asr_param_is_antisymmetric(self.kind, int(self.antisymmetric)))
+
+    def w_src_bwd(self, device):
+        """Device map of W_bwd = -flip(W)^T (asr_param_map_transpose), for
+        parametrisations whose operator is not antisymmetric."""
+        key = ("bwd", str(device))
+        if key not in self._dev:
+            wb = np.empty_like(self.w_src)
+            _lib.call("asr_param_map_transpose", self.C, self.w_src.ctypes.data, wb.ctypes.data)
+            self._dev[key] = torch.from_numpy(wb).to(device)
+        return self._dev[key]
+
+    @property
     def n_theta(self) -> int:
         return self.theta_dst.size // 2
 
@@ -117,6 +132,34 @@ def theta_to_w(theta: torch.Tensor, C: int, pmap: ParamMap, gamma: float, dtype:
     return out.view(layers, per)
 
 
+def theta_to_w_transposed(theta: torch.Tensor, C: int, pmap: ParamMap, dtype: int) -> torch.Tensor:
+    """W_bwd = -flip(W)^T for the backward of a non-antisymmetric operator
+    (pass it to conv_backward with gamma 0)."""
+    dev = theta.device
+    wb = pmap.w_src_bwd(dev)
+    if dtype == ASR_BF16:
+        per = wpack_elems(C)
+        out = torch.empty(per, dtype=torch.bfloat16, device=dev)
+    else:
+        per = 9 * C * C
+        out = torch.empty(per, dtype=torch.float32, device=dev)
+    _lib.call("asr_theta_to_w", _p(theta), pmap.n_theta, 1, C, _p(wb), 0.0, _p(out), per, dtype, _stream())
+    return out.view(1, 3, 3, C, C) if dtype == ASR_F32 else out.view(1, per)
+
+
+def segment_sq_norms(x: torch.Tensor, offsets: torch.Tensor) -> torch.Tensor:
+    """out[i] = sum(x[offsets[i]:offsets[i+1]]**2) (asr_segment_sq_norms)."""
+    n = offsets.numel() - 1
+    out = torch.empty(n, dtype=torch.float32, device=x.device)
+    _lib.call("asr_segment_sq_norms", _p(x), _p(offsets), n, _p(out), _stream())
+    return out
+
+
+def batch_metrics(probs, targets, loss, accum):
+    N, K = probs.shape
+    _lib.call("asr_batch_metrics", _p(probs), _p(targets), _p(loss), N, K, _p(accum), _stream())
+
+
 def conv_forward(mode: int, x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, h: float = 1.0,
                  mask: torch.Tensor | None = None) -> torch.Tensor:
     N, H, W, C = x.shape
@@ -162,13 +205,13 @@ class NetExecutor:
     get_weights() order."""
 
     def __init__(self, N, H, W, Cin, C, L, num_classes, h, gamma=0.0, subtract_mean=None, divide_by_stddev=None,
-                 dtype="bfloat16", input_u8=True, device=None):
+                 dtype="bfloat16", input_u8=True, device=None, param_kind=ASR_PARAM_3BY3, antisymmetric=True):
         self.device = device or require_gpu()
         use_norm = subtract_mean is not None or divide_by_stddev is not None
         self.cfg = NetConfig(int(N), int(H), int(W), int(Cin), int(C), int(L), int(num_classes), float(h),
                              float(gamma), float(subtract_mean or 0.0),
                              float(divide_by_stddev if divide_by_stddev is not None else 1.0), int(use_norm),
-                             dtype_code(dtype), int(bool(input_u8)))
+                             dtype_code(dtype), int(bool(input_u8)), int(param_kind), int(bool(antisymmetric)))
         lib = _lib.load()
         self.n_params = int(lib.asr_net_param_count(ct.byref(self.cfg)))
         if self.n_params < 0:

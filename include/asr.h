@@ -53,6 +53,9 @@ typedef void* asr_stream_t; /* a hipStream_t (0 = null stream) */
                                centro_sym_{i}_{j} scalars then
                                input_kernels_for_output_kernel_{o}[3,3,C-o-1,1]
                                (…Conv2DAntisymmetric.py:109-145)              */
+#define ASR_PARAM_REGULAR 2 /* plain Conv2D kernel [3,3,C,C] (the regular
+                               identity block, tfkeras_resnets.py:76-83):
+                               theta IS W in HWIO order                       */
 
 /* conv modes */
 #define ASR_MODE_EULER 0 /* y = x + h*relu(conv(x)+b); mask = [conv(x)+b > 0]
@@ -84,6 +87,16 @@ long asr_theta_count(int C, int kind, int antisymmetric);
  *      weight-gradient projection (autodiff of …3By3.py:115-141).
  * w_src: 9*C*C int32, theta_dst: 2*asr_theta_count int32 (host memory). */
 int asr_param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta_dst);
+
+/* Host: 1 if the operator A of this parametrisation satisfies
+ * A + A^T = 2*gamma*I (3by3, general with antisymmetric=1), else 0; <0 on
+ * bad arguments.  For such kinds the backward pass applies A^T with the
+ * forward W (asr_conv_backward's identity).  Otherwise the caller
+ * materialises the transposed operator W_bwd = -flip(W)^T from the map
+ * asr_param_map_transpose returns and passes it (with gamma 0) as the
+ * backward's w. */
+int asr_param_is_antisymmetric(int kind, int antisymmetric);
+int asr_param_map_transpose(int C, const int32_t* w_src, int32_t* w_src_bwd);
 
 /* Elements of the packed bf16 W consumed by the MFMA kernels. */
 long asr_wpack_elems(int C);
@@ -139,7 +152,7 @@ int asr_conv_backward(int mode, const void* dy, const void* x, const uint8_t* ma
  * on the probabilities (training.py:295).
  * Parameters are ONE float32 buffer in Keras get_weights() order:
  *   conv1 kernel [3,3,Cin,C], conv1 bias [C],
- *   L x (theta_3by3 [asr_theta_count(C)], bias [C]),
+ *   L x (theta [asr_theta_count(C, param_kind, antisymmetric)], bias [C]),
  *   fc kernel [C,K], fc bias [K].
  * --------------------------------------------------------------------- */
 typedef struct asr_net_config {
@@ -149,6 +162,8 @@ typedef struct asr_net_config {
   int use_norm;
   int dtype;    /* activation dtype: ASR_F32 or ASR_BF16                */
   int input_u8; /* images are uint8 (1) or float32 (0), NHWC            */
+  int param_kind;    /* ASR_PARAM_3BY3 / _GENERAL / _REGULAR of the blocks */
+  int antisymmetric; /* Conv2DAntisymmetric(antisymmetric=...); 1 otherwise */
 } asr_net_config;
 
 long asr_net_param_count(const asr_net_config* cfg);
@@ -171,6 +186,23 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
 int asr_adam_update(float* params, const float* grads, float* m, float* v, long n, float lr,
                     float beta1, float beta2, float eps, long step, float grad_scale,
                     asr_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Training-loop metrics, accumulated on the device (no per-step host sync).
+ * ---------------------------------------------------------------------- */
+
+/* out[i] = sum_{j in [offsets[i], offsets[i+1])} x[j]^2 for i < n_segments
+ * (offsets: device int64 [n_segments+1]).  The per-layer gradient
+ * mean-norm ||g|| / size of training.py:356-409 is sqrt(out[i]) / size. */
+int asr_segment_sq_norms(const float* x, const long* offsets, int n_segments, float* out,
+                         asr_stream_t stream);
+
+/* Streaming mean loss + accuracy (tf.metrics.mean / tf.metrics.accuracy,
+ * training.py:316-354): accum[0] += *loss, accum[1] += #{argmax probs ==
+ * argmax targets}, accum[2] += N, accum[3] += 1.  loss may be NULL: the
+ * batch-mean Keras categorical cross-entropy of probs is used (evaluation). */
+int asr_batch_metrics(const float* probs, const float* targets, const float* loss, int N, int K,
+                      float* accum, asr_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -359,6 +359,15 @@ def euler_bwd(dy, x, z, W, h, gamma=0.0):
     return dx, dW, db
 
 
+def euler_bwd_generic(dy, x, z, W, h):
+    """Autodiff of euler_fwd for any W (no antisymmetry assumed): dx = dy +
+    Conv2DBackpropInput(dz, W)."""
+    dzr = dy * (z > 0)
+    dz = h * dzr if h != 1.0 else dzr
+    dx = dy + conv2d_backprop_input(dz, W, x.shape)
+    return dx, conv2d_backprop_filter(x, dz), dz.sum(axis=(0, 1, 2))
+
+
 def conv_bwd(dz, x, W, gamma=0.0):
     """Backward of the bare layer call (conv + bias): dx = A^T dz, dW, db."""
     dx = -conv2d_same(dz, W) + 2.0 * gamma * dz
@@ -393,13 +402,30 @@ class NetSpec:
     Cin: int = 3
     subtract_mean: float | None = 127.5
     divide_by_stddev: float | None = 127.5
+    kind: str = "3by3"           # "3by3" | "general" | "regular" (identity-block conv type)
+    antisymmetric: bool = True   # Conv2DAntisymmetric(antisymmetric=...)
+
+    def theta_shapes(self):
+        """Block conv weights in creation order: Conv2DAntisymmetric3By3
+        (…3By3.py:113-124, :219-245), Conv2DAntisymmetric (…Conv2DAntisymmetric.py:117-128,
+        :231-264) or the regular Conv2D kernel (tfkeras_resnets.py:76-83)."""
+        if self.kind == "3by3":
+            return theta_shapes_3by3(self.C)
+        if self.kind == "general":
+            return theta_shapes_general(self.C, 3, self.antisymmetric)[0]
+        if self.kind == "regular":
+            return [(3, 3, self.C, self.C)]
+        raise ValueError(self.kind)
+
+    def operator_antisymmetric(self):
+        return self.kind == "3by3" or (self.kind == "general" and self.antisymmetric)
 
     def param_shapes(self):
         """Keras `model.get_weights()` order: conv1 kernel/bias, then per
-        block [a,b,c,d, indep_0..indep_{C-2}, bias], then fc kernel/bias."""
+        block [theta..., bias], then fc kernel/bias."""
         s = [(3, 3, self.Cin, self.C), (self.C,)]
         for _ in range(self.L):
-            s += theta_shapes_3by3(self.C) + [(self.C,)]
+            s += self.theta_shapes() + [(self.C,)]
         s += [(self.C, self.num_classes), (self.num_classes,)]
         return s
 
@@ -413,8 +439,12 @@ def init_params(spec: NetSpec, rng, dtype=np.float64, bias_std=0.0):
     out = []
     out.append(truncated_normal(rng, (3, 3, spec.Cin, spec.C), math.sqrt(2.0 / (9 * spec.Cin)), dtype))
     out.append(np.zeros(spec.C, dtype) if bias_std == 0 else (rng.standard_normal(spec.C) * bias_std).astype(dtype))
+    std = math.sqrt(2.0 / (9 * spec.C))
     for _ in range(spec.L):
-        out += init_theta_3by3(spec.C, rng, dtype)
+        if spec.kind == "3by3":
+            out += init_theta_3by3(spec.C, rng, dtype)
+        else:
+            out += [truncated_normal(rng, sh, std, dtype) for sh in spec.theta_shapes()]
         out.append(np.zeros(spec.C, dtype) if bias_std == 0 else (rng.standard_normal(spec.C) * bias_std).astype(dtype))
     out.append(truncated_normal(rng, (spec.C, spec.num_classes), math.sqrt(2.0 / spec.C), dtype))
     out.append(np.zeros(spec.num_classes, dtype))
@@ -422,7 +452,7 @@ def init_params(spec: NetSpec, rng, dtype=np.float64, bias_std=0.0):
 
 
 def split_params(spec: NetSpec, params):
-    nt = 4 + spec.C - 1
+    nt = len(spec.theta_shapes())
     conv1_k, conv1_b = params[0], params[1]
     blocks = []
     i = 2
@@ -481,9 +511,14 @@ def net_forward(spec: NetSpec, params, images, dtype=np.float64):
     x = np.maximum(z1, 0)
     xs, zs, Ws = [x], [], []
     for theta, b in blocks:
-        W = assemble_3by3_literal(theta, spec.gamma) if spec.C <= 32 else None
-        if W is None:
-            src, sign = _cached_map(spec.C)
+        if spec.kind == "3by3" and spec.C <= 32:
+            W = assemble_3by3_literal(theta, spec.gamma)
+        elif spec.kind == "general" and spec.C <= 32:
+            W = assemble_general_literal(theta, spec.C, 3, spec.gamma, spec.antisymmetric)
+        elif spec.kind == "regular":
+            W = np.asarray(theta[0])
+        else:
+            src, sign = _cached_map(spec.C, spec.kind, spec.antisymmetric)
             W = assemble_from_map(flatten(theta), spec.C, src, sign, spec.gamma)
         x, z = euler_fwd(x, W, b, spec.h)
         xs.append(x)
@@ -499,10 +534,14 @@ def net_forward(spec: NetSpec, params, images, dtype=np.float64):
 _MAPS = {}
 
 
-def _cached_map(C):
-    if C not in _MAPS:
-        _MAPS[C] = param_map(C, "3by3")
-    return _MAPS[C]
+def _cached_map(C, kind="3by3", antisymmetric=True):
+    key = (C, kind, antisymmetric)
+    if key not in _MAPS:
+        if kind == "regular":
+            _MAPS[key] = (np.arange(9 * C * C), np.ones(9 * C * C, dtype=np.int64))
+        else:
+            _MAPS[key] = param_map(C, kind, 3, antisymmetric)
+    return _MAPS[key]
 
 
 def net_loss(probs, onehot):
@@ -520,14 +559,18 @@ def net_backward(spec: NetSpec, params, cache, onehot):
     dgap = dlogits @ fc_k.T
     xL = cache["xs"][-1]
     dx = np.broadcast_to(dgap[:, None, None, :] / (spec.H * spec.W), xL.shape).copy()
-    src, sign = _cached_map(spec.C)
-    ntheta = theta_count_3by3(spec.C)
+    src, sign = _cached_map(spec.C, spec.kind, spec.antisymmetric)
+    shapes = spec.theta_shapes()
+    ntheta = int(sum(np.prod(x) for x in shapes))
     block_grads = []
     for li in range(spec.L - 1, -1, -1):
         x_in = cache["xs"][li]
-        dx, dW, db = euler_bwd(dx, x_in, cache["zs"][li], cache["Ws"][li], spec.h, spec.gamma)
+        if spec.operator_antisymmetric():
+            dx, dW, db = euler_bwd(dx, x_in, cache["zs"][li], cache["Ws"][li], spec.h, spec.gamma)
+        else:
+            dx, dW, db = euler_bwd_generic(dx, x_in, cache["zs"][li], cache["Ws"][li], spec.h)
         dth = project_dW(dW, src, sign, ntheta)
-        block_grads.append((unflatten(dth, theta_shapes_3by3(spec.C)), db))
+        block_grads.append((unflatten(dth, shapes), db))
     block_grads.reverse()
     dz1 = dx * (cache["z1"] > 0)
     d_c1k = conv2d_backprop_filter(cache["x0"], dz1)

@@ -39,7 +39,8 @@ def test_python_binding_covers_header():
 
 
 def test_abi_version_and_errors(lib):
-    assert lib.asr_abi_version() == 1
+    from differential_equations_resnet_amd import _lib
+    assert lib.asr_abi_version() == _lib.ABI_VERSION
     assert lib.asr_theta_count(0, 0, 1) < 0
     # a bad-argument call reports through asr_last_error without a GPU
     rc = lib.asr_param_map(0, 0, 1, None, None)
@@ -100,11 +101,11 @@ def test_sizes(lib):
     assert lib.asr_wpack_elems(20) < 0
     assert lib.asr_mask_bytes(2, 32, 32, 64) == 2 * 32 * 32 * 64 // 8
     assert lib.asr_conv_backward_workspace_bytes(2, 32, 32, 64, 1) > 0
-    cfg = _lib.NetConfig(512, 32, 32, 3, 64, 30, 10, 8 / 30, 0.0, 127.5, 127.5, 1, 1, 1)
+    cfg = _lib.NetConfig(512, 32, 32, 3, 64, 30, 10, 8 / 30, 0.0, 127.5, 127.5, 1, 1, 1, 0, 1)
     assert lib.asr_net_param_count(ct.byref(cfg)) == O.NetSpec(C=64, L=30).n_params()
     ws = lib.asr_net_workspace_bytes(ct.byref(cfg))
     assert 2e9 < ws < 8e9  # activations of 31 layers + masks + slabs
-    bad = _lib.NetConfig(512, 32, 24, 3, 64, 30, 10, 0.1, 0.0, 0.0, 1.0, 0, 1, 1)  # bf16 needs W == 32
+    bad = _lib.NetConfig(512, 32, 24, 3, 64, 30, 10, 0.1, 0.0, 0.0, 1.0, 0, 1, 1, 0, 1)  # bf16 needs W == 32
     assert lib.asr_net_workspace_bytes(ct.byref(bad)) == 0
 
 
@@ -113,3 +114,39 @@ def test_netparams_layout_matches_oracle():
     assert netparams.net_param_shapes(16, 3) == O.NetSpec(C=16, L=3).param_shapes()
     flat = netparams.init_net_params(16, 3, seed=1)
     assert flat.dtype == np.float32 and flat.size == O.NetSpec(C=16, L=3).n_params()
+
+
+def test_net_param_count_per_kind(lib):
+    from differential_equations_resnet_amd import _lib
+    for kind, anti in [(0, 1), (1, 1), (1, 0), (2, 0)]:
+        cfg = _lib.NetConfig(4, 8, 8, 3, 6, 2, 10, 0.5, 0.0, 0.0, 1.0, 0, 0, 1, kind, anti)
+        nt = lib.asr_theta_count(6, kind, anti)
+        assert lib.asr_net_param_count(ct.byref(cfg)) == 27 * 6 + 6 + 2 * (nt + 6) + 6 * 10 + 10
+    bad = _lib.NetConfig(4, 8, 8, 3, 6, 2, 10, 0.5, 0.0, 0.0, 1.0, 0, 0, 1, 0, 0)
+    assert lib.asr_net_param_count(ct.byref(bad)) == -1
+
+
+@pytest.mark.parametrize("kind,anti", [(0, 1), (1, 1), (1, 0), (2, 0)])
+def test_transposed_operator_map(lib, kind, anti):
+    """asr_param_map_transpose gives W_bwd = -flip(W)^T; for antisymmetric
+    kinds that equals W with the centre negated (so A^T = -A + 2 gamma I)."""
+    C = 5
+    n = lib.asr_theta_count(C, kind, anti)
+    w_src = np.empty(9 * C * C, np.int32)
+    lib.asr_param_map(C, kind, anti, w_src.ctypes.data, None)
+    th = np.random.default_rng(kind).standard_normal(n)
+    W = np.where(w_src >= 0, th[np.maximum(w_src, 0) >> 1] * np.where(w_src & 1, -1.0, 1.0), 0.3).reshape(3, 3, C, C)
+    want = -W[::-1, ::-1].transpose(0, 1, 3, 2)
+    assert lib.asr_param_is_antisymmetric(kind, anti) == (1 if (kind == 0 or (kind == 1 and anti)) else 0)
+    wb = np.empty_like(w_src)
+    rc = lib.asr_param_map_transpose(C, w_src.ctypes.data, wb.ctypes.data)
+    if lib.asr_param_is_antisymmetric(kind, anti):
+        assert rc == -1  # constant centre: the forward W (with the identity) is used instead
+        Wg = W.copy()
+        for o in range(C):
+            Wg[1, 1, o, o] = -0.3
+        assert np.array_equal(want, Wg)
+    else:
+        assert rc == 0
+        Wb = (th[wb >> 1] * np.where(wb & 1, -1.0, 1.0)).reshape(3, 3, C, C)
+        assert np.array_equal(Wb, want)

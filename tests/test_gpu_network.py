@@ -16,8 +16,8 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-def _setup(C=16, L=3, N=4, H=32, W=32, h=0.5, gamma=0.0, seed=0):
-    spec = O.NetSpec(C=C, L=L, h=h, gamma=gamma, H=H, W=W)
+def _setup(C=16, L=3, N=4, H=32, W=32, h=0.5, gamma=0.0, seed=0, kind="3by3", antisymmetric=True):
+    spec = O.NetSpec(C=C, L=L, h=h, gamma=gamma, H=H, W=W, kind=kind, antisymmetric=antisymmetric)
     rng = np.random.default_rng(seed)
     params = O.init_params(spec, rng, np.float64, bias_std=0.05)
     params = [p.astype(np.float32).astype(np.float64) for p in params]
@@ -27,15 +27,21 @@ def _setup(C=16, L=3, N=4, H=32, W=32, h=0.5, gamma=0.0, seed=0):
     return spec, params, imgs, onehot
 
 
+KINDS = {"3by3": 0, "general": 1, "regular": 2}
+
+
 def _executor(spec, N, dtype):
     from differential_equations_resnet_amd.runtime import NetExecutor
     return NetExecutor(N, spec.H, spec.W, 3, spec.C, spec.L, spec.num_classes, spec.h, spec.gamma,
-                       subtract_mean=127.5, divide_by_stddev=127.5, dtype=dtype, input_u8=True)
+                       subtract_mean=127.5, divide_by_stddev=127.5, dtype=dtype, input_u8=True,
+                       param_kind=KINDS[spec.kind], antisymmetric=spec.antisymmetric)
 
 
-@pytest.mark.parametrize("gamma", [0.0, -0.05])
-def test_network_fp32_parity(gamma):
-    spec, params, imgs, onehot = _setup(gamma=gamma)
+@pytest.mark.parametrize("gamma,kind,anti,C,W", [(0.0, "3by3", True, 16, 32), (-0.05, "3by3", True, 16, 32),
+                                                   (-0.05, "general", True, 6, 9), (0.0, "general", False, 5, 7),
+                                                   (0.0, "regular", False, 16, 32)])
+def test_network_fp32_parity(gamma, kind, anti, C, W):
+    spec, params, imgs, onehot = _setup(gamma=gamma, kind=kind, antisymmetric=anti, C=C, W=W, H=W)
     N = imgs.shape[0]
     ex = _executor(spec, N, "float32")
     flat = torch.from_numpy(O.flatten(params).astype(np.float32)).cuda()
@@ -53,8 +59,9 @@ def test_network_fp32_parity(gamma):
         assert_close(a, b, rtol=0, atol=1e-4 * max(np.abs(b).max(), 1e-12), what=f"grad[{i}] {b.shape}")
 
 
-def test_network_bf16_close():
-    spec, params, imgs, onehot = _setup(C=16, L=4, N=8, h=0.25)
+@pytest.mark.parametrize("kind,anti", [("3by3", True), ("general", False), ("regular", False)])
+def test_network_bf16_close(kind, anti):
+    spec, params, imgs, onehot = _setup(C=16, L=4, N=8, h=0.25, kind=kind, antisymmetric=anti)
     N = imgs.shape[0]
     ex = _executor(spec, N, "bfloat16")
     flat = torch.from_numpy(O.flatten(params).astype(np.float32)).cuda()

@@ -126,9 +126,10 @@ def test_euler_block_gradients_finite_difference():
     assert np.abs(dx - (R + O.conv2d_backprop_input(dz, W, x.shape))).max() < 1e-12
 
 
-def test_network_gradients_finite_difference():
+@pytest.mark.parametrize("kind,anti", [("3by3", True), ("general", True), ("general", False), ("regular", False)])
+def test_network_gradients_finite_difference(kind, anti):
     rng = np.random.default_rng(2)
-    spec = O.NetSpec(C=4, L=2, h=0.5, H=5, W=4)
+    spec = O.NetSpec(C=4, L=2, h=0.5, H=5, W=4, gamma=-0.1 if anti else 0.0, kind=kind, antisymmetric=anti)
     params = O.init_params(spec, rng, bias_std=0.1)
     imgs = rng.integers(0, 256, (3, 5, 4, 3)).astype(np.uint8)
     oh = np.eye(10)[rng.integers(0, 10, 3)]
