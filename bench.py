@@ -98,22 +98,26 @@ def block_roofline(rt, lib, C, N, dtype_name, reps, h):
         fwd()
         bwd()
     torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3 * reps)]
-    for r in range(reps):
-        ev[3 * r].record()
-        fwd()
-        ev[3 * r + 1].record()
-        bwd()
-        ev[3 * r + 2].record()
-    torch.cuda.synchronize()
-    tf = sum(ev[3 * r].elapsed_time(ev[3 * r + 1]) for r in range(reps)) / reps * 1e-3
-    tb = sum(ev[3 * r + 1].elapsed_time(ev[3 * r + 2]) for r in range(reps)) / reps * 1e-3
+    def timed(fn):
+        # one event pair around `reps` back-to-back launches: the per-launch
+        # average then matches rocprofv3's kernel durations (events between
+        # every launch would add their own serialisation gaps)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e-3
+
+    tf = timed(fwd)
+    tb = timed(bwd)
+    t_blk = timed(lambda: (fwd(), bwd()))
     esz = 2 if dt == rt.ASR_BF16 else 4
     P = N * H * W * C
     bytes_alg = 5 * P * esz  # fwd read x + write y; bwd read dy, read x, write dx
     flops = 3 * 2 * 9 * C * C * N * H * W
-    t = tf + tb
-    return dict(t_fwd=tf, t_bwd=tb, t=t, bytes=bytes_alg, flops=flops)
+    return dict(t_fwd=tf, t_bwd=tb, t=t_blk, bytes=bytes_alg, flops=flops)
 
 
 def cpu_baseline(C, L, h, batch, steps):
