@@ -203,6 +203,32 @@ __device__ __forceinline__ void lgkm_wait() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// LDS accesses the compiler must not order behind in-flight LDS-DMA: hipcc
+// waits vmcnt(0) before any plain LDS access while a global_load_lds is
+// outstanding (it cannot tell the DMA's destination buffer apart), which
+// would serialise the next band's prefetch with this band's work.  The
+// caller waits lgkmcnt itself (lgkm_wait) before using a read result.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u32x4 lds_rd128(unsigned addr) {
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ u32x2 lds_rd64(unsigned addr) {
+  u32x2 v;
+  asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ unsigned lds_rd_u8(unsigned addr) {
+  unsigned v;
+  asm volatile("ds_read_u8 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+__device__ __forceinline__ void lds_wr128(unsigned addr, u32x4 v) {
+  asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+
 template <int C, int W, int ks>
 __device__ __forceinline__ void conv_issue(const unsigned (&ra)[Frag<C, W>::NB], bf16x8 (&B)[W / 16]) {
   if constexpr (W / 16 >= 1) B[0] = ds_read128<Frag<C, W>::template imm<ks, 0>()>(ra[Frag<C, W>::template slot<ks>()]);
@@ -413,38 +439,42 @@ __device__ __forceinline__ void bwd_issue(const bf16* dy, const bf16* x, const u
   if constexpr (EULER) dma_mask_rows<C, W>(mask, lds + L::MSK + buf * L::MTB, n, y0 - 1, nr, H, wave, nwaves, lane);
 }
 
-// dz = h*dy*mask (or dy) for all staged rows, into the DZ tile.
+// dz = h*dy*mask (or dy) for all staged rows, into the DZ tile.  LDS
+// accesses through asm (see lds_rd128): the dgrad waves run this with the
+// next band's DMA in flight.
 template <int C, int W, int BR, bool EULER>
 __device__ __forceinline__ void bwd_convert(unsigned char* lds, int buf, int nr, float h, int tid, int nthreads) {
   using L = BwdLds<C, W, BR>;
   constexpr int TW = W + 2, NQ = C / 8, KB = 4;
-  const unsigned char* dyt = lds + L::DY + buf * L::TILE;
-  const unsigned char* mt = lds + L::MSK + buf * L::MTB;
-  unsigned char* dzt = lds + L::DZ;
+  const unsigned dyt = lds_u32(lds + L::DY + buf * L::TILE);
+  const unsigned mt = lds_u32(lds + L::MSK + buf * L::MTB);
+  const unsigned dzt = lds_u32(lds + L::DZ);
   const int nch = nr * TW * NQ;
   for (int c0 = tid; c0 < nch; c0 += KB * nthreads) {
-    uint4 v[KB];
+    u32x4 v[KB];
     unsigned mb[KB];
     int off[KB];
+    bool inner[KB];
 #pragma unroll
     for (int k = 0; k < KB; ++k) {  // all LDS reads first (latencies overlap)
       const int c = c0 + k * nthreads;
       const int cc = c < nch ? c : 0;
       const int q = cc % NQ, pc = cc / NQ, col = pc % TW, r = pc / TW;
       off[k] = toff<C>(r, col, q, TW);
-      v[k] = *(const uint4*)(dyt + off[k]);
-      mb[k] = 0xffu;
-      if constexpr (EULER) mb[k] = (col >= 1 && col <= W) ? mt[(r * W + col - 1) * NQ + q] : 0u;
+      v[k] = lds_rd128(dyt + off[k]);
+      inner[k] = col >= 1 && col <= W;
+      if constexpr (EULER) mb[k] = lds_rd_u8(mt + (inner[k] ? (r * W + col - 1) * NQ + q : 0));
     }
+    lgkm_wait<0>();
 #pragma unroll
     for (int k = 0; k < KB; ++k) {
       if (c0 + k * nthreads < nch) {
+        const unsigned m = EULER ? (inner[k] ? mb[k] : 0u) : 0xffu;
         const bf16x8 d8 = *(const bf16x8*)&v[k];
         bf16x8 z8;
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          z8[j] = (bf16)(((mb[k] >> j) & 1u) ? (EULER ? h * (float)d8[j] : (float)d8[j]) : 0.f);
-        *(bf16x8*)(dzt + off[k]) = z8;
+        for (int j = 0; j < 8; ++j) z8[j] = (bf16)(((m >> j) & 1u) ? (EULER ? h * (float)d8[j] : (float)d8[j]) : 0.f);
+        lds_wr128(dzt + off[k], *(const u32x4*)&z8);
       }
     }
   }
@@ -519,17 +549,30 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
         }
         const int gy = y0 + r;
         if (dx) nst += PT * OTW;
+        u32x2 dzv[PT][OTW], dyv[PT][OTW];
+        unsigned mbv[PT][OTW];
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt)
+#pragma unroll
+          for (int t = 0; t < OTW; ++t) {
+            const int px = 16 * pt + lx, o0 = 16 * (oh * OTW + t) + 4 * g;
+            const int co = toff<C>(r + 1, px + 1, o0 >> 3, TW) + (o0 & 4) * 2;
+            dzv[pt][t] = lds_rd64(lds_u32(dzt + co));
+            dyv[pt][t] = lds_rd64(lds_u32(dyt + co));
+            if constexpr (EULER)
+              mbv[pt][t] = lds_rd_u8(lds_u32(lds + L::MSK + buf * L::MTB) + ((r + 1) * W + px) * NQ + (o0 >> 3));
+          }
+        lgkm_wait<0>();
 #pragma unroll
         for (int pt = 0; pt < PT; ++pt) {
           const int px = 16 * pt + lx;
 #pragma unroll
           for (int t = 0; t < OTW; ++t) {
             const int o0 = 16 * (oh * OTW + t) + 4 * g;
-            const int co = toff<C>(r + 1, px + 1, o0 >> 3, TW) + (o0 & 4) * 2;
-            const bf16x4 dzr = *(const bf16x4*)(dzt + co);
-            const bf16x4 dyr = *(const bf16x4*)(dyt + co);
+            const bf16x4 dzr = *(const bf16x4*)&dzv[pt][t];
+            const bf16x4 dyr = *(const bf16x4*)&dyv[pt][t];
             unsigned mb = 0xffu;
-            if constexpr (EULER) mb = (lds + L::MSK + buf * L::MTB)[((r + 1) * W + px) * NQ + (o0 >> 3)] >> (o0 & 4);
+            if constexpr (EULER) mb = mbv[pt][t] >> (o0 & 4);
 #pragma unroll
             for (int e = 0; e < 4; ++e)
               dbacc[t][e] += ((mb >> e) & 1u) ? (EULER ? h * (float)dyr[e] : (float)dyr[e]) : 0.f;

@@ -266,9 +266,14 @@ __global__ void k_project(const float* __restrict__ red_groups, int G, long E, c
   const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
   const long ES = E + Cb;
   auto red_at = [&](long e) {  // sum of the G group partials (fixed order: deterministic)
-    float a = 0.f;
-    for (int g = 0; g < G; ++g) a += red_groups[(long)g * ES + e];
-    return a;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    int g = 0;
+    for (; g + 3 < G; g += 4) {  // four independent loads in flight
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] += red_groups[(long)(g + q) * ES + e];
+    }
+    for (; g < G; ++g) a[0] += red_groups[(long)g * ES + e];
+    return (a[0] + a[1]) + (a[2] + a[3]);
   };
   if (dtheta && t < n_theta) {
     float acc = 0.f;

@@ -189,3 +189,21 @@ def test_adam_matches_tf1(rt):
         rt.adam_update(P, torch.from_numpy(g).cuda(), M, V, 1e-3, 0.9, 0.999, 1e-7, t, 1.0)
         O.adam_tf1(ps, [g.astype(np.float64)], ms, vs, t, 1e-3, 0.9, 0.999, 1e-7)
     assert_close(P.cpu().numpy(), ps[0], rtol=1e-6, atol=1e-7, what="adam")
+
+
+@pytest.mark.parametrize("C", [16, 32, 64])
+def test_backward_projection_in_epilogue(rt, C):
+    """dtheta projected inside the backward kernel (slabs of n_theta + C)
+    equals the projection of the separately reduced dW (slabs of 9C^2 + C)."""
+    N, H, W_ = 3, 32, 32
+    rng = np.random.default_rng(C)
+    x_np = rng.standard_normal((N, H, W_, C)).astype(np.float32)
+    dy = torch.from_numpy(rng.standard_normal((N, H, W_, C)).astype(np.float32)).cuda().to(torch.bfloat16)
+    th = _theta(C, 2)
+    b = (rng.standard_normal(C) * 0.1).astype(np.float32)
+    x, w, y, mask, pm = _run_forward(rt, rt.ASR_MODE_EULER, x_np, th, b, C, -0.05, 0.5, rt.ASR_BF16)
+    _, th_a, db_a, _ = rt.conv_backward(rt.ASR_MODE_EULER, dy, x, mask, w, pm, 0.5, -0.05)
+    _, th_b, db_b, dw = rt.conv_backward(rt.ASR_MODE_EULER, dy, x, mask, w, pm, 0.5, -0.05, want_dw=True)
+    a, bb = th_a.cpu().numpy(), th_b.cpu().numpy()
+    assert np.abs(a - bb).max() <= 1e-5 * np.abs(bb).max()
+    np.testing.assert_allclose(db_a.cpu().numpy(), db_b.cpu().numpy(), rtol=0, atol=1e-6)
