@@ -439,11 +439,12 @@ __device__ __forceinline__ void bwd_issue(const bf16* dy, const bf16* x, const u
   if constexpr (EULER) dma_mask_rows<C, W>(mask, lds + L::MSK + buf * L::MTB, n, y0 - 1, nr, H, wave, nwaves, lane);
 }
 
-// dz = h*dy*mask (or dy) for all staged rows, into the DZ tile.  LDS
-// accesses through asm (see lds_rd128): the dgrad waves run this with the
-// next band's DMA in flight.
+// dzm = dy * mask for all staged rows, into the DZ tile: a bit operation on
+// the bf16 values (the factor h of dz = h*dy*mask is applied in fp32 in the
+// epilogues: dx, dW and db are linear in dz).  LDS accesses through asm (see
+// lds_rd128): the dgrad waves run this with the next band's DMA in flight.
 template <int C, int W, int BR, bool EULER>
-__device__ __forceinline__ void bwd_convert(unsigned char* lds, int buf, int nr, float h, int tid, int nthreads) {
+__device__ __forceinline__ void bwd_convert(unsigned char* lds, int buf, int nr, int tid, int nthreads) {
   using L = BwdLds<C, W, BR>;
   constexpr int TW = W + 2, NQ = C / 8, KB = 4;
   const unsigned dyt = lds_u32(lds + L::DY + buf * L::TILE);
@@ -461,20 +462,29 @@ __device__ __forceinline__ void bwd_convert(unsigned char* lds, int buf, int nr,
       const int cc = c < nch ? c : 0;
       const int q = cc % NQ, pc = cc / NQ, col = pc % TW, r = pc / TW;
       off[k] = toff<C>(r, col, q, TW);
-      v[k] = lds_rd128(dyt + off[k]);
       inner[k] = col >= 1 && col <= W;
-      if constexpr (EULER) mb[k] = lds_rd_u8(mt + (inner[k] ? (r * W + col - 1) * NQ + q : 0));
+      if constexpr (EULER) {
+        v[k] = lds_rd128(dyt + off[k]);
+        mb[k] = lds_rd_u8(mt + (inner[k] ? (r * W + col - 1) * NQ + q : 0));
+      } else {
+        v[k] = lds_rd128(dyt + off[k]);
+      }
     }
     lgkm_wait<0>();
 #pragma unroll
     for (int k = 0; k < KB; ++k) {
       if (c0 + k * nthreads < nch) {
-        const unsigned m = EULER ? (inner[k] ? mb[k] : 0u) : 0xffu;
-        const bf16x8 d8 = *(const bf16x8*)&v[k];
-        bf16x8 z8;
+        u32x4 z = v[k];
+        if constexpr (EULER) {
+          const unsigned m = inner[k] ? mb[k] : 0u;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) z8[j] = (bf16)(((m >> j) & 1u) ? (EULER ? h * (float)d8[j] : (float)d8[j]) : 0.f);
-        lds_wr128(dzt + off[k], *(const u32x4*)&z8);
+          for (int d = 0; d < 4; ++d) {  // element pair (2d, 2d+1) of this 16-byte chunk
+            const unsigned lo = (unsigned)(((int)(m << (31 - 2 * d))) >> 31);
+            const unsigned hi = (unsigned)(((int)(m << (30 - 2 * d))) >> 31);
+            z[d] &= (lo & 0xffffu) | (hi & 0xffff0000u);
+          }
+        }
+        lds_wr128(dzt + off[k], z);
       }
     }
   }
@@ -505,6 +515,8 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
   if (i0 < i1) bwd_issue<C, W, BR, EULER>(dy, x, mask, lds, 0, i0, nb, H, wave, lane, 8);
 
   float* slab = slabs + (long)blockIdx.x * (9 * C * C + C);
+  const float hs = EULER ? h : 1.f;  // dz = hs * dzm (dzm = dy*mask in LDS)
+  const float hs2g = hs * two_gamma;
   if (wave < 4) {
     // ---------------- dgrad waves ----------------
     constexpr int RS = 4 / G::OSPLIT;
@@ -526,7 +538,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
       barrier_vm(nst);  // item's DMA landed; previous item fully consumed
       nst = 0;
       if (it + 1 < i1) bwd_issue<C, W, BR, EULER>(dy, x, mask, lds, buf ^ 1, it + 1, nb, H, wave, lane, 4);
-      if (ASR_ABLATE != 4) bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, h, tid, 512);
+      if (ASR_ABLATE != 4) bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, tid, 512);
       barrier_lds();  // dz ready
       const unsigned char* dzt = lds + L::DZ;
       const unsigned char* dyt = lds + L::DY + buf * L::TILE;
@@ -550,7 +562,6 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
         const int gy = y0 + r;
         if (dx) nst += PT * OTW;
         u32x2 dzv[PT][OTW], dyv[PT][OTW];
-        unsigned mbv[PT][OTW];
 #pragma unroll
         for (int pt = 0; pt < PT; ++pt)
 #pragma unroll
@@ -558,9 +569,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
             const int px = 16 * pt + lx, o0 = 16 * (oh * OTW + t) + 4 * g;
             const int co = toff<C>(r + 1, px + 1, o0 >> 3, TW) + (o0 & 4) * 2;
             dzv[pt][t] = lds_rd64(lds_u32(dzt + co));
-            dyv[pt][t] = lds_rd64(lds_u32(dyt + co));
-            if constexpr (EULER)
-              mbv[pt][t] = lds_rd_u8(lds_u32(lds + L::MSK + buf * L::MTB) + ((r + 1) * W + px) * NQ + (o0 >> 3));
+            if constexpr (EULER) dyv[pt][t] = lds_rd64(lds_u32(dyt + co));
           }
         lgkm_wait<0>();
 #pragma unroll
@@ -570,16 +579,21 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
           for (int t = 0; t < OTW; ++t) {
             const int o0 = 16 * (oh * OTW + t) + 4 * g;
             const bf16x4 dzr = *(const bf16x4*)&dzv[pt][t];
-            const bf16x4 dyr = *(const bf16x4*)&dyv[pt][t];
-            unsigned mb = 0xffu;
-            if constexpr (EULER) mb = mbv[pt][t] >> (o0 & 4);
+            float dzf[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              dbacc[t][e] += ((mb >> e) & 1u) ? (EULER ? h * (float)dyr[e] : (float)dyr[e]) : 0.f;
+            for (int e = 0; e < 4; ++e) {
+              dzf[e] = (float)dzr[e];
+              dbacc[t][e] += dzf[e];
+            }
             bf16x4 o4;
+            if constexpr (EULER) {
+              const bf16x4 dyr = *(const bf16x4*)&dyv[pt][t];
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              o4[e] = (bf16)((EULER ? (float)dyr[e] : 0.f) - acc[t][pt][e] + two_gamma * (float)dzr[e]);
+              for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(hs2g, dzf[e], fmaf(-hs, acc[t][pt][e], (float)dyr[e]));
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(two_gamma, dzf[e], -acc[t][pt][e]);
+            }
             if (dx) *(bf16x4*)(dx + (((long)n * H + gy) * W + px) * C + o0) = o4;
           }
         }
@@ -603,7 +617,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
 #pragma unroll
       for (int t = 0; t < OTW; ++t)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) dbl[rg * C + 16 * (oh * OTW + t) + 4 * g + e] = dbacc[t][e];
+        for (int e = 0; e < 4; ++e) dbl[rg * C + 16 * (oh * OTW + t) + 4 * g + e] = hs * dbacc[t][e];
     }
     if constexpr (G::KSPLIT > 1) {
       __syncthreads();
@@ -624,7 +638,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
       const int y0 = (int)(it % nb) * BR;
       const int rows = min(BR, H - y0);
       barrier_vm(0);
-      if (ASR_ABLATE != 4) bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, h, tid, 512);
+      if (ASR_ABLATE != 4) bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, tid, 512);
       barrier_lds();
       const unsigned char* dzt = lds + L::DZ;
       const unsigned char* xt = lds + L::X + buf * L::TILE;
@@ -690,7 +704,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int m = 16 * (tg * MTW + mi) + 4 * g + e;
-            slab[(long)m * C + 16 * ot + lx] = acc[mi][ot][e];
+            slab[(long)m * C + 16 * ot + lx] = hs * acc[mi][ot][e];
           }
     }
   }
