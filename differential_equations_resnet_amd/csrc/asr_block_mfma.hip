@@ -125,13 +125,15 @@ __device__ __forceinline__ void dma_mask_rows(const uint8_t* __restrict__ mask, 
 // order).  Used so that the barrier guarding an LDS-DMA'd buffer does not
 // also wait for the global stores issued after that DMA.
 __device__ __forceinline__ void barrier_vm(int n) {
+#define ASR_BVM(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ") lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
   switch (n) {
-    case 4: asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    ASR_BVM(1) ASR_BVM(2) ASR_BVM(3) ASR_BVM(4) ASR_BVM(5) ASR_BVM(6) ASR_BVM(7) ASR_BVM(8)
+    ASR_BVM(9) ASR_BVM(10) ASR_BVM(11) ASR_BVM(12) ASR_BVM(13) ASR_BVM(14) ASR_BVM(15) ASR_BVM(16)
+    ASR_BVM(17) ASR_BVM(18) ASR_BVM(19) ASR_BVM(20) ASR_BVM(21) ASR_BVM(22) ASR_BVM(23) ASR_BVM(24)
     default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
   }
+#undef ASR_BVM
 }
 // barrier for LDS data only (in-flight DMA and stores keep flying)
 __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -258,16 +260,13 @@ __device__ __forceinline__ void conv_step(const unsigned (&ra)[Frag<C, W>::NB],
   }
 }
 
-// conv GEMM of one output row (tile row r is the row above it)
+// conv GEMM of one output row (tile row r is the row above it), accumulated
+// onto the caller's initial acc (the bias in the forward)
 template <int C, int W>
 __device__ __forceinline__ void conv_row(const unsigned char* tile, int r, const bf16x8 (&A)[Geo<C>::OTW][Geo<C>::KS],
                                          const Frag<C, W>& f, f32x4 (&acc)[Geo<C>::OTW][W / 16]) {
   using G = Geo<C>;
   constexpr int TW = W + 2, PT = W / 16;
-#pragma unroll
-  for (int t = 0; t < G::OTW; ++t)
-#pragma unroll
-    for (int pt = 0; pt < PT; ++pt) acc[t][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
   const unsigned rb = lds_u32(tile + r * TW * G::NQ * 16);
   unsigned ra[Frag<C, W>::NB];
 #pragma unroll
@@ -277,6 +276,95 @@ __device__ __forceinline__ void conv_row(const unsigned char* tile, int r, const
   conv_issue<C, W, 0>(ra, B[0]);
   if constexpr (G::KS > 1) conv_issue<C, W, 1>(ra, B[1]);
   conv_step<C, W, 0>(ra, A, acc, B);
+}
+
+// ---------------------------------------------------------------------------
+// Band conv (C >= 32): one wave = one 16-channel output tile over RB output
+// rows.  The B fragment of input row ir (tap column kx, channel block cb)
+// serves the MFMAs of every (output row r, tap row ky) with r + ky = ir, so
+// RB+2 fragment reads feed 3*RB MFMAs per pixel tile (0.5 reads per MFMA
+// at one o-tile per wave, the W fragments of that tile, 4*KS VGPRs, stay
+// resident).  Fully unrolled, LDS reads software-pipelined two stages ahead.
+// ---------------------------------------------------------------------------
+template <int C, int W, int RB>
+struct Band {
+  static constexpr int TW = W + 2, NQ = C / 8, PT = W / 16, NCB = C / 32, KS = Geo<C>::KS;
+  static constexpr int NR = RB + 2;             // input rows per band
+  static constexpr int NS = 3 * NCB * NR;       // pipeline stages (kx, cb, input row)
+  static constexpr int ROWB = TW * NQ * 16;     // LDS bytes per tile row
+  static constexpr int PTB = 16 * NQ * 16;      // LDS bytes per 16-pixel tile
+  static_assert(C % 32 == 0, "band conv needs whole 32-channel k-steps per tap");
+  static_assert(NR * ROWB < 65536, "ds_read immediate offset range");
+};
+
+template <int C, int W, int RB, int S>
+__device__ __forceinline__ void band_issue(unsigned base, const unsigned (&lo)[3 * Band<C, W, RB>::NCB],
+                                           bf16x8 (&B)[Band<C, W, RB>::PT]) {
+  using BD = Band<C, W, RB>;
+  constexpr int blk = S / BD::NR, ir = S % BD::NR;
+  B[0] = ds_read128<ir * BD::ROWB>(base + lo[blk]);
+  if constexpr (BD::PT >= 2) B[1] = ds_read128<ir * BD::ROWB + BD::PTB>(base + lo[blk]);
+  static_assert(BD::PT <= 2, "band conv handles up to two pixel tiles");
+}
+
+// MFMAs of output row ir - KY (if inside the band) with tap (KY, kx)
+template <int C, int W, int RB, int ir, int kx, int cb, int KY>
+__device__ __forceinline__ void band_mfma(const bf16x8 (&A)[Geo<C>::KS], f32x4 (&acc)[RB][W / 16],
+                                          const bf16x8 (&B)[W / 16]) {
+  constexpr int r = ir - KY;
+  if constexpr (r >= 0 && r < RB) {
+    constexpr int ks = (KY * 3 + kx) * Band<C, W, RB>::NCB + cb;
+#pragma unroll
+    for (int pt = 0; pt < W / 16; ++pt)
+      acc[r][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], B[pt], acc[r][pt], 0, 0, 0);
+  }
+}
+
+template <int C, int W, int RB, int S>
+__device__ __forceinline__ void band_step(unsigned base, const unsigned (&lo)[3 * Band<C, W, RB>::NCB],
+                                          const bf16x8 (&A)[Geo<C>::KS], f32x4 (&acc)[RB][W / 16],
+                                          bf16x8 (&B)[3][W / 16]) {
+  using BD = Band<C, W, RB>;
+  constexpr int PT = BD::PT;
+  if constexpr (S < BD::NS) {
+    constexpr int blk = S / BD::NR, ir = S % BD::NR;
+    constexpr int kx = blk / BD::NCB, cb = blk % BD::NCB;
+    lgkm_wait<(S + 1 < BD::NS) ? PT : 0>();
+    band_mfma<C, W, RB, ir, kx, cb, 0>(A, acc, B[S % 3]);
+    band_mfma<C, W, RB, ir, kx, cb, 1>(A, acc, B[S % 3]);
+    band_mfma<C, W, RB, ir, kx, cb, 2>(A, acc, B[S % 3]);
+    if constexpr (S + 2 < BD::NS) band_issue<C, W, RB, S + 2>(base, lo, B[(S + 2) % 3]);
+    band_step<C, W, RB, S + 1>(base, lo, A, acc, B);
+  }
+}
+
+// acc[r][pt] += conv over the RB output rows whose first input row is the
+// tile row at LDS byte address `base`
+template <int C, int W, int RB>
+__device__ __forceinline__ void conv_band(unsigned base, const unsigned (&lo)[3 * Band<C, W, RB>::NCB],
+                                          const bf16x8 (&A)[Geo<C>::KS], f32x4 (&acc)[RB][W / 16]) {
+  bf16x8 B[3][W / 16];
+  lgkm_wait<0>();
+  band_issue<C, W, RB, 0>(base, lo, B[0]);
+  band_issue<C, W, RB, 1>(base, lo, B[1]);
+  band_step<C, W, RB, 0>(base, lo, A, acc, B);
+}
+
+template <int C, int W, int RB>
+__device__ __forceinline__ void band_lane_offsets(int g, int lx, unsigned (&lo)[3 * Band<C, W, RB>::NCB]) {
+  using BD = Band<C, W, RB>;
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+    for (int cb = 0; cb < BD::NCB; ++cb) lo[kx * BD::NCB + cb] = (unsigned)toff<C>(0, lx + kx, 4 * cb + g, BD::TW);
+}
+
+// W^T fragments of one 16-channel output tile
+template <int C>
+__device__ __forceinline__ void load_A1(const bf16* __restrict__ wpack, int ot, int lane, bf16x8 (&A)[Geo<C>::KS]) {
+#pragma unroll
+  for (int ks = 0; ks < Geo<C>::KS; ++ks)
+    A[ks] = *(const bf16x8*)(wpack + (((long)ot * Geo<C>::KS + ks) * 64 + lane) * 8);
 }
 
 template <int C>
@@ -291,12 +379,24 @@ __device__ __forceinline__ void load_A(const bf16* __restrict__ wpack, int oh, i
 }
 
 // contiguous run of items for this workgroup
-__device__ __forceinline__ void item_range(long items, long* i0, long* i1) {
-  const long per = items / gridDim.x, rem = items % gridDim.x;
-  const long b = blockIdx.x;
+__device__ __forceinline__ void item_range(int items, int* i0, int* i1) {
+  const int per = items / (int)gridDim.x, rem = items % (int)gridDim.x;
+  const int b = blockIdx.x;
   *i0 = b * per + min(b, rem);
   *i1 = *i0 + per + (b < rem ? 1 : 0);
 }
+
+// (image, band) of consecutive items without a division per item
+struct ItemCursor {
+  int n, b;
+  __device__ __forceinline__ ItemCursor(int it, int nb) : n(it / nb), b(it % nb) {}
+  __device__ __forceinline__ void next(int nb) {
+    if (++b == nb) {
+      b = 0;
+      ++n;
+    }
+  }
+};
 
 // ===========================================================================
 // forward
@@ -328,26 +428,32 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(const bf16* __restrict__ x, bf1
   zero_halo_cols<C, W>(lds, BR + 2, tid, 64 * NW);
   zero_halo_cols<C, W>(lds + TILE, BR + 2, tid, 64 * NW);
   const int nb = (H + BR - 1) / BR;
-  long i0, i1;
-  item_range((long)N * nb, &i0, &i1);
+  int i0, i1;
+  item_range(N * nb, &i0, &i1);
+  ItemCursor cur(i0, nb), nxt(i0, nb);
   if (i0 < i1) {
-    const int n = (int)(i0 / nb), y0 = (int)(i0 % nb) * BR;
-    dma_rows<C, W>(x, lds, n, y0 - 1, min(BR, H - y0) + 2, H, wave, NW, lane);
+    const int y0 = cur.b * BR;
+    dma_rows<C, W>(x, lds, cur.n, y0 - 1, min(BR, H - y0) + 2, H, wave, NW, lane);
   }
+  nxt.next(nb);
   int nst = 0;  // global stores this wave issued after the DMA it must now wait for
-  for (long it = i0; it < i1; ++it) {
-    const int buf = (int)((it - i0) & 1);
+  for (int it = i0; it < i1; ++it, cur.next(nb), nxt.next(nb)) {
+    const int buf = (it - i0) & 1;
     unsigned char* tile = lds + buf * TILE;
     barrier_vm(nst);  // this item's DMA has landed; the other buffer is free
     nst = 0;
     if (ASR_ABLATE != 3 && it + 1 < i1) {
-      const int n1 = (int)((it + 1) / nb), y1 = (int)((it + 1) % nb) * BR;
-      dma_rows<C, W>(x, lds + (buf ^ 1) * TILE, n1, y1 - 1, min(BR, H - y1) + 2, H, wave, NW, lane);
+      const int y1 = nxt.b * BR;
+      dma_rows<C, W>(x, lds + (buf ^ 1) * TILE, nxt.n, y1 - 1, min(BR, H - y1) + 2, H, wave, NW, lane);
     }
-    const int n = (int)(it / nb), y0 = (int)(it % nb) * BR;
+    const int n = cur.n, y0 = cur.b * BR;
     const int rows = min(BR, H - y0);
     for (int r = rg; r < rows; r += RS) {
       f32x4 acc[OTW][PT];
+#pragma unroll
+      for (int t = 0; t < OTW; ++t)
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt) acc[t][pt] = f32x4{bz[t][0], bz[t][1], bz[t][2], bz[t][3]};
       if (ASR_ABLATE != 2) {
         conv_row<C, W>(tile, r, A, boff, acc);
       } else {
@@ -378,20 +484,24 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(const bf16* __restrict__ x, bf1
             unsigned nib = 0;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float z = acc[t][pt][e] + bz[t][e];
-              nib |= (z > 0.f ? 1u : 0u) << e;
-              o4[e] = (bf16)((float)xr[e] + h * fmaxf(z, 0.f));
+              const float z = acc[t][pt][e];
+              const bool pos = z > 0.f;  // relu'(z) as TF's ReluGrad: z > 0
+              nib |= (pos ? 1u : 0u) << e;
+              o4[e] = (bf16)fmaf(h, pos ? z : 0.f, (float)xr[e]);
             }
             mword |= nib << (16 * t + 4 * g);
           } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o4[e] = (bf16)(acc[t][pt][e] + bz[t][e]);
+            for (int e = 0; e < 4; ++e) o4[e] = (bf16)acc[t][pt][e];
           }
           *(bf16x4*)(y + (((long)n * H + gy) * W + px) * C + o0) = o4;
         }
         if constexpr (EULER) {
-          mword |= __shfl_xor(mword, 16);
-          mword |= __shfl_xor(mword, 32);
+          // OR over the four lane groups g (lanes lx, lx+16, lx+32, lx+48)
+          const auto s16 = __builtin_amdgcn_permlane16_swap(mword, mword, false, false);
+          mword = s16[0] | s16[1];
+          const auto s32 = __builtin_amdgcn_permlane32_swap(mword, mword, false, false);
+          mword = s32[0] | s32[1];
           if (mask && g == 0) {
             uint8_t* mp = mask + ((((long)n * H + gy) * W + px) * C + 16 * oh * OTW) / 8;
             if constexpr (OTW == 2)
@@ -400,6 +510,124 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(const bf16* __restrict__ x, bf1
               *(uint16_t*)mp = (uint16_t)mword;
           }
         }
+      }
+    }
+  }
+}
+
+// Forward, band form (C >= 32): wave = (o-tile ot, row group rg); RB rows.
+template <int C, int W, int BR, int MODE, int NW>
+__global__ __launch_bounds__(64 * NW) void k_fwd_band(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                  uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
+                                                  const float* __restrict__ bias, float h, int N, int H) {
+  using G = Geo<C>;
+  constexpr int TW = W + 2, PT = W / 16, NQ = G::NQ, OT = C / 16;
+  constexpr int TILE = (BR + 2) * TW * NQ * 16;
+  static_assert(NW % OT == 0, "waves must cover the o-tiles");
+  constexpr int RS = NW / OT, RB = BR / RS;  // row groups, rows per wave
+  static_assert(BR % RS == 0, "row groups must split the band");
+  using BD = Band<C, W, RB>;
+  constexpr bool EULER = MODE == FWD_EULER;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ot = wave % OT, rg = wave / OT;
+  const int g = lane >> 4, lx = lane & 15;
+  const int o0 = 16 * ot + 4 * g;  // this lane's 4 output channels
+
+  bf16x8 A[G::KS];
+  load_A1<C>(wpack, ot, lane, A);
+  unsigned lo[3 * BD::NCB];
+  band_lane_offsets<C, W, RB>(g, lx, lo);
+  float bz[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) bz[e] = bias ? bias[o0 + e] : 0.f;
+
+  zero_halo_cols<C, W>(lds, BR + 2, tid, 64 * NW);
+  zero_halo_cols<C, W>(lds + TILE, BR + 2, tid, 64 * NW);
+  const int nb = (H + BR - 1) / BR;
+  int i0, i1;
+  item_range(N * nb, &i0, &i1);
+  ItemCursor cur(i0, nb), nxt(i0, nb);
+  if (i0 < i1) {
+    const int y0 = cur.b * BR;
+    dma_rows<C, W>(x, lds, cur.n, y0 - 1, min(BR, H - y0) + 2, H, wave, NW, lane);
+  }
+  nxt.next(nb);
+  int nst = 0;  // global stores this wave issued after the DMA it must now wait for
+  for (int it = i0; it < i1; ++it, cur.next(nb), nxt.next(nb)) {
+    const int buf = (it - i0) & 1;
+    unsigned char* tile = lds + buf * TILE;
+    barrier_vm(nst);  // this item's DMA has landed; the other buffer is free
+    nst = 0;
+    if (ASR_ABLATE != 3 && it + 1 < i1) {
+      const int y1 = nxt.b * BR;
+      dma_rows<C, W>(x, lds + (buf ^ 1) * TILE, nxt.n, y1 - 1, min(BR, H - y1) + 2, H, wave, NW, lane);
+    }
+    const int n = cur.n, y0 = cur.b * BR;
+    const int rows = min(BR, H - y0);
+    const int r0 = rg * RB;
+    if (r0 >= rows) continue;
+    f32x4 acc[RB][PT];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int pt = 0; pt < PT; ++pt) acc[r][pt] = f32x4{bz[0], bz[1], bz[2], bz[3]};
+    if (ASR_ABLATE != 2) conv_band<C, W, RB>(lds_u32(tile + r0 * BD::ROWB), lo, A, acc);
+    if (ASR_ABLATE == 1) {
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt) asm volatile("" ::"v"(acc[r][pt]));
+      continue;
+    }
+    // residual x of the lane's outputs (LDS, asm: the next band's DMA is in flight)
+    u32x2 xr2[RB][PT];
+    if constexpr (EULER) {
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt)
+          xr2[r][pt] = lds_rd64(lds_u32(tile + toff<C>(r0 + r + 1, 16 * pt + lx + 1, o0 >> 3, TW) + (o0 & 4) * 2));
+      lgkm_wait<0>();
+    }
+    // wave-uniform row bases + one 32-bit lane offset: stores need no 64-bit math
+    const long row0 = ((long)n * H + y0 + r0) * W;
+    bf16* yb = y + row0 * C;
+    uint8_t* mkb = mask ? mask + row0 * (C / 8) : nullptr;
+    const unsigned ly = (unsigned)(lx * C + o0);
+    const unsigned lm = (unsigned)(lx * (C / 8) + 2 * ot);
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      if (r0 + r >= rows) break;
+      nst += PT * ((EULER && mask) ? 2 : 1);
+#pragma unroll
+      for (int pt = 0; pt < PT; ++pt) {
+        const unsigned pix = (unsigned)(r * W + 16 * pt);  // compile-time
+        bf16x4 o4;
+        if constexpr (EULER) {
+          const bf16x4 xr = *(const bf16x4*)&xr2[r][pt];
+          unsigned nib = 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float z = acc[r][pt][e];
+            const bool pos = z > 0.f;  // relu'(z) as TF's ReluGrad: z > 0
+            nib |= (pos ? 1u : 0u) << e;
+            // relu as a select on the compare (a max would need NaN canonicalisation)
+            const float rz = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, z) & (pos ? ~0u : 0u));
+            o4[e] = (bf16)fmaf(h, rz, (float)xr[e]);
+          }
+          // the tile's 16 channel bits of pixel px: OR over the lane groups g
+          unsigned mword = nib << (4 * g);
+          const auto s16 = __builtin_amdgcn_permlane16_swap(mword, mword, false, false);
+          mword = s16[0] | s16[1];
+          const auto s32 = __builtin_amdgcn_permlane32_swap(mword, mword, false, false);
+          mword = s32[0] | s32[1];
+          if (mkb && g == 0) *(uint16_t*)(mkb + lm + pix * (C / 8)) = (uint16_t)mword;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o4[e] = (bf16)acc[r][pt][e];
+        }
+        *(bf16x4*)(yb + ly + pix * C) = o4;
       }
     }
   }
@@ -430,9 +658,8 @@ struct BwdLds {
 
 template <int C, int W, int BR, bool EULER>
 __device__ __forceinline__ void bwd_issue(const bf16* dy, const bf16* x, const uint8_t* mask, unsigned char* lds,
-                                          int buf, long it, int nb, int H, int wave, int lane, int nwaves) {
+                                          int buf, int n, int y0, int H, int wave, int lane, int nwaves) {
   using L = BwdLds<C, W, BR>;
-  const int n = (int)(it / nb), y0 = (int)(it % nb) * BR;
   const int nr = min(BR, H - y0) + 2;
   dma_rows<C, W>(dy, lds + L::DY + buf * L::TILE, n, y0 - 1, nr, H, wave, nwaves, lane);
   dma_rows<C, W>(x, lds + L::X + buf * L::TILE, n, y0 - 1, nr, H, wave, nwaves, lane);
@@ -510,9 +737,12 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
     zero_halo_cols<C, W>(lds + L::X + b * L::TILE, BR + 2, tid, 512);
   }
   const int nb = (H + BR - 1) / BR;
-  long i0, i1;
-  item_range((long)N * nb, &i0, &i1);
-  if (i0 < i1) bwd_issue<C, W, BR, EULER>(dy, x, mask, lds, 0, i0, nb, H, wave, lane, 8);
+  int i0, i1;
+  item_range(N * nb, &i0, &i1);
+  if (i0 < i1) {
+    const ItemCursor c0(i0, nb);
+    bwd_issue<C, W, BR, EULER>(dy, x, mask, lds, 0, c0.n, c0.b * BR, H, wave, lane, 8);
+  }
 
   float* slab = slabs + (long)blockIdx.x * (9 * C * C + C);
   const float hs = EULER ? h : 1.f;  // dz = hs * dzm (dzm = dy*mask in LDS)
@@ -531,19 +761,25 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
 #pragma unroll
       for (int e = 0; e < 4; ++e) dbacc[t][e] = 0.f;
     int nst = 0;
-    for (long it = i0; it < i1; ++it) {
-      const int buf = (int)((it - i0) & 1);
-      const int n = (int)(it / nb), y0 = (int)(it % nb) * BR;
+    ItemCursor cur(i0, nb), nxt(i0, nb);
+    nxt.next(nb);
+    for (int it = i0; it < i1; ++it, cur.next(nb), nxt.next(nb)) {
+      const int buf = (it - i0) & 1;
+      const int n = cur.n, y0 = cur.b * BR;
       const int rows = min(BR, H - y0);
       barrier_vm(nst);  // item's DMA landed; previous item fully consumed
       nst = 0;
-      if (it + 1 < i1) bwd_issue<C, W, BR, EULER>(dy, x, mask, lds, buf ^ 1, it + 1, nb, H, wave, lane, 4);
+      if (it + 1 < i1) bwd_issue<C, W, BR, EULER>(dy, x, mask, lds, buf ^ 1, nxt.n, nxt.b * BR, H, wave, lane, 4);
       if (ASR_ABLATE != 4) bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, tid, 512);
       barrier_lds();  // dz ready
       const unsigned char* dzt = lds + L::DZ;
       const unsigned char* dyt = lds + L::DY + buf * L::TILE;
       for (int r = rg; r < rows; r += RS) {
         f32x4 acc[OTW][PT];
+#pragma unroll
+        for (int t = 0; t < OTW; ++t)
+#pragma unroll
+          for (int pt = 0; pt < PT; ++pt) acc[t][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (ASR_ABLATE != 5) {
           conv_row<C, W>(dzt, r, A, boff, acc);
         } else {
@@ -589,7 +825,10 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
             if constexpr (EULER) {
               const bf16x4 dyr = *(const bf16x4*)&dyv[pt][t];
 #pragma unroll
-              for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(hs2g, dzf[e], fmaf(-hs, acc[t][pt][e], (float)dyr[e]));
+              for (int e = 0; e < 4; ++e) {
+                const float v = fmaf(-hs, acc[t][pt][e], (float)dyr[e]);
+                o4[e] = (bf16)(hs2g != 0.f ? fmaf(hs2g, dzf[e], v) : v);
+              }
             } else {
 #pragma unroll
               for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(two_gamma, dzf[e], -acc[t][pt][e]);
@@ -633,9 +872,10 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
     for (int mi = 0; mi < MTW; ++mi)
 #pragma unroll
       for (int ot = 0; ot < OT; ++ot) acc[mi][ot] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (long it = i0; it < i1; ++it) {
-      const int buf = (int)((it - i0) & 1);
-      const int y0 = (int)(it % nb) * BR;
+    ItemCursor cur(i0, nb);
+    for (int it = i0; it < i1; ++it, cur.next(nb)) {
+      const int buf = (it - i0) & 1;
+      const int y0 = cur.b * BR;
       const int rows = min(BR, H - y0);
       barrier_vm(0);
       if (ASR_ABLATE != 4) bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, tid, 512);
@@ -737,16 +977,26 @@ static int launch_fwd_v(int mode, const void* x, void* y, uint8_t* mask, const v
                         int N, int H, hipStream_t s) {
   static_assert(NW % blk::Geo<C>::OSPLIT == 0, "waves must cover the o-split");
   const long items = (long)N * ((H + BR - 1) / BR);
+  if (items > 0x7fffffffL) return fail(ASR_E_UNSUPPORTED, "bf16 block: too many row bands (%ld)", items);
   int cus = cu_count();
   if (cus <= 0) cus = 256;
   const int grid = (int)std::max<long>(1, std::min<long>(items, (long)cus * (8 / NW)));
   const size_t lds = 2 * (size_t)(BR + 2) * (W + 2) * C * 2;
-  if (mode == blk::FWD_EULER)
-    hipLaunchKernelGGL((blk::k_fwd<C, W, BR, blk::FWD_EULER, NW>), dim3(grid), dim3(64 * NW), lds, s,
-                       (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
-  else
-    hipLaunchKernelGGL((blk::k_fwd<C, W, BR, blk::FWD_CONV, NW>), dim3(grid), dim3(64 * NW), lds, s,
-                       (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+  if constexpr (C >= 32) {
+    if (mode == blk::FWD_EULER)
+      hipLaunchKernelGGL((blk::k_fwd_band<C, W, BR, blk::FWD_EULER, NW>), dim3(grid), dim3(64 * NW), lds, s,
+                         (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+    else
+      hipLaunchKernelGGL((blk::k_fwd_band<C, W, BR, blk::FWD_CONV, NW>), dim3(grid), dim3(64 * NW), lds, s,
+                         (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+  } else {
+    if (mode == blk::FWD_EULER)
+      hipLaunchKernelGGL((blk::k_fwd<C, W, BR, blk::FWD_EULER, NW>), dim3(grid), dim3(64 * NW), lds, s,
+                         (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+    else
+      hipLaunchKernelGGL((blk::k_fwd<C, W, BR, blk::FWD_CONV, NW>), dim3(grid), dim3(64 * NW), lds, s,
+                         (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+  }
   ASR_LAUNCH_CHECK("k_fwd");
   return ASR_OK;
 }
@@ -760,7 +1010,9 @@ static int launch_fwd(int mode, const void* x, void* y, uint8_t* mask, const voi
   }();
   switch (variant) {
     case 0: return launch_fwd_v<C, W, 8, 8>(mode, x, y, mask, w, bias, h, N, H, s);
-    case 2: return launch_fwd_v<C, W, 2, 2>(mode, x, y, mask, w, bias, h, N, H, s);
+    case 2:
+      if constexpr (C >= 32) return launch_fwd_v<C, W, 4, 8>(mode, x, y, mask, w, bias, h, N, H, s);
+      else return launch_fwd_v<C, W, 2, 2>(mode, x, y, mask, w, bias, h, N, H, s);
     case 3: return launch_fwd_v<C, W, 8, 4>(mode, x, y, mask, w, bias, h, N, H, s);
     default: return launch_fwd_v<C, W, 4, 4>(mode, x, y, mask, w, bias, h, N, H, s);
   }
@@ -770,6 +1022,7 @@ template <int C, int W>
 static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
                       float two_gamma, int N, int H, void* dx, float* slabs, int* nslabs, hipStream_t s) {
   const long items = (long)N * ((H + kBwdBR - 1) / kBwdBR);
+  if (items > 0x7fffffffL) return fail(ASR_E_UNSUPPORTED, "bf16 block: too many row bands (%ld)", items);
   const int grid = persistent_grid(items);
   *nslabs = grid;
   using L = blk::BwdLds<C, W, kBwdBR>;
