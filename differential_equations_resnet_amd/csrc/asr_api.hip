@@ -21,6 +21,10 @@ int param_map_transpose(int C, const int32_t* w_src, int32_t* w_bwd);
 int reduce_and_project(const float* slabs, int P, long E, int Cb, const int32_t* theta_dst, long n_theta,
                        float* dtheta, float* dbias, float* dw_out, float* ws, hipStream_t s);
 size_t reduce_ws_bytes(int P, long ES);
+int reduce_groups(int P);
+int reduce_slabs_to_groups(const float* slabs, int P, long ES, float* grp, hipStream_t s);
+int project_layers(const float* grp, long grp_stride, int G, long E, int Cb, const int32_t* theta_dst, long n_theta,
+                   int L, float* out, long out_stride, hipStream_t s);
 // asr_block_mfma.hip
 int block_fwd_mfma(int mode, const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h, int N,
                    int H, int W, int C, hipStream_t s);
@@ -81,7 +85,7 @@ static BwdWs bwd_ws_layout(int N, int H, int W, int C, int dtype) {
 static int conv_backward_impl(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w,
                               const int32_t* theta_dst, long n_theta, float h, float gamma, int N, int H, int W,
                               int C, int dtype, void* dx, float* dtheta, float* dbias, float* dw_hwio, void* ws,
-                              hipStream_t s) {
+                              hipStream_t s, float* grp_defer = nullptr, int* nsl_out = nullptr) {
   const BwdWs L = bwd_ws_layout(N, H, W, C, dtype);
   unsigned char* base = (unsigned char*)ws;
   float* slabs = (float*)(base + L.slabs);
@@ -99,6 +103,10 @@ static int conv_backward_impl(int mode, const void* dy, const void* x, const uin
       ASR_TRY(conv_f32(mode == ASR_MODE_EULER ? B_EULER : B_CONV, dz, dx, nullptr, (const float*)w, nullptr, h,
                        2.f * gamma, (const float*)dy, N, H, W, C, C, 0, s));
     if (need_w) ASR_TRY(wgrad_f32(x, 0, dz, N, H, W, C, C, slabs, &nsl, s));
+  }
+  if (grp_defer) {  // the network defers pass 2 + projection to one launch for all layers
+    if (nsl_out) *nsl_out = nsl;
+    return reduce_slabs_to_groups(slabs, nsl, 9L * C * C + C, grp_defer, s);
   }
   if (need_w)
     ASR_TRY(reduce_and_project(slabs, nsl, 9L * C * C, C, dtheta ? theta_dst : nullptr, n_theta, dtheta, dbias,
@@ -191,6 +199,7 @@ struct NetLayout {
   long ntheta, P, E, wstride;  // wstride in elements of the W dtype
   long off_c1k, off_c1b, off_blk, blk_stride, off_fck, off_fcb, nparams;
   bool sep_bwd;  // operator not antisymmetric: dgrad uses W_bwd = -flip(W)^T
+  size_t grp;  // per-layer slab group sums, projected after the whole backward
   size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, x0, acts, masks, dxa, dxb, bwdws, slabs, red, probs, loss_per, dlogits, gap, total;
   long mask_bytes;
   int act_bytes;
@@ -251,6 +260,7 @@ static NetLayout net_layout(const asr_net_config* c) {
   const size_t stem_ws = align_up((size_t)L.P * 4, 256) + align_up((size_t)kMaxSlabsApi * (E1 + C) * 4, 256) +
                          align_up(reduce_ws_bytes(kMaxSlabsApi, E1 + C), 256);
   L.bwdws = take(std::max(bw.total, stem_ws));
+  L.grp = take((size_t)c->L * reduce_groups(kMaxSlabsApi) * (L.E + C) * 4);
   L.probs = take((size_t)c->N * K * 4);
   L.loss_per = take((size_t)c->N * 4);
   L.dlogits = take((size_t)c->N * K * 4);
@@ -424,15 +434,21 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
                            grads + L.off_fcb, (const float*)(b + L.loss_per), loss, s));
   // Euler blocks, last to first
   const int32_t* theta_dst = (const int32_t*)(b + L.theta_dst);
+  int nsl_blk = 0;
   for (int l = cfg->L - 1; l >= 0; --l) {
     const unsigned char* wl = b + (L.sep_bwd ? L.wbuf_bwd : L.wbuf) + (size_t)l * L.wstride * L.act_bytes;
     const uint8_t* mask = (const uint8_t*)(b + L.masks) + (size_t)l * L.mask_bytes;
     float* dth = grads + L.off_blk + (long)l * L.blk_stride;
+    float* grp_l = (float*)(b + L.grp) + (size_t)l * reduce_groups(kMaxSlabsApi) * (L.E + C);
     ASR_TRY(conv_backward_impl(ASR_MODE_EULER, dcur, act(l), mask, wl, theta_dst, L.ntheta, cfg->h,
                                L.sep_bwd ? 0.f : cfg->gamma, N, H, W, C, cfg->dtype, dnext, dth, dth + L.ntheta,
-                               nullptr, b + L.bwdws, s));
+                               nullptr, b + L.bwdws, s, grp_l, &nsl_blk));
     std::swap(dcur, dnext);
   }
+  // pass 2 of every block's weight-gradient reduction + projection onto theta, one launch
+  ASR_TRY(project_layers((const float*)(b + L.grp), (long)reduce_groups(kMaxSlabsApi) * (L.E + C),
+                         reduce_groups(nsl_blk), L.E, C, theta_dst, L.ntheta, cfg->L, grads + L.off_blk, L.blk_stride,
+                         s));
   // stem: dz1 = dx1 * [x1 > 0]; conv1 weight/bias gradient from the normalised input
   const long E1 = 9L * cfg->Cin * C;
   unsigned char* sw = b + L.bwdws;

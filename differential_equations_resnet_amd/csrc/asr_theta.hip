@@ -372,4 +372,56 @@ int reduce_and_project(const float* slabs, int P, long E, int Cb, const int32_t*
 
 size_t reduce_ws_bytes(int P, long ES) { return (size_t)((P + 31) / 32 + 1) * ES * sizeof(float); }
 
+int reduce_groups(int P) { return (P + 31) / 32; }
+
+// Pass 1 only: P slab rows of ES floats -> reduce_groups(P) group rows at grp.
+int reduce_slabs_to_groups(const float* slabs, int P, long ES, float* grp, hipStream_t s) {
+  const int G = reduce_groups(P);
+  dim3 g1((unsigned)((ES + 255) / 256), G);
+  hipLaunchKernelGGL(k_reduce_slabs, g1, dim3(256), 0, s, slabs, ES, P, 32, grp);
+  ASR_LAUNCH_CHECK("k_reduce_slabs");
+  return ASR_OK;
+}
+
+// Pass 2 + projection for L layers in one launch: layer l's G group rows of
+// [dW (E) | db (Cb)] at grp + l*grp_stride -> dtheta at out + l*out_stride,
+// db right after it (the network's [theta | bias] block layout).
+__global__ void k_project_layers(const float* __restrict__ grp, long grp_stride, int G, long E, int Cb,
+                                 const int32_t* __restrict__ theta_dst, long n_theta, float* __restrict__ out,
+                                 long out_stride) {
+  const int l = blockIdx.y;
+  const float* rg = grp + (long)l * grp_stride;
+  const long ES = E + Cb;
+  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  auto red_at = [&](long e) {
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    int g = 0;
+    for (; g + 3 < G; g += 4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] += rg[(long)(g + q) * ES + e];
+    }
+    for (; g < G; ++g) a[0] += rg[(long)g * ES + e];
+    return (a[0] + a[1]) + (a[2] + a[3]);
+  };
+  float* o = out + (long)l * out_stride;
+  if (t < n_theta) {
+    const int32_t v0 = theta_dst[2 * t], v1 = theta_dst[2 * t + 1];
+    float acc = 0.f;
+    if (v0 >= 0) acc += (v0 & 1) ? -red_at(v0 >> 1) : red_at(v0 >> 1);
+    if (v1 >= 0) acc += (v1 & 1) ? -red_at(v1 >> 1) : red_at(v1 >> 1);
+    o[t] = acc;
+  } else if (t < n_theta + Cb) {
+    o[t] = red_at(E + (t - n_theta));
+  }
+}
+
+int project_layers(const float* grp, long grp_stride, int G, long E, int Cb, const int32_t* theta_dst, long n_theta,
+                   int L, float* out, long out_stride, hipStream_t s) {
+  const long n = n_theta + Cb;
+  hipLaunchKernelGGL(k_project_layers, dim3((unsigned)((n + 255) / 256), L), dim3(256), 0, s, grp, grp_stride, G, E,
+                     Cb, theta_dst, n_theta, out, out_stride);
+  ASR_LAUNCH_CHECK("k_project_layers");
+  return ASR_OK;
+}
+
 }  // namespace asr
