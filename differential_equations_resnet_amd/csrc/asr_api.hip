@@ -23,7 +23,7 @@ int reduce_and_project(const float* slabs, int P, long E, int Cb, const int32_t*
 size_t reduce_ws_bytes(int P, long ES);
 int reduce_groups(int P);
 int reduce_slabs_to_groups(const float* slabs, int P, long ES, float* grp, hipStream_t s);
-int project_layers(const float* grp, long grp_stride, int G, long E, int Cb, const int32_t* theta_dst, long n_theta,
+int project_layers(float* grp, long grp_stride, int G, long E, int Cb, const int32_t* theta_dst, long n_theta,
                    int L, float* out, long out_stride, hipStream_t s);
 // asr_block_mfma.hip
 int block_fwd_mfma(int mode, const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h, int N,
@@ -446,7 +446,7 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
     std::swap(dcur, dnext);
   }
   // pass 2 of every block's weight-gradient reduction + projection onto theta, one launch
-  ASR_TRY(project_layers((const float*)(b + L.grp), (long)reduce_groups(kMaxSlabsApi) * (L.E + C),
+  ASR_TRY(project_layers((float*)(b + L.grp), (long)reduce_groups(kMaxSlabsApi) * (L.E + C),
                          reduce_groups(nsl_blk), L.E, C, theta_dst, L.ntheta, cfg->L, grads + L.off_blk, L.blk_stride,
                          s));
   // stem: dz1 = dx1 * [x1 > 0]; conv1 weight/bias gradient from the normalised input

@@ -27,6 +27,8 @@
 // images of dz (computed once per item from dy and the relu mask) and x.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "asr_common.h"
 
 #ifndef ASR_ABLATE
@@ -320,10 +322,18 @@ __device__ __forceinline__ void band_mfma(const bf16x8 (&A)[Geo<C>::KS], f32x4 (
   }
 }
 
-template <int C, int W, int RB, int S>
+struct NoHook {
+  template <typename U>
+  __device__ __forceinline__ void operator()(U) const {}
+};
+
+// hook(integral_constant<int, u>) is called once for u = 0 .. NU-1, spread
+// evenly over the pipeline stages (the forward interleaves the previous
+// band's epilogue with this band's MFMAs that way)
+template <int C, int W, int RB, int NU, int S, typename Hook>
 __device__ __forceinline__ void band_step(unsigned base, const unsigned (&lo)[3 * Band<C, W, RB>::NCB],
                                           const bf16x8 (&A)[Geo<C>::KS], f32x4 (&acc)[RB][W / 16],
-                                          bf16x8 (&B)[3][W / 16]) {
+                                          bf16x8 (&B)[3][W / 16], Hook& hook) {
   using BD = Band<C, W, RB>;
   constexpr int PT = BD::PT;
   if constexpr (S < BD::NS) {
@@ -334,20 +344,24 @@ __device__ __forceinline__ void band_step(unsigned base, const unsigned (&lo)[3 
     band_mfma<C, W, RB, ir, kx, cb, 1>(A, acc, B[S % 3]);
     band_mfma<C, W, RB, ir, kx, cb, 2>(A, acc, B[S % 3]);
     if constexpr (S + 2 < BD::NS) band_issue<C, W, RB, S + 2>(base, lo, B[(S + 2) % 3]);
-    band_step<C, W, RB, S + 1>(base, lo, A, acc, B);
+    if constexpr (NU > 0) {
+      constexpr int SP = BD::NS / NU;
+      if constexpr (SP > 0 && S % SP == SP / 2 && S / SP < NU) hook(std::integral_constant<int, S / SP>{});
+    }
+    band_step<C, W, RB, NU, S + 1>(base, lo, A, acc, B, hook);
   }
 }
 
 // acc[r][pt] += conv over the RB output rows whose first input row is the
 // tile row at LDS byte address `base`
-template <int C, int W, int RB>
+template <int C, int W, int RB, int NU = 0, typename Hook = NoHook>
 __device__ __forceinline__ void conv_band(unsigned base, const unsigned (&lo)[3 * Band<C, W, RB>::NCB],
-                                          const bf16x8 (&A)[Geo<C>::KS], f32x4 (&acc)[RB][W / 16]) {
+                                          const bf16x8 (&A)[Geo<C>::KS], f32x4 (&acc)[RB][W / 16], Hook hook = {}) {
   bf16x8 B[3][W / 16];
   lgkm_wait<0>();
   band_issue<C, W, RB, 0>(base, lo, B[0]);
   band_issue<C, W, RB, 1>(base, lo, B[1]);
-  band_step<C, W, RB, 0>(base, lo, A, acc, B);
+  band_step<C, W, RB, NU, 0>(base, lo, A, acc, B, hook);
 }
 
 template <int C, int W, int RB>
@@ -630,6 +644,166 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_band(const bf16* __restrict__ x
         *(bf16x4*)(yb + ly + pix * C) = o4;
       }
     }
+  }
+}
+
+template <int NU, int U = 0, typename F, typename Acc, typename Xr, typename Cur>
+__device__ __forceinline__ void epi_all_units(F& f, const Acc& acc, const Xr& xr, const Cur& c) {
+  if constexpr (U < NU) {
+    f(std::integral_constant<int, U>{}, acc, xr, c);
+    epi_all_units<NU, U + 1>(f, acc, xr, c);
+  }
+}
+
+// Forward, band form with a software pipeline across bands: the MFMAs of
+// band i+1 are interleaved with the epilogue (VALU + stores) of band i, so
+// the matrix pipe and the vector ALU of one wave work at the same time.
+template <int C, int W, int BR, int MODE, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                  uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
+                                                  const float* __restrict__ bias, float h, int N, int H) {
+  using G = Geo<C>;
+  constexpr int TW = W + 2, PT = W / 16, NQ = G::NQ, OT = C / 16;
+  constexpr int TILE = (BR + 2) * TW * NQ * 16;
+  static_assert(NW % OT == 0, "waves must cover the o-tiles");
+  constexpr int RS = NW / OT, RB = BR / RS;
+  static_assert(BR % RS == 0, "row groups must split the band");
+  using BD = Band<C, W, RB>;
+  constexpr int NU = RB * PT;  // epilogue units (row, pixel tile)
+  constexpr bool EULER = MODE == FWD_EULER;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ot = wave % OT, rg = wave / OT;
+  const int g = lane >> 4, lx = lane & 15;
+  const int o0 = 16 * ot + 4 * g;
+  const int r0 = rg * RB;
+
+  bf16x8 A[G::KS];
+  load_A1<C>(wpack, ot, lane, A);
+  unsigned lo[3 * BD::NCB];
+  band_lane_offsets<C, W, RB>(g, lx, lo);
+  float bz[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) bz[e] = bias ? bias[o0 + e] : 0.f;
+  const unsigned ly = (unsigned)(lx * C + o0);
+  const unsigned lm = (unsigned)(lx * (C / 8) + 2 * ot);
+  const unsigned lxr = (unsigned)(toff<C>(r0 + 1, lx + 1, o0 >> 3, TW) + (o0 & 4) * 2);
+
+  zero_halo_cols<C, W>(lds, BR + 2, tid, 64 * NW);
+  zero_halo_cols<C, W>(lds + TILE, BR + 2, tid, 64 * NW);
+  const int nb = (H + BR - 1) / BR;
+  int i0, i1;
+  item_range(N * nb, &i0, &i1);
+  if (i0 >= i1) return;
+  ItemCursor cur(i0, nb), nx1(i0, nb), nx2(i0, nb);  // items it, it+1, it+2
+  nx1.next(nb);
+  nx2.next(nb);
+  nx2.next(nb);
+  auto dma = [&](const ItemCursor& c, int buf) {
+    const int yy = c.b * BR;
+    dma_rows<C, W>(x, lds + buf * TILE, c.n, yy - 1, min(BR, H - yy) + 2, H, wave, NW, lane);
+  };
+  auto xres_read = [&](int buf, u32x2 (&xr)[RB][PT]) {
+    if constexpr (EULER) {
+      const unsigned tb = lds_u32(lds + buf * TILE) + lxr;
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt) xr[r][pt] = lds_rd64(tb + (unsigned)(r * BD::ROWB + pt * BD::PTB));
+      lgkm_wait<0>();
+    }
+  };
+  auto init = [&](f32x4 (&acc)[RB][PT]) {
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int pt = 0; pt < PT; ++pt) acc[r][pt] = f32x4{bz[0], bz[1], bz[2], bz[3]};
+  };
+  int nst = 0;
+  // one epilogue unit (row r, pixel tile pt) of the band at cursor c
+  auto epi_unit = [&](auto U, const f32x4 (&acc)[RB][PT], const u32x2 (&xr)[RB][PT], const ItemCursor& c) {
+    constexpr int u = decltype(U)::value, r = u / PT, pt = u % PT;
+    const int y0 = c.b * BR;
+    if (r0 + r >= min(BR, H - y0)) return;
+    const long row = ((long)c.n * H + y0 + r0 + r) * W + 16 * pt;
+    nst += (EULER && mask) ? 2 : 1;
+    bf16x4 o4;
+    if constexpr (EULER) {
+      const bf16x4 xv = *(const bf16x4*)&xr[r][pt];
+      unsigned nib = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float z = acc[r][pt][e];
+        const bool pos = z > 0.f;  // relu'(z) as TF's ReluGrad: z > 0
+        nib |= (pos ? 1u : 0u) << e;
+        const float rz = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, z) & (pos ? ~0u : 0u));
+        o4[e] = (bf16)fmaf(h, rz, (float)xv[e]);
+      }
+      unsigned mword = nib << (4 * g);
+      const auto s16 = __builtin_amdgcn_permlane16_swap(mword, mword, false, false);
+      mword = s16[0] | s16[1];
+      const auto s32 = __builtin_amdgcn_permlane32_swap(mword, mword, false, false);
+      mword = s32[0] | s32[1];
+      if (mask && g == 0) *(uint16_t*)(mask + row * (C / 8) + lm) = (uint16_t)mword;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o4[e] = (bf16)acc[r][pt][e];
+    }
+    *(bf16x4*)(y + row * C + ly) = o4;
+  };
+  auto epi_all = [&](const f32x4 (&acc)[RB][PT], const u32x2 (&xr)[RB][PT], const ItemCursor& c) {
+    epi_all_units<NU>(epi_unit, acc, xr, c);
+  };
+
+  f32x4 accA[RB][PT], accB[RB][PT];
+  u32x2 xrA[RB][PT], xrB[RB][PT];
+  // prologue: band i0 computed (its epilogue waits for the next band's MFMAs)
+  dma(cur, 0);
+  barrier_vm(0);
+  if (i0 + 1 < i1) dma(nx1, 1);
+  init(accA);
+  conv_band<C, W, RB>(lds_u32(lds + r0 * BD::ROWB), lo, A, accA);
+  xres_read(0, xrA);
+  int it = i0;
+  while (true) {
+    // accA / xrA: band it.  In flight: DMA of band it+1 into buffer (it+1-i0)&1.
+    if (it + 1 >= i1) {
+      epi_all(accA, xrA, cur);
+      break;
+    }
+    barrier_vm(nst);  // band it+1 landed, every wave is done with band it's tile
+    nst = 0;
+    if (it + 2 < i1) dma(nx2, (it - i0) & 1);
+    init(accB);
+    {
+      const ItemCursor c = cur;
+      auto hook = [&](auto U) { epi_unit(U, accA, xrA, c); };
+      conv_band<C, W, RB, NU>(lds_u32(lds + ((it + 1 - i0) & 1) * TILE + r0 * BD::ROWB), lo, A, accB, hook);
+    }
+    xres_read((it + 1 - i0) & 1, xrB);
+    ++it;
+    cur.next(nb);
+    nx1.next(nb);
+    nx2.next(nb);
+    // the same with the roles of A and B swapped
+    if (it + 1 >= i1) {
+      epi_all(accB, xrB, cur);
+      break;
+    }
+    barrier_vm(nst);
+    nst = 0;
+    if (it + 2 < i1) dma(nx2, (it - i0) & 1);
+    init(accA);
+    {
+      const ItemCursor c = cur;
+      auto hook = [&](auto U) { epi_unit(U, accB, xrB, c); };
+      conv_band<C, W, RB, NU>(lds_u32(lds + ((it + 1 - i0) & 1) * TILE + r0 * BD::ROWB), lo, A, accA, hook);
+    }
+    xres_read((it + 1 - i0) & 1, xrA);
+    ++it;
+    cur.next(nb);
+    nx1.next(nb);
+    nx2.next(nb);
   }
 }
 
@@ -982,13 +1156,23 @@ static int launch_fwd_v(int mode, const void* x, void* y, uint8_t* mask, const v
   if (cus <= 0) cus = 256;
   const int grid = (int)std::max<long>(1, std::min<long>(items, (long)cus * (8 / NW)));
   const size_t lds = 2 * (size_t)(BR + 2) * (W + 2) * C * 2;
+  static const bool no_pipe = getenv("ASR_FWD_NOPIPE") != nullptr;  // development A/B
   if constexpr (C >= 32) {
-    if (mode == blk::FWD_EULER)
-      hipLaunchKernelGGL((blk::k_fwd_band<C, W, BR, blk::FWD_EULER, NW>), dim3(grid), dim3(64 * NW), lds, s,
-                         (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
-    else
-      hipLaunchKernelGGL((blk::k_fwd_band<C, W, BR, blk::FWD_CONV, NW>), dim3(grid), dim3(64 * NW), lds, s,
-                         (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+    if (no_pipe) {
+      if (mode == blk::FWD_EULER)
+        hipLaunchKernelGGL((blk::k_fwd_band<C, W, BR, blk::FWD_EULER, NW>), dim3(grid), dim3(64 * NW), lds, s,
+                           (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+      else
+        hipLaunchKernelGGL((blk::k_fwd_band<C, W, BR, blk::FWD_CONV, NW>), dim3(grid), dim3(64 * NW), lds, s,
+                           (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+    } else {
+      if (mode == blk::FWD_EULER)
+        hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_EULER, NW>), dim3(grid), dim3(64 * NW), lds, s,
+                           (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+      else
+        hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_CONV, NW>), dim3(grid), dim3(64 * NW), lds, s,
+                           (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+    }
   } else {
     if (mode == blk::FWD_EULER)
       hipLaunchKernelGGL((blk::k_fwd<C, W, BR, blk::FWD_EULER, NW>), dim3(grid), dim3(64 * NW), lds, s,

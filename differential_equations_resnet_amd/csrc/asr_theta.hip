@@ -415,10 +415,30 @@ __global__ void k_project_layers(const float* __restrict__ grp, long grp_stride,
   }
 }
 
-int project_layers(const float* grp, long grp_stride, int G, long E, int Cb, const int32_t* theta_dst, long n_theta,
+// rows [l][0] = sum_g grp[l][g] (coalesced, fixed order), in place
+__global__ void k_sum_groups(float* __restrict__ grp, long grp_stride, int G, long ES) {
+  const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e >= ES) return;
+  float* rg = grp + (long)blockIdx.y * grp_stride;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  int g = 0;
+  for (; g + 3 < G; g += 4) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[q] += rg[(long)(g + q) * ES + e];
+  }
+  for (; g < G; ++g) a[0] += rg[(long)g * ES + e];
+  rg[e] = (a[0] + a[1]) + (a[2] + a[3]);
+}
+
+int project_layers(float* grp, long grp_stride, int G, long E, int Cb, const int32_t* theta_dst, long n_theta,
                    int L, float* out, long out_stride, hipStream_t s) {
   const long n = n_theta + Cb;
-  hipLaunchKernelGGL(k_project_layers, dim3((unsigned)((n + 255) / 256), L), dim3(256), 0, s, grp, grp_stride, G, E,
+  if (G > 1) {  // pass 2 coalesced, then the projection gathers from one row per layer
+    hipLaunchKernelGGL(k_sum_groups, dim3((unsigned)((E + Cb + 255) / 256), L), dim3(256), 0, s, grp, grp_stride, G,
+                       E + Cb);
+    ASR_LAUNCH_CHECK("k_sum_groups");
+  }
+  hipLaunchKernelGGL(k_project_layers, dim3((unsigned)((n + 255) / 256), L), dim3(256), 0, s, grp, grp_stride, 1, E,
                      Cb, theta_dst, n_theta, out, out_stride);
   ASR_LAUNCH_CHECK("k_project_layers");
   return ASR_OK;
