@@ -36,12 +36,13 @@ BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (spec)
 F32_PEAK_TFLOPS = 157.3
 
 CONFIGS = {
-    # name: (C, L, per-GPU batch, dtype, description)
-    "c2": (64, 30, 512, "bfloat16", "antisym-ResNet-32 (C=64, 30 Euler blocks) batch 512/GPU bf16"),
-    "c2_16": (16, 30, 512, "bfloat16", "antisym-ResNet-32 (C=16, 30 Euler blocks) batch 512/GPU bf16"),
-    "c1": (16, 18, 128, "float32", "antisym-ResNet-20 (C=16, 18 Euler blocks) batch 128 fp32"),
-    "c3": (16, 108, 1024, "bfloat16", "antisym-ResNet-110 (C=16, 108 Euler blocks) batch 1024 bf16"),
-    "c3_64": (64, 108, 1024, "bfloat16", "antisym-ResNet-110 (C=64, 108 Euler blocks) batch 1024 bf16"),
+    # name: (C, L, per-GPU batch, dtype, description, integrator)
+    "c2": (64, 30, 512, "bfloat16", "antisym-ResNet-32 (C=64, 30 Euler blocks) batch 512/GPU bf16", "euler"),
+    "c2_16": (16, 30, 512, "bfloat16", "antisym-ResNet-32 (C=16, 30 Euler blocks) batch 512/GPU bf16", "euler"),
+    "c1": (16, 18, 128, "float32", "antisym-ResNet-20 (C=16, 18 Euler blocks) batch 128 fp32", "euler"),
+    "c3": (16, 108, 1024, "bfloat16", "antisym-ResNet-110 (C=16, 108 Euler blocks) batch 1024 bf16", "euler"),
+    "c3_64": (64, 108, 1024, "bfloat16", "antisym-ResNet-110 (C=64, 108 Euler blocks) batch 1024 bf16", "euler"),
+    "c5": (64, 30, 512, "bfloat16", "antisym-ResNet-32 (C=64, 30 RK2 midpoint blocks) batch 512/GPU bf16", "rk2"),
 }
 
 
@@ -59,9 +60,15 @@ def parse():
     return ap.parse_args()
 
 
-def block_roofline(rt, lib, C, N, dtype_name, reps, h):
-    """Time one Euler block (fwd + full bwd) at the workload shape with HIP
-    events on the launch stream; return per-launch averages."""
+def block_roofline(rt, lib, C, N, dtype_name, reps, h, integrator="euler"):
+    """Time one block (fwd + full bwd) at the workload shape with HIP events
+    on the launch stream; return per-launch averages.
+
+    Algorithmic bytes (SURVEY §8d): Euler block 5·P·s (fwd: read x, write y;
+    bwd: read dy, read x, write dx).  RK2 block 12·P·s, the minimum of its
+    two-stage composition with the midpoint stored: fwd read x, write xm,
+    read xm, read x, write y; bwd stage 2 read dy, read xm, write g; stage 1
+    read g, read x, read dy, write dx."""
     import torch
     from differential_equations_resnet_amd import _lib
     dev = torch.device("cuda")
@@ -94,6 +101,23 @@ def block_roofline(rt, lib, C, N, dtype_name, reps, h):
                                          theta_dst.data_ptr(), pm.n_theta, h, 0.0, N, H, W, C, dt, dx.data_ptr(),
                                          dth.data_ptr(), db.data_ptr(), None, ws.data_ptr(), ws_bytes, s), "bwd")
 
+    if integrator == "rk2":
+        xm = torch.empty_like(x)
+        mask2 = torch.zeros_like(mask)
+        ws_bytes = int(lib.asr_rk2_backward_workspace_bytes(N, H, W, C, dt))
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+
+        def fwd():  # noqa: F811
+            _lib.check(lib.asr_rk2_forward(x.data_ptr(), xm.data_ptr(), y.data_ptr(), mask.data_ptr(),
+                                           mask2.data_ptr(), w.data_ptr(), bias.data_ptr(), h, N, H, W, C, dt, s),
+                       "rk2 fwd")
+
+        def bwd():  # noqa: F811
+            _lib.check(lib.asr_rk2_backward(dy.data_ptr(), x.data_ptr(), xm.data_ptr(), mask.data_ptr(),
+                                            mask2.data_ptr(), w.data_ptr(), theta_dst.data_ptr(), pm.n_theta, h, 0.0,
+                                            N, H, W, C, dt, dx.data_ptr(), dth.data_ptr(), db.data_ptr(), None,
+                                            ws.data_ptr(), ws_bytes, s), "rk2 bwd")
+
     for _ in range(10):
         fwd()
         bwd()
@@ -115,8 +139,9 @@ def block_roofline(rt, lib, C, N, dtype_name, reps, h):
     t_blk = timed(lambda: (fwd(), bwd()))
     esz = 2 if dt == rt.ASR_BF16 else 4
     P = N * H * W * C
-    bytes_alg = 5 * P * esz  # fwd read x + write y; bwd read dy, read x, write dx
-    flops = 3 * 2 * 9 * C * C * N * H * W
+    stages = 2 if integrator == "rk2" else 1
+    bytes_alg = (12 if stages == 2 else 5) * P * esz  # see the docstring
+    flops = stages * 3 * 2 * 9 * C * C * N * H * W
     return dict(t_fwd=tf, t_bwd=tb, t=t_blk, bytes=bytes_alg, flops=flops)
 
 
@@ -173,10 +198,10 @@ def main():
     dev = rt.require_gpu()
     lib = _lib.load()
 
-    C, L, N, dtype_name, desc = CONFIGS[args.config]
+    C, L, N, dtype_name, desc, integrator = CONFIGS[args.config]
     h = 8.0 / L  # final_time 8 (experiments_antisymmetric_resnet_v6.ipynb cell 1)
     ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, h, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
-                        dtype=dtype_name, input_u8=True, device=dev)
+                        dtype=dtype_name, input_u8=True, device=dev, integrator=integrator)
     params = torch.from_numpy(init_net_params(C, L, 3, 10, seed=0)).to(dev)
     if world > 1:
         dist.broadcast(params, 0)
@@ -219,7 +244,7 @@ def main():
     roof = None
     cpu = None
     if rank == 0:
-        rb = block_roofline(rt, lib, C, N, dtype_name, args.block_reps, h)
+        rb = block_roofline(rt, lib, C, N, dtype_name, args.block_reps, h, integrator)
         achieved = rb["bytes"] / rb["t"] / 1e9
         tflops = rb["flops"] / rb["t"] / 1e12
         peak_tf = BF16_PEAK_TFLOPS if dtype_name == "bfloat16" else F32_PEAK_TFLOPS
@@ -230,12 +255,15 @@ def main():
                 traffic = json.load(f).get("hbm_bytes_per_block")
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "Euler block fwd+bwd (blk::k_fwd, blk::k_bwd fused dgrad+wgrad, k_reduce_slabs, k_project)",
+                "kernel": ("RK2 block fwd+bwd (2x blk::k_fwd_pipe, 2x blk::k_bwd, k_reduce_slabs, k_project)"
+                           if integrator == "rk2" else
+                           "Euler block fwd+bwd (blk::k_fwd_pipe, blk::k_bwd fused dgrad+wgrad, k_reduce_slabs, "
+                           "k_project)"),
                 "algorithmic_bytes": rb["bytes"], "avg_us": round(rb["t"] * 1e6, 2),
                 "avg_us_fwd": round(rb["t_fwd"] * 1e6, 2), "avg_us_bwd": round(rb["t_bwd"] * 1e6, 2),
                 "mfma_tflops": round(tflops, 1), "mfma_frac": round(tflops / peak_tf, 4)}
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(C, L, h, args.cpu_batch, args.cpu_steps)
+            cpu = cpu_baseline(C, L, h, args.cpu_batch, args.cpu_steps) if integrator == "euler" else None
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
@@ -243,7 +271,7 @@ def main():
             "dtype": "bf16" if dtype_name == "bfloat16" else "f32",
             "data": "synthetic (uniform uint8 32x32x3 images, random one-hot labels; random-init weights)",
             "config": {"workload": desc + "; train step = fwd + bwd + Adam", "global_batch": N * world,
-                       "per_gpu_batch": N, "channels": C, "euler_blocks": L, "h": round(h, 6),
+                       "per_gpu_batch": N, "channels": C, "blocks": L, "integrator": integrator, "h": round(h, 6),
                        "parallelism": f"dp{world}", "final_loss": round(final_loss, 4)},
             "roofline": roof, "cpu_baseline": cpu,
         }

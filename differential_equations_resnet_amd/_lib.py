@@ -29,9 +29,11 @@ ASR_BF16 = 1
 ASR_PARAM_3BY3 = 0
 ASR_PARAM_GENERAL = 1
 ASR_PARAM_REGULAR = 2
-ABI_VERSION = 2
+ABI_VERSION = 3
 ASR_MODE_EULER = 0
 ASR_MODE_CONV = 1
+ASR_INTEGRATOR_EULER = 0
+ASR_INTEGRATOR_RK2 = 1
 
 
 class AsrError(RuntimeError):
@@ -47,7 +49,7 @@ class NetConfig(ct.Structure):
         ("N", ct.c_int), ("H", ct.c_int), ("W", ct.c_int), ("Cin", ct.c_int), ("C", ct.c_int), ("L", ct.c_int),
         ("num_classes", ct.c_int), ("h", ct.c_float), ("gamma", ct.c_float), ("subtract_mean", ct.c_float),
         ("divide_by_stddev", ct.c_float), ("use_norm", ct.c_int), ("dtype", ct.c_int), ("input_u8", ct.c_int),
-        ("param_kind", ct.c_int), ("antisymmetric", ct.c_int),
+        ("param_kind", ct.c_int), ("antisymmetric", ct.c_int), ("integrator", ct.c_int),
     ]
 
 
@@ -72,6 +74,10 @@ SIGNATURES = [
     ("asr_mask_bytes", _L, [_I, _I, _I, _I]),
     ("asr_conv_backward_workspace_bytes", _S, [_I, _I, _I, _I, _I]),
     ("asr_conv_backward", _I, [_I, _P, _P, _P, _P, _P, _L, _F, _F, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _S, _P]),
+    ("asr_rk2_forward", _I, [_P, _P, _P, _P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P]),
+    ("asr_rk2_backward_workspace_bytes", _S, [_I, _I, _I, _I, _I]),
+    ("asr_rk2_backward", _I, [_P, _P, _P, _P, _P, _P, _P, _L, _F, _F, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _S,
+                              _P]),
     ("asr_net_param_count", _L, [ct.POINTER(NetConfig)]),
     ("asr_net_workspace_bytes", _S, [ct.POINTER(NetConfig)]),
     ("asr_net_prepare", _I, [ct.POINTER(NetConfig), _P, _S]),

@@ -26,14 +26,16 @@ int reduce_slabs_to_groups(const float* slabs, int P, long ES, float* grp, hipSt
 int project_layers(float* grp, long grp_stride, int G, long E, int Cb, const int32_t* theta_dst, long n_theta,
                    int L, float* out, long out_stride, hipStream_t s);
 // asr_block_mfma.hip
-int block_fwd_mfma(int mode, const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h, int N,
-                   int H, int W, int C, hipStream_t s);
+int block_fwd_mfma(int mode, const void* x, const void* resid, void* y, uint8_t* mask, const void* w,
+                   const float* bias, float h, int N, int H, int W, int C, hipStream_t s);
 int block_bwd_mfma(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
-                   float two_gamma, int N, int H, int W, int C, void* dx, float* slabs, int* nslabs, hipStream_t s);
+                   float two_gamma, int N, int H, int W, int C, void* dx, float* slabs, int* nslabs, const void* extra,
+                   int skip_dy, hipStream_t s);
 static bool mfma_supported(int C, int W) { return (C == 16 || C == 32 || C == 64) && W == 32; }
 // asr_conv_f32.hip
 int conv_f32(int fmode, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
-             float two_gamma, const float* dy, int N, int H, int W, int Ci, int Co, int out_bf16, hipStream_t s);
+             float two_gamma, const float* dy, int N, int H, int W, int Ci, int Co, int out_bf16, hipStream_t s,
+             const float* extra = nullptr);
 int make_dz(int fmode, const void* dy, const uint8_t* mask, const void* relu_src, float h, int N, int H, int W, int C,
             int src_bf16, float* dz, hipStream_t s);
 int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, int Ci, int Co, float* slabs,
@@ -62,15 +64,18 @@ static int check_shape(int N, int H, int W, int C) {
 // ---------------------------------------------------------------------------
 // conv backward workspace
 // ---------------------------------------------------------------------------
+// `stages` = conv applications whose weight-gradient slabs are reduced
+// together (1: Euler block / bare conv, 2: RK2 midpoint block).  RK2 also
+// needs the inter-stage gradient g.
 struct BwdWs {
-  size_t dz, slabs, red, total;
+  size_t dz, slabs, red, g, total;
 };
 
-static BwdWs bwd_ws_layout(int N, int H, int W, int C, int dtype) {
+static BwdWs bwd_ws_layout(int N, int H, int W, int C, int dtype, int stages = 1) {
   BwdWs b{};
   const long E = 9L * C * C;
   const long P = (long)N * H * W * C;
-  const int nsl = kMaxSlabsApi;
+  const int nsl = kMaxSlabsApi * stages;
   size_t off = 0;
   b.dz = off;
   if (dtype == ASR_F32) off += align_up((size_t)P * 4, 256);
@@ -78,8 +83,33 @@ static BwdWs bwd_ws_layout(int N, int H, int W, int C, int dtype) {
   off += align_up((size_t)nsl * (E + C) * 4, 256);
   b.red = off;
   off += align_up(reduce_ws_bytes(nsl, E + C), 256);
+  b.g = off;
+  if (stages > 1) off += align_up((size_t)P * (dtype == ASR_BF16 ? 2 : 4), 256);
   b.total = off;
   return b;
+}
+
+// One conv application's backward: dx = [dy] + extra + A^T dz and the
+// weight-gradient slabs (written at `slabs`, count in *nsl).
+//   EULER: dz = h*dy*mask; CONV: dz = dy.  skip_dy drops the +dy residual of
+//   EULER (the second RK2 stage); extra (nullable) is added to dx (the first
+//   RK2 stage adds the step's outer dy).
+static int block_backward(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
+                          float gamma, int N, int H, int W, int C, int dtype, void* dx, bool need_w, const void* extra,
+                          bool skip_dy, float* slabs, float* dz_scratch, int* nsl, hipStream_t s) {
+  *nsl = 0;
+  if (dtype == ASR_BF16) {
+    if (!dx && !need_w) return ASR_OK;
+    const int cm = (mode == ASR_MODE_EULER) ? 2 : 3;  // BWD_EULER / BWD_CONV
+    return block_bwd_mfma(cm, dy, x, mask, w, h, 2.f * gamma, N, H, W, C, dx, slabs, nsl, extra, skip_dy ? 1 : 0, s);
+  }
+  const bool euler = mode == ASR_MODE_EULER;
+  ASR_TRY(make_dz(euler ? F_EULER : F_CONV, dy, mask, nullptr, h, N, H, W, C, 0, dz_scratch, s));
+  if (dx)
+    ASR_TRY(conv_f32((euler && !skip_dy) ? B_EULER : B_CONV, dz_scratch, dx, nullptr, (const float*)w, nullptr, h,
+                     2.f * gamma, (const float*)dy, N, H, W, C, C, 0, s, (const float*)extra));
+  if (need_w) ASR_TRY(wgrad_f32(x, 0, dz_scratch, N, H, W, C, C, slabs, nsl, s));
+  return ASR_OK;
 }
 
 static int conv_backward_impl(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w,
@@ -91,19 +121,9 @@ static int conv_backward_impl(int mode, const void* dy, const void* x, const uin
   float* slabs = (float*)(base + L.slabs);
   float* red = (float*)(base + L.red);
   const bool need_w = dtheta || dbias || dw_hwio;
-  const int cm = (mode == ASR_MODE_EULER) ? 2 : 3;  // BWD_EULER / BWD_CONV
   int nsl = 0;
-  if (dtype == ASR_BF16) {
-    if (!dx && !need_w) return ASR_OK;
-    ASR_TRY(block_bwd_mfma(cm, dy, x, mask, w, h, 2.f * gamma, N, H, W, C, dx, slabs, &nsl, s));
-  } else {
-    float* dz = (float*)(base + L.dz);
-    ASR_TRY(make_dz(mode == ASR_MODE_EULER ? F_EULER : F_CONV, dy, mask, nullptr, h, N, H, W, C, 0, dz, s));
-    if (dx)
-      ASR_TRY(conv_f32(mode == ASR_MODE_EULER ? B_EULER : B_CONV, dz, dx, nullptr, (const float*)w, nullptr, h,
-                       2.f * gamma, (const float*)dy, N, H, W, C, C, 0, s));
-    if (need_w) ASR_TRY(wgrad_f32(x, 0, dz, N, H, W, C, C, slabs, &nsl, s));
-  }
+  ASR_TRY(block_backward(mode, dy, x, mask, w, h, gamma, N, H, W, C, dtype, dx, need_w || grp_defer, nullptr, false,
+                         slabs, (float*)(base + L.dz), &nsl, s));
   if (grp_defer) {  // the network defers pass 2 + projection to one launch for all layers
     if (nsl_out) *nsl_out = nsl;
     return reduce_slabs_to_groups(slabs, nsl, 9L * C * C + C, grp_defer, s);
@@ -111,6 +131,38 @@ static int conv_backward_impl(int mode, const void* dy, const void* x, const uin
   if (need_w)
     ASR_TRY(reduce_and_project(slabs, nsl, 9L * C * C, C, dtheta ? theta_dst : nullptr, n_theta, dtheta, dbias,
                                dw_hwio, red, s));
+  return ASR_OK;
+}
+
+// RK2 (explicit midpoint) block, BASELINE config 5 (an extension: the
+// reference integrates with forward Euler only, tfkeras_resnets.py:69-92):
+//   xm = x + (h/2) relu(A x + b)          (mask1 = [A x + b > 0])
+//   y  = x + h relu(A xm + b)             (mask2 = [A xm + b > 0])
+// Both stages run the Euler kernels; the second takes its residual from x.
+static int rk2_forward_impl(const void* x, void* xmid, void* y, uint8_t* mask1, uint8_t* mask2, const void* w,
+                            const float* bias, float h, int N, int H, int W, int C, int dtype, hipStream_t s) {
+  if (dtype == ASR_BF16) {
+    ASR_TRY(block_fwd_mfma(0, x, nullptr, xmid, mask1, w, bias, 0.5f * h, N, H, W, C, s));
+    return block_fwd_mfma(0, xmid, x, y, mask2, w, bias, h, N, H, W, C, s);
+  }
+  ASR_TRY(conv_f32(F_EULER, x, xmid, mask1, (const float*)w, bias, 0.5f * h, 0.f, nullptr, N, H, W, C, C, 0, s));
+  return conv_f32(F_EULER, xmid, y, mask2, (const float*)w, bias, h, 0.f, nullptr, N, H, W, C, C, 0, s,
+                  (const float*)x);
+}
+
+// Backward of rk2_forward_impl: with dz2 = h dy mask2 and g = A^T dz2 (the
+// gradient reaching xm), dz1 = (h/2) g mask1 and dx = dy + g + A^T dz1;
+// dW collects x (x) dz1 + xm (x) dz2 (both stages' slabs, reduced together).
+static int rk2_backward_slabs(const void* dy, const void* x, const void* xmid, const uint8_t* mask1,
+                              const uint8_t* mask2, const void* w, float h, float gamma, int N, int H, int W, int C,
+                              int dtype, void* dx, void* g, bool need_w, float* slabs, float* dz_scratch, int* nsl,
+                              hipStream_t s) {
+  int n2 = 0, n1 = 0;
+  ASR_TRY(block_backward(ASR_MODE_EULER, dy, xmid, mask2, w, h, gamma, N, H, W, C, dtype, g, need_w, nullptr, true,
+                         slabs, dz_scratch, &n2, s));
+  ASR_TRY(block_backward(ASR_MODE_EULER, g, x, mask1, w, 0.5f * h, gamma, N, H, W, C, dtype, dx, need_w, dy, false,
+                         slabs + (long)n2 * (9L * C * C + C), dz_scratch, &n1, s));
+  *nsl = n1 + n2;
   return ASR_OK;
 }
 
@@ -199,8 +251,12 @@ struct NetLayout {
   long ntheta, P, E, wstride;  // wstride in elements of the W dtype
   long off_c1k, off_c1b, off_blk, blk_stride, off_fck, off_fcb, nparams;
   bool sep_bwd;  // operator not antisymmetric: dgrad uses W_bwd = -flip(W)^T
+  bool rk2;      // RK2 midpoint blocks (x_mid activations, two masks per block)
+  int stages;    // conv applications per block (1 Euler, 2 RK2)
+  long grp_stride;  // floats of slab group sums per layer
   size_t grp;  // per-layer slab group sums, projected after the whole backward
-  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, x0, acts, masks, dxa, dxb, bwdws, slabs, red, probs, loss_per, dlogits, gap, total;
+  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, x0, acts, xmids, masks, dxa, dxb, dxg, bwdws, slabs, red, probs,
+      loss_per, dlogits, gap, total;
   long mask_bytes;
   int act_bytes;
   bool fast_stem;
@@ -215,6 +271,8 @@ static int net_check(const asr_net_config* c) {
   if (param_is_antisymmetric(c->param_kind, c->antisymmetric) < 0) return ASR_E_ARG;
   if (c->param_kind == ASR_PARAM_3BY3 && !c->antisymmetric)
     return fail(ASR_E_ARG, "the 3by3 parametrisation is always antisymmetric");
+  if (c->integrator != ASR_INTEGRATOR_EULER && c->integrator != ASR_INTEGRATOR_RK2)
+    return fail(ASR_E_ARG, "bad integrator %d", c->integrator);
   if (c->dtype == ASR_BF16 && !mfma_supported(c->C, c->W))
     return fail(ASR_E_UNSUPPORTED, "bf16 network needs C in {16,32,64} and W == 32 (C=%d W=%d)", c->C, c->W);
   return ASR_OK;
@@ -225,6 +283,8 @@ static NetLayout net_layout(const asr_net_config* c) {
   const int C = c->C, K = c->num_classes;
   L.ntheta = theta_count(C, c->param_kind, c->antisymmetric);
   L.sep_bwd = param_is_antisymmetric(c->param_kind, c->antisymmetric) == 0;
+  L.rk2 = c->integrator == ASR_INTEGRATOR_RK2;
+  L.stages = L.rk2 ? 2 : 1;
   L.P = (long)c->N * c->H * c->W * C;
   L.E = 9L * C * C;
   L.act_bytes = c->dtype == ASR_BF16 ? 2 : 4;
@@ -251,16 +311,19 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.wbuf_bwd = take(L.sep_bwd ? (size_t)c->L * L.wstride * L.act_bytes : 0);
   L.x0 = take(L.fast_stem ? 0 : (size_t)c->N * c->H * c->W * c->Cin * 4);
   L.acts = take((size_t)(c->L + 1) * L.P * L.act_bytes);
-  L.masks = take((size_t)c->L * L.mask_bytes);
+  L.xmids = take(L.rk2 ? (size_t)c->L * L.P * L.act_bytes : 0);
+  L.masks = take((size_t)L.stages * c->L * L.mask_bytes);  // RK2: mask1 of every block, then mask2
   L.dxa = take((size_t)L.P * L.act_bytes);
   L.dxb = take((size_t)L.P * L.act_bytes);
+  L.dxg = take(L.rk2 ? (size_t)L.P * L.act_bytes : 0);
   // per-block backward workspace (asr_conv_backward layout), reused by the stem
-  const BwdWs bw = bwd_ws_layout(c->N, c->H, c->W, C, c->dtype);
+  const BwdWs bw = bwd_ws_layout(c->N, c->H, c->W, C, c->dtype, L.stages);
   const long E1 = 9L * c->Cin * C;
   const size_t stem_ws = align_up((size_t)L.P * 4, 256) + align_up((size_t)kMaxSlabsApi * (E1 + C) * 4, 256) +
                          align_up(reduce_ws_bytes(kMaxSlabsApi, E1 + C), 256);
   L.bwdws = take(std::max(bw.total, stem_ws));
-  L.grp = take((size_t)c->L * reduce_groups(kMaxSlabsApi) * (L.E + C) * 4);
+  L.grp_stride = (long)reduce_groups(L.stages * kMaxSlabsApi) * (L.E + C);
+  L.grp = take((size_t)c->L * L.grp_stride * 4);
   L.probs = take((size_t)c->N * K * 4);
   L.loss_per = take((size_t)c->N * 4);
   L.dlogits = take((size_t)c->N * K * 4);
@@ -303,16 +366,21 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
     ASR_TRY(conv_f32(F_RELU, x0, act(0), nullptr, params + L.off_c1k, params + L.off_c1b, 1.f, 0.f, nullptr, N, H,
                      W, c->Cin, C, bf ? 1 : 0, s));
   }
-  // 3. L Euler blocks (tfkeras_resnets.py:579-582 -> :28-94)
+  // 3. L Euler blocks (tfkeras_resnets.py:579-582 -> :28-94), or RK2 blocks
   for (int l = 0; l < c->L; ++l) {
     const float* bias = params + L.off_blk + (long)l * L.blk_stride + L.ntheta;
     const unsigned char* wl = ws + L.wbuf + (size_t)l * L.wstride * L.act_bytes;
     uint8_t* mask = training ? (uint8_t*)(ws + L.masks) + (size_t)l * L.mask_bytes : nullptr;
-    if (bf)
-      ASR_TRY(block_fwd_mfma(0, act(l), act(l + 1), mask, wl, bias, c->h, N, H, W, C, s));
-    else
+    if (L.rk2) {
+      unsigned char* xm = ws + L.xmids + (training ? (size_t)l * L.P * L.act_bytes : 0);
+      uint8_t* mask2 = training ? mask + (size_t)c->L * L.mask_bytes : nullptr;
+      ASR_TRY(rk2_forward_impl(act(l), xm, act(l + 1), mask, mask2, wl, bias, c->h, N, H, W, C, c->dtype, s));
+    } else if (bf) {
+      ASR_TRY(block_fwd_mfma(0, act(l), nullptr, act(l + 1), mask, wl, bias, c->h, N, H, W, C, s));
+    } else {
       ASR_TRY(conv_f32(F_EULER, act(l), act(l + 1), mask, (const float*)wl, bias, c->h, 0.f, nullptr, N, H, W, C, C,
                        0, s));
+    }
   }
   return ASR_OK;
 }
@@ -337,7 +405,7 @@ int asr_conv_forward(int mode, const void* x, void* y, uint8_t* mask, const void
   if (dtype == ASR_BF16) {
     if (!mfma_supported(C, W))
       return fail(ASR_E_UNSUPPORTED, "bf16 conv needs C in {16,32,64} and W == 32 (C=%d W=%d)", C, W);
-    return block_fwd_mfma(mode == ASR_MODE_EULER ? 0 : 1, x, y, mask, w, bias, h, N, H, W, C, s);
+    return block_fwd_mfma(mode == ASR_MODE_EULER ? 0 : 1, x, nullptr, y, mask, w, bias, h, N, H, W, C, s);
   }
   if (dtype == ASR_F32)
     return conv_f32(mode == ASR_MODE_EULER ? F_EULER : F_CONV, x, y, mask, (const float*)w, bias, h, 0.f, nullptr, N,
@@ -366,6 +434,49 @@ int asr_conv_backward(int mode, const void* dy, const void* x, const uint8_t* ma
     return fail(ASR_E_WORKSPACE, "asr_conv_backward: workspace too small");
   return conv_backward_impl(mode, dy, x, mask, w, theta_dst, n_theta, h, gamma, N, H, W, C, dtype, dx, dtheta, dbias,
                             dw_hwio, ws, (hipStream_t)stream);
+}
+
+static int check_block_args(const char* fn, int N, int H, int W, int C, int dtype) {
+  ASR_TRY(check_shape(N, H, W, C));
+  if (dtype != ASR_F32 && dtype != ASR_BF16) return fail(ASR_E_ARG, "%s: bad dtype %d", fn, dtype);
+  if (dtype == ASR_BF16 && !mfma_supported(C, W))
+    return fail(ASR_E_UNSUPPORTED, "%s: bf16 needs C in {16,32,64} and W == 32 (C=%d W=%d)", fn, C, W);
+  return ASR_OK;
+}
+
+int asr_rk2_forward(const void* x, void* xmid, void* y, uint8_t* mask1, uint8_t* mask2, const void* w,
+                    const float* bias, float h, int N, int H, int W, int C, int dtype, asr_stream_t stream) {
+  ASR_TRY(check_block_args("asr_rk2_forward", N, H, W, C, dtype));
+  if (!x || !xmid || !y || !w) return fail(ASR_E_ARG, "asr_rk2_forward: null pointer");
+  if (x == xmid || x == y || xmid == y) return fail(ASR_E_ARG, "asr_rk2_forward: x, xmid and y must not alias");
+  return rk2_forward_impl(x, xmid, y, mask1, mask2, w, bias, h, N, H, W, C, dtype, (hipStream_t)stream);
+}
+
+size_t asr_rk2_backward_workspace_bytes(int N, int H, int W, int C, int dtype) {
+  if (check_shape(N, H, W, C) != ASR_OK) return 0;
+  return bwd_ws_layout(N, H, W, C, dtype, 2).total;
+}
+
+int asr_rk2_backward(const void* dy, const void* x, const void* xmid, const uint8_t* mask1, const uint8_t* mask2,
+                     const void* w, const int32_t* theta_dst, long n_theta, float h, float gamma, int N, int H, int W,
+                     int C, int dtype, void* dx, float* dtheta, float* dbias, float* dw_hwio, void* ws,
+                     size_t ws_bytes, asr_stream_t stream) {
+  ASR_TRY(check_block_args("asr_rk2_backward", N, H, W, C, dtype));
+  if (!dy || !x || !xmid || !mask1 || !mask2 || !w) return fail(ASR_E_ARG, "asr_rk2_backward: null pointer");
+  if (dtheta && !theta_dst) return fail(ASR_E_ARG, "asr_rk2_backward: theta_dst needed for dtheta");
+  const BwdWs L = bwd_ws_layout(N, H, W, C, dtype, 2);
+  if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_rk2_backward: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  unsigned char* base = (unsigned char*)ws;
+  float* slabs = (float*)(base + L.slabs);
+  const bool need_w = dtheta || dbias || dw_hwio;
+  int nsl = 0;
+  ASR_TRY(rk2_backward_slabs(dy, x, xmid, mask1, mask2, w, h, gamma, N, H, W, C, dtype, dx, base + L.g, need_w, slabs,
+                             (float*)(base + L.dz), &nsl, s));
+  if (need_w)
+    ASR_TRY(reduce_and_project(slabs, nsl, 9L * C * C, C, dtheta ? theta_dst : nullptr, n_theta, dtheta, dbias,
+                               dw_hwio, (float*)(base + L.red), s));
+  return ASR_OK;
 }
 
 long asr_net_param_count(const asr_net_config* cfg) {
@@ -432,23 +543,32 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
                (float*)(b + L.loss_per), (float*)(b + L.dlogits), (float*)(b + L.gap), dcur, s));
   ASR_TRY(head_param_grads((const float*)(b + L.gap), (const float*)(b + L.dlogits), N, C, K, grads + L.off_fck,
                            grads + L.off_fcb, (const float*)(b + L.loss_per), loss, s));
-  // Euler blocks, last to first
+  // blocks, last to first
   const int32_t* theta_dst = (const int32_t*)(b + L.theta_dst);
   int nsl_blk = 0;
+  const BwdWs bw = bwd_ws_layout(N, H, W, C, cfg->dtype, L.stages);
   for (int l = cfg->L - 1; l >= 0; --l) {
     const unsigned char* wl = b + (L.sep_bwd ? L.wbuf_bwd : L.wbuf) + (size_t)l * L.wstride * L.act_bytes;
     const uint8_t* mask = (const uint8_t*)(b + L.masks) + (size_t)l * L.mask_bytes;
-    float* dth = grads + L.off_blk + (long)l * L.blk_stride;
-    float* grp_l = (float*)(b + L.grp) + (size_t)l * reduce_groups(kMaxSlabsApi) * (L.E + C);
-    ASR_TRY(conv_backward_impl(ASR_MODE_EULER, dcur, act(l), mask, wl, theta_dst, L.ntheta, cfg->h,
-                               L.sep_bwd ? 0.f : cfg->gamma, N, H, W, C, cfg->dtype, dnext, dth, dth + L.ntheta,
-                               nullptr, b + L.bwdws, s, grp_l, &nsl_blk));
+    const float gam = L.sep_bwd ? 0.f : cfg->gamma;
+    float* grp_l = (float*)(b + L.grp) + (size_t)l * L.grp_stride;
+    if (L.rk2) {
+      float* slabs = (float*)(b + L.bwdws + bw.slabs);
+      const unsigned char* xm = b + L.xmids + (size_t)l * L.P * L.act_bytes;
+      ASR_TRY(rk2_backward_slabs(dcur, act(l), xm, mask, mask + (size_t)cfg->L * L.mask_bytes, wl, cfg->h, gam, N, H,
+                                 W, C, cfg->dtype, dnext, b + L.dxg, true, slabs, (float*)(b + L.bwdws + bw.dz),
+                                 &nsl_blk, s));
+      ASR_TRY(reduce_slabs_to_groups(slabs, nsl_blk, L.E + C, grp_l, s));
+    } else {
+      float* dth = grads + L.off_blk + (long)l * L.blk_stride;
+      ASR_TRY(conv_backward_impl(ASR_MODE_EULER, dcur, act(l), mask, wl, theta_dst, L.ntheta, cfg->h, gam, N, H, W,
+                                 C, cfg->dtype, dnext, dth, dth + L.ntheta, nullptr, b + L.bwdws, s, grp_l, &nsl_blk));
+    }
     std::swap(dcur, dnext);
   }
   // pass 2 of every block's weight-gradient reduction + projection onto theta, one launch
-  ASR_TRY(project_layers((float*)(b + L.grp), (long)reduce_groups(kMaxSlabsApi) * (L.E + C),
-                         reduce_groups(nsl_blk), L.E, C, theta_dst, L.ntheta, cfg->L, grads + L.off_blk, L.blk_stride,
-                         s));
+  ASR_TRY(project_layers((float*)(b + L.grp), L.grp_stride, reduce_groups(nsl_blk), L.E, C, theta_dst, L.ntheta,
+                         cfg->L, grads + L.off_blk, L.blk_stride, s));
   // stem: dz1 = dx1 * [x1 > 0]; conv1 weight/bias gradient from the normalised input
   const long E1 = 9L * cfg->Cin * C;
   unsigned char* sw = b + L.bwdws;

@@ -233,6 +233,28 @@ __device__ __forceinline__ void lds_wr128(unsigned addr, u32x4 v) {
   asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
 }
 
+// Wait until at most n of this wave's vector-memory ops are outstanding
+// (vmcnt retires in issue order): used for LDS-DMA'd data the compiler does
+// not track.  n above 24 waits for more than needed, which stays correct.
+__device__ __forceinline__ void vm_wait(int n) {
+#define ASR_VMW(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+  switch (n) {
+    ASR_VMW(1) ASR_VMW(2) ASR_VMW(3) ASR_VMW(4) ASR_VMW(5) ASR_VMW(6) ASR_VMW(7) ASR_VMW(8)
+    ASR_VMW(9) ASR_VMW(10) ASR_VMW(11) ASR_VMW(12) ASR_VMW(13) ASR_VMW(14) ASR_VMW(15) ASR_VMW(16)
+    ASR_VMW(17) ASR_VMW(18) ASR_VMW(19) ASR_VMW(20) ASR_VMW(21) ASR_VMW(22) ASR_VMW(23) ASR_VMW(24)
+    default:
+      if (n > 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // waits for more: still correct
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      break;
+  }
+#undef ASR_VMW
+}
+// instructions one wave issues in a `for (j = wave; j < total; j += nw)` loop
+__device__ __forceinline__ int strided_count(int total, int wave, int nw) {
+  return total > wave ? (total - wave + nw - 1) / nw : 0;
+}
+
 template <int C, int W, int ks>
 __device__ __forceinline__ void conv_issue(const unsigned (&ra)[Frag<C, W>::NB], bf16x8 (&B)[W / 16]) {
   if constexpr (W / 16 >= 1) B[0] = ds_read128<Frag<C, W>::template imm<ks, 0>()>(ra[Frag<C, W>::template slot<ks>()]);
@@ -416,9 +438,10 @@ struct ItemCursor {
 // forward
 // ===========================================================================
 template <int C, int W, int BR, int MODE, int NW>
-__global__ __launch_bounds__(64 * NW) void k_fwd(const bf16* __restrict__ x, bf16* __restrict__ y,
-                                             uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
-                                             const float* __restrict__ bias, float h, int N, int H) {
+__global__ __launch_bounds__(64 * NW) void k_fwd(const bf16* __restrict__ x, const bf16* __restrict__ resid,
+                                             bf16* __restrict__ y, uint8_t* __restrict__ mask,
+                                             const bf16* __restrict__ wpack, const float* __restrict__ bias,
+                                             float h, int N, int H) {
   using G = Geo<C>;
   constexpr int TW = W + 2, PT = W / 16, NQ = G::NQ, OTW = G::OTW;
   constexpr int TILE = (BR + 2) * TW * NQ * 16;
@@ -494,7 +517,9 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(const bf16* __restrict__ x, bf1
           const int o0 = 16 * (oh * OTW + t) + 4 * g;
           bf16x4 o4;
           if constexpr (EULER) {
-            const bf16x4 xr = *(const bf16x4*)(tile + toff<C>(r + 1, px + 1, o0 >> 3, TW) + (o0 & 4) * 2);
+            // residual: x itself (LDS tile) or, for the second RK2 stage, the step's input
+            const bf16x4 xr = resid ? *(const bf16x4*)(resid + (((long)n * H + gy) * W + px) * C + o0)
+                                    : *(const bf16x4*)(tile + toff<C>(r + 1, px + 1, o0 >> 3, TW) + (o0 & 4) * 2);
             unsigned nib = 0;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -531,9 +556,10 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(const bf16* __restrict__ x, bf1
 
 // Forward, band form (C >= 32): wave = (o-tile ot, row group rg); RB rows.
 template <int C, int W, int BR, int MODE, int NW>
-__global__ __launch_bounds__(64 * NW) void k_fwd_band(const bf16* __restrict__ x, bf16* __restrict__ y,
-                                                  uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
-                                                  const float* __restrict__ bias, float h, int N, int H) {
+__global__ __launch_bounds__(64 * NW) void k_fwd_band(const bf16* __restrict__ x, const bf16* __restrict__ resid,
+                                                  bf16* __restrict__ y, uint8_t* __restrict__ mask,
+                                                  const bf16* __restrict__ wpack, const float* __restrict__ bias,
+                                                  float h, int N, int H) {
   using G = Geo<C>;
   constexpr int TW = W + 2, PT = W / 16, NQ = G::NQ, OT = C / 16;
   constexpr int TILE = (BR + 2) * TW * NQ * 16;
@@ -601,7 +627,8 @@ __global__ __launch_bounds__(64 * NW) void k_fwd_band(const bf16* __restrict__ x
       for (int r = 0; r < RB; ++r)
 #pragma unroll
         for (int pt = 0; pt < PT; ++pt)
-          xr2[r][pt] = lds_rd64(lds_u32(tile + toff<C>(r0 + r + 1, 16 * pt + lx + 1, o0 >> 3, TW) + (o0 & 4) * 2));
+          xr2[r][pt] = resid ? *(const u32x2*)(resid + (((long)n * H + y0 + min(r0 + r, rows - 1)) * W + 16 * pt + lx) * C + o0)
+                             : lds_rd64(lds_u32(tile + toff<C>(r0 + r + 1, 16 * pt + lx + 1, o0 >> 3, TW) + (o0 & 4) * 2));
       lgkm_wait<0>();
     }
     // wave-uniform row bases + one 32-bit lane offset: stores need no 64-bit math
@@ -658,10 +685,11 @@ __device__ __forceinline__ void epi_all_units(F& f, const Acc& acc, const Xr& xr
 // Forward, band form with a software pipeline across bands: the MFMAs of
 // band i+1 are interleaved with the epilogue (VALU + stores) of band i, so
 // the matrix pipe and the vector ALU of one wave work at the same time.
-template <int C, int W, int BR, int MODE, int NW>
-__global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict__ x, bf16* __restrict__ y,
-                                                  uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
-                                                  const float* __restrict__ bias, float h, int N, int H) {
+template <int C, int W, int BR, int MODE, int NW, bool RES>
+__global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict__ x, const bf16* __restrict__ resid,
+                                                  bf16* __restrict__ y, uint8_t* __restrict__ mask,
+                                                  const bf16* __restrict__ wpack, const float* __restrict__ bias,
+                                                  float h, int N, int H) {
   using G = Geo<C>;
   constexpr int TW = W + 2, PT = W / 16, NQ = G::NQ, OT = C / 16;
   constexpr int TILE = (BR + 2) * TW * NQ * 16;
@@ -703,13 +731,45 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
     const int yy = c.b * BR;
     dma_rows<C, W>(x, lds + buf * TILE, c.n, yy - 1, min(BR, H - yy) + 2, H, wave, NW, lane);
   };
+  int nst = 0;  // vector-memory ops this wave issued after the DMA the next barrier waits for
+  // residual of a band: x from its LDS tile (read after the band's conv)
   auto xres_read = [&](int buf, u32x2 (&xr)[RB][PT]) {
-    if constexpr (EULER) {
+    if constexpr (EULER && !RES) {
       const unsigned tb = lds_u32(lds + buf * TILE) + lxr;
 #pragma unroll
       for (int r = 0; r < RB; ++r)
 #pragma unroll
         for (int pt = 0; pt < PT; ++pt) xr[r][pt] = lds_rd64(tb + (unsigned)(r * BD::ROWB + pt * BD::PTB));
+      lgkm_wait<0>();
+    }
+  };
+  // RES (second RK2 stage): the residual is the step input `resid`.  Each
+  // wave DMAs exactly its RB rows x W pixels x 16 channels into a private
+  // double buffer (1 KiB per row, 16-B chunks XOR-swizzled by pixel bit 3 so
+  // the epilogue's 8-B reads are conflict-free), one band ahead, BEFORE the
+  // next x tile's DMA: the barrier that waits for that tile also covers it.
+  static_assert(!RES || W * 32 == 1024, "private residual rows are one 1 KiB DMA each");
+  constexpr int PRB = RB * 1024;
+  unsigned char* priv = lds + 2 * TILE + wave * 2 * PRB;
+  auto dma_res = [&](const ItemCursor& c, int pb) {
+    if constexpr (RES) {
+      const int y0 = c.b * BR, rows = min(BR, H - y0);
+      const int px = lane >> 1, ch = 16 * ot + 8 * ((lane & 1) ^ ((px >> 3) & 1));
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const void* src = (r0 + r < rows) ? (const void*)(resid + (((long)c.n * H + y0 + r0 + r) * W + px) * C + ch)
+                                          : (const void*)(g_zero_page + lane);
+        dma16(src, priv + pb * PRB + r * 1024);
+      }
+    }
+  };
+  auto res_read = [&](int pb, u32x2 (&xr)[RB][PT]) {
+    if constexpr (RES) {
+      const unsigned b = lds_u32(priv + pb * PRB) + (unsigned)(lx * 32 + (((g >> 1) ^ (lx >> 3)) * 16) + (g & 1) * 8);
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt) xr[r][pt] = lds_rd64(b + (unsigned)(r * 1024 + pt * 512));
       lgkm_wait<0>();
     }
   };
@@ -719,7 +779,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
 #pragma unroll
       for (int pt = 0; pt < PT; ++pt) acc[r][pt] = f32x4{bz[0], bz[1], bz[2], bz[3]};
   };
-  int nst = 0;
   // one epilogue unit (row r, pixel tile pt) of the band at cursor c
   auto epi_unit = [&](auto U, const f32x4 (&acc)[RB][PT], const u32x2 (&xr)[RB][PT], const ItemCursor& c) {
     constexpr int u = decltype(U)::value, r = u / PT, pt = u % PT;
@@ -759,6 +818,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
   u32x2 xrA[RB][PT], xrB[RB][PT];
   // prologue: band i0 computed (its epilogue waits for the next band's MFMAs)
   dma(cur, 0);
+  dma_res(cur, 0);
   barrier_vm(0);
   if (i0 + 1 < i1) dma(nx1, 1);
   init(accA);
@@ -768,12 +828,18 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
   while (true) {
     // accA / xrA: band it.  In flight: DMA of band it+1 into buffer (it+1-i0)&1.
     if (it + 1 >= i1) {
+      if constexpr (RES) {
+        vm_wait(0);  // this wave's residual rows of band it (private: no barrier needed)
+        res_read((it - i0) & 1, xrA);
+      }
       epi_all(accA, xrA, cur);
       break;
     }
     barrier_vm(nst);  // band it+1 landed, every wave is done with band it's tile
     nst = 0;
+    dma_res(nx1, (it + 1 - i0) & 1);
     if (it + 2 < i1) dma(nx2, (it - i0) & 1);
+    res_read((it - i0) & 1, xrA);
     init(accB);
     {
       const ItemCursor c = cur;
@@ -787,12 +853,18 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
     nx2.next(nb);
     // the same with the roles of A and B swapped
     if (it + 1 >= i1) {
+      if constexpr (RES) {
+        vm_wait(0);
+        res_read((it - i0) & 1, xrB);
+      }
       epi_all(accB, xrB, cur);
       break;
     }
     barrier_vm(nst);
     nst = 0;
+    dma_res(nx1, (it + 1 - i0) & 1);
     if (it + 2 < i1) dma(nx2, (it - i0) & 1);
+    res_read((it - i0) & 1, xrB);
     init(accA);
     {
       const ItemCursor c = cur;
@@ -828,7 +900,42 @@ struct BwdLds {
   static constexpr int DZ = X + 2 * TILE;      // 1 x TILE (dz, halo rows)
   static constexpr int MSK = DZ + TILE;        // 2 x MTB
   static constexpr int TOTAL = MSK + 2 * MTB;
+  // XT (RK2 first stage): per dgrad wave, a private copy of the extra dx
+  // term for its MR rows x W pixels x its OTW o-tiles (NCH 16-B chunks/pixel)
+  static constexpr int RS = 4 / Geo<C>::OSPLIT, MR = (BR + RS - 1) / RS;
+  static constexpr int NCH = 2 * Geo<C>::OTW;
+  static constexpr int ROWX = W * NCH * 16;    // bytes per private row
+  static constexpr int EXT = TOTAL;            // 4 x MR x ROWX
+  static constexpr int TOTAL_XT = EXT + 4 * MR * ROWX;
+  static_assert(ROWX % 1024 == 0, "private extra rows are whole 1 KiB DMAs");
 };
+
+// DMA the extra dx term of one dgrad wave's rows (rg + k*RS) of the band at
+// image row y0, its channels [16*OTW*oh, +16*OTW), into the wave's private
+// rows: 16-B chunk j of pixel px sits in slot j ^ ((px / PXG) % NCH), PXG =
+// the pixels one 64-bank span holds, so the epilogue's 8-B reads do not
+// conflict.  Rows outside the band read the zero page.  Issues MR*ROWX/1024
+// instructions.
+template <int C, int W, int BR>
+__device__ __forceinline__ void dma_extra(const bf16* __restrict__ extra, unsigned char* priv, int n, int y0, int rows,
+                                          int H, int rg, int oh, int lane) {
+  using L = BwdLds<C, W, BR>;
+  constexpr int NCH = L::NCH, PXG = 64 / (NCH * 4);
+#pragma unroll
+  for (int k = 0; k < L::MR; ++k) {
+    const int r = rg + k * L::RS;
+#pragma unroll
+    for (int q = 0; q < L::ROWX / 1024; ++q) {
+      const int lb = q * 1024 + lane * 16;
+      const int px = lb / (NCH * 16), slot = (lb / 16) % NCH;
+      const int chunk = slot ^ ((px / PXG) % NCH);
+      const void* src = (r < rows) ? (const void*)(extra + (((long)n * H + y0 + r) * W + px) * C +
+                                                   16 * Geo<C>::OTW * oh + 8 * chunk)
+                                   : (const void*)(g_zero_page + lane);
+      dma16(src, priv + k * L::ROWX + q * 1024);
+    }
+  }
+}
 
 template <int C, int W, int BR, bool EULER>
 __device__ __forceinline__ void bwd_issue(const bf16* dy, const bf16* x, const uint8_t* mask, unsigned char* lds,
@@ -891,17 +998,22 @@ __device__ __forceinline__ void bwd_convert(unsigned char* lds, int buf, int nr,
   }
 }
 
-template <int C, int W, int BR, int MODE>
+template <int C, int W, int BR, int MODE, bool XT>
 __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                              const uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
                                              float h, float two_gamma, int N, int H, bf16* __restrict__ dx,
-                                             float* __restrict__ slabs) {
+                                             float* __restrict__ slabs, const bf16* __restrict__ extra,
+                                             int skip_dy) {
   using G = Geo<C>;
   using L = BwdLds<C, W, BR>;
   constexpr int TW = W + 2, PT = W / 16, NQ = G::NQ, OTW = G::OTW, OT = G::OT, MTW = G::MTW;
   constexpr int KPR = W / 32;
   constexpr bool EULER = MODE == BWD_EULER;
   static_assert(W % 32 == 0, "wgrad k-steps are 32 pixels of one row");
+  // XT: the RK2 variant (extra dx term and/or no +dy residual); compiled out
+  // of the Euler block's kernel
+  const bool has_extra = XT && extra != nullptr;
+  const bool no_dy = XT && skip_dy != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, lx = lane & 15;
@@ -935,6 +1047,18 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
 #pragma unroll
       for (int e = 0; e < 4; ++e) dbacc[t][e] = 0.f;
     int nst = 0;
+    // the extra dx term (RK2: the outer dy of the first stage): each dgrad
+    // wave DMAs the rows it needs into its private LDS rows after its last
+    // epilogue of the previous band (prologue: before the loop), so it is
+    // older than the next band's prefetch and vm_wait(nd) covers it
+    using LX = BwdLds<C, W, BR>;
+    constexpr int MR = LX::MR, NEX = MR * LX::ROWX / 1024;
+    unsigned char* priv = lds + LX::EXT + wave * MR * LX::ROWX;
+    if (has_extra && i0 < i1) {
+      const ItemCursor c0(i0, nb);
+      dma_extra<C, W, BR>(extra, priv, c0.n, c0.b * BR, min(BR, H - c0.b * BR), H, rg, oh, lane);
+      nst = NEX;
+    }
     ItemCursor cur(i0, nb), nxt(i0, nb);
     nxt.next(nb);
     for (int it = i0; it < i1; ++it, cur.next(nb), nxt.next(nb)) {
@@ -943,12 +1067,22 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
       const int rows = min(BR, H - y0);
       barrier_vm(nst);  // item's DMA landed; previous item fully consumed
       nst = 0;
-      if (it + 1 < i1) bwd_issue<C, W, BR, EULER>(dy, x, mask, lds, buf ^ 1, nxt.n, nxt.b * BR, H, wave, lane, 4);
+      int nd = 0;  // DMA instructions this wave issues below
+      if (it + 1 < i1) {
+        bwd_issue<C, W, BR, EULER>(dy, x, mask, lds, buf ^ 1, nxt.n, nxt.b * BR, H, wave, lane, 4);
+        const int nr = min(BR, H - nxt.b * BR) + 2;
+        nd = 2 * strided_count(nr * (W / G::PPI), wave, 4);
+        if (EULER) nd += strided_count((nr * (W * C / 8) + 1023) / 1024, wave, 4);
+      }
+      bool ex_wait = has_extra;
       if (ASR_ABLATE != 4) bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, tid, 512);
       barrier_lds();  // dz ready
       const unsigned char* dzt = lds + L::DZ;
       const unsigned char* dyt = lds + L::DY + buf * L::TILE;
-      for (int r = rg; r < rows; r += RS) {
+#pragma unroll
+      for (int k = 0; k < MR; ++k) {
+        const int r = rg + k * RS;
+        if (r >= rows) break;
         f32x4 acc[OTW][PT];
 #pragma unroll
         for (int t = 0; t < OTW; ++t)
@@ -979,9 +1113,13 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
             const int px = 16 * pt + lx, o0 = 16 * (oh * OTW + t) + 4 * g;
             const int co = toff<C>(r + 1, px + 1, o0 >> 3, TW) + (o0 & 4) * 2;
             dzv[pt][t] = lds_rd64(lds_u32(dzt + co));
-            if constexpr (EULER) dyv[pt][t] = lds_rd64(lds_u32(dyt + co));
+            if (EULER && !no_dy) dyv[pt][t] = lds_rd64(lds_u32(dyt + co));
           }
         lgkm_wait<0>();
+        if (ex_wait) {
+          vm_wait(nd);  // this wave's private extra rows (older than the next band's prefetch)
+          ex_wait = false;
+        }
 #pragma unroll
         for (int pt = 0; pt < PT; ++pt) {
           const int px = 16 * pt + lx;
@@ -995,21 +1133,42 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
               dzf[e] = (float)dzr[e];
               dbacc[t][e] += dzf[e];
             }
-            bf16x4 o4;
-            if constexpr (EULER) {
+            // residual terms: dy (unless skip_dy) + extra
+            float res[4] = {0.f, 0.f, 0.f, 0.f};
+            if (EULER && !no_dy) {
               const bf16x4 dyr = *(const bf16x4*)&dyv[pt][t];
 #pragma unroll
+              for (int e = 0; e < 4; ++e) res[e] = (float)dyr[e];
+            }
+            if (has_extra) {
+              constexpr int PXG = 64 / (LX::NCH * 4);
+              const int px = 16 * pt + lx;
+              const unsigned a = lds_u32(priv + k * LX::ROWX + px * LX::NCH * 16 +
+                                         (((2 * t + (g >> 1)) ^ ((px / PXG) % LX::NCH)) * 16) + (g & 1) * 8);
+              u32x2 ev = lds_rd64(a);
+              lgkm_wait<0>();
+              const bf16x4 exr = *(const bf16x4*)&ev;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) res[e] += (float)exr[e];
+            }
+            bf16x4 o4;
+            if constexpr (EULER) {
+#pragma unroll
               for (int e = 0; e < 4; ++e) {
-                const float v = fmaf(-hs, acc[t][pt][e], (float)dyr[e]);
+                const float v = fmaf(-hs, acc[t][pt][e], res[e]);
                 o4[e] = (bf16)(hs2g != 0.f ? fmaf(hs2g, dzf[e], v) : v);
               }
             } else {
 #pragma unroll
-              for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(two_gamma, dzf[e], -acc[t][pt][e]);
+              for (int e = 0; e < 4; ++e) o4[e] = (bf16)(fmaf(two_gamma, dzf[e], -acc[t][pt][e]) + res[e]);
             }
             if (dx) *(bf16x4*)(dx + (((long)n * H + gy) * W + px) * C + o0) = o4;
           }
         }
+      }
+      if (has_extra && it + 1 < i1) {  // next band's extra rows into the (now read) private rows
+        dma_extra<C, W, BR>(extra, priv, nxt.n, nxt.b * BR, min(BR, H - nxt.b * BR), H, rg, oh, lane);
+        nst += NEX;
       }
     }
     // reduce db over the 16 pixel lanes, then over the row-group waves (LDS)
@@ -1146,9 +1305,27 @@ static int persistent_grid(long items) {
   return (int)std::max<long>(1, std::min<long>({items, (long)cus, (long)kMaxBlockSlabs}));
 }
 
+// second RK2 stage (residual from `resid`): 8-row bands, 8 waves, one WG per
+// CU (the private residual buffers need the LDS of two 4-wave WGs)
+template <int C, int W>
+static int launch_fwd_res(const void* x, const void* resid, void* y, uint8_t* mask, const void* w, const float* bias,
+                          float h, int N, int H, hipStream_t s) {
+  constexpr int BR = 8, NW = 8, RB = BR / (NW / (C / 16));
+  const long items = (long)N * ((H + BR - 1) / BR);
+  if (items > 0x7fffffffL) return fail(ASR_E_UNSUPPORTED, "bf16 block: too many row bands (%ld)", items);
+  int cus = cu_count();
+  if (cus <= 0) cus = 256;
+  const int grid = (int)std::max<long>(1, std::min<long>(items, (long)cus));
+  const size_t lds = 2 * (size_t)(BR + 2) * (W + 2) * C * 2 + (size_t)NW * 2 * RB * 1024;
+  hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_EULER, NW, true>), dim3(grid), dim3(64 * NW), lds, s,
+                     (const bf16*)x, (const bf16*)resid, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+  ASR_LAUNCH_CHECK("k_fwd_pipe(res)");
+  return ASR_OK;
+}
+
 template <int C, int W, int BR, int NW>
-static int launch_fwd_v(int mode, const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h,
-                        int N, int H, hipStream_t s) {
+static int launch_fwd_v(int mode, const void* x, const void* resid, void* y, uint8_t* mask, const void* w,
+                        const float* bias, float h, int N, int H, hipStream_t s) {
   static_assert(NW % blk::Geo<C>::OSPLIT == 0, "waves must cover the o-split");
   const long items = (long)N * ((H + BR - 1) / BR);
   if (items > 0x7fffffffL) return fail(ASR_E_UNSUPPORTED, "bf16 block: too many row bands (%ld)", items);
@@ -1161,85 +1338,89 @@ static int launch_fwd_v(int mode, const void* x, void* y, uint8_t* mask, const v
     if (no_pipe) {
       if (mode == blk::FWD_EULER)
         hipLaunchKernelGGL((blk::k_fwd_band<C, W, BR, blk::FWD_EULER, NW>), dim3(grid), dim3(64 * NW), lds, s,
-                           (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+                           (const bf16*)x, (const bf16*)resid, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
       else
         hipLaunchKernelGGL((blk::k_fwd_band<C, W, BR, blk::FWD_CONV, NW>), dim3(grid), dim3(64 * NW), lds, s,
-                           (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+                           (const bf16*)x, (const bf16*)resid, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
     } else {
+      if (mode == blk::FWD_EULER && resid)
+        return launch_fwd_res<C, W>(x, resid, y, mask, w, bias, h, N, H, s);
       if (mode == blk::FWD_EULER)
-        hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_EULER, NW>), dim3(grid), dim3(64 * NW), lds, s,
-                           (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+        hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_EULER, NW, false>), dim3(grid), dim3(64 * NW), lds, s,
+                           (const bf16*)x, nullptr, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
       else
-        hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_CONV, NW>), dim3(grid), dim3(64 * NW), lds, s,
-                           (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+        hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_CONV, NW, false>), dim3(grid), dim3(64 * NW), lds, s,
+                           (const bf16*)x, nullptr, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
     }
   } else {
     if (mode == blk::FWD_EULER)
       hipLaunchKernelGGL((blk::k_fwd<C, W, BR, blk::FWD_EULER, NW>), dim3(grid), dim3(64 * NW), lds, s,
-                         (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+                         (const bf16*)x, (const bf16*)resid, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
     else
       hipLaunchKernelGGL((blk::k_fwd<C, W, BR, blk::FWD_CONV, NW>), dim3(grid), dim3(64 * NW), lds, s,
-                         (const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+                         (const bf16*)x, (const bf16*)resid, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
   }
   ASR_LAUNCH_CHECK("k_fwd");
   return ASR_OK;
 }
 
 template <int C, int W>
-static int launch_fwd(int mode, const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h,
-                      int N, int H, hipStream_t s) {
-  static const int variant = [] {
-    const char* e = getenv("ASR_FWD_VARIANT");  // development: A/B of the workgroup geometry
-    return e ? atoi(e) : 1;
-  }();
-  switch (variant) {
-    case 0: return launch_fwd_v<C, W, 8, 8>(mode, x, y, mask, w, bias, h, N, H, s);
-    case 2:
-      if constexpr (C >= 32) return launch_fwd_v<C, W, 4, 8>(mode, x, y, mask, w, bias, h, N, H, s);
-      else return launch_fwd_v<C, W, 2, 2>(mode, x, y, mask, w, bias, h, N, H, s);
-    case 3: return launch_fwd_v<C, W, 8, 4>(mode, x, y, mask, w, bias, h, N, H, s);
-    default: return launch_fwd_v<C, W, 4, 4>(mode, x, y, mask, w, bias, h, N, H, s);
-  }
+static int launch_fwd(int mode, const void* x, const void* resid, void* y, uint8_t* mask, const void* w,
+                      const float* bias, float h, int N, int H, hipStream_t s) {
+  // 4-row bands, 4 waves (one 16-channel o-tile each at C=64), 2 WGs per CU
+  // (geometry chosen by A/B on MI355X against 8x8, 4x8 and 8x4)
+  return launch_fwd_v<C, W, 4, 4>(mode, x, resid, y, mask, w, bias, h, N, H, s);
 }
 
 template <int C, int W>
 static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
-                      float two_gamma, int N, int H, void* dx, float* slabs, int* nslabs, hipStream_t s) {
+                      float two_gamma, int N, int H, void* dx, float* slabs, int* nslabs, const void* extra,
+                      int skip_dy, hipStream_t s) {
   const long items = (long)N * ((H + kBwdBR - 1) / kBwdBR);
   if (items > 0x7fffffffL) return fail(ASR_E_UNSUPPORTED, "bf16 block: too many row bands (%ld)", items);
   const int grid = persistent_grid(items);
   *nslabs = grid;
   using L = blk::BwdLds<C, W, kBwdBR>;
   const size_t red = (size_t)(12288 + 4 * 64) * 4;
-  const size_t lds = std::max((size_t)L::TOTAL, red);
-  if (mode == blk::BWD_EULER)
-    hipLaunchKernelGGL((blk::k_bwd<C, W, kBwdBR, blk::BWD_EULER>), dim3(grid), dim3(512), lds, s, (const bf16*)dy,
-                       (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs);
-  else
-    hipLaunchKernelGGL((blk::k_bwd<C, W, kBwdBR, blk::BWD_CONV>), dim3(grid), dim3(512), lds, s, (const bf16*)dy,
-                       (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs);
+  const size_t lds = std::max((size_t)(extra ? L::TOTAL_XT : L::TOTAL), red);
+#define ASR_LAUNCH_BWD(M, XT)                                                                                    \
+  hipLaunchKernelGGL((blk::k_bwd<C, W, kBwdBR, M, XT>), dim3(grid), dim3(512), lds, s, (const bf16*)dy, (const bf16*)x, \
+                     mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs, (const bf16*)extra, skip_dy)
+  const bool xt = extra != nullptr || skip_dy != 0;
+  if (mode == blk::BWD_EULER) {
+    if (xt) ASR_LAUNCH_BWD(blk::BWD_EULER, true);
+    else ASR_LAUNCH_BWD(blk::BWD_EULER, false);
+  } else {
+    if (xt) ASR_LAUNCH_BWD(blk::BWD_CONV, true);
+    else ASR_LAUNCH_BWD(blk::BWD_CONV, false);
+  }
+#undef ASR_LAUNCH_BWD
   ASR_LAUNCH_CHECK("k_bwd");
   return ASR_OK;
 }
 
-int block_fwd_mfma(int mode, const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h, int N,
-                   int H, int W, int C, hipStream_t s) {
+int block_fwd_mfma(int mode, const void* x, const void* resid, void* y, uint8_t* mask, const void* w,
+                   const float* bias, float h, int N, int H, int W, int C, hipStream_t s) {
   if (W != 32) return fail(ASR_E_UNSUPPORTED, "bf16 block: W=%d not supported (W must be 32)", W);
   switch (C) {
-    case 16: return launch_fwd<16, 32>(mode, x, y, mask, w, bias, h, N, H, s);
-    case 32: return launch_fwd<32, 32>(mode, x, y, mask, w, bias, h, N, H, s);
-    case 64: return launch_fwd<64, 32>(mode, x, y, mask, w, bias, h, N, H, s);
+    case 16: return launch_fwd<16, 32>(mode, x, resid, y, mask, w, bias, h, N, H, s);
+    case 32: return launch_fwd<32, 32>(mode, x, resid, y, mask, w, bias, h, N, H, s);
+    case 64: return launch_fwd<64, 32>(mode, x, resid, y, mask, w, bias, h, N, H, s);
   }
   return fail(ASR_E_UNSUPPORTED, "bf16 block: C=%d not supported (16, 32, 64)", C);
 }
 
 int block_bwd_mfma(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
-                   float two_gamma, int N, int H, int W, int C, void* dx, float* slabs, int* nslabs, hipStream_t s) {
+                   float two_gamma, int N, int H, int W, int C, void* dx, float* slabs, int* nslabs, const void* extra,
+                   int skip_dy, hipStream_t s) {
   if (W != 32) return fail(ASR_E_UNSUPPORTED, "bf16 block: W=%d not supported (W must be 32)", W);
   switch (C) {
-    case 16: return launch_bwd<16, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, s);
-    case 32: return launch_bwd<32, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, s);
-    case 64: return launch_bwd<64, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, s);
+    case 16:
+      return launch_bwd<16, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, extra, skip_dy, s);
+    case 32:
+      return launch_bwd<32, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, extra, skip_dy, s);
+    case 64:
+      return launch_bwd<64, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, extra, skip_dy, s);
   }
   return fail(ASR_E_UNSUPPORTED, "bf16 block: C=%d not supported (16, 32, 64)", C);
 }

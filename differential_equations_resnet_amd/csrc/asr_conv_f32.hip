@@ -20,7 +20,8 @@ template <typename Tin, typename Tout, int MODE>
 __global__ __launch_bounds__(256) void k_conv_f32(const Tin* __restrict__ xin, Tout* __restrict__ out,
                                                   uint32_t* __restrict__ mask, const float* __restrict__ w,
                                                   const float* __restrict__ bias, float h, float two_gamma,
-                                                  const float* __restrict__ dy, int N, int H, int W, int Ci, int Co) {
+                                                  const float* __restrict__ dy, const float* __restrict__ extra,
+                                                  int N, int H, int W, int Ci, int Co) {
   const int PT = (W + 15) / 16, OT = (Co + 15) / 16;
   const long tasks = (long)N * H * PT * OT;
   const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -61,7 +62,8 @@ __global__ __launch_bounds__(256) void k_conv_f32(const Tin* __restrict__ xin, T
       const float z = acc[e] + ((bias && o < Co) ? bias[o] : 0.f);
       if constexpr (MODE == F_EULER) {
         if (ok && z > 0.f) nib |= 1u << e;
-        if (ok) v = to_f32(xin[pix * Ci + o]) + h * fmaxf(z, 0.f);
+        // residual: the input, or `extra` (the step input of the second RK2 stage)
+        if (ok) v = (extra ? extra[pix * Co + o] : to_f32(xin[pix * Ci + o])) + h * fmaxf(z, 0.f);
       } else if constexpr (MODE == F_CONV) {
         v = z;
       } else {
@@ -72,6 +74,7 @@ __global__ __launch_bounds__(256) void k_conv_f32(const Tin* __restrict__ xin, T
       if (ok) {
         const float dz = to_f32(xin[pix * Ci + o]);
         v = (MODE == B_EULER ? dy[pix * Co + o] : 0.f) - acc[e] + two_gamma * dz;
+        if (extra) v += extra[pix * Co + o];  // RK2 first stage: + the step's outer dy
       }
     }
     if (ok) out[pix * Co + o] = from_f32<Tout>(v);
@@ -146,7 +149,8 @@ __global__ void k_db_f32(const float* __restrict__ dz, long rows, int W, int C, 
 
 template <typename Tin, typename Tout, int MODE>
 static int launch_conv_f32(const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
-                           float two_gamma, const float* dy, int N, int H, int W, int Ci, int Co, hipStream_t s) {
+                           float two_gamma, const float* dy, const float* extra, int N, int H, int W, int Ci, int Co,
+                           hipStream_t s) {
   const long tasks = (long)N * H * ((W + 15) / 16) * ((Co + 15) / 16);
   const long blocks = (tasks + 3) / 4;
   if (blocks > 0x7fffffffL) return fail(ASR_E_ARG, "conv f32: problem too large");
@@ -155,26 +159,27 @@ static int launch_conv_f32(const void* xin, void* out, uint8_t* mask, const floa
     ASR_TRY(hip_check(hipMemsetAsync(mask, 0, bytes, s), "hipMemsetAsync(mask)"));
   }
   hipLaunchKernelGGL((k_conv_f32<Tin, Tout, MODE>), dim3((unsigned)blocks), dim3(256), 0, s, (const Tin*)xin,
-                     (Tout*)out, (uint32_t*)mask, w, bias, h, two_gamma, dy, N, H, W, Ci, Co);
+                     (Tout*)out, (uint32_t*)mask, w, bias, h, two_gamma, dy, extra, N, H, W, Ci, Co);
   ASR_LAUNCH_CHECK("k_conv_f32");
   return ASR_OK;
 }
 
 int conv_f32(int fmode, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
-             float two_gamma, const float* dy, int N, int H, int W, int Ci, int Co, int out_bf16, hipStream_t s) {
+             float two_gamma, const float* dy, int N, int H, int W, int Ci, int Co, int out_bf16, hipStream_t s,
+             const float* extra) {
   switch (fmode) {
     case F_EULER:
-      return launch_conv_f32<float, float, F_EULER>(xin, out, mask, w, bias, h, two_gamma, dy, N, H, W, Ci, Co, s);
+      return launch_conv_f32<float, float, F_EULER>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, W, Ci, Co, s);
     case F_CONV:
-      return launch_conv_f32<float, float, F_CONV>(xin, out, mask, w, bias, h, two_gamma, dy, N, H, W, Ci, Co, s);
+      return launch_conv_f32<float, float, F_CONV>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, W, Ci, Co, s);
     case F_RELU:
       if (out_bf16)
-        return launch_conv_f32<float, bf16, F_RELU>(xin, out, mask, w, bias, h, two_gamma, dy, N, H, W, Ci, Co, s);
-      return launch_conv_f32<float, float, F_RELU>(xin, out, mask, w, bias, h, two_gamma, dy, N, H, W, Ci, Co, s);
+        return launch_conv_f32<float, bf16, F_RELU>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, W, Ci, Co, s);
+      return launch_conv_f32<float, float, F_RELU>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, W, Ci, Co, s);
     case B_EULER:
-      return launch_conv_f32<float, float, B_EULER>(xin, out, mask, w, bias, h, two_gamma, dy, N, H, W, Ci, Co, s);
+      return launch_conv_f32<float, float, B_EULER>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, W, Ci, Co, s);
     case B_CONV:
-      return launch_conv_f32<float, float, B_CONV>(xin, out, mask, w, bias, h, two_gamma, dy, N, H, W, Ci, Co, s);
+      return launch_conv_f32<float, float, B_CONV>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, W, Ci, Co, s);
   }
   return fail(ASR_E_ARG, "conv f32: bad mode");
 }

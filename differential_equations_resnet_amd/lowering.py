@@ -11,9 +11,16 @@ runs (_v6.ipynb cells 5-9):
                    -> relu -> Lambda(h*x)? -> add(branch, block input) ]
           -> GlobalAveragePooling2D -> Dense(K, softmax)
 
+or, with integrator="rk2" (extension, BASELINE config 5), every block as
+the midpoint step built by single_layer_identity_block:
+
+          xm = add(Lambda(h/2*x)?(relu(conv(x))), x);  add(Lambda(h*x)?(relu(conv(xm))), x)
+
+with the SAME conv layer applied twice.
+
 Anything else (BN, pooling, stage transitions, strided or non-3x3 convs,
-per-block differing h/gamma) raises AsrUnsupported naming the layer: there
-is no fallback executor.
+per-block differing h/gamma/integrator) raises AsrUnsupported naming the
+layer: there is no fallback executor.
 """
 from __future__ import annotations
 
@@ -43,6 +50,7 @@ class NetPlan:
     divide_by_stddev: float | None
     param_kind: int
     antisymmetric: bool
+    integrator: str = "euler"
     conv1: Conv2D = None
     blocks: list = field(default_factory=list)
     fc: Dense = None
@@ -85,6 +93,34 @@ def _conv3x3_same(layer: Conv2D, what):
         raise _unsupported(layer, "dilated conv")
 
 
+def _euler_step(t: SymbolicTensor):
+    """Match t = add(Lambda(h*x)?(relu(conv(inner))), skip); return (conv, h, inner)."""
+    if len(t.inbound) != 2:
+        raise _unsupported(t.layer, "add of more than two tensors")
+    branch, skip = t.inbound
+    h = 1.0
+    if isinstance(branch.layer, Lambda):
+        s, off = _affine_scalar(branch.layer, branch.shape)
+        if off != 0.0:
+            raise _unsupported(branch.layer, "block scaling must be h*x")
+        h = s
+        branch = branch.inbound[0]
+    if not _is_relu(branch):
+        raise _unsupported(branch.layer, "expected relu in the block branch (BN is not supported)")
+    conv_t = branch.inbound[0]
+    conv = conv_t.layer
+    if isinstance(conv, AntisymmetricConvBase):
+        if conv.kernel_size != 3 or tuple(conv.strides) != (1, 1) or not conv.use_bias:
+            raise _unsupported(conv, "antisymmetric block conv must be 3x3, stride 1, with bias")
+    elif isinstance(conv, Conv2D):
+        _conv3x3_same(conv, "regular block conv")
+        if conv.activation not in (None, "linear"):
+            raise _unsupported(conv, "conv activation inside an identity block")
+    else:
+        raise _unsupported(conv, "unsupported block conv")
+    return conv, h, conv_t.inbound[0]
+
+
 def analyze(model: Model) -> NetPlan:
     if len(model.inputs) != 1 or len(model.outputs) != 1:
         raise _lib.AsrUnsupported("the native executor runs single-input single-output models")
@@ -100,33 +136,22 @@ def analyze(model: Model) -> NetPlan:
         raise _unsupported(t.layer, "expected GlobalAveragePooling2D before fc")
     t = t.inbound[0]
     # identity blocks, last to first
-    blocks, hs = [], []
+    blocks, hs, integ = [], [], []
     while isinstance(t.layer, Add):
-        if len(t.inbound) != 2:
-            raise _unsupported(t.layer, "add of more than two tensors")
-        branch, skip = t.inbound
-        h = 1.0
-        if isinstance(branch.layer, Lambda):
-            s, off = _affine_scalar(branch.layer, branch.shape)
-            if off != 0.0:
-                raise _unsupported(branch.layer, "block scaling must be h*x")
-            h = s
-            branch = branch.inbound[0]
-        if not _is_relu(branch):
-            raise _unsupported(branch.layer, "expected relu in the block branch (BN is not supported)")
-        conv_t = branch.inbound[0]
-        conv = conv_t.layer
-        if conv_t.inbound[0] is not skip:
-            raise _unsupported(conv, "block branch must start at the block input")
-        if isinstance(conv, AntisymmetricConvBase):
-            if conv.kernel_size != 3 or tuple(conv.strides) != (1, 1) or not conv.use_bias:
-                raise _unsupported(conv, "antisymmetric block conv must be 3x3, stride 1, with bias")
-        elif isinstance(conv, Conv2D):
-            _conv3x3_same(conv, "regular block conv")
-            if conv.activation not in (None, "linear"):
-                raise _unsupported(conv, "conv activation inside an identity block")
+        conv, h, inner = _euler_step(t)
+        skip = t.inbound[1]
+        if inner is skip:
+            integ.append("euler")
         else:
-            raise _unsupported(conv, "unsupported block conv")
+            # RK2: the conv's input is the midpoint xm = x + (h/2) relu(conv(x))
+            if not isinstance(inner.layer, Add) or inner.inbound[1] is not skip:
+                raise _unsupported(conv, "block branch must start at the block input (or its RK2 midpoint)")
+            conv1_, h1, inner1 = _euler_step(inner)
+            if conv1_ is not conv or inner1 is not skip:
+                raise _unsupported(inner.layer, "RK2 midpoint must apply the block's own conv to the block input")
+            if abs(h1 - 0.5 * h) > 1e-12 * max(1.0, abs(h)):
+                raise _unsupported(inner.layer, f"RK2 midpoint scale {h1} is not h/2 (h = {h})")
+            integ.append("rk2")
         blocks.append(conv)
         hs.append(h)
         t = skip
@@ -161,15 +186,15 @@ def analyze(model: Model) -> NetPlan:
     first = blocks[0]
     kinds = {(type(b), getattr(b, "param_kind", _lib.ASR_PARAM_REGULAR), getattr(b, "antisymmetric", False),
               float(getattr(b, "gamma", 0.0))) for b in blocks}
-    if len(kinds) != 1 or len(set(hs)) != 1:
-        raise _lib.AsrUnsupported("all identity blocks must share conv type, gamma and h")
+    if len(kinds) != 1 or len(set(hs)) != 1 or len(set(integ)) != 1:
+        raise _lib.AsrUnsupported("all identity blocks must share conv type, gamma, h and integrator")
     if isinstance(first, AntisymmetricConvBase):
         kind, anti, gamma = first.param_kind, bool(first.antisymmetric), float(first.gamma)
     else:
         kind, anti, gamma = _lib.ASR_PARAM_REGULAR, False, 0.0
     plan = NetPlan(H=int(H), W=int(W), Cin=int(Cin), C=int(C), L=len(blocks), num_classes=fc.units, h=float(hs[0]),
                    gamma=gamma, subtract_mean=mean, divide_by_stddev=std, param_kind=kind, antisymmetric=anti,
-                   conv1=conv1, blocks=blocks, fc=fc)
+                   integrator=integ[0], conv1=conv1, blocks=blocks, fc=fc)
     for b in blocks:
         if b.weights[-1].shape != (C,):
             raise _unsupported(b, f"block channels must equal conv1 filters ({C})")
@@ -236,7 +261,8 @@ class NativeModel:
             ex = self._rt.NetExecutor(self.batch_size, p.H, p.W, p.Cin, p.C, p.L, p.num_classes, p.h, p.gamma,
                                       subtract_mean=p.subtract_mean, divide_by_stddev=p.divide_by_stddev,
                                       dtype=self.dtype, input_u8=input_u8, device=self.device,
-                                      param_kind=p.param_kind, antisymmetric=p.antisymmetric)
+                                      param_kind=p.param_kind, antisymmetric=p.antisymmetric,
+                                      integrator=p.integrator)
             if ex.n_params != self.n_params:
                 raise _lib.AsrError(f"executor expects {ex.n_params} parameters, model has {self.n_params}")
             self._executors[input_u8] = ex

@@ -36,9 +36,13 @@ def _scale(h):
     return scale
 
 
-def _antisym_conv(x, gamma, strides, kernel_regularizer, name):
+def _antisym_conv_layer(gamma, strides, kernel_regularizer, name):
     return Conv2DAntisymmetric3By3(gamma=gamma, strides=strides, use_bias=True, kernel_initializer="he_normal",
-                                   kernel_regularizer=kernel_regularizer, name=name)(x)
+                                   kernel_regularizer=kernel_regularizer, name=name)
+
+
+def _antisym_conv(x, gamma, strides, kernel_regularizer, name):
+    return _antisym_conv_layer(gamma, strides, kernel_regularizer, name)(x)
 
 
 def _conv(x, filters, kernel_size, name, strides=(1, 1), padding="same", kernel_regularizer=None,
@@ -49,17 +53,38 @@ def _conv(x, filters, kernel_size, name, strides=(1, 1), padding="same", kernel_
 
 
 def single_layer_identity_block(input_tensor, kernel_size, antisymmetric, use_batch_norm, stage, block, h=1.0,
-                                gamma=0.0, kernel_regularizer=None, bias_regularizer=None):
+                                gamma=0.0, kernel_regularizer=None, bias_regularizer=None, integrator="euler"):
     """One Euler step x + h*relu(conv(x)) (tfkeras_resnets.py:28-94): the
     conv is Conv2DAntisymmetric3By3 when `antisymmetric`, else a regular
     'same' Conv2D with C filters; optional BN after it; the h-scaling Lambda
-    exists only when h != 1."""
+    exists only when h != 1.
+
+    integrator="rk2" (extension, not in the reference; BASELINE config 5)
+    builds the explicit midpoint step with the SAME conv layer (shared
+    weights) applied twice:
+        xm = x + (h/2)*relu(conv(x)),   out = x + h*relu(conv(xm))
+    with the half-step scaling Lambda named scale{stage}_{block}_half."""
+    if integrator not in ("euler", "rk2"):
+        raise ValueError(f"integrator must be 'euler' or 'rk2', got {integrator!r}")
     conv_name, bn_name = _names(stage, block)
     if antisymmetric:
-        x = _antisym_conv(input_tensor, gamma, (1, 1), kernel_regularizer, conv_name + "2")
+        conv = _antisym_conv_layer(gamma, (1, 1), kernel_regularizer, conv_name + "2")
     else:
-        x = _conv(input_tensor, int(input_tensor.shape[-1]), kernel_size, conv_name + "2",
-                  kernel_regularizer=kernel_regularizer, bias_regularizer=bias_regularizer)
+        conv = Conv2D(filters=int(input_tensor.shape[-1]), kernel_size=kernel_size, strides=(1, 1), padding="same",
+                      kernel_initializer="he_normal", kernel_regularizer=kernel_regularizer,
+                      bias_regularizer=bias_regularizer, name=conv_name + "2")
+    if integrator == "rk2":
+        if use_batch_norm:
+            raise ValueError("integrator='rk2' does not support use_batch_norm")
+        k1 = Activation("relu")(conv(input_tensor))
+        if 0.5 * h != 1.0:
+            k1 = Lambda(_scale(0.5 * h), name=f"scale{stage}_{block}_half")(k1)
+        xm = add([k1, input_tensor])
+        x = Activation("relu")(conv(xm))
+        if h != 1.0:
+            x = Lambda(_scale(h), name=f"scale{stage}_{block}")(x)
+        return add([x, input_tensor])
+    x = conv(input_tensor)
     if use_batch_norm:
         x = BatchNormalization(axis=3, name=bn_name + "2")(x)
     x = Activation("relu")(x)
@@ -164,9 +189,11 @@ def get_single_block_resnet_build_function(kernel_type="antisymmetric", kernel_s
                                            strides=[(2, 2), (2, 2), (2, 2), (2, 2)], include_top=True,
                                            fc_activation="softmax", num_classes=None, use_batch_norm=False,
                                            use_max_pooling=[False, False, False, False], l2_regularization=0.0,
-                                           subtract_mean=None, divide_by_stddev=None, verbose=False):
+                                           subtract_mean=None, divide_by_stddev=None, verbose=False,
+                                           integrator="euler"):
     """Returns build(input_tensor) -> Model for the single-conv-per-block
-    ResNet (tfkeras_resnets.py:511-604)."""
+    ResNet (tfkeras_resnets.py:511-604).  `integrator` (extension, default
+    the reference's forward Euler) is passed to every identity block."""
     if include_top and num_classes is None:
         raise ValueError("You must pass a positive integer for `num_classes` if `include_top` is `True`.")
     antisymmetric = kernel_type == "antisymmetric"
@@ -188,7 +215,8 @@ def get_single_block_resnet_build_function(kernel_type="antisymmetric", kernel_s
             if verbose:
                 print(f"Building identity block {stage}-{b + 1}")
             return single_layer_identity_block(x, kernel_size, antisymmetric, use_batch_norm, stage=stage, block=b,
-                                               h=h, gamma=gamma, kernel_regularizer=l2(l2_regularization))
+                                               h=h, gamma=gamma, kernel_regularizer=l2(l2_regularization),
+                                               integrator=integrator)
 
         for s in range(num_stages - 1):
             stage = s + 2
@@ -219,14 +247,15 @@ def build_single_block_resnet(image_shape, kernel_type="antisymmetric", kernel_s
                               num_stages=5, blocks_per_stage=[3, 4, 6, 3], filters_per_block=[64, 128, 256, 512],
                               strides=[(2, 2), (2, 2), (2, 2), (2, 2)], include_top=True, fc_activation="softmax",
                               num_classes=None, use_batch_norm=False, use_max_pooling=[False, False, False, False],
-                              l2_regularization=0.0, subtract_mean=None, divide_by_stddev=None, verbose=False):
+                              l2_regularization=0.0, subtract_mean=None, divide_by_stddev=None, verbose=False,
+                              integrator="euler"):
     """tfkeras_resnets.py:427-509: build function applied to Input(image_shape)."""
     fn = get_single_block_resnet_build_function(
         kernel_type=kernel_type, kernel_size=kernel_size, h=h, gamma=gamma, num_stages=num_stages,
         blocks_per_stage=blocks_per_stage, filters_per_block=filters_per_block, strides=strides,
         include_top=include_top, fc_activation=fc_activation, num_classes=num_classes, use_batch_norm=use_batch_norm,
         use_max_pooling=use_max_pooling, l2_regularization=l2_regularization, subtract_mean=subtract_mean,
-        divide_by_stddev=divide_by_stddev, verbose=verbose)
+        divide_by_stddev=divide_by_stddev, verbose=verbose, integrator=integrator)
     return fn(Input(shape=image_shape))
 
 

@@ -12,13 +12,21 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import (ASR_BF16, ASR_F32, ASR_MODE_CONV, ASR_MODE_EULER, ASR_PARAM_3BY3, ASR_PARAM_GENERAL,
-                   ASR_PARAM_REGULAR, NetConfig)
+from ._lib import (ASR_BF16, ASR_F32, ASR_INTEGRATOR_EULER, ASR_INTEGRATOR_RK2, ASR_MODE_CONV, ASR_MODE_EULER,
+                   ASR_PARAM_3BY3, ASR_PARAM_GENERAL, ASR_PARAM_REGULAR, NetConfig)
 
 __all__ = [
     "require_gpu", "dtype_code", "torch_dtype", "ParamMap", "param_map", "theta_count", "theta_to_w",
-    "conv_forward", "conv_backward", "NetExecutor", "adam_update",
+    "conv_forward", "conv_backward", "rk2_forward", "rk2_backward", "integrator_code", "NetExecutor", "adam_update",
 ]
+
+
+def integrator_code(integrator) -> int:
+    if integrator in ("euler", ASR_INTEGRATOR_EULER, None):
+        return ASR_INTEGRATOR_EULER
+    if integrator in ("rk2", "midpoint", ASR_INTEGRATOR_RK2):
+        return ASR_INTEGRATOR_RK2
+    raise ValueError(f"unknown integrator {integrator!r} ('euler' or 'rk2')")
 
 
 def require_gpu() -> torch.device:
@@ -193,6 +201,40 @@ def conv_backward(mode: int, dy: torch.Tensor, x: torch.Tensor, mask: torch.Tens
     return dx, dth, db, dw
 
 
+def rk2_forward(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, h: float, want_masks=True):
+    """RK2 midpoint block (asr_rk2_forward): returns (y, xmid, mask1, mask2)."""
+    N, H, W, C = x.shape
+    dt = dtype_code(x.dtype)
+    if not x.is_contiguous():
+        raise ValueError("x must be contiguous NHWC")
+    y = torch.empty_like(x)
+    xm = torch.empty_like(x)
+    mb = mask_bytes(N, H, W, C)
+    m1 = torch.zeros(mb, dtype=torch.uint8, device=x.device) if want_masks else None
+    m2 = torch.zeros(mb, dtype=torch.uint8, device=x.device) if want_masks else None
+    _lib.call("asr_rk2_forward", _p(x), _p(xm), _p(y), _p(m1), _p(m2), _p(w), _p(bias), float(h), N, H, W, C, dt,
+              _stream())
+    return y, xm, m1, m2
+
+
+def rk2_backward(dy, x, xmid, mask1, mask2, w, pmap: ParamMap, h: float, gamma: float, want_dx=True,
+                 want_dtheta=True, want_dbias=True, want_dw=False):
+    """Backward of rk2_forward (asr_rk2_backward): (dx, dtheta, dbias, dw)."""
+    N, H, W, C = dy.shape
+    dt = dtype_code(dy.dtype)
+    dev = dy.device
+    ws_bytes = int(_lib.load().asr_rk2_backward_workspace_bytes(N, H, W, C, dt))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    dx = torch.empty_like(dy) if want_dx else None
+    dth = torch.empty(pmap.n_theta, dtype=torch.float32, device=dev) if want_dtheta else None
+    db = torch.empty(C, dtype=torch.float32, device=dev) if want_dbias else None
+    dw = torch.empty(3, 3, C, C, dtype=torch.float32, device=dev) if want_dw else None
+    _, theta_dst = pmap.device(dev)
+    _lib.call("asr_rk2_backward", _p(dy), _p(x), _p(xmid), _p(mask1), _p(mask2), _p(w), _p(theta_dst), pmap.n_theta,
+              float(h), float(gamma), N, H, W, C, dt, _p(dx), _p(dth), _p(db), _p(dw), _p(ws), ws_bytes, _stream())
+    return dx, dth, db, dw
+
+
 def adam_update(params, grads, m, v, lr, beta1, beta2, eps, step, grad_scale=1.0):
     _lib.call("asr_adam_update", _p(params), _p(grads), _p(m), _p(v), params.numel(), float(lr), float(beta1),
               float(beta2), float(eps), int(step), float(grad_scale), _stream())
@@ -205,13 +247,15 @@ class NetExecutor:
     get_weights() order."""
 
     def __init__(self, N, H, W, Cin, C, L, num_classes, h, gamma=0.0, subtract_mean=None, divide_by_stddev=None,
-                 dtype="bfloat16", input_u8=True, device=None, param_kind=ASR_PARAM_3BY3, antisymmetric=True):
+                 dtype="bfloat16", input_u8=True, device=None, param_kind=ASR_PARAM_3BY3, antisymmetric=True,
+                 integrator="euler"):
         self.device = device or require_gpu()
         use_norm = subtract_mean is not None or divide_by_stddev is not None
         self.cfg = NetConfig(int(N), int(H), int(W), int(Cin), int(C), int(L), int(num_classes), float(h),
                              float(gamma), float(subtract_mean or 0.0),
                              float(divide_by_stddev if divide_by_stddev is not None else 1.0), int(use_norm),
-                             dtype_code(dtype), int(bool(input_u8)), int(param_kind), int(bool(antisymmetric)))
+                             dtype_code(dtype), int(bool(input_u8)), int(param_kind), int(bool(antisymmetric)),
+                             integrator_code(integrator))
         lib = _lib.load()
         self.n_params = int(lib.asr_net_param_count(ct.byref(self.cfg)))
         if self.n_params < 0:

@@ -57,6 +57,10 @@ typedef void* asr_stream_t; /* a hipStream_t (0 = null stream) */
                                identity block, tfkeras_resnets.py:76-83):
                                theta IS W in HWIO order                       */
 
+/* block integrators (asr_net_config.integrator) */
+#define ASR_INTEGRATOR_EULER 0
+#define ASR_INTEGRATOR_RK2 1
+
 /* conv modes */
 #define ASR_MODE_EULER 0 /* y = x + h*relu(conv(x)+b); mask = [conv(x)+b > 0]
                             (tfkeras_resnets.py:69-92)                        */
@@ -145,6 +149,31 @@ int asr_conv_backward(int mode, const void* dy, const void* x, const uint8_t* ma
                       asr_stream_t stream);
 
 /* ------------------------------------------------------------------------
+ * RK2 (explicit midpoint) block — an EXTENSION, not in the reference
+ * (BASELINE.json config 5; the reference integrates with forward Euler,
+ * tfkeras_resnets.py:69-92).  Same W and bias in both stages:
+ *   xmid = x + (h/2)*relu(conv(x,W)+b)      mask1 = [conv(x,W)+b > 0]
+ *   y    = x + h*relu(conv(xmid,W)+b)       mask2 = [conv(xmid,W)+b > 0]
+ * Each stage is the fused Euler kernel (the second takes its residual from x).
+ * xmid and both masks are kept for the backward; masks may be NULL for
+ * inference.
+ * --------------------------------------------------------------------- */
+int asr_rk2_forward(const void* x, void* xmid, void* y, uint8_t* mask1, uint8_t* mask2, const void* w,
+                    const float* bias, float h, int N, int H, int W, int C, int dtype,
+                    asr_stream_t stream);
+
+/* Backward of asr_rk2_forward: dz2 = h*dy*mask2, g = A^T dz2,
+ * dz1 = (h/2)*g*mask1, dx = dy + g + A^T dz1; dW = patch(x) (x) dz1 +
+ * patch(xmid) (x) dz2 projected onto theta; db = sum(dz1 + dz2).
+ * Outputs as asr_conv_backward; ws of asr_rk2_backward_workspace_bytes. */
+size_t asr_rk2_backward_workspace_bytes(int N, int H, int W, int C, int dtype);
+int asr_rk2_backward(const void* dy, const void* x, const void* xmid, const uint8_t* mask1,
+                     const uint8_t* mask2, const void* w, const int32_t* theta_dst, long n_theta,
+                     float h, float gamma, int N, int H, int W, int C, int dtype, void* dx,
+                     float* dtheta, float* dbias, float* dw_hwio, void* ws, size_t ws_bytes,
+                     asr_stream_t stream);
+
+/* ------------------------------------------------------------------------
  * Whole single-block network (get_single_block_resnet_build_function,
  * tfkeras_resnets.py:511-604, antisymmetric, num_stages=2, strides (1,1),
  * no BN/pooling):  normalise -> conv1+relu -> L Euler blocks -> GAP ->
@@ -164,6 +193,8 @@ typedef struct asr_net_config {
   int input_u8; /* images are uint8 (1) or float32 (0), NHWC            */
   int param_kind;    /* ASR_PARAM_3BY3 / _GENERAL / _REGULAR of the blocks */
   int antisymmetric; /* Conv2DAntisymmetric(antisymmetric=...); 1 otherwise */
+  int integrator;    /* ASR_INTEGRATOR_EULER (the reference's block) or
+                        ASR_INTEGRATOR_RK2 (extension, asr_rk2_forward)     */
 } asr_net_config;
 
 long asr_net_param_count(const asr_net_config* cfg);

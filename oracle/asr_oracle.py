@@ -376,11 +376,38 @@ def conv_bwd(dz, x, W, gamma=0.0):
 
 def rk2_fwd(x, W, bias, h):
     """Extension (not in the reference; BASELINE config 5): explicit midpoint
-    step with the same W in both stages."""
-    k1 = np.maximum(conv2d_same(x, W) + bias, 0)
-    xm = x + 0.5 * h * k1
-    zm = conv2d_same(xm, W) + bias
-    return x + h * np.maximum(zm, 0)
+    step with the same W and bias in both stages, each stage composed of the
+    reference's Euler-block operations (tfkeras_resnets.py:69-92):
+        xm = x + (h/2) relu(conv(x) + b),   y = x + h relu(conv(xm) + b).
+    Returns (y, cache) with cache = (xm, z1, z2)."""
+    z1 = conv2d_same(x, W)
+    if bias is not None:
+        z1 = z1 + np.asarray(bias)
+    xm = x + (0.5 * h) * np.maximum(z1, 0)
+    z2 = conv2d_same(xm, W)
+    if bias is not None:
+        z2 = z2 + np.asarray(bias)
+    return x + h * np.maximum(z2, 0), (xm, z1, z2)
+
+
+def rk2_bwd(dy, x, cache, W, h, gamma=0.0, antisymmetric=True):
+    """Autodiff of rk2_fwd: dz2 = h dy [z2>0]; g = A^T dz2 (gradient at xm);
+    dz1 = (h/2) g [z1>0]; dx = dy + g + A^T dz1; dW = dW(x, dz1) + dW(xm, dz2);
+    db = sum(dz1 + dz2).  A^T = -A + 2 gamma I when `antisymmetric`, else the
+    generic Conv2DBackpropInput."""
+    xm, z1, z2 = cache
+
+    def at(dz):
+        if antisymmetric:
+            return -conv2d_same(dz, W) + 2.0 * gamma * dz
+        return conv2d_backprop_input(dz, W, dz.shape)
+    dz2 = h * dy * (z2 > 0)
+    g = at(dz2)
+    dz1 = (0.5 * h) * g * (z1 > 0)
+    dx = dy + g + at(dz1)
+    dW = conv2d_backprop_filter(x, dz1) + conv2d_backprop_filter(xm, dz2)
+    db = dz1.sum(axis=(0, 1, 2)) + dz2.sum(axis=(0, 1, 2))
+    return dx, dW, db
 
 
 # --------------------------------------------------------------------------
@@ -404,6 +431,7 @@ class NetSpec:
     divide_by_stddev: float | None = 127.5
     kind: str = "3by3"           # "3by3" | "general" | "regular" (identity-block conv type)
     antisymmetric: bool = True   # Conv2DAntisymmetric(antisymmetric=...)
+    integrator: str = "euler"    # "euler" (the reference) | "rk2" (extension, rk2_fwd)
 
     def theta_shapes(self):
         """Block conv weights in creation order: Conv2DAntisymmetric3By3
@@ -520,7 +548,10 @@ def net_forward(spec: NetSpec, params, images, dtype=np.float64):
         else:
             src, sign = _cached_map(spec.C, spec.kind, spec.antisymmetric)
             W = assemble_from_map(flatten(theta), spec.C, src, sign, spec.gamma)
-        x, z = euler_fwd(x, W, b, spec.h)
+        if spec.integrator == "rk2":
+            x, z = rk2_fwd(x, W, b, spec.h)
+        else:
+            x, z = euler_fwd(x, W, b, spec.h)
         xs.append(x)
         zs.append(z)
         Ws.append(W)
@@ -565,7 +596,10 @@ def net_backward(spec: NetSpec, params, cache, onehot):
     block_grads = []
     for li in range(spec.L - 1, -1, -1):
         x_in = cache["xs"][li]
-        if spec.operator_antisymmetric():
+        if spec.integrator == "rk2":
+            dx, dW, db = rk2_bwd(dx, x_in, cache["zs"][li], cache["Ws"][li], spec.h, spec.gamma,
+                                 spec.operator_antisymmetric())
+        elif spec.operator_antisymmetric():
             dx, dW, db = euler_bwd(dx, x_in, cache["zs"][li], cache["Ws"][li], spec.h, spec.gamma)
         else:
             dx, dW, db = euler_bwd_generic(dx, x_in, cache["zs"][li], cache["Ws"][li], spec.h)

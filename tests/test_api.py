@@ -109,6 +109,35 @@ def test_analyze_single_block_plan():
     assert r.param_kind == _lib.ASR_PARAM_REGULAR and r.h == 1.0 and r.L == 2
 
 
+@pytest.mark.parametrize("kernel_type,h", [("antisymmetric", 0.5), ("regular", 2.0)])
+def test_rk2_builder_and_lowering(kernel_type, h):
+    """integrator='rk2' (extension, BASELINE config 5): the same conv layer is
+    applied twice per block (shared weights), so the weight list, names and
+    parameter count are those of the Euler model; the lowering recognises the
+    midpoint pattern."""
+    m = _single_block(C=8, L=3, h=h, kernel_type=kernel_type, integrator="rk2")
+    e = _single_block(C=8, L=3, h=h, kernel_type=kernel_type)
+    assert [w.shape for w in m.weights] == [w.shape for w in e.weights]
+    assert len(m.get_layer("res2_1_branch2").inbound_nodes) == 2
+    names = [l.name for l in m.layers]
+    assert ("scale2_0_half" in names) == (h != 2.0) and "scale2_0" in names
+    p = analyze(m)
+    assert p.integrator == "rk2" and p.L == 3 and p.h == h
+    assert analyze(e).integrator == "euler"
+    with pytest.raises(ValueError):
+        _single_block(L=1, integrator="rk4")
+
+
+def test_analyze_rejects_mixed_integrators():
+    x = Input(shape=(32, 32, 3))
+    y = graph.Conv2D(8, 3, padding="same", activation="relu", name="conv1")(x)
+    y = R.single_layer_identity_block(y, 3, True, False, 2, 0, h=0.5)
+    y = R.single_layer_identity_block(y, 3, True, False, 2, 1, h=0.5, integrator="rk2")
+    y = graph.Dense(10, activation="softmax")(graph.GlobalAveragePooling2D()(y))
+    with pytest.raises(_lib.AsrUnsupported, match="integrator"):
+        analyze(graph.Model(x, y))
+
+
 def test_analyze_general_layer_model():
     x = Input(shape=(32, 32, 3))
     y = graph.Conv2D(8, 3, padding="same", activation="relu", name="conv1")(x)

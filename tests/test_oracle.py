@@ -126,6 +126,61 @@ def test_euler_block_gradients_finite_difference():
     assert np.abs(dx - (R + O.conv2d_backprop_input(dz, W, x.shape))).max() < 1e-12
 
 
+@pytest.mark.parametrize("kind,anti", [("3by3", True), ("regular", False)])
+def test_rk2_block_gradients_finite_difference(kind, anti):
+    """RK2 midpoint block (extension, BASELINE config 5): analytic backward vs
+    finite differences, for the antisymmetric (A^T = -A + 2 gamma I) and the
+    generic transpose path."""
+    rng = np.random.default_rng(5)
+    C, N, H, Wd, h = 3, 2, 4, 5, 0.7
+    g = -0.1 if anti else 0.0
+    if kind == "3by3":
+        th = O.flatten(O.init_theta_3by3(C, rng))
+        src, sign = O.param_map(C)
+    else:
+        th = rng.standard_normal(9 * C * C) * 0.3
+        src, sign = np.arange(9 * C * C), np.ones(9 * C * C, dtype=np.int64)
+    b = rng.standard_normal(C) * 0.1
+    x = rng.standard_normal((N, H, Wd, C))
+    R = rng.standard_normal((N, H, Wd, C))
+
+    def f(t, bb, xx):
+        y, _ = O.rk2_fwd(xx, O.assemble_from_map(t, C, src, sign, g), bb, h)
+        return (y * R).sum()
+
+    W = O.assemble_from_map(th, C, src, sign, g)
+    y, cache = O.rk2_fwd(x, W, b, h)
+    dx, dW, db = O.rk2_bwd(R, x, cache, W, h, g, anti)
+    dth = O.project_dW(dW, src, sign, th.size)
+    assert np.abs(_fd(lambda t: f(t, b, x), th) - dth).max() < 1e-6
+    assert np.abs(_fd(lambda v: f(th, v, x), b) - db).max() < 1e-6
+    assert np.abs(_fd(lambda v: f(th, b, v), x) - dx).max() < 1e-6
+    # the midpoint step is the composition of two Euler-block evaluations
+    xm, _ = O.euler_fwd(x, W, b, 0.5 * h)
+    assert np.abs(cache[0] - xm).max() < 1e-14
+
+
+def test_rk2_network_gradients_finite_difference():
+    rng = np.random.default_rng(6)
+    spec = O.NetSpec(C=4, L=2, h=0.5, H=5, W=4, gamma=-0.1, integrator="rk2")
+    params = O.init_params(spec, rng, bias_std=0.1)
+    imgs = rng.integers(0, 256, (3, 5, 4, 3)).astype(np.uint8)
+    oh = np.eye(10)[rng.integers(0, 10, 3)]
+    probs, cache = O.net_forward(spec, params, imgs)
+    g = O.flatten(O.net_backward(spec, params, cache, oh))
+    flat = O.flatten(params)
+    shapes = [p.shape for p in params]
+
+    def loss(fl):
+        pr, _ = O.net_forward(spec, O.unflatten(fl, shapes), imgs)
+        return O.net_loss(pr, oh)
+
+    for i in rng.choice(flat.size, 25, replace=False):
+        e = np.zeros_like(flat)
+        e[i] = 1e-6
+        assert abs((loss(flat + e) - loss(flat - e)) / 2e-6 - g[i]) < 1e-6
+
+
 @pytest.mark.parametrize("kind,anti", [("3by3", True), ("general", True), ("general", False), ("regular", False)])
 def test_network_gradients_finite_difference(kind, anti):
     rng = np.random.default_rng(2)
