@@ -31,9 +31,14 @@
 
 #include "asr_common.h"
 
+#ifndef ASR_BWD_DMA_HOOK
+#define ASR_BWD_DMA_HOOK 1  // issue the backward's prefetch inside the dgrad k-steps (0: before the convert)
+#endif
 #ifndef ASR_ABLATE
 #define ASR_ABLATE 0  // development only: fwd 1 no epilogue, 2 no MFMA, 3 no prefetch DMA;
-                      // bwd 4 no convert, 5 no dgrad MFMA, 6 no wgrad MFMA, 7 no dgrad epilogue
+                      // bwd 4 no convert, 5 no dgrad MFMA, 6 no wgrad MFMA, 7 no dgrad epilogue,
+                      // 8 no prefetch DMA, 9 wgrad fragments from registers (no LDS reads),
+                      // 10 dgrad waves do not wait for the prefetch at the band barrier
 #endif
 
 namespace asr {
@@ -87,39 +92,63 @@ __device__ __forceinline__ int dma_lane_off(int lane) {
   return pl * C + (p ^ G::swz(1 + pl)) * 8;  // elements
 }
 
+// The loops below run on a wave-uniform index (readfirstlane), so they are
+// scalar loops: per instruction only an SGPR base (row start or the zero
+// page) and M0 change; the per-lane part is one 32-bit offset.
+//
+// One instruction j of a row stream: image rows [gy0, gy0+nrows) of image n
+// (rows outside [0,H) -> zeros) into tile rows [0, nrows), interior columns.
+template <int C, int W>
+__device__ __forceinline__ void dma_row_instr(const bf16* __restrict__ src, unsigned char* tile, int n, int gy0, int j,
+                                              int H, unsigned loff) {
+  using G = Geo<C>;
+  constexpr int TW = W + 2, NQ = G::NQ, PPI = G::PPI, IPR = W / PPI;
+  const int r = (unsigned)j / IPR, seg = (unsigned)j % IPR;  // wave-uniform
+  const int gy = gy0 + r;
+  const unsigned char* base = ((unsigned)gy < (unsigned)H)
+                                  ? (const unsigned char*)src + ((long)n * H + gy) * (W * C * 2) + seg * (PPI * C * 2)
+                                  : (const unsigned char*)g_zero_page;
+  dma16(base + loff, tile + ((r * TW + 1 + seg * PPI) * NQ) * 16);
+}
+
 template <int C, int W>
 __device__ __forceinline__ void dma_rows(const bf16* __restrict__ src, unsigned char* tile, int n, int gy0,
                                          int nrows, int H, int wave, int nwaves, int lane) {
   using G = Geo<C>;
-  constexpr int TW = W + 2, NQ = G::NQ, PPI = G::PPI, IPR = W / PPI;
+  constexpr int PPI = G::PPI, IPR = W / PPI;
   static_assert(W % PPI == 0, "image width must be a multiple of the DMA pixel group");
   static_assert(PPI % 16 == 0 || (PPI % 8 == 0 && C == 64), "segment-invariant swizzle");
-  const int loff = dma_lane_off<C, W>(lane);
-  const bf16* img = src + (long)n * H * W * C;
-  for (int j = wave; j < nrows * IPR; j += nwaves) {
-    const int r = j / IPR, seg = j - r * IPR;  // wave-uniform
-    const int gy = gy0 + r;
-    const void* s = (gy >= 0 && gy < H) ? (const void*)(img + ((long)gy * W + seg * PPI) * C + loff)
-                                        : (const void*)(g_zero_page + lane);
-    dma16(s, tile + ((r * TW + 1 + seg * PPI) * NQ) * 16);
-  }
+  const unsigned loff = (unsigned)dma_lane_off<C, W>(lane) * 2u;  // bytes, < 1 KiB
+  for (int j = __builtin_amdgcn_readfirstlane(wave); j < nrows * IPR; j += nwaves)
+    dma_row_instr<C, W>(src, tile, n, gy0, j, H, loff);
 }
 
-// DMA the relu-mask bytes of rows [gy0, gy0+nrows) (W*C/8 bytes per row) into
-// a lane-linear LDS array (rows outside the image -> zeros).
+// One 1 KiB chunk j of the relu-mask bytes of rows [gy0, gy0+nrows) (W*C/8
+// bytes per row) into a lane-linear LDS array (bytes outside the image ->
+// zeros).  The band's rows are contiguous in memory; only chunks that reach
+// outside the image take the per-lane select.
+template <int C, int W>
+__device__ __forceinline__ void dma_mask_instr(const uint8_t* __restrict__ mask, unsigned char* mt, int n, int gy0,
+                                               int nrows, int j, int H, int lane) {
+  constexpr int RB = W * C / 8;  // bytes per image row
+  const int total = nrows * RB;
+  const long band0 = ((long)n * H + gy0) * RB;
+  const int lo = max(0, -gy0) * RB, hi = (min(H, gy0 + nrows) - gy0) * RB;  // valid bytes of the band
+  const int b0 = j * 1024, b = b0 + lane * 16;
+  const void* s;
+  if (b0 >= lo && b0 + 1024 <= hi && b0 + 1024 <= total)  // whole chunk valid (uniform)
+    s = (const void*)(mask + band0 + b);
+  else
+    s = (b >= lo && b < hi && b < total) ? (const void*)(mask + band0 + b) : (const void*)(g_zero_page + lane);
+  dma16(s, mt + b0);
+}
+
 template <int C, int W>
 __device__ __forceinline__ void dma_mask_rows(const uint8_t* __restrict__ mask, unsigned char* mt, int n, int gy0,
                                               int nrows, int H, int wave, int nwaves, int lane) {
-  constexpr int RB = W * C / 8;  // bytes per image row
-  const int total = nrows * RB;
-  for (int j = wave; j * 1024 < total; j += nwaves) {
-    const int b = j * 1024 + lane * 16;
-    const int r = b / RB, off = b % RB;
-    const int gy = gy0 + r;
-    const void* s = (b < total && gy >= 0 && gy < H) ? (const void*)(mask + ((long)n * H + gy) * RB + off)
-                                                     : (const void*)(g_zero_page + lane);
-    dma16(s, mt + j * 1024);
-  }
+  const int total = nrows * (W * C / 8);
+  for (int j = __builtin_amdgcn_readfirstlane(wave); j * 1024 < total; j += nwaves)
+    dma_mask_instr<C, W>(mask, mt, n, gy0, nrows, j, H, lane);
 }
 
 // Workgroup barrier that waits only for this wave's vector-memory ops OLDER
@@ -266,10 +295,10 @@ __device__ __forceinline__ void conv_issue(const unsigned (&ra)[Frag<C, W>::NB],
 // the reads of step ks+1 are in flight, those of ks+2 are issued after the
 // MFMAs of ks (three buffers: a read never targets registers an MFMA issued
 // in the previous step may still be reading).
-template <int C, int W, int ks>
+template <int C, int W, int ks, typename Hook>
 __device__ __forceinline__ void conv_step(const unsigned (&ra)[Frag<C, W>::NB],
                                           const bf16x8 (&A)[Geo<C>::OTW][Geo<C>::KS],
-                                          f32x4 (&acc)[Geo<C>::OTW][W / 16], bf16x8 (&B)[3][W / 16]) {
+                                          f32x4 (&acc)[Geo<C>::OTW][W / 16], bf16x8 (&B)[3][W / 16], Hook& hook) {
   using G = Geo<C>;
   constexpr int PT = W / 16, KS = G::KS;
   if constexpr (ks < KS) {
@@ -280,15 +309,22 @@ __device__ __forceinline__ void conv_step(const unsigned (&ra)[Frag<C, W>::NB],
       for (int t = 0; t < G::OTW; ++t)
         acc[t][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[t][ks], B[ks % 3][pt], acc[t][pt], 0, 0, 0);
     if constexpr (ks + 2 < KS) conv_issue<C, W, ks + 2>(ra, B[(ks + 2) % 3]);
-    conv_step<C, W, ks + 1>(ra, A, acc, B);
+    hook();
+    conv_step<C, W, ks + 1>(ra, A, acc, B, hook);
   }
 }
 
 // conv GEMM of one output row (tile row r is the row above it), accumulated
 // onto the caller's initial acc (the bias in the forward)
-template <int C, int W>
+struct NoStepHook {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+// hook() runs once per k-step, after that step's MFMAs are issued (the
+// backward interleaves its next-band DMA issue with the dgrad MFMAs that way)
+template <int C, int W, typename Hook = NoStepHook>
 __device__ __forceinline__ void conv_row(const unsigned char* tile, int r, const bf16x8 (&A)[Geo<C>::OTW][Geo<C>::KS],
-                                         const Frag<C, W>& f, f32x4 (&acc)[Geo<C>::OTW][W / 16]) {
+                                         const Frag<C, W>& f, f32x4 (&acc)[Geo<C>::OTW][W / 16], Hook hook = {}) {
   using G = Geo<C>;
   constexpr int TW = W + 2, PT = W / 16;
   const unsigned rb = lds_u32(tile + r * TW * G::NQ * 16);
@@ -299,7 +335,7 @@ __device__ __forceinline__ void conv_row(const unsigned char* tile, int r, const
   lgkm_wait<0>();  // nothing else of ours outstanding on the LDS counter
   conv_issue<C, W, 0>(ra, B[0]);
   if constexpr (G::KS > 1) conv_issue<C, W, 1>(ra, B[1]);
-  conv_step<C, W, 0>(ra, A, acc, B);
+  conv_step<C, W, 0>(ra, A, acc, B, hook);
 }
 
 // ---------------------------------------------------------------------------
@@ -949,34 +985,32 @@ __device__ __forceinline__ void bwd_issue(const bf16* dy, const bf16* x, const u
 
 // dzm = dy * mask for all staged rows, into the DZ tile: a bit operation on
 // the bf16 values (the factor h of dz = h*dy*mask is applied in fp32 in the
-// epilogues: dx, dW and db are linear in dz).  LDS accesses through asm (see
-// lds_rd128): the dgrad waves run this with the next band's DMA in flight.
+// epilogues: dx, dW and db are linear in dz).  Interior columns only (the DZ
+// tile's halo columns are zeroed once per launch), so chunk c of the band is
+// (row, col, q) by shifts and its mask byte is byte c of the staged mask
+// rows.  LDS accesses through asm (see lds_rd128): the dgrad waves run this
+// with the next band's DMA in flight.
 template <int C, int W, int BR, bool EULER>
 __device__ __forceinline__ void bwd_convert(unsigned char* lds, int buf, int nr, int tid, int nthreads) {
   using L = BwdLds<C, W, BR>;
   constexpr int TW = W + 2, NQ = C / 8, KB = 4;
+  static_assert((NQ & (NQ - 1)) == 0 && (W & (W - 1)) == 0, "power-of-two chunk decomposition");
   const unsigned dyt = lds_u32(lds + L::DY + buf * L::TILE);
   const unsigned mt = lds_u32(lds + L::MSK + buf * L::MTB);
   const unsigned dzt = lds_u32(lds + L::DZ);
-  const int nch = nr * TW * NQ;
+  const int nch = nr * W * NQ;
   for (int c0 = tid; c0 < nch; c0 += KB * nthreads) {
     u32x4 v[KB];
     unsigned mb[KB];
-    int off[KB];
-    bool inner[KB];
+    unsigned off[KB];
 #pragma unroll
     for (int k = 0; k < KB; ++k) {  // all LDS reads first (latencies overlap)
       const int c = c0 + k * nthreads;
       const int cc = c < nch ? c : 0;
-      const int q = cc % NQ, pc = cc / NQ, col = pc % TW, r = pc / TW;
-      off[k] = toff<C>(r, col, q, TW);
-      inner[k] = col >= 1 && col <= W;
-      if constexpr (EULER) {
-        v[k] = lds_rd128(dyt + off[k]);
-        mb[k] = lds_rd_u8(mt + (inner[k] ? (r * W + col - 1) * NQ + q : 0));
-      } else {
-        v[k] = lds_rd128(dyt + off[k]);
-      }
+      const int q = cc & (NQ - 1), col = 1 + ((cc / NQ) & (W - 1)), r = cc / (NQ * W);
+      off[k] = (unsigned)toff<C>(r, col, q, TW);
+      v[k] = lds_rd128(dyt + off[k]);
+      if constexpr (EULER) mb[k] = lds_rd_u8(mt + (unsigned)cc);
     }
     lgkm_wait<0>();
 #pragma unroll
@@ -984,12 +1018,11 @@ __device__ __forceinline__ void bwd_convert(unsigned char* lds, int buf, int nr,
       if (c0 + k * nthreads < nch) {
         u32x4 z = v[k];
         if constexpr (EULER) {
-          const unsigned m = inner[k] ? mb[k] : 0u;
 #pragma unroll
           for (int d = 0; d < 4; ++d) {  // element pair (2d, 2d+1) of this 16-byte chunk
-            const unsigned lo = (unsigned)(((int)(m << (31 - 2 * d))) >> 31);
-            const unsigned hi = (unsigned)(((int)(m << (30 - 2 * d))) >> 31);
-            z[d] &= (lo & 0xffffu) | (hi & 0xffff0000u);
+            const unsigned lo = (unsigned)__builtin_amdgcn_sbfe((int)mb[k], 2 * d, 1);
+            const unsigned hi = (unsigned)__builtin_amdgcn_sbfe((int)mb[k], 2 * d + 1, 1);
+            z[d] &= __builtin_amdgcn_perm(hi, lo, 0x07060100u);  // bytes 0-1 of lo, 2-3 of hi
           }
         }
         lds_wr128(dzt + off[k], z);
@@ -1022,6 +1055,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
     zero_halo_cols<C, W>(lds + L::DY + b * L::TILE, BR + 2, tid, 512);
     zero_halo_cols<C, W>(lds + L::X + b * L::TILE, BR + 2, tid, 512);
   }
+  zero_halo_cols<C, W>(lds + L::DZ, BR + 2, tid, 512);
   const int nb = (H + BR - 1) / BR;
   int i0, i1;
   item_range(N * nb, &i0, &i1);
@@ -1037,6 +1071,8 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
     // ---------------- dgrad waves ----------------
     constexpr int RS = 4 / G::OSPLIT;
     const int oh = wave % G::OSPLIT, rg = wave / G::OSPLIT;
+    const int wv4 = __builtin_amdgcn_readfirstlane(wave);
+    const unsigned loff = (unsigned)dma_lane_off<C, W>(lane) * 2u;
     bf16x8 A[OTW][G::KS];
     load_A<C>(wpack, oh, lane, A);
     Frag<C, W> boff;
@@ -1065,15 +1101,36 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
       const int buf = (it - i0) & 1;
       const int n = cur.n, y0 = cur.b * BR;
       const int rows = min(BR, H - y0);
-      barrier_vm(nst);  // item's DMA landed; previous item fully consumed
+      if (ASR_ABLATE == 10) barrier_lds();
+      else barrier_vm(nst);  // item's DMA landed; previous item fully consumed
       nst = 0;
-      int nd = 0;  // DMA instructions this wave issues below
-      if (it + 1 < i1) {
-        bwd_issue<C, W, BR, EULER>(dy, x, mask, lds, buf ^ 1, nxt.n, nxt.b * BR, H, wave, lane, 4);
-        const int nr = min(BR, H - nxt.b * BR) + 2;
-        nd = 2 * strided_count(nr * (W / G::PPI), wave, 4);
-        if (EULER) nd += strided_count((nr * (W * C / 8) + 1023) / 1024, wave, 4);
+      // prefetch of band it+1: dy rows, x rows, mask chunks as one stream of
+      // instructions dealt round-robin to the 4 dgrad waves; issued one per
+      // k-step of the wave's first dgrad row (so the issue cost overlaps the
+      // MFMAs of both roles), the rest flushed before that row's epilogue
+      int nd = 0;                               // prefetch instructions this wave issued
+      int du = wv4, dend = 0, dni = 0, dnr = 0;  // wave-uniform stream cursor
+      const int dy0 = nxt.b * BR - 1;
+      if (ASR_ABLATE != 8 && it + 1 < i1) {
+        dnr = min(BR, H - nxt.b * BR) + 2;
+        dni = dnr * (W / G::PPI);
+        dend = 2 * dni + (EULER ? (dnr * (W * C / 8) + 1023) / 1024 : 0);
       }
+      auto dma_one = [&]() {
+        if (du < dend) {
+          if (du < dni)
+            dma_row_instr<C, W>(dy, lds + L::DY + (buf ^ 1) * L::TILE, nxt.n, dy0, du, H, loff);
+          else if (du < 2 * dni)
+            dma_row_instr<C, W>(x, lds + L::X + (buf ^ 1) * L::TILE, nxt.n, dy0, du - dni, H, loff);
+          else
+            dma_mask_instr<C, W>(mask, lds + L::MSK + (buf ^ 1) * L::MTB, nxt.n, dy0, dnr, du - 2 * dni, H, lane);
+          du += 4;
+          nst = 0;  // the next barrier waits for this prefetch; stores issued after it need not finish
+          ++nd;
+        }
+      };
+      if (!ASR_BWD_DMA_HOOK)
+        while (du < dend) dma_one();
       bool ex_wait = has_extra;
       if (ASR_ABLATE != 4) bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, tid, 512);
       barrier_lds();  // dz ready
@@ -1089,7 +1146,12 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
 #pragma unroll
           for (int pt = 0; pt < PT; ++pt) acc[t][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (ASR_ABLATE != 5) {
-          conv_row<C, W>(dzt, r, A, boff, acc);
+          if (ASR_BWD_DMA_HOOK && k == 0) {
+            conv_row<C, W>(dzt, r, A, boff, acc, dma_one);
+            while (du < dend) dma_one();
+          } else {
+            conv_row<C, W>(dzt, r, A, boff, acc);
+          }
         } else {
 #pragma unroll
           for (int t = 0; t < OTW; ++t)
@@ -1166,6 +1228,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
           }
         }
       }
+      while (du < dend) dma_one();  // a wave without rows in this band
       if (has_extra && it + 1 < i1) {  // next band's extra rows into the (now read) private rows
         dma_extra<C, W, BR>(extra, priv, nxt.n, nxt.b * BR, min(BR, H - nxt.b * BR), H, rg, oh, lane);
         nst += NEX;
@@ -1219,6 +1282,12 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
         const int r = kk / KPR, kb = kk % KPR;
         const int pb = 32 * kb + 8 * g + tq;
         auto loadA = [&](int mi) {
+          if (ASR_ABLATE == 9) {
+            bf16x8 v;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = (bf16)(float)(lane + mi + kk + e);
+            return v;
+          }
           const int mt = tg * MTW + mi;
           const int tap = (16 * mt) / C, itile = ((16 * mt) % C) / 16;
           const int ky = tap / 3, kx = tap % 3;
@@ -1232,6 +1301,9 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
           const int q = 2 * ot + (tp >> 1);
           Bf[ot] = tr_pair(dzt + toff<C>(r + 1, pb + 1, q, TW) + 8 * (tp & 1),
                            dzt + toff<C>(r + 1, pb + 5, q, TW) + 8 * (tp & 1));
+          if (ASR_ABLATE == 9)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) Bf[ot][e] = (bf16)(float)(lane + ot + kk + e);
         }
         bf16x8 Ac = loadA(0), An;
 #pragma unroll
