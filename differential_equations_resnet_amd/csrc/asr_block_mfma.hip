@@ -31,6 +31,9 @@
 
 #include "asr_common.h"
 
+#ifndef ASR_BWD_DGRAD_DMA_PCT
+#define ASR_BWD_DGRAD_DMA_PCT 75  // share of the backward's prefetch DMAs issued by the dgrad waves
+#endif
 #ifndef ASR_BWD_DMA_HOOK
 #define ASR_BWD_DMA_HOOK 1  // issue the backward's prefetch inside the dgrad k-steps (0: before the convert)
 #endif
@@ -44,6 +47,31 @@
 namespace asr {
 
 namespace blk {
+
+// Diagnostic build only (-DASR_STAMP_BUILD=1, cdna_hip_programming.md §7
+// in-kernel stamps): s_memtime at phase boundaries of the fused backward,
+// lane 0 of waves 0 (dgrad) and 4 (wgrad), into a buffer nothing else reads.
+#ifndef ASR_STAMP_BUILD
+#define ASR_STAMP_BUILD 0
+#endif
+#if ASR_STAMP_BUILD
+constexpr int kStampBands = 16, kStampSlots = 8;
+__device__ unsigned long long g_stamps[512][2][kStampBands][kStampSlots];
+#define ASR_STAMP(band, slot)                                                                      \
+  do {                                                                                             \
+    if ((wave == 0 || wave == 4) && (band) < kStampBands) {                                        \
+      unsigned long long _t;                                                                       \
+      __builtin_amdgcn_sched_barrier(0);                                                           \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                   \
+      __builtin_amdgcn_sched_barrier(0);                                                           \
+      if (lane == 0) g_stamps[blockIdx.x][wave >> 2][(band)][(slot)] = _t;                         \
+    }                                                                                              \
+  } while (0)
+#else
+#define ASR_STAMP(band, slot) \
+  do {                        \
+  } while (0)
+#endif
 
 enum { FWD_EULER = 0, FWD_CONV = 1, BWD_EULER = 2, BWD_CONV = 3 };
 
@@ -76,8 +104,24 @@ __device__ __attribute__((aligned(16))) uint4 g_zero_page[64];  // 1 KiB of zero
 typedef const __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
+// One 1 KiB LDS-DMA (16 B per lane, lane-linear at the LDS address).  Inline
+// asm, not the builtin: the compiler would otherwise wait vmcnt(0) before
+// every later LDS read of the wave (it cannot tell the DMA's destination
+// apart), serialising the prefetch with the compute.  Every reader of DMA'd
+// data waits with a counted barrier_vm / vm_wait instead.  M0 is reserved
+// by the compiler, so it is saved and restored around the DMA.
 __device__ __forceinline__ void dma16(const void* src, unsigned char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds_wave_base, 16, 0, 0);
+  const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)((ASR_LDS unsigned char*)lds_wave_base));
+  unsigned sv;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(sv)
+      : "v"(src), "s"(l)
+      : "memory");
 }
 
 // DMA image rows [gy0, gy0+nrows) of image n (rows outside [0,H) -> zeros) into
@@ -930,7 +974,11 @@ template <int C, int W, int BR>
 struct BwdLds {
   static constexpr int TW = W + 2;
   static constexpr int TILE = (BR + 2) * TW * (C / 8) * 16;
-  static constexpr int MTB = (((BR + 2) * W * C / 8) + 1023) / 1024 * 1024;  // mask bytes, 1 KiB-rounded
+  static constexpr int RBM = W * C / 8;  // mask bytes per image row
+  // mask bytes per buffer: the band's rows, or 2 copied rows + whole 1 KiB DMAs of the other BR
+  static constexpr int MTB0 = ((BR + 2) * RBM + 1023) / 1024 * 1024;
+  static constexpr int MTB1 = (2 * RBM + (BR * RBM + 1023) / 1024 * 1024 + 1023) / 1024 * 1024;
+  static constexpr int MTB = MTB0 > MTB1 ? MTB0 : MTB1;
   static constexpr int DY = 0;                 // 2 x TILE (dy, halo rows)
   static constexpr int X = DY + 2 * TILE;      // 2 x TILE (x, halo rows)
   static constexpr int DZ = X + 2 * TILE;      // 1 x TILE (dz, halo rows)
@@ -971,6 +1019,71 @@ __device__ __forceinline__ void dma_extra(const bf16* __restrict__ extra, unsign
       dma16(src, priv + k * L::ROWX + q * 1024);
     }
   }
+}
+
+// The prefetch of the next band as one stream of 1 KiB DMA instructions
+// [dy rows | x rows | mask chunks].  When the next band continues the same
+// image, its two top tile rows are this band's two bottom rows: they are
+// copied inside LDS (bwd_halo_copy) and the stream starts at tile row 2.
+template <int C, int W, int BR, bool EULER>
+struct BwdPrefetch {
+  using L = BwdLds<C, W, BR>;
+  static constexpr int IPR = W / Geo<C>::PPI, ROWB = (W + 2) * (C / 8) * 16;
+  int n, gy0, nrows, ni, end;
+  unsigned char *dyt, *xt, *mt;
+  __device__ __forceinline__ void init(const ItemCursor& nx, bool active, bool reuse, unsigned char* lds, int buf, int H) {
+    const int y0 = nx.b * BR, r0 = reuse ? 2 : 0;
+    n = nx.n;
+    gy0 = y0 - 1 + r0;
+    nrows = min(BR, H - y0) + 2 - r0;
+    ni = nrows * IPR;
+    dyt = lds + L::DY + buf * L::TILE + r0 * ROWB;
+    xt = lds + L::X + buf * L::TILE + r0 * ROWB;
+    mt = lds + L::MSK + buf * L::MTB + r0 * L::RBM;
+    end = active ? 2 * ni + (EULER ? (nrows * L::RBM + 1023) / 1024 : 0) : 0;
+  }
+  __device__ __forceinline__ void issue(int u, const bf16* dy, const bf16* x, const uint8_t* mask, int H, unsigned loff,
+                                        int lane) const {
+    if (u < ni)
+      dma_row_instr<C, W>(dy, dyt, n, gy0, u, H, loff);
+    else if (u < 2 * ni)
+      dma_row_instr<C, W>(x, xt, n, gy0, u - ni, H, loff);
+    else
+      dma_mask_instr<C, W>(mask, mt, n, gy0, nrows, u - 2 * ni, H, lane);
+  }
+};
+
+// tile rows BR, BR+1 of this band's dy/x tiles and mask rows -> rows 0, 1 of
+// the next band's buffers (all threads; asm LDS accesses, see lds_rd128)
+template <int C, int W, int BR, bool EULER>
+__device__ __forceinline__ void bwd_halo_copy(unsigned char* lds, int buf, int tid, int nthreads) {
+  using L = BwdLds<C, W, BR>;
+  constexpr int ROWB = (W + 2) * (C / 8) * 16, NR = 2 * ROWB / 16, NM = EULER ? 2 * L::RBM / 16 : 0;
+  constexpr int TOT = 2 * NR + NM, KB = (TOT + 511) / 512;
+  const unsigned base = lds_u32(lds);
+  u32x4 v[KB];
+  unsigned dst[KB];
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    const int c = tid + k * nthreads;
+    const int cc = c < TOT ? c : 0;
+    unsigned src;
+    if (cc < NR) {
+      src = L::DY + buf * L::TILE + BR * ROWB + cc * 16;
+      dst[k] = L::DY + (buf ^ 1) * L::TILE + cc * 16;
+    } else if (cc < 2 * NR) {
+      src = L::X + buf * L::TILE + BR * ROWB + (cc - NR) * 16;
+      dst[k] = L::X + (buf ^ 1) * L::TILE + (cc - NR) * 16;
+    } else {
+      src = L::MSK + buf * L::MTB + BR * L::RBM + (cc - 2 * NR) * 16;
+      dst[k] = L::MSK + (buf ^ 1) * L::MTB + (cc - 2 * NR) * 16;
+    }
+    v[k] = lds_rd128(base + src);
+  }
+  lgkm_wait<0>();
+#pragma unroll
+  for (int k = 0; k < KB; ++k)
+    if (tid + k * nthreads < TOT) lds_wr128(base + dst[k], v[k]);
 }
 
 template <int C, int W, int BR, bool EULER>
@@ -1101,29 +1214,25 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
       const int buf = (it - i0) & 1;
       const int n = cur.n, y0 = cur.b * BR;
       const int rows = min(BR, H - y0);
+      ASR_STAMP(it - i0, 0);
       if (ASR_ABLATE == 10) barrier_lds();
       else barrier_vm(nst);  // item's DMA landed; previous item fully consumed
+      ASR_STAMP(it - i0, 1);
       nst = 0;
       // prefetch of band it+1: dy rows, x rows, mask chunks as one stream of
-      // instructions dealt round-robin to the 4 dgrad waves; issued one per
-      // k-step of the wave's first dgrad row (so the issue cost overlaps the
-      // MFMAs of both roles), the rest flushed before that row's epilogue
-      int nd = 0;                               // prefetch instructions this wave issued
-      int du = wv4, dend = 0, dni = 0, dnr = 0;  // wave-uniform stream cursor
-      const int dy0 = nxt.b * BR - 1;
-      if (ASR_ABLATE != 8 && it + 1 < i1) {
-        dnr = min(BR, H - nxt.b * BR) + 2;
-        dni = dnr * (W / G::PPI);
-        dend = 2 * dni + (EULER ? (dnr * (W * C / 8) + 1023) / 1024 : 0);
-      }
+      // instructions dealt round-robin to all 8 waves; a dgrad wave issues
+      // its share one per k-step of its first dgrad row (so the issue cost
+      // overlaps MFMAs), the rest flushed before that row's epilogue
+      int nd = 0;  // prefetch instructions this wave issued
+      const bool reuse = it + 1 < i1 && nxt.n == cur.n;
+      BwdPrefetch<C, W, BR, EULER> pf;
+      pf.init(nxt, ASR_ABLATE != 8 && it + 1 < i1, reuse, lds, buf ^ 1, H);
+      const int dsplit = (pf.end * ASR_BWD_DGRAD_DMA_PCT) / 100;  // dgrad waves: [0, dsplit)
+      int du = wv4;                                               // wave-uniform stream cursor
+      const int dend = dsplit;
       auto dma_one = [&]() {
         if (du < dend) {
-          if (du < dni)
-            dma_row_instr<C, W>(dy, lds + L::DY + (buf ^ 1) * L::TILE, nxt.n, dy0, du, H, loff);
-          else if (du < 2 * dni)
-            dma_row_instr<C, W>(x, lds + L::X + (buf ^ 1) * L::TILE, nxt.n, dy0, du - dni, H, loff);
-          else
-            dma_mask_instr<C, W>(mask, lds + L::MSK + (buf ^ 1) * L::MTB, nxt.n, dy0, dnr, du - 2 * dni, H, lane);
+          pf.issue(du, dy, x, mask, H, loff, lane);
           du += 4;
           nst = 0;  // the next barrier waits for this prefetch; stores issued after it need not finish
           ++nd;
@@ -1132,8 +1241,11 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
       if (!ASR_BWD_DMA_HOOK)
         while (du < dend) dma_one();
       bool ex_wait = has_extra;
+      if (reuse) bwd_halo_copy<C, W, BR, EULER>(lds, buf, tid, 512);
       if (ASR_ABLATE != 4) bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, tid, 512);
+      ASR_STAMP(it - i0, 2);
       barrier_lds();  // dz ready
+      ASR_STAMP(it - i0, 3);
       const unsigned char* dzt = lds + L::DZ;
       const unsigned char* dyt = lds + L::DY + buf * L::TILE;
 #pragma unroll
@@ -1149,6 +1261,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
           if (ASR_BWD_DMA_HOOK && k == 0) {
             conv_row<C, W>(dzt, r, A, boff, acc, dma_one);
             while (du < dend) dma_one();
+            ASR_STAMP(it - i0, 4);
           } else {
             conv_row<C, W>(dzt, r, A, boff, acc);
           }
@@ -1227,6 +1340,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
             if (dx) *(bf16x4*)(dx + (((long)n * H + gy) * W + px) * C + o0) = o4;
           }
         }
+        ASR_STAMP(it - i0, 5 + k);
       }
       while (du < dend) dma_one();  // a wave without rows in this band
       if (has_extra && it + 1 < i1) {  // next band's extra rows into the (now read) private rows
@@ -1268,14 +1382,38 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
     for (int mi = 0; mi < MTW; ++mi)
 #pragma unroll
       for (int ot = 0; ot < OT; ++ot) acc[mi][ot] = f32x4{0.f, 0.f, 0.f, 0.f};
-    ItemCursor cur(i0, nb);
-    for (int it = i0; it < i1; ++it, cur.next(nb)) {
+    const int wv8 = __builtin_amdgcn_readfirstlane(wave);
+    const unsigned loff = (unsigned)dma_lane_off<C, W>(lane) * 2u;
+    ItemCursor cur(i0, nb), nxt(i0, nb);
+    nxt.next(nb);
+    for (int it = i0; it < i1; ++it, cur.next(nb), nxt.next(nb)) {
       const int buf = (it - i0) & 1;
       const int y0 = cur.b * BR;
       const int rows = min(BR, H - y0);
-      barrier_vm(0);
+      ASR_STAMP(it - i0, 0);
+      barrier_vm(0);  // this wave's share of the band's prefetch landed (no stores in flight)
+      ASR_STAMP(it - i0, 1);
+      // this wave's share of band it+1's prefetch (see the dgrad waves),
+      // issued after the dz barrier, while the dgrad wave on this SIMD runs
+      // its MFMAs
+      const bool reuse = it + 1 < i1 && nxt.n == cur.n;
+      BwdPrefetch<C, W, BR, EULER> pf;
+      pf.init(nxt, ASR_ABLATE != 8 && it + 1 < i1, reuse, lds, buf ^ 1, H);
+      int du = (pf.end * ASR_BWD_DGRAD_DMA_PCT) / 100 + wv8 - 4;  // wgrad waves: [dsplit, end)
+      const int dend = pf.end;
+      auto dma_one = [&]() {
+        if (du < dend) {
+          pf.issue(du, dy, x, mask, H, loff, lane);
+          du += 4;
+        }
+      };
+      if (reuse) bwd_halo_copy<C, W, BR, EULER>(lds, buf, tid, 512);
       if (ASR_ABLATE != 4) bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, tid, 512);
+      ASR_STAMP(it - i0, 2);
       barrier_lds();
+      ASR_STAMP(it - i0, 3);
+      while (du < dend) dma_one();
+      ASR_STAMP(it - i0, 4);
       const unsigned char* dzt = lds + L::DZ;
       const unsigned char* xt = lds + L::X + buf * L::TILE;
       for (int kk = kg; kk < (ASR_ABLATE == 6 ? 0 : rows * KPR); kk += G::KSPLIT) {
@@ -1315,6 +1453,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
           if (mi + 1 < MTW) Ac = An;
         }
       }
+      ASR_STAMP(it - i0, 5);
     }
     barrier_vm(0);  // all items consumed: LDS reusable
     float* red = (float*)lds;
@@ -1498,3 +1637,10 @@ int block_bwd_mfma(int mode, const void* dy, const void* x, const uint8_t* mask,
 }
 
 }  // namespace asr
+
+#if ASR_STAMP_BUILD
+extern "C" int asr_debug_stamps(void* host, size_t bytes) {
+  if (bytes > sizeof(asr::blk::g_stamps)) bytes = sizeof(asr::blk::g_stamps);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(asr::blk::g_stamps), bytes) == hipSuccess ? 0 : -4;
+}
+#endif
