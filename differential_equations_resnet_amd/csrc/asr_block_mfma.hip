@@ -915,10 +915,13 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
       epi_all(accA, xrA, cur);
       break;
     }
+    ASR_STAMP(it - i0, 0);
     barrier_vm(nst);  // band it+1 landed, every wave is done with band it's tile
+    ASR_STAMP(it - i0, 1);
     nst = 0;
     dma_res(nx1, (it + 1 - i0) & 1);
     if (it + 2 < i1) dma(nx2, (it - i0) & 1);
+    ASR_STAMP(it - i0, 2);
     res_read((it - i0) & 1, xrA);
     init(accB);
     {
@@ -926,7 +929,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
       auto hook = [&](auto U) { epi_unit(U, accA, xrA, c); };
       conv_band<C, W, RB, NU>(lds_u32(lds + ((it + 1 - i0) & 1) * TILE + r0 * BD::ROWB), lo, A, accB, hook);
     }
+    ASR_STAMP(it - i0, 3);
     xres_read((it + 1 - i0) & 1, xrB);
+    ASR_STAMP(it - i0, 4);
     ++it;
     cur.next(nb);
     nx1.next(nb);
@@ -940,10 +945,13 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
       epi_all(accB, xrB, cur);
       break;
     }
+    ASR_STAMP(it - i0, 0);
     barrier_vm(nst);
+    ASR_STAMP(it - i0, 1);
     nst = 0;
     dma_res(nx1, (it + 1 - i0) & 1);
     if (it + 2 < i1) dma(nx2, (it - i0) & 1);
+    ASR_STAMP(it - i0, 2);
     res_read((it - i0) & 1, xrB);
     init(accA);
     {
@@ -951,7 +959,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
       auto hook = [&](auto U) { epi_unit(U, accB, xrB, c); };
       conv_band<C, W, RB, NU>(lds_u32(lds + ((it + 1 - i0) & 1) * TILE + r0 * BD::ROWB), lo, A, accA, hook);
     }
+    ASR_STAMP(it - i0, 3);
     xres_read((it + 1 - i0) & 1, xrA);
+    ASR_STAMP(it - i0, 4);
     ++it;
     cur.next(nb);
     nx1.next(nb);

@@ -11,46 +11,88 @@
 
 #include "asr_common.h"
 
+#ifndef ASR_ABLATE
+#define ASR_ABLATE 0  // development only: stem wgrad 11 no FMA loop, 12 no dx1/x1 loads
+#endif
+
 namespace asr {
 
-// LDS image: (H+2) x (W+2) x CIN floats, normalised, zero halo
+// LDS image: (H+2) x (W+2) x CIN floats, normalised, zero halo.  The halo
+// is written once (zero_tile_halo); stage_image fills the interior from
+// 16-byte vector loads, all of a thread's loads issued before their use (one
+// image per workgroup: a latency-serialised element loop dominated the stem).
+template <int CIN>
+__device__ __forceinline__ void zero_tile(float* tile, int H, int W) {
+  for (int i = threadIdx.x; i < (H + 2) * (W + 2) * CIN; i += blockDim.x) tile[i] = 0.f;
+}
+
 template <int CIN, typename Tin>
 __device__ __forceinline__ void stage_image(const Tin* __restrict__ img, float* tile, int H, int W, float mean,
                                             float inv_std, int use_norm) {
-  const int TW = W + 2;
-  const int n = (H + 2) * TW * CIN;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const int c = i % CIN, pc = i / CIN, col = pc % TW, r = pc / TW;
-    const int y = r - 1, x = col - 1;
-    float v = 0.f;
-    if (y >= 0 && y < H && x >= 0 && x < W) {
-      v = (float)img[((long)y * W + x) * CIN + c];
-      if (use_norm) v = (v - mean) * inv_std;
+  constexpr int EPV = 16 / sizeof(Tin);  // elements per 16-B vector
+  constexpr int KV = 4;                  // vectors in flight per thread
+  const int TW = W + 2, nel = H * W * CIN;
+  const bool vec_ok = ((uintptr_t)img % 16 == 0);  // images of a 16-B multiple (e.g. 32x32x3 u8) stay aligned
+  const int nvec = vec_ok ? nel / EPV : 0;
+  for (int v0 = threadIdx.x; v0 < nvec; v0 += KV * blockDim.x) {
+    uint4 r[KV];
+#pragma unroll
+    for (int k = 0; k < KV; ++k) {
+      const int vi = v0 + k * blockDim.x;
+      r[k] = vi < nvec ? *(const uint4*)(img + (long)vi * EPV) : make_uint4(0, 0, 0, 0);
     }
-    tile[i] = v;
+#pragma unroll
+    for (int k = 0; k < KV; ++k) {
+      const int vi = v0 + k * blockDim.x;
+      if (vi >= nvec) continue;
+      const Tin* e = (const Tin*)&r[k];
+#pragma unroll
+      for (int j = 0; j < EPV; ++j) {
+        const int o = vi * EPV + j, c = o % CIN, pix = o / CIN;
+        float v = (float)e[j];
+        if (use_norm) v = (v - mean) * inv_std;
+        tile[((pix / W + 1) * TW + pix % W + 1) * CIN + c] = v;
+      }
+    }
+  }
+  for (int o = nvec * EPV + threadIdx.x; o < nel; o += blockDim.x) {  // tail (nel % EPV)
+    const int c = o % CIN, pix = o / CIN;
+    float v = (float)img[o];
+    if (use_norm) v = (v - mean) * inv_std;
+    tile[((pix / W + 1) * TW + pix % W + 1) * CIN + c] = v;
   }
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 // conv1 forward: out = relu(conv3x3(norm(img)) + b); one image per block
 // iteration; thread = (VEC-channel group, pixel lane) with its 9*CIN*VEC
-// weights in registers, the normalised image tile in LDS.
+// weights in registers, the normalised image tile in LDS.  Channel pairs
+// are accumulated with packed FMAs (v_pk_fma_f32: two fp32 FMAs per lane,
+// bitwise the fmaf chain of the scalar form).
 template <int CIN, typename Tin, typename Tout, int VEC>
 __global__ __launch_bounds__(256) void k_stem_fwd(const Tin* __restrict__ img, const float* __restrict__ w1,
                                                   const float* __restrict__ b1, int N, int H, int W, int C,
                                                   float mean, float inv_std, int use_norm, Tout* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* tile = sm;  // (H+2)(W+2)CIN
+  constexpr int VP = (VEC + 1) / 2;  // channel pairs
   const int NG = C / VEC, PLN = max(1, 256 / NG);
   const int cg = threadIdx.x % NG, pl = threadIdx.x / NG;
   const bool active = threadIdx.x < PLN * NG;
-  float wr[9 * CIN][VEC], bz[VEC];
+  f32x2 wr[9 * CIN][VP], bz[VP];
 #pragma unroll
   for (int k = 0; k < 9 * CIN; ++k)
 #pragma unroll
-    for (int v = 0; v < VEC; ++v) wr[k][v] = active ? w1[k * C + cg * VEC + v] : 0.f;
+    for (int v = 0; v < VP; ++v)
+      wr[k][v] = f32x2{active ? w1[k * C + cg * VEC + 2 * v] : 0.f,
+                       (active && 2 * v + 1 < VEC) ? w1[k * C + cg * VEC + 2 * v + 1] : 0.f};
 #pragma unroll
-  for (int v = 0; v < VEC; ++v) bz[v] = (active && b1) ? b1[cg * VEC + v] : 0.f;
+  for (int v = 0; v < VP; ++v)
+    bz[v] = f32x2{(active && b1) ? b1[cg * VEC + 2 * v] : 0.f,
+                  (active && b1 && 2 * v + 1 < VEC) ? b1[cg * VEC + 2 * v + 1] : 0.f};
   const int TW = W + 2;
+  zero_tile<CIN>(tile, H, W);
   for (int n = blockIdx.x; n < N; n += gridDim.x) {
     __syncthreads();
     stage_image<CIN>(img + (long)n * H * W * CIN, tile, H, W, mean, inv_std, use_norm);
@@ -58,9 +100,9 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const Tin* __restrict__ img, c
     if (!active) continue;
     for (int p = pl; p < H * W; p += PLN) {
       const int x = p % W, y = p / W;
-      float acc[VEC];
+      f32x2 acc[VP];
 #pragma unroll
-      for (int v = 0; v < VEC; ++v) acc[v] = bz[v];
+      for (int v = 0; v < VP; ++v) acc[v] = bz[v];
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const float* tp = tile + ((y + tap / 3) * TW + x + tap % 3) * CIN;
@@ -68,85 +110,121 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const Tin* __restrict__ img, c
         for (int ci = 0; ci < CIN; ++ci) {
           const float xv = tp[ci];
 #pragma unroll
-          for (int v = 0; v < VEC; ++v) acc[v] = fmaf(xv, wr[tap * CIN + ci][v], acc[v]);
+          for (int v = 0; v < VP; ++v) acc[v] = __builtin_elementwise_fma(f32x2{xv, xv}, wr[tap * CIN + ci][v], acc[v]);
         }
       }
       Tout* o = out + ((long)n * H * W + p) * C + cg * VEC;
       if constexpr (VEC == 4 && sizeof(Tout) == 2) {
         bf16x4 r;
 #pragma unroll
-        for (int v = 0; v < 4; ++v) r[v] = (bf16)fmaxf(acc[v], 0.f);
+        for (int v = 0; v < 4; ++v) r[v] = (bf16)fmaxf(acc[v / 2][v % 2], 0.f);
         *(bf16x4*)o = r;
       } else {
 #pragma unroll
-        for (int v = 0; v < VEC; ++v) o[v] = from_f32<Tout>(fmaxf(acc[v], 0.f));
+        for (int v = 0; v < VEC; ++v) o[v] = from_f32<Tout>(fmaxf(acc[v / 2][v % 2], 0.f));
       }
     }
   }
 }
 
-// conv1 weight gradient: dz1 = dx1 * [x1 > 0]; slab[blk] = [dW1 (9*CIN*C) | db1 (C)]
-// thread = (pixel lane pl, output channel o); one image per block iteration.
+// conv1 weight gradient: dz1 = dx1 * [x1 > 0]; slab[blk] = [dW1 (9*CIN*C) | db1 (C)].
+// Thread = (4-channel group cg, pixel lane); the normalised image tile in
+// LDS, one broadcast LDS read per tap feeds 4 channels (packed FMAs).  The
+// pixel lanes of a wave reduce by shuffles, the 4 waves through LDS (fixed
+// order: deterministic).  C % 4 == 0 and C <= 64.
 template <int CIN, typename Tin, typename T>
 __global__ __launch_bounds__(256) void k_stem_wgrad(const Tin* __restrict__ img, const T* __restrict__ dx1,
                                                     const T* __restrict__ x1, int N, int H, int W, int C, float mean,
                                                     float inv_std, int use_norm, float* __restrict__ slabs) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int KC = 9 * CIN;
-  const int PG = max(1, 256 / C);
-  const int tid = threadIdx.x;
-  const int o = tid % C, pl = tid / C;
-  const bool active = pl < PG && tid < PG * C;
-  float acc[KC + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int NG = C / 4;     // channel groups (<= 16)
+  const int PL = 256 / NG;  // pixel lanes
+  const int cg = tid % NG, pl = tid / NG;
+  f32x2 acc[KC + 1][2];
 #pragma unroll
-  for (int k = 0; k <= KC; ++k) acc[k] = 0.f;
+  for (int k = 0; k <= KC; ++k) acc[k][0] = acc[k][1] = f32x2{0.f, 0.f};
   float* tile = sm;
   const int TW = W + 2;
+  zero_tile<CIN>(tile, H, W);
   for (int n = blockIdx.x; n < N; n += gridDim.x) {
     __syncthreads();
     stage_image<CIN>(img + (long)n * H * W * CIN, tile, H, W, mean, inv_std, use_norm);
     __syncthreads();
-    if (active) {
-      const T* d = dx1 + (long)n * H * W * C;
-      const T* a = x1 + (long)n * H * W * C;
-      constexpr int U = 8;  // pixels per batch: all global loads issued before use
-      for (int p0 = pl; p0 < H * W; p0 += U * PG) {
-        float gv[U];
+    const T* d = dx1 + (long)n * H * W * C + cg * 4;
+    const T* a = x1 + (long)n * H * W * C + cg * 4;
+    constexpr int U = 4;  // pixels per batch: all global loads issued before use
+    for (int p0 = pl; p0 < H * W; p0 += U * PL) {
+      f32x2 gv[U][2];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int p = p0 + u * PG;
-          const int pc = p < H * W ? p : 0;
-          const float dv = to_f32(d[(long)pc * C + o]);
-          const float av = to_f32(a[(long)pc * C + o]);
-          gv[u] = (p < H * W && av > 0.f) ? dv : 0.f;
+      for (int u = 0; u < U; ++u) {
+        const int p = p0 + u * PL;
+        const int pc = p < H * W ? p : 0;
+        float dv[4], av[4];
+        if (ASR_ABLATE == 12) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) dv[v] = (float)(pc + v), av[v] = 1.f;
+        } else if constexpr (sizeof(T) == 2) {
+          const bf16x4 d4 = *(const bf16x4*)(d + (long)pc * C), a4 = *(const bf16x4*)(a + (long)pc * C);
+#pragma unroll
+          for (int v = 0; v < 4; ++v) dv[v] = (float)d4[v], av[v] = (float)a4[v];
+        } else {
+          const float4 d4 = *(const float4*)(d + (long)pc * C), a4 = *(const float4*)(a + (long)pc * C);
+          dv[0] = d4.x, dv[1] = d4.y, dv[2] = d4.z, dv[3] = d4.w;
+          av[0] = a4.x, av[1] = a4.y, av[2] = a4.z, av[3] = a4.w;
         }
+        float g4[4];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int p = p0 + u * PG;
-          const int pc = p < H * W ? p : 0;
-          const int x = pc % W, y = pc / W;
+        for (int v = 0; v < 4; ++v) g4[v] = (p < H * W && av[v] > 0.f) ? dv[v] : 0.f;
+        gv[u][0] = f32x2{g4[0], g4[1]};
+        gv[u][1] = f32x2{g4[2], g4[3]};
+        if (ASR_ABLATE == 11) acc[u][0] += gv[u][0] + gv[u][1];
+      }
 #pragma unroll
-          for (int tap = 0; tap < 9; ++tap) {
-            const float* tp = tile + ((y + tap / 3) * TW + x + tap % 3) * CIN;
+      for (int u = 0; u < (ASR_ABLATE == 11 ? 0 : U); ++u) {
+        const int p = p0 + u * PL;
+        const int pc = p < H * W ? p : 0;
+        const int x = pc % W, y = pc / W;
 #pragma unroll
-            for (int ci = 0; ci < CIN; ++ci) acc[tap * CIN + ci] = fmaf(tp[ci], gv[u], acc[tap * CIN + ci]);
+        for (int tap = 0; tap < 9; ++tap) {
+          const float* tp = tile + ((y + tap / 3) * TW + x + tap % 3) * CIN;
+#pragma unroll
+          for (int ci = 0; ci < CIN; ++ci) {
+            const float xv = tp[ci];
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+              acc[tap * CIN + ci][h] = __builtin_elementwise_fma(f32x2{xv, xv}, gv[u][h], acc[tap * CIN + ci][h]);
           }
-          acc[KC] += gv[u];
         }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) acc[KC][h] += gv[u][h];
       }
     }
   }
-  __syncthreads();
-  float* red = sm;  // [PG][KC+1][C]
-  if (active)
+  // pixel lanes of this wave: lanes cg, cg+NG, ... (NG divides 64)
 #pragma unroll
-    for (int k = 0; k <= KC; ++k) red[((long)pl * (KC + 1) + k) * C + o] = acc[k];
+  for (int k = 0; k <= KC; ++k)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        float v = acc[k][h][e];
+        for (int off = NG; off < 64; off <<= 1) v += __shfl_xor(v, off);
+        acc[k][h][e] = v;
+      }
+  __syncthreads();
+  float* red = sm;  // [4 waves][KC+1][C]
+  if (lane < NG)
+#pragma unroll
+    for (int k = 0; k <= KC; ++k)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) red[((long)wave * (KC + 1) + k) * C + cg * 4 + v] = acc[k][v / 2][v % 2];
   __syncthreads();
   float* slab = slabs + (long)blockIdx.x * (KC * C + C);
   for (int i = tid; i < (KC + 1) * C; i += blockDim.x) {
-    float s = 0.f;
-    for (int g = 0; g < PG; ++g) s += red[(long)g * (KC + 1) * C + i];
-    slab[i] = s;  // i = k*C + o: k < KC -> HWIO dW1, k == KC -> db1
+    const long st = (long)(KC + 1) * C;
+    slab[i] = (red[i] + red[st + i]) + (red[2 * st + i] + red[3 * st + i]);  // i = k*C + o
   }
 }
 
@@ -322,9 +400,9 @@ __global__ __launch_bounds__(256) void k_head_param_grads(const float* __restric
 constexpr int kMaxSlabsStem = 512;
 
 bool stem_supported(int Cin, int H, int W, int C) {
-  const size_t lds = ((size_t)9 * Cin * C + ((C + 3) & ~3) + (size_t)(H + 2) * (W + 2) * Cin) * 4;
-  const size_t red = (size_t)std::max(1, 256 / C) * (9 * Cin + 1) * C * 4;
-  return (Cin == 1 || Cin == 3) && C <= 256 && lds <= 64 * 1024 && red <= 64 * 1024;
+  const size_t lds = (size_t)(H + 2) * (W + 2) * Cin * 4;
+  const size_t red = (size_t)4 * (9 * Cin + 1) * C * 4;
+  return (Cin == 1 || Cin == 3) && C % 4 == 0 && C <= 64 && lds <= 64 * 1024 && red <= 64 * 1024;
 }
 
 static int stem_grid(int N) { return std::max(1, std::min(N, kMaxSlabsStem)); }
@@ -362,8 +440,7 @@ int stem_wgrad(const void* img, int input_u8, const void* dx1, const void* x1, i
   if (!stem_supported(Cin, H, W, C)) return fail(ASR_E_UNSUPPORTED, "stem: unsupported shape");
   const int grid = stem_grid(N);
   *nslabs = grid;
-  const size_t lds = std::max((size_t)(H + 2) * (W + 2) * Cin * 4,
-                              (size_t)std::max(1, 256 / C) * (9 * Cin + 1) * C * 4);
+  const size_t lds = std::max((size_t)(H + 2) * (W + 2) * Cin * 4, (size_t)4 * (9 * Cin + 1) * C * 4);
 #define ASR_STEM_W(CI, TI, T)                                                                                   \
   hipLaunchKernelGGL((k_stem_wgrad<CI, TI, T>), dim3(grid), dim3(256), lds, s, (const TI*)img, (const T*)dx1, \
                      (const T*)x1, N, H, W, C, mean, inv_std, use_norm, slabs)

@@ -14,6 +14,7 @@ import torch  # noqa: E402
 
 from differential_equations_resnet_amd import _lib, runtime as rt  # noqa: E402
 
+WHAT = os.environ.get("STAMP_WHAT", "bwd")
 dev = rt.require_gpu()
 lib = _lib.load()
 N, H, W, C = 512, 32, 32, 64
@@ -35,10 +36,13 @@ _, tdst = pm.device(dev)
 s = torch.cuda.current_stream().cuda_stream
 _lib.check(lib.asr_conv_forward(0, x.data_ptr(), y.data_ptr(), mask.data_ptr(), w.data_ptr(), bias.data_ptr(), 0.25,
                                 N, H, W, C, 1, s))
-for _ in range(3):
+for _ in range(3 if WHAT == "bwd" else 0):
     _lib.check(lib.asr_conv_backward(0, dy.data_ptr(), x.data_ptr(), mask.data_ptr(), w.data_ptr(), tdst.data_ptr(),
                                      pm.n_theta, 0.25, 0.0, N, H, W, C, 1, dx.data_ptr(), dth.data_ptr(),
                                      db.data_ptr(), None, ws.data_ptr(), wsb, s))
+for _ in range(3 if WHAT == "fwd" else 0):
+    _lib.check(lib.asr_conv_forward(0, x.data_ptr(), y.data_ptr(), mask.data_ptr(), w.data_ptr(), bias.data_ptr(),
+                                    0.25, N, H, W, C, 1, s))
 torch.cuda.synchronize()
 st = np.zeros((512, 2, 16, 8), dtype=np.uint64)
 fn = lib.asr_debug_stamps
@@ -48,10 +52,13 @@ assert fn(st.ctypes.data, st.nbytes) == 0
 st = st.astype(np.int64)
 grid = int((st[:, 0, 0, 0] != 0).sum())
 st = st[:grid]
-names = {0: ["barrier_vm", "convert", "barrier_lds", "row0 conv+dma", "row0 epi", "row1 conv+epi", "tail"],
-         1: ["barrier_vm", "convert", "barrier_lds", "dma share", "wgrad kk loop", "tail"]}
-nb = 16
-for role in (0, 1):
+if WHAT == "fwd":
+    names = {0: ["barrier_vm", "dma issue", "conv+epilogue hooks", "xres read", "loop"]}
+else:
+    names = {0: ["barrier_vm", "convert", "barrier_lds", "row0 conv+dma", "row0 epi", "row1 conv+epi", "tail"],
+             1: ["barrier_vm", "convert", "barrier_lds", "dma share", "wgrad kk loop", "tail"]}
+nb = 16 if WHAT == "bwd" else 8
+for role in names:
     seg = []
     for b in range(1, nb - 1):
         row = st[:, role, b, :]
@@ -61,6 +68,6 @@ for role in (0, 1):
         seg.append(np.stack(d, 1))
     seg = np.concatenate(seg)
     tot = seg.sum(1).mean()
-    print(f"role {'dgrad' if role == 0 else 'wgrad'}: band = {tot:.0f} cycles")
+    print(f"{WHAT} role {role} ({['dgrad/fwd wave 0', 'wgrad wave 4'][role]}): band = {tot:.0f} cycles")
     for i, n in enumerate(names[role]):
         print(f"   {n:>16s} {seg[:, i].mean():8.0f}  {100 * seg[:, i].mean() / tot:5.1f}%")
