@@ -1,0 +1,122 @@
+"""GPU checks at BASELINE.json's full sizes (configs[1] C2: N=512, C=64;
+configs[2] C3: N=1024, C=16, 108 blocks; configs[4] C5: RK2 at the C2 shape).
+
+The fp64 oracle cannot run a whole batch at these sizes in seconds, so parity
+is checked through properties that do not depend on the size:
+  * per-image spot checks: a block's forward output and input gradient of an
+    image depend only on that image, so 2 sampled images are compared with
+    the oracle (bf16 tolerances of test_gpu_kernels.py);
+  * additivity over the batch: the weight gradient of the whole batch equals
+    the sum of the gradients of its two halves (the slab reduction at full
+    grid size) within fp32 reduction-order noise (1e-5 of max|g|);
+  * the network: the batch-mean loss and gradients of the whole batch equal
+    the mean of the two halves' (1e-4 of max|g| per tensor, bf16 ordering
+    noise), and two calls are bitwise identical (deterministic reductions).
+"""
+import numpy as np
+import pytest
+
+from helpers import assert_close, bf16_round, decode_mask
+from oracle import asr_oracle as O
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def rt():
+    from differential_equations_resnet_amd import runtime
+    runtime.require_gpu()
+    return runtime
+
+
+def _theta(C, seed):
+    return O.flatten(O.init_theta_3by3(C, np.random.default_rng(seed), np.float64)).astype(np.float32)
+
+
+@pytest.mark.parametrize("N,C,integrator", [(512, 64, "euler"), (1024, 16, "euler"), (512, 64, "rk2")])
+def test_block_fullsize(rt, N, C, integrator):
+    H = W = 32
+    h, gamma = 8.0 / 30, -0.05
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(N + C)
+    x = torch.randn(N, H, W, C, device=dev, generator=g).to(torch.bfloat16)
+    dy = torch.randn(N, H, W, C, device=dev, generator=g).to(torch.bfloat16)
+    th = _theta(C, 3)
+    pm = rt.param_map(C)
+    w = rt.theta_to_w(torch.from_numpy(th).to(dev), C, pm, gamma, rt.ASR_BF16)
+    b = (np.random.default_rng(1).standard_normal(C) * 0.1).astype(np.float32)
+    bias = torch.from_numpy(b).to(dev)
+
+    def run(sl):
+        xs, dys = x[sl].contiguous(), dy[sl].contiguous()
+        if integrator == "rk2":
+            y, xm, m1, m2 = rt.rk2_forward(xs, w, bias, h)
+            dx, dth, db, _ = rt.rk2_backward(dys, xs, xm, m1, m2, w, pm, h, gamma)
+            return y, dx, dth, db, (xm, m1, m2)
+        mask = torch.zeros(rt.mask_bytes(xs.shape[0], H, W, C), dtype=torch.uint8, device=dev)
+        y = rt.conv_forward(rt.ASR_MODE_EULER, xs, w, bias, h, mask)
+        dx, dth, db, _ = rt.conv_backward(rt.ASR_MODE_EULER, dys, xs, mask, w, pm, h, gamma)
+        return y, dx, dth, db, (mask,)
+
+    y, dx, dth, db, aux = run(slice(None))
+    _, _, dth1, db1, _ = run(slice(0, N // 2))
+    _, _, dth2, db2, _ = run(slice(N // 2, N))
+    torch.cuda.synchronize()
+    # additivity of the weight gradient over the batch (full-grid slab reduction)
+    for full, a, bb, what in ((dth, dth1, dth2, "dtheta"), (db, db1, db2, "dbias")):
+        f, s = full.cpu().numpy(), (a + bb).cpu().numpy()
+        assert np.abs(f - s).max() <= 1e-5 * np.abs(f).max(), what
+    # per-image spot checks against the oracle (same bf16-rounded inputs)
+    src, sign = O.param_map(C)
+    Wo = bf16_round(O.assemble_from_map(th.astype(np.float64), C, src, sign, gamma)).astype(np.float64)
+    for n in (0, N - 1):
+        xo = x[n:n + 1].float().cpu().numpy().astype(np.float64)
+        dyo = dy[n:n + 1].float().cpu().numpy().astype(np.float64)
+        if integrator == "rk2":
+            xm_gpu = aux[0][n:n + 1].float().cpu().numpy().astype(np.float64)
+            z1 = O.conv2d_same(xo, Wo) + b
+            assert_close(xm_gpu, xo + 0.5 * h * np.maximum(z1, 0), rtol=2 ** -8,
+                         atol=4e-3 * np.abs(xm_gpu).max(), what="xmid")
+            z2 = O.conv2d_same(xm_gpu, Wo) + b
+            y_want = xo + h * np.maximum(z2, 0)
+        else:
+            z = O.conv2d_same(xo, Wo) + b
+            y_want = xo + h * np.maximum(z, 0)
+            m = decode_mask(aux[0].cpu().numpy(), N, H, W, C)[n:n + 1]
+            dz = bf16_round(h * dyo * m).astype(np.float64)
+            dx_want = dyo - O.conv2d_same(dz, Wo) + 2 * gamma * dz
+            assert_close(dx[n:n + 1].float().cpu().numpy(), dx_want, rtol=2 ** -8,
+                         atol=4e-3 * np.abs(dx_want).max(), what="dx")
+        assert_close(y[n:n + 1].float().cpu().numpy(), y_want, rtol=2 ** -8, atol=4e-3 * np.abs(y_want).max(),
+                     what="y")
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c5"])
+def test_network_fullsize_properties(rt, cfg):
+    C, L, N, integ = {"c2": (64, 30, 512, "euler"), "c3": (16, 108, 1024, "euler"), "c5": (64, 30, 512, "rk2")}[cfg]
+    from differential_equations_resnet_amd.netparams import init_net_params
+    h = 8.0 / L
+    dev = torch.device("cuda")
+    params = torch.from_numpy(init_net_params(C, L, 3, 10, seed=0) * 0.5).to(dev)
+    rng = np.random.default_rng(7)
+    imgs = torch.from_numpy(rng.integers(0, 256, (N, 32, 32, 3), dtype=np.uint8)).to(dev)
+    tgt = torch.from_numpy(np.eye(10, dtype=np.float32)[rng.integers(0, 10, N)]).to(dev)
+
+    def ex(n):
+        return rt.NetExecutor(n, 32, 32, 3, C, L, 10, h, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
+                              dtype="bfloat16", input_u8=True, device=dev, integrator=integ)
+    full, half = ex(N), ex(N // 2)
+    loss, g = full.forward_backward(params, imgs, tgt)
+    loss, g = loss.clone(), g.clone()
+    loss2, g2 = full.forward_backward(params, imgs, tgt)
+    assert torch.equal(g, g2) and torch.equal(loss, loss2), "forward_backward is not deterministic"
+    la, ga = half.forward_backward(params, imgs[:N // 2].contiguous(), tgt[:N // 2].contiguous())
+    la, ga = la.clone(), ga.clone()
+    lb, gb = half.forward_backward(params, imgs[N // 2:].contiguous(), tgt[N // 2:].contiguous())
+    torch.cuda.synchronize()
+    assert np.isfinite(loss.item())
+    assert abs(loss.item() - 0.5 * (la.item() + lb.item())) <= 1e-5 * abs(loss.item())
+    gm = (0.5 * (ga + gb)).cpu().numpy()
+    gf = g.cpu().numpy()
+    assert np.abs(gf - gm).max() <= 1e-4 * np.abs(gf).max()
