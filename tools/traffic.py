@@ -16,10 +16,23 @@ for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursiv
     for r in csv.DictReader(open(f)):
         vals[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 per = {}
+def demangle(name):
+    """c++filt does not know the __bf16 mangling (DF16b): name our kernels by hand."""
+    if name.startswith("_Z") and "3asr" in name:
+        import re
+        m = re.search(r"\d+(k_[a-z_0-9]+)", name)
+        if m:
+            return "asr::" + m.group(1) + "<" + name + ">("
+    return name
+
+
 for k, cs in vals.items():
+    k = demangle(k)
     if "asr::" not in k or "theta_to_w" in k:  # W materialisation: once per step for all L blocks
         continue
     short = k.split("(")[0].replace("void ", "")
+    if "<_Z" in short:
+        short = short.split("<")[0]
     fetch = sum(cs["FETCH_SIZE"]) / max(len(cs["FETCH_SIZE"]), 1) * 1024 * 2 if "FETCH_SIZE" in cs else 0.0
     write = sum(cs["WRITE_SIZE"]) / max(len(cs["WRITE_SIZE"]), 1) * 1024 if "WRITE_SIZE" in cs else 0.0
     per[short] = {"read_bytes": round(fetch), "write_bytes": round(write), "launches": len(cs.get("FETCH_SIZE", []))}
