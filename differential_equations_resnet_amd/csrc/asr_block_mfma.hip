@@ -37,6 +37,18 @@
 #ifndef ASR_BWD_DMA_HOOK
 #define ASR_BWD_DMA_HOOK 1  // issue the backward's prefetch inside the dgrad k-steps (0: before the convert)
 #endif
+#ifndef ASR_V2_MASKTAB
+#define ASR_V2_MASKTAB 1  // v2 backward convert: relu-mask expansion from a 4 KiB LDS table (0: bit ops)
+#endif
+#ifndef ASR_V2_XHOOK
+#define ASR_V2_XHOOK 0  // v2 backward: wgrad waves issue the x prefetch one per k-step (0: before the k-steps)
+#endif
+#ifndef ASR_V2_SPREAD
+#define ASR_V2_SPREAD 1  // v2 backward: dgrad waves issue one dy DMA every N conv k-steps
+#endif
+#ifndef ASR_V2_WPIPE
+#define ASR_V2_WPIPE 1  // v2 backward: wgrad k-steps software-pipelined across m-tiles and k-steps
+#endif
 #ifndef ASR_ABLATE
 #define ASR_ABLATE 0  // development only: fwd 1 no epilogue, 2 no MFMA, 3 no prefetch DMA;
                       // bwd 4 no convert, 5 no dgrad MFMA, 6 no wgrad MFMA, 7 no dgrad epilogue,
@@ -1511,6 +1523,452 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
   }
 }
 
+// ===========================================================================
+// Backward v2 (C=64, W=32, BR=4; the Euler block and the plain conv, no
+// RK2 extra term).  The dz = dy*mask conversion of band it+1 runs on the
+// dgrad waves at the end of band it, while the wgrad waves still run band
+// it's MFMAs (v1 converts on all 8 waves between two barriers, with the MFMA
+// pipe idle).  dy, x and dz tiles are double-buffered (6 tiles, 153 KiB);
+// the relu mask goes to registers, not LDS.  Each dgrad wave owns whole
+// tile rows of the next band: it DMAs their dy, loads their mask dwords and
+// converts them, so its own vmcnt covers everything it converts and no
+// cross-wave wait is needed before the band barrier.  The wgrad waves DMA
+// the next band's x rows and, after their MFMAs, copy the halo rows of a
+// band that continues the previous band's image (dz rows 0,1 already
+// masked, x rows 0,1, dy row 1 = the residual's first interior row).
+// ===========================================================================
+template <int C, int W, int BR>
+struct Bwd2Lds {
+  static constexpr int ROWB = (W + 2) * (C / 8) * 16;
+  static constexpr int TILE = (BR + 2) * ROWB;
+  static constexpr int DY = 0, X = 2 * TILE, DZ = 4 * TILE;
+  // 256 x 16 B: the 16-bit-lane AND masks of one 16-B chunk per mask byte
+  static constexpr int MTAB = 6 * TILE, TOTAL = MTAB + (ASR_V2_MASKTAB ? 4096 : 0);
+};
+
+// tile rows of band `nx` owned by dgrad wave wv (0..3): reuse -> row 2+wv;
+// else rows wv and wv+4 (wv < 2)
+struct Bwd2Own {
+  int ra, rb;  // rb < 0: one row
+  __device__ __forceinline__ Bwd2Own(bool reuse, int wv) {
+    ra = reuse ? 2 + wv : wv;
+    rb = (!reuse && wv < 2) ? wv + 4 : -1;
+  }
+  __device__ __forceinline__ int count() const { return rb < 0 ? 1 : 2; }
+  __device__ __forceinline__ int row(int k) const { return k == 0 ? ra : rb; }
+};
+
+// mask dword of lane (pixel lane&31, channel half lane>>5) of tile row r of
+// band (n, y0): bytes 8*px + 4*h .. +3 of the image row (zeros outside)
+template <int C, int W>
+__device__ __forceinline__ unsigned bwd2_mask_word(const uint8_t* __restrict__ mask, int n, int y0, int r, int H,
+                                                   int lane) {
+  const int gy = y0 - 1 + r;
+  if ((unsigned)gy >= (unsigned)H) return 0u;
+  return *(const unsigned*)(mask + ((long)n * H + gy) * (W * C / 8) + (2 * (lane & 31) + (lane >> 5)) * 4);
+}
+
+// wgrad waves, after band it's MFMAs, when band it+1 continues band it's
+// image: dz rows BR, BR+1 -> rows 0, 1 (already masked), x rows BR, BR+1 ->
+// rows 0, 1, dy row BR+1 -> row 1 (the residual's first interior row) of
+// the next buffers.  Interior columns, physical chunk slots (the swizzle
+// depends on the column only).  t in [0, 256).
+template <int C, int W, int BR>
+__device__ __forceinline__ void bwd2_copy_halo(unsigned char* lds, int buf, int t) {
+  using L = Bwd2Lds<C, W, BR>;
+  constexpr int NQ = C / 8, ROWB = L::ROWB;
+  static_assert(W * NQ == 256, "one interior row = 256 chunks");
+  const unsigned base = lds_u32(lds);
+  const int nb = buf ^ 1;
+  const unsigned o = (unsigned)(t + NQ) * 16u;
+  u32x4 cv[5];
+  cv[0] = lds_rd128(base + L::DZ + buf * L::TILE + BR * ROWB + o);
+  cv[1] = lds_rd128(base + L::DZ + buf * L::TILE + (BR + 1) * ROWB + o);
+  cv[2] = lds_rd128(base + L::X + buf * L::TILE + BR * ROWB + o);
+  cv[3] = lds_rd128(base + L::X + buf * L::TILE + (BR + 1) * ROWB + o);
+  cv[4] = lds_rd128(base + L::DY + buf * L::TILE + (BR + 1) * ROWB + o);
+  lgkm_wait<0>();
+  lds_wr128(base + L::DZ + nb * L::TILE + o, cv[0]);
+  lds_wr128(base + L::DZ + nb * L::TILE + ROWB + o, cv[1]);
+  lds_wr128(base + L::X + nb * L::TILE + o, cv[2]);
+  lds_wr128(base + L::X + nb * L::TILE + ROWB + o, cv[3]);
+  lds_wr128(base + L::DY + nb * L::TILE + ROWB + o, cv[4]);
+}
+
+// dgrad waves: convert the wave's own rows of the next band (buffer nb):
+// lane = (pixel lane&31, chunks 4h..4h+3, h = lane>>5), mask dword mw[k]
+template <int C, int W, int BR, bool EULER>
+__device__ __forceinline__ void bwd2_convert_own(unsigned char* lds, int nb, const Bwd2Own& own,
+                                                 const unsigned (&mw)[2], int lane) {
+  using L = Bwd2Lds<C, W, BR>;
+  constexpr int TW = W + 2;
+  static_assert(C == 64 && W == 32 && BR == 4, "v2 backward geometry");
+  const unsigned base = lds_u32(lds);
+  const int px = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {  // one row at a time (the second only on a band that starts an image)
+    if (k == 1 && own.rb < 0) break;
+    const int r = own.row(k);
+    u32x4 v[4], mt[4];
+    unsigned off[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      off[j] = (unsigned)toff<C>(r, px + 1, 4 * h + j, TW);
+      v[j] = lds_rd128(base + L::DY + nb * L::TILE + off[j]);
+      if (EULER && ASR_V2_MASKTAB) mt[j] = lds_rd128(base + L::MTAB + __builtin_amdgcn_ubfe(mw[k], 8 * j, 8) * 16);
+    }
+    lgkm_wait<0>();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      u32x4 z = v[j];
+      if constexpr (EULER && ASR_V2_MASKTAB) {
+        z &= mt[j];
+      } else if constexpr (EULER) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {  // element pair (2d, 2d+1) of chunk 4h+j: mask bits 8j+2d, 8j+2d+1
+          const unsigned lo = (unsigned)__builtin_amdgcn_sbfe((int)mw[k], 8 * j + 2 * d, 1);
+          const unsigned hi = (unsigned)__builtin_amdgcn_sbfe((int)mw[k], 8 * j + 2 * d + 1, 1);
+          z[d] &= __builtin_amdgcn_perm(hi, lo, 0x07060100u);
+        }
+      }
+      lds_wr128(base + L::DZ + nb * L::TILE + off[j], z);
+    }
+  }
+}
+
+template <int C, int W, int BR, int MODE>
+__global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                              const uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
+                                              float h, float two_gamma, int N, int H, bf16* __restrict__ dx,
+                                              float* __restrict__ slabs) {
+  using G = Geo<C>;
+  using L = Bwd2Lds<C, W, BR>;
+  constexpr int TW = W + 2, PT = W / 16, OTW = G::OTW, OT = G::OT, MTW = G::MTW, IPR = W / G::PPI;
+  constexpr int KPR = W / 32;
+  constexpr bool EULER = MODE == BWD_EULER;
+  static_assert(C == 64 && W == 32 && BR == 4 && G::KSPLIT == 1 && G::OSPLIT == 2 && MTW % 3 == 0, "v2 backward geometry");
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, lx = lane & 15;
+
+  for (int b = 0; b < 2; ++b) {
+    zero_halo_cols<C, W>(lds + L::DY + b * L::TILE, BR + 2, tid, 512);
+    zero_halo_cols<C, W>(lds + L::X + b * L::TILE, BR + 2, tid, 512);
+    zero_halo_cols<C, W>(lds + L::DZ + b * L::TILE, BR + 2, tid, 512);
+  }
+  if (ASR_V2_MASKTAB && EULER) {  // dword d of byte m's entry: 0xffff per set bit of (m >> 2d) & 3
+    unsigned* tab = (unsigned*)(lds + L::MTAB);
+    for (int i = tid; i < 1024; i += 512) {
+      const unsigned m = (unsigned)i >> 2, d = (unsigned)i & 3;
+      tab[i] = (((m >> (2 * d)) & 1u) ? 0xffffu : 0u) | (((m >> (2 * d + 1)) & 1u) ? 0xffff0000u : 0u);
+    }
+  }
+  const int nb = (H + BR - 1) / BR;
+  int i0, i1;
+  item_range(N * nb, &i0, &i1);
+  const unsigned loff = (unsigned)dma_lane_off<C, W>(lane) * 2u;
+  float* slab = slabs + (long)blockIdx.x * (9 * C * C + C);
+  const float hs = EULER ? h : 1.f;  // dz = hs * dzm (dzm = dy*mask in LDS)
+  const float hs2g = hs * two_gamma;
+  __syncthreads();  // halo columns zeroed before any convert / copy writes near them
+
+  if (wave < 4) {
+    // ---------------- dgrad waves ----------------
+    constexpr int RS = 4 / G::OSPLIT;
+    const int oh = wave % G::OSPLIT, rg = wave / G::OSPLIT;
+    const int wv4 = __builtin_amdgcn_readfirstlane(wave);
+    bf16x8 A[OTW][G::KS];
+    load_A<C>(wpack, oh, lane, A);
+    Frag<C, W> boff;
+    boff.init(g, lx);
+    float dbacc[OTW][4];
+#pragma unroll
+    for (int t = 0; t < OTW; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dbacc[t][e] = 0.f;
+    int nst = 0;
+    // prologue: own rows of band i0 (a band with no predecessor: all BR+2 rows)
+    if (i0 < i1) {
+      const ItemCursor c0(i0, nb);
+      const Bwd2Own own(false, wv4);
+      unsigned mw[2] = {0u, 0u};
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (k == 1 && own.rb < 0) break;
+        const int r = own.row(k);
+        if constexpr (EULER) mw[k] = bwd2_mask_word<C, W>(mask, c0.n, c0.b * BR, r, H, lane);
+        for (int j = 0; j < IPR; ++j)
+          dma_row_instr<C, W>(dy, lds + L::DY + r * L::ROWB, c0.n, c0.b * BR - 1 + r, j, H, loff);
+      }
+      vm_wait(0);
+      bwd2_convert_own<C, W, BR, EULER>(lds, 0, own, mw, lane);
+    }
+    ItemCursor cur(i0, nb), nxt(i0, nb);
+    nxt.next(nb);
+    for (int it = i0; it < i1; ++it, cur.next(nb), nxt.next(nb)) {
+      const int buf = (it - i0) & 1;
+      const int n = cur.n, y0 = cur.b * BR;
+      const int rows = min(BR, H - y0);
+      ASR_STAMP(it - i0, 0);
+      barrier_vm(nst);  // band it staged everywhere; band it-1 fully consumed
+      ASR_STAMP(it - i0, 1);
+      nst = 0;
+      const bool more = it + 1 < i1;
+      const bool reuse = more && nxt.n == cur.n;
+      const Bwd2Own own(reuse, wv4);
+      const int y1 = nxt.b * BR;
+      // mask dwords of the own rows of band it+1 (registers until the convert)
+      unsigned mw[2] = {0u, 0u};
+      if (EULER && more) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          if (k == 1 && own.rb < 0) break;
+          mw[k] = bwd2_mask_word<C, W>(mask, nxt.n, y1, own.row(k), H, lane);
+        }
+      }
+      // dy DMA of the own rows of band it+1, one instruction per k-step of
+      // the first dgrad row
+      const int dend = more ? own.count() * IPR : 0;
+      int du = 0, kstep = 0;
+      unsigned char* dyn = lds + L::DY + (buf ^ 1) * L::TILE;
+      auto dma_now = [&]() {
+        if (du < dend) {
+          const int r = own.row(du / IPR);
+          dma_row_instr<C, W>(dy, dyn + r * L::ROWB, nxt.n, y1 - 1 + r, du % IPR, H, loff);
+          ++du;
+        }
+      };
+      auto dma_one = [&]() {  // conv k-step hook: one DMA every ASR_V2_SPREAD k-steps
+        if (kstep++ % ASR_V2_SPREAD == 0) dma_now();
+      };
+      const unsigned char* dzt = lds + L::DZ + buf * L::TILE;
+      const unsigned char* dyt = lds + L::DY + buf * L::TILE;
+      int nstores = 0;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int r = rg + k * RS;
+        if (r >= rows) break;
+        f32x4 acc[OTW][PT];
+#pragma unroll
+        for (int t = 0; t < OTW; ++t)
+#pragma unroll
+          for (int pt = 0; pt < PT; ++pt) acc[t][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (k == 0) {
+          conv_row<C, W>(dzt, r, A, boff, acc, dma_one);
+          while (du < dend) dma_now();
+        } else {
+          conv_row<C, W>(dzt, r, A, boff, acc);
+        }
+        ASR_STAMP(it - i0, 2 + k);
+        const int gy = y0 + r;
+        if (dx) nstores += PT * OTW;
+        u32x2 dzv[PT][OTW], dyv[PT][OTW];
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt)
+#pragma unroll
+          for (int t = 0; t < OTW; ++t) {
+            const int px = 16 * pt + lx, o0 = 16 * (oh * OTW + t) + 4 * g;
+            const int co = toff<C>(r + 1, px + 1, o0 >> 3, TW) + (o0 & 4) * 2;
+            dzv[pt][t] = lds_rd64(lds_u32(dzt + co));
+            if (EULER) dyv[pt][t] = lds_rd64(lds_u32(dyt + co));
+          }
+        lgkm_wait<0>();
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt) {
+          const int px = 16 * pt + lx;
+#pragma unroll
+          for (int t = 0; t < OTW; ++t) {
+            const int o0 = 16 * (oh * OTW + t) + 4 * g;
+            const bf16x4 dzr = *(const bf16x4*)&dzv[pt][t];
+            float dzf[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              dzf[e] = (float)dzr[e];
+              dbacc[t][e] += dzf[e];
+            }
+            bf16x4 o4;
+            if constexpr (EULER) {
+              const bf16x4 dyr = *(const bf16x4*)&dyv[pt][t];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float v = fmaf(-hs, acc[t][pt][e], (float)dyr[e]);
+                o4[e] = (bf16)(hs2g != 0.f ? fmaf(hs2g, dzf[e], v) : v);
+              }
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(two_gamma, dzf[e], -acc[t][pt][e]);
+            }
+            if (dx) *(bf16x4*)(dx + (((long)n * H + gy) * W + px) * C + o0) = o4;
+          }
+        }
+        ASR_STAMP(it - i0, 4 + k);
+      }
+      while (du < dend) dma_now();  // a wave without rows in this band
+      if (more) {
+        vm_wait(nstores);  // own dy rows and mask dwords of band it+1 (older than this band's stores)
+        bwd2_convert_own<C, W, BR, EULER>(lds, buf ^ 1, own, mw, lane);
+      }
+      nst = nstores;
+      ASR_STAMP(it - i0, 6);
+    }
+    // reduce db over the 16 pixel lanes, then over the row-group waves (LDS)
+#pragma unroll
+    for (int t = 0; t < OTW; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = dbacc[t][e];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        dbacc[t][e] = v;
+      }
+    barrier_vm(0);  // matches the wgrad waves' end-of-loop barrier
+    float* dbl = (float*)lds + 12288;  // [RS][C]
+    if (lx == 0) {
+#pragma unroll
+      for (int t = 0; t < OTW; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dbl[rg * C + 16 * (oh * OTW + t) + 4 * g + e] = hs * dbacc[t][e];
+    }
+  } else {
+    // ---------------- wgrad waves ----------------
+    const int w4 = wave - 4;
+    const int tg = w4;  // KSPLIT == 1: one m-tile group per wave, all k-steps
+    const int tq = lx >> 2, tp = lx & 3;
+    const int wv8 = __builtin_amdgcn_readfirstlane(wave) - 4;
+    f32x4 acc[MTW][OT];
+#pragma unroll
+    for (int mi = 0; mi < MTW; ++mi)
+#pragma unroll
+      for (int ot = 0; ot < OT; ++ot) acc[mi][ot] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (i0 < i1) {  // prologue: x rows of band i0
+      const ItemCursor c0(i0, nb);
+      for (int j = wv8; j < (BR + 2) * IPR; j += 4)
+        dma_row_instr<C, W>(x, lds + L::X, c0.n, c0.b * BR - 1, j, H, loff);
+    }
+    ItemCursor cur(i0, nb), nxt(i0, nb);
+    nxt.next(nb);
+    for (int it = i0; it < i1; ++it, cur.next(nb), nxt.next(nb)) {
+      const int buf = (it - i0) & 1;
+      const int y0 = cur.b * BR;
+      const int rows = min(BR, H - y0);
+      ASR_STAMP(it - i0, 0);
+      barrier_vm(0);  // this wave's x rows of band it landed
+      ASR_STAMP(it - i0, 1);
+      // x rows of band it+1 (rows 2.. when it continues this band's image)
+      const int xr0 = nxt.n == cur.n ? 2 : 0;
+      unsigned char* xn = lds + L::X + (buf ^ 1) * L::TILE + xr0 * L::ROWB;
+      const int xy = nxt.b * BR - 1 + xr0;
+      const int xend = it + 1 < i1 ? (BR + 2 - xr0) * IPR : 0;
+      int xj = wv8;
+      auto xdma = [&]() {
+        if (xj < xend) {
+          dma_row_instr<C, W>(x, xn, nxt.n, xy, xj, H, loff);
+          xj += 4;
+        }
+      };
+      if (!ASR_V2_XHOOK)
+        while (xj < xend) xdma();
+      ASR_STAMP(it - i0, 2);
+      const unsigned char* dzt = lds + L::DZ + buf * L::TILE;
+      const unsigned char* xt = lds + L::X + buf * L::TILE;
+#if ASR_V2_WPIPE
+      // A fragments two m-tiles ahead (a ring of 3; the next k-step's first
+      // one during this one's last m-tiles), so an MFMA group does not wait a
+      // whole LDS latency for its A
+      const int nkk = rows * KPR;
+      auto loadA = [&](int kk, int mi) {
+        const int r = kk / KPR, kb = kk % KPR;
+        const int pb = 32 * kb + 8 * g + tq;
+        const int mt = tg * MTW + mi;
+        const int tap = (16 * mt) / C, itile = ((16 * mt) % C) / 16;
+        const int ky = tap / 3, kx = tap % 3;
+        const int q = 2 * itile + (tp >> 1);
+        return tr_pair(xt + toff<C>(r + ky, pb + kx, q, TW) + 8 * (tp & 1),
+                       xt + toff<C>(r + ky, pb + 4 + kx, q, TW) + 8 * (tp & 1));
+      };
+      auto loadB = [&](int kk, bf16x8 (&B)[OT]) {
+        const int r = kk / KPR, kb = kk % KPR;
+        const int pb = 32 * kb + 8 * g + tq;
+#pragma unroll
+        for (int ot = 0; ot < OT; ++ot) {
+          const int q = 2 * ot + (tp >> 1);
+          B[ot] = tr_pair(dzt + toff<C>(r + 1, pb + 1, q, TW) + 8 * (tp & 1),
+                          dzt + toff<C>(r + 1, pb + 5, q, TW) + 8 * (tp & 1));
+        }
+      };
+      bf16x8 Bf[OT], Ar[3];
+      if (nkk > 0) Ar[0] = loadA(0, 0);
+      for (int kk = 0; kk < nkk; ++kk) {
+        const bool more = kk + 1 < nkk;
+        loadB(kk, Bf);
+        Ar[1] = loadA(kk, 1);
+#pragma unroll
+        for (int mi = 0; mi < MTW; ++mi) {
+          if (mi + 2 < MTW) Ar[(mi + 2) % 3] = loadA(kk, mi + 2);
+          else if (mi + 2 == MTW && more) Ar[0] = loadA(kk + 1, 0);  // MTW % 3 == 0: slot 0 again
+#pragma unroll
+          for (int ot = 0; ot < OT; ++ot)
+            acc[mi][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ar[mi % 3], Bf[ot], acc[mi][ot], 0, 0, 0);
+        }
+        if (ASR_V2_XHOOK) xdma();
+      }
+#else
+      for (int kk = 0; kk < rows * KPR; ++kk) {
+        const int r = kk / KPR, kb = kk % KPR;
+        const int pb = 32 * kb + 8 * g + tq;
+        auto loadA = [&](int mi) {
+          const int mt = tg * MTW + mi;
+          const int tap = (16 * mt) / C, itile = ((16 * mt) % C) / 16;
+          const int ky = tap / 3, kx = tap % 3;
+          const int q = 2 * itile + (tp >> 1);
+          return tr_pair(xt + toff<C>(r + ky, pb + kx, q, TW) + 8 * (tp & 1),
+                         xt + toff<C>(r + ky, pb + 4 + kx, q, TW) + 8 * (tp & 1));
+        };
+        bf16x8 Bf[OT];
+#pragma unroll
+        for (int ot = 0; ot < OT; ++ot) {
+          const int q = 2 * ot + (tp >> 1);
+          Bf[ot] = tr_pair(dzt + toff<C>(r + 1, pb + 1, q, TW) + 8 * (tp & 1),
+                           dzt + toff<C>(r + 1, pb + 5, q, TW) + 8 * (tp & 1));
+        }
+        bf16x8 Ac = loadA(0), An;
+#pragma unroll
+        for (int mi = 0; mi < MTW; ++mi) {
+          if (mi + 1 < MTW) An = loadA(mi + 1);
+#pragma unroll
+          for (int ot = 0; ot < OT; ++ot)
+            acc[mi][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ac, Bf[ot], acc[mi][ot], 0, 0, 0);
+          if (mi + 1 < MTW) Ac = An;
+        }
+        if (ASR_V2_XHOOK) xdma();
+      }
+#endif
+      while (xj < xend) xdma();
+      if (it + 1 < i1 && nxt.n == cur.n) bwd2_copy_halo<C, W, BR>(lds, buf, tid - 256);
+      ASR_STAMP(it - i0, 3);
+    }
+    barrier_vm(0);  // all items consumed: LDS reusable
+#pragma unroll
+    for (int mi = 0; mi < MTW; ++mi)
+#pragma unroll
+      for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = 16 * (tg * MTW + mi) + 4 * g + e;
+          slab[(long)m * C + 16 * ot + lx] = hs * acc[mi][ot][e];
+        }
+  }
+  __syncthreads();
+  if (tid < C) {
+    const float* dbl = (const float*)lds + 12288;
+    float s = 0.f;
+    for (int q = 0; q < 4 / G::OSPLIT; ++q) s += dbl[q * C + tid];
+    slab[9 * C * C + tid] = s;
+  }
+}
+
 }  // namespace blk
 
 // ---------------------------------------------------------------------------
@@ -1608,6 +2066,21 @@ static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* ma
   hipLaunchKernelGGL((blk::k_bwd<C, W, kBwdBR, M, XT>), dim3(grid), dim3(512), lds, s, (const bf16*)dy, (const bf16*)x, \
                      mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs, (const bf16*)extra, skip_dy)
   const bool xt = extra != nullptr || skip_dy != 0;
+  static const bool v1 = getenv("ASR_BWD_V1") != nullptr;  // development A/B
+  if constexpr (C == 64) {
+    if (!xt && !v1) {
+      using L2 = blk::Bwd2Lds<C, W, kBwdBR>;
+      const size_t lds2 = std::max((size_t)L2::TOTAL, red);
+      if (mode == blk::BWD_EULER)
+        hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_EULER>), dim3(grid), dim3(512), lds2, s, (const bf16*)dy,
+                           (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs);
+      else
+        hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_CONV>), dim3(grid), dim3(512), lds2, s, (const bf16*)dy,
+                           (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs);
+      ASR_LAUNCH_CHECK("k_bwd2");
+      return ASR_OK;
+    }
+  }
   if (mode == blk::BWD_EULER) {
     if (xt) ASR_LAUNCH_BWD(blk::BWD_EULER, true);
     else ASR_LAUNCH_BWD(blk::BWD_EULER, false);

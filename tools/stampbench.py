@@ -36,7 +36,7 @@ _, tdst = pm.device(dev)
 s = torch.cuda.current_stream().cuda_stream
 _lib.check(lib.asr_conv_forward(0, x.data_ptr(), y.data_ptr(), mask.data_ptr(), w.data_ptr(), bias.data_ptr(), 0.25,
                                 N, H, W, C, 1, s))
-for _ in range(3 if WHAT == "bwd" else 0):
+for _ in range(3 if WHAT.startswith("bwd") else 0):
     _lib.check(lib.asr_conv_backward(0, dy.data_ptr(), x.data_ptr(), mask.data_ptr(), w.data_ptr(), tdst.data_ptr(),
                                      pm.n_theta, 0.25, 0.0, N, H, W, C, 1, dx.data_ptr(), dth.data_ptr(),
                                      db.data_ptr(), None, ws.data_ptr(), wsb, s))
@@ -51,17 +51,30 @@ fn.argtypes = [ct.c_void_p, ct.c_size_t]
 assert fn(st.ctypes.data, st.nbytes) == 0
 st = st.astype(np.int64)
 grid = int((st[:, 0, 0, 0] != 0).sum())
+if WHAT.startswith("bwd"):  # the forward (run first) stamps more WGs than the backward's persistent grid
+    grid = min(grid, torch.cuda.get_device_properties(dev).multi_processor_count)
 st = st[:grid]
+if os.environ.get("STAMP_RAW"):
+    for b in (4, 5):
+        for role in (0, 1):
+            print("raw wg0 band", b, "role", role, (st[0, role, b, :] - st[0, 0, b, 0]).tolist())
+order = None
 if WHAT == "fwd":
     names = {0: ["barrier_vm", "dma issue", "conv+epilogue hooks", "xres read", "loop"]}
+elif WHAT == "bwd2":  # k_bwd2 slots: dgrad 0 1 2(conv0) 4(epi0) 3(conv1) 5(epi1) 6(staged next); wgrad 0 1 2 3
+    names = {0: ["barrier_vm", "row0 conv+dma", "row0 epi", "row1 conv", "row1 epi", "stage next band", "loop"],
+             1: ["barrier_vm", "x dma", "wgrad kk loop", "tail"]}
+    order = {0: [0, 1, 2, 4, 3, 5, 6], 1: [0, 1, 2, 3]}
 else:
     names = {0: ["barrier_vm", "convert", "barrier_lds", "row0 conv+dma", "row0 epi", "row1 conv+epi", "tail"],
              1: ["barrier_vm", "convert", "barrier_lds", "dma share", "wgrad kk loop", "tail"]}
-nb = 16 if WHAT == "bwd" else 8
+nb = 16 if WHAT.startswith("bwd") else 8
 for role in names:
     seg = []
     for b in range(1, nb - 1):
         row = st[:, role, b, :]
+        if order is not None:
+            row = row[:, order[role]]
         nxt = st[:, role, b + 1, 0]
         k = len(names[role])
         d = [row[:, i + 1] - row[:, i] for i in range(k - 1)] + [nxt - row[:, k - 1]]
