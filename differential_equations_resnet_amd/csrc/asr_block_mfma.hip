@@ -46,6 +46,15 @@
 #ifndef ASR_V2_SPREAD
 #define ASR_V2_SPREAD 1  // v2 backward: dgrad waves issue one dy DMA every N conv k-steps
 #endif
+#ifndef ASR_DMA_M0_CLOBBER
+#define ASR_DMA_M0_CLOBBER 1  // LDS-DMA: declare M0 clobbered instead of saving/restoring it per DMA
+#endif
+#ifndef ASR_V2_ST16
+#define ASR_V2_ST16 1  // v2 backward: dx as 16-B stores (row swap between the two o-tiles)
+#endif
+#ifndef ASR_FWD_ST16
+#define ASR_FWD_ST16 1  // forward pipe: y as 16-B stores (row swap between the two pixel tiles)
+#endif
 #ifndef ASR_V2_WPIPE
 #define ASR_V2_WPIPE 1  // v2 backward: wgrad k-steps software-pipelined across m-tiles and k-steps
 #endif
@@ -124,6 +133,16 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 // by the compiler, so it is saved and restored around the DMA.
 __device__ __forceinline__ void dma16(const void* src, unsigned char* lds_wave_base) {
   const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)((ASR_LDS unsigned char*)lds_wave_base));
+#if ASR_DMA_M0_CLOBBER
+  // M0 declared clobbered: the compiler re-establishes it only where it uses it
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off"
+      :
+      : "v"(src), "s"(l)
+      : "memory", "m0");
+#else
   unsigned sv;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
@@ -134,6 +153,7 @@ __device__ __forceinline__ void dma16(const void* src, unsigned char* lds_wave_b
       : "=&s"(sv)
       : "v"(src), "s"(l)
       : "memory");
+#endif
 }
 
 // DMA image rows [gy0, gy0+nrows) of image n (rows outside [0,H) -> zeros) into
@@ -789,7 +809,10 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
   constexpr int RS = NW / OT, RB = BR / RS;
   static_assert(BR % RS == 0, "row groups must split the band");
   using BD = Band<C, W, RB>;
-  constexpr int NU = RB * PT;  // epilogue units (row, pixel tile)
+  // epilogue units: (row, pixel tile), or rows with both pixel tiles stored
+  // as 16-B chunks (ASR_FWD_ST16)
+  constexpr bool ST16 = ASR_FWD_ST16 && PT == 2;
+  constexpr int NU = ST16 ? RB : RB * PT;
   constexpr bool EULER = MODE == FWD_EULER;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -871,14 +894,12 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
 #pragma unroll
       for (int pt = 0; pt < PT; ++pt) acc[r][pt] = f32x4{bz[0], bz[1], bz[2], bz[3]};
   };
-  // one epilogue unit (row r, pixel tile pt) of the band at cursor c
-  auto epi_unit = [&](auto U, const f32x4 (&acc)[RB][PT], const u32x2 (&xr)[RB][PT], const ItemCursor& c) {
-    constexpr int u = decltype(U)::value, r = u / PT, pt = u % PT;
-    const int y0 = c.b * BR;
-    if (r0 + r >= min(BR, H - y0)) return;
-    const long row = ((long)c.n * H + y0 + r0 + r) * W + 16 * pt;
-    nst += (EULER && mask) ? 2 : 1;
+  // y and the relu-mask word of output row r, pixel tile pt (every lane
+  // ends with the 16-bit mask word of its pixel: OR over the 4 lane rows)
+  auto epi_vals = [&](int r, int pt, const f32x4 (&acc)[RB][PT], const u32x2 (&xr)[RB][PT], u32x2& ov,
+                      unsigned& mword) {
     bf16x4 o4;
+    mword = 0;
     if constexpr (EULER) {
       const bf16x4 xv = *(const bf16x4*)&xr[r][pt];
       unsigned nib = 0;
@@ -890,17 +911,47 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
         const float rz = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, z) & (pos ? ~0u : 0u));
         o4[e] = (bf16)fmaf(h, rz, (float)xv[e]);
       }
-      unsigned mword = nib << (4 * g);
+      mword = nib << (4 * g);
       const auto s16 = __builtin_amdgcn_permlane16_swap(mword, mword, false, false);
       mword = s16[0] | s16[1];
       const auto s32 = __builtin_amdgcn_permlane32_swap(mword, mword, false, false);
       mword = s32[0] | s32[1];
-      if (mask && g == 0) *(uint16_t*)(mask + row * (C / 8) + lm) = (uint16_t)mword;
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) o4[e] = (bf16)acc[r][pt][e];
     }
-    *(bf16x4*)(y + row * C + ly) = o4;
+    ov = *(const u32x2*)&o4;
+  };
+  // one epilogue unit of the band at cursor c
+  auto epi_unit = [&](auto U, const f32x4 (&acc)[RB][PT], const u32x2 (&xr)[RB][PT], const ItemCursor& c) {
+    constexpr int u = decltype(U)::value;
+    const int y0 = c.b * BR;
+    if constexpr (ST16) {
+      // row r, both pixel tiles: a 16-lane row swap between the tiles gives
+      // lane row g the 8 channels 16*ot + 8*(g>>1) of pixel 16*(g&1) + lx
+      constexpr int r = u;
+      if (r0 + r >= min(BR, H - y0)) return;
+      const long row = ((long)c.n * H + y0 + r0 + r) * W;
+      nst += (EULER && mask) ? 2 : 1;
+      u32x2 ov[2];
+      unsigned mw[2];
+      epi_vals(r, 0, acc, xr, ov[0], mw[0]);
+      epi_vals(r, 1, acc, xr, ov[1], mw[1]);
+      const auto s0 = __builtin_amdgcn_permlane16_swap(ov[0][0], ov[1][0], false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(ov[0][1], ov[1][1], false, false);
+      *(u32x4*)(y + (row + 16 * (g & 1) + lx) * C + 16 * ot + 8 * (g >> 1)) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+      if (EULER && mask && g < 2) *(uint16_t*)(mask + (row + 16 * g) * (C / 8) + lm) = (uint16_t)(g ? mw[1] : mw[0]);
+    } else {
+      constexpr int r = u / PT, pt = u % PT;
+      if (r0 + r >= min(BR, H - y0)) return;
+      const long row = ((long)c.n * H + y0 + r0 + r) * W + 16 * pt;
+      nst += (EULER && mask) ? 2 : 1;
+      u32x2 ov;
+      unsigned mword;
+      epi_vals(r, pt, acc, xr, ov, mword);
+      if (EULER && mask && g == 0) *(uint16_t*)(mask + row * (C / 8) + lm) = (uint16_t)mword;
+      *(u32x2*)(y + row * C + ly) = ov;
+    }
   };
   auto epi_all = [&](const f32x4 (&acc)[RB][PT], const u32x2 (&xr)[RB][PT], const ItemCursor& c) {
     epi_all_units<NU>(epi_unit, acc, xr, c);
@@ -1761,7 +1812,7 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
         }
         ASR_STAMP(it - i0, 2 + k);
         const int gy = y0 + r;
-        if (dx) nstores += PT * OTW;
+        if (dx) nstores += ASR_V2_ST16 ? PT : PT * OTW;
         u32x2 dzv[PT][OTW], dyv[PT][OTW];
 #pragma unroll
         for (int pt = 0; pt < PT; ++pt)
@@ -1773,12 +1824,13 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
             if (EULER) dyv[pt][t] = lds_rd64(lds_u32(dyt + co));
           }
         lgkm_wait<0>();
+        const bool g2 = hs2g != 0.f;  // wave-uniform: the 2*gamma*dz term (0 in the network: gamma is in W)
 #pragma unroll
         for (int pt = 0; pt < PT; ++pt) {
           const int px = 16 * pt + lx;
+          u32x2 ov[OTW];
 #pragma unroll
           for (int t = 0; t < OTW; ++t) {
-            const int o0 = 16 * (oh * OTW + t) + 4 * g;
             const bf16x4 dzr = *(const bf16x4*)&dzv[pt][t];
             float dzf[4];
 #pragma unroll
@@ -1789,16 +1841,30 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
             bf16x4 o4;
             if constexpr (EULER) {
               const bf16x4 dyr = *(const bf16x4*)&dyv[pt][t];
+              if (g2) {
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const float v = fmaf(-hs, acc[t][pt][e], (float)dyr[e]);
-                o4[e] = (bf16)(hs2g != 0.f ? fmaf(hs2g, dzf[e], v) : v);
+                for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(hs2g, dzf[e], fmaf(-hs, acc[t][pt][e], (float)dyr[e]));
+              } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(-hs, acc[t][pt][e], (float)dyr[e]);
               }
             } else {
 #pragma unroll
               for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(two_gamma, dzf[e], -acc[t][pt][e]);
             }
-            if (dx) *(bf16x4*)(dx + (((long)n * H + gy) * W + px) * C + o0) = o4;
+            ov[t] = *(const u32x2*)&o4;
+          }
+          if (!dx) continue;
+          bf16* drow = dx + (((long)n * H + gy) * W + px) * C;
+          if (ASR_V2_ST16) {
+            // 16-B stores: swap 16-lane rows between the two o-tiles, so lane
+            // row g holds 8 consecutive channels 16*(2oh + (g&1)) + 8*(g>>1)
+            const auto s0 = __builtin_amdgcn_permlane16_swap(ov[0][0], ov[1][0], false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(ov[0][1], ov[1][1], false, false);
+            *(u32x4*)(drow + 16 * (oh * OTW + (g & 1)) + 8 * (g >> 1)) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+          } else {
+#pragma unroll
+            for (int t = 0; t < OTW; ++t) *(u32x2*)(drow + 16 * (oh * OTW + t) + 4 * g) = ov[t];
           }
         }
         ASR_STAMP(it - i0, 4 + k);
