@@ -44,7 +44,7 @@
 #define ASR_V2_XHOOK 0  // v2 backward: wgrad waves issue the x prefetch one per k-step (0: before the k-steps)
 #endif
 #ifndef ASR_V2_SPREAD
-#define ASR_V2_SPREAD 1  // v2 backward: dgrad waves issue one dy DMA every N conv k-steps
+#define ASR_V2_SPREAD 0  // v2 backward: dgrad waves issue one dy DMA every N conv k-steps (0: one burst after the barrier)
 #endif
 #ifndef ASR_DMA_M0_CLOBBER
 #define ASR_DMA_M0_CLOBBER 1  // LDS-DMA: declare M0 clobbered instead of saving/restoring it per DMA
@@ -1790,8 +1790,10 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
         }
       };
       auto dma_one = [&]() {  // conv k-step hook: one DMA every ASR_V2_SPREAD k-steps
-        if (kstep++ % ASR_V2_SPREAD == 0) dma_now();
+        if (ASR_V2_SPREAD > 0 && kstep++ % (ASR_V2_SPREAD > 0 ? ASR_V2_SPREAD : 1) == 0) dma_now();
       };
+      if (ASR_V2_SPREAD == 0)
+        while (du < dend) dma_now();  // one burst after the barrier
       const unsigned char* dzt = lds + L::DZ + buf * L::TILE;
       const unsigned char* dyt = lds + L::DY + buf * L::TILE;
       int nstores = 0;
