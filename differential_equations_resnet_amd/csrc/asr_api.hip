@@ -28,9 +28,13 @@ int project_layers(float* grp, long grp_stride, int G, long E, int Cb, const int
 // asr_block_mfma.hip
 int block_fwd_mfma(int mode, const void* x, const void* resid, void* y, uint8_t* mask, const void* w,
                    const float* bias, float h, int N, int H, int W, int C, hipStream_t s);
+// relu_dx (optional): dx *= [x > 0] when the kernel supports it (*relu_done = 1)
 int block_bwd_mfma(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
                    float two_gamma, int N, int H, int W, int C, void* dx, float* slabs, int* nslabs, const void* extra,
-                   int skip_dy, hipStream_t s);
+                   int skip_dy, hipStream_t s, int relu_dx = 0, int* relu_done = nullptr);
+int stem_wgrad_mfma(const void* img, int input_u8, const void* dz1, int N, int H, int W, int Cin, int C, float mean,
+                    float inv_std, int use_norm, float* slabs, int* nslabs, hipStream_t s);
+bool stem_wgrad_mfma_supported(int Cin, int H, int W, int C);
 static bool mfma_supported(int C, int W) { return (C == 16 || C == 32 || C == 64) && W == 32; }
 // asr_conv_f32.hip
 int conv_f32(int fmode, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
@@ -96,12 +100,15 @@ static BwdWs bwd_ws_layout(int N, int H, int W, int C, int dtype, int stages = 1
 //   RK2 stage adds the step's outer dy).
 static int block_backward(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
                           float gamma, int N, int H, int W, int C, int dtype, void* dx, bool need_w, const void* extra,
-                          bool skip_dy, float* slabs, float* dz_scratch, int* nsl, hipStream_t s) {
+                          bool skip_dy, float* slabs, float* dz_scratch, int* nsl, hipStream_t s, bool relu_dx = false,
+                          int* relu_done = nullptr) {
   *nsl = 0;
+  if (relu_done) *relu_done = 0;
   if (dtype == ASR_BF16) {
     if (!dx && !need_w) return ASR_OK;
     const int cm = (mode == ASR_MODE_EULER) ? 2 : 3;  // BWD_EULER / BWD_CONV
-    return block_bwd_mfma(cm, dy, x, mask, w, h, 2.f * gamma, N, H, W, C, dx, slabs, nsl, extra, skip_dy ? 1 : 0, s);
+    return block_bwd_mfma(cm, dy, x, mask, w, h, 2.f * gamma, N, H, W, C, dx, slabs, nsl, extra, skip_dy ? 1 : 0, s,
+                          relu_dx ? 1 : 0, relu_done);
   }
   const bool euler = mode == ASR_MODE_EULER;
   ASR_TRY(make_dz(euler ? F_EULER : F_CONV, dy, mask, nullptr, h, N, H, W, C, 0, dz_scratch, s));
@@ -115,7 +122,8 @@ static int block_backward(int mode, const void* dy, const void* x, const uint8_t
 static int conv_backward_impl(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w,
                               const int32_t* theta_dst, long n_theta, float h, float gamma, int N, int H, int W,
                               int C, int dtype, void* dx, float* dtheta, float* dbias, float* dw_hwio, void* ws,
-                              hipStream_t s, float* grp_defer = nullptr, int* nsl_out = nullptr) {
+                              hipStream_t s, float* grp_defer = nullptr, int* nsl_out = nullptr, bool relu_dx = false,
+                              int* relu_done = nullptr) {
   const BwdWs L = bwd_ws_layout(N, H, W, C, dtype);
   unsigned char* base = (unsigned char*)ws;
   float* slabs = (float*)(base + L.slabs);
@@ -123,7 +131,7 @@ static int conv_backward_impl(int mode, const void* dy, const void* x, const uin
   const bool need_w = dtheta || dbias || dw_hwio;
   int nsl = 0;
   ASR_TRY(block_backward(mode, dy, x, mask, w, h, gamma, N, H, W, C, dtype, dx, need_w || grp_defer, nullptr, false,
-                         slabs, (float*)(base + L.dz), &nsl, s));
+                         slabs, (float*)(base + L.dz), &nsl, s, relu_dx, relu_done));
   if (grp_defer) {  // the network defers pass 2 + projection to one launch for all layers
     if (nsl_out) *nsl_out = nsl;
     return reduce_slabs_to_groups(slabs, nsl, 9L * C * C + C, grp_defer, s);
@@ -547,6 +555,8 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   const int32_t* theta_dst = (const int32_t*)(b + L.theta_dst);
   int nsl_blk = 0;
   const BwdWs bw = bwd_ws_layout(N, H, W, C, cfg->dtype, L.stages);
+  int dz1_fused = 0;  // dcur holds dz1 = dx1 * [x1 > 0] after the block loop
+  const bool stem_v1 = getenv("ASR_STEM_V1") != nullptr;  // A/B and parity tests: the fp32 VALU stem wgrad
   for (int l = cfg->L - 1; l >= 0; --l) {
     const unsigned char* wl = b + (L.sep_bwd ? L.wbuf_bwd : L.wbuf) + (size_t)l * L.wstride * L.act_bytes;
     const uint8_t* mask = (const uint8_t*)(b + L.masks) + (size_t)l * L.mask_bytes;
@@ -561,8 +571,11 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
       ASR_TRY(reduce_slabs_to_groups(slabs, nsl_blk, L.E + C, grp_l, s));
     } else {
       float* dth = grads + L.off_blk + (long)l * L.blk_stride;
+      // the first block's dx goes only to the stem: let its kernel apply the
+      // stem's relu' (dz1 = dx1 * [x1 > 0]) when it can
       ASR_TRY(conv_backward_impl(ASR_MODE_EULER, dcur, act(l), mask, wl, theta_dst, L.ntheta, cfg->h, gam, N, H, W,
-                                 C, cfg->dtype, dnext, dth, dth + L.ntheta, nullptr, b + L.bwdws, s, grp_l, &nsl_blk));
+                                 C, cfg->dtype, dnext, dth, dth + L.ntheta, nullptr, b + L.bwdws, s, grp_l, &nsl_blk,
+                                 l == 0 && L.fast_stem && bf && !stem_v1, l == 0 ? &dz1_fused : nullptr));
     }
     std::swap(dcur, dnext);
   }
@@ -577,7 +590,10 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   float* red = (float*)(sw + align_up((size_t)L.P * 4, 256) + align_up((size_t)kMaxSlabsApi * (E1 + C) * 4, 256));
   int nsl = 0;
   const float inv_std = cfg->use_norm ? 1.f / cfg->divide_by_stddev : 1.f;
-  if (L.fast_stem) {
+  if (L.fast_stem && dz1_fused && stem_wgrad_mfma_supported(cfg->Cin, H, W, C)) {
+    ASR_TRY(stem_wgrad_mfma(images, cfg->input_u8, dcur, N, H, W, cfg->Cin, C, cfg->subtract_mean, inv_std,
+                            cfg->use_norm, slabs, &nsl, s));
+  } else if (L.fast_stem) {  // (masking an already-masked dz1 again is exact)
     ASR_TRY(stem_wgrad(images, cfg->input_u8, dcur, act(0), bf, N, H, W, cfg->Cin, C, cfg->subtract_mean, inv_std,
                        cfg->use_norm, slabs, &nsl, s));
   } else {

@@ -1687,7 +1687,9 @@ __device__ __forceinline__ void bwd2_convert_own(unsigned char* lds, int nb, con
   }
 }
 
-template <int C, int W, int BR, int MODE>
+// RO: dx *= [x > 0] (x = this block's input; the network's first block, so
+// that dx is the stem's dz1 = dx1 * relu'(x1) directly)
+template <int C, int W, int BR, int MODE, bool RO>
 __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                               const uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
                                               float h, float two_gamma, int N, int H, bf16* __restrict__ dx,
@@ -1815,7 +1817,7 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
         ASR_STAMP(it - i0, 2 + k);
         const int gy = y0 + r;
         if (dx) nstores += ASR_V2_ST16 ? PT : PT * OTW;
-        u32x2 dzv[PT][OTW], dyv[PT][OTW];
+        u32x2 dzv[PT][OTW], dyv[PT][OTW], xv[RO ? PT : 1][OTW];
 #pragma unroll
         for (int pt = 0; pt < PT; ++pt)
 #pragma unroll
@@ -1824,6 +1826,7 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
             const int co = toff<C>(r + 1, px + 1, o0 >> 3, TW) + (o0 & 4) * 2;
             dzv[pt][t] = lds_rd64(lds_u32(dzt + co));
             if (EULER) dyv[pt][t] = lds_rd64(lds_u32(dyt + co));
+            if constexpr (RO) xv[pt][t] = lds_rd64(lds_u32(lds + L::X + buf * L::TILE + co));
           }
         lgkm_wait<0>();
         const bool g2 = hs2g != 0.f;  // wave-uniform: the 2*gamma*dz term (0 in the network: gamma is in W)
@@ -1855,6 +1858,14 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
               for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(two_gamma, dzf[e], -acc[t][pt][e]);
             }
             ov[t] = *(const u32x2*)&o4;
+            if constexpr (RO) {  // bf16 x > 0: positive as a signed 16-bit integer
+#pragma unroll
+              for (int d = 0; d < 2; ++d) {
+                const unsigned xw = xv[pt][t][d];
+                const unsigned keep = ((int)(short)(xw & 0xffffu) > 0 ? 0xffffu : 0u) | ((int)xw > 0xffff ? 0xffff0000u : 0u);
+                ov[t][d] &= keep;
+              }
+            }
           }
           if (!dx) continue;
           bf16* drow = dx + (((long)n * H + gy) * W + px) * C;
@@ -2037,6 +2048,119 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
   }
 }
 
+// ===========================================================================
+// Stem weight gradient on MFMA (C=64, CIN=3, W=32, H % 8 == 0), from dz1 =
+// dx1 * [x1 > 0] (written by the first block's backward, k_bwd2<..., RO>):
+//   dW1[kappa][o] = inv_std * sum_p (img[p + tap] - mean)[ci] * dz1[p][o]
+//   db1[o]        = sum_p dz1[p][o]
+// (models/tfkeras_resnets.py:555-572: input normalisation, then the 3x3 SAME
+// conv1 + relu).  K = pixels (one image row per k-step), M = kappa = tap*3 +
+// ci (27, a row of ones at 27 for db1, padded to 32), N = o.  The image's
+// im2col sits in LDS as a 32-channel tile of bf16 (v - mean): exact for u8
+// input with a half-integer mean, so the bf16 products are exact and only
+// the fp32 accumulation rounds.  dz1 rows stream in by LDS-DMA, 8-row bands
+// double-buffered; both operands come from transposed LDS reads exactly as
+// in the blocks' weight gradient.  One slab [dW1 (27*C) | db1 (C)] per WG.
+// ===========================================================================
+template <typename Tin>
+__global__ __launch_bounds__(256) void k_stem_wgrad_mfma(const Tin* __restrict__ img, const bf16* __restrict__ dz1,
+                                                         int N, int H, float mean, float inv_std,
+                                                         float* __restrict__ slabs) {
+  constexpr int C = 64, W = 32, CIN = 3, TW = W + 2, BRS = 8, KC = 9 * CIN;
+  constexpr int IMROW = TW * 4 * 16, DZROW = TW * (C / 8) * 16, DZT = BRS * DZROW;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int IM = 0, DZ0 = H * IMROW, FT = DZ0 + 2 * DZT;  // im2col | 2 dz1 bands | staged image (fp32, halo)
+  float* ft = (float*)(lds + FT);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, lx = lane & 15, tq = lx >> 2, tp = lx & 3;
+  const int nbands = H / BRS;
+  for (int i = tid; i < (H + 2) * TW * CIN; i += 256) ft[i] = 0.f;  // halo stays zero
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int n0 = blockIdx.x, items = ((N - n0 + (int)gridDim.x - 1) / (int)gridDim.x) * nbands;
+  auto band_n = [&](int it) { return n0 + (it / nbands) * (int)gridDim.x; };
+  auto dma_band = [&](int it, int buf) {
+    dma_rows<C, W>(dz1, lds + DZ0 + buf * DZT, band_n(it), (it % nbands) * BRS, BRS, H, wave, 4, lane);
+  };
+  if (items > 0) dma_band(0, 0);
+  for (int it = 0; it < items; ++it) {
+    const int buf = it & 1, b = it % nbands;
+    if (b == 0) {  // a new image: stage it (fp32, v - mean) and build its im2col
+      const int n = band_n(it);
+      __syncthreads();  // the previous image's im2col fully read
+      const Tin* src = img + (long)n * H * W * CIN;
+      for (int i = tid; i < H * W * CIN; i += 256) {
+        const int ci = i % CIN, p = i / CIN;
+        ft[((p / W + 1) * TW + p % W + 1) * CIN + ci] = (float)src[i] - mean;
+      }
+      __syncthreads();
+      for (int p = tid; p < H * W; p += 256) {
+        const int y = p / W, x = p % W;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          bf16x8 v;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int kap = 8 * q + j;
+            float f = 0.f;
+            if (kap < KC) {
+              const int tap = kap / CIN, ci = kap % CIN;
+              f = ft[((y + tap / 3) * TW + x + tap % 3) * CIN + ci];
+            } else if (kap == KC) {
+              f = 1.f;  // db1 row
+            }
+            v[j] = (bf16)f;
+          }
+          *(bf16x8*)(lds + IM + toff<32>(y, x + 1, q, TW)) = v;
+        }
+      }
+    }
+    barrier_vm(0);  // band it landed (and the im2col is written)
+    if (it + 1 < items) dma_band(it + 1, buf ^ 1);
+    const unsigned char* dzt = lds + DZ0 + buf * DZT;
+#pragma unroll
+    for (int k = 0; k < BRS / 4; ++k) {  // this wave's rows of the band
+      const int r = wave + 4 * k, y = b * BRS + r;
+      const int pb = 8 * g + tq;
+      bf16x8 A[2], B[4];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int q = 2 * mt + (tp >> 1);
+        A[mt] = tr_pair(lds + IM + toff<32>(y, pb + 1, q, TW) + 8 * (tp & 1),
+                        lds + IM + toff<32>(y, pb + 5, q, TW) + 8 * (tp & 1));
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int q = 2 * nt + (tp >> 1);
+        B[nt] = tr_pair(dzt + toff<C>(r, pb + 1, q, TW) + 8 * (tp & 1), dzt + toff<C>(r, pb + 5, q, TW) + 8 * (tp & 1));
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mt], B[nt], acc[mt][nt], 0, 0, 0);
+    }
+  }
+  // the 4 waves' partials, summed in a fixed order (deterministic)
+  barrier_vm(0);
+  float* red = (float*)lds;  // [4 waves][32 m][C]
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[(wave * 32 + 16 * mt + 4 * g + e) * C + 16 * nt + lx] = acc[mt][nt][e];
+  __syncthreads();
+  float* slab = slabs + (long)blockIdx.x * (KC * C + C);
+  for (int i = tid; i < (KC + 1) * C; i += 256) {
+    const float v = (red[i] + red[32 * C + i]) + (red[2 * 32 * C + i] + red[3 * 32 * C + i]);
+    slab[i] = i < KC * C ? v * inv_std : v;  // rows 0..26 dW1, row 27 db1
+  }
+}
+
 }  // namespace blk
 
 // ---------------------------------------------------------------------------
@@ -2122,7 +2246,7 @@ static int launch_fwd(int mode, const void* x, const void* resid, void* y, uint8
 template <int C, int W>
 static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
                       float two_gamma, int N, int H, void* dx, float* slabs, int* nslabs, const void* extra,
-                      int skip_dy, hipStream_t s) {
+                      int skip_dy, int relu_dx, int* relu_done, hipStream_t s) {
   const long items = (long)N * ((H + kBwdBR - 1) / kBwdBR);
   if (items > 0x7fffffffL) return fail(ASR_E_UNSUPPORTED, "bf16 block: too many row bands (%ld)", items);
   const int grid = persistent_grid(items);
@@ -2139,12 +2263,17 @@ static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* ma
     if (!xt && !v1) {
       using L2 = blk::Bwd2Lds<C, W, kBwdBR>;
       const size_t lds2 = std::max((size_t)L2::TOTAL, red);
-      if (mode == blk::BWD_EULER)
-        hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_EULER>), dim3(grid), dim3(512), lds2, s, (const bf16*)dy,
-                           (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs);
-      else
-        hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_CONV>), dim3(grid), dim3(512), lds2, s, (const bf16*)dy,
-                           (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs);
+      if (mode == blk::BWD_EULER && relu_dx) {
+        hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_EULER, true>), dim3(grid), dim3(512), lds2, s,
+                           (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs);
+        if (relu_done) *relu_done = 1;
+      } else if (mode == blk::BWD_EULER) {
+        hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_EULER, false>), dim3(grid), dim3(512), lds2, s,
+                           (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs);
+      } else {
+        hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_CONV, false>), dim3(grid), dim3(512), lds2, s,
+                           (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs);
+      }
       ASR_LAUNCH_CHECK("k_bwd2");
       return ASR_OK;
     }
@@ -2161,6 +2290,33 @@ static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* ma
   return ASR_OK;
 }
 
+// ---------------------------------------------------------------------------
+// stem weight gradient on MFMA (see k_stem_wgrad_mfma)
+// ---------------------------------------------------------------------------
+bool stem_wgrad_mfma_supported(int Cin, int H, int W, int C) {
+  const size_t lds = (size_t)H * 34 * 64 + 2 * 8 * 34 * 128 + (size_t)(H + 2) * 34 * 3 * 4;
+  return Cin == 3 && W == 32 && C == 64 && H % 8 == 0 && H >= 8 && lds <= 160 * 1024;
+}
+
+int stem_wgrad_mfma(const void* img, int input_u8, const void* dz1, int N, int H, int W, int Cin, int C, float mean,
+                    float inv_std, int use_norm, float* slabs, int* nslabs, hipStream_t s) {
+  if (!stem_wgrad_mfma_supported(Cin, H, W, C)) return fail(ASR_E_UNSUPPORTED, "stem wgrad (MFMA): unsupported shape");
+  int cus = cu_count();
+  if (cus <= 0) cus = 256;
+  const int grid = std::max(1, std::min(N, std::min(cus, kMaxBlockSlabs)));
+  *nslabs = grid;
+  const size_t lds = (size_t)H * 34 * 64 + 2 * 8 * 34 * 128 + (size_t)(H + 2) * 34 * 3 * 4;
+  const float m = use_norm ? mean : 0.f, is = use_norm ? inv_std : 1.f;
+  if (input_u8)
+    hipLaunchKernelGGL(blk::k_stem_wgrad_mfma<uint8_t>, dim3(grid), dim3(256), lds, s, (const uint8_t*)img,
+                       (const bf16*)dz1, N, H, m, is, slabs);
+  else
+    hipLaunchKernelGGL(blk::k_stem_wgrad_mfma<float>, dim3(grid), dim3(256), lds, s, (const float*)img,
+                       (const bf16*)dz1, N, H, m, is, slabs);
+  ASR_LAUNCH_CHECK("k_stem_wgrad_mfma");
+  return ASR_OK;
+}
+
 int block_fwd_mfma(int mode, const void* x, const void* resid, void* y, uint8_t* mask, const void* w,
                    const float* bias, float h, int N, int H, int W, int C, hipStream_t s) {
   if (W != 32) return fail(ASR_E_UNSUPPORTED, "bf16 block: W=%d not supported (W must be 32)", W);
@@ -2174,15 +2330,19 @@ int block_fwd_mfma(int mode, const void* x, const void* resid, void* y, uint8_t*
 
 int block_bwd_mfma(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
                    float two_gamma, int N, int H, int W, int C, void* dx, float* slabs, int* nslabs, const void* extra,
-                   int skip_dy, hipStream_t s) {
+                   int skip_dy, hipStream_t s, int relu_dx, int* relu_done) {
+  if (relu_done) *relu_done = 0;
   if (W != 32) return fail(ASR_E_UNSUPPORTED, "bf16 block: W=%d not supported (W must be 32)", W);
   switch (C) {
     case 16:
-      return launch_bwd<16, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, extra, skip_dy, s);
+      return launch_bwd<16, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, extra, skip_dy, relu_dx,
+                                relu_done, s);
     case 32:
-      return launch_bwd<32, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, extra, skip_dy, s);
+      return launch_bwd<32, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, extra, skip_dy, relu_dx,
+                                relu_done, s);
     case 64:
-      return launch_bwd<64, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, extra, skip_dy, s);
+      return launch_bwd<64, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, extra, skip_dy, relu_dx,
+                                relu_done, s);
   }
   return fail(ASR_E_UNSUPPORTED, "bf16 block: C=%d not supported (16, 32, 64)", C);
 }

@@ -120,3 +120,38 @@ def test_network_fullsize_properties(rt, cfg):
     gm = (0.5 * (ga + gb)).cpu().numpy()
     gf = g.cpu().numpy()
     assert np.abs(gf - gm).max() <= 1e-4 * np.abs(gf).max()
+
+
+@pytest.mark.parametrize("N,u8", [(64, True), (512, True), (64, False)])
+def test_stem_wgrad_mfma_matches_fp32_path(rt, N, u8, monkeypatch):
+    """The network's default bf16 path fuses the stem's relu' into the first
+    block's backward (dx -> dz1) and computes the stem weight gradient on
+    MFMA from bf16 (v - mean) (exact for u8 input and mean 127.5); with
+    ASR_STEM_V1 set it runs the fp32 VALU stem kernel from dx1 and x1.  The
+    stem gradients agree to fp32 summation-order noise (u8) or bf16 rounding
+    of the centred float input (1e-3 of max|g|); every other gradient and the
+    loss are bitwise unchanged."""
+    C, L = 64, 2
+    from differential_equations_resnet_amd.netparams import init_net_params
+    dev = torch.device("cuda")
+    params = torch.from_numpy(init_net_params(C, L, 3, 10, seed=3) * 0.5).to(dev)
+    rng = np.random.default_rng(11)
+    raw = rng.integers(0, 256, (N, 32, 32, 3), dtype=np.uint8)
+    imgs = torch.from_numpy(raw if u8 else raw.astype(np.float32) + rng.random(raw.shape, np.float32)).to(dev)
+    tgt = torch.from_numpy(np.eye(10, dtype=np.float32)[rng.integers(0, 10, N)]).to(dev)
+    ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / L, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
+                        dtype="bfloat16", input_u8=u8, device=dev)
+    loss, g = ex.forward_backward(params, imgs, tgt)
+    loss, g = loss.clone(), g.clone()
+    monkeypatch.setenv("ASR_STEM_V1", "1")
+    loss1, g1 = ex.forward_backward(params, imgs, tgt)
+    loss1, g1 = loss1.clone(), g1.clone()
+    monkeypatch.delenv("ASR_STEM_V1")
+    torch.cuda.synchronize()
+    E1 = 9 * 3 * C + C
+    assert torch.equal(loss, loss1)
+    assert torch.equal(g[E1:], g1[E1:]), "only the stem gradients may differ"
+    s, s1 = g[:E1].cpu().numpy(), g1[:E1].cpu().numpy()
+    assert np.isfinite(s).all() and np.abs(s1).max() > 0
+    tol = (1e-5 if u8 else 1e-3) * np.abs(s1).max()
+    assert np.abs(s - s1).max() <= tol, (np.abs(s - s1).max(), tol)
