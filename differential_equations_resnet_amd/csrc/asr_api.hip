@@ -28,10 +28,15 @@ int project_layers(float* grp, long grp_stride, int G, long E, int Cb, const int
 // asr_block_mfma.hip
 int block_fwd_mfma(int mode, const void* x, const void* resid, void* y, uint8_t* mask, const void* w,
                    const float* bias, float h, int N, int H, int W, int C, hipStream_t s);
-// relu_dx (optional): dx *= [x > 0] when the kernel supports it (*relu_done = 1)
+// relu_dx (optional): dx *= [x > 0] when the kernel supports it (*relu_done = 1).
+// fold_* (optional): pass 1 of another slab set's reduction (fold_P slabs ->
+// reduce_groups(fold_P) group rows at fold_grp), folded into the kernel when
+// it supports it (*fold_done = 1); else the caller reduces them itself.
 int block_bwd_mfma(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
                    float two_gamma, int N, int H, int W, int C, void* dx, float* slabs, int* nslabs, const void* extra,
-                   int skip_dy, hipStream_t s, int relu_dx = 0, int* relu_done = nullptr);
+                   int skip_dy, hipStream_t s, int relu_dx = 0, int* relu_done = nullptr,
+                   const float* fold_slabs = nullptr, int fold_P = 0, float* fold_grp = nullptr,
+                   int* fold_done = nullptr);
 int stem_wgrad_mfma(const void* img, int input_u8, const void* dz1, int N, int H, int W, int Cin, int C, float mean,
                     float inv_std, int use_norm, float* slabs, int* nslabs, hipStream_t s);
 bool stem_wgrad_mfma_supported(int Cin, int H, int W, int C);
@@ -101,14 +106,16 @@ static BwdWs bwd_ws_layout(int N, int H, int W, int C, int dtype, int stages = 1
 static int block_backward(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
                           float gamma, int N, int H, int W, int C, int dtype, void* dx, bool need_w, const void* extra,
                           bool skip_dy, float* slabs, float* dz_scratch, int* nsl, hipStream_t s, bool relu_dx = false,
-                          int* relu_done = nullptr) {
+                          int* relu_done = nullptr, const float* fold_slabs = nullptr, int fold_P = 0,
+                          float* fold_grp = nullptr, int* fold_done = nullptr) {
   *nsl = 0;
   if (relu_done) *relu_done = 0;
+  if (fold_done) *fold_done = 0;
   if (dtype == ASR_BF16) {
     if (!dx && !need_w) return ASR_OK;
     const int cm = (mode == ASR_MODE_EULER) ? 2 : 3;  // BWD_EULER / BWD_CONV
     return block_bwd_mfma(cm, dy, x, mask, w, h, 2.f * gamma, N, H, W, C, dx, slabs, nsl, extra, skip_dy ? 1 : 0, s,
-                          relu_dx ? 1 : 0, relu_done);
+                          relu_dx ? 1 : 0, relu_done, fold_slabs, fold_P, fold_grp, fold_done);
   }
   const bool euler = mode == ASR_MODE_EULER;
   ASR_TRY(make_dz(euler ? F_EULER : F_CONV, dy, mask, nullptr, h, N, H, W, C, 0, dz_scratch, s));
@@ -263,7 +270,7 @@ struct NetLayout {
   int stages;    // conv applications per block (1 Euler, 2 RK2)
   long grp_stride;  // floats of slab group sums per layer
   size_t grp;  // per-layer slab group sums, projected after the whole backward
-  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, x0, acts, xmids, masks, dxa, dxb, dxg, bwdws, slabs, red, probs,
+  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, x0, acts, xmids, masks, dxa, dxb, dxg, bwdws, slabs2, slabs, red, probs,
       loss_per, dlogits, gap, total;
   long mask_bytes;
   int act_bytes;
@@ -330,6 +337,9 @@ static NetLayout net_layout(const asr_net_config* c) {
   const size_t stem_ws = align_up((size_t)L.P * 4, 256) + align_up((size_t)kMaxSlabsApi * (E1 + C) * 4, 256) +
                          align_up(reduce_ws_bytes(kMaxSlabsApi, E1 + C), 256);
   L.bwdws = take(std::max(bw.total, stem_ws));
+  // odd Euler blocks' slabs (even ones use the backward workspace's): a
+  // block's slabs stay readable while the next block's kernel reduces them
+  L.slabs2 = L.rk2 ? 0 : take((size_t)kMaxSlabsApi * (L.E + C) * 4);
   L.grp_stride = (long)reduce_groups(L.stages * kMaxSlabsApi) * (L.E + C);
   L.grp = take((size_t)c->L * L.grp_stride * 4);
   L.probs = take((size_t)c->N * K * 4);
@@ -556,6 +566,10 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   int nsl_blk = 0;
   const BwdWs bw = bwd_ws_layout(N, H, W, C, cfg->dtype, L.stages);
   int dz1_fused = 0;  // dcur holds dz1 = dx1 * [x1 > 0] after the block loop
+  const float* pend_slabs = nullptr;  // Euler blocks: the slabs whose pass-1 reduction is still pending
+  int pend_P = 0;
+  float* pend_grp = nullptr;
+  const bool fold_on = getenv("ASR_NO_FOLD") == nullptr;  // A/B: the reduction as separate launches
   const bool stem_v1 = getenv("ASR_STEM_V1") != nullptr;  // A/B and parity tests: the fp32 VALU stem wgrad
   for (int l = cfg->L - 1; l >= 0; --l) {
     const unsigned char* wl = b + (L.sep_bwd ? L.wbuf_bwd : L.wbuf) + (size_t)l * L.wstride * L.act_bytes;
@@ -570,15 +584,25 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
                                  &nsl_blk, s));
       ASR_TRY(reduce_slabs_to_groups(slabs, nsl_blk, L.E + C, grp_l, s));
     } else {
-      float* dth = grads + L.off_blk + (long)l * L.blk_stride;
-      // the first block's dx goes only to the stem: let its kernel apply the
-      // stem's relu' (dz1 = dx1 * [x1 > 0]) when it can
-      ASR_TRY(conv_backward_impl(ASR_MODE_EULER, dcur, act(l), mask, wl, theta_dst, L.ntheta, cfg->h, gam, N, H, W,
-                                 C, cfg->dtype, dnext, dth, dth + L.ntheta, nullptr, b + L.bwdws, s, grp_l, &nsl_blk,
-                                 l == 0 && L.fast_stem && bf && !stem_v1, l == 0 ? &dz1_fused : nullptr));
+      // Euler block: its slabs alternate between two buffers; pass 1 of the
+      // previous (deeper) block's reduction rides in this block's kernel when
+      // it can (else it runs here), and this block's waits for the next
+      // block (or the end of the loop)
+      float* slabs_l = (float*)(b + ((l & 1) ? L.slabs2 : L.bwdws + bw.slabs));
+      int nsl = 0, folded = 0;
+      ASR_TRY(block_backward(ASR_MODE_EULER, dcur, act(l), mask, wl, cfg->h, gam, N, H, W, C, cfg->dtype, dnext, true,
+                             nullptr, false, slabs_l, (float*)(b + L.bwdws + bw.dz), &nsl, s,
+                             l == 0 && L.fast_stem && bf && !stem_v1, l == 0 ? &dz1_fused : nullptr,
+                             fold_on ? pend_slabs : nullptr, fold_on ? pend_P : 0, pend_grp, &folded));
+      if (pend_P > 0 && !folded) ASR_TRY(reduce_slabs_to_groups(pend_slabs, pend_P, L.E + C, pend_grp, s));
+      pend_slabs = slabs_l;
+      pend_P = nsl;
+      pend_grp = grp_l;
+      nsl_blk = nsl;
     }
     std::swap(dcur, dnext);
   }
+  if (pend_P > 0) ASR_TRY(reduce_slabs_to_groups(pend_slabs, pend_P, L.E + C, pend_grp, s));
   // pass 2 of every block's weight-gradient reduction + projection onto theta, one launch
   ASR_TRY(project_layers((float*)(b + L.grp), L.grp_stride, reduce_groups(nsl_blk), L.E, C, theta_dst, L.ntheta,
                          cfg->L, grads + L.off_blk, L.blk_stride, s));

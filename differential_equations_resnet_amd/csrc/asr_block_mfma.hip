@@ -1693,7 +1693,8 @@ template <int C, int W, int BR, int MODE, bool RO>
 __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                               const uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
                                               float h, float two_gamma, int N, int H, bf16* __restrict__ dx,
-                                              float* __restrict__ slabs) {
+                                              float* __restrict__ slabs, const float* __restrict__ pslabs, int pP,
+                                              float* __restrict__ pgrp) {
   using G = Geo<C>;
   using L = Bwd2Lds<C, W, BR>;
   constexpr int TW = W + 2, PT = W / 16, OTW = G::OTW, OT = G::OT, MTW = G::MTW, IPR = W / G::PPI;
@@ -1724,6 +1725,38 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
   const float hs = EULER ? h : 1.f;  // dz = hs * dzm (dzm = dy*mask in LDS)
   const float hs2g = hs * two_gamma;
   __syncthreads();  // halo columns zeroed before any convert / copy writes near them
+
+  // Pass 1 of the previous (deeper) block's slab reduction, folded in: the
+  // pP slabs at pslabs -> ceil(pP/32) group rows at pgrp, as k_reduce_slabs
+  // (each output 16-B chunk summed over its group's slabs in slab order by
+  // one thread: deterministic), two slab loads per band and thread, issued
+  // after the band barrier and added at the band's end.
+  constexpr int ES = 9 * C * C + C, ECH = ES / 4;
+  static_assert(ES % 4 == 0, "16-B slab chunks");
+  const long fT = (long)((pP + 31) / 32) * ECH;
+  const long fc0 = (long)blockIdx.x * fT / gridDim.x, fc1 = (long)(blockIdx.x + 1) * fT / gridDim.x;
+  const bool fold = pP > 0 && fc0 + tid < fc1;
+  const int fg = fold ? (int)((fc0 + tid) / ECH) : 0;
+  const int fpe = min(pP, 32 * fg + 32);
+  int fp = 32 * fg;
+  unsigned foff = fold ? (unsigned)fp * ES + (unsigned)((fc0 + tid) % ECH) * 4 : 0u;  // < 2^32: pP <= 512
+  f32x4 facc = {0.f, 0.f, 0.f, 0.f}, fv[2];
+  auto fold_issue = [&](auto NQ) {  // loads of the next NQ slabs
+#pragma unroll
+    for (int q = 0; q < decltype(NQ)::value; ++q)
+      if (fold && fp + q < fpe) fv[q] = *(const f32x4*)(pslabs + foff + (unsigned)q * ES);
+  };
+  auto fold_acc = [&](auto NQ) {
+#pragma unroll
+    for (int q = 0; q < decltype(NQ)::value; ++q)
+      if (fold && fp < fpe) {
+        facc += fv[q];
+        ++fp;
+        foff += ES;
+      }
+  };
+  using One = std::integral_constant<int, 1>;
+  using Two = std::integral_constant<int, 2>;
 
   if (wave < 4) {
     // ---------------- dgrad waves ----------------
@@ -1766,6 +1799,7 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
       barrier_vm(nst);  // band it staged everywhere; band it-1 fully consumed
       ASR_STAMP(it - i0, 1);
       nst = 0;
+      fold_issue(One{});  // dgrad: one slab load in flight at a time (registers)
       const bool more = it + 1 < i1;
       const bool reuse = more && nxt.n == cur.n;
       const Bwd2Own own(reuse, wv4);
@@ -1881,8 +1915,13 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
           }
         }
         ASR_STAMP(it - i0, 4 + k);
+        if (k == 0) {  // second slab of this band
+          fold_acc(One{});
+          fold_issue(One{});
+        }
       }
       while (du < dend) dma_now();  // a wave without rows in this band
+      fold_acc(One{});
       if (more) {
         vm_wait(nstores);  // own dy rows and mask dwords of band it+1 (older than this band's stores)
         bwd2_convert_own<C, W, BR, EULER>(lds, buf ^ 1, own, mw, lane);
@@ -1935,6 +1974,7 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
       ASR_STAMP(it - i0, 0);
       barrier_vm(0);  // this wave's x rows of band it landed
       ASR_STAMP(it - i0, 1);
+      fold_issue(Two{});
       // x rows of band it+1 (rows 2.. when it continues this band's image)
       const int xr0 = nxt.n == cur.n ? 2 : 0;
       unsigned char* xn = lds + L::X + (buf ^ 1) * L::TILE + xr0 * L::ROWB;
@@ -2026,6 +2066,7 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
 #endif
       while (xj < xend) xdma();
       if (it + 1 < i1 && nxt.n == cur.n) bwd2_copy_halo<C, W, BR>(lds, buf, tid - 256);
+      fold_acc(Two{});
       ASR_STAMP(it - i0, 3);
     }
     barrier_vm(0);  // all items consumed: LDS reusable
@@ -2045,6 +2086,10 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
     float s = 0.f;
     for (int q = 0; q < 4 / G::OSPLIT; ++q) s += dbl[q * C + tid];
     slab[9 * C * C + tid] = s;
+  }
+  if (fold) {  // slabs the bands did not cover (a WG with fewer than 16 bands)
+    for (; fp < fpe; ++fp, foff += ES) facc += *(const f32x4*)(pslabs + foff);
+    *(f32x4*)(pgrp + (long)fg * ES + (foff - (unsigned)fpe * ES)) = facc;
   }
 }
 
@@ -2246,7 +2291,8 @@ static int launch_fwd(int mode, const void* x, const void* resid, void* y, uint8
 template <int C, int W>
 static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
                       float two_gamma, int N, int H, void* dx, float* slabs, int* nslabs, const void* extra,
-                      int skip_dy, int relu_dx, int* relu_done, hipStream_t s) {
+                      int skip_dy, int relu_dx, int* relu_done, const float* fold_slabs, int fold_P, float* fold_grp,
+                      int* fold_done, hipStream_t s) {
   const long items = (long)N * ((H + kBwdBR - 1) / kBwdBR);
   if (items > 0x7fffffffL) return fail(ASR_E_UNSUPPORTED, "bf16 block: too many row bands (%ld)", items);
   const int grid = persistent_grid(items);
@@ -2265,16 +2311,20 @@ static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* ma
       const size_t lds2 = std::max((size_t)L2::TOTAL, red);
       if (mode == blk::BWD_EULER && relu_dx) {
         hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_EULER, true>), dim3(grid), dim3(512), lds2, s,
-                           (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs);
+                           (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs,
+                           fold_slabs, fold_P, fold_grp);
         if (relu_done) *relu_done = 1;
       } else if (mode == blk::BWD_EULER) {
         hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_EULER, false>), dim3(grid), dim3(512), lds2, s,
-                           (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs);
+                           (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs,
+                           fold_slabs, fold_P, fold_grp);
       } else {
         hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_CONV, false>), dim3(grid), dim3(512), lds2, s,
-                           (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs);
+                           (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs,
+                           fold_slabs, fold_P, fold_grp);
       }
       ASR_LAUNCH_CHECK("k_bwd2");
+      if (fold_done) *fold_done = fold_P > 0;
       return ASR_OK;
     }
   }
@@ -2330,19 +2380,22 @@ int block_fwd_mfma(int mode, const void* x, const void* resid, void* y, uint8_t*
 
 int block_bwd_mfma(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
                    float two_gamma, int N, int H, int W, int C, void* dx, float* slabs, int* nslabs, const void* extra,
-                   int skip_dy, hipStream_t s, int relu_dx, int* relu_done) {
+                   int skip_dy, hipStream_t s, int relu_dx, int* relu_done, const float* fold_slabs, int fold_P,
+                   float* fold_grp, int* fold_done) {
   if (relu_done) *relu_done = 0;
+  if (fold_done) *fold_done = 0;
+  if (fold_P > kMaxBlockSlabs) fold_P = 0;  // (never: slab counts are grid sizes)
   if (W != 32) return fail(ASR_E_UNSUPPORTED, "bf16 block: W=%d not supported (W must be 32)", W);
   switch (C) {
     case 16:
       return launch_bwd<16, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, extra, skip_dy, relu_dx,
-                                relu_done, s);
+                                relu_done, fold_slabs, fold_P, fold_grp, fold_done, s);
     case 32:
       return launch_bwd<32, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, extra, skip_dy, relu_dx,
-                                relu_done, s);
+                                relu_done, fold_slabs, fold_P, fold_grp, fold_done, s);
     case 64:
       return launch_bwd<64, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, extra, skip_dy, relu_dx,
-                                relu_done, s);
+                                relu_done, fold_slabs, fold_P, fold_grp, fold_done, s);
   }
   return fail(ASR_E_UNSUPPORTED, "bf16 block: C=%d not supported (16, 32, 64)", C);
 }

@@ -155,3 +155,41 @@ def test_stem_wgrad_mfma_matches_fp32_path(rt, N, u8, monkeypatch):
     assert np.isfinite(s).all() and np.abs(s1).max() > 0
     tol = (1e-5 if u8 else 1e-3) * np.abs(s1).max()
     assert np.abs(s - s1).max() <= tol, (np.abs(s - s1).max(), tol)
+
+
+@pytest.mark.parametrize("N", [64, 512])
+def test_folded_slab_reduction_matches_separate(rt, N, monkeypatch):
+    """The network folds pass 1 of block l+1's slab reduction into block l's
+    backward kernel (two slab loads per band and thread, the rest after the
+    last band: N=64 leaves most for that tail).  With ASR_NO_FOLD set every
+    block's slabs are reduced by its own k_reduce_slabs launch.  Sums in a
+    different order: equal to fp32 reduction-order noise (1e-5 of max|g|
+    per block); the loss and the non-block gradients are bitwise equal."""
+    C, L = 64, 4
+    from differential_equations_resnet_amd.netparams import init_net_params, net_param_shapes
+    dev = torch.device("cuda")
+    params = torch.from_numpy(init_net_params(C, L, 3, 10, seed=5) * 0.5).to(dev)
+    rng = np.random.default_rng(13)
+    imgs = torch.from_numpy(rng.integers(0, 256, (N, 32, 32, 3), dtype=np.uint8)).to(dev)
+    tgt = torch.from_numpy(np.eye(10, dtype=np.float32)[rng.integers(0, 10, N)]).to(dev)
+    ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / L, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
+                        dtype="bfloat16", input_u8=True, device=dev)
+    loss, g = ex.forward_backward(params, imgs, tgt)
+    loss, g = loss.clone(), g.clone()
+    monkeypatch.setenv("ASR_NO_FOLD", "1")
+    loss1, g1 = ex.forward_backward(params, imgs, tgt)
+    loss1, g1 = loss1.clone(), g1.clone()
+    monkeypatch.delenv("ASR_NO_FOLD")
+    torch.cuda.synchronize()
+    assert torch.equal(loss, loss1)
+    sizes = [int(np.prod(s)) for s in net_param_shapes(C, L, 3, 10)]
+    stem = sizes[0] + sizes[1]
+    per_block = sum(sizes[2:2 + len(sizes[2:-2]) // L])
+    head = sizes[-2] + sizes[-1]
+    a, b = g.cpu().numpy(), g1.cpu().numpy()
+    assert np.array_equal(a[:stem], b[:stem]) and np.array_equal(a[-head:], b[-head:])
+    for l in range(L):
+        o = stem + l * per_block
+        ga, gb = a[o:o + per_block], b[o:o + per_block]
+        assert np.abs(gb).max() > 0
+        assert np.abs(ga - gb).max() <= 1e-5 * np.abs(gb).max(), (l, np.abs(ga - gb).max(), np.abs(gb).max())
