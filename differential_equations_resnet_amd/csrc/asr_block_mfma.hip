@@ -55,6 +55,9 @@
 #ifndef ASR_FWD_ST16
 #define ASR_FWD_ST16 1  // forward pipe: y as 16-B stores (row swap between the two pixel tiles)
 #endif
+#ifndef ASR_FWD_REUSE
+#define ASR_FWD_REUSE 1  // forward pipe: halo rows of a band continuing the previous band's image copied in LDS
+#endif
 #ifndef ASR_V2_WPIPE
 #define ASR_V2_WPIPE 1  // v2 backward: wgrad k-steps software-pipelined across m-tiles and k-steps
 #endif
@@ -846,6 +849,27 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
     const int yy = c.b * BR;
     dma_rows<C, W>(x, lds + buf * TILE, c.n, yy - 1, min(BR, H - yy) + 2, H, wave, NW, lane);
   };
+  // band c continues band p's image (p's tile in the other buffer, complete):
+  // its halo rows 0, 1 are p's rows BR, BR+1 -> copy them (interior columns),
+  // DMA only rows 2.. (ASR_FWD_REUSE)
+  auto dma_next2 = [&](const ItemCursor& c, const ItemCursor& p, int buf) {
+    if (!ASR_FWD_REUSE || c.n != p.n || c.b != p.b + 1) {
+      dma(c, buf);
+      return;
+    }
+    const int yy = c.b * BR;
+    constexpr int ROWB = TW * NQ * 16;
+    if (ASR_FWD_REUSE == 2) dma(c, buf);  // debug: full DMA, then the copy over rows 0, 1
+    else dma_rows<C, W>(x, lds + buf * TILE + 2 * ROWB, c.n, yy + 1, min(BR, H - yy), H, wave, NW, lane);
+    // plain LDS accesses (the DMA is inline asm, invisible to the compiler,
+    // so it waits only lgkmcnt for these; asm reads with a deferred wait are
+    // unsafe where hipcc copies their results before the wait)
+    const uint4* src = (const uint4*)(lds + (buf ^ 1) * TILE + BR * ROWB);
+    uint4* dst = (uint4*)(lds + buf * TILE);
+    constexpr int NCH = 2 * W * NQ;
+    for (int i = tid; i < NCH; i += 64 * NW) dst[((i / (W * NQ)) * TW + 1) * NQ + i % (W * NQ)] =
+        src[((i / (W * NQ)) * TW + 1) * NQ + i % (W * NQ)];
+  };
   int nst = 0;  // vector-memory ops this wave issued after the DMA the next barrier waits for
   // residual of a band: x from its LDS tile (read after the band's conv)
   auto xres_read = [&](int buf, u32x2 (&xr)[RB][PT]) {
@@ -983,7 +1007,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
     ASR_STAMP(it - i0, 1);
     nst = 0;
     dma_res(nx1, (it + 1 - i0) & 1);
-    if (it + 2 < i1) dma(nx2, (it - i0) & 1);
+    if (it + 2 < i1) dma_next2(nx2, nx1, (it - i0) & 1);
     ASR_STAMP(it - i0, 2);
     res_read((it - i0) & 1, xrA);
     init(accB);
@@ -1013,7 +1037,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
     ASR_STAMP(it - i0, 1);
     nst = 0;
     dma_res(nx1, (it + 1 - i0) & 1);
-    if (it + 2 < i1) dma(nx2, (it - i0) & 1);
+    if (it + 2 < i1) dma_next2(nx2, nx1, (it - i0) & 1);
     ASR_STAMP(it - i0, 2);
     res_read((it - i0) & 1, xrB);
     init(accA);
