@@ -257,7 +257,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": ("RK2 block fwd+bwd (2x blk::k_fwd_pipe, 2x blk::k_bwd, k_reduce_slabs, k_project)"
                            if integrator == "rk2" else
-                           "Euler block fwd+bwd (blk::k_fwd_pipe, blk::k_bwd fused dgrad+wgrad, k_reduce_slabs, "
+                           "Euler block fwd+bwd (blk::k_fwd_pipe, blk::k_bwd2 fused dgrad+wgrad, k_reduce_slabs, "
                            "k_project)"),
                 "algorithmic_bytes": rb["bytes"], "avg_us": round(rb["t"] * 1e6, 2),
                 "avg_us_fwd": round(rb["t_fwd"] * 1e6, 2), "avg_us_bwd": round(rb["t_bwd"] * 1e6, 2),
