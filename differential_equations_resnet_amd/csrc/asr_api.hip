@@ -40,6 +40,9 @@ int block_bwd_mfma(int mode, const void* dy, const void* x, const uint8_t* mask,
 int stem_wgrad_mfma(const void* img, int input_u8, const void* dz1, int N, int H, int W, int Cin, int C, float mean,
                     float inv_std, int use_norm, float* slabs, int* nslabs, hipStream_t s);
 bool stem_wgrad_mfma_supported(int Cin, int H, int W, int C);
+int stem_fwd_mfma(const void* img, int input_u8, const float* w1, const float* b1, int N, int H, int W, int Cin, int C,
+                  float mean, float inv_std, int use_norm, void* out, hipStream_t s);
+bool stem_fwd_mfma_supported(int Cin, int H, int W, int C);
 static bool mfma_supported(int C, int W) { return (C == 16 || C == 32 || C == 64) && W == 32; }
 // asr_conv_f32.hip
 int conv_f32(int fmode, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
@@ -367,7 +370,10 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
     return acts + (size_t)slot * L.P * L.act_bytes;
   };
   // 2. normalisation + conv1 + relu (tfkeras_resnets.py:555-572)
-  if (L.fast_stem) {
+  if (L.fast_stem && bf && stem_fwd_mfma_supported(c->Cin, H, W, C) && getenv("ASR_STEM_FWD_V1") == nullptr) {
+    ASR_TRY(stem_fwd_mfma(images, c->input_u8, params + L.off_c1k, params + L.off_c1b, N, H, W, c->Cin, C,
+                          c->subtract_mean, inv_std, c->use_norm, act(0), s));
+  } else if (L.fast_stem) {
     ASR_TRY(stem_forward(images, c->input_u8, params + L.off_c1k, params + L.off_c1b, N, H, W, c->Cin, C,
                          c->subtract_mean, inv_std, c->use_norm, act(0), bf ? 1 : 0, s));
   } else {

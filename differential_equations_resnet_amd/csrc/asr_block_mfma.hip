@@ -2230,6 +2230,95 @@ __global__ __launch_bounds__(256) void k_stem_wgrad_mfma(const Tin* __restrict__
   }
 }
 
+// ===========================================================================
+// Stem forward on MFMA (C=64, CIN=3, W=32): x1 = relu(conv3x3((v - mean) *
+// inv_std, W1) + b1), bf16 NHWC out (models/tfkeras_resnets.py:555-572).
+// M = o (4 tiles), K = kappa = tap*3 + ci (27, padded to 32: one k-step),
+// N = 16 pixels.  B: lane (pixel lx, kappa 8g..8g+7) gathers its 8 patch
+// values from the image staged in LDS as fp32 v - mean (bf16-exact for u8
+// input with a half-integer mean); A = inv_std * W1^T split into bf16 hi +
+// lo parts held in registers (two MFMAs per tile: W1 to ~16 mantissa bits,
+// so the result matches the fp32 VALU kernel to accumulation-order noise).
+// Epilogue: + b1 (fp32), relu, bf16, 16-B stores (a 16-lane row swap between
+// o-tile pairs gives each lane 8 consecutive channels).
+// ===========================================================================
+template <typename Tin>
+__global__ __launch_bounds__(256) void k_stem_fwd_mfma(const Tin* __restrict__ img, const float* __restrict__ w1,
+                                                       const float* __restrict__ b1, int N, int H, float mean,
+                                                       float inv_std, bf16* __restrict__ out) {
+  constexpr int C = 64, W = 32, CIN = 3, TW = W + 2, KC = 9 * CIN;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  float* ft = (float*)lds;  // staged image (fp32 v - mean), zero halo
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, lx = lane & 15;
+  for (int i = tid; i < (H + 2) * TW * CIN; i += 256) ft[i] = 0.f;  // halo stays zero
+  // A fragments: lane (o = 16 mt + lx, kappa 8g..8g+7), hi and lo bf16 parts
+  bf16x8 Ah[4], Al[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kap = 8 * g + j;
+      const float wv = kap < KC ? w1[kap * C + 16 * mt + lx] * inv_std : 0.f;
+      const bf16 hi = (bf16)wv;
+      Ah[mt][j] = hi;
+      Al[mt][j] = (bf16)(wv - (float)hi);
+    }
+  float bz[4][4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bz[mt][e] = b1 ? b1[16 * mt + 4 * g + e] : 0.f;
+  // B operand: lane (pixel lx, kappa 8g..8g+7) read straight from the staged
+  // image: tap (ky, kx), channel ci of kappa = offset (ky*TW + kx)*CIN + ci
+  int koff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int kap = min(8 * g + j, KC - 1), tap = kap / CIN, ci = kap % CIN;
+    koff[j] = ((tap / 3) * TW + tap % 3) * CIN + ci;
+  }
+  for (int n = blockIdx.x; n < N; n += gridDim.x) {
+    __syncthreads();  // the previous image fully read
+    const Tin* src = img + (long)n * H * W * CIN;
+    for (int i = tid; i < H * W * CIN; i += 256) {
+      const int ci = i % CIN, p = i / CIN;
+      ft[((p / W + 1) * TW + p % W + 1) * CIN + ci] = (float)src[i] - mean;
+    }
+    __syncthreads();
+    // pixel tiles: wave w takes tiles w, w+4, ... (16 pixels of one row each)
+    for (int pt = wave; pt < H * W / 16; pt += 4) {
+      const int y = pt / (W / 16), x0 = (pt % (W / 16)) * 16;
+      const float* pb = ft + (y * TW + x0 + lx) * CIN;
+      bf16x8 B;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) B[j] = (bf16)((8 * g + j < KC) ? pb[koff[j]] : 0.f);
+      f32x4 acc[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        acc[mt] = f32x4{bz[mt][0], bz[mt][1], bz[mt][2], bz[mt][3]};
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[mt], B, acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al[mt], B, acc[mt], 0, 0, 0);
+      }
+      // lane (g, lx): channels 16 mt + 4g + e of pixel x0 + lx
+      u32x2 ov[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        bf16x4 o4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaxf(acc[mt][e], 0.f);
+        ov[mt] = *(const u32x2*)&o4;
+      }
+      bf16* orow = out + (((long)n * H + y) * W + x0 + lx) * C;
+#pragma unroll
+      for (int mp = 0; mp < 2; ++mp) {  // o-tiles 2mp, 2mp+1 -> lane row g: channels 16(2mp + (g&1)) + 8(g>>1)
+        const auto s0 = __builtin_amdgcn_permlane16_swap(ov[2 * mp][0], ov[2 * mp + 1][0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(ov[2 * mp][1], ov[2 * mp + 1][1], false, false);
+        *(u32x4*)(orow + 16 * (2 * mp + (g & 1)) + 8 * (g >> 1)) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+      }
+    }
+  }
+}
+
 }  // namespace blk
 
 // ---------------------------------------------------------------------------
@@ -2388,6 +2477,29 @@ int stem_wgrad_mfma(const void* img, int input_u8, const void* dz1, int N, int H
     hipLaunchKernelGGL(blk::k_stem_wgrad_mfma<float>, dim3(grid), dim3(256), lds, s, (const float*)img,
                        (const bf16*)dz1, N, H, m, is, slabs);
   ASR_LAUNCH_CHECK("k_stem_wgrad_mfma");
+  return ASR_OK;
+}
+
+bool stem_fwd_mfma_supported(int Cin, int H, int W, int C) {
+  const size_t lds = (size_t)(H + 2) * 34 * 3 * 4;
+  return Cin == 3 && W == 32 && C == 64 && H >= 1 && lds <= 160 * 1024;
+}
+
+int stem_fwd_mfma(const void* img, int input_u8, const float* w1, const float* b1, int N, int H, int W, int Cin, int C,
+                  float mean, float inv_std, int use_norm, void* out, hipStream_t s) {
+  if (!stem_fwd_mfma_supported(Cin, H, W, C)) return fail(ASR_E_UNSUPPORTED, "stem fwd (MFMA): unsupported shape");
+  int cus = cu_count();
+  if (cus <= 0) cus = 256;
+  const int grid = std::max(1, std::min(N, 4 * cus));
+  const size_t lds = (size_t)(H + 2) * 34 * 3 * 4;
+  const float m = use_norm ? mean : 0.f, is = use_norm ? inv_std : 1.f;
+  if (input_u8)
+    hipLaunchKernelGGL(blk::k_stem_fwd_mfma<uint8_t>, dim3(grid), dim3(256), lds, s, (const uint8_t*)img, w1, b1, N,
+                       H, m, is, (bf16*)out);
+  else
+    hipLaunchKernelGGL(blk::k_stem_fwd_mfma<float>, dim3(grid), dim3(256), lds, s, (const float*)img, w1, b1, N, H,
+                       m, is, (bf16*)out);
+  ASR_LAUNCH_CHECK("k_stem_fwd_mfma");
   return ASR_OK;
 }
 

@@ -193,3 +193,30 @@ def test_folded_slab_reduction_matches_separate(rt, N, monkeypatch):
         ga, gb = a[o:o + per_block], b[o:o + per_block]
         assert np.abs(gb).max() > 0
         assert np.abs(ga - gb).max() <= 1e-5 * np.abs(gb).max(), (l, np.abs(ga - gb).max(), np.abs(gb).max())
+
+
+@pytest.mark.parametrize("N,u8", [(64, True), (512, True), (64, False)])
+def test_stem_fwd_mfma_matches_fp32_path(rt, N, u8, monkeypatch):
+    """The bf16 network's stem forward runs on MFMA (im2col of bf16 (v - mean)
+    from LDS, inv_std * W1 split into bf16 hi + lo); with ASR_STEM_FWD_V1 set
+    it runs the fp32 VALU stem kernel.  Same probabilities to bf16 noise
+    propagated through the blocks (1e-3 absolute; the stem output itself is
+    rounded to bf16 in both)."""
+    C, L = 64, 2
+    from differential_equations_resnet_amd.netparams import init_net_params
+    dev = torch.device("cuda")
+    params = torch.from_numpy(init_net_params(C, L, 3, 10, seed=4) * 0.5).to(dev)
+    rng = np.random.default_rng(17)
+    raw = rng.integers(0, 256, (N, 32, 32, 3), dtype=np.uint8)
+    imgs = torch.from_numpy(raw if u8 else raw.astype(np.float32) + rng.random(raw.shape, np.float32)).to(dev)
+    ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / L, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
+                        dtype="bfloat16", input_u8=u8, device=dev)
+    p = ex.forward(params, imgs).clone()
+    monkeypatch.setenv("ASR_STEM_FWD_V1", "1")
+    p1 = ex.forward(params, imgs).clone()
+    monkeypatch.delenv("ASR_STEM_FWD_V1")
+    torch.cuda.synchronize()
+    a, b = p.cpu().numpy(), p1.cpu().numpy()
+    assert np.isfinite(a).all()
+    assert np.abs(a - b).max() <= 1e-3, np.abs(a - b).max()
+    assert (a.argmax(1) == b.argmax(1)).mean() >= 0.98
