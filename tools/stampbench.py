@@ -71,7 +71,7 @@ else:
 nb = 16 if WHAT.startswith("bwd") else 8
 for role in names:
     seg = []
-    for b in range(1, nb - 1):
+    for b in range(1, nb - 2 if WHAT == "fwd" else nb - 1):  # the forward's last band exits before its stamps
         row = st[:, role, b, :]
         if order is not None:
             row = row[:, order[role]]
