@@ -58,9 +58,6 @@
 #ifndef ASR_FWD_REUSE
 #define ASR_FWD_REUSE 1  // forward pipe: halo rows of a band continuing the previous band's image copied in LDS
 #endif
-#ifndef ASR_FWD_COPY_LATE
-#define ASR_FWD_COPY_LATE 0  // forward pipe: the halo copy after the band's conv instead of before it
-#endif
 #ifndef ASR_V2_WPIPE
 #define ASR_V2_WPIPE 1  // v2 backward: wgrad k-steps software-pipelined across m-tiles and k-steps
 #endif
@@ -855,31 +852,23 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
   // band c continues band p's image (p's tile in the other buffer, complete):
   // its halo rows 0, 1 are p's rows BR, BR+1 -> copy them (interior columns),
   // DMA only rows 2.. (ASR_FWD_REUSE)
-  auto halo_copy = [&](int buf) {
+  auto dma_next2 = [&](const ItemCursor& c, const ItemCursor& p, int buf) {
+    if (!ASR_FWD_REUSE || c.n != p.n || c.b != p.b + 1) {
+      dma(c, buf);
+      return;
+    }
+    const int yy = c.b * BR;
+    constexpr int ROWB = TW * NQ * 16;
+    if (ASR_FWD_REUSE == 2) dma(c, buf);  // debug: full DMA, then the copy over rows 0, 1
+    else dma_rows<C, W>(x, lds + buf * TILE + 2 * ROWB, c.n, yy + 1, min(BR, H - yy), H, wave, NW, lane);
     // plain LDS accesses (the DMA is inline asm, invisible to the compiler,
     // so it waits only lgkmcnt for these; asm reads with a deferred wait are
     // unsafe where hipcc copies their results before the wait)
-    constexpr int ROWB = TW * NQ * 16;
     const uint4* src = (const uint4*)(lds + (buf ^ 1) * TILE + BR * ROWB);
     uint4* dst = (uint4*)(lds + buf * TILE);
     constexpr int NCH = 2 * W * NQ;
     for (int i = tid; i < NCH; i += 64 * NW) dst[((i / (W * NQ)) * TW + 1) * NQ + i % (W * NQ)] =
         src[((i / (W * NQ)) * TW + 1) * NQ + i % (W * NQ)];
-  };
-  // DMA of band c into buffer buf; when c continues band p's image (p's tile
-  // in the other buffer, complete) only rows 2.. and returns true: the caller
-  // then copies p's rows BR, BR+1 into c's rows 0, 1 (halo_copy) before the
-  // next barrier (ASR_FWD_REUSE)
-  auto dma_next2 = [&](const ItemCursor& c, const ItemCursor& p, int buf) -> bool {
-    if (!ASR_FWD_REUSE || c.n != p.n || c.b != p.b + 1) {
-      dma(c, buf);
-      return false;
-    }
-    const int yy = c.b * BR;
-    constexpr int ROWB = TW * NQ * 16;
-    dma_rows<C, W>(x, lds + buf * TILE + 2 * ROWB, c.n, yy + 1, min(BR, H - yy), H, wave, NW, lane);
-    if (!ASR_FWD_COPY_LATE) halo_copy(buf);
-    return ASR_FWD_COPY_LATE;
   };
   int nst = 0;  // vector-memory ops this wave issued after the DMA the next barrier waits for
   // residual of a band: x from its LDS tile (read after the band's conv)
@@ -1018,7 +1007,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
     ASR_STAMP(it - i0, 1);
     nst = 0;
     dma_res(nx1, (it + 1 - i0) & 1);
-    const bool hc = it + 2 < i1 && dma_next2(nx2, nx1, (it - i0) & 1);
+    if (it + 2 < i1) dma_next2(nx2, nx1, (it - i0) & 1);
     ASR_STAMP(it - i0, 2);
     res_read((it - i0) & 1, xrA);
     init(accB);
@@ -1028,7 +1017,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
       conv_band<C, W, RB, NU>(lds_u32(lds + ((it + 1 - i0) & 1) * TILE + r0 * BD::ROWB), lo, A, accB, hook);
     }
     ASR_STAMP(it - i0, 3);
-    if (hc) halo_copy((it - i0) & 1);
     xres_read((it + 1 - i0) & 1, xrB);
     ASR_STAMP(it - i0, 4);
     ++it;
@@ -1049,7 +1037,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
     ASR_STAMP(it - i0, 1);
     nst = 0;
     dma_res(nx1, (it + 1 - i0) & 1);
-    const bool hc2 = it + 2 < i1 && dma_next2(nx2, nx1, (it - i0) & 1);
+    if (it + 2 < i1) dma_next2(nx2, nx1, (it - i0) & 1);
     ASR_STAMP(it - i0, 2);
     res_read((it - i0) & 1, xrB);
     init(accA);
@@ -1059,7 +1047,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
       conv_band<C, W, RB, NU>(lds_u32(lds + ((it + 1 - i0) & 1) * TILE + r0 * BD::ROWB), lo, A, accA, hook);
     }
     ASR_STAMP(it - i0, 3);
-    if (hc2) halo_copy((it - i0) & 1);
     xres_read((it + 1 - i0) & 1, xrA);
     ASR_STAMP(it - i0, 4);
     ++it;
