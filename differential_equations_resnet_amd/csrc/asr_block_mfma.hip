@@ -814,7 +814,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
   using BD = Band<C, W, RB>;
   // epilogue units: (row, pixel tile), or rows with both pixel tiles stored
   // as 16-B chunks (ASR_FWD_ST16)
-  constexpr bool ST16 = ASR_FWD_ST16 && PT == 2;
+  constexpr bool ST16 = ASR_FWD_ST16 && PT == 2 && !RES;  // (RES: register-tight already)
   constexpr int NU = ST16 ? RB : RB * PT;
   constexpr bool EULER = MODE == FWD_EULER;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -853,7 +853,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
   // its halo rows 0, 1 are p's rows BR, BR+1 -> copy them (interior columns),
   // DMA only rows 2.. (ASR_FWD_REUSE)
   auto dma_next2 = [&](const ItemCursor& c, const ItemCursor& p, int buf) {
-    if (!ASR_FWD_REUSE || c.n != p.n || c.b != p.b + 1) {
+    if (!ASR_FWD_REUSE || RES || c.n != p.n || c.b != p.b + 1) {
       dma(c, buf);
       return;
     }
