@@ -1718,7 +1718,7 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
                                               const uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
                                               float h, float two_gamma, int N, int H, bf16* __restrict__ dx,
                                               float* __restrict__ slabs, const float* __restrict__ pslabs, int pP,
-                                              float* __restrict__ pgrp) {
+                                              float* __restrict__ pgrp, int skip_dy) {
   using G = Geo<C>;
   using L = Bwd2Lds<C, W, BR>;
   constexpr int TW = W + 2, PT = W / 16, OTW = G::OTW, OT = G::OT, MTW = G::MTW, IPR = W / G::PPI;
@@ -1904,12 +1904,15 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
             bf16x4 o4;
             if constexpr (EULER) {
               const bf16x4 dyr = *(const bf16x4*)&dyv[pt][t];
+              float res[4];  // the +dy residual (none in the second RK2 stage)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) res[e] = skip_dy ? 0.f : (float)dyr[e];
               if (g2) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(hs2g, dzf[e], fmaf(-hs, acc[t][pt][e], (float)dyr[e]));
+                for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(hs2g, dzf[e], fmaf(-hs, acc[t][pt][e], res[e]));
               } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(-hs, acc[t][pt][e], (float)dyr[e]);
+                for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(-hs, acc[t][pt][e], res[e]);
               }
             } else {
 #pragma unroll
@@ -2419,22 +2422,22 @@ static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* ma
   const bool xt = extra != nullptr || skip_dy != 0;
   static const bool v1 = getenv("ASR_BWD_V1") != nullptr;  // development A/B
   if constexpr (C == 64) {
-    if (!xt && !v1) {
+    if (!extra && (mode == blk::BWD_EULER || !skip_dy) && !v1) {  // v2: no extra dx term (RK2 stage 1 stays on v1)
       using L2 = blk::Bwd2Lds<C, W, kBwdBR>;
       const size_t lds2 = std::max((size_t)L2::TOTAL, red);
       if (mode == blk::BWD_EULER && relu_dx) {
         hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_EULER, true>), dim3(grid), dim3(512), lds2, s,
                            (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs,
-                           fold_slabs, fold_P, fold_grp);
+                           fold_slabs, fold_P, fold_grp, skip_dy);
         if (relu_done) *relu_done = 1;
       } else if (mode == blk::BWD_EULER) {
         hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_EULER, false>), dim3(grid), dim3(512), lds2, s,
                            (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs,
-                           fold_slabs, fold_P, fold_grp);
+                           fold_slabs, fold_P, fold_grp, skip_dy);
       } else {
         hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_CONV, false>), dim3(grid), dim3(512), lds2, s,
                            (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs,
-                           fold_slabs, fold_P, fold_grp);
+                           fold_slabs, fold_P, fold_grp, skip_dy);
       }
       ASR_LAUNCH_CHECK("k_bwd2");
       if (fold_done) *fold_done = fold_P > 0;
