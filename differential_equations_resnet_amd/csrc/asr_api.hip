@@ -36,7 +36,7 @@ int block_bwd_mfma(int mode, const void* dy, const void* x, const uint8_t* mask,
                    float two_gamma, int N, int H, int W, int C, void* dx, float* slabs, int* nslabs, const void* extra,
                    int skip_dy, hipStream_t s, int relu_dx = 0, int* relu_done = nullptr,
                    const float* fold_slabs = nullptr, int fold_P = 0, float* fold_grp = nullptr,
-                   int* fold_done = nullptr);
+                   int* fold_done = nullptr, int accum = 0);
 int stem_wgrad_mfma(const void* img, int input_u8, const void* dz1, int N, int H, int W, int Cin, int C, float mean,
                     float inv_std, int use_norm, float* slabs, int* nslabs, hipStream_t s);
 bool stem_wgrad_mfma_supported(int Cin, int H, int W, int C);
@@ -110,7 +110,7 @@ static int block_backward(int mode, const void* dy, const void* x, const uint8_t
                           float gamma, int N, int H, int W, int C, int dtype, void* dx, bool need_w, const void* extra,
                           bool skip_dy, float* slabs, float* dz_scratch, int* nsl, hipStream_t s, bool relu_dx = false,
                           int* relu_done = nullptr, const float* fold_slabs = nullptr, int fold_P = 0,
-                          float* fold_grp = nullptr, int* fold_done = nullptr) {
+                          float* fold_grp = nullptr, int* fold_done = nullptr, bool accum_slabs = false) {
   *nsl = 0;
   if (relu_done) *relu_done = 0;
   if (fold_done) *fold_done = 0;
@@ -118,8 +118,9 @@ static int block_backward(int mode, const void* dy, const void* x, const uint8_t
     if (!dx && !need_w) return ASR_OK;
     const int cm = (mode == ASR_MODE_EULER) ? 2 : 3;  // BWD_EULER / BWD_CONV
     return block_bwd_mfma(cm, dy, x, mask, w, h, 2.f * gamma, N, H, W, C, dx, slabs, nsl, extra, skip_dy ? 1 : 0, s,
-                          relu_dx ? 1 : 0, relu_done, fold_slabs, fold_P, fold_grp, fold_done);
+                          relu_dx ? 1 : 0, relu_done, fold_slabs, fold_P, fold_grp, fold_done, accum_slabs ? 1 : 0);
   }
+  if (accum_slabs) return fail(ASR_E_UNSUPPORTED, "slab accumulation: bf16 path only");
   const bool euler = mode == ASR_MODE_EULER;
   ASR_TRY(make_dz(euler ? F_EULER : F_CONV, dy, mask, nullptr, h, N, H, W, C, 0, dz_scratch, s));
   if (dx)
@@ -170,17 +171,24 @@ static int rk2_forward_impl(const void* x, void* xmid, void* y, uint8_t* mask1, 
 
 // Backward of rk2_forward_impl: with dz2 = h dy mask2 and g = A^T dz2 (the
 // gradient reaching xm), dz1 = (h/2) g mask1 and dx = dy + g + A^T dz1;
-// dW collects x (x) dz1 + xm (x) dz2 (both stages' slabs, reduced together).
+// dW collects x (x) dz1 + xm (x) dz2.  bf16: both stages run on the same
+// persistent grid, so the first stage adds its slabs onto the second's (one
+// slab set per block, *nsl = the grid); fp32: two slab sets, reduced together.
+// fold_* as block_bwd_mfma (carried by the second stage's kernel).
 static int rk2_backward_slabs(const void* dy, const void* x, const void* xmid, const uint8_t* mask1,
                               const uint8_t* mask2, const void* w, float h, float gamma, int N, int H, int W, int C,
                               int dtype, void* dx, void* g, bool need_w, float* slabs, float* dz_scratch, int* nsl,
-                              hipStream_t s) {
+                              hipStream_t s, const float* fold_slabs = nullptr, int fold_P = 0,
+                              float* fold_grp = nullptr, int* fold_done = nullptr) {
   int n2 = 0, n1 = 0;
+  const bool one_set = dtype == ASR_BF16 && getenv("ASR_RK2_TWO_SETS") == nullptr;  // (A/B: two slab sets)
   ASR_TRY(block_backward(ASR_MODE_EULER, dy, xmid, mask2, w, h, gamma, N, H, W, C, dtype, g, need_w, nullptr, true,
-                         slabs, dz_scratch, &n2, s));
+                         slabs, dz_scratch, &n2, s, false, nullptr, fold_slabs, fold_P, fold_grp, fold_done));
   ASR_TRY(block_backward(ASR_MODE_EULER, g, x, mask1, w, 0.5f * h, gamma, N, H, W, C, dtype, dx, need_w, dy, false,
-                         slabs + (long)n2 * (9L * C * C + C), dz_scratch, &n1, s));
-  *nsl = n1 + n2;
+                         one_set ? slabs : slabs + (long)n2 * (9L * C * C + C), dz_scratch, &n1, s, false, nullptr,
+                         nullptr, 0, nullptr, nullptr, one_set));
+  if (one_set && n1 != n2) return fail(ASR_E_UNSUPPORTED, "rk2 backward: stage grids differ (%d vs %d)", n1, n2);
+  *nsl = one_set ? n2 : n1 + n2;
   return ASR_OK;
 }
 
@@ -196,6 +204,18 @@ __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float
     m[i] = mi;
     v[i] = vi;
     p[i] -= lr_t * mi / (sqrtf(vi) + eps);
+  }
+}
+
+// dz1 = dx1 * [x1 > 0] in place (bf16, 8 elements per thread): the stem's
+// relu' for networks whose first block's backward cannot fuse it (RK2)
+__global__ __launch_bounds__(256) void k_relu_grad_bf16(bf16* __restrict__ d, const bf16* __restrict__ x, long n8) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    bf16x8 dv = ((const bf16x8*)d)[i];
+    const bf16x8 xv = ((const bf16x8*)x)[i];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dv[e] = (float)xv[e] > 0.f ? dv[e] : (bf16)0.f;
+    ((bf16x8*)d)[i] = dv;
   }
 }
 
@@ -342,7 +362,7 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.bwdws = take(std::max(bw.total, stem_ws));
   // odd Euler blocks' slabs (even ones use the backward workspace's): a
   // block's slabs stay readable while the next block's kernel reduces them
-  L.slabs2 = L.rk2 ? 0 : take((size_t)kMaxSlabsApi * (L.E + C) * 4);
+  L.slabs2 = take((size_t)L.stages * kMaxSlabsApi * (L.E + C) * 4);  // every other block's slabs
   L.grp_stride = (long)reduce_groups(L.stages * kMaxSlabsApi) * (L.E + C);
   L.grp = take((size_t)c->L * L.grp_stride * 4);
   L.probs = take((size_t)c->N * K * 4);
@@ -572,7 +592,7 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   int nsl_blk = 0;
   const BwdWs bw = bwd_ws_layout(N, H, W, C, cfg->dtype, L.stages);
   int dz1_fused = 0;  // dcur holds dz1 = dx1 * [x1 > 0] after the block loop
-  const float* pend_slabs = nullptr;  // Euler blocks: the slabs whose pass-1 reduction is still pending
+  const float* pend_slabs = nullptr;  // the slabs whose pass-1 reduction is still pending
   int pend_P = 0;
   float* pend_grp = nullptr;
   const bool fold_on = getenv("ASR_NO_FOLD") == nullptr;  // A/B: the reduction as separate launches
@@ -582,30 +602,28 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
     const uint8_t* mask = (const uint8_t*)(b + L.masks) + (size_t)l * L.mask_bytes;
     const float gam = L.sep_bwd ? 0.f : cfg->gamma;
     float* grp_l = (float*)(b + L.grp) + (size_t)l * L.grp_stride;
+    // a block's slabs alternate between two buffers; pass 1 of the previous
+    // (deeper) block's reduction rides in this block's (second-stage) kernel
+    // when it can (else it runs here), and this block's waits for the next
+    // block (or the end of the loop)
+    float* slabs_l = (float*)(b + ((l & 1) ? L.slabs2 : L.bwdws + bw.slabs));
+    int nsl = 0, folded = 0;
     if (L.rk2) {
-      float* slabs = (float*)(b + L.bwdws + bw.slabs);
       const unsigned char* xm = b + L.xmids + (size_t)l * L.P * L.act_bytes;
       ASR_TRY(rk2_backward_slabs(dcur, act(l), xm, mask, mask + (size_t)cfg->L * L.mask_bytes, wl, cfg->h, gam, N, H,
-                                 W, C, cfg->dtype, dnext, b + L.dxg, true, slabs, (float*)(b + L.bwdws + bw.dz),
-                                 &nsl_blk, s));
-      ASR_TRY(reduce_slabs_to_groups(slabs, nsl_blk, L.E + C, grp_l, s));
+                                 W, C, cfg->dtype, dnext, b + L.dxg, true, slabs_l, (float*)(b + L.bwdws + bw.dz),
+                                 &nsl, s, fold_on ? pend_slabs : nullptr, fold_on ? pend_P : 0, pend_grp, &folded));
     } else {
-      // Euler block: its slabs alternate between two buffers; pass 1 of the
-      // previous (deeper) block's reduction rides in this block's kernel when
-      // it can (else it runs here), and this block's waits for the next
-      // block (or the end of the loop)
-      float* slabs_l = (float*)(b + ((l & 1) ? L.slabs2 : L.bwdws + bw.slabs));
-      int nsl = 0, folded = 0;
       ASR_TRY(block_backward(ASR_MODE_EULER, dcur, act(l), mask, wl, cfg->h, gam, N, H, W, C, cfg->dtype, dnext, true,
                              nullptr, false, slabs_l, (float*)(b + L.bwdws + bw.dz), &nsl, s,
                              l == 0 && L.fast_stem && bf && !stem_v1, l == 0 ? &dz1_fused : nullptr,
                              fold_on ? pend_slabs : nullptr, fold_on ? pend_P : 0, pend_grp, &folded));
-      if (pend_P > 0 && !folded) ASR_TRY(reduce_slabs_to_groups(pend_slabs, pend_P, L.E + C, pend_grp, s));
-      pend_slabs = slabs_l;
-      pend_P = nsl;
-      pend_grp = grp_l;
-      nsl_blk = nsl;
     }
+    if (pend_P > 0 && !folded) ASR_TRY(reduce_slabs_to_groups(pend_slabs, pend_P, L.E + C, pend_grp, s));
+    pend_slabs = slabs_l;
+    pend_P = nsl;
+    pend_grp = grp_l;
+    nsl_blk = nsl;
     std::swap(dcur, dnext);
   }
   if (pend_P > 0) ASR_TRY(reduce_slabs_to_groups(pend_slabs, pend_P, L.E + C, pend_grp, s));
@@ -620,6 +638,13 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   float* red = (float*)(sw + align_up((size_t)L.P * 4, 256) + align_up((size_t)kMaxSlabsApi * (E1 + C) * 4, 256));
   int nsl = 0;
   const float inv_std = cfg->use_norm ? 1.f / cfg->divide_by_stddev : 1.f;
+  if (L.fast_stem && bf && !dz1_fused && !stem_v1 && stem_wgrad_mfma_supported(cfg->Cin, H, W, C) && L.P % 8 == 0) {
+    const long n8 = (long)L.P / 8;
+    hipLaunchKernelGGL(k_relu_grad_bf16, dim3((unsigned)std::min<long>((n8 + 255) / 256, 4096)), dim3(256), 0, s,
+                       (bf16*)dcur, (const bf16*)act(0), n8);
+    ASR_LAUNCH_CHECK("k_relu_grad_bf16");
+    dz1_fused = 1;
+  }
   if (L.fast_stem && dz1_fused && stem_wgrad_mfma_supported(cfg->Cin, H, W, C)) {
     ASR_TRY(stem_wgrad_mfma(images, cfg->input_u8, dcur, N, H, W, cfg->Cin, C, cfg->subtract_mean, inv_std,
                             cfg->use_norm, slabs, &nsl, s));

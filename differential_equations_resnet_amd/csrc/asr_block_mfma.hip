@@ -1246,7 +1246,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
                                              const uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
                                              float h, float two_gamma, int N, int H, bf16* __restrict__ dx,
                                              float* __restrict__ slabs, const bf16* __restrict__ extra,
-                                             int skip_dy) {
+                                             int skip_dy, int accum) {
   using G = Geo<C>;
   using L = BwdLds<C, W, BR>;
   constexpr int TW = W + 2, PT = W / 16, NQ = G::NQ, OTW = G::OTW, OT = G::OT, MTW = G::MTW;
@@ -1257,6 +1257,9 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
   // of the Euler block's kernel
   const bool has_extra = XT && extra != nullptr;
   const bool no_dy = XT && skip_dy != 0;
+  // XT && accum: add to the slab this WG's slot already holds (the RK2 first
+  // stage onto the second stage's slabs: same grid, so one slab set per block)
+  const bool acc_slab = XT && accum != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, lx = lane & 15;
@@ -1578,15 +1581,31 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
       __syncthreads();
     }
     if (kg == 0) {
+      // acc_slab: the old values of MC m-tiles loaded before their first
+      // store (one latency per chunk, not one per element: the compiler keeps
+      // load/store pairs to the slab in order)
+      constexpr int MC = MTW % 3 == 0 ? 3 : 1;
 #pragma unroll
-      for (int mi = 0; mi < MTW; ++mi)
+      for (int m0 = 0; m0 < MTW; m0 += MC) {
+        float prev[MC][OT][4];
 #pragma unroll
-        for (int ot = 0; ot < OT; ++ot)
+        for (int mi = 0; mi < MC; ++mi)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int m = 16 * (tg * MTW + mi) + 4 * g + e;
-            slab[(long)m * C + 16 * ot + lx] = hs * acc[mi][ot][e];
-          }
+          for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              prev[mi][ot][e] =
+                  acc_slab ? slab[(long)(16 * (tg * MTW + m0 + mi) + 4 * g + e) * C + 16 * ot + lx] : 0.f;
+#pragma unroll
+        for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+          for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int m = 16 * (tg * MTW + m0 + mi) + 4 * g + e;
+              slab[(long)m * C + 16 * ot + lx] = fmaf(hs, acc[m0 + mi][ot][e], prev[mi][ot][e]);
+            }
+      }
     }
   }
   __syncthreads();
@@ -1594,7 +1613,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
     const float* dbl = (const float*)lds + 12288;
     float s = 0.f;
     for (int q = 0; q < 4 / G::OSPLIT; ++q) s += dbl[q * C + tid];
-    slab[9 * C * C + tid] = s;
+    slab[9 * C * C + tid] = acc_slab ? slab[9 * C * C + tid] + s : s;
   }
 }
 
@@ -2408,7 +2427,7 @@ template <int C, int W>
 static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
                       float two_gamma, int N, int H, void* dx, float* slabs, int* nslabs, const void* extra,
                       int skip_dy, int relu_dx, int* relu_done, const float* fold_slabs, int fold_P, float* fold_grp,
-                      int* fold_done, hipStream_t s) {
+                      int* fold_done, int accum, hipStream_t s) {
   const long items = (long)N * ((H + kBwdBR - 1) / kBwdBR);
   if (items > 0x7fffffffL) return fail(ASR_E_UNSUPPORTED, "bf16 block: too many row bands (%ld)", items);
   const int grid = persistent_grid(items);
@@ -2418,13 +2437,16 @@ static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* ma
   const size_t lds = std::max((size_t)(extra ? L::TOTAL_XT : L::TOTAL), red);
 #define ASR_LAUNCH_BWD(M, XT)                                                                                    \
   hipLaunchKernelGGL((blk::k_bwd<C, W, kBwdBR, M, XT>), dim3(grid), dim3(512), lds, s, (const bf16*)dy, (const bf16*)x, \
-                     mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs, (const bf16*)extra, skip_dy)
-  const bool xt = extra != nullptr || skip_dy != 0;
+                     mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs, (const bf16*)extra, skip_dy, accum)
+  const bool xt = extra != nullptr || skip_dy != 0 || accum != 0;
   static const bool v1 = getenv("ASR_BWD_V1") != nullptr;  // development A/B
   if constexpr (C == 64) {
-    if (!extra && (mode == blk::BWD_EULER || !skip_dy) && !v1) {  // v2: no extra dx term (RK2 stage 1 stays on v1)
+    if (!extra && !accum && (mode == blk::BWD_EULER || !skip_dy) && !v1) {  // v2: no extra dx term (RK2 stage 1 stays on v1)
       using L2 = blk::Bwd2Lds<C, W, kBwdBR>;
       const size_t lds2 = std::max((size_t)L2::TOTAL, red);
+      // the folded pass gives each thread one 16-B chunk: at most 512 per WG
+      const long fchunks = (long)((fold_P + 31) / 32) * ((9 * C * C + C) / 4);
+      if ((fchunks + grid - 1) / grid > 512) fold_P = 0;
       if (mode == blk::BWD_EULER && relu_dx) {
         hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_EULER, true>), dim3(grid), dim3(512), lds2, s,
                            (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs,
@@ -2520,7 +2542,7 @@ int block_fwd_mfma(int mode, const void* x, const void* resid, void* y, uint8_t*
 int block_bwd_mfma(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
                    float two_gamma, int N, int H, int W, int C, void* dx, float* slabs, int* nslabs, const void* extra,
                    int skip_dy, hipStream_t s, int relu_dx, int* relu_done, const float* fold_slabs, int fold_P,
-                   float* fold_grp, int* fold_done) {
+                   float* fold_grp, int* fold_done, int accum) {
   if (relu_done) *relu_done = 0;
   if (fold_done) *fold_done = 0;
   if (fold_P > kMaxBlockSlabs) fold_P = 0;  // (never: slab counts are grid sizes)
@@ -2528,13 +2550,13 @@ int block_bwd_mfma(int mode, const void* dy, const void* x, const uint8_t* mask,
   switch (C) {
     case 16:
       return launch_bwd<16, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, extra, skip_dy, relu_dx,
-                                relu_done, fold_slabs, fold_P, fold_grp, fold_done, s);
+                                relu_done, fold_slabs, fold_P, fold_grp, fold_done, accum, s);
     case 32:
       return launch_bwd<32, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, extra, skip_dy, relu_dx,
-                                relu_done, fold_slabs, fold_P, fold_grp, fold_done, s);
+                                relu_done, fold_slabs, fold_P, fold_grp, fold_done, accum, s);
     case 64:
       return launch_bwd<64, 32>(mode, dy, x, mask, w, h, two_gamma, N, H, dx, slabs, nslabs, extra, skip_dy, relu_dx,
-                                relu_done, fold_slabs, fold_P, fold_grp, fold_done, s);
+                                relu_done, fold_slabs, fold_P, fold_grp, fold_done, accum, s);
   }
   return fail(ASR_E_UNSUPPORTED, "bf16 block: C=%d not supported (16, 32, 64)", C);
 }
