@@ -61,6 +61,9 @@
 #ifndef ASR_V2_WPIPE
 #define ASR_V2_WPIPE 1  // v2 backward: wgrad k-steps software-pipelined across m-tiles and k-steps
 #endif
+#ifndef ASR_XT_EARLY
+#define ASR_XT_EARLY 1  // v2 backward, RK2 first stage: extra-term loads of row 0 before the dy DMA burst (0: after)
+#endif
 #ifndef ASR_ABLATE
 #define ASR_ABLATE 0  // development only: fwd 1 no epilogue, 2 no MFMA, 3 no prefetch DMA;
                       // bwd 4 no convert, 5 no dgrad MFMA, 6 no wgrad MFMA, 7 no dgrad epilogue,
@@ -1732,12 +1735,16 @@ __device__ __forceinline__ void bwd2_convert_own(unsigned char* lds, int nb, con
 
 // RO: dx *= [x > 0] (x = this block's input; the network's first block, so
 // that dx is the stem's dz1 = dx1 * relu'(x1) directly)
-template <int C, int W, int BR, int MODE, bool RO>
+// XT (RK2 first stage): dx gets the extra term `extra` (the step's outer dy,
+// read from global memory in the epilogue, issued before the row's conv) and
+// the slabs are added onto the ones this WG's slot holds (the second stage's).
+template <int C, int W, int BR, int MODE, bool RO, bool XT = false>
 __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                               const uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
                                               float h, float two_gamma, int N, int H, bf16* __restrict__ dx,
                                               float* __restrict__ slabs, const float* __restrict__ pslabs, int pP,
-                                              float* __restrict__ pgrp, int skip_dy) {
+                                              float* __restrict__ pgrp, int skip_dy,
+                                              const bf16* __restrict__ extra = nullptr) {
   using G = Geo<C>;
   using L = Bwd2Lds<C, W, BR>;
   constexpr int TW = W + 2, PT = W / 16, OTW = G::OTW, OT = G::OT, MTW = G::MTW, IPR = W / G::PPI;
@@ -1815,6 +1822,7 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
     for (int t = 0; t < OTW; ++t)
 #pragma unroll
       for (int e = 0; e < 4; ++e) dbacc[t][e] = 0.f;
+    const unsigned lex = (unsigned)(2 * (lx * C + 16 * oh * OTW + 4 * g));  // XT: extra-term lane byte offset
     int nst = 0;
     // prologue: own rows of band i0 (a band with no predecessor: all BR+2 rows)
     if (i0 < i1) {
@@ -1871,8 +1879,26 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
       auto dma_one = [&]() {  // conv k-step hook: one DMA every ASR_V2_SPREAD k-steps
         if (ASR_V2_SPREAD > 0 && kstep++ % (ASR_V2_SPREAD > 0 ? ASR_V2_SPREAD : 1) == 0) dma_now();
       };
+      // XT: the extra term of own row k (wave-uniform row base in SGPRs + the
+      // lane's 32-bit offset + immediates).  Row 0's loads go out before the
+      // dy DMA burst, so waiting for them (in-order vmcnt) does not wait for
+      // it; row 1's before its conv (both rows' early: 10 spilled VGPRs).
+      u32x2 exv[2][XT ? PT : 1][OTW];
+      auto ex_load = [&](int k) {
+        if constexpr (XT) {
+          const int ur = __builtin_amdgcn_readfirstlane((n * H + y0 + rg + k * RS) * W);
+          const unsigned char* erow = (const unsigned char*)(extra + (long)ur * C);
+#pragma unroll
+          for (int pt = 0; pt < PT; ++pt)
+#pragma unroll
+            for (int t = 0; t < OTW; ++t)
+              exv[k][pt][t] = *(const u32x2*)(erow + lex + (unsigned)(2 * (16 * pt * C + 16 * t)));
+        }
+      };
+      if (XT && ASR_XT_EARLY && rg < rows) ex_load(0);
       if (ASR_V2_SPREAD == 0)
         while (du < dend) dma_now();  // one burst after the barrier
+      if (XT && !ASR_XT_EARLY && rg < rows) ex_load(0);
       const unsigned char* dzt = lds + L::DZ + buf * L::TILE;
       const unsigned char* dyt = lds + L::DY + buf * L::TILE;
       int nstores = 0;
@@ -1889,6 +1915,7 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
           conv_row<C, W>(dzt, r, A, boff, acc, dma_one);
           while (du < dend) dma_now();
         } else {
+          if constexpr (XT) ex_load(1);
           conv_row<C, W>(dzt, r, A, boff, acc);
         }
         ASR_STAMP(it - i0, 2 + k);
@@ -1926,6 +1953,11 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
               float res[4];  // the +dy residual (none in the second RK2 stage)
 #pragma unroll
               for (int e = 0; e < 4; ++e) res[e] = skip_dy ? 0.f : (float)dyr[e];
+              if constexpr (XT) {
+                const bf16x4 exr = *(const bf16x4*)&exv[k][pt][t];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) res[e] += (float)exr[e];
+              }
               if (g2) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(hs2g, dzf[e], fmaf(-hs, acc[t][pt][e], res[e]));
@@ -2116,21 +2148,40 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
       ASR_STAMP(it - i0, 3);
     }
     barrier_vm(0);  // all items consumed: LDS reusable
+    // XT: the old values of MC m-tiles loaded before their first store (one
+    // latency per chunk: the compiler keeps load/store pairs to the slab in order)
+    constexpr int MC = XT ? (MTW % 3 == 0 ? 3 : 1) : MTW;
 #pragma unroll
-    for (int mi = 0; mi < MTW; ++mi)
+    for (int m0 = 0; m0 < MTW; m0 += MC) {
+      float prev[XT ? MC : 1][OT][4];
+      if constexpr (XT) {
 #pragma unroll
-      for (int ot = 0; ot < OT; ++ot)
+        for (int mi = 0; mi < MC; ++mi)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int m = 16 * (tg * MTW + mi) + 4 * g + e;
-          slab[(long)m * C + 16 * ot + lx] = hs * acc[mi][ot][e];
-        }
+          for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              prev[mi][ot][e] = slab[(long)(16 * (tg * MTW + m0 + mi) + 4 * g + e) * C + 16 * ot + lx];
+      }
+#pragma unroll
+      for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+        for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int m = 16 * (tg * MTW + m0 + mi) + 4 * g + e;
+            float v = hs * acc[m0 + mi][ot][e];
+            if constexpr (XT) v += prev[mi][ot][e];
+            slab[(long)m * C + 16 * ot + lx] = v;
+          }
+    }
   }
   __syncthreads();
   if (tid < C) {
     const float* dbl = (const float*)lds + 12288;
     float s = 0.f;
     for (int q = 0; q < 4 / G::OSPLIT; ++q) s += dbl[q * C + tid];
+    if constexpr (XT) s += slab[9 * C * C + tid];
     slab[9 * C * C + tid] = s;
   }
   if (fold) {  // slabs the bands did not cover (a WG with fewer than 16 bands)
@@ -2441,13 +2492,19 @@ static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* ma
   const bool xt = extra != nullptr || skip_dy != 0 || accum != 0;
   static const bool v1 = getenv("ASR_BWD_V1") != nullptr;  // development A/B
   if constexpr (C == 64) {
-    if (!extra && !accum && (mode == blk::BWD_EULER || !skip_dy) && !v1) {  // v2: no extra dx term (RK2 stage 1 stays on v1)
+    static const bool xt_v1 = getenv("ASR_RK2_BWD_V1") != nullptr;  // development A/B: RK2 first stage on v1
+    const bool xt2 = extra && accum && !skip_dy && mode == blk::BWD_EULER && !relu_dx && !xt_v1;
+    if ((xt2 || (!extra && !accum && (mode == blk::BWD_EULER || !skip_dy))) && !v1) {  // v2: no extra dx term (RK2 stage 1 stays on v1)
       using L2 = blk::Bwd2Lds<C, W, kBwdBR>;
       const size_t lds2 = std::max((size_t)L2::TOTAL, red);
       // the folded pass gives each thread one 16-B chunk: at most 512 per WG
       const long fchunks = (long)((fold_P + 31) / 32) * ((9 * C * C + C) / 4);
       if ((fchunks + grid - 1) / grid > 512) fold_P = 0;
-      if (mode == blk::BWD_EULER && relu_dx) {
+      if (xt2) {
+        hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_EULER, false, true>), dim3(grid), dim3(512), lds2, s,
+                           (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs,
+                           fold_slabs, fold_P, fold_grp, skip_dy, (const bf16*)extra);
+      } else if (mode == blk::BWD_EULER && relu_dx) {
         hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_EULER, true>), dim3(grid), dim3(512), lds2, s,
                            (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs,
                            fold_slabs, fold_P, fold_grp, skip_dy);
