@@ -255,7 +255,7 @@ def main():
                 traffic = json.load(f).get("hbm_bytes_per_block")
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": ("RK2 block fwd+bwd (2x blk::k_fwd_pipe, 2x blk::k_bwd, k_reduce_slabs, k_project)"
+                "kernel": ("RK2 block fwd+bwd (2x blk::k_fwd_pipe, blk::k_bwd2 stage 2 + blk::k_bwd2<XT> stage 1 on one slab set, k_reduce_slabs, k_project)"
                            if integrator == "rk2" else
                            "Euler block fwd+bwd (blk::k_fwd_pipe, blk::k_bwd2 fused dgrad+wgrad, k_reduce_slabs, "
                            "k_project)"),
