@@ -251,6 +251,9 @@ __global__ __launch_bounds__(256) void k_head(const T* __restrict__ xL, const fl
   for (int v = 0; v < VEC; ++v) s[v] = 0.f;
   if (pl < PL && tid < PL * NQ) {
     const T* base = xL + (long)n * HW * C + q * VEC;
+    // 8 independent loads in flight per thread: at 2 blocks per CU the read
+    // is latency-bound otherwise
+#pragma unroll 8
     for (int p = pl; p < HW; p += PL) {
       if constexpr (VEC == 8 && sizeof(T) == 2) {
         const bf16x8 v8 = *(const bf16x8*)(base + (long)p * C);
