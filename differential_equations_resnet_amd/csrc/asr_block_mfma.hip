@@ -803,7 +803,12 @@ __device__ __forceinline__ void epi_all_units(F& f, const Acc& acc, const Xr& xr
 // Forward, band form with a software pipeline across bands: the MFMAs of
 // band i+1 are interleaved with the epilogue (VALU + stores) of band i, so
 // the matrix pipe and the vector ALU of one wave work at the same time.
-template <int C, int W, int BR, int MODE, int NW, bool RES>
+// RESG (second RK2 stage, default): the residual `resid` read from global
+// memory.  Band i+1's loads are issued right after band i+2's DMA and
+// consumed (an empty asm that reads them) right after the next barrier, before
+// any later DMA: hipcc's own vmcnt wait for a load counts only the memory ops
+// it sees, so a use behind a younger inline-asm DMA would wait for that DMA.
+template <int C, int W, int BR, int MODE, int NW, bool RES, bool RESG = false>
 __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict__ x, const bf16* __restrict__ resid,
                                                   bf16* __restrict__ y, uint8_t* __restrict__ mask,
                                                   const bf16* __restrict__ wpack, const float* __restrict__ bias,
@@ -876,7 +881,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
   int nst = 0;  // vector-memory ops this wave issued after the DMA the next barrier waits for
   // residual of a band: x from its LDS tile (read after the band's conv)
   auto xres_read = [&](int buf, u32x2 (&xr)[RB][PT]) {
-    if constexpr (EULER && !RES) {
+    if constexpr (EULER && !RES && !RESG) {
       const unsigned tb = lds_u32(lds + buf * TILE) + lxr;
 #pragma unroll
       for (int r = 0; r < RB; ++r)
@@ -913,6 +918,30 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
 #pragma unroll
         for (int pt = 0; pt < PT; ++pt) xr[r][pt] = lds_rd64(b + (unsigned)(r * 1024 + pt * 512));
       lgkm_wait<0>();
+    }
+  };
+  // RESG: every lane issues exactly RB*PT loads (rows past the image end
+  // re-read its last row), so the barrier counts stay exact
+  const unsigned lres = (unsigned)(2 * (lx * C + o0));
+  auto xg_load = [&](const ItemCursor& c, u32x2 (&xr)[RB][PT]) {
+    if constexpr (RESG) {
+      const int y0 = c.b * BR, rows = min(BR, H - y0);
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int ur = __builtin_amdgcn_readfirstlane((c.n * H + y0 + min(r0 + r, rows - 1)) * W);
+        const unsigned char* rb = (const unsigned char*)(resid + (long)ur * C);
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt) xr[r][pt] = *(const u32x2*)(rb + lres + (unsigned)(2 * 16 * pt * C));
+      }
+      nst += RB * PT;
+    }
+  };
+  auto xg_consume = [&](u32x2 (&xr)[RB][PT]) {
+    if constexpr (RESG) {
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt) asm volatile("" : "+v"(xr[r][pt]));
     }
   };
   auto init = [&](f32x4 (&acc)[RB][PT]) {
@@ -991,6 +1020,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
   dma_res(cur, 0);
   barrier_vm(0);
   if (i0 + 1 < i1) dma(nx1, 1);
+  xg_load(cur, xrA);
   init(accA);
   conv_band<C, W, RB>(lds_u32(lds + r0 * BD::ROWB), lo, A, accA);
   xres_read(0, xrA);
@@ -1009,8 +1039,10 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
     barrier_vm(nst);  // band it+1 landed, every wave is done with band it's tile
     ASR_STAMP(it - i0, 1);
     nst = 0;
+    xg_consume(xrA);
     dma_res(nx1, (it + 1 - i0) & 1);
     if (it + 2 < i1) dma_next2(nx2, nx1, (it - i0) & 1);
+    xg_load(nx1, xrB);
     ASR_STAMP(it - i0, 2);
     res_read((it - i0) & 1, xrA);
     init(accB);
@@ -1039,8 +1071,10 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
     barrier_vm(nst);
     ASR_STAMP(it - i0, 1);
     nst = 0;
+    xg_consume(xrB);
     dma_res(nx1, (it + 1 - i0) & 1);
     if (it + 2 < i1) dma_next2(nx2, nx1, (it - i0) & 1);
+    xg_load(nx1, xrA);
     ASR_STAMP(it - i0, 2);
     res_read((it - i0) & 1, xrB);
     init(accA);
@@ -2445,8 +2479,15 @@ static int launch_fwd_v(int mode, const void* x, const void* resid, void* y, uin
         hipLaunchKernelGGL((blk::k_fwd_band<C, W, BR, blk::FWD_CONV, NW>), dim3(grid), dim3(64 * NW), lds, s,
                            (const bf16*)x, (const bf16*)resid, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
     } else {
-      if (mode == blk::FWD_EULER && resid)
+      static const bool res_v1 = getenv("ASR_FWD_RES_V1") != nullptr;  // development A/B: private-LDS residual
+      if (mode == blk::FWD_EULER && resid && res_v1)
         return launch_fwd_res<C, W>(x, resid, y, mask, w, bias, h, N, H, s);
+      if (mode == blk::FWD_EULER && resid) {
+        hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_EULER, NW, false, true>), dim3(grid), dim3(64 * NW),
+                           lds, s, (const bf16*)x, (const bf16*)resid, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+        ASR_LAUNCH_CHECK("k_fwd_pipe(resg)");
+        return ASR_OK;
+      }
       if (mode == blk::FWD_EULER)
         hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_EULER, NW, false>), dim3(grid), dim3(64 * NW), lds, s,
                            (const bf16*)x, nullptr, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
