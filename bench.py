@@ -7,14 +7,22 @@ get_single_block_resnet_build_function(kernel_type='antisymmetric',
 num_stages=2, blocks_per_stage=[30], filters_per_block=[64], strides=[(1,1)],
 subtract_mean=127.5, divide_by_stddev=127.5, num_classes=10), h = 8/30,
 batch 512 per GPU, bf16 activations with fp32 accumulation and fp32
-parameters/Adam.  Synthetic uniform uint8 images and random one-hot labels
-(no dataset on the box), random-init weights of that architecture.
+parameters/Adam.  Synthetic data (no dataset on the box): 8 batches of
+uniform uint8 images with random labels, resident in HBM and cycled.
+Weights: the reference initialisation (he_normal, truncated-normal thetas,
+zero biases) with the block thetas scaled by 0.5 and the fc kernel by 0.1, so
+that the timed steps are NOT in the saturated-softmax regime (at the plain
+reference init this 30-block net starts at loss 13 with |logits| ~ 50 and
+the Keras clip zeroes the gradient of most images; the line reports the
+loss and the fraction of images with a live gradient, and fails below 0.9).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
 
-N > 1 is launched by torch.distributed.run, one process per GPU; the batch is
-sharded by rank (512 per GPU, weak scaling) and the fp32 gradient buffer is
-all-reduced with RCCL (backend "nccl") before the replicated Adam update.
+--gpus N > 1 without WORLD_SIZE in the environment re-launches this script
+under torch.distributed.run (N processes, one per GPU) before touching the
+GPU; with WORLD_SIZE set (the driver's own torchrun launch) each rank takes
+512 images per step (weak scaling), the fp32 gradient buffer is all-reduced
+through asr_dist_allreduce_sum (RCCL over xGMI) and Adam runs replicated.
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -22,6 +30,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -34,6 +44,8 @@ METRIC = "CIFAR-10 images/sec (fwd+bwd) antisym-ResNet-32 @ batch 512; 1/2/4/8 G
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (spec)
 F32_PEAK_TFLOPS = 157.3
+THETA_SCALE, FC_SCALE = 0.5, 0.1  # bench init (see the module docstring)
+N_BATCHES = 8
 
 CONFIGS = {
     # name: (C, L, per-GPU batch, dtype, description, integrator)
@@ -55,20 +67,50 @@ def parse():
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--block-reps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=16)
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this process may run on")
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """Re-run this script as N ranks under torch.distributed.run; the parent
+    never touches the GPU and only relays the children's exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def bench_params(C, L):
+    from differential_equations_resnet_amd.netparams import init_net_params, net_param_shapes
+    flat = init_net_params(C, L, 3, 10, seed=0)
+    sizes = [int(np.prod(s)) for s in net_param_shapes(C, L, 3, 10)]
+    nt = 4 + C - 1  # theta arrays per block
+    off = sizes[0] + sizes[1]
+    for _ in range(L):
+        n = sum(sizes[2:2 + nt])
+        flat[off:off + n] *= THETA_SCALE
+        off += n + C
+    flat[off:off + C * 10] *= FC_SCALE
+    return flat
+
+
 def block_roofline(rt, lib, C, N, dtype_name, reps, h, integrator="euler"):
-    """Time one block (fwd + full bwd) at the workload shape with HIP events
-    on the launch stream; return per-launch averages.
+    """Time one block's kernels at the workload shape on random operands with
+    HIP events on the launch stream (torch's current stream, which every
+    libasr call here launches on); per-launch averages.
 
     Algorithmic bytes (SURVEY §8d): Euler block 5·P·s (fwd: read x, write y;
-    bwd: read dy, read x, write dx).  RK2 block 12·P·s, the minimum of its
-    two-stage composition with the midpoint stored: fwd read x, write xm,
-    read xm, read x, write y; bwd stage 2 read dy, read xm, write g; stage 1
-    read g, read x, read dy, write dx."""
+    bwd: read dy, read x, write dx), forward 2·P·s, backward 3·P·s.  RK2 block
+    12·P·s, the minimum of its two-stage composition with the midpoint stored:
+    fwd read x, write xm, read xm, read x, write y; bwd stage 2 read dy, read
+    xm, write g; stage 1 read g, read x, read dy, write dx."""
     import torch
     from differential_equations_resnet_amd import _lib
     dev = torch.device("cuda")
@@ -96,6 +138,11 @@ def block_roofline(rt, lib, C, N, dtype_name, reps, h, integrator="euler"):
         _lib.check(lib.asr_conv_forward(0, x.data_ptr(), y.data_ptr(), mask.data_ptr(), w.data_ptr(),
                                         bias.data_ptr(), h, N, H, W, C, dt, s), "fwd")
 
+    def bwd_kernel():  # dx only: the fused dgrad + wgrad kernel alone (no slab reduction / projection)
+        _lib.check(lib.asr_conv_backward(0, dy.data_ptr(), x.data_ptr(), mask.data_ptr(), w.data_ptr(),
+                                         theta_dst.data_ptr(), pm.n_theta, h, 0.0, N, H, W, C, dt, dx.data_ptr(),
+                                         None, None, None, ws.data_ptr(), ws_bytes, s), "bwd")
+
     def bwd():
         _lib.check(lib.asr_conv_backward(0, dy.data_ptr(), x.data_ptr(), mask.data_ptr(), w.data_ptr(),
                                          theta_dst.data_ptr(), pm.n_theta, h, 0.0, N, H, W, C, dt, dx.data_ptr(),
@@ -117,11 +164,13 @@ def block_roofline(rt, lib, C, N, dtype_name, reps, h, integrator="euler"):
                                             mask2.data_ptr(), w.data_ptr(), theta_dst.data_ptr(), pm.n_theta, h, 0.0,
                                             N, H, W, C, dt, dx.data_ptr(), dth.data_ptr(), db.data_ptr(), None,
                                             ws.data_ptr(), ws_bytes, s), "rk2 bwd")
+        bwd_kernel = None
 
     for _ in range(10):
         fwd()
         bwd()
     torch.cuda.synchronize()
+
     def timed(fn):
         # one event pair around `reps` back-to-back launches: the per-launch
         # average then matches rocprofv3's kernel durations (events between
@@ -135,6 +184,7 @@ def block_roofline(rt, lib, C, N, dtype_name, reps, h, integrator="euler"):
         return e0.elapsed_time(e1) / reps * 1e-3
 
     tf = timed(fwd)
+    tbk = timed(bwd_kernel) if bwd_kernel is not None else None
     tb = timed(bwd)
     t_blk = timed(lambda: (fwd(), bwd()))
     esz = 2 if dt == rt.ASR_BF16 else 4
@@ -142,28 +192,21 @@ def block_roofline(rt, lib, C, N, dtype_name, reps, h, integrator="euler"):
     stages = 2 if integrator == "rk2" else 1
     bytes_alg = (12 if stages == 2 else 5) * P * esz  # see the docstring
     flops = stages * 3 * 2 * 9 * C * C * N * H * W
-    return dict(t_fwd=tf, t_bwd=tb, t=t_blk, bytes=bytes_alg, flops=flops)
+    return dict(t_fwd=tf, t_bwd_kernel=tbk, t_bwd=tb, t=t_blk, bytes=bytes_alg, flops=flops,
+                bytes_fwd=2 * P * esz, bytes_bwd=3 * P * esz)
 
 
-def cpu_baseline(C, L, h, batch, steps):
-    """The oracle's op-by-op PyTorch-CPU restatement of the reference TF graph
-    (oracle/torch_cpu_ref.py), timed on this box's host cores."""
+def cpu_baseline(threads):
+    """The oracle's PyTorch-CPU restatements of the reference TF graph
+    (oracle/torch_cpu_ref.py), timed on this box's host cores: the metric's
+    workload (C2: C=64, 30 blocks, batch 512) with the reference's op-by-op
+    kernel assembly (the headline value) and with the vectorised assembly, and
+    BASELINE config C1 (C=16, 18 blocks, batch 128).  One untimed step (oneDNN
+    primitive creation), then whole training steps (fwd + bwd + Adam)."""
     import torch
     from oracle import asr_oracle as O
     from oracle.torch_cpu_ref import RefNet
-    cores = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(cores)
-    spec = O.NetSpec(C=C, L=L, h=h)
-    rng = np.random.default_rng(0)
-    params = O.init_params(spec, rng, np.float32)
-    net = RefNet(params, C, L, h)
-    imgs = rng.integers(0, 256, (batch, 32, 32, 3)).astype(np.uint8)
-    onehot = np.eye(10, dtype=np.float32)[rng.integers(0, 10, batch)]
-    net.train_step(imgs, onehot)  # warm-up (allocations, oneDNN primitive creation)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        net.train_step(imgs, onehot)
-    dt = time.perf_counter() - t0
+    torch.set_num_threads(threads)
     cpu = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -173,18 +216,69 @@ def cpu_baseline(C, L, h, batch, steps):
                     break
     except OSError:
         pass
-    return {"value": round(batch * steps / dt, 3), "unit": "images/s", "cores": cores, "kind": "port",
-            "sample": f"{steps} training steps (fwd+bwd+Adam) of the same model (C={C}, {L} blocks) at batch {batch}, "
-                      f"fp32, torch-CPU op-by-op restatement of the reference TF graph (per-step slice/neg/concat "
-                      f"kernel assembly); {dt:.1f} s on {cores} threads of {cpu}"}
+
+    def run(C, L, batch, steps, assembly):
+        spec = O.NetSpec(C=C, L=L, h=8.0 / L)
+        rng = np.random.default_rng(0)
+        net = RefNet(O.init_params(spec, rng, np.float32), C, L, 8.0 / L, assembly=assembly)
+        imgs = rng.integers(0, 256, (batch, 32, 32, 3)).astype(np.uint8)
+        onehot = np.eye(10, dtype=np.float32)[rng.integers(0, 10, batch)]
+        net.train_step(imgs, onehot)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            net.train_step(imgs, onehot)
+        dt = time.perf_counter() - t0
+        print(f"bench: cpu baseline C={C} L={L} batch {batch} ({assembly}): {batch * steps / dt:.2f} images/s",
+              file=sys.stderr, flush=True)
+        return round(batch * steps / dt, 3), dt
+
+    c2, t2 = run(64, 30, 512, 1, "reference")
+    c2v, t2v = run(64, 30, 512, 1, "vectorised")
+    c1, t1 = run(16, 18, 128, 2, "reference")
+    return {"value": c2, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"1 training step (fwd+bwd+Adam) of the metric's model (C=64, 30 blocks, batch 512, fp32) in "
+                      f"the torch-CPU op-by-op restatement of the reference TF graph (per-step slice/neg/concat "
+                      f"kernel assembly), after 1 untimed step; {t2:.1f} s on {threads} threads of {cpu}",
+            "vectorised_assembly": {"value": c2v, "unit": "images/s", "seconds": round(t2v, 2),
+                                    "sample": "same, W = P - P* + gamma*I as one gather per block"},
+            "c1": {"value": c1, "unit": "images/s", "seconds": round(t1, 2),
+                   "sample": "BASELINE C1: C=16, 18 blocks, batch 128, fp32, op-by-op assembly, 2 steps"}}
+
+
+def host_threads() -> int:
+    """CPUs this process may use: its affinity set, capped by a cgroup CPU
+    quota when one is set (the GPU box shows the whole machine's CPUs)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(-(-int(quota) // int(period)))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def traffic_record(config):
+    """HBM traffic per block from the committed rocprofv3 PMC summary
+    (profiles/traffic_<config>.json, written by tools/traffic.py from
+    separate FETCH_SIZE / WRITE_SIZE passes with the gfx950 x2 read
+    correction) — labelled with its round tag; null if none."""
+    path = os.path.join(HERE, "profiles", f"traffic_{config}.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_block"), f"profiles/traffic_{config}.json ({d.get('round', '?')})"
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+
     import torch
-    import torch.distributed as dist
-    from differential_equations_resnet_amd import _lib, runtime as rt
-    from differential_equations_resnet_amd.netparams import init_net_params
+    from differential_equations_resnet_amd import _lib, distributed, runtime as rt
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -192,93 +286,108 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     torch.cuda.set_device(local)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
     dev = rt.require_gpu()
+    distributed.init_from_env(device=dev)  # RCCL communicator through asr_dist_init (world > 1)
     lib = _lib.load()
 
     C, L, N, dtype_name, desc, integrator = CONFIGS[args.config]
     h = 8.0 / L  # final_time 8 (experiments_antisymmetric_resnet_v6.ipynb cell 1)
     ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, h, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
                         dtype=dtype_name, input_u8=True, device=dev, integrator=integrator)
-    params = torch.from_numpy(init_net_params(C, L, 3, 10, seed=0)).to(dev)
-    if world > 1:
-        dist.broadcast(params, 0)
+    params = torch.from_numpy(bench_params(C, L)).to(dev)
+    distributed.broadcast_params(params, 0)
     m = torch.zeros_like(params)
     v = torch.zeros_like(params)
     rng = np.random.default_rng(1234 + rank)
-    images = torch.from_numpy(rng.integers(0, 256, (N, 32, 32, 3), dtype=np.uint8)).to(dev)
-    targets = torch.from_numpy(np.eye(10, dtype=np.float32)[rng.integers(0, 10, N)]).to(dev)
+    batches = []
+    for _ in range(N_BATCHES):
+        labels = rng.integers(0, 10, N)
+        batches.append((torch.from_numpy(rng.integers(0, 256, (N, 32, 32, 3), dtype=np.uint8)).to(dev),
+                        torch.from_numpy(np.eye(10, dtype=np.float32)[labels]).to(dev), torch.from_numpy(labels)))
     step_no = [0]
 
     def step():
-        loss, grads = ex.forward_backward(params, images, targets)
-        if world > 1:
-            dist.all_reduce(grads)
+        images, targets, _ = batches[step_no[0] % N_BATCHES]
+        loss, grads = ex.forward_backward(params, images, targets, want_probs=True)
+        distributed.allreduce_grads(grads)
         step_no[0] += 1
         rt.adam_update(params, grads, m, v, args.lr, 0.9, 0.999, 1e-7, step_no[0], 1.0 / world)
         return loss
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    def live_fraction():
+        """Images of the last step whose target probability lies inside the
+        Keras clip range (their loss gradient is not clipped to zero)."""
+        labels = batches[(step_no[0] - 1) % N_BATCHES][2].numpy()
+        p = ex.probs.cpu().numpy()[np.arange(N), labels]
+        return float(((p > 1e-7) & (p < 1 - 1e-7)).mean())
+
+    for i in range(args.warmup):
+        loss = step()
+        if i == 0:
+            initial_loss = float(loss.item())
+    if args.warmup == 0:
+        initial_loss = None
+    distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    distributed.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = distributed.max_over_ranks(elapsed)
     final_loss = float(loss.item())
+    live = distributed.max_over_ranks(-live_fraction())  # min over ranks
+    live = -live
     value = N * world * args.steps / elapsed
 
-    roof = None
-    cpu = None
     if rank == 0:
         rb = block_roofline(rt, lib, C, N, dtype_name, args.block_reps, h, integrator)
         achieved = rb["bytes"] / rb["t"] / 1e9
         tflops = rb["flops"] / rb["t"] / 1e12
         peak_tf = BF16_PEAK_TFLOPS if dtype_name == "bfloat16" else F32_PEAK_TFLOPS
-        traffic = None
-        tpath = os.path.join(HERE, "profiles", f"traffic_{args.config}.json")
-        if os.path.exists(tpath):
-            with open(tpath) as f:
-                traffic = json.load(f).get("hbm_bytes_per_block")
+        traffic, traffic_src = traffic_record(args.config)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": ("RK2 block fwd+bwd (2x blk::k_fwd_pipe, blk::k_bwd2 stage 2 + blk::k_bwd2<XT> stage 1 on one slab set, k_reduce_slabs, k_project)"
-                           if integrator == "rk2" else
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                "kernel": ("RK2 block fwd+bwd (2x blk::k_fwd_pipe, blk::k_bwd2 stage 2 + blk::k_bwd2<XT> stage 1 on "
+                           "one slab set, k_reduce_slabs, k_project)" if integrator == "rk2" else
                            "Euler block fwd+bwd (blk::k_fwd_pipe, blk::k_bwd2 fused dgrad+wgrad, k_reduce_slabs, "
                            "k_project)"),
+                "operands": "random (x, dy ~ N(0,1) in bf16, theta ~ N(0, 0.05^2))",
                 "algorithmic_bytes": rb["bytes"], "avg_us": round(rb["t"] * 1e6, 2),
-                "avg_us_fwd": round(rb["t_fwd"] * 1e6, 2), "avg_us_bwd": round(rb["t_bwd"] * 1e6, 2),
-                "mfma_tflops": round(tflops, 1), "mfma_frac": round(tflops / peak_tf, 4)}
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(C, L, h, args.cpu_batch, args.cpu_steps) if integrator == "euler" else None
+                "mfma_tflops": round(tflops, 1), "mfma_frac": round(tflops / peak_tf, 4),
+                "kernels": {"fwd": {"avg_us": round(rb["t_fwd"] * 1e6, 2), "algorithmic_bytes": rb["bytes_fwd"],
+                                    "frac": round(rb["bytes_fwd"] / rb["t_fwd"] / 1e9 / HBM_PEAK_GBS, 4)},
+                            "bwd_with_reduction": {"avg_us": round(rb["t_bwd"] * 1e6, 2)}}}
+        if rb["t_bwd_kernel"] is not None:
+            roof["kernels"]["bwd"] = {"avg_us": round(rb["t_bwd_kernel"] * 1e6, 2),
+                                      "algorithmic_bytes": rb["bytes_bwd"],
+                                      "frac": round(rb["bytes_bwd"] / rb["t_bwd_kernel"] / 1e9 / HBM_PEAK_GBS, 4)}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline and integrator == "euler" and args.config == "c2":
+            threads = args.cpu_threads or host_threads()
+            cpu = cpu_baseline(threads)
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16" if dtype_name == "bfloat16" else "f32",
-            "data": "synthetic (uniform uint8 32x32x3 images, random one-hot labels; random-init weights)",
+            "data": f"synthetic ({N_BATCHES} HBM-resident batches of uniform uint8 32x32x3 images with random one-hot "
+                    f"labels, cycled; reference init with block thetas x{THETA_SCALE} and fc kernel x{FC_SCALE})",
             "config": {"workload": desc + "; train step = fwd + bwd + Adam", "global_batch": N * world,
                        "per_gpu_batch": N, "channels": C, "blocks": L, "integrator": integrator, "h": round(h, 6),
-                       "parallelism": f"dp{world}", "final_loss": round(final_loss, 4)},
+                       "parallelism": f"dp{world}",
+                       "collective": "asr_dist_allreduce_sum (RCCL)" if world > 1 else None,
+                       "initial_loss": None if initial_loss is None else round(initial_loss, 4),
+                       "final_loss": round(final_loss, 4), "live_gradient_fraction": round(live, 4)},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    distributed.shutdown()
+    if live < 0.9:
+        print(f"bench: only {live:.3f} of the images have a live loss gradient (saturated softmax)", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

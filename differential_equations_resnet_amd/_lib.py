@@ -29,11 +29,15 @@ ASR_BF16 = 1
 ASR_PARAM_3BY3 = 0
 ASR_PARAM_GENERAL = 1
 ASR_PARAM_REGULAR = 2
-ABI_VERSION = 3
+ABI_VERSION = 4
 ASR_MODE_EULER = 0
 ASR_MODE_CONV = 1
 ASR_INTEGRATOR_EULER = 0
 ASR_INTEGRATOR_RK2 = 1
+ASR_VARIANT_NO_FOLD = 1
+ASR_VARIANT_STEM_FWD_VALU = 2
+ASR_VARIANT_STEM_WGRAD_VALU = 4
+ASR_DIST_UNIQUE_ID_BYTES = 128
 
 
 class AsrError(RuntimeError):
@@ -49,7 +53,7 @@ class NetConfig(ct.Structure):
         ("N", ct.c_int), ("H", ct.c_int), ("W", ct.c_int), ("Cin", ct.c_int), ("C", ct.c_int), ("L", ct.c_int),
         ("num_classes", ct.c_int), ("h", ct.c_float), ("gamma", ct.c_float), ("subtract_mean", ct.c_float),
         ("divide_by_stddev", ct.c_float), ("use_norm", ct.c_int), ("dtype", ct.c_int), ("input_u8", ct.c_int),
-        ("param_kind", ct.c_int), ("antisymmetric", ct.c_int), ("integrator", ct.c_int),
+        ("param_kind", ct.c_int), ("antisymmetric", ct.c_int), ("integrator", ct.c_int), ("variant", ct.c_int),
     ]
 
 
@@ -86,6 +90,12 @@ SIGNATURES = [
     ("asr_adam_update", _I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _L, _F, _P]),
     ("asr_segment_sq_norms", _I, [_P, _P, _I, _P, _P]),
     ("asr_batch_metrics", _I, [_P, _P, _P, _I, _I, _P, _P]),
+    ("asr_dist_unique_id", _I, [_P]),
+    ("asr_dist_init", _I, [_I, _I, _P]),
+    ("asr_dist_allreduce_sum", _I, [_P, _S, _I, _P]),
+    ("asr_dist_broadcast", _I, [_P, _S, _I, _I, _P]),
+    ("asr_dist_world_size", _I, []),
+    ("asr_dist_finalize", _I, []),
 ]
 
 _lib = None
@@ -95,17 +105,24 @@ def lib_path() -> str:
     return _build.LIB
 
 
-def load(build_if_missing: bool = True):
-    """Load (building first if needed) libasr.so and bind its C ABI."""
+def load(build_if_missing: bool = True, path: str | None = None):
+    """Load (building first if needed) libasr.so and bind its C ABI.
+
+    `path` (development tools only: A/B timing of variant builds) loads
+    another build of the same sources; it must be given before the first
+    load of the process."""
     global _lib
     if _lib is not None:
+        if path is not None and getattr(_lib, "_asr_path", None) != path:
+            raise AsrError(f"libasr already loaded from {_lib._asr_path}")
         return _lib
-    path = os.environ.get("ASR_LIB_OVERRIDE", _build.LIB)  # development: ablation builds
+    path = path or _build.LIB
     if not os.path.exists(path):
         if not build_if_missing:
             raise AsrError(f"libasr.so not found at {path}; run differential_equations_resnet_amd._build.build()")
         _build.build()
     lib = ct.CDLL(path, mode=ct.RTLD_GLOBAL)
+    lib._asr_path = path
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)
         fn.restype = res

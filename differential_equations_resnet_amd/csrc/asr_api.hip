@@ -64,7 +64,7 @@ int head(const void* xL, int act_bf16, const float* fck, const float* fcb, const
 int head_param_grads(const float* gap, const float* dlogits, int N, int C, int K, float* dfck, float* dfcb,
                      const float* loss_per, float* loss_out, hipStream_t s);
 
-constexpr int kMaxSlabsApi = 512;  // matches asr_conv_mfma.hip kMaxSlabs
+constexpr int kMaxSlabsApi = 512;  // matches asr_block_mfma.hip kMaxBlockSlabs
 enum { F_EULER = 0, F_CONV = 1, F_RELU = 2, B_EULER = 3, B_CONV = 4 };
 
 static int check_shape(int N, int H, int W, int C) {
@@ -181,13 +181,14 @@ static int rk2_backward_slabs(const void* dy, const void* x, const void* xmid, c
                               hipStream_t s, const float* fold_slabs = nullptr, int fold_P = 0,
                               float* fold_grp = nullptr, int* fold_done = nullptr) {
   int n2 = 0, n1 = 0;
-  const bool one_set = dtype == ASR_BF16 && getenv("ASR_RK2_TWO_SETS") == nullptr;  // (A/B: two slab sets)
+  // bf16: both stages run on the same persistent grid (block_bwd_grid of the
+  // same shape), so the first stage can add onto the second's slabs
+  const bool one_set = dtype == ASR_BF16;
   ASR_TRY(block_backward(ASR_MODE_EULER, dy, xmid, mask2, w, h, gamma, N, H, W, C, dtype, g, need_w, nullptr, true,
                          slabs, dz_scratch, &n2, s, false, nullptr, fold_slabs, fold_P, fold_grp, fold_done));
   ASR_TRY(block_backward(ASR_MODE_EULER, g, x, mask1, w, 0.5f * h, gamma, N, H, W, C, dtype, dx, need_w, dy, false,
                          one_set ? slabs : slabs + (long)n2 * (9L * C * C + C), dz_scratch, &n1, s, false, nullptr,
                          nullptr, 0, nullptr, nullptr, one_set));
-  if (one_set && n1 != n2) return fail(ASR_E_UNSUPPORTED, "rk2 backward: stage grids differ (%d vs %d)", n1, n2);
   *nsl = one_set ? n2 : n1 + n2;
   return ASR_OK;
 }
@@ -311,6 +312,8 @@ static int net_check(const asr_net_config* c) {
     return fail(ASR_E_ARG, "the 3by3 parametrisation is always antisymmetric");
   if (c->integrator != ASR_INTEGRATOR_EULER && c->integrator != ASR_INTEGRATOR_RK2)
     return fail(ASR_E_ARG, "bad integrator %d", c->integrator);
+  if (c->variant & ~(ASR_VARIANT_NO_FOLD | ASR_VARIANT_STEM_FWD_VALU | ASR_VARIANT_STEM_WGRAD_VALU))
+    return fail(ASR_E_ARG, "bad variant bits 0x%x", c->variant);
   if (c->dtype == ASR_BF16 && !mfma_supported(c->C, c->W))
     return fail(ASR_E_UNSUPPORTED, "bf16 network needs C in {16,32,64} and W == 32 (C=%d W=%d)", c->C, c->W);
   return ASR_OK;
@@ -390,7 +393,7 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
     return acts + (size_t)slot * L.P * L.act_bytes;
   };
   // 2. normalisation + conv1 + relu (tfkeras_resnets.py:555-572)
-  if (L.fast_stem && bf && stem_fwd_mfma_supported(c->Cin, H, W, C) && getenv("ASR_STEM_FWD_V1") == nullptr) {
+  if (L.fast_stem && bf && stem_fwd_mfma_supported(c->Cin, H, W, C) && !(c->variant & ASR_VARIANT_STEM_FWD_VALU)) {
     ASR_TRY(stem_fwd_mfma(images, c->input_u8, params + L.off_c1k, params + L.off_c1b, N, H, W, c->Cin, C,
                           c->subtract_mean, inv_std, c->use_norm, act(0), s));
   } else if (L.fast_stem) {
@@ -595,8 +598,8 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   const float* pend_slabs = nullptr;  // the slabs whose pass-1 reduction is still pending
   int pend_P = 0;
   float* pend_grp = nullptr;
-  const bool fold_on = getenv("ASR_NO_FOLD") == nullptr;  // A/B: the reduction as separate launches
-  const bool stem_v1 = getenv("ASR_STEM_V1") != nullptr;  // A/B and parity tests: the fp32 VALU stem wgrad
+  const bool fold_on = !(cfg->variant & ASR_VARIANT_NO_FOLD);               // else the reduction as separate launches
+  const bool stem_v1 = (cfg->variant & ASR_VARIANT_STEM_WGRAD_VALU) != 0;  // fp32 VALU stem wgrad
   for (int l = cfg->L - 1; l >= 0; --l) {
     const unsigned char* wl = b + (L.sep_bwd ? L.wbuf_bwd : L.wbuf) + (size_t)l * L.wstride * L.act_bytes;
     const uint8_t* mask = (const uint8_t*)(b + L.masks) + (size_t)l * L.mask_bytes;

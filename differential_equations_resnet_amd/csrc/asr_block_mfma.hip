@@ -672,126 +672,6 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(const bf16* __restrict__ x, con
   }
 }
 
-// Forward, band form (C >= 32): wave = (o-tile ot, row group rg); RB rows.
-template <int C, int W, int BR, int MODE, int NW>
-__global__ __launch_bounds__(64 * NW) void k_fwd_band(const bf16* __restrict__ x, const bf16* __restrict__ resid,
-                                                  bf16* __restrict__ y, uint8_t* __restrict__ mask,
-                                                  const bf16* __restrict__ wpack, const float* __restrict__ bias,
-                                                  float h, int N, int H) {
-  using G = Geo<C>;
-  constexpr int TW = W + 2, PT = W / 16, NQ = G::NQ, OT = C / 16;
-  constexpr int TILE = (BR + 2) * TW * NQ * 16;
-  static_assert(NW % OT == 0, "waves must cover the o-tiles");
-  constexpr int RS = NW / OT, RB = BR / RS;  // row groups, rows per wave
-  static_assert(BR % RS == 0, "row groups must split the band");
-  using BD = Band<C, W, RB>;
-  constexpr bool EULER = MODE == FWD_EULER;
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ot = wave % OT, rg = wave / OT;
-  const int g = lane >> 4, lx = lane & 15;
-  const int o0 = 16 * ot + 4 * g;  // this lane's 4 output channels
-
-  bf16x8 A[G::KS];
-  load_A1<C>(wpack, ot, lane, A);
-  unsigned lo[3 * BD::NCB];
-  band_lane_offsets<C, W, RB>(g, lx, lo);
-  float bz[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) bz[e] = bias ? bias[o0 + e] : 0.f;
-
-  zero_halo_cols<C, W>(lds, BR + 2, tid, 64 * NW);
-  zero_halo_cols<C, W>(lds + TILE, BR + 2, tid, 64 * NW);
-  const int nb = (H + BR - 1) / BR;
-  int i0, i1;
-  item_range(N * nb, &i0, &i1);
-  ItemCursor cur(i0, nb), nxt(i0, nb);
-  if (i0 < i1) {
-    const int y0 = cur.b * BR;
-    dma_rows<C, W>(x, lds, cur.n, y0 - 1, min(BR, H - y0) + 2, H, wave, NW, lane);
-  }
-  nxt.next(nb);
-  int nst = 0;  // global stores this wave issued after the DMA it must now wait for
-  for (int it = i0; it < i1; ++it, cur.next(nb), nxt.next(nb)) {
-    const int buf = (it - i0) & 1;
-    unsigned char* tile = lds + buf * TILE;
-    barrier_vm(nst);  // this item's DMA has landed; the other buffer is free
-    nst = 0;
-    if (ASR_ABLATE != 3 && it + 1 < i1) {
-      const int y1 = nxt.b * BR;
-      dma_rows<C, W>(x, lds + (buf ^ 1) * TILE, nxt.n, y1 - 1, min(BR, H - y1) + 2, H, wave, NW, lane);
-    }
-    const int n = cur.n, y0 = cur.b * BR;
-    const int rows = min(BR, H - y0);
-    const int r0 = rg * RB;
-    if (r0 >= rows) continue;
-    f32x4 acc[RB][PT];
-#pragma unroll
-    for (int r = 0; r < RB; ++r)
-#pragma unroll
-      for (int pt = 0; pt < PT; ++pt) acc[r][pt] = f32x4{bz[0], bz[1], bz[2], bz[3]};
-    if (ASR_ABLATE != 2) conv_band<C, W, RB>(lds_u32(tile + r0 * BD::ROWB), lo, A, acc);
-    if (ASR_ABLATE == 1) {
-#pragma unroll
-      for (int r = 0; r < RB; ++r)
-#pragma unroll
-        for (int pt = 0; pt < PT; ++pt) asm volatile("" ::"v"(acc[r][pt]));
-      continue;
-    }
-    // residual x of the lane's outputs (LDS, asm: the next band's DMA is in flight)
-    u32x2 xr2[RB][PT];
-    if constexpr (EULER) {
-#pragma unroll
-      for (int r = 0; r < RB; ++r)
-#pragma unroll
-        for (int pt = 0; pt < PT; ++pt)
-          xr2[r][pt] = resid ? *(const u32x2*)(resid + (((long)n * H + y0 + min(r0 + r, rows - 1)) * W + 16 * pt + lx) * C + o0)
-                             : lds_rd64(lds_u32(tile + toff<C>(r0 + r + 1, 16 * pt + lx + 1, o0 >> 3, TW) + (o0 & 4) * 2));
-      lgkm_wait<0>();
-    }
-    // wave-uniform row bases + one 32-bit lane offset: stores need no 64-bit math
-    const long row0 = ((long)n * H + y0 + r0) * W;
-    bf16* yb = y + row0 * C;
-    uint8_t* mkb = mask ? mask + row0 * (C / 8) : nullptr;
-    const unsigned ly = (unsigned)(lx * C + o0);
-    const unsigned lm = (unsigned)(lx * (C / 8) + 2 * ot);
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      if (r0 + r >= rows) break;
-      nst += PT * ((EULER && mask) ? 2 : 1);
-#pragma unroll
-      for (int pt = 0; pt < PT; ++pt) {
-        const unsigned pix = (unsigned)(r * W + 16 * pt);  // compile-time
-        bf16x4 o4;
-        if constexpr (EULER) {
-          const bf16x4 xr = *(const bf16x4*)&xr2[r][pt];
-          unsigned nib = 0;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float z = acc[r][pt][e];
-            const bool pos = z > 0.f;  // relu'(z) as TF's ReluGrad: z > 0
-            nib |= (pos ? 1u : 0u) << e;
-            // relu as a select on the compare (a max would need NaN canonicalisation)
-            const float rz = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, z) & (pos ? ~0u : 0u));
-            o4[e] = (bf16)fmaf(h, rz, (float)xr[e]);
-          }
-          // the tile's 16 channel bits of pixel px: OR over the lane groups g
-          unsigned mword = nib << (4 * g);
-          const auto s16 = __builtin_amdgcn_permlane16_swap(mword, mword, false, false);
-          mword = s16[0] | s16[1];
-          const auto s32 = __builtin_amdgcn_permlane32_swap(mword, mword, false, false);
-          mword = s32[0] | s32[1];
-          if (mkb && g == 0) *(uint16_t*)(mkb + lm + pix * (C / 8)) = (uint16_t)mword;
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o4[e] = (bf16)acc[r][pt][e];
-        }
-        *(bf16x4*)(yb + ly + pix * C) = o4;
-      }
-    }
-  }
-}
-
 template <int NU, int U = 0, typename F, typename Acc, typename Xr, typename Cur>
 __device__ __forceinline__ void epi_all_units(F& f, const Acc& acc, const Xr& xr, const Cur& c) {
   if constexpr (U < NU) {
@@ -808,7 +688,7 @@ __device__ __forceinline__ void epi_all_units(F& f, const Acc& acc, const Xr& xr
 // consumed (an empty asm that reads them) right after the next barrier, before
 // any later DMA: hipcc's own vmcnt wait for a load counts only the memory ops
 // it sees, so a use behind a younger inline-asm DMA would wait for that DMA.
-template <int C, int W, int BR, int MODE, int NW, bool RES, bool RESG = false>
+template <int C, int W, int BR, int MODE, int NW, bool RESG = false>
 __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict__ x, const bf16* __restrict__ resid,
                                                   bf16* __restrict__ y, uint8_t* __restrict__ mask,
                                                   const bf16* __restrict__ wpack, const float* __restrict__ bias,
@@ -822,7 +702,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
   using BD = Band<C, W, RB>;
   // epilogue units: (row, pixel tile), or rows with both pixel tiles stored
   // as 16-B chunks (ASR_FWD_ST16)
-  constexpr bool ST16 = ASR_FWD_ST16 && PT == 2 && !RES;  // (RES: register-tight already)
+  constexpr bool ST16 = ASR_FWD_ST16 && PT == 2;
   constexpr int NU = ST16 ? RB : RB * PT;
   constexpr bool EULER = MODE == FWD_EULER;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -861,7 +741,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
   // its halo rows 0, 1 are p's rows BR, BR+1 -> copy them (interior columns),
   // DMA only rows 2.. (ASR_FWD_REUSE)
   auto dma_next2 = [&](const ItemCursor& c, const ItemCursor& p, int buf) {
-    if (!ASR_FWD_REUSE || RES || c.n != p.n || c.b != p.b + 1) {
+    if (!ASR_FWD_REUSE || c.n != p.n || c.b != p.b + 1) {
       dma(c, buf);
       return;
     }
@@ -881,42 +761,12 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
   int nst = 0;  // vector-memory ops this wave issued after the DMA the next barrier waits for
   // residual of a band: x from its LDS tile (read after the band's conv)
   auto xres_read = [&](int buf, u32x2 (&xr)[RB][PT]) {
-    if constexpr (EULER && !RES && !RESG) {
+    if constexpr (EULER && !RESG) {
       const unsigned tb = lds_u32(lds + buf * TILE) + lxr;
 #pragma unroll
       for (int r = 0; r < RB; ++r)
 #pragma unroll
         for (int pt = 0; pt < PT; ++pt) xr[r][pt] = lds_rd64(tb + (unsigned)(r * BD::ROWB + pt * BD::PTB));
-      lgkm_wait<0>();
-    }
-  };
-  // RES (second RK2 stage): the residual is the step input `resid`.  Each
-  // wave DMAs exactly its RB rows x W pixels x 16 channels into a private
-  // double buffer (1 KiB per row, 16-B chunks XOR-swizzled by pixel bit 3 so
-  // the epilogue's 8-B reads are conflict-free), one band ahead, BEFORE the
-  // next x tile's DMA: the barrier that waits for that tile also covers it.
-  static_assert(!RES || W * 32 == 1024, "private residual rows are one 1 KiB DMA each");
-  constexpr int PRB = RB * 1024;
-  unsigned char* priv = lds + 2 * TILE + wave * 2 * PRB;
-  auto dma_res = [&](const ItemCursor& c, int pb) {
-    if constexpr (RES) {
-      const int y0 = c.b * BR, rows = min(BR, H - y0);
-      const int px = lane >> 1, ch = 16 * ot + 8 * ((lane & 1) ^ ((px >> 3) & 1));
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        const void* src = (r0 + r < rows) ? (const void*)(resid + (((long)c.n * H + y0 + r0 + r) * W + px) * C + ch)
-                                          : (const void*)(g_zero_page + lane);
-        dma16(src, priv + pb * PRB + r * 1024);
-      }
-    }
-  };
-  auto res_read = [&](int pb, u32x2 (&xr)[RB][PT]) {
-    if constexpr (RES) {
-      const unsigned b = lds_u32(priv + pb * PRB) + (unsigned)(lx * 32 + (((g >> 1) ^ (lx >> 3)) * 16) + (g & 1) * 8);
-#pragma unroll
-      for (int r = 0; r < RB; ++r)
-#pragma unroll
-        for (int pt = 0; pt < PT; ++pt) xr[r][pt] = lds_rd64(b + (unsigned)(r * 1024 + pt * 512));
       lgkm_wait<0>();
     }
   };
@@ -1017,7 +867,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
   u32x2 xrA[RB][PT], xrB[RB][PT];
   // prologue: band i0 computed (its epilogue waits for the next band's MFMAs)
   dma(cur, 0);
-  dma_res(cur, 0);
   barrier_vm(0);
   if (i0 + 1 < i1) dma(nx1, 1);
   xg_load(cur, xrA);
@@ -1028,10 +877,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
   while (true) {
     // accA / xrA: band it.  In flight: DMA of band it+1 into buffer (it+1-i0)&1.
     if (it + 1 >= i1) {
-      if constexpr (RES) {
-        vm_wait(0);  // this wave's residual rows of band it (private: no barrier needed)
-        res_read((it - i0) & 1, xrA);
-      }
       epi_all(accA, xrA, cur);
       break;
     }
@@ -1040,11 +885,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
     ASR_STAMP(it - i0, 1);
     nst = 0;
     xg_consume(xrA);
-    dma_res(nx1, (it + 1 - i0) & 1);
     if (it + 2 < i1) dma_next2(nx2, nx1, (it - i0) & 1);
     xg_load(nx1, xrB);
     ASR_STAMP(it - i0, 2);
-    res_read((it - i0) & 1, xrA);
     init(accB);
     {
       const ItemCursor c = cur;
@@ -1060,10 +903,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
     nx2.next(nb);
     // the same with the roles of A and B swapped
     if (it + 1 >= i1) {
-      if constexpr (RES) {
-        vm_wait(0);
-        res_read((it - i0) & 1, xrB);
-      }
       epi_all(accB, xrB, cur);
       break;
     }
@@ -1072,11 +911,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
     ASR_STAMP(it - i0, 1);
     nst = 0;
     xg_consume(xrB);
-    dma_res(nx1, (it + 1 - i0) & 1);
     if (it + 2 < i1) dma_next2(nx2, nx1, (it - i0) & 1);
     xg_load(nx1, xrA);
     ASR_STAMP(it - i0, 2);
-    res_read((it - i0) & 1, xrB);
     init(accA);
     {
       const ItemCursor c = cur;
@@ -2431,7 +2268,6 @@ __global__ __launch_bounds__(256) void k_stem_fwd_mfma(const Tin* __restrict__ i
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
-constexpr int kFwdBR = 8;
 constexpr int kBwdBR = 4;
 constexpr int kMaxBlockSlabs = 512;
 
@@ -2439,24 +2275,6 @@ static int persistent_grid(long items) {
   int cus = cu_count();
   if (cus <= 0) cus = 256;
   return (int)std::max<long>(1, std::min<long>({items, (long)cus, (long)kMaxBlockSlabs}));
-}
-
-// second RK2 stage (residual from `resid`): 8-row bands, 8 waves, one WG per
-// CU (the private residual buffers need the LDS of two 4-wave WGs)
-template <int C, int W>
-static int launch_fwd_res(const void* x, const void* resid, void* y, uint8_t* mask, const void* w, const float* bias,
-                          float h, int N, int H, hipStream_t s) {
-  constexpr int BR = 8, NW = 8, RB = BR / (NW / (C / 16));
-  const long items = (long)N * ((H + BR - 1) / BR);
-  if (items > 0x7fffffffL) return fail(ASR_E_UNSUPPORTED, "bf16 block: too many row bands (%ld)", items);
-  int cus = cu_count();
-  if (cus <= 0) cus = 256;
-  const int grid = (int)std::max<long>(1, std::min<long>(items, (long)cus));
-  const size_t lds = 2 * (size_t)(BR + 2) * (W + 2) * C * 2 + (size_t)NW * 2 * RB * 1024;
-  hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_EULER, NW, true>), dim3(grid), dim3(64 * NW), lds, s,
-                     (const bf16*)x, (const bf16*)resid, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
-  ASR_LAUNCH_CHECK("k_fwd_pipe(res)");
-  return ASR_OK;
 }
 
 template <int C, int W, int BR, int NW>
@@ -2469,31 +2287,16 @@ static int launch_fwd_v(int mode, const void* x, const void* resid, void* y, uin
   if (cus <= 0) cus = 256;
   const int grid = (int)std::max<long>(1, std::min<long>(items, (long)cus * (8 / NW)));
   const size_t lds = 2 * (size_t)(BR + 2) * (W + 2) * C * 2;
-  static const bool no_pipe = getenv("ASR_FWD_NOPIPE") != nullptr;  // development A/B
   if constexpr (C >= 32) {
-    if (no_pipe) {
-      if (mode == blk::FWD_EULER)
-        hipLaunchKernelGGL((blk::k_fwd_band<C, W, BR, blk::FWD_EULER, NW>), dim3(grid), dim3(64 * NW), lds, s,
-                           (const bf16*)x, (const bf16*)resid, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
-      else
-        hipLaunchKernelGGL((blk::k_fwd_band<C, W, BR, blk::FWD_CONV, NW>), dim3(grid), dim3(64 * NW), lds, s,
-                           (const bf16*)x, (const bf16*)resid, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+    if (mode == blk::FWD_EULER && resid) {  // second RK2 stage: residual from the step input
+      hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_EULER, NW, true>), dim3(grid), dim3(64 * NW), lds, s,
+                         (const bf16*)x, (const bf16*)resid, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+    } else if (mode == blk::FWD_EULER) {
+      hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_EULER, NW>), dim3(grid), dim3(64 * NW), lds, s,
+                         (const bf16*)x, nullptr, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
     } else {
-      static const bool res_v1 = getenv("ASR_FWD_RES_V1") != nullptr;  // development A/B: private-LDS residual
-      if (mode == blk::FWD_EULER && resid && res_v1)
-        return launch_fwd_res<C, W>(x, resid, y, mask, w, bias, h, N, H, s);
-      if (mode == blk::FWD_EULER && resid) {
-        hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_EULER, NW, false, true>), dim3(grid), dim3(64 * NW),
-                           lds, s, (const bf16*)x, (const bf16*)resid, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
-        ASR_LAUNCH_CHECK("k_fwd_pipe(resg)");
-        return ASR_OK;
-      }
-      if (mode == blk::FWD_EULER)
-        hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_EULER, NW, false>), dim3(grid), dim3(64 * NW), lds, s,
-                           (const bf16*)x, nullptr, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
-      else
-        hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_CONV, NW, false>), dim3(grid), dim3(64 * NW), lds, s,
-                           (const bf16*)x, nullptr, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+      hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_CONV, NW>), dim3(grid), dim3(64 * NW), lds, s,
+                         (const bf16*)x, nullptr, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
     }
   } else {
     if (mode == blk::FWD_EULER)
@@ -2531,11 +2334,11 @@ static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* ma
   hipLaunchKernelGGL((blk::k_bwd<C, W, kBwdBR, M, XT>), dim3(grid), dim3(512), lds, s, (const bf16*)dy, (const bf16*)x, \
                      mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs, (const bf16*)extra, skip_dy, accum)
   const bool xt = extra != nullptr || skip_dy != 0 || accum != 0;
-  static const bool v1 = getenv("ASR_BWD_V1") != nullptr;  // development A/B
   if constexpr (C == 64) {
-    static const bool xt_v1 = getenv("ASR_RK2_BWD_V1") != nullptr;  // development A/B: RK2 first stage on v1
-    const bool xt2 = extra && accum && !skip_dy && mode == blk::BWD_EULER && !relu_dx && !xt_v1;
-    if ((xt2 || (!extra && !accum && (mode == blk::BWD_EULER || !skip_dy))) && !v1) {  // v2: no extra dx term (RK2 stage 1 stays on v1)
+    // v2: the Euler block, the plain conv, and both RK2 stages (the first: extra
+    // dx term + slab accumulation); other compositions run the v1 kernel
+    const bool xt2 = extra && accum && !skip_dy && mode == blk::BWD_EULER && !relu_dx;
+    if (xt2 || (!extra && !accum && (mode == blk::BWD_EULER || !skip_dy))) {
       using L2 = blk::Bwd2Lds<C, W, kBwdBR>;
       const size_t lds2 = std::max((size_t)L2::TOTAL, red);
       // the folded pass gives each thread one 16-B chunk: at most 512 per WG

@@ -298,7 +298,7 @@ using namespace asr;
 extern "C" {
 
 const char* asr_last_error(void) { return g_err; }
-int asr_abi_version(void) { return 3; }
+int asr_abi_version(void) { return 4; }
 int asr_device_cu_count(void) { return cu_count(); }
 
 long asr_theta_count(int C, int kind, int antisymmetric) { return theta_count(C, kind, antisymmetric); }

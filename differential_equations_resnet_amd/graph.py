@@ -544,21 +544,21 @@ class Model:
             self._native.push_weights()
 
     def compile_native(self, batch_size, dtype="bfloat16", device=None):
-        """Lower this model onto the native executor (lowering.py)."""
+        """Lower this model onto the native executor (lowering.py).  The
+        model owns one device parameter set; every (batch size, dtype) view
+        returned here shares it."""
         from .lowering import NativeModel
-        if self._native is not None and self._native.matches(batch_size, dtype):
-            return self._native
-        if self._native is not None:
-            self._native.pull_weights()
-        self._native = NativeModel(self, batch_size, dtype, device)
-        return self._native
+        if self._native is None:
+            self._native = NativeModel(self, device)
+        return self._native.view(batch_size, dtype)
 
     def predict(self, x, batch_size=None, dtype="bfloat16"):
-        """Softmax outputs for images `x` (numpy or device, NHWC)."""
+        """Softmax outputs for images `x` (numpy or device, NHWC), in batches
+        of `batch_size` (default: min(len(x), 256), so the executor's
+        training-sized workspace stays bounded)."""
         n = int(x.shape[0])
-        bs = int(batch_size or n)
-        nm = self.compile_native(bs, dtype)
-        return nm.predict(x)
+        bs = int(batch_size or min(n, 256))
+        return self.compile_native(bs, dtype).predict(x)
 
     def __call__(self, *args, **kwargs):
         raise TypeError("Model objects are executed with predict()/Training, not called as layers")

@@ -202,19 +202,22 @@ def analyze(model: Model) -> NetPlan:
 
 
 class NativeModel:
-    """A Model lowered onto the native executor for a fixed per-process batch.
+    """The device state of one Model lowered onto the native executor.
 
-    Holds the flat fp32 device parameters (Keras order), the Adam moments,
-    and one executor per input kind (uint8 or float32 images).  Host-side
-    Variables stay the source of truth between push_weights/pull_weights."""
+    ONE instance per Model owns the flat fp32 device parameters (Keras
+    order), the Adam moments and step, and every executor built for it,
+    keyed by (batch size, activation dtype, input kind) — so a predict() at
+    another batch size or dtype reads the trained parameters and a
+    set_weights()/load_variables() reaches every executor.  Host-side
+    Variables and the device buffer are kept coherent through
+    push_weights/pull_weights.  Callers use views (view(batch, dtype)) that
+    fix the batch size and dtype of their calls."""
 
-    def __init__(self, model: Model, batch_size: int, dtype="bfloat16", device=None):
+    def __init__(self, model: Model, device=None):
         from . import runtime
         import torch
         self.model = model
         self.plan = analyze(model)
-        self.batch_size = int(batch_size)
-        self.dtype = dtype
         self.device = device or runtime.require_gpu()
         self._torch = torch
         self._rt = runtime
@@ -228,8 +231,8 @@ class NativeModel:
         self._host_stale = False
         self.push_weights()
 
-    def matches(self, batch_size, dtype):
-        return self.batch_size == int(batch_size) and self.dtype == dtype
+    def view(self, batch_size: int, dtype="bfloat16") -> "NativeView":
+        return NativeView(self, int(batch_size), dtype)
 
     # -- weights ---------------------------------------------------------------
     def push_weights(self):
@@ -254,18 +257,19 @@ class NativeModel:
         self._host_stale = True
 
     # -- execution ---------------------------------------------------------------
-    def executor(self, input_u8: bool):
-        ex = self._executors.get(input_u8)
+    def executor(self, batch_size: int, dtype, input_u8: bool):
+        key = (int(batch_size), dtype, bool(input_u8))
+        ex = self._executors.get(key)
         if ex is None:
             p = self.plan
-            ex = self._rt.NetExecutor(self.batch_size, p.H, p.W, p.Cin, p.C, p.L, p.num_classes, p.h, p.gamma,
+            ex = self._rt.NetExecutor(int(batch_size), p.H, p.W, p.Cin, p.C, p.L, p.num_classes, p.h, p.gamma,
                                       subtract_mean=p.subtract_mean, divide_by_stddev=p.divide_by_stddev,
-                                      dtype=self.dtype, input_u8=input_u8, device=self.device,
+                                      dtype=dtype, input_u8=input_u8, device=self.device,
                                       param_kind=p.param_kind, antisymmetric=p.antisymmetric,
                                       integrator=p.integrator)
             if ex.n_params != self.n_params:
                 raise _lib.AsrError(f"executor expects {ex.n_params} parameters, model has {self.n_params}")
-            self._executors[input_u8] = ex
+            self._executors[key] = ex
         return ex
 
     def _images(self, x):
@@ -275,6 +279,42 @@ class NativeModel:
         if x.dtype not in (torch.uint8, torch.float32):
             x = x.float()
         return x.to(self.device, non_blocking=True).contiguous()
+
+    def apply_adam(self, grads, lr, beta1=0.9, beta2=0.999, epsilon=1e-7, grad_scale=1.0):
+        torch = self._torch
+        if self.m is None:
+            self.m = torch.zeros_like(self.params)
+            self.v = torch.zeros_like(self.params)
+        self.step += 1
+        self._rt.adam_update(self.params, grads, self.m, self.v, lr, beta1, beta2, epsilon, self.step, grad_scale)
+        self._host_stale = True
+
+
+class NativeView:
+    """A NativeModel at a fixed batch size and dtype.  Everything else
+    (parameters, Adam state, weight sync) is the shared NativeModel's."""
+
+    _SHARED = ("params", "m", "v", "step")
+
+    def __init__(self, state: NativeModel, batch_size: int, dtype):
+        object.__setattr__(self, "state", state)
+        object.__setattr__(self, "batch_size", int(batch_size))
+        object.__setattr__(self, "dtype", dtype)
+
+    def __getattr__(self, name):
+        return getattr(self.state, name)
+
+    def __setattr__(self, name, value):
+        if name in self._SHARED:
+            setattr(self.state, name, value)
+        else:
+            object.__setattr__(self, name, value)
+
+    def matches(self, batch_size, dtype):
+        return self.batch_size == int(batch_size) and self.dtype == dtype
+
+    def executor(self, input_u8: bool):
+        return self.state.executor(self.batch_size, self.dtype, input_u8)
 
     def predict(self, x):
         """Softmax outputs [n, K] (numpy) for n images, in batches of
@@ -305,12 +345,3 @@ class NativeModel:
         ex = self.executor(x.dtype == torch.uint8)
         loss, grads = ex.forward_backward(self.params, x, targets, want_probs=want_probs)
         return loss, grads, ex.probs
-
-    def apply_adam(self, grads, lr, beta1=0.9, beta2=0.999, epsilon=1e-7, grad_scale=1.0):
-        torch = self._torch
-        if self.m is None:
-            self.m = torch.zeros_like(self.params)
-            self.v = torch.zeros_like(self.params)
-        self.step += 1
-        self._rt.adam_update(self.params, grads, self.m, self.v, lr, beta1, beta2, epsilon, self.step, grad_scale)
-        self._host_stale = True

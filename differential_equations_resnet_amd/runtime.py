@@ -13,7 +13,8 @@ import torch
 
 from . import _lib
 from ._lib import (ASR_BF16, ASR_F32, ASR_INTEGRATOR_EULER, ASR_INTEGRATOR_RK2, ASR_MODE_CONV, ASR_MODE_EULER,
-                   ASR_PARAM_3BY3, ASR_PARAM_GENERAL, ASR_PARAM_REGULAR, NetConfig)
+                   ASR_PARAM_3BY3, ASR_PARAM_GENERAL, ASR_PARAM_REGULAR, ASR_VARIANT_NO_FOLD, ASR_VARIANT_STEM_FWD_VALU,
+                   ASR_VARIANT_STEM_WGRAD_VALU, NetConfig)
 
 __all__ = [
     "require_gpu", "dtype_code", "torch_dtype", "ParamMap", "param_map", "theta_count", "theta_to_w",
@@ -164,7 +165,15 @@ def segment_sq_norms(x: torch.Tensor, offsets: torch.Tensor) -> torch.Tensor:
 
 
 def batch_metrics(probs, targets, loss, accum):
+    """Streaming loss/accuracy accumulation (asr_batch_metrics): probs and
+    targets are contiguous float32 device [N, K]; loss a device float or None."""
     N, K = probs.shape
+    for name, t in (("probs", probs), ("targets", targets), ("accum", accum)) + ((("loss", loss),) if loss is not None
+                                                                                  else ()):
+        if not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError(f"batch_metrics: {name} must be a contiguous float32 device tensor")
+    if tuple(targets.shape) != (N, K) or accum.numel() < 4:
+        raise ValueError(f"batch_metrics: targets must be [{N}, {K}] and accum hold 4 floats")
     _lib.call("asr_batch_metrics", _p(probs), _p(targets), _p(loss), N, K, _p(accum), _stream())
 
 
@@ -248,14 +257,14 @@ class NetExecutor:
 
     def __init__(self, N, H, W, Cin, C, L, num_classes, h, gamma=0.0, subtract_mean=None, divide_by_stddev=None,
                  dtype="bfloat16", input_u8=True, device=None, param_kind=ASR_PARAM_3BY3, antisymmetric=True,
-                 integrator="euler"):
+                 integrator="euler", variant=0):
         self.device = device or require_gpu()
         use_norm = subtract_mean is not None or divide_by_stddev is not None
         self.cfg = NetConfig(int(N), int(H), int(W), int(Cin), int(C), int(L), int(num_classes), float(h),
                              float(gamma), float(subtract_mean or 0.0),
                              float(divide_by_stddev if divide_by_stddev is not None else 1.0), int(use_norm),
                              dtype_code(dtype), int(bool(input_u8)), int(param_kind), int(bool(antisymmetric)),
-                             integrator_code(integrator))
+                             integrator_code(integrator), int(variant))
         lib = _lib.load()
         self.n_params = int(lib.asr_net_param_count(ct.byref(self.cfg)))
         if self.n_params < 0:
@@ -282,6 +291,15 @@ class NetExecutor:
         _lib.call("asr_net_forward", ct.byref(self.cfg), _p(params), _p(images), _p(self.probs), _p(self.ws),
                   self.ws_bytes, _stream())
         return self.probs
+
+    @property
+    def variant(self) -> int:
+        return int(self.cfg.variant)
+
+    @variant.setter
+    def variant(self, bits: int):
+        """Select ASR_VARIANT_* kernel compositions for later calls (tests)."""
+        self.cfg.variant = int(bits)
 
     def forward_backward(self, params, images, targets, want_probs=False):
         self._check_inputs(params, images)

@@ -209,10 +209,7 @@ class Training:
         self._accum.zero_()
 
     def _metric_values(self):
-        a = self._accum.clone()
-        if self.dist is not None:
-            self.dist.all_reduce(a)
-        a = a.cpu().numpy().astype(np.float64)
+        a = np.asarray(distributed.sum_over_ranks(self._accum.cpu().double().tolist()), dtype=np.float64)
         batches = max(a[3], 1.0)
         return [float(a[0] / batches), float(a[1] / max(a[2], 1.0))]
 
@@ -224,11 +221,26 @@ class Training:
         except StopIteration:
             raise RuntimeError("dataset exhausted (use repeat=True for training)")
 
+    def _targets(self, labels):
+        """One-hot labels as the contiguous float32 device [N, K] tensor both
+        the executor and the metrics kernel read (numpy, CPU or other-dtype
+        batches are converted once here)."""
+        torch = self._torch
+        if isinstance(labels, np.ndarray):
+            labels = torch.from_numpy(np.ascontiguousarray(labels))
+        if not torch.is_tensor(labels):
+            raise ValueError("labels must be a numpy array or a tensor of one-hot rows")
+        t = labels.to(self.native.device, dtype=torch.float32, non_blocking=True).contiguous()
+        if t.dim() != 2 or t.shape[0] != self.batch_size:
+            raise ValueError(f"labels must be one-hot [{self.batch_size}, num_classes], got {tuple(t.shape)}")
+        return t
+
     def train_step(self, learning_rate, with_norms=False):
         """One optimisation step on the next training batch; returns the
         gradient mean-norms when with_norms (else None)."""
         from .. import runtime
         images, labels = self._next("_train_iter")
+        labels = self._targets(labels)
         loss, grads, probs = self.native.forward_backward(images, labels, want_probs=True)
         distributed.allreduce_grads(grads)
         norms = self._gradient_mean_norms(grads) if with_norms else None
@@ -319,6 +331,8 @@ class Training:
         ex_u8 = None
         for _ in tr:
             images, labels = self._next(it)
+            images = self.native._images(images)
+            labels = self._targets(labels)
             if ex_u8 is None:
                 ex_u8 = self.native.executor(images.dtype == self._torch.uint8)
             probs = ex_u8.forward(self.native.params, images)

@@ -195,7 +195,19 @@ typedef struct asr_net_config {
   int antisymmetric; /* Conv2DAntisymmetric(antisymmetric=...); 1 otherwise */
   int integrator;    /* ASR_INTEGRATOR_EULER (the reference's block) or
                         ASR_INTEGRATOR_RK2 (extension, asr_rk2_forward)     */
+  int variant;       /* 0 = the production kernel composition; ASR_VARIANT_*
+                        bits select slower, independently written kernels
+                        for the same math (cross-checks in the tests)      */
 } asr_net_config;
+
+/* asr_net_config.variant bits (all 0 in production) */
+#define ASR_VARIANT_NO_FOLD 1      /* reduce every block's weight-gradient slabs in
+                                      its own launch instead of folding the pass
+                                      into the next block's backward kernel      */
+#define ASR_VARIANT_STEM_FWD_VALU 2 /* bf16 stem forward on the fp32 VALU kernel  */
+#define ASR_VARIANT_STEM_WGRAD_VALU 4 /* stem weight gradient on the fp32 VALU
+                                        kernel from dx1 and x1 (relu' not fused
+                                        into the first block's backward)       */
 
 long asr_net_param_count(const asr_net_config* cfg);
 size_t asr_net_workspace_bytes(const asr_net_config* cfg);
@@ -234,6 +246,30 @@ int asr_segment_sq_norms(const float* x, const long* offsets, int n_segments, fl
  * batch-mean Keras categorical cross-entropy of probs is used (evaluation). */
 int asr_batch_metrics(const float* probs, const float* targets, const float* loss, int N, int K,
                       float* accum, asr_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Data-parallel collectives (RCCL over xGMI; one process per GPU).  NEW: the
+ * reference is single-device (experiments_antisymmetric_resnet_v6.ipynb:361);
+ * SURVEY.md §8(e) adds one all-reduce of the flat fp32 gradient buffer per
+ * step (the batch is split by image: no BatchNorm, batch-mean loss,
+ * training.py:295) and one broadcast of the initial parameters.
+ * ---------------------------------------------------------------------- */
+#define ASR_DIST_UNIQUE_ID_BYTES 128
+
+/* Host: rank 0 creates the communicator id (out: 128 host bytes) and hands
+ * it to every rank out of band (file, TCP store, ...). */
+int asr_dist_unique_id(void* out);
+/* Host, blocking, collective over all ranks: create this process's
+ * communicator on the current HIP device. */
+int asr_dist_init(int rank, int world, const void* unique_id);
+/* In place on the caller's stream: buf = sum over ranks (dtype ASR_F32/BF16). */
+int asr_dist_allreduce_sum(void* buf, size_t count, int dtype, asr_stream_t stream);
+/* In place on the caller's stream: buf = root's buf. */
+int asr_dist_broadcast(void* buf, size_t count, int dtype, int root, asr_stream_t stream);
+/* World size of the live communicator (0 when none). */
+int asr_dist_world_size(void);
+/* Destroy the communicator (no-op without one). */
+int asr_dist_finalize(void);
 
 #ifdef __cplusplus
 }

@@ -16,6 +16,12 @@ reference slow:
   * loss = mean Keras categorical cross-entropy on softmax probabilities
     (training/training.py:295), TF1 Adam with epsilon 1e-7 (training.py:300-301).
 Everything is float32, like the reference.
+
+RefNet(..., assembly="vectorised") replaces the per-step op-by-op assembly by
+one gather W = sign * theta[src] (the closed form W = P - P* + gamma*I of
+SURVEY §8a-4, through oracle.asr_oracle.param_map): the same math with the
+framework overhead of ~C^2 tiny ops per layer removed, so the two CPU numbers
+separate that overhead from the convolution arithmetic.
 """
 from __future__ import annotations
 
@@ -79,8 +85,17 @@ def conv2d_nhwc_same(x, w_hwio):
 class RefNet:
     """antisymmetric single-block ResNet (tfkeras_resnets.py:547-597) in float32."""
 
-    def __init__(self, params_np, C, L, h, gamma=0.0, num_classes=10, mean=127.5, std=127.5):
+    def __init__(self, params_np, C, L, h, gamma=0.0, num_classes=10, mean=127.5, std=127.5, assembly="reference"):
+        if assembly not in ("reference", "vectorised"):
+            raise ValueError(assembly)
         self.C, self.L, self.h, self.gamma, self.K = C, L, h, gamma, num_classes
+        self.assembly = assembly
+        if assembly == "vectorised":
+            from .asr_oracle import param_map
+            src, sign = param_map(C)
+            self._src = torch.from_numpy(np.maximum(src, 0))
+            self._sign = torch.from_numpy(sign.astype(np.float32))
+            self._is_gamma = torch.from_numpy(src < 0)
         self.mean, self.std = mean, std
         self.params = [torch.tensor(np.asarray(p, dtype=np.float32), requires_grad=True) for p in params_np]
         self.m = [torch.zeros_like(p) for p in self.params]
@@ -104,8 +119,13 @@ class RefNet:
         x = conv2d_nhwc_same(x.contiguous(), c1k) + c1b
         x = torch.relu(x)
         for theta, b in blocks:
-            a, bb, c, d = theta[:4]
-            W = assemble_kernel(a, bb, c, d, theta[4:], self.gamma)
+            if self.assembly == "vectorised":
+                flat = torch.cat([t.reshape(-1) for t in theta])
+                W = torch.where(self._is_gamma, torch.full((), self.gamma), self._sign * flat[self._src])
+                W = W.view(3, 3, self.C, self.C)
+            else:
+                a, bb, c, d = theta[:4]
+                W = assemble_kernel(a, bb, c, d, theta[4:], self.gamma)
             z = conv2d_nhwc_same(x, W)
             z = z + b
             r = torch.relu(z)

@@ -34,3 +34,40 @@ def assert_close(got, want, rtol, atol=0.0, what=""):
         i = np.unravel_index(np.argmax(err - lim), err.shape)
         raise AssertionError(f"{what}: {bad.sum()} / {bad.size} elements outside tolerance "
                              f"(rtol={rtol}, atol={atol}); worst at {i}: got {got[i]!r} want {want[i]!r}")
+
+
+def rel_l2(got, want):
+    """||got - want||_2 / ||want||_2 over the flattened arrays."""
+    got = np.asarray(got, np.float64).ravel()
+    want = np.asarray(want, np.float64).ravel()
+    return float(np.linalg.norm(got - want) / max(np.linalg.norm(want), 1e-30))
+
+
+def grad_groups(spec, g):
+    """(name, flat array) per gradient group in Keras weight order: conv1
+    kernel and bias, per block its merged theta (all kernel variables) and
+    bias, fc kernel and bias — the per-layer groups of the reference's
+    gradient norms (training.py:385-409)."""
+    nt = len(spec.theta_shapes())
+    out = [("conv1/kernel", np.ravel(g[0])), ("conv1/bias", np.ravel(g[1]))]
+    i = 2
+    for b in range(spec.L):
+        out.append((f"block{b}/theta", np.concatenate([np.ravel(a) for a in g[i:i + nt]])))
+        out.append((f"block{b}/bias", np.ravel(g[i + nt])))
+        i += nt + 1
+    out += [("fc/kernel", np.ravel(g[i])), ("fc/bias", np.ravel(g[i + 1]))]
+    return out
+
+
+def assert_grad_groups_rel_l2(spec, got, want, tol=2e-2):
+    """bf16 network gradients vs the fp64 oracle: relative L2 <= tol per
+    gradient group."""
+    bad = []
+    for (name, a), (_, b) in zip(grad_groups(spec, got), grad_groups(spec, want)):
+        if np.linalg.norm(b) == 0:
+            assert np.linalg.norm(a) == 0, name
+            continue
+        e = rel_l2(a, b)
+        if not e <= tol:
+            bad.append(f"{name}: rel-L2 {e:.3e}")
+    assert not bad, "; ".join(bad)

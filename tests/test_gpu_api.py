@@ -143,7 +143,7 @@ def test_training_driver_end_to_end(tmp_path):
                   csv_logger_name="gradient_history", dtype="float32")
     # gradient mean-norms match a host recomputation from the same gradient buffer
     norms = tr.train_step(1e-3, with_norms=True)
-    g = tr.native._executors[True].grads.cpu().numpy().astype(np.float64)
+    g = tr.native.executor(True).grads.cpu().numpy().astype(np.float64)
     plan = tr.native.plan
     want0 = np.linalg.norm(g[:plan.conv1.kernel.value.size]) / plan.conv1.kernel.value.size
     assert abs(norms[0] - want0) <= 1e-5 * want0
@@ -159,9 +159,19 @@ def test_training_driver_end_to_end(tmp_path):
     assert ev[0] == ["global_step", "mean_loss", "accuracy"] and len(ev) == 3
     res = tr.evaluate("val", 4)
     assert 0.0 <= res["accuracy"] <= 1.0 and np.isfinite(res["mean_loss"])
-    # evaluation loss (native CE from probabilities) equals the oracle's
+    # predict() and the evaluation metrics (native CE from the probabilities,
+    # argmax accuracy) equal the oracle's on the trained parameters
     probs = tr.predict(feats[:B], argmax=False)
-    assert probs.shape == (B, 10) and np.allclose(probs.sum(1), 1.0, atol=1e-5)
+    spec = O.NetSpec(C=16, L=3, h=0.5)
+    params = [w.astype(np.float64) for w in tr.model.get_weights()]
+    want, _ = O.net_forward(spec, params, feats[:B])
+    assert_close(probs, want, rtol=1e-5, atol=1e-6, what="Training.predict")
+    one = ArrayDataset(feats[:B], labels[:B], B, shuffle=False, num_classes=10)
+    tr._val_iter = iter(one)
+    res1 = tr.evaluate("val", 1)
+    onehot = np.eye(10)[labels[:B]]
+    assert abs(res1["mean_loss"] - O.net_loss(want, onehot)) <= 1e-5 * O.net_loss(want, onehot)
+    assert res1["accuracy"] == float((want.argmax(1) == labels[:B]).mean())
     path = tr.save(str(tmp_path / "ckpt"), "train_saver")
     assert path and os.path.exists(os.path.join(path, "variables.npz")) and "globalstep-9" in path
     w_before = tr.model.get_weights()
@@ -191,3 +201,96 @@ def test_training_overfits_one_batch():
         tr.train_step(3e-3)
     last = tr.evaluate("train", 1)["mean_loss"]
     assert last < 0.5 * first, (first, last)
+
+
+def _merged_theta_norms(spec, grads):
+    """The reference's per-layer gradient mean-norms for an antisymmetric
+    model (training.py:385-409, generalised from the hard-coded 20 variables):
+    conv1's kernel, then per block ||merged theta gradient||_2 / size (bias
+    excluded)."""
+    out = [np.linalg.norm(grads[0]) / grads[0].size]
+    nt = 4 + spec.C - 1
+    i = 2
+    for _ in range(spec.L):
+        th = np.concatenate([g.ravel() for g in grads[i:i + nt]])
+        out.append(np.linalg.norm(th) / th.size)
+        i += nt + 1
+    return out
+
+
+def test_training_metrics_match_oracle(tmp_path):
+    """Three Training.train_step calls on one fixed batch (fp32): every
+    per-block merged-theta gradient mean-norm equals the oracle's on the same
+    parameters (the device's, read back before each step; 1e-5 relative), and
+    the streaming mean_loss / accuracy equal the oracle's means over the three
+    steps (training.py:316-354, :385-409, :578-597).  The Adam update itself
+    is checked against the oracle in test_gpu_kernels.py."""
+    from differential_equations_resnet_amd.dataset_utils import ArrayDataset
+    from differential_equations_resnet_amd.training import AdamOptimizer, Training
+    rng = np.random.default_rng(5)
+    B, C, L, h = 8, 16, 3, 0.5
+    feats = rng.integers(0, 256, (B, 32, 32, 3)).astype(np.uint8)
+    labels = rng.integers(0, 10, B)
+    onehot = np.eye(10)[labels]
+    ds = ArrayDataset(feats, labels, B, shuffle=False, num_classes=10)
+    graph.set_seed(3)
+    build = R.get_single_block_resnet_build_function(h=h, num_stages=2, blocks_per_stage=[L],
+                                                     filters_per_block=[C], strides=[(1, 1)], subtract_mean=127.5,
+                                                     divide_by_stddev=127.5, num_classes=10)
+    tr = Training(build, "antisymmetric", AdamOptimizer(epsilon=1e-7), train_dataset=ds,
+                  summaries_dir=str(tmp_path), summaries_name="run", csv_logger_dir=str(tmp_path),
+                  csv_logger_name="gradient_history", dtype="float32")
+    spec = O.NetSpec(C=C, L=L, h=h)
+    losses, correct = [], 0
+    tr._reset_metrics()
+    for t in range(1, 4):
+        params = [w.astype(np.float64) for w in tr.model.get_weights()]
+        probs, cache = O.net_forward(spec, params, feats)
+        grads = O.net_backward(spec, params, cache, onehot)
+        losses.append(O.net_loss(probs, onehot))
+        correct += int((probs.argmax(1) == labels).sum())
+        want_norms = _merged_theta_norms(spec, grads)
+        got_norms = tr.train_step(1e-3, with_norms=True)
+        assert len(got_norms) == 1 + L
+        assert_close(got_norms, want_norms, rtol=1e-5, what=f"step {t} gradient mean-norms")
+    mean_loss, acc = tr._metric_values()
+    assert abs(mean_loss - np.mean(losses)) <= 1e-5 * np.mean(losses)
+    assert acc == correct / (3 * B)
+    tr.close()
+
+
+def test_native_state_shared_across_batch_sizes(tmp_path):
+    """One device parameter set per Model: predict() at another batch size
+    or dtype after training reads the trained parameters, get_weights and
+    save/load_variables see them, and training continues from them (ADVICE
+    r01: executors used to snapshot the weights when re-lowered)."""
+    from differential_equations_resnet_amd.dataset_utils import ArrayDataset
+    from differential_equations_resnet_amd.training import AdamOptimizer, Training
+    rng = np.random.default_rng(9)
+    feats = rng.integers(0, 256, (8, 32, 32, 3)).astype(np.uint8)
+    labels = rng.integers(0, 10, 8)
+    ds = ArrayDataset(feats, labels, 8, shuffle=False, num_classes=10)
+    graph.set_seed(1)
+    build = R.get_single_block_resnet_build_function(h=0.5, num_stages=2, blocks_per_stage=[2],
+                                                     filters_per_block=[16], strides=[(1, 1)], subtract_mean=127.5,
+                                                     divide_by_stddev=127.5, num_classes=10)
+    tr = Training(build, "antisymmetric", AdamOptimizer(epsilon=1e-7), train_dataset=ds, record_summaries=False,
+                  dtype="float32")
+    spec = O.NetSpec(C=16, L=2, h=0.5)
+    tr.train_step(1e-2)
+    p1 = tr.model.predict(feats[:3], batch_size=3, dtype="float32")  # a new executor (batch 3)
+    w1 = [w.astype(np.float64) for w in tr.model.get_weights()]
+    assert_close(p1, O.net_forward(spec, w1, feats[:3])[0], rtol=1e-5, atol=1e-6, what="predict after step 1")
+    tr.train_step(1e-2)  # continues from the trained parameters
+    w2 = [w.astype(np.float64) for w in tr.model.get_weights()]
+    assert any(np.abs(a - b).max() > 0 for a, b in zip(w1, w2))
+    p2 = tr.model.predict(feats[:3], batch_size=3, dtype="float32")
+    assert_close(p2, O.net_forward(spec, w2, feats[:3])[0], rtol=1e-5, atol=1e-6, what="predict after step 2")
+    path = tr.save(str(tmp_path / "ckpt"), "train_saver")
+    tr.train_step(1e-2)
+    tr.load_variables(path)  # restores every executor's parameters, the training one included
+    for a, b in zip(tr.model.get_weights(), w2):
+        np.testing.assert_array_equal(a, b.astype(np.float32))
+    p3 = tr.model.predict(feats[:3], batch_size=3, dtype="float32")
+    np.testing.assert_array_equal(p3, p2)
+    tr.close()

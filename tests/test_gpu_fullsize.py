@@ -123,11 +123,11 @@ def test_network_fullsize_properties(rt, cfg):
 
 
 @pytest.mark.parametrize("N,u8", [(64, True), (512, True), (64, False)])
-def test_stem_wgrad_mfma_matches_fp32_path(rt, N, u8, monkeypatch):
+def test_stem_wgrad_mfma_matches_fp32_path(rt, N, u8):
     """The network's default bf16 path fuses the stem's relu' into the first
     block's backward (dx -> dz1) and computes the stem weight gradient on
     MFMA from bf16 (v - mean) (exact for u8 input and mean 127.5); with
-    ASR_STEM_V1 set it runs the fp32 VALU stem kernel from dx1 and x1.  The
+    variant ASR_VARIANT_STEM_WGRAD_VALU it runs the fp32 VALU stem kernel from dx1 and x1.  The
     stem gradients agree to fp32 summation-order noise (u8) or bf16 rounding
     of the centred float input (1e-3 of max|g|); every other gradient and the
     loss are bitwise unchanged."""
@@ -143,10 +143,10 @@ def test_stem_wgrad_mfma_matches_fp32_path(rt, N, u8, monkeypatch):
                         dtype="bfloat16", input_u8=u8, device=dev)
     loss, g = ex.forward_backward(params, imgs, tgt)
     loss, g = loss.clone(), g.clone()
-    monkeypatch.setenv("ASR_STEM_V1", "1")
+    ex.variant = rt.ASR_VARIANT_STEM_WGRAD_VALU
     loss1, g1 = ex.forward_backward(params, imgs, tgt)
     loss1, g1 = loss1.clone(), g1.clone()
-    monkeypatch.delenv("ASR_STEM_V1")
+    ex.variant = 0
     torch.cuda.synchronize()
     E1 = 9 * 3 * C + C
     assert torch.equal(loss, loss1)
@@ -158,10 +158,10 @@ def test_stem_wgrad_mfma_matches_fp32_path(rt, N, u8, monkeypatch):
 
 
 @pytest.mark.parametrize("N", [64, 512])
-def test_folded_slab_reduction_matches_separate(rt, N, monkeypatch):
+def test_folded_slab_reduction_matches_separate(rt, N):
     """The network folds pass 1 of block l+1's slab reduction into block l's
     backward kernel (two slab loads per band and thread, the rest after the
-    last band: N=64 leaves most for that tail).  With ASR_NO_FOLD set every
+    last band: N=64 leaves most for that tail).  With variant ASR_VARIANT_NO_FOLD every
     block's slabs are reduced by its own k_reduce_slabs launch.  Sums in a
     different order: equal to fp32 reduction-order noise (1e-5 of max|g|
     per block); the loss and the non-block gradients are bitwise equal."""
@@ -176,10 +176,10 @@ def test_folded_slab_reduction_matches_separate(rt, N, monkeypatch):
                         dtype="bfloat16", input_u8=True, device=dev)
     loss, g = ex.forward_backward(params, imgs, tgt)
     loss, g = loss.clone(), g.clone()
-    monkeypatch.setenv("ASR_NO_FOLD", "1")
+    ex.variant = rt.ASR_VARIANT_NO_FOLD
     loss1, g1 = ex.forward_backward(params, imgs, tgt)
     loss1, g1 = loss1.clone(), g1.clone()
-    monkeypatch.delenv("ASR_NO_FOLD")
+    ex.variant = 0
     torch.cuda.synchronize()
     assert torch.equal(loss, loss1)
     sizes = [int(np.prod(s)) for s in net_param_shapes(C, L, 3, 10)]
@@ -196,10 +196,10 @@ def test_folded_slab_reduction_matches_separate(rt, N, monkeypatch):
 
 
 @pytest.mark.parametrize("N,u8", [(64, True), (512, True), (64, False)])
-def test_stem_fwd_mfma_matches_fp32_path(rt, N, u8, monkeypatch):
+def test_stem_fwd_mfma_matches_fp32_path(rt, N, u8):
     """The bf16 network's stem forward runs on MFMA (im2col of bf16 (v - mean)
-    from LDS, inv_std * W1 split into bf16 hi + lo); with ASR_STEM_FWD_V1 set
-    it runs the fp32 VALU stem kernel.  Same probabilities to bf16 noise
+    from LDS, inv_std * W1 split into bf16 hi + lo); with variant
+    ASR_VARIANT_STEM_FWD_VALU it runs the fp32 VALU stem kernel.  Same probabilities to bf16 noise
     propagated through the blocks (1e-3 absolute; the stem output itself is
     rounded to bf16 in both)."""
     C, L = 64, 2
@@ -212,9 +212,9 @@ def test_stem_fwd_mfma_matches_fp32_path(rt, N, u8, monkeypatch):
     ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / L, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
                         dtype="bfloat16", input_u8=u8, device=dev)
     p = ex.forward(params, imgs).clone()
-    monkeypatch.setenv("ASR_STEM_FWD_V1", "1")
+    ex.variant = rt.ASR_VARIANT_STEM_FWD_VALU
     p1 = ex.forward(params, imgs).clone()
-    monkeypatch.delenv("ASR_STEM_FWD_V1")
+    ex.variant = 0
     torch.cuda.synchronize()
     a, b = p.cpu().numpy(), p1.cpu().numpy()
     assert np.isfinite(a).all()

@@ -3,13 +3,13 @@ restatement of get_single_block_resnet_build_function + Keras CE + TF1 Adam.
 
 Tolerances: fp32 — probabilities and loss within 1e-5 relative, every
 gradient within 1e-4 of its tensor's max |oracle| value; bf16 — probabilities
-within 2e-2 absolute, loss within 1% relative, gradients: cosine similarity
-with the fp64 oracle >= 0.99 per parameter tensor.
+within 2e-2 absolute, loss within 1% relative, gradients: relative L2
+error vs the fp64 oracle <= 2e-2 per gradient group.
 """
 import numpy as np
 import pytest
 
-from helpers import assert_close
+from helpers import assert_close, assert_grad_groups_rel_l2
 from oracle import asr_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -74,11 +74,7 @@ def test_network_bf16_close(kind, anti):
     assert abs(loss.item() - want_loss) <= 1e-2 * abs(want_loss)
     g_want = O.net_backward(spec, params, cache, onehot)
     g_got = O.unflatten(grads.cpu().numpy().astype(np.float64), [p.shape for p in params])
-    for i, (a, b) in enumerate(zip(g_got, g_want)):
-        if np.abs(b).max() == 0:
-            continue
-        cos = (a * b).sum() / (np.linalg.norm(a) * np.linalg.norm(b) + 1e-30)
-        assert cos >= 0.99, f"grad[{i}] {b.shape}: cosine {cos}"
+    assert_grad_groups_rel_l2(spec, g_got, g_want, 2e-2)
 
 
 def test_network_train_steps_decrease_loss():

@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 LIST=$1; shift
 mkdir -p gpurun_out/ab
 for v in $LIST; do
-  if [ $v = cur ]; then unset ASR_LIB_OVERRIDE; else export ASR_LIB_OVERRIDE=$PWD/build_abl_$v.so; fi
-  timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ab/$v -o run -- python3 tools/blockbench.py --reps 20 "$@" > gpurun_out/ab/$v.log 2>&1 || { echo fail $v; tail gpurun_out/ab/$v.log; exit 1; }
+  if [ $v = cur ]; then LIBARG=""; else LIBARG="--lib $PWD/build_abl_$v.so"; fi
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ab/$v -o run -- python3 tools/blockbench.py --reps 20 $LIBARG "$@" > gpurun_out/ab/$v.log 2>&1 || { echo fail $v; tail gpurun_out/ab/$v.log; exit 1; }
   echo "== $v"; python3 tools/kstats.py gpurun_out/ab/$v/run_kernel_stats.csv 2 | tail -2
 done

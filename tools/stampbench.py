@@ -1,6 +1,6 @@
 """Diagnostic: per-phase cycles of the fused backward from the stamp build.
   tools/build_variants.sh stamp "-DASR_STAMP_BUILD=1"
-  ASR_LIB_OVERRIDE=$PWD/build_abl_stamp.so python3 tools/stampbench.py
+  python3 tools/stampbench.py $PWD/build_abl_stamp.so
 Reads SHARES (the stamps' own waits slow the build), averaged over WGs and
 interior bands."""
 import ctypes as ct
@@ -15,8 +15,8 @@ import torch  # noqa: E402
 from differential_equations_resnet_amd import _lib, runtime as rt  # noqa: E402
 
 WHAT = os.environ.get("STAMP_WHAT", "bwd")
+lib = _lib.load(path=sys.argv[1] if len(sys.argv) > 1 else None)
 dev = rt.require_gpu()
-lib = _lib.load()
 N, H, W, C = 512, 32, 32, 64
 g = torch.Generator(device=dev).manual_seed(0)
 x = torch.randn(N, H, W, C, device=dev, generator=g).to(torch.bfloat16)

@@ -2,7 +2,7 @@
 tools/traffic.sh, corrected as MI355X_MICROARCH.md § HBM prescribes:
 FETCH_SIZE (KiB) counts half the bytes of 16-B/lane streaming reads on
 gfx950 -> x2; WRITE_SIZE (KiB) is exact for 16-B/lane stores.
-usage: traffic.py PMC_DIR CONFIG OUT_JSON"""
+usage: traffic.py PMC_DIR CONFIG OUT_JSON [ROUND_TAG]"""
 import csv
 import glob
 import json
@@ -11,6 +11,7 @@ import sys
 from collections import defaultdict
 
 root, config, out = sys.argv[1], sys.argv[2], sys.argv[3]
+tag = sys.argv[4] if len(sys.argv) > 4 else "?"
 vals = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
@@ -37,7 +38,7 @@ for k, cs in vals.items():
     write = sum(cs["WRITE_SIZE"]) / max(len(cs["WRITE_SIZE"]), 1) * 1024 if "WRITE_SIZE" in cs else 0.0
     per[short] = {"read_bytes": round(fetch), "write_bytes": round(write), "launches": len(cs.get("FETCH_SIZE", []))}
 total = sum(v["read_bytes"] + v["write_bytes"] for v in per.values())
-res = {"config": config, "hbm_bytes_per_block": total, "per_kernel": per,
+res = {"config": config, "round": tag, "hbm_bytes_per_block": total, "per_kernel": per,
        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over tools/blockbench.py "
                  "(one fwd + one bwd per rep); FETCH_SIZE x2 (gfx950 16B/lane read correction), KiB->B"}
 json.dump(res, open(out, "w"), indent=1)
