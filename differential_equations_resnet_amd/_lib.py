@@ -76,6 +76,10 @@ SIGNATURES = [
     ("asr_theta_to_w", _I, [_P, _L, _I, _I, _P, _F, _P, _L, _I, _P]),
     ("asr_conv_forward", _I, [_I, _P, _P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P]),
     ("asr_mask_bytes", _L, [_I, _I, _I, _I]),
+    ("asr_block_stack_forward", _I, [_P, _P, _L, _P, _L, _P, _L, _P, _L, _F, _I, _I, _I, _I, _I, _I, _I, _P]),
+    ("asr_block_stack_backward_workspace_bytes", _S, [_I, _I, _I, _I, _I, _I]),
+    ("asr_block_stack_backward", _I, [_P, _P, _L, _P, _L, _P, _L, _P, _L, _F, _F, _I, _I, _I, _I, _I, _I, _P, _P, _P,
+                                      _S, _P]),
     ("asr_conv_backward_workspace_bytes", _S, [_I, _I, _I, _I, _I]),
     ("asr_conv_backward", _I, [_I, _P, _P, _P, _P, _P, _L, _F, _F, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _S, _P]),
     ("asr_rk2_forward", _I, [_P, _P, _P, _P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P]),

@@ -44,6 +44,14 @@ int stem_fwd_mfma(const void* img, int input_u8, const float* w1, const float* b
                   float mean, float inv_std, int use_norm, void* out, hipStream_t s);
 bool stem_fwd_mfma_supported(int Cin, int H, int W, int C);
 static bool mfma_supported(int C, int W) { return (C == 16 || C == 32 || C == 64) && W == 32; }
+// asr_deep16.hip
+bool deep16_supported(int H, int W, int C);
+int deep16_forward(const void* x0, void* y0, long y_stride, uint8_t* mask0, long mask_stride, const void* wpack,
+                   const float* bias, long bias_stride, float h, int N, int L, bool store_all, hipStream_t s);
+size_t deep16_slab_bytes(int N, int L);
+int deep16_backward(void* dbufA, void* dbufB, const void* xs, long x_stride, const uint8_t* masks, long mask_stride,
+                    const void* wpack, float h, float two_gamma, int N, int L, float* slabs, int* slab_rows,
+                    int* dx0_in_b, hipStream_t s);
 // asr_conv_f32.hip
 int conv_f32(int fmode, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
              float two_gamma, const float* dy, int N, int H, int W, int Ci, int Co, int out_bf16, hipStream_t s,
@@ -299,6 +307,8 @@ struct NetLayout {
   long mask_bytes;
   int act_bytes;
   bool fast_stem;
+  bool deep;          // C=16 stack path: one fused launch forward, one backward (asr_deep16.hip)
+  size_t deep_slabs;  // its weight-gradient slabs [L][rows][E+C]
 };
 
 static int net_check(const asr_net_config* c) {
@@ -339,6 +349,7 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.nparams = L.off_fcb + K;
   L.mask_bytes = asr_mask_bytes(c->N, c->H, c->W, C);
   L.fast_stem = stem_supported(c->Cin, c->H, c->W, C);
+  L.deep = c->dtype == ASR_BF16 && !L.rk2 && deep16_supported(c->H, c->W, C);
   size_t off = 0;
   auto take = [&](size_t bytes) {
     size_t o = off;
@@ -368,6 +379,7 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.slabs2 = take((size_t)L.stages * kMaxSlabsApi * (L.E + C) * 4);  // every other block's slabs
   L.grp_stride = (long)reduce_groups(L.stages * kMaxSlabsApi) * (L.E + C);
   L.grp = take((size_t)c->L * L.grp_stride * 4);
+  L.deep_slabs = take(L.deep ? deep16_slab_bytes(c->N, c->L) : 0);
   L.probs = take((size_t)c->N * K * 4);
   L.loss_per = take((size_t)c->N * 4);
   L.dlogits = take((size_t)c->N * K * 4);
@@ -414,6 +426,11 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
                      W, c->Cin, C, bf ? 1 : 0, s));
   }
   // 3. L Euler blocks (tfkeras_resnets.py:579-582 -> :28-94), or RK2 blocks
+  if (L.deep) {  // C=16: all L steps in one launch, images resident in LDS
+    return deep16_forward(act(0), act(training ? 1 : c->L), L.P, training ? (uint8_t*)(ws + L.masks) : nullptr,
+                          L.mask_bytes, ws + L.wbuf, params + L.off_blk + L.ntheta, L.blk_stride, c->h, N, c->L,
+                          training, s);
+  }
   for (int l = 0; l < c->L; ++l) {
     const float* bias = params + L.off_blk + (long)l * L.blk_stride + L.ntheta;
     const unsigned char* wl = ws + L.wbuf + (size_t)l * L.wstride * L.act_bytes;
@@ -452,12 +469,121 @@ int asr_conv_forward(int mode, const void* x, void* y, uint8_t* mask, const void
   if (dtype == ASR_BF16) {
     if (!mfma_supported(C, W))
       return fail(ASR_E_UNSUPPORTED, "bf16 conv needs C in {16,32,64} and W == 32 (C=%d W=%d)", C, W);
+    if (mode == ASR_MODE_EULER && deep16_supported(H, W, C))
+      return deep16_forward(x, y, 0, mask, 0, w, bias, 0, h, N, 1, true, s);
     return block_fwd_mfma(mode == ASR_MODE_EULER ? 0 : 1, x, nullptr, y, mask, w, bias, h, N, H, W, C, s);
   }
   if (dtype == ASR_F32)
     return conv_f32(mode == ASR_MODE_EULER ? F_EULER : F_CONV, x, y, mask, (const float*)w, bias, h, 0.f, nullptr, N,
                     H, W, C, C, 0, s);
   return fail(ASR_E_ARG, "asr_conv_forward: bad dtype %d", dtype);
+}
+
+int asr_block_stack_forward(const void* x0, void* ys, long y_stride, uint8_t* masks, long mask_stride, const void* w,
+                            long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C,
+                            int L, int dtype, int store_all, asr_stream_t stream) {
+  ASR_TRY(check_shape(N, H, W, C));
+  if (!x0 || !ys || !w || L < 1) return fail(ASR_E_ARG, "asr_block_stack_forward: null pointer or L < 1");
+  if (store_all && L > 1 && y_stride < (long)N * H * W * C)
+    return fail(ASR_E_ARG, "asr_block_stack_forward: y_stride smaller than one activation");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == ASR_BF16 && deep16_supported(H, W, C))
+    return deep16_forward(x0, ys, y_stride, masks, mask_stride, w, bias, bias_stride, h, N, L, store_all != 0, s);
+  if (dtype == ASR_BF16 && !mfma_supported(C, W))
+    return fail(ASR_E_UNSUPPORTED, "bf16 conv needs C in {16,32,64} and W == 32 (C=%d W=%d)", C, W);
+  if (dtype != ASR_F32 && dtype != ASR_BF16) return fail(ASR_E_ARG, "asr_block_stack_forward: bad dtype");
+  const size_t es = dtype == ASR_BF16 ? 2 : 4;
+  if (!store_all && L > 1) return fail(ASR_E_UNSUPPORTED, "asr_block_stack_forward: store_all=0 needs the fused path");
+  for (int l = 0; l < L; ++l) {
+    const void* xi = l == 0 ? x0 : (const unsigned char*)ys + (size_t)(l - 1) * y_stride * es;
+    void* yo = (unsigned char*)ys + (size_t)l * y_stride * es;
+    ASR_TRY(asr_conv_forward(ASR_MODE_EULER, xi, yo, masks ? masks + (size_t)l * mask_stride : nullptr,
+                             (const unsigned char*)w + (size_t)l * w_stride * es, bias ? bias + l * bias_stride : nullptr,
+                             h, N, H, W, C, dtype, stream));
+  }
+  return ASR_OK;
+}
+
+// workspace of asr_block_stack_backward: two dx buffers, then either the
+// fused path's slabs + group rows or one per-block backward workspace
+struct StackWs {
+  size_t da, db, slabs, grp, blk, total;
+  bool deep;
+};
+static StackWs stack_ws_layout(int N, int H, int W, int C, int L, int dtype) {
+  StackWs w{};
+  const size_t act = align_up((size_t)N * H * W * C * (dtype == ASR_BF16 ? 2 : 4), 256);
+  const long ES = 9L * C * C + C;
+  w.deep = dtype == ASR_BF16 && deep16_supported(H, W, C);
+  size_t off = 0;
+  w.da = off;
+  off += act;
+  w.db = off;
+  off += act;
+  if (w.deep) {
+    w.slabs = off;
+    off += align_up(deep16_slab_bytes(N, L), 256);
+    w.grp = off;
+    off += align_up((size_t)L * reduce_groups(kMaxSlabsApi) * ES * 4, 256);
+  } else {
+    w.blk = off;
+    off += bwd_ws_layout(N, H, W, C, dtype).total;
+  }
+  w.total = off;
+  return w;
+}
+
+size_t asr_block_stack_backward_workspace_bytes(int N, int H, int W, int C, int L, int dtype) {
+  if (check_shape(N, H, W, C) != ASR_OK || L < 1) return 0;
+  return stack_ws_layout(N, H, W, C, L, dtype).total;
+}
+
+int asr_block_stack_backward(const void* dyL, const void* xs, long x_stride, const uint8_t* masks, long mask_stride,
+                             const void* w, long w_stride, const int32_t* theta_dst, long n_theta, float h,
+                             float gamma, int N, int H, int W, int C, int L, int dtype, void* dx0, float* dparams,
+                             void* ws, size_t ws_bytes, asr_stream_t stream) {
+  ASR_TRY(check_shape(N, H, W, C));
+  if (!dyL || !xs || !masks || !w || !dx0 || L < 1) return fail(ASR_E_ARG, "asr_block_stack_backward: null pointer");
+  if (dparams && !theta_dst) return fail(ASR_E_ARG, "asr_block_stack_backward: theta_dst needed for dparams");
+  if (dtype != ASR_F32 && dtype != ASR_BF16) return fail(ASR_E_ARG, "asr_block_stack_backward: bad dtype");
+  if (dtype == ASR_BF16 && !mfma_supported(C, W))
+    return fail(ASR_E_UNSUPPORTED, "bf16 conv needs C in {16,32,64} and W == 32 (C=%d W=%d)", C, W);
+  const StackWs Lw = stack_ws_layout(N, H, W, C, L, dtype);
+  if (!ws || ws_bytes < Lw.total) return fail(ASR_E_WORKSPACE, "asr_block_stack_backward: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  unsigned char* base = (unsigned char*)ws;
+  const size_t es = dtype == ASR_BF16 ? 2 : 4, act = (size_t)N * H * W * C * es;
+  const long E = 9L * C * C;
+  if (Lw.deep) {
+    if (w_stride != (long)asr_wpack_elems(C))
+      return fail(ASR_E_ARG, "asr_block_stack_backward: w_stride must be asr_wpack_elems(C) on the fused path");
+    ASR_TRY(hip_check(hipMemcpyAsync(base + Lw.da, dyL, act, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync"));
+    int rows = 0, in_b = 0;
+    float* slabs = (float*)(base + Lw.slabs);
+    ASR_TRY(deep16_backward(base + Lw.da, base + Lw.db, xs, x_stride, masks, mask_stride, w, h, 2.f * gamma, N, L,
+                            slabs, &rows, &in_b, s));
+    ASR_TRY(hip_check(hipMemcpyAsync(dx0, base + (in_b ? Lw.db : Lw.da), act, hipMemcpyDeviceToDevice, s),
+                      "hipMemcpyAsync"));
+    if (dparams) {
+      const int G = reduce_groups(rows);
+      ASR_TRY(reduce_slabs_to_groups(slabs, L * rows, E + C, (float*)(base + Lw.grp), s));
+      ASR_TRY(project_layers((float*)(base + Lw.grp), (long)G * (E + C), G, E, C, theta_dst, n_theta, L, dparams,
+                             n_theta + C, s));
+    }
+    return ASR_OK;
+  }
+  // per-block kernels, last block first
+  const void* dcur = dyL;
+  for (int l = L - 1; l >= 0; --l) {
+    void* dnext = l == 0 ? dx0 : base + ((l & 1) ? Lw.db : Lw.da);
+    float* dp = dparams ? dparams + (long)l * (n_theta + C) : nullptr;
+    ASR_TRY(conv_backward_impl(ASR_MODE_EULER, dcur, (const unsigned char*)xs + (size_t)l * x_stride * es,
+                               masks + (size_t)l * mask_stride, (const unsigned char*)w + (size_t)l * w_stride * es,
+                               theta_dst, n_theta, h, gamma, N, H, W, C, dtype, dnext, dp, dp ? dp + n_theta : nullptr,
+                               nullptr, base + Lw.blk, s));
+    dcur = dnext;
+  }
+  return ASR_OK;
 }
 
 size_t asr_conv_backward_workspace_bytes(int N, int H, int W, int C, int dtype) {
@@ -600,7 +726,19 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   float* pend_grp = nullptr;
   const bool fold_on = !(cfg->variant & ASR_VARIANT_NO_FOLD);               // else the reduction as separate launches
   const bool stem_v1 = (cfg->variant & ASR_VARIANT_STEM_WGRAD_VALU) != 0;  // fp32 VALU stem wgrad
-  for (int l = cfg->L - 1; l >= 0; --l) {
+  if (L.deep) {  // C=16: all L blocks in one launch (dx resident in LDS), one slab set per layer
+    int rows = 0, in_b = 0;
+    float* slabs = (float*)(b + L.deep_slabs);
+    ASR_TRY(deep16_backward(dcur, dnext, act(0), L.P, (const uint8_t*)(b + L.masks), L.mask_bytes,
+                            b + (L.sep_bwd ? L.wbuf_bwd : L.wbuf), cfg->h, L.sep_bwd ? 0.f : 2.f * cfg->gamma, N,
+                            cfg->L, slabs, &rows, &in_b, s));
+    if (in_b) std::swap(dcur, dnext);
+    const int G = reduce_groups(rows);
+    ASR_TRY(reduce_slabs_to_groups(slabs, cfg->L * rows, L.E + C, (float*)(b + L.grp), s));
+    ASR_TRY(project_layers((float*)(b + L.grp), (long)G * (L.E + C), G, L.E, C, theta_dst, L.ntheta, cfg->L,
+                           grads + L.off_blk, L.blk_stride, s));
+  }
+  for (int l = L.deep ? -1 : cfg->L - 1; l >= 0; --l) {
     const unsigned char* wl = b + (L.sep_bwd ? L.wbuf_bwd : L.wbuf) + (size_t)l * L.wstride * L.act_bytes;
     const uint8_t* mask = (const uint8_t*)(b + L.masks) + (size_t)l * L.mask_bytes;
     const float gam = L.sep_bwd ? 0.f : cfg->gamma;
@@ -631,8 +769,9 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   }
   if (pend_P > 0) ASR_TRY(reduce_slabs_to_groups(pend_slabs, pend_P, L.E + C, pend_grp, s));
   // pass 2 of every block's weight-gradient reduction + projection onto theta, one launch
-  ASR_TRY(project_layers((float*)(b + L.grp), L.grp_stride, reduce_groups(nsl_blk), L.E, C, theta_dst, L.ntheta,
-                         cfg->L, grads + L.off_blk, L.blk_stride, s));
+  if (!L.deep)
+    ASR_TRY(project_layers((float*)(b + L.grp), L.grp_stride, reduce_groups(nsl_blk), L.E, C, theta_dst, L.ntheta,
+                           cfg->L, grads + L.off_blk, L.blk_stride, s));
   // stem: dz1 = dx1 * [x1 > 0]; conv1 weight/bias gradient from the normalised input
   const long E1 = 9L * cfg->Cin * C;
   unsigned char* sw = b + L.bwdws;

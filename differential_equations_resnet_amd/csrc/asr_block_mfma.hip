@@ -30,6 +30,7 @@
 #include <type_traits>
 
 #include "asr_common.h"
+#include "asr_device.h"
 
 #ifndef ASR_BWD_DGRAD_DMA_PCT
 #define ASR_BWD_DGRAD_DMA_PCT 75  // share of the backward's prefetch DMAs issued by the dgrad waves
@@ -45,9 +46,6 @@
 #endif
 #ifndef ASR_V2_SPREAD
 #define ASR_V2_SPREAD 0  // v2 backward: dgrad waves issue one dy DMA every N conv k-steps (0: one burst after the barrier)
-#endif
-#ifndef ASR_DMA_M0_CLOBBER
-#define ASR_DMA_M0_CLOBBER 1  // LDS-DMA: declare M0 clobbered instead of saving/restoring it per DMA
 #endif
 #ifndef ASR_V2_ST16
 #define ASR_V2_ST16 1  // v2 backward: dx as 16-B stores (row swap between the two o-tiles)
@@ -126,42 +124,6 @@ __device__ __forceinline__ int toff(int row, int col, int q, int TW) {
   return ((row * TW + col) * Geo<C>::NQ + (q ^ Geo<C>::swz(col))) * 16;
 }
 
-__device__ __attribute__((aligned(16))) uint4 g_zero_page[64];  // 1 KiB of zeros (DMA source for padding)
-
-typedef const __attribute__((address_space(1))) void* gptr_t;
-typedef __attribute__((address_space(3))) void* lptr_t;
-
-// One 1 KiB LDS-DMA (16 B per lane, lane-linear at the LDS address).  Inline
-// asm, not the builtin: the compiler would otherwise wait vmcnt(0) before
-// every later LDS read of the wave (it cannot tell the DMA's destination
-// apart), serialising the prefetch with the compute.  Every reader of DMA'd
-// data waits with a counted barrier_vm / vm_wait instead.  M0 is reserved
-// by the compiler, so it is saved and restored around the DMA.
-__device__ __forceinline__ void dma16(const void* src, unsigned char* lds_wave_base) {
-  const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)((ASR_LDS unsigned char*)lds_wave_base));
-#if ASR_DMA_M0_CLOBBER
-  // M0 declared clobbered: the compiler re-establishes it only where it uses it
-  asm volatile(
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %0, off"
-      :
-      : "v"(src), "s"(l)
-      : "memory", "m0");
-#else
-  unsigned sv;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(sv)
-      : "v"(src), "s"(l)
-      : "memory");
-#endif
-}
-
 // DMA image rows [gy0, gy0+nrows) of image n (rows outside [0,H) -> zeros) into
 // tile rows [0, nrows), interior columns 1..W.  One instruction = PPI pixels.
 // The lane's source offset inside a PPI-pixel segment does not depend on the
@@ -233,24 +195,6 @@ __device__ __forceinline__ void dma_mask_rows(const uint8_t* __restrict__ mask, 
     dma_mask_instr<C, W>(mask, mt, n, gy0, nrows, j, H, lane);
 }
 
-// Workgroup barrier that waits only for this wave's vector-memory ops OLDER
-// than its `n` youngest (vmcnt counts loads, stores and LDS-DMA in issue
-// order).  Used so that the barrier guarding an LDS-DMA'd buffer does not
-// also wait for the global stores issued after that DMA.
-__device__ __forceinline__ void barrier_vm(int n) {
-#define ASR_BVM(k) \
-  case k: asm volatile("s_waitcnt vmcnt(" #k ") lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
-  switch (n) {
-    ASR_BVM(1) ASR_BVM(2) ASR_BVM(3) ASR_BVM(4) ASR_BVM(5) ASR_BVM(6) ASR_BVM(7) ASR_BVM(8)
-    ASR_BVM(9) ASR_BVM(10) ASR_BVM(11) ASR_BVM(12) ASR_BVM(13) ASR_BVM(14) ASR_BVM(15) ASR_BVM(16)
-    ASR_BVM(17) ASR_BVM(18) ASR_BVM(19) ASR_BVM(20) ASR_BVM(21) ASR_BVM(22) ASR_BVM(23) ASR_BVM(24)
-    default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
-  }
-#undef ASR_BVM
-}
-// barrier for LDS data only (in-flight DMA and stores keep flying)
-__device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
 // zero the halo columns (0 and W+1) of a tile with `rows` rows
 template <int C, int W>
 __device__ __forceinline__ void zero_halo_cols(unsigned char* tile, int rows, int tid, int nthreads) {
@@ -298,73 +242,6 @@ struct Frag {
     else return pt * 16 * NQ * 16;
   }
 };
-
-__device__ __forceinline__ unsigned lds_u32(const void* p) {
-  return (unsigned)(uintptr_t)((ASR_LDS const unsigned char*)p);
-}
-
-// Hand-scheduled LDS reads (hipcc would otherwise wait lgkmcnt(0) on the
-// just-issued prefetch): "=v" output + explicit counted wait +
-// sched_barrier (cdna_hip_programming.md §5.7, rule 18).
-template <int OFF>
-__device__ __forceinline__ bf16x8 ds_read128(unsigned addr) {
-  bf16x8 v;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
-  return v;
-}
-template <int N>
-__device__ __forceinline__ void lgkm_wait() {
-  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N) : "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-// LDS accesses the compiler must not order behind in-flight LDS-DMA: hipcc
-// waits vmcnt(0) before any plain LDS access while a global_load_lds is
-// outstanding (it cannot tell the DMA's destination buffer apart), which
-// would serialise the next band's prefetch with this band's work.  The
-// caller waits lgkmcnt itself (lgkm_wait) before using a read result.
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ u32x4 lds_rd128(unsigned addr) {
-  u32x4 v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
-  return v;
-}
-__device__ __forceinline__ u32x2 lds_rd64(unsigned addr) {
-  u32x2 v;
-  asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(addr));
-  return v;
-}
-__device__ __forceinline__ unsigned lds_rd_u8(unsigned addr) {
-  unsigned v;
-  asm volatile("ds_read_u8 %0, %1" : "=v"(v) : "v"(addr));
-  return v;
-}
-__device__ __forceinline__ void lds_wr128(unsigned addr, u32x4 v) {
-  asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
-}
-
-// Wait until at most n of this wave's vector-memory ops are outstanding
-// (vmcnt retires in issue order): used for LDS-DMA'd data the compiler does
-// not track.  n above 24 waits for more than needed, which stays correct.
-__device__ __forceinline__ void vm_wait(int n) {
-#define ASR_VMW(k) \
-  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-  switch (n) {
-    ASR_VMW(1) ASR_VMW(2) ASR_VMW(3) ASR_VMW(4) ASR_VMW(5) ASR_VMW(6) ASR_VMW(7) ASR_VMW(8)
-    ASR_VMW(9) ASR_VMW(10) ASR_VMW(11) ASR_VMW(12) ASR_VMW(13) ASR_VMW(14) ASR_VMW(15) ASR_VMW(16)
-    ASR_VMW(17) ASR_VMW(18) ASR_VMW(19) ASR_VMW(20) ASR_VMW(21) ASR_VMW(22) ASR_VMW(23) ASR_VMW(24)
-    default:
-      if (n > 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // waits for more: still correct
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      break;
-  }
-#undef ASR_VMW
-}
-// instructions one wave issues in a `for (j = wave; j < total; j += nw)` loop
-__device__ __forceinline__ int strided_count(int total, int wave, int nw) {
-  return total > wave ? (total - wave + nw - 1) / nw : 0;
-}
 
 template <int C, int W, int ks>
 __device__ __forceinline__ void conv_issue(const unsigned (&ra)[Frag<C, W>::NB], bf16x8 (&B)[W / 16]) {
@@ -933,14 +810,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
 // ===========================================================================
 // fused backward
 // ===========================================================================
-__device__ __forceinline__ bf16x8 tr_pair(const unsigned char* p0, const unsigned char* p1) {
-  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ASR_LDS s16x4*)p0);
-  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ASR_LDS s16x4*)p1);
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
-  s16x8 c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-  return *(bf16x8*)&c;
-}
-
 template <int C, int W, int BR>
 struct BwdLds {
   static constexpr int TW = W + 2;

@@ -18,7 +18,7 @@ from ._lib import (ASR_BF16, ASR_F32, ASR_INTEGRATOR_EULER, ASR_INTEGRATOR_RK2, 
 
 __all__ = [
     "require_gpu", "dtype_code", "torch_dtype", "ParamMap", "param_map", "theta_count", "theta_to_w",
-    "conv_forward", "conv_backward", "rk2_forward", "rk2_backward", "integrator_code", "NetExecutor", "adam_update",
+    "conv_forward", "block_stack_forward", "block_stack_backward", "conv_backward", "rk2_forward", "rk2_backward", "integrator_code", "NetExecutor", "adam_update",
 ]
 
 
@@ -186,6 +186,50 @@ def conv_forward(mode: int, x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor
     y = torch.empty_like(x)
     _lib.call("asr_conv_forward", mode, _p(x), _p(y), _p(mask), _p(w), _p(bias), float(h), N, H, W, C, dt, _stream())
     return y
+
+
+def block_stack_forward(x0: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, h: float, store_all=True,
+                        want_masks=True):
+    """L Euler blocks (asr_block_stack_forward).  w: [L, per-layer W] as
+    theta_to_w(..., layers=L) returns; bias: [L, C] float32 or None.
+    Returns (ys [L,N,H,W,C] with ys[l] = x_{l+1}, masks [L, mask_bytes]) or,
+    with store_all=False, (x_L, None)."""
+    N, H, W, C = x0.shape
+    dt = dtype_code(x0.dtype)
+    L = int(w.shape[0])
+    if not x0.is_contiguous():
+        raise ValueError("x0 must be contiguous NHWC")
+    P = N * H * W * C
+    ys = torch.empty((L if store_all else 1, N, H, W, C), dtype=x0.dtype, device=x0.device)
+    mb = mask_bytes(N, H, W, C)
+    masks = torch.zeros(L, mb, dtype=torch.uint8, device=x0.device) if (want_masks and store_all) else None
+    if bias is not None and (tuple(bias.shape) != (L, C) or bias.dtype != torch.float32 or not bias.is_contiguous()):
+        raise ValueError(f"bias must be contiguous float32 [{L}, {C}]")
+    per = w[0].numel()
+    _lib.call("asr_block_stack_forward", _p(x0), _p(ys), P, _p(masks), mb, _p(w), per, _p(bias), C, float(h), N, H, W,
+              C, L, dt, int(bool(store_all)), _stream())
+    return (ys, masks) if store_all else (ys[0], None)
+
+
+def block_stack_backward(dyL, x0, ys, masks, w, pmap: ParamMap, h: float, gamma: float, want_dparams=True):
+    """Backward of block_stack_forward (asr_block_stack_backward): returns
+    (dx0, dparams [L, n_theta + C] or None).  The inputs of the L blocks are
+    x0, ys[0], ..., ys[L-2]; they are passed as one [L, N, H, W, C] stack."""
+    L = int(w.shape[0])
+    N, H, W, C = x0.shape
+    dt = dtype_code(x0.dtype)
+    xs = torch.cat([x0.unsqueeze(0), ys[:L - 1]]) if L > 1 else x0.unsqueeze(0)
+    xs = xs.contiguous()
+    P = N * H * W * C
+    mb = mask_bytes(N, H, W, C)
+    wsb = int(_lib.load().asr_block_stack_backward_workspace_bytes(N, H, W, C, L, dt))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=x0.device)
+    dx0 = torch.empty_like(x0)
+    dparams = torch.empty(L, pmap.n_theta + C, dtype=torch.float32, device=x0.device) if want_dparams else None
+    _, theta_dst = pmap.device(x0.device)
+    _lib.call("asr_block_stack_backward", _p(dyL), _p(xs), P, _p(masks), mb, _p(w), w[0].numel(), _p(theta_dst),
+              pmap.n_theta, float(h), float(gamma), N, H, W, C, L, dt, _p(dx0), _p(dparams), _p(ws), wsb, _stream())
+    return dx0, dparams
 
 
 def mask_bytes(N: int, H: int, W: int, C: int) -> int:

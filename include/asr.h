@@ -141,6 +141,32 @@ long asr_mask_bytes(int N, int H, int W, int C);
  * dtheta / dbias / dx may be NULL to skip that output; dw_hwio (float
  * [3][3][C][C], may be NULL) receives the unprojected dW.
  * ws: caller workspace of asr_conv_backward_workspace_bytes bytes. */
+/* A stack of L Euler blocks in one call (the deep-stack path, BASELINE
+ * config C3: single_layer_identity_block applied L times,
+ * tfkeras_resnets.py:579-582).  Layer l reads x_l (x0 for l = 0) and writes
+ * x_{l+1} to ys + l*y_stride elements and its relu mask to masks +
+ * l*mask_stride bytes (masks may be NULL); with store_all == 0 only x_L is
+ * written, to ys.  w: layer l's asr_theta_to_w output at w + l*w_stride
+ * elements; bias: layer l's at bias + l*bias_stride (may be NULL).  bf16 at
+ * C=16, H=W=32 runs all L steps in one launch with every image resident in
+ * LDS; other shapes run the per-block kernels in sequence. */
+int asr_block_stack_forward(const void* x0, void* ys, long y_stride, uint8_t* masks, long mask_stride,
+                            const void* w, long w_stride, const float* bias, long bias_stride, float h,
+                            int N, int H, int W, int C, int L, int dtype, int store_all, asr_stream_t stream);
+
+/* Backward of asr_block_stack_forward over all L blocks: dyL = dL/dx_L;
+ * xs: x_l at xs + l*x_stride elements (x_0 first, i.e. the stack's input
+ * followed by its stored outputs); masks / w as the forward.  dx0 receives
+ * dL/dx_0; dparams (may be NULL) layer l's [dtheta (n_theta) | dbias (C)] at
+ * dparams + l*(n_theta + C), projected through theta_dst.  bf16 at C=16,
+ * H=W=32 runs one fused launch with dx resident in LDS (w_stride must be
+ * asr_wpack_elems(16)); other shapes run asr_conv_backward per block. */
+size_t asr_block_stack_backward_workspace_bytes(int N, int H, int W, int C, int L, int dtype);
+int asr_block_stack_backward(const void* dyL, const void* xs, long x_stride, const uint8_t* masks, long mask_stride,
+                             const void* w, long w_stride, const int32_t* theta_dst, long n_theta, float h,
+                             float gamma, int N, int H, int W, int C, int L, int dtype, void* dx0, float* dparams,
+                             void* ws, size_t ws_bytes, asr_stream_t stream);
+
 size_t asr_conv_backward_workspace_bytes(int N, int H, int W, int C, int dtype);
 int asr_conv_backward(int mode, const void* dy, const void* x, const uint8_t* mask,
                       const void* w, const int32_t* theta_dst, long n_theta, float h,
