@@ -168,226 +168,277 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
 // accumulate in registers over all images of the workgroup, so each layer
 // gets ONE slab [dW (9*16*16) | db (16)] fp32 per workgroup (the layout
 // asr_api's reduce_slabs_to_groups / project_layers consume), and dx crosses
-// HBM only at segment boundaries.  x_{l-1} and mask_{l-1} are DMA'd into the
-// second buffers while layer l computes.
+// HBM only at segment boundaries.
 //
-// dgrad: the forward's implicit GEMM with dzm in place of x (bitwise the
-// per-block kernel's dx).  wgrad: GEMM with M = tap-channel (16 per m-tile:
-// one tap), N = o, K = pixels (one image row of 32 per k-step); both operands
-// by ds_read_b64_tr_b16 (T10) from the x tile (shifted by the tap) and the dz
-// tile.  The 8 k-rows of lane group g are pixels 8g + 4*(hh ^ (g & 1)) + q for
-// the two reads hh: the halves of odd groups are swapped so the two 16-lane
-// groups of each 32-lane half read disjoint banks.
+// One 512-thread workgroup per CU, two waves per SIMD with split roles:
+//   waves 0-3 (dgrad): image rows [8w, 8w+8): the forward's implicit GEMM on
+//     dzm (bitwise the per-block kernel's dx), dx updated in place, db;
+//   waves 4-6 (wgrad): tap column kx = w-4 of all 32 rows: a GEMM with M = the
+//     tap's 16 input channels, N = o, K = the 32 pixels of a row.  The x
+//     fragment of tile row ir (ds_read_b64_tr_b16, T10) serves the three taps
+//     (ky, kx) of output rows ir - ky, so every x row is read once per wave;
+//     the dz fragments of the last three rows stay in registers.  The 8
+//     k-pixels of lane group g are 8g + 4*(hh ^ (g & 1)) + q for the two reads
+//     hh: odd groups swap halves, so the two 16-lane groups of each 32-lane
+//     half read disjoint banks;
+//   wave 7 DMAs x_{l-1} and mask_{l-1} into the second buffers meanwhile.
+// All 8 waves build dzm (phase 1) between two barriers.
 // LDS: dx (32 KiB) | dz tile | 2 x tiles | 2 x 2 KiB masks | 4 KiB mask table.
 // ---------------------------------------------------------------------------
-constexpr int KSEG = 6;                  // layers per segment (dW accumulators in registers)
+constexpr int KSEG = 12;                 // layers per segment (dW accumulators in registers)
+constexpr int NWB = 8;                   // waves per backward workgroup
 constexpr int ES = 9 * C * C + C;        // slab floats per layer
 constexpr int DXB = H * W * C * 2;       // 32 KiB
 constexpr int MB = H * W * C / 8;        // 2 KiB of relu bits per image
 constexpr int L_DX = 0, L_DZ = L_DX + DXB, L_X = L_DZ + TILE, L_M = L_X + 2 * TILE, L_TAB = L_M + 2 * MB;
 constexpr int L_TOTAL = L_TAB + 4096;
 static_assert(L_TOTAL <= 160 * 1024, "LDS budget");
-static_assert(4 * 9 * 4 * 64 * 4 + 4 * C * 4 <= 2 * TILE, "segment-end reduction area");
 
-__device__ __forceinline__ bf16x8 tr2(const unsigned char* base, unsigned o0, unsigned o1) {
-  return tr_pair(base + o0, base + o1);
+// f(integral_constant<int, k>) for k = K .. N-1: compile-time register-array
+// indices (a runtime index would put the array in scratch memory)
+template <int K, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (K < N) {
+    f(std::integral_constant<int, K>{});
+    static_for<K + 1, N>(f);
+  }
 }
 
-__global__ __launch_bounds__(64 * NWAVE, 1) void k_bwd16_fused(bf16* __restrict__ dbufA, bf16* __restrict__ dbufB,
-                                                              const bf16* __restrict__ xs, long x_stride,
-                                                              const uint8_t* __restrict__ masks, long mask_stride,
-                                                              const bf16* __restrict__ wpack, float h, float two_gamma,
-                                                              int N, int L, float* __restrict__ slabs, int PS) {
+__device__ __forceinline__ bf16x8 tr2(const unsigned char* base, const unsigned (&o)[2]) {
+  return tr_pair(base + o[0], base + o[1]);
+}
+
+__global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ dbufA, bf16* __restrict__ dbufB,
+                                                            const bf16* __restrict__ xs, long x_stride,
+                                                            const uint8_t* __restrict__ masks, long mask_stride,
+                                                            const bf16* __restrict__ wpack, float h, float two_gamma,
+                                                            int N, int L, float* __restrict__ slabs, int PS) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, lx = lane & 15, q = lx >> 2, p = lx & 3;
-  const int r0 = wave * RPW;
   const int P = gridDim.x, b = blockIdx.x;
-  const float hs2g = h * two_gamma;
   // zero the dz tile and both x tiles (halo rows / columns stay zero), build the mask table
-  for (int i = tid; i < 3 * TILE / 16; i += 64 * NWAVE) ((uint4*)(lds + L_DZ))[i] = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < 3 * TILE / 16; i += 64 * NWB) ((uint4*)(lds + L_DZ))[i] = make_uint4(0, 0, 0, 0);
   {
     unsigned* tab = (unsigned*)(lds + L_TAB);  // dword d of byte m: 0xffff per set bit of (m >> 2d) & 3
-    for (int i = tid; i < 1024; i += 64 * NWAVE) {
+    for (int i = tid; i < 1024; i += 64 * NWB) {
       const unsigned m = (unsigned)i >> 2, d = (unsigned)i & 3;
       tab[i] = (((m >> (2 * d)) & 1u) ? 0xffffu : 0u) | (((m >> (2 * d + 1)) & 1u) ? 0xffff0000u : 0u);
     }
   }
-  unsigned boff[KS];  // dgrad B (dz tile), as the forward
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    const int tap = min(2 * ks + (g >> 1), 8);
-    boff[ks] = (unsigned)(((tap / 3) * TW + tap % 3 + lx) * 32 + (g & 1) * 16);
-  }
-  const unsigned zoff = (unsigned)((TW + 1 + lx) * 32 + 8 * g);  // dz interior value of the D layout
-  const unsigned doff = (unsigned)(lx * 32 + 8 * g);              // dx (no halo) of the D layout
-  unsigned toff2[2];  // wgrad tr-read lane offsets (pixel 8g + 4*(hh ^ (g&1)) + q, channels 4p..4p+3)
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh) toff2[hh] = (unsigned)((8 * g + 4 * (hh ^ (g & 1)) + q) * 32 + 8 * p);
   __syncthreads();
-
-  f32x4 acc[KSEG][9];
-  float dbacc[KSEG][4];
   const int nseg = (L + KSEG - 1) / KSEG;
-  for (int sg = 0; sg < nseg; ++sg) {
-    const int ltop = L - 1 - sg * KSEG, kcount = min(KSEG, ltop + 1);
-    const bf16* din = (sg & 1) ? dbufB : dbufA;
-    bf16* dout = (sg & 1) ? dbufA : dbufB;
-#pragma unroll
-    for (int k = 0; k < KSEG; ++k) {
-#pragma unroll
-      for (int t = 0; t < 9; ++t) acc[k][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) dbacc[k][e] = 0.f;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+
+  // ---- role-independent steps (every wave takes part; identical barrier sequence) ----
+  // dx at the segment top, x_ltop and mask_ltop of image n: 66 DMAs dealt round-robin
+  auto stage = [&](const bf16* din, long img, int ltop, int n) {
+    const unsigned char* ds = (const unsigned char*)(din + img);
+    const unsigned char* xsrc = (const unsigned char*)(xs + ltop * x_stride + img);
+    for (int j = wv; j < 66; j += NWB) {
+      if (j < 32) dma16(ds + j * 1024 + lane * 16, lds + L_DX + j * 1024);
+      else if (j < 64) dma16(xsrc + (j - 32) * 1024 + lane * 16, lds + L_X + (j - 31) * ROWB + 32);
+      else dma16(masks + ltop * mask_stride + (long)n * MB + (j - 64) * 1024 + lane * 16, lds + L_M + (j - 64) * 1024);
     }
-    for (int n = b; n < N; n += P) {
-      const long img = (long)n * H * W * C;
-      // stage dx at the segment top, x_ltop and mask_ltop
-      {
-        const unsigned char* ds = (const unsigned char*)(din + img);
-        const unsigned char* xsrc = (const unsigned char*)(xs + ltop * x_stride + img);
+  };
+  // phase 1: dzm = dx & mask (cur mask buffer) for the whole image, 4 chunks per thread
+  auto build_dz = [&](int cur) {
+    const unsigned char* mt = lds + L_M + cur * MB;
 #pragma unroll
-        for (int k = 0; k < RPW; ++k) {
-          const int r = r0 + k;
-          dma16(ds + r * 1024 + lane * 16, lds + L_DX + r * 1024);
-          dma16(xsrc + r * 1024 + lane * 16, lds + L_X + (r + 1) * ROWB + 32);
-        }
-        if (wave < 2) dma16(masks + ltop * mask_stride + (long)n * MB + wave * 1024 + lane * 16, lds + L_M + wave * 1024);
-      }
-      bf16x8 A[KS], An[KS];
-      load_wt(wpack + (long)ltop * WSTRIDE, lane, A);
-      barrier_vm(0);
+    for (int j = 0; j < 4; ++j) {
+      const int c = tid + 64 * NWB * j;
+      const int r = c >> 6, px = (c & 63) >> 1, hc = c & 1;
+      const uint4 dv = *(const uint4*)(lds + L_DX + (r * W + px) * 32 + hc * 16);
+      const unsigned mb = mt[(r * W + px) * 2 + hc];
+      const uint4 mv = *(const uint4*)(lds + L_TAB + mb * 16);
+      *(uint4*)(lds + L_DZ + ((r + 1) * TW + px + 1) * 32 + hc * 16) =
+          make_uint4(dv.x & mv.x, dv.y & mv.y, dv.z & mv.z, dv.w & mv.w);
+    }
+  };
+  auto store_dx = [&](bf16* dout, long img) {
+    unsigned char* dst = (unsigned char*)(dout + img);
 #pragma unroll
-      for (int k = 0; k < KSEG; ++k) {
-        if (k >= kcount) break;
-        const int l = ltop - k, cur = k & 1;
-        const bool more = k + 1 < kcount;
-        unsigned char* xt = lds + L_X + cur * TILE;
-        const unsigned char* mt = lds + L_M + cur * MB;
-        if (more) {  // x_{l-1}, mask_{l-1} into the other buffers; W of layer l-1
-          const unsigned char* xsrc = (const unsigned char*)(xs + (l - 1) * x_stride + img);
+    for (int j = 0; j < 4; ++j) {
+      const int o = (tid + j * 64 * NWB) * 16;
+      *(uint4*)(dst + o) = *(const uint4*)(lds + L_DX + o);
+    }
+  };
+  float* dbr = (float*)(lds + L_DZ + (TW + 1) * 32);  // [4][C] db partials (dz interior, free at segment end)
+
+  if (wave < 4) {
+    // ------------------------------ dgrad waves ------------------------------
+    const int r0 = wave * RPW;
+    const float hs2g = h * two_gamma;
+    unsigned boff[KS];
 #pragma unroll
-          for (int kk = 0; kk < RPW; ++kk) {
-            const int r = r0 + kk;
-            dma16(xsrc + r * 1024 + lane * 16, lds + L_X + (cur ^ 1) * TILE + (r + 1) * ROWB + 32);
-          }
-          if (wave < 2)
-            dma16(masks + (l - 1) * mask_stride + (long)n * MB + wave * 1024 + lane * 16,
-                  lds + L_M + (cur ^ 1) * MB + wave * 1024);
-          load_wt(wpack + (long)(l - 1) * WSTRIDE, lane, An);
-        }
-        // phase 1: dzm = dx & mask for the wave's rows (16-B chunks)
+    for (int ks = 0; ks < KS; ++ks) {
+      const int tap = min(2 * ks + (g >> 1), 8);
+      boff[ks] = (unsigned)(((tap / 3) * TW + tap % 3 + lx) * 32 + (g & 1) * 16);
+    }
+    const unsigned zoff = (unsigned)((TW + 1 + lx) * 32 + 8 * g);  // dz interior value of the D layout
+    const unsigned doff = (unsigned)(lx * 32 + 8 * g);              // dx (no halo) of the D layout
+    float dbacc[KSEG][4];
+    for (int sg = 0; sg < nseg; ++sg) {
+      const int ltop = L - 1 - sg * KSEG, kcount = min(KSEG, ltop + 1);
+      const bf16* din = (sg & 1) ? dbufB : dbufA;
+      bf16* dout = (sg & 1) ? dbufA : dbufB;
+#pragma unroll
+      for (int k = 0; k < KSEG; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dbacc[k][e] = 0.f;
+      for (int n = b; n < N; n += P) {
+        const long img = (long)n * H * W * C;
+        stage(din, img, ltop, n);
+        bf16x8 A[KS], An[KS];
+        load_wt(wpack + (long)ltop * WSTRIDE, lane, A);
+        barrier_vm(0);
+        static_for<0, KSEG>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          if (k >= kcount) return;
+          const int l = ltop - k;
+          const bool more = k + 1 < kcount;
+          if (more) load_wt(wpack + (long)(l - 1) * WSTRIDE, lane, An);
+          build_dz(k & 1);
+          barrier_lds();  // dzm complete (the prefetch DMA keeps flying)
 #pragma unroll 2
-        for (int j = 0; j < RPW; ++j) {
-          const int r = r0 + j, px = lane >> 1, hc = lane & 1;
-          const unsigned char* dsrc = lds + L_DX + (r * W + px) * 32 + hc * 16;
-          const uint4 dv = *(const uint4*)dsrc;
-          const unsigned mb = mt[(r * W + px) * 2 + hc];
-          const uint4 mv = *(const uint4*)(lds + L_TAB + mb * 16);
-          *(uint4*)(lds + L_DZ + ((r + 1) * TW + px + 1) * 32 + hc * 16) =
-              make_uint4(dv.x & mv.x, dv.y & mv.y, dv.z & mv.z, dv.w & mv.w);
-        }
-        barrier_lds();  // dz complete (the prefetch DMA keeps flying)
-        // phase 2a: dgrad over the wave's rows, dx updated in place, db
-#pragma unroll 1
-        for (int j = 0; j < RPW; ++j) {
-          const int r = r0 + j;
+          for (int j = 0; j < RPW; ++j) {
+            const int r = r0 + j;
+            const unsigned char* tb = lds + L_DZ + r * ROWB;
+            bf16x8 B0[KS], B1[KS];
 #pragma unroll
-          for (int pt = 0; pt < 2; ++pt) {
-            const unsigned char* tb = lds + L_DZ + r * ROWB + pt * 512;
-            bf16x8 B[KS];
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) B[ks] = *(const bf16x8*)(tb + boff[ks]);
-            f32x4 c = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], B[ks], c, 0, 0, 0);
-            const bf16x4 zr = *(const bf16x4*)(tb + zoff);
-            unsigned char* dxp = lds + L_DX + (r * W + 16 * pt) * 32 + doff;
-            const bf16x4 dr = *(const bf16x4*)dxp;
-            bf16x4 o4;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float zf = (float)zr[e];
-              dbacc[k][e] += zf;
-              const float v = fmaf(-h, c[e], (float)dr[e]);
-              o4[e] = (bf16)(hs2g != 0.f ? fmaf(hs2g, zf, v) : v);
+            for (int ks = 0; ks < KS; ++ks) {
+              B0[ks] = *(const bf16x8*)(tb + boff[ks]);
+              B1[ks] = *(const bf16x8*)(tb + 512 + boff[ks]);
             }
-            *(bf16x4*)dxp = o4;
+            f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+              c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], B0[ks], c0, 0, 0, 0);
+              c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], B1[ks], c1, 0, 0, 0);
+            }
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt) {
+              const f32x4 c = pt ? c1 : c0;
+              const bf16x4 zr = *(const bf16x4*)(tb + pt * 512 + zoff);
+              unsigned char* dxp = lds + L_DX + (r * W + 16 * pt) * 32 + doff;
+              const bf16x4 dr = *(const bf16x4*)dxp;
+              bf16x4 o4;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float zf = (float)zr[e];
+                dbacc[k][e] += zf;
+                const float v = fmaf(-h, c[e], (float)dr[e]);
+                o4[e] = (bf16)(hs2g != 0.f ? fmaf(hs2g, zf, v) : v);
+              }
+              *(bf16x4*)dxp = o4;
+            }
           }
-        }
-        // phase 2b: wgrad over the wave's rows (one k-step of 32 pixels per row)
-#pragma unroll 1
-        for (int j = 0; j < RPW; ++j) {
-          const int r = r0 + j;
-          const unsigned char* zrow = lds + L_DZ + (r + 1) * ROWB + 32;  // interior pixel 0 of row r
-          const bf16x8 Bz = tr2(zrow, toff2[0], toff2[1]);
+          if (more) {
 #pragma unroll
-          for (int tap = 0; tap < 9; ++tap) {
-            const unsigned char* xrow = xt + (r + tap / 3) * ROWB + (tap % 3) * 32;
-            const bf16x8 Ax = tr2(xrow, toff2[0], toff2[1]);
-            acc[k][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ax, Bz, acc[k][tap], 0, 0, 0);
+            for (int ks = 0; ks < KS; ++ks) A[ks] = An[ks];
           }
-        }
-        if (more) {
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) A[ks] = An[ks];
-        }
-        barrier_vm(0);  // dx updated, dz and x_l consumed; x_{l-1} / mask_{l-1} landed
+          barrier_vm(0);  // dx updated, dz and x_l consumed; x_{l-1} / mask_{l-1} landed
+        });
+        store_dx(dout, img);
+        barrier_lds();  // dx read out before the next image's DMA overwrites it
       }
-      // dx at the segment bottom -> HBM (the next segment's input, or dx_0)
-      {
-        unsigned char* dst = (unsigned char*)(dout + img);
+      // segment end: db of each layer (lanes, then the four dgrad waves in a fixed order)
+      static_for<0, KSEG>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if (k >= kcount) return;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int o = (tid + j * 64 * NWAVE) * 16;
-          *(uint4*)(dst + o) = *(const uint4*)(lds + L_DX + o);
+        for (int e = 0; e < 4; ++e) {
+          float v = dbacc[k][e];
+          v += __shfl_xor(v, 1);
+          v += __shfl_xor(v, 2);
+          v += __shfl_xor(v, 4);
+          v += __shfl_xor(v, 8);
+          if (lx == 0) dbr[wave * C + 4 * g + e] = v;
         }
-      }
-      barrier_lds();  // dx read out before the next image's DMA overwrites it
+        __syncthreads();
+        if (tid < C) {
+          const float v = (dbr[tid] + dbr[C + tid]) + (dbr[2 * C + tid] + dbr[3 * C + tid]);
+          slabs[((long)(ltop - k) * PS + b) * ES + 9 * C * C + tid] = h * v;
+        }
+        __syncthreads();
+      });
     }
-    // segment end: one slab per layer (the four waves' partials summed in a fixed order)
-    float* red = (float*)(lds + L_X);
-    float* dbr = red + 4 * 9 * 4 * 64;
+  } else {
+    // ------------------------------ wgrad waves ------------------------------
+    const int kx = wave - 4;  // 0..2; wave 7: prefetch only
+    unsigned to2[2];          // tr-read lane offsets (pixel 8g + 4*(hh ^ (g&1)) + q, channels 4p..4p+3)
 #pragma unroll
-    for (int k = 0; k < KSEG; ++k) {
-      if (k >= kcount) break;
-      const int l = ltop - k;
+    for (int hh = 0; hh < 2; ++hh) to2[hh] = (unsigned)((8 * g + 4 * (hh ^ (g & 1)) + q) * 32 + 8 * p);
+    f32x4 acc[KSEG][3];
+    for (int sg = 0; sg < nseg; ++sg) {
+      const int ltop = L - 1 - sg * KSEG, kcount = min(KSEG, ltop + 1);
+      const bf16* din = (sg & 1) ? dbufB : dbufA;
 #pragma unroll
-      for (int t = 0; t < 9; ++t)
+      for (int k = 0; k < KSEG; ++k)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) red[((wave * 9 + t) * 4 + e) * 64 + lane] = acc[k][t][e];
+        for (int t = 0; t < 3; ++t) acc[k][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int n = b; n < N; n += P) {
+        const long img = (long)n * H * W * C;
+        stage(din, img, ltop, n);
+        barrier_vm(0);
+        static_for<0, KSEG>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          if (k >= kcount) return;
+          const int l = ltop - k, cur = k & 1;
+          if (wave == 7 && k + 1 < kcount) {  // x_{l-1}, mask_{l-1} into the other buffers
+            const unsigned char* xsrc = (const unsigned char*)(xs + (l - 1) * x_stride + img);
+            for (int j = 0; j < 32; ++j)
+              dma16(xsrc + j * 1024 + lane * 16, lds + L_X + (cur ^ 1) * TILE + (j + 1) * ROWB + 32);
+            for (int j = 0; j < 2; ++j)
+              dma16(masks + (l - 1) * mask_stride + (long)n * MB + j * 1024 + lane * 16,
+                    lds + L_M + (cur ^ 1) * MB + j * 1024);
+          }
+          build_dz(cur);
+          barrier_lds();
+          if (wave < 7) {
+            const unsigned char* xt = lds + L_X + cur * TILE + kx * 32;  // tile column pixel + kx
+            const unsigned char* zt = lds + L_DZ + ROWB + 32;           // dz of output row 0, pixel 0
+            bf16x8 Bm1 = tr2(zt, to2), Bm2;                              // B of output row 0
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float v = dbacc[k][e];
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 8);
-        if (lx == 0) dbr[wave * C + 4 * g + e] = v;
+            for (int ir = 1; ir <= H; ++ir) {  // tile rows holding image rows 0 .. 31
+              const bf16x8 Ax = tr2(xt + ir * ROWB, to2);
+              bf16x8 Bc;
+              if (ir < H) {
+                Bc = tr2(zt + ir * ROWB, to2);  // output row ir
+                acc[k][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ax, Bc, acc[k][0], 0, 0, 0);  // ky=0
+              }
+              acc[k][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ax, Bm1, acc[k][1], 0, 0, 0);   // ky=1, row ir-1
+              if (ir >= 2)
+                acc[k][2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ax, Bm2, acc[k][2], 0, 0, 0);  // ky=2, row ir-2
+              Bm2 = Bm1;
+              if (ir < H) Bm1 = Bc;
+            }
+          }
+          barrier_vm(0);
+        });
+        store_dx((sg & 1) ? dbufA : dbufB, img);
+        barrier_lds();
       }
-      __syncthreads();
-      float* slab = slabs + ((long)l * PS + b) * ES;
-      for (int i = tid; i < ES; i += 64 * NWAVE) {
-        float v;
-        if (i < 9 * C * C) {
-          const int t = i >> 8, m = (i >> 4) & 15, o = i & 15;
-          const int ri = ((t * 4 + (m & 3)) * 64 + (m >> 2) * 16 + o);
-          v = (red[ri] + red[9 * 4 * 64 + ri]) + (red[2 * 9 * 4 * 64 + ri] + red[3 * 9 * 4 * 64 + ri]);
+      // segment end: dW of each layer straight from the accumulators (complete sums)
+      static_for<0, KSEG>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if (k >= kcount) return;
+        float* slab = slabs + ((long)(ltop - k) * PS + b) * ES;
+        if (wave < 7) {
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) slab[((3 * ky + kx) * 16 + 4 * g + e) * 16 + lx] = h * acc[k][ky][e];
         } else {
-          const int o = i - 9 * C * C;
-          v = (dbr[o] + dbr[C + o]) + (dbr[2 * C + o] + dbr[3 * C + o]);
+          for (int j = P + b; j < PS; j += P) {  // padding slabs of the 32-slab reduction groups
+            float* zs = slabs + ((long)(ltop - k) * PS + j) * ES;
+            for (int i = lane; i < ES; i += 64) zs[i] = 0.f;
+          }
         }
-        slab[i] = h * v;
-      }
-      for (int j = P + b; j < PS; j += P) {  // padding slabs of the 32-slab reduction groups
-        float* zs = slabs + ((long)l * PS + j) * ES;
-        for (int i = tid; i < ES; i += 64 * NWAVE) zs[i] = 0.f;
-      }
-      __syncthreads();
+        __syncthreads();
+        __syncthreads();
+      });
     }
-    // the reduction area overlapped the x tiles: restore their zero halos
-    for (int i = tid; i < 2 * TILE / 16; i += 64 * NWAVE) ((uint4*)(lds + L_X))[i] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
   }
 }
 }  // namespace deep
@@ -433,7 +484,7 @@ int deep16_backward(void* dbufA, void* dbufB, const void* xs, long x_stride, con
   if (cus <= 0) cus = 256;
   const int P = std::max(1, std::min(N, cus));
   const int PS = deep16_slab_rows(N);
-  hipLaunchKernelGGL(deep::k_bwd16_fused, dim3(P), dim3(64 * deep::NWAVE), (size_t)deep::L_TOTAL, s, (bf16*)dbufA,
+  hipLaunchKernelGGL(deep::k_bwd16_fused, dim3(P), dim3(64 * deep::NWB), (size_t)deep::L_TOTAL, s, (bf16*)dbufA,
                      (bf16*)dbufB, (const bf16*)xs, x_stride, masks, mask_stride, (const bf16*)wpack, h, two_gamma,
                      N, L, slabs, PS);
   ASR_LAUNCH_CHECK("k_bwd16_fused");
