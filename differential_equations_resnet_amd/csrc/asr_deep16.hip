@@ -108,26 +108,38 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
       const bool store = STORE_ALL || l == L - 1;
       bf16* yl = y0 + (STORE_ALL ? (long)l * y_stride : 0) + (long)n * H * W * C;
       uint8_t* ml = mask0 ? mask0 + (long)l * mask_stride + (long)n * H * W * (C / 8) : nullptr;
+      // rows software-pipelined: the B fragments of row k+1 are read during row k's MFMAs
+      bf16x8 B[2][2][KS];
+      auto loadB = [&](int k, bf16x8 (&Bd)[2][KS]) {
+        const unsigned char* tb = src + (r0 + k) * ROWB;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          Bd[0][ks] = *(const bf16x8*)(tb + boff[ks]);
+          Bd[1][ks] = *(const bf16x8*)(tb + 512 + boff[ks]);
+        }
+      };
+      loadB(0, B[0]);
+      unsigned mw[RPW][2];
 #pragma unroll
       for (int k = 0; k < RPW; ++k) {
         const int r = r0 + k;
-        unsigned mw[2];
+        if (k + 1 < RPW) loadB(k + 1, B[(k + 1) & 1]);
+        f32x4 acc[2] = {{bz[0], bz[1], bz[2], bz[3]}, {bz[0], bz[1], bz[2], bz[3]}};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], B[k & 1][0][ks], acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], B[k & 1][1][ks], acc[1], 0, 0, 0);
+        }
 #pragma unroll
         for (int pt = 0; pt < 2; ++pt) {
           const unsigned char* tb = src + r * ROWB + pt * 512;
-          f32x4 acc = {bz[0], bz[1], bz[2], bz[3]};
-          bf16x8 B[KS];
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) B[ks] = *(const bf16x8*)(tb + boff[ks]);
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], B[ks], acc, 0, 0, 0);
           // epilogue: y = x + h * relu(z) (fp32, one rounding), relu bits
           const bf16x4 xr = *(const bf16x4*)(tb + xoff);
           bf16x4 o4;
           unsigned nib = 0;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float z = acc[e];
+            const float z = acc[pt][e];
             const bool pos = z > 0.f;  // relu'(z) as TF's ReluGrad: z > 0
             nib |= (pos ? 1u : 0u) << e;
             const float rz = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, z) & (pos ? ~0u : 0u));
@@ -140,10 +152,15 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
           const auto s16 = __builtin_amdgcn_permlane16_swap(m, m, false, false);
           m = s16[0] | s16[1];
           const auto s32 = __builtin_amdgcn_permlane32_swap(m, m, false, false);
-          mw[pt] = s32[0] | s32[1];
+          mw[k][pt] = s32[0] | s32[1];
         }
-        // row r's 32 mask words (64 B): lanes 0-15 pixel tile 0, 16-31 tile 1
-        if (ml && lane < 32) *(uint16_t*)(ml + (r * W + lane) * 2) = (uint16_t)(lane < 16 ? mw[0] : mw[1]);
+      }
+      // the rows' 32 mask words each (64 B per row): lanes 0-15 pixel tile 0, 16-31 tile 1
+      if (ml && lane < 32) {
+        const unsigned hi = lane < 16 ? 0u : ~0u;  // a select, not an index (a lane-indexed array goes to scratch)
+#pragma unroll
+        for (int k = 0; k < RPW; ++k)
+          *(uint16_t*)(ml + ((r0 + k) * W + lane) * 2) = (uint16_t)((mw[k][0] & ~hi) | (mw[k][1] & hi));
       }
       if (more) {
 #pragma unroll
@@ -191,7 +208,8 @@ constexpr int ES = 9 * C * C + C;        // slab floats per layer
 constexpr int DXB = H * W * C * 2;       // 32 KiB
 constexpr int MB = H * W * C / 8;        // 2 KiB of relu bits per image
 constexpr int L_DX = 0, L_DZ = L_DX + DXB, L_X = L_DZ + TILE, L_M = L_X + 2 * TILE, L_TAB = L_M + 2 * MB;
-constexpr int L_TOTAL = L_TAB + 4096;
+constexpr int L_DBS = L_TAB + 4096;       // [KSEG][4][C] fp32 db partials
+constexpr int L_TOTAL = L_DBS + KSEG * 4 * C * 4;
 static_assert(L_TOTAL <= 160 * 1024, "LDS budget");
 
 // f(integral_constant<int, k>) for k = K .. N-1: compile-time register-array
@@ -242,18 +260,25 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
     }
   };
   // phase 1: dzm = dx & mask (cur mask buffer) for the whole image, 4 chunks per thread
+  // (all reads first, so their latencies overlap)
   auto build_dz = [&](int cur) {
     const unsigned char* mt = lds + L_M + cur * MB;
+    uint4 dv[4], mv[4];
+    unsigned mb[4], zo[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int c = tid + 64 * NWB * j;
       const int r = c >> 6, px = (c & 63) >> 1, hc = c & 1;
-      const uint4 dv = *(const uint4*)(lds + L_DX + (r * W + px) * 32 + hc * 16);
-      const unsigned mb = mt[(r * W + px) * 2 + hc];
-      const uint4 mv = *(const uint4*)(lds + L_TAB + mb * 16);
-      *(uint4*)(lds + L_DZ + ((r + 1) * TW + px + 1) * 32 + hc * 16) =
-          make_uint4(dv.x & mv.x, dv.y & mv.y, dv.z & mv.z, dv.w & mv.w);
+      dv[j] = *(const uint4*)(lds + L_DX + (r * W + px) * 32 + hc * 16);
+      mb[j] = mt[(r * W + px) * 2 + hc];
+      zo[j] = (unsigned)(((r + 1) * TW + px + 1) * 32 + hc * 16);
     }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mv[j] = *(const uint4*)(lds + L_TAB + mb[j] * 16);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      *(uint4*)(lds + L_DZ + zo[j]) = make_uint4(dv[j].x & mv[j].x, dv[j].y & mv[j].y, dv[j].z & mv[j].z,
+                                                 dv[j].w & mv[j].w);
   };
   auto store_dx = [&](bf16* dout, long img) {
     unsigned char* dst = (unsigned char*)(dout + img);
@@ -263,7 +288,7 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
       *(uint4*)(dst + o) = *(const uint4*)(lds + L_DX + o);
     }
   };
-  float* dbr = (float*)(lds + L_DZ + (TW + 1) * 32);  // [4][C] db partials (dz interior, free at segment end)
+  float* dbs = (float*)(lds + L_DBS);  // [KSEG][4 dgrad waves][C] db partial sums of the segment
 
   if (wave < 4) {
     // ------------------------------ dgrad waves ------------------------------
@@ -277,48 +302,48 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
     }
     const unsigned zoff = (unsigned)((TW + 1 + lx) * 32 + 8 * g);  // dz interior value of the D layout
     const unsigned doff = (unsigned)(lx * 32 + 8 * g);              // dx (no halo) of the D layout
-    float dbacc[KSEG][4];
     for (int sg = 0; sg < nseg; ++sg) {
       const int ltop = L - 1 - sg * KSEG, kcount = min(KSEG, ltop + 1);
       const bf16* din = (sg & 1) ? dbufB : dbufA;
       bf16* dout = (sg & 1) ? dbufA : dbufB;
-#pragma unroll
-      for (int k = 0; k < KSEG; ++k)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dbacc[k][e] = 0.f;
+      for (int i = lane; i < KSEG * C; i += 64) dbs[(i / C) * 4 * C + wave * C + i % C] = 0.f;
       for (int n = b; n < N; n += P) {
         const long img = (long)n * H * W * C;
         stage(din, img, ltop, n);
         bf16x8 A[KS], An[KS];
         load_wt(wpack + (long)ltop * WSTRIDE, lane, A);
         barrier_vm(0);
-        static_for<0, KSEG>([&](auto kc) {
-          constexpr int k = decltype(kc)::value;
-          if (k >= kcount) return;
+        for (int k = 0; k < kcount; ++k) {
           const int l = ltop - k;
           const bool more = k + 1 < kcount;
           if (more) load_wt(wpack + (long)(l - 1) * WSTRIDE, lane, An);
           build_dz(k & 1);
           barrier_lds();  // dzm complete (the prefetch DMA keeps flying)
-#pragma unroll 2
+          float dsum[4] = {0.f, 0.f, 0.f, 0.f};
+          // rows software-pipelined: the B fragments of row j+1 are read during row j's MFMAs
+          bf16x8 B[2][2][KS];
+          auto loadB = [&](int j, bf16x8 (&Bd)[2][KS]) {
+            const unsigned char* tb = lds + L_DZ + (r0 + j) * ROWB;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+              Bd[0][ks] = *(const bf16x8*)(tb + boff[ks]);
+              Bd[1][ks] = *(const bf16x8*)(tb + 512 + boff[ks]);
+            }
+          };
+          loadB(0, B[0]);
+#pragma unroll
           for (int j = 0; j < RPW; ++j) {
             const int r = r0 + j;
+            if (j + 1 < RPW) loadB(j + 1, B[(j + 1) & 1]);
+            f32x4 c[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+              c[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], B[j & 1][0][ks], c[0], 0, 0, 0);
+              c[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], B[j & 1][1][ks], c[1], 0, 0, 0);
+            }
             const unsigned char* tb = lds + L_DZ + r * ROWB;
-            bf16x8 B0[KS], B1[KS];
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-              B0[ks] = *(const bf16x8*)(tb + boff[ks]);
-              B1[ks] = *(const bf16x8*)(tb + 512 + boff[ks]);
-            }
-            f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-              c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], B0[ks], c0, 0, 0, 0);
-              c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], B1[ks], c1, 0, 0, 0);
-            }
 #pragma unroll
             for (int pt = 0; pt < 2; ++pt) {
-              const f32x4 c = pt ? c1 : c0;
               const bf16x4 zr = *(const bf16x4*)(tb + pt * 512 + zoff);
               unsigned char* dxp = lds + L_DX + (r * W + 16 * pt) * 32 + doff;
               const bf16x4 dr = *(const bf16x4*)dxp;
@@ -326,42 +351,40 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const float zf = (float)zr[e];
-                dbacc[k][e] += zf;
-                const float v = fmaf(-h, c[e], (float)dr[e]);
+                dsum[e] += zf;
+                const float v = fmaf(-h, c[pt][e], (float)dr[e]);
                 o4[e] = (bf16)(hs2g != 0.f ? fmaf(hs2g, zf, v) : v);
               }
               *(bf16x4*)dxp = o4;
             }
+          }
+          // db of this layer: the wave's 16 pixel lanes, added to its own slot (no other writer)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float v = dsum[e];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 8);
+            if (lx == 0) dbs[(k * 4 + wave) * C + 4 * g + e] += v;
           }
           if (more) {
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) A[ks] = An[ks];
           }
           barrier_vm(0);  // dx updated, dz and x_l consumed; x_{l-1} / mask_{l-1} landed
-        });
+        }
         store_dx(dout, img);
         barrier_lds();  // dx read out before the next image's DMA overwrites it
       }
-      // segment end: db of each layer (lanes, then the four dgrad waves in a fixed order)
-      static_for<0, KSEG>([&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        if (k >= kcount) return;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = dbacc[k][e];
-          v += __shfl_xor(v, 1);
-          v += __shfl_xor(v, 2);
-          v += __shfl_xor(v, 4);
-          v += __shfl_xor(v, 8);
-          if (lx == 0) dbr[wave * C + 4 * g + e] = v;
+      // segment end: db of each layer, the four dgrad waves summed in a fixed order
+      __syncthreads();
+      if (tid < C)
+        for (int k = 0; k < kcount; ++k) {
+          const float* d = dbs + k * 4 * C + tid;
+          slabs[((long)(ltop - k) * PS + b) * ES + 9 * C * C + tid] = h * ((d[0] + d[C]) + (d[2 * C] + d[3 * C]));
         }
-        __syncthreads();
-        if (tid < C) {
-          const float v = (dbr[tid] + dbr[C + tid]) + (dbr[2 * C + tid] + dbr[3 * C + tid]);
-          slabs[((long)(ltop - k) * PS + b) * ES + 9 * C * C + tid] = h * v;
-        }
-        __syncthreads();
-      });
+      __syncthreads();
     }
   } else {
     // ------------------------------ wgrad waves ------------------------------
@@ -370,6 +393,34 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) to2[hh] = (unsigned)((8 * g + 4 * (hh ^ (g & 1)) + q) * 32 + 8 * p);
     f32x4 acc[KSEG][3];
+    // one layer's weight gradient for tap column kx into a[ky] (ky = 0..2): x fragment of
+    // tile row ir feeds output rows ir - ky; reads run DEPTH rows ahead of the MFMAs
+    auto wgrad_layer = [&](f32x4 (&a)[3], int cur) {
+      constexpr int DEPTH = 2;
+      const unsigned char* xt = lds + L_X + cur * TILE + kx * 32;  // tile column pixel + kx
+      const unsigned char* zt = lds + L_DZ + ROWB + 32;           // dz of output row 0, pixel 0
+      bf16x8 Aq[DEPTH + 1], Bq[DEPTH + 1];
+      const bf16x8 Bz = tr2(zt, to2);  // B of output row 0
+#pragma unroll
+      for (int d = 1; d <= DEPTH; ++d) {
+        Aq[d % (DEPTH + 1)] = tr2(xt + d * ROWB, to2);
+        if (d < H) Bq[d % (DEPTH + 1)] = tr2(zt + d * ROWB, to2);
+      }
+      bf16x8 Bm1 = Bz, Bm2 = Bz;
+#pragma unroll
+      for (int ir = 1; ir <= H; ++ir) {  // tile rows holding image rows 0 .. 31
+        if (ir + DEPTH <= H) {
+          Aq[(ir + DEPTH) % (DEPTH + 1)] = tr2(xt + (ir + DEPTH) * ROWB, to2);
+          if (ir + DEPTH < H) Bq[(ir + DEPTH) % (DEPTH + 1)] = tr2(zt + (ir + DEPTH) * ROWB, to2);
+        }
+        const bf16x8 Ax = Aq[ir % (DEPTH + 1)];
+        if (ir < H) a[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ax, Bq[ir % (DEPTH + 1)], a[0], 0, 0, 0);  // ky=0
+        a[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ax, Bm1, a[1], 0, 0, 0);  // ky=1: output row ir-1
+        if (ir >= 2) a[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ax, Bm2, a[2], 0, 0, 0);  // ky=2: row ir-2
+        Bm2 = Bm1;
+        if (ir < H) Bm1 = Bq[ir % (DEPTH + 1)];
+      }
+    };
     for (int sg = 0; sg < nseg; ++sg) {
       const int ltop = L - 1 - sg * KSEG, kcount = min(KSEG, ltop + 1);
       const bf16* din = (sg & 1) ? dbufB : dbufA;
@@ -381,9 +432,7 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
         const long img = (long)n * H * W * C;
         stage(din, img, ltop, n);
         barrier_vm(0);
-        static_for<0, KSEG>([&](auto kc) {
-          constexpr int k = decltype(kc)::value;
-          if (k >= kcount) return;
+        for (int k = 0; k < kcount; ++k) {
           const int l = ltop - k, cur = k & 1;
           if (wave == 7 && k + 1 < kcount) {  // x_{l-1}, mask_{l-1} into the other buffers
             const unsigned char* xsrc = (const unsigned char*)(xs + (l - 1) * x_stride + img);
@@ -395,31 +444,18 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
           }
           build_dz(cur);
           barrier_lds();
-          if (wave < 7) {
-            const unsigned char* xt = lds + L_X + cur * TILE + kx * 32;  // tile column pixel + kx
-            const unsigned char* zt = lds + L_DZ + ROWB + 32;           // dz of output row 0, pixel 0
-            bf16x8 Bm1 = tr2(zt, to2), Bm2;                              // B of output row 0
-#pragma unroll
-            for (int ir = 1; ir <= H; ++ir) {  // tile rows holding image rows 0 .. 31
-              const bf16x8 Ax = tr2(xt + ir * ROWB, to2);
-              bf16x8 Bc;
-              if (ir < H) {
-                Bc = tr2(zt + ir * ROWB, to2);  // output row ir
-                acc[k][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ax, Bc, acc[k][0], 0, 0, 0);  // ky=0
-              }
-              acc[k][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ax, Bm1, acc[k][1], 0, 0, 0);   // ky=1, row ir-1
-              if (ir >= 2)
-                acc[k][2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ax, Bm2, acc[k][2], 0, 0, 0);  // ky=2, row ir-2
-              Bm2 = Bm1;
-              if (ir < H) Bm1 = Bc;
-            }
+          if (wave < 7) {  // this layer's accumulators (a compile-time index per branch)
+            static_for<0, KSEG>([&](auto kc) {
+              if (k == decltype(kc)::value) wgrad_layer(acc[decltype(kc)::value], cur);
+            });
           }
           barrier_vm(0);
-        });
+        }
         store_dx((sg & 1) ? dbufA : dbufB, img);
         barrier_lds();
       }
       // segment end: dW of each layer straight from the accumulators (complete sums)
+      __syncthreads();
       static_for<0, KSEG>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
         if (k >= kcount) return;
@@ -435,9 +471,8 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
             for (int i = lane; i < ES; i += 64) zs[i] = 0.f;
           }
         }
-        __syncthreads();
-        __syncthreads();
       });
+      __syncthreads();
     }
   }
 }
