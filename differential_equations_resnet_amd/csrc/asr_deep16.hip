@@ -12,15 +12,27 @@
 // stores only x_L.  HBM traffic per block: one activation write (+ the 1/16
 // mask) instead of a read and a write.
 //
-// Conv = implicit GEMM on v_mfma_f32_16x16x32_bf16, kappa = tap*16 + i:
+// Conv = implicit GEMM on v_mfma_f32_16x16x32_bf16 over kappa = (tap, i):
 //   Z^T[o][p] = b[o] + sum_kappa W^T[o][kappa] X[p][kappa]
-// A = W^T (16 x 144, padded to 5 k-steps of 32) in VGPRs per layer; B read
-// from the LDS image: lane (pixel lx, group g) of k-step ks reads the 16-B
-// chunk (g & 1) of tap 2ks + (g >> 1) at pixel lx, one ds_read_b128 (the
-// NHWC 32-B pixels are bank-conflict-free for the b128 lane groups).  The
-// padded tap 9 re-reads tap 8 (finite data, multiplied by A = 0).
-// Same accumulation order as the per-block kernel (bias, then k-steps 0..4),
-// so a layer's result is bitwise that of k_fwd<16,...>.
+// with the 9 taps paired into 5 k-steps so that B fragments are shared
+// between output rows ("row-reuse" order):
+//   ks 0..2: taps (ky, 0) | (ky, 1) of tile row r + ky   -> fragment F(r + ky)
+//   ks 3:    taps (0, 2)  | (1, 2)  of tile rows r, r+1  -> fragment G(r)
+//   ks 4:    taps (2, 2)  | zero    of tile rows r+2, r+3 -> fragment G(r + 2)
+// F(R) serves output rows R-2 .. R and G(R) rows R and R-2, so a wave reads
+// each of its 10 tile rows twice (F, G) instead of 10 fragments per output
+// row.  A = W^T (5 k-steps, the pad half multiplies the zero tap 9 of the
+// standard packing) in VGPRs per layer, gathered from asr_theta_to_w's
+// packing by a per-lane permutation.
+//
+// LDS tile: 34 x 34 pixels (zero halo) x 32 B; chunk c (channels 8c..8c+7)
+// of tile column tc is stored at tc*32 + 16*(c ^ bit2(tc)).  The swizzle
+// makes the 16-B epilogue stores (ds_write_b128: 8 lanes, banks mod 32)
+// conflict-free and keeps the B reads (ds_read_b128 lane groups, banks mod
+// 64) conflict-free.  The accumulators of a row's two pixel tiles are
+// regrouped with v_permlane16_swap so each lane owns 8 consecutive channels
+// of one pixel: one 16-B LDS store, one 16-B global store and one mask byte
+// per lane and row, and the residual x stays in the lane's registers.
 #include <type_traits>
 
 #include "asr_common.h"
@@ -34,28 +46,97 @@ using namespace blk;
 constexpr int C = 16, W = 32, H = 32, TW = W + 2;
 constexpr int ROWB = TW * C * 2;       // 1088 B per tile row (halo columns included)
 constexpr int TILE = (H + 2) * ROWB;   // 36992 B per image tile (halo rows included)
-constexpr int KS = 5;                  // k-steps of 32 over kappa = 9 taps x 16 channels (+ pad)
+constexpr int IMG = H * W * C;         // elements per image
+constexpr int KS = 5;                  // k-steps of 32 over kappa = 9 taps x 16 channels (+ zero tap)
 constexpr int WSTRIDE = KS * 512;      // packed W^T elements per layer (asr_wpack_elems(16))
-constexpr int NWAVE = 4;               // waves per workgroup; wave w owns image rows [8w, 8w+8)
+constexpr int NWAVE = 4;               // forward waves per workgroup; wave w owns image rows [8w, 8w+8)
 constexpr int RPW = H / NWAVE;
+constexpr int ROW_G = W * C * 2;       // 1024 B per image row in HBM
 
-__device__ __forceinline__ void load_wt(const bf16* __restrict__ w, int lane, bf16x8 (&A)[KS]) {
+static __device__ float g_zero_bias[C];  // bias of layers without one (never written)
+
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+
+// byte offset of chunk c of tile column tc within a tile row
+__device__ __forceinline__ unsigned swz(int tc, int c) { return (unsigned)(tc * 32 + 16 * (c ^ ((tc >> 2) & 1))); }
+
+// per-lane element offsets of the 5 A fragments within one layer's packed
+// W^T: lane (o, kg) of row-reuse k-step ks needs tap t (first of the pair for
+// kg < 2), channels 8(kg&1)..+7, found in the standard packing at k-step
+// t/2, lane group 2(t&1) + (kg&1)
+__device__ __forceinline__ void wt_offsets(int lane, unsigned (&wo)[KS]) {
+  const int o = lane & 15, kg = lane >> 4, sec = kg >> 1;
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) A[ks] = *(const bf16x8*)(w + (ks * 64 + lane) * 8);
+  for (int ks = 0; ks < KS; ++ks) {
+    const int t = ks < 3 ? 3 * ks + sec : (ks == 3 ? 2 + 3 * sec : 8 + sec);
+    wo[ks] = (unsigned)(((t >> 1) * 64 + o + 16 * ((t & 1) * 2 + (kg & 1))) * 8);
+  }
+}
+__device__ __forceinline__ void load_wt(const bf16* __restrict__ w, const unsigned (&wo)[KS], bf16x8 (&A)[KS]) {
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) A[ks] = *(const bf16x8*)(w + wo[ks]);
 }
 
-// zero the whole tile (halo included); interiors are overwritten later
-__device__ __forceinline__ void zero_tile(unsigned char* t, int tid, int nt) {
-  for (int i = tid; i < TILE / 16; i += nt) ((uint4*)t)[i] = make_uint4(0, 0, 0, 0);
+// The two pixel tiles' accumulators of one output row (D layout: lane (lx, g)
+// holds channels 4g..4g+3 of pixels lx and 16+lx) regrouped so that lane
+// (lx, g) holds channels 8(g>>1) + i, i = 0..7, of pixel lx + 16(g&1)
+// (v_permlane16_swap: odd rows of the first operand <-> even rows of the second).
+__device__ __forceinline__ void regroup(const f32x4& c0, const f32x4& c1, float (&z)[8]) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(c0[e]), __float_as_uint(c1[e]), false, false);
+    z[e] = __uint_as_float(s[0]);
+    z[4 + e] = __uint_as_float(s[1]);
+  }
 }
+__device__ __forceinline__ float lo_f(unsigned w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi_f(unsigned w) { return __uint_as_float(w & 0xffff0000u); }
+// two fp32 -> packed bf16 pair (RNE, one v_cvt_pk_bf16_f32)
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const bf16x2 v = {(bf16)a, (bf16)b};
+  return __builtin_bit_cast(unsigned, v);
+}
+
+// One output row of the implicit GEMM for both pixel tiles from the row-reuse
+// fragments (fixed accumulation order: init, k-steps 0..4).
+__device__ __forceinline__ void row_mfma(const bf16x8 (&A)[KS], const bf16x8 (&F0)[2], const bf16x8 (&F1)[2],
+                                         const bf16x8 (&F2)[2], const bf16x8 (&G0)[2], const bf16x8 (&G2)[2],
+                                         f32x4 (&acc)[2]) {
+#pragma unroll
+  for (int pt = 0; pt < 2; ++pt) acc[pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], F0[pt], acc[pt], 0, 0, 0);
+#pragma unroll
+  for (int pt = 0; pt < 2; ++pt) acc[pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1], F1[pt], acc[pt], 0, 0, 0);
+#pragma unroll
+  for (int pt = 0; pt < 2; ++pt) acc[pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[2], F2[pt], acc[pt], 0, 0, 0);
+#pragma unroll
+  for (int pt = 0; pt < 2; ++pt) acc[pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[3], G0[pt], acc[pt], 0, 0, 0);
+#pragma unroll
+  for (int pt = 0; pt < 2; ++pt) acc[pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[4], G2[pt], acc[pt], 0, 0, 0);
+}
+
+// Row-reuse B fragments of the wave's 10 tile rows: F(R), G(R) for R = j..j+3
+// live in a ring of 4 (slot R & 3); row j's MFMAs read F(j..j+2), G(j), G(j+2)
+// while the fragments of tile row j+3 load.
+struct Frag {
+  bf16x8 F[4][2], G[4][2];
+  __device__ __forceinline__ void load(const unsigned char* tile, unsigned bF, unsigned bG, int R) {
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt) {
+      F[R & 3][pt] = *(const bf16x8*)(tile + bF + R * ROWB + pt * 512);
+      G[R & 3][pt] = *(const bf16x8*)(tile + bG + R * ROWB + pt * 512);
+    }
+  }
+};
 
 // x_{l+1} for l = 0 .. L-1 of every image the workgroup owns.
 //   x0:    [N,32,32,16] bf16 (the stem output)
-//   y0:    output of layer 0; layer l writes y0 + l*y_stride (store_all), or
+//   y0:    output of layer 0; layer l writes y0 + l*y_stride (STORE_ALL), or
 //          only layer L-1 writes y0 (inference)
-//   mask0: relu masks, layer l at mask0 + l*mask_stride bytes (may be null)
+//   mask0: relu masks (MASK), layer l at mask0 + l*mask_stride bytes; per
+//          pixel 16 bits, bit c = channel c
 //   wpack: packed W^T, layer l at wpack + l*WSTRIDE; bias: layer l at bias + l*bias_stride
-template <bool STORE_ALL>
+template <bool STORE_ALL, bool MASK>
 __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __restrict__ x0, bf16* __restrict__ y0,
                                                             long y_stride, uint8_t* __restrict__ mask0,
                                                             long mask_stride, const bf16* __restrict__ wpack,
@@ -65,109 +146,82 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, lx = lane & 15;
   const int r0 = wave * RPW;
-  zero_tile(lds, tid, 64 * NWAVE);
-  zero_tile(lds + TILE, tid, 64 * NWAVE);
-  // per-lane B offsets of the 5 k-steps relative to (output row, pixel tile)
-  unsigned boff[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    const int tap = min(2 * ks + (g >> 1), 8);
-    boff[ks] = (unsigned)(((tap / 3) * TW + tap % 3 + lx) * 32 + (g & 1) * 16);
-  }
-  // residual / output offset of the lane's 4 channels 4g..4g+3 of pixel lx
-  const unsigned xoff = (unsigned)((TW + 1 + lx) * 32 + 8 * g);
+  // both tiles and the zero row behind them (G(33) of the second tile reads it)
+  for (int i = tid; i < (2 * TILE + ROWB) / 16; i += 64 * NWAVE) ((uint4*)lds)[i] = make_uint4(0, 0, 0, 0);
+  const unsigned bF = (unsigned)(r0 * ROWB) + swz(lx + (g >> 1), g & 1);
+  const unsigned bG = (unsigned)((r0 + (g >> 1)) * ROWB) + swz(lx + 2, g & 1);
+  const int px = lx + 16 * (g & 1), cg = g >> 1;  // the lane's pixel / channel chunk after regroup
+  const unsigned oT = (unsigned)((r0 + 1) * ROWB) + swz(px + 1, cg);
+  const unsigned oG = (unsigned)(((r0 * W + px) * C + 8 * cg) * 2);
+  const unsigned oM = (unsigned)((r0 * W + px) * 2 + cg);
+  unsigned wo[KS];
+  wt_offsets(lane, wo);
+  // branch-free prefetch below (loads on a conditional path make the compiler's
+  // loop-header wait vmcnt(0), which would also wait for the previous layer's stores)
+  const float* bsrc = bias ? bias : g_zero_bias;
+  const long bstr = bias ? bias_stride : 0;
   __syncthreads();
 
   for (int n = blockIdx.x; n < N; n += gridDim.x) {
-    // stage x0 of image n in tile 0 (interiors: one 1 KiB DMA per image row)
-    {
-      const unsigned char* src = (const unsigned char*)(x0 + (long)n * H * W * C);
+    // x0 of image n: the lane's own chunks (the residual of layer 0) into tile 0
+    const unsigned char* xin = (const unsigned char*)(x0 + (long)n * IMG);
+    bf16x8 xr[RPW];
 #pragma unroll
-      for (int k = 0; k < RPW; ++k) {
-        const int r = r0 + k;
-        dma16(src + r * 1024 + lane * 16, lds + (r + 1) * ROWB + 32);
-      }
-    }
+    for (int j = 0; j < RPW; ++j) xr[j] = *(const bf16x8*)(xin + oG + j * ROW_G);
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) *(bf16x8*)(lds + oT + j * ROWB) = xr[j];
     bf16x8 A[KS], An[KS];
-    load_wt(wpack, lane, A);
+    load_wt(wpack, wo, A);
     float bz[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) bz[e] = bias ? bias[4 * g + e] : 0.f;
-    barrier_vm(0);  // the image's rows landed in every wave's share
+    for (int e = 0; e < 4; ++e) bz[e] = bsrc[4 * g + e];
+    barrier_lds();
 
     for (int l = 0; l < L; ++l) {
       const unsigned char* src = lds + (l & 1) * TILE;
       unsigned char* dst = lds + ((l + 1) & 1) * TILE;
-      const bool more = l + 1 < L;
+      const int ln = min(l + 1, L - 1);
       float bn[4];
-      if (more) {  // next layer's W^T fragments and bias (L2-resident) while this one runs
-        load_wt(wpack + (long)(l + 1) * WSTRIDE, lane, An);
+      // next layer's W^T fragments and bias (L2-resident) while this one runs
+      load_wt(wpack + (long)ln * WSTRIDE, wo, An);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) bn[e] = bias ? bias[(l + 1) * bias_stride + 4 * g + e] : 0.f;
-      }
+      for (int e = 0; e < 4; ++e) bn[e] = bsrc[ln * bstr + 4 * g + e];
       const bool store = STORE_ALL || l == L - 1;
-      bf16* yl = y0 + (STORE_ALL ? (long)l * y_stride : 0) + (long)n * H * W * C;
-      uint8_t* ml = mask0 ? mask0 + (long)l * mask_stride + (long)n * H * W * (C / 8) : nullptr;
-      // rows software-pipelined: the B fragments of row k+1 are read during row k's MFMAs
-      bf16x8 B[2][2][KS];
-      auto loadB = [&](int k, bf16x8 (&Bd)[2][KS]) {
-        const unsigned char* tb = src + (r0 + k) * ROWB;
+      unsigned char* yl = (unsigned char*)(y0 + (STORE_ALL ? (long)l * y_stride : 0) + (long)n * IMG);
+      uint8_t* ml = MASK ? mask0 + (long)l * mask_stride + (long)n * (IMG / 8) : nullptr;
+      Frag fr;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          Bd[0][ks] = *(const bf16x8*)(tb + boff[ks]);
-          Bd[1][ks] = *(const bf16x8*)(tb + 512 + boff[ks]);
-        }
-      };
-      loadB(0, B[0]);
-      unsigned mw[RPW][2];
+      for (int R = 0; R < 3; ++R) fr.load(src, bF, bG, R);
 #pragma unroll
-      for (int k = 0; k < RPW; ++k) {
-        const int r = r0 + k;
-        if (k + 1 < RPW) loadB(k + 1, B[(k + 1) & 1]);
+      for (int j = 0; j < RPW; ++j) {
+        if (j + 3 <= RPW + 1) fr.load(src, bF, bG, j + 3);
         f32x4 acc[2] = {{bz[0], bz[1], bz[2], bz[3]}, {bz[0], bz[1], bz[2], bz[3]}};
+        row_mfma(A, fr.F[j & 3], fr.F[(j + 1) & 3], fr.F[(j + 2) & 3], fr.G[j & 3], fr.G[(j + 2) & 3], acc);
+        // epilogue on the regrouped chunk: y = x + h * relu(z) (fp32, one rounding),
+        // relu bits as TF's ReluGrad (z > 0)
+        float z[8];
+        regroup(acc[0], acc[1], z);
+        const u32x4v xw = __builtin_bit_cast(u32x4v, xr[j]);
+        u32x4v yw;
+        unsigned bits = 0;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], B[k & 1][0][ks], acc[0], 0, 0, 0);
-          acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], B[k & 1][1][ks], acc[1], 0, 0, 0);
+        for (int d = 0; d < 4; ++d) {
+          // relu on the bit pattern: a float is > 0 iff its bits are a positive int
+          const int ra = max(__float_as_int(z[2 * d]), 0), rb = max(__float_as_int(z[2 * d + 1]), 0);
+          yw[d] = pk_bf16(fmaf(h, __int_as_float(ra), lo_f(xw[d])), fmaf(h, __int_as_float(rb), hi_f(xw[d])));
+          bits |= min((unsigned)ra, 1u) << (2 * d);
+          bits |= min((unsigned)rb, 1u) << (2 * d + 1);
         }
-#pragma unroll
-        for (int pt = 0; pt < 2; ++pt) {
-          const unsigned char* tb = src + r * ROWB + pt * 512;
-          // epilogue: y = x + h * relu(z) (fp32, one rounding), relu bits
-          const bf16x4 xr = *(const bf16x4*)(tb + xoff);
-          bf16x4 o4;
-          unsigned nib = 0;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float z = acc[pt][e];
-            const bool pos = z > 0.f;  // relu'(z) as TF's ReluGrad: z > 0
-            nib |= (pos ? 1u : 0u) << e;
-            const float rz = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, z) & (pos ? ~0u : 0u));
-            o4[e] = (bf16)fmaf(h, rz, (float)xr[e]);
-          }
-          *(bf16x4*)(dst + r * ROWB + pt * 512 + xoff) = o4;
-          if (store) *(bf16x4*)(yl + ((r * W) + 16 * pt + lx) * C + 4 * g) = o4;
-          // the pixel's 16 channel bits: OR over the four lane groups g
-          unsigned m = nib << (4 * g);
-          const auto s16 = __builtin_amdgcn_permlane16_swap(m, m, false, false);
-          m = s16[0] | s16[1];
-          const auto s32 = __builtin_amdgcn_permlane32_swap(m, m, false, false);
-          mw[k][pt] = s32[0] | s32[1];
-        }
+        const bf16x8 y = __builtin_bit_cast(bf16x8, yw);
+        *(bf16x8*)(dst + oT + j * ROWB) = y;
+        if (store) *(bf16x8*)(yl + oG + j * ROW_G) = y;
+        if (MASK) ml[oM + j * 64] = (uint8_t)bits;
+        xr[j] = y;
       }
-      // the rows' 32 mask words each (64 B per row): lanes 0-15 pixel tile 0, 16-31 tile 1
-      if (ml && lane < 32) {
-        const unsigned hi = lane < 16 ? 0u : ~0u;  // a select, not an index (a lane-indexed array goes to scratch)
 #pragma unroll
-        for (int k = 0; k < RPW; ++k)
-          *(uint16_t*)(ml + ((r0 + k) * W + lane) * 2) = (uint16_t)((mw[k][0] & ~hi) | (mw[k][1] & hi));
-      }
-      if (more) {
+      for (int ks = 0; ks < KS; ++ks) A[ks] = An[ks];
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) A[ks] = An[ks];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bz[e] = bn[e];
-      }
+      for (int e = 0; e < 4; ++e) bz[e] = bn[e];
       barrier_lds();  // layer l+1's tile complete; layer l's tile free
     }
   }
@@ -180,36 +234,37 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
 //   dx_l = dx_{l+1} - h*conv(dzm, W_l) + 2*gamma*h*dzm   (A^T = -A + 2 gamma I;
 //          for non-antisymmetric kinds W_l is W_bwd = -flip(W)^T, gamma 0)
 //   dW_l += h * sum_p x_l[p + s(tap)] (x) dzm[p],  db_l += h * sum_p dzm[p]
-// with dx kept in LDS across layers (no HBM round trip per block).  The
-// layers run in segments of KSEG: the weight gradients of a segment's layers
-// accumulate in registers over all images of the workgroup, so each layer
-// gets ONE slab [dW (9*16*16) | db (16)] fp32 per workgroup (the layout
+// The layers run in segments of KSEG: the weight gradients of a segment's
+// layers accumulate in registers over all images of the workgroup, so each
+// layer gets ONE slab [dW (9*16*16) | db (16)] fp32 per workgroup (the layout
 // asr_api's reduce_slabs_to_groups / project_layers consume), and dx crosses
 // HBM only at segment boundaries.
 //
 // One 512-thread workgroup per CU, two waves per SIMD with split roles:
-//   waves 0-3 (dgrad): image rows [8w, 8w+8): the forward's implicit GEMM on
-//     dzm (bitwise the per-block kernel's dx), dx updated in place, db;
+//   waves 0-3 (dgrad): image rows [8w, 8w+8): the forward's row-reuse implicit
+//     GEMM on the dzm tile; dx of the wave's pixels stays in registers (the
+//     regrouped layout), and the epilogue writes dzm_{l-1} = dx_l & mask_{l-1}
+//     straight into the other dz tile (no separate masking pass), plus db;
 //   waves 4-6 (wgrad): tap column kx = w-4 of all 32 rows: a GEMM with M = the
 //     tap's 16 input channels, N = o, K = the 32 pixels of a row.  The x
-//     fragment of tile row ir (ds_read_b64_tr_b16, T10) serves the three taps
-//     (ky, kx) of output rows ir - ky, so every x row is read once per wave;
+//     fragment of image row i (ds_read_b64_tr_b16, T10) serves the three taps
+//     (ky, kx) of output rows i+1-ky, so every x row is read once per wave;
 //     the dz fragments of the last three rows stay in registers.  The 8
 //     k-pixels of lane group g are 8g + 4*(hh ^ (g & 1)) + q for the two reads
-//     hh: odd groups swap halves, so the two 16-lane groups of each 32-lane
-//     half read disjoint banks;
-//   wave 7 DMAs x_{l-1} and mask_{l-1} into the second buffers meanwhile.
-// All 8 waves build dzm (phase 1) between two barriers.
-// LDS: dx (32 KiB) | dz tile | 2 x tiles | 2 x 2 KiB masks | 4 KiB mask table.
+//     hh: odd groups swap halves, so the lane groups read disjoint banks;
+//   wave 7 DMAs x_{l-1} and mask_{l-2} (the dgrad epilogue of layer l-1 needs
+//     mask_{l-2}) meanwhile, and at an image's last layer the next image's
+//     x_ltop and masks; the dgrad waves load the next image's dx then.
+// One barrier per layer.  LDS: 2 dz tiles (swizzled, zero halo) + zero row |
+// 2 x tiles (image rows, zero halo columns) | 2 x 2 KiB masks | db partials.
 // ---------------------------------------------------------------------------
 constexpr int KSEG = 12;                 // layers per segment (dW accumulators in registers)
 constexpr int NWB = 8;                   // waves per backward workgroup
 constexpr int ES = 9 * C * C + C;        // slab floats per layer
-constexpr int DXB = H * W * C * 2;       // 32 KiB
-constexpr int MB = H * W * C / 8;        // 2 KiB of relu bits per image
-constexpr int L_DX = 0, L_DZ = L_DX + DXB, L_X = L_DZ + TILE, L_M = L_X + 2 * TILE, L_TAB = L_M + 2 * MB;
-constexpr int L_DBS = L_TAB + 4096;       // [KSEG][4][C] fp32 db partials
-constexpr int L_TOTAL = L_DBS + KSEG * 4 * C * 4;
+constexpr int XT = H * ROWB;             // x tile: 32 image rows x 34 columns
+constexpr int MB = IMG / 8;              // 2 KiB of relu bits per image
+constexpr int L_Z = 0, L_X = L_Z + 2 * TILE + ROWB, L_M = L_X + 2 * XT, L_DBS = L_M + 2 * MB;
+constexpr int L_TOTAL = L_DBS + KSEG * 4 * C * 4;  // [KSEG][4 dgrad waves][C] fp32 db partials
 static_assert(L_TOTAL <= 160 * 1024, "LDS budget");
 
 // f(integral_constant<int, k>) for k = K .. N-1: compile-time register-array
@@ -226,6 +281,23 @@ __device__ __forceinline__ bf16x8 tr2(const unsigned char* base, const unsigned 
   return tr_pair(base + o[0], base + o[1]);
 }
 
+// dwords of 0xffff per set bit of the lane's mask byte, ANDed into 8 bf16
+__device__ __forceinline__ u32x4v mask_bf16x8(u32x4v v, unsigned m) {
+  u32x4v r;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const unsigned lo = (unsigned)((int)(m << (31 - 2 * d)) >> 31);
+    const unsigned hi = (unsigned)((int)(m << (30 - 2 * d)) >> 31);
+    r[d] = v[d] & ((lo & 0xffffu) | (hi & 0xffff0000u));
+  }
+  return r;
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+
 __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ dbufA, bf16* __restrict__ dbufB,
                                                             const bf16* __restrict__ xs, long x_stride,
                                                             const uint8_t* __restrict__ masks, long mask_stride,
@@ -235,147 +307,116 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, lx = lane & 15, q = lx >> 2, p = lx & 3;
   const int P = gridDim.x, b = blockIdx.x;
-  // zero the dz tile and both x tiles (halo rows / columns stay zero), build the mask table
-  for (int i = tid; i < 3 * TILE / 16; i += 64 * NWB) ((uint4*)(lds + L_DZ))[i] = make_uint4(0, 0, 0, 0);
-  {
-    unsigned* tab = (unsigned*)(lds + L_TAB);  // dword d of byte m: 0xffff per set bit of (m >> 2d) & 3
-    for (int i = tid; i < 1024; i += 64 * NWB) {
-      const unsigned m = (unsigned)i >> 2, d = (unsigned)i & 3;
-      tab[i] = (((m >> (2 * d)) & 1u) ? 0xffffu : 0u) | (((m >> (2 * d + 1)) & 1u) ? 0xffff0000u : 0u);
-    }
-  }
+  // dz tiles, their zero row and the x tiles (halos stay zero)
+  for (int i = tid; i < L_M / 16; i += 64 * NWB) ((uint4*)lds)[i] = make_uint4(0, 0, 0, 0);
   __syncthreads();
   const int nseg = (L + KSEG - 1) / KSEG;
-  const int wv = __builtin_amdgcn_readfirstlane(wave);
-
-  // ---- role-independent steps (every wave takes part; identical barrier sequence) ----
-  // dx at the segment top, x_ltop and mask_ltop of image n: 66 DMAs dealt round-robin
-  auto stage = [&](const bf16* din, long img, int ltop, int n) {
-    const unsigned char* ds = (const unsigned char*)(din + img);
-    const unsigned char* xsrc = (const unsigned char*)(xs + ltop * x_stride + img);
-    for (int j = wv; j < 66; j += NWB) {
-      if (j < 32) dma16(ds + j * 1024 + lane * 16, lds + L_DX + j * 1024);
-      else if (j < 64) dma16(xsrc + (j - 32) * 1024 + lane * 16, lds + L_X + (j - 31) * ROWB + 32);
-      else dma16(masks + ltop * mask_stride + (long)n * MB + (j - 64) * 1024 + lane * 16, lds + L_M + (j - 64) * 1024);
-    }
-  };
-  // phase 1: dzm = dx & mask (cur mask buffer) for the whole image, 4 chunks per thread
-  // (all reads first, so their latencies overlap)
-  auto build_dz = [&](int cur) {
-    const unsigned char* mt = lds + L_M + cur * MB;
-    uint4 dv[4], mv[4];
-    unsigned mb[4], zo[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = tid + 64 * NWB * j;
-      const int r = c >> 6, px = (c & 63) >> 1, hc = c & 1;
-      dv[j] = *(const uint4*)(lds + L_DX + (r * W + px) * 32 + hc * 16);
-      mb[j] = mt[(r * W + px) * 2 + hc];
-      zo[j] = (unsigned)(((r + 1) * TW + px + 1) * 32 + hc * 16);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) mv[j] = *(const uint4*)(lds + L_TAB + mb[j] * 16);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      *(uint4*)(lds + L_DZ + zo[j]) = make_uint4(dv[j].x & mv[j].x, dv[j].y & mv[j].y, dv[j].z & mv[j].z,
-                                                 dv[j].w & mv[j].w);
-  };
-  auto store_dx = [&](bf16* dout, long img) {
-    unsigned char* dst = (unsigned char*)(dout + img);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int o = (tid + j * 64 * NWB) * 16;
-      *(uint4*)(dst + o) = *(const uint4*)(lds + L_DX + o);
-    }
-  };
-  float* dbs = (float*)(lds + L_DBS);  // [KSEG][4 dgrad waves][C] db partial sums of the segment
+  float* dbs = (float*)(lds + L_DBS);
 
   if (wave < 4) {
     // ------------------------------ dgrad waves ------------------------------
     const int r0 = wave * RPW;
     const float hs2g = h * two_gamma;
-    unsigned boff[KS];
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int tap = min(2 * ks + (g >> 1), 8);
-      boff[ks] = (unsigned)(((tap / 3) * TW + tap % 3 + lx) * 32 + (g & 1) * 16);
-    }
-    const unsigned zoff = (unsigned)((TW + 1 + lx) * 32 + 8 * g);  // dz interior value of the D layout
-    const unsigned doff = (unsigned)(lx * 32 + 8 * g);              // dx (no halo) of the D layout
+    const unsigned bF = (unsigned)(r0 * ROWB) + swz(lx + (g >> 1), g & 1);
+    const unsigned bG = (unsigned)((r0 + (g >> 1)) * ROWB) + swz(lx + 2, g & 1);
+    const int px = lx + 16 * (g & 1), cg = g >> 1;
+    const unsigned oT = (unsigned)((r0 + 1) * ROWB) + swz(px + 1, cg);
+    const unsigned oG = (unsigned)(((r0 * W + px) * C + 8 * cg) * 2);
+    const unsigned oM = (unsigned)((r0 * W + px) * 2 + cg);
+    unsigned wo[KS];
+    wt_offsets(lane, wo);
+    int t = 0;  // layer steps so far: buffer parity (identical count in every role)
     for (int sg = 0; sg < nseg; ++sg) {
       const int ltop = L - 1 - sg * KSEG, kcount = min(KSEG, ltop + 1);
-      const bf16* din = (sg & 1) ? dbufB : dbufA;
-      bf16* dout = (sg & 1) ? dbufA : dbufB;
+      const unsigned char* din = (const unsigned char*)((sg & 1) ? dbufB : dbufA);
+      unsigned char* dout = (unsigned char*)((sg & 1) ? dbufA : dbufB);
       for (int i = lane; i < KSEG * C; i += 64) dbs[(i / C) * 4 * C + wave * C + i % C] = 0.f;
+      bf16x8 dxr[RPW];  // dx_{l+1} of the wave's pixels (regrouped chunks)
       for (int n = b; n < N; n += P) {
-        const long img = (long)n * H * W * C;
-        stage(din, img, ltop, n);
-        bf16x8 A[KS], An[KS];
-        load_wt(wpack + (long)ltop * WSTRIDE, lane, A);
-        barrier_vm(0);
-        for (int k = 0; k < kcount; ++k) {
-          const int l = ltop - k;
-          const bool more = k + 1 < kcount;
-          if (more) load_wt(wpack + (long)(l - 1) * WSTRIDE, lane, An);
-          build_dz(k & 1);
-          barrier_lds();  // dzm complete (the prefetch DMA keeps flying)
-          float dsum[4] = {0.f, 0.f, 0.f, 0.f};
-          // rows software-pipelined: the B fragments of row j+1 are read during row j's MFMAs
-          bf16x8 B[2][2][KS];
-          auto loadB = [&](int j, bf16x8 (&Bd)[2][KS]) {
-            const unsigned char* tb = lds + L_DZ + (r0 + j) * ROWB;
+        const long img = (long)n * IMG * 2;
+        if (n == b) {  // the segment's first image: dx from HBM (later images: prefetched)
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-              Bd[0][ks] = *(const bf16x8*)(tb + boff[ks]);
-              Bd[1][ks] = *(const bf16x8*)(tb + 512 + boff[ks]);
-            }
-          };
-          loadB(0, B[0]);
+          for (int j = 0; j < RPW; ++j) dxr[j] = *(const bf16x8*)(din + img + oG + j * ROW_G);
+          barrier_lds();  // wave 7's DMA of x_ltop / masks
+        }
+        // dzm_ltop = dx & mask_ltop into dz tile t
+        {
+          const unsigned char* mt = lds + L_M + (t & 1) * MB;
+#pragma unroll
+          for (int j = 0; j < RPW; ++j)
+            *(u32x4v*)(lds + L_Z + (t & 1) * TILE + oT + j * ROWB) =
+                mask_bf16x8(__builtin_bit_cast(u32x4v, dxr[j]), mt[oM + j * 64]);
+        }
+        bf16x8 A[KS], An[KS];
+        load_wt(wpack + (long)ltop * WSTRIDE, wo, A);
+        barrier_lds();
+        // one layer step; LAST: the image's last layer of the segment (dx out, next image's dx in)
+        auto step = [&](int k, auto last_c) {
+          constexpr bool LAST = decltype(last_c)::value;
+          const int l = ltop - k;
+          const unsigned char* zt = lds + L_Z + (t & 1) * TILE;
+          unsigned char* zn = lds + L_Z + ((t + 1) & 1) * TILE;
+          const unsigned char* mn = lds + L_M + ((t + 1) & 1) * MB;  // mask_{l-1}
+          load_wt(wpack + (long)max(l - 1, 0) * WSTRIDE, wo, An);      // branch-free prefetch
+          const int nn = n + P < N ? n + P : n;
+          const unsigned char* dnext = din + (long)nn * IMG * 2;
+          float dsum[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) dsum[i] = 0.f;
+          Frag fr;
+#pragma unroll
+          for (int R = 0; R < 3; ++R) fr.load(zt, bF, bG, R);
 #pragma unroll
           for (int j = 0; j < RPW; ++j) {
-            const int r = r0 + j;
-            if (j + 1 < RPW) loadB(j + 1, B[(j + 1) & 1]);
-            f32x4 c[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+            if (j + 3 <= RPW + 1) fr.load(zt, bF, bG, j + 3);
+            f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+            row_mfma(A, fr.F[j & 3], fr.F[(j + 1) & 3], fr.F[(j + 2) & 3], fr.G[j & 3], fr.G[(j + 2) & 3], acc);
+            const u32x4v zw = *(const u32x4v*)(zt + oT + j * ROWB);  // dzm_l of the lane's chunk
+            float c[8];
+            regroup(acc[0], acc[1], c);
+            const u32x4v xw = __builtin_bit_cast(u32x4v, dxr[j]);
+            u32x4v ow;
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-              c[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], B[j & 1][0][ks], c[0], 0, 0, 0);
-              c[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], B[j & 1][1][ks], c[1], 0, 0, 0);
+            for (int d = 0; d < 4; ++d) {
+              const float za = lo_f(zw[d]), zb = hi_f(zw[d]);
+              dsum[2 * d] += za;
+              dsum[2 * d + 1] += zb;
+              ow[d] = pk_bf16(fmaf(hs2g, za, fmaf(-h, c[2 * d], lo_f(xw[d]))),
+                              fmaf(hs2g, zb, fmaf(-h, c[2 * d + 1], hi_f(xw[d]))));
             }
-            const unsigned char* tb = lds + L_DZ + r * ROWB;
-#pragma unroll
-            for (int pt = 0; pt < 2; ++pt) {
-              const bf16x4 zr = *(const bf16x4*)(tb + pt * 512 + zoff);
-              unsigned char* dxp = lds + L_DX + (r * W + 16 * pt) * 32 + doff;
-              const bf16x4 dr = *(const bf16x4*)dxp;
-              bf16x4 o4;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const float zf = (float)zr[e];
-                dsum[e] += zf;
-                const float v = fmaf(-h, c[pt][e], (float)dr[e]);
-                o4[e] = (bf16)(hs2g != 0.f ? fmaf(hs2g, zf, v) : v);
-              }
-              *(bf16x4*)dxp = o4;
+            const bf16x8 o = __builtin_bit_cast(bf16x8, ow);
+            if constexpr (!LAST) {
+              *(u32x4v*)(zn + oT + j * ROWB) = mask_bf16x8(ow, mn[oM + j * 64]);
+              dxr[j] = o;
+            } else {
+              *(bf16x8*)(dout + img + oG + j * ROW_G) = o;
+              dxr[j] = *(const bf16x8*)(dnext + oG + j * ROW_G);
             }
           }
-          // db of this layer: the wave's 16 pixel lanes, added to its own slot (no other writer)
+          // db of this layer: sum over the wave's pixels per channel (fixed order:
+          // DPP within 16 lanes, then the partner row), into the wave's own slot
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float v = dsum[e];
-            v += __shfl_xor(v, 1);
-            v += __shfl_xor(v, 2);
-            v += __shfl_xor(v, 4);
-            v += __shfl_xor(v, 8);
-            if (lx == 0) dbs[(k * 4 + wave) * C + 4 * g + e] += v;
+          for (int i = 0; i < 8; ++i) {
+            float v = dsum[i];
+            v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+            v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+            v += dpp<0x141>(v);  // row_half_mirror
+            v += dpp<0x140>(v);  // row_mirror
+            const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+            dsum[i] = __uint_as_float(s[0]) + __uint_as_float(s[1]);
           }
-          if (more) {
+          if (lx == 0 && (g & 1) == 0) {
+            float* d = dbs + (k * 4 + wave) * C + 8 * cg;
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) A[ks] = An[ks];
+            for (int i = 0; i < 8; ++i) d[i] += dsum[i];
           }
-          barrier_vm(0);  // dx updated, dz and x_l consumed; x_{l-1} / mask_{l-1} landed
-        }
-        store_dx(dout, img);
-        barrier_lds();  // dx read out before the next image's DMA overwrites it
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) A[ks] = An[ks];
+          ++t;
+          barrier_lds();  // dz_{l-1} complete, dz_l / x_l consumed
+        };
+        for (int k = 0; k + 1 < kcount; ++k) step(k, std::false_type{});
+        step(kcount - 1, std::true_type{});
       }
       // segment end: db of each layer, the four dgrad waves summed in a fixed order
       __syncthreads();
@@ -386,32 +427,37 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
         }
       __syncthreads();
     }
-  } else {
+  } else if (wave < 7) {
     // ------------------------------ wgrad waves ------------------------------
-    const int kx = wave - 4;  // 0..2; wave 7: prefetch only
-    unsigned to2[2];          // tr-read lane offsets (pixel 8g + 4*(hh ^ (g&1)) + q, channels 4p..4p+3)
+    const int kx = wave - 4;
+    unsigned tx2[2], tz2[2];  // tr-read lane offsets: pixel 8g + 4*(hh ^ (g&1)) + q, channels 4p..4p+3
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) to2[hh] = (unsigned)((8 * g + 4 * (hh ^ (g & 1)) + q) * 32 + 8 * p);
+    for (int hh = 0; hh < 2; ++hh) {
+      const int pix = 8 * g + 4 * (hh ^ (g & 1)) + q;
+      tx2[hh] = (unsigned)(pix * 32 + 8 * p);
+      tz2[hh] = swz(pix + 1, p >> 1) + 8 * (p & 1);
+    }
     f32x4 acc[KSEG][3];
-    // one layer's weight gradient for tap column kx into a[ky] (ky = 0..2): x fragment of
-    // tile row ir feeds output rows ir - ky; reads run DEPTH rows ahead of the MFMAs
-    auto wgrad_layer = [&](f32x4 (&a)[3], int cur) {
+    // one layer's weight gradient for tap column kx into a[ky] (ky = 0..2): the x
+    // fragment of image row ir-1 feeds output rows ir - ky; reads run DEPTH rows
+    // ahead of the MFMAs
+    auto wgrad_layer = [&](f32x4 (&a)[3], int par) {
       constexpr int DEPTH = 2;
-      const unsigned char* xt = lds + L_X + cur * TILE + kx * 32;  // tile column pixel + kx
-      const unsigned char* zt = lds + L_DZ + ROWB + 32;           // dz of output row 0, pixel 0
+      const unsigned char* xt = lds + L_X + par * XT + kx * 32 - ROWB;  // + ir*ROWB: image row ir-1
+      const unsigned char* zt = lds + L_Z + par * TILE + ROWB;          // + d*ROWB: output row d
       bf16x8 Aq[DEPTH + 1], Bq[DEPTH + 1];
-      const bf16x8 Bz = tr2(zt, to2);  // B of output row 0
+      const bf16x8 Bz = tr2(zt, tz2);
 #pragma unroll
       for (int d = 1; d <= DEPTH; ++d) {
-        Aq[d % (DEPTH + 1)] = tr2(xt + d * ROWB, to2);
-        if (d < H) Bq[d % (DEPTH + 1)] = tr2(zt + d * ROWB, to2);
+        Aq[d % (DEPTH + 1)] = tr2(xt + d * ROWB, tx2);
+        if (d < H) Bq[d % (DEPTH + 1)] = tr2(zt + d * ROWB, tz2);
       }
       bf16x8 Bm1 = Bz, Bm2 = Bz;
 #pragma unroll
-      for (int ir = 1; ir <= H; ++ir) {  // tile rows holding image rows 0 .. 31
+      for (int ir = 1; ir <= H; ++ir) {
         if (ir + DEPTH <= H) {
-          Aq[(ir + DEPTH) % (DEPTH + 1)] = tr2(xt + (ir + DEPTH) * ROWB, to2);
-          if (ir + DEPTH < H) Bq[(ir + DEPTH) % (DEPTH + 1)] = tr2(zt + (ir + DEPTH) * ROWB, to2);
+          Aq[(ir + DEPTH) % (DEPTH + 1)] = tr2(xt + (ir + DEPTH) * ROWB, tx2);
+          if (ir + DEPTH < H) Bq[(ir + DEPTH) % (DEPTH + 1)] = tr2(zt + (ir + DEPTH) * ROWB, tz2);
         }
         const bf16x8 Ax = Aq[ir % (DEPTH + 1)];
         if (ir < H) a[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ax, Bq[ir % (DEPTH + 1)], a[0], 0, 0, 0);  // ky=0
@@ -421,38 +467,23 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
         if (ir < H) Bm1 = Bq[ir % (DEPTH + 1)];
       }
     };
+    int t = 0;
     for (int sg = 0; sg < nseg; ++sg) {
       const int ltop = L - 1 - sg * KSEG, kcount = min(KSEG, ltop + 1);
-      const bf16* din = (sg & 1) ? dbufB : dbufA;
 #pragma unroll
       for (int k = 0; k < KSEG; ++k)
 #pragma unroll
-        for (int t = 0; t < 3; ++t) acc[k][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int e = 0; e < 3; ++e) acc[k][e] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int n = b; n < N; n += P) {
-        const long img = (long)n * H * W * C;
-        stage(din, img, ltop, n);
-        barrier_vm(0);
+        if (n == b) barrier_lds();
+        barrier_lds();  // dzm_ltop written
         for (int k = 0; k < kcount; ++k) {
-          const int l = ltop - k, cur = k & 1;
-          if (wave == 7 && k + 1 < kcount) {  // x_{l-1}, mask_{l-1} into the other buffers
-            const unsigned char* xsrc = (const unsigned char*)(xs + (l - 1) * x_stride + img);
-            for (int j = 0; j < 32; ++j)
-              dma16(xsrc + j * 1024 + lane * 16, lds + L_X + (cur ^ 1) * TILE + (j + 1) * ROWB + 32);
-            for (int j = 0; j < 2; ++j)
-              dma16(masks + (l - 1) * mask_stride + (long)n * MB + j * 1024 + lane * 16,
-                    lds + L_M + (cur ^ 1) * MB + j * 1024);
-          }
-          build_dz(cur);
+          static_for<0, KSEG>([&](auto kc) {
+            if (k == decltype(kc)::value) wgrad_layer(acc[decltype(kc)::value], t & 1);
+          });
+          ++t;
           barrier_lds();
-          if (wave < 7) {  // this layer's accumulators (a compile-time index per branch)
-            static_for<0, KSEG>([&](auto kc) {
-              if (k == decltype(kc)::value) wgrad_layer(acc[decltype(kc)::value], cur);
-            });
-          }
-          barrier_vm(0);
         }
-        store_dx((sg & 1) ? dbufA : dbufB, img);
-        barrier_lds();
       }
       // segment end: dW of each layer straight from the accumulators (complete sums)
       __syncthreads();
@@ -460,18 +491,55 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
         constexpr int k = decltype(kc)::value;
         if (k >= kcount) return;
         float* slab = slabs + ((long)(ltop - k) * PS + b) * ES;
-        if (wave < 7) {
 #pragma unroll
-          for (int ky = 0; ky < 3; ++ky)
+        for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) slab[((3 * ky + kx) * 16 + 4 * g + e) * 16 + lx] = h * acc[k][ky][e];
-        } else {
-          for (int j = P + b; j < PS; j += P) {  // padding slabs of the 32-slab reduction groups
-            float* zs = slabs + ((long)(ltop - k) * PS + j) * ES;
-            for (int i = lane; i < ES; i += 64) zs[i] = 0.f;
-          }
-        }
+          for (int e = 0; e < 4; ++e) slab[((3 * ky + kx) * 16 + 4 * g + e) * 16 + lx] = h * acc[k][ky][e];
       });
+      __syncthreads();
+    }
+  } else {
+    // ---------------------------- DMA wave (7) ----------------------------
+    auto dma_x = [&](int l, int n, int par) {
+      const unsigned char* xsrc = (const unsigned char*)(xs + l * x_stride + (long)n * IMG);
+      for (int j = 0; j < H; ++j) dma16(xsrc + j * ROW_G + lane * 16, lds + L_X + par * XT + j * ROWB + 32);
+    };
+    auto dma_m = [&](int l, int n, int par) {
+      const uint8_t* msrc = masks + l * mask_stride + (long)n * MB;
+      for (int j = 0; j < 2; ++j) dma16(msrc + j * 1024 + lane * 16, lds + L_M + par * MB + j * 1024);
+    };
+    int t = 0;
+    for (int sg = 0; sg < nseg; ++sg) {
+      const int ltop = L - 1 - sg * KSEG, kcount = min(KSEG, ltop + 1);
+      for (int n = b; n < N; n += P) {
+        if (n == b) {
+          dma_x(ltop, n, t & 1);
+          dma_m(ltop, n, t & 1);
+          dma_m(max(ltop - 1, 0), n, (t + 1) & 1);
+          barrier_vm(0);
+        }
+        barrier_lds();  // dzm_ltop written
+        const int nn = n + P < N ? n + P : n;
+        for (int k = 0; k < kcount; ++k) {
+          const int l = ltop - k;
+          if (k + 1 < kcount) {
+            dma_x(l - 1, n, (t + 1) & 1);
+            dma_m(max(l - 2, 0), n, t & 1);
+          } else {  // the next image's first layer (a clamped repeat after the segment's last image)
+            dma_x(ltop, nn, (t + 1) & 1);
+            dma_m(ltop, nn, (t + 1) & 1);
+            dma_m(max(ltop - 1, 0), nn, t & 1);
+          }
+          ++t;
+          barrier_vm(0);
+        }
+      }
+      __syncthreads();
+      for (int k = 0; k < kcount; ++k)  // padding slabs of the 32-slab reduction groups
+        for (int j = P + b; j < PS; j += P) {
+          float* zs = slabs + ((long)(ltop - k) * PS + j) * ES;
+          for (int i = lane; i < ES; i += 64) zs[i] = 0.f;
+        }
       __syncthreads();
     }
   }
@@ -488,13 +556,18 @@ int deep16_forward(const void* x0, void* y0, long y_stride, uint8_t* mask0, long
   int cus = cu_count();
   if (cus <= 0) cus = 256;
   const int grid = std::max(1, std::min(N, 2 * cus));
-  const size_t lds = 2 * (size_t)deep::TILE;
-  if (store_all)
-    hipLaunchKernelGGL(deep::k_fwd16_fused<true>, dim3(grid), dim3(64 * deep::NWAVE), lds, s, (const bf16*)x0,
-                       (bf16*)y0, y_stride, mask0, mask_stride, (const bf16*)wpack, bias, bias_stride, h, N, L);
-  else
-    hipLaunchKernelGGL(deep::k_fwd16_fused<false>, dim3(grid), dim3(64 * deep::NWAVE), lds, s, (const bf16*)x0,
-                       (bf16*)y0, y_stride, mask0, mask_stride, (const bf16*)wpack, bias, bias_stride, h, N, L);
+  const size_t lds = 2 * (size_t)deep::TILE + deep::ROWB;
+#define ASR_FWD16(SA, MK)                                                                                      \
+  hipLaunchKernelGGL((deep::k_fwd16_fused<SA, MK>), dim3(grid), dim3(64 * deep::NWAVE), lds, s, (const bf16*)x0, \
+                     (bf16*)y0, y_stride, mask0, mask_stride, (const bf16*)wpack, bias, bias_stride, h, N, L)
+  if (store_all) {
+    if (mask0) ASR_FWD16(true, true);
+    else ASR_FWD16(true, false);
+  } else {
+    if (mask0) ASR_FWD16(false, true);
+    else ASR_FWD16(false, false);
+  }
+#undef ASR_FWD16
   ASR_LAUNCH_CHECK("k_fwd16_fused");
   return ASR_OK;
 }

@@ -4,9 +4,8 @@ blocks in one launch with every 32x32x16 image resident in LDS
 executor).
 
 Checks:
-  * a stack of L blocks equals L single-block calls bitwise (same MFMA
-    accumulation order; the fused launch only keeps x_l in LDS between
-    layers), the relu masks included;
+  * a stack of L blocks equals L single-block calls (asr_conv_forward, which
+    runs the same kernel with L=1) bitwise, the relu masks included;
   * every layer against the oracle's Euler step fed the GPU's own bf16 input
     of that layer (models/tfkeras_resnets.py:69-92 via oracle.euler_fwd):
     2^-8 relative + 4e-3 * max|ref|, relu bits equal wherever |z| is not at
@@ -17,7 +16,7 @@ Checks:
 import numpy as np
 import pytest
 
-from helpers import assert_close, bf16_round, decode_mask
+from helpers import assert_close, bf16_round, decode_mask, rel_l2
 from oracle import asr_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -90,15 +89,17 @@ def test_stack_many_images(rt):
 
 @pytest.mark.parametrize("N,L,gamma", [(3, 5, 0.0), (5, 13, -0.1), (300, 7, 0.0)])
 def test_stack_backward_matches_per_block_and_oracle(rt, N, L, gamma):
-    """The fused backward over the stack (dx resident in LDS, weight
+    """The fused backward over the stack (dx resident in registers, weight
     gradients accumulated per segment in registers) against the per-block
-    backward kernels run layer by layer (asr_conv_backward): dx_0 bitwise
-    equal (same dz masking, same MFMA order, dx rounded to bf16 per layer in
-    both), dtheta / dbias within 1e-5 of max|.| per layer (fp32 summation
-    order); the last layer's dtheta / dbias also against the oracle on the
-    GPU's bf16 inputs (1e-3 of max|.|, the bf16-network tolerance of
-    test_gpu_kernels.py).  L=13 covers two full 6-layer segments and a
-    partial one; N=300 several images per workgroup."""
+    backward kernels run layer by layer (asr_conv_backward, the standard tap
+    order): the fused dgrad sums the 9 taps in its row-reuse order, so dx
+    differs by fp32 summation order before each bf16 rounding -- dx_0 within
+    rel-L2 1e-2 and 2^-6 of max|dx_0| per element; dtheta / dbias of the top
+    layer (identical dzm) within 1e-5 of max|.|, lower layers within rel-L2
+    1e-2; the top layer's dtheta / dbias also against the oracle on the GPU's
+    bf16 inputs (1e-3 of max|.|, the bf16-network tolerance of
+    test_gpu_kernels.py).  L=13 covers a full 12-layer segment and a partial
+    one; N=300 several images per workgroup."""
     h = 8.0 / 30
     x0, w, bias, th, b, pm = _stack_inputs(rt, N, L, gamma, seed=7 * N + L)
     ys, masks = rt.block_stack_forward(x0, w, bias, h)
@@ -111,8 +112,11 @@ def test_stack_backward_matches_per_block_and_oracle(rt, N, L, gamma):
         dx, dth, db, dw = rt.conv_backward(rt.ASR_MODE_EULER, dy, xl.contiguous(), masks[l], w[l:l + 1], pm, h, gamma,
                                            want_dw=(l == L - 1))
         for got, want, what in ((dp[l, :pm.n_theta], dth, "dtheta"), (dp[l, pm.n_theta:], db, "dbias")):
-            a, bb = got.cpu().numpy(), want.cpu().numpy()
-            assert np.abs(a - bb).max() <= 1e-5 * max(np.abs(bb).max(), 1e-30), (l, what, np.abs(a - bb).max())
+            a, bb = got.cpu().numpy().astype(np.float64), want.cpu().numpy().astype(np.float64)
+            if l == L - 1:
+                assert np.abs(a - bb).max() <= 1e-5 * max(np.abs(bb).max(), 1e-30), (l, what, np.abs(a - bb).max())
+            else:
+                assert rel_l2(a, bb) <= 1e-2, (l, what, rel_l2(a, bb))
         if l == L - 1:  # oracle on the GPU's bf16 operands
             xo = xl.float().cpu().numpy().astype(np.float64)
             mk = decode_mask(masks[l].cpu().numpy(), N, 32, 32, 16)
@@ -126,4 +130,6 @@ def test_stack_backward_matches_per_block_and_oracle(rt, N, L, gamma):
             a = dp[l, pm.n_theta:].cpu().numpy()
             assert np.abs(a - db_want).max() <= 1e-3 * max(np.abs(db_want).max(), 1e-30)
         dy = dx
-    assert torch.equal(dx0, dy), "fused dx_0 != per-block dx_0"
+    a, bb = dx0.float().cpu().numpy().astype(np.float64), dy.float().cpu().numpy().astype(np.float64)
+    assert rel_l2(a, bb) <= 1e-2, rel_l2(a, bb)
+    assert np.abs(a - bb).max() <= 2 ** -6 * np.abs(bb).max(), np.abs(a - bb).max()
