@@ -43,6 +43,10 @@ namespace deep {
 
 using namespace blk;
 
+#ifndef ASR_DEEP_EXP
+#define ASR_DEEP_EXP 0  // development A/B only (tools/build_variants.sh): 0 = the product kernels
+#endif
+
 constexpr int C = 16, W = 32, H = 32, TW = W + 2;
 constexpr int ROWB = TW * C * 2;       // 1088 B per tile row (halo columns included)
 constexpr int TILE = (H + 2) * ROWB;   // 36992 B per image tile (halo rows included)
@@ -91,9 +95,14 @@ __device__ __forceinline__ void regroup(const f32x4& c0, const f32x4& c1, float 
 }
 __device__ __forceinline__ float lo_f(unsigned w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hi_f(unsigned w) { return __uint_as_float(w & 0xffff0000u); }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// (a, b) * s + (c, d) on one v_pk_fma_f32
+__device__ __forceinline__ f32x2 pk_fma(float s, f32x2 ab, f32x2 cd) {
+  return __builtin_elementwise_fma((f32x2){s, s}, ab, cd);
+}
 // two fp32 -> packed bf16 pair (RNE, one v_cvt_pk_bf16_f32)
 __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
-  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
   const bf16x2 v = {(bf16)a, (bf16)b};
   return __builtin_bit_cast(unsigned, v);
 }
@@ -196,7 +205,11 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
       for (int j = 0; j < RPW; ++j) {
         if (j + 3 <= RPW + 1) fr.load(src, bF, bG, j + 3);
         f32x4 acc[2] = {{bz[0], bz[1], bz[2], bz[3]}, {bz[0], bz[1], bz[2], bz[3]}};
+#if ASR_DEEP_EXP == 5
+        acc[0][0] += (float)fr.F[j & 3][0][0] + (float)fr.G[(j + 2) & 3][1][3];
+#else
         row_mfma(A, fr.F[j & 3], fr.F[(j + 1) & 3], fr.F[(j + 2) & 3], fr.G[j & 3], fr.G[(j + 2) & 3], acc);
+#endif
         // epilogue on the regrouped chunk: y = x + h * relu(z) (fp32, one rounding),
         // relu bits as TF's ReluGrad (z > 0)
         float z[8];
@@ -208,14 +221,17 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
         for (int d = 0; d < 4; ++d) {
           // relu on the bit pattern: a float is > 0 iff its bits are a positive int
           const int ra = max(__float_as_int(z[2 * d]), 0), rb = max(__float_as_int(z[2 * d + 1]), 0);
-          yw[d] = pk_bf16(fmaf(h, __int_as_float(ra), lo_f(xw[d])), fmaf(h, __int_as_float(rb), hi_f(xw[d])));
+          const f32x2 y2 = pk_fma(h, (f32x2){__int_as_float(ra), __int_as_float(rb)}, (f32x2){lo_f(xw[d]), hi_f(xw[d])});
+          yw[d] = pk_bf16(y2.x, y2.y);
           bits |= min((unsigned)ra, 1u) << (2 * d);
           bits |= min((unsigned)rb, 1u) << (2 * d + 1);
         }
         const bf16x8 y = __builtin_bit_cast(bf16x8, yw);
         *(bf16x8*)(dst + oT + j * ROWB) = y;
+#if ASR_DEEP_EXP != 4
         if (store) *(bf16x8*)(yl + oG + j * ROW_G) = y;
         if (MASK) ml[oM + j * 64] = (uint8_t)bits;
+#endif
         xr[j] = y;
       }
 #pragma unroll
@@ -263,8 +279,8 @@ constexpr int NWB = 8;                   // waves per backward workgroup
 constexpr int ES = 9 * C * C + C;        // slab floats per layer
 constexpr int XT = H * ROWB;             // x tile: 32 image rows x 34 columns
 constexpr int MB = IMG / 8;              // 2 KiB of relu bits per image
-constexpr int L_Z = 0, L_X = L_Z + 2 * TILE + ROWB, L_M = L_X + 2 * XT, L_DBS = L_M + 2 * MB;
-constexpr int L_TOTAL = L_DBS + KSEG * 4 * C * 4;  // [KSEG][4 dgrad waves][C] fp32 db partials
+constexpr int L_Z = 0, L_X = L_Z + 2 * TILE + ROWB, L_M = L_X + 2 * XT, L_TAB = L_M + 2 * MB;
+constexpr int L_TOTAL = L_TAB + 256 * 16;  // mask byte -> 8 x 0xffff/0 bf16 AND masks
 static_assert(L_TOTAL <= 160 * 1024, "LDS budget");
 
 // f(integral_constant<int, k>) for k = K .. N-1: compile-time register-array
@@ -281,23 +297,24 @@ __device__ __forceinline__ bf16x8 tr2(const unsigned char* base, const unsigned 
   return tr_pair(base + o[0], base + o[1]);
 }
 
-// dwords of 0xffff per set bit of the lane's mask byte, ANDed into 8 bf16
-__device__ __forceinline__ u32x4v mask_bf16x8(u32x4v v, unsigned m) {
-  u32x4v r;
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const unsigned lo = (unsigned)((int)(m << (31 - 2 * d)) >> 31);
-    const unsigned hi = (unsigned)((int)(m << (30 - 2 * d)) >> 31);
-    r[d] = v[d] & ((lo & 0xffffu) | (hi & 0xffff0000u));
-  }
-  return r;
+// 8 bf16 ANDed with the relu bits of the lane's mask byte (table: 0xffff per set bit)
+__device__ __forceinline__ u32x4v mask_bf16x8(const unsigned char* lds, u32x4v v, unsigned m) {
+  return v & *(const u32x4v*)(lds + L_TAB + m * 16);
+}
+template <int N>
+__device__ __forceinline__ void barrier_vmt() {  // barrier after all but the N youngest vector-memory ops
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
 }
 
-template <int CTRL>
-__device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
-}
+#if ASR_DEEP_EXP == 8  // development: per-step timestamps of block 0 (waves 0, 4, 7)
+__device__ unsigned long long g_trace[3][160][2];
+#define ASR_TRACE(role, t, which) \
+  if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (t) < 160) g_trace[role][t][which] = __builtin_amdgcn_s_memtime();
+#else
+#define ASR_TRACE(role, t, which)
+#endif
 
+template <bool GAMMA>
 __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ dbufA, bf16* __restrict__ dbufB,
                                                             const bf16* __restrict__ xs, long x_stride,
                                                             const uint8_t* __restrict__ masks, long mask_stride,
@@ -309,9 +326,14 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
   const int P = gridDim.x, b = blockIdx.x;
   // dz tiles, their zero row and the x tiles (halos stay zero)
   for (int i = tid; i < L_M / 16; i += 64 * NWB) ((uint4*)lds)[i] = make_uint4(0, 0, 0, 0);
+  if (tid < 256) {
+    u32x4v e;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) e[d] = ((tid >> (2 * d)) & 1 ? 0xffffu : 0u) | ((tid >> (2 * d + 1)) & 1 ? 0xffff0000u : 0u);
+    *(u32x4v*)(lds + L_TAB + tid * 16) = e;
+  }
   __syncthreads();
   const int nseg = (L + KSEG - 1) / KSEG;
-  float* dbs = (float*)(lds + L_DBS);
 
   if (wave < 4) {
     // ------------------------------ dgrad waves ------------------------------
@@ -330,22 +352,25 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
       const int ltop = L - 1 - sg * KSEG, kcount = min(KSEG, ltop + 1);
       const unsigned char* din = (const unsigned char*)((sg & 1) ? dbufB : dbufA);
       unsigned char* dout = (unsigned char*)((sg & 1) ? dbufA : dbufB);
-      for (int i = lane; i < KSEG * C; i += 64) dbs[(i / C) * 4 * C + wave * C + i % C] = 0.f;
-      bf16x8 dxr[RPW];  // dx_{l+1} of the wave's pixels (regrouped chunks)
+      f32x2 dxf[RPW][4];  // dx_{l+1} of the wave's pixels (regrouped chunks), fp32 between layers
+      bf16x8 dnx[RPW];    // dx at the segment top of the next image (bf16 in HBM)
       for (int n = b; n < N; n += P) {
         const long img = (long)n * IMG * 2;
         if (n == b) {  // the segment's first image: dx from HBM (later images: prefetched)
 #pragma unroll
-          for (int j = 0; j < RPW; ++j) dxr[j] = *(const bf16x8*)(din + img + oG + j * ROW_G);
+          for (int j = 0; j < RPW; ++j) dnx[j] = *(const bf16x8*)(din + img + oG + j * ROW_G);
           barrier_lds();  // wave 7's DMA of x_ltop / masks
         }
         // dzm_ltop = dx & mask_ltop into dz tile t
         {
           const unsigned char* mt = lds + L_M + (t & 1) * MB;
 #pragma unroll
-          for (int j = 0; j < RPW; ++j)
-            *(u32x4v*)(lds + L_Z + (t & 1) * TILE + oT + j * ROWB) =
-                mask_bf16x8(__builtin_bit_cast(u32x4v, dxr[j]), mt[oM + j * 64]);
+          for (int j = 0; j < RPW; ++j) {
+            const u32x4v w = __builtin_bit_cast(u32x4v, dnx[j]);
+            *(u32x4v*)(lds + L_Z + (t & 1) * TILE + oT + j * ROWB) = mask_bf16x8(lds, w, mt[oM + j * 64]);
+#pragma unroll
+            for (int d = 0; d < 4; ++d) dxf[j][d] = (f32x2){lo_f(w[d]), hi_f(w[d])};
+          }
         }
         bf16x8 A[KS], An[KS];
         load_wt(wpack + (long)ltop * WSTRIDE, wo, A);
@@ -353,6 +378,7 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
         // one layer step; LAST: the image's last layer of the segment (dx out, next image's dx in)
         auto step = [&](int k, auto last_c) {
           constexpr bool LAST = decltype(last_c)::value;
+          if (wave == 0) ASR_TRACE(0, t, 0);
           const int l = ltop - k;
           const unsigned char* zt = lds + L_Z + (t & 1) * TILE;
           unsigned char* zn = lds + L_Z + ((t + 1) & 1) * TILE;
@@ -360,9 +386,6 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
           load_wt(wpack + (long)max(l - 1, 0) * WSTRIDE, wo, An);      // branch-free prefetch
           const int nn = n + P < N ? n + P : n;
           const unsigned char* dnext = din + (long)nn * IMG * 2;
-          float dsum[8];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) dsum[i] = 0.f;
           Frag fr;
 #pragma unroll
           for (int R = 0; R < 3; ++R) fr.load(zt, bF, bG, R);
@@ -370,61 +393,40 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
           for (int j = 0; j < RPW; ++j) {
             if (j + 3 <= RPW + 1) fr.load(zt, bF, bG, j + 3);
             f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#if ASR_DEEP_EXP == 2 || ASR_DEEP_EXP == 3 || ASR_DEEP_EXP == 7
+            acc[0][0] = (float)fr.F[j & 3][0][0] + (float)fr.G[(j + 2) & 3][1][3];
+#else
             row_mfma(A, fr.F[j & 3], fr.F[(j + 1) & 3], fr.F[(j + 2) & 3], fr.G[j & 3], fr.G[(j + 2) & 3], acc);
-            const u32x4v zw = *(const u32x4v*)(zt + oT + j * ROWB);  // dzm_l of the lane's chunk
+#endif
+            u32x4v zw;
+            if constexpr (GAMMA) zw = *(const u32x4v*)(zt + oT + j * ROWB);  // dzm_l of the lane's chunk
             float c[8];
             regroup(acc[0], acc[1], c);
-            const u32x4v xw = __builtin_bit_cast(u32x4v, dxr[j]);
             u32x4v ow;
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
-              const float za = lo_f(zw[d]), zb = hi_f(zw[d]);
-              dsum[2 * d] += za;
-              dsum[2 * d + 1] += zb;
-              ow[d] = pk_bf16(fmaf(hs2g, za, fmaf(-h, c[2 * d], lo_f(xw[d]))),
-                              fmaf(hs2g, zb, fmaf(-h, c[2 * d + 1], hi_f(xw[d]))));
+              f32x2 v = pk_fma(-h, (f32x2){c[2 * d], c[2 * d + 1]}, dxf[j][d]);
+              if constexpr (GAMMA) v = pk_fma(hs2g, (f32x2){lo_f(zw[d]), hi_f(zw[d])}, v);
+              dxf[j][d] = v;
+              ow[d] = pk_bf16(v.x, v.y);
             }
-            const bf16x8 o = __builtin_bit_cast(bf16x8, ow);
             if constexpr (!LAST) {
-              *(u32x4v*)(zn + oT + j * ROWB) = mask_bf16x8(ow, mn[oM + j * 64]);
-              dxr[j] = o;
+              *(u32x4v*)(zn + oT + j * ROWB) = mask_bf16x8(lds, ow, mn[oM + j * 64]);
             } else {
-              *(bf16x8*)(dout + img + oG + j * ROW_G) = o;
-              dxr[j] = *(const bf16x8*)(dnext + oG + j * ROW_G);
+              *(u32x4v*)(dout + img + oG + j * ROW_G) = ow;
+              dnx[j] = *(const bf16x8*)(dnext + oG + j * ROW_G);
             }
-          }
-          // db of this layer: sum over the wave's pixels per channel (fixed order:
-          // DPP within 16 lanes, then the partner row), into the wave's own slot
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            float v = dsum[i];
-            v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
-            v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
-            v += dpp<0x141>(v);  // row_half_mirror
-            v += dpp<0x140>(v);  // row_mirror
-            const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-            dsum[i] = __uint_as_float(s[0]) + __uint_as_float(s[1]);
-          }
-          if (lx == 0 && (g & 1) == 0) {
-            float* d = dbs + (k * 4 + wave) * C + 8 * cg;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) d[i] += dsum[i];
           }
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) A[ks] = An[ks];
+          if (wave == 0) ASR_TRACE(0, t, 1);
           ++t;
           barrier_lds();  // dz_{l-1} complete, dz_l / x_l consumed
         };
         for (int k = 0; k + 1 < kcount; ++k) step(k, std::false_type{});
         step(kcount - 1, std::true_type{});
       }
-      // segment end: db of each layer, the four dgrad waves summed in a fixed order
-      __syncthreads();
-      if (tid < C)
-        for (int k = 0; k < kcount; ++k) {
-          const float* d = dbs + k * 4 * C + tid;
-          slabs[((long)(ltop - k) * PS + b) * ES + 9 * C * C + tid] = h * ((d[0] + d[C]) + (d[2 * C] + d[3 * C]));
-        }
+      __syncthreads();  // segment end (slabs written by the wgrad waves and wave 7)
       __syncthreads();
     }
   } else if (wave < 7) {
@@ -478,9 +480,14 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
         if (n == b) barrier_lds();
         barrier_lds();  // dzm_ltop written
         for (int k = 0; k < kcount; ++k) {
+          if (wave == 4) ASR_TRACE(1, t, 0);
           static_for<0, KSEG>([&](auto kc) {
+#if ASR_DEEP_EXP == 1 || ASR_DEEP_EXP == 3 || ASR_DEEP_EXP == 7
+            if (two_gamma == 1234.5f)  // never: the wgrad MFMAs skipped at run time
+#endif
             if (k == decltype(kc)::value) wgrad_layer(acc[decltype(kc)::value], t & 1);
           });
+          if (wave == 4) ASR_TRACE(1, t, 1);
           ++t;
           barrier_lds();
         }
@@ -499,10 +506,45 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
       __syncthreads();
     }
   } else {
-    // ---------------------------- DMA wave (7) ----------------------------
-    auto dma_x = [&](int l, int n, int par) {
+    // -------------------------- x / mask staging wave (7) --------------------------
+    // x of the step after next, rows 0..HS-1: global loads into 64 VGPRs (a third
+    // x buffer, in registers), written to the free LDS x tile one step later, so
+    // those loads have about two layer steps to land; rows HS.. by LDS-DMA one
+    // step ahead; masks by LDS-DMA two layers ahead.  (Staging all 32 rows in
+    // registers trips a register-class error in the ROCm 7.2 compiler.)
+    constexpr int HS = 16;
+    u32x4v st[HS];
+    unsigned tz2[2];  // dz tr-read lane offsets (as the wgrad waves)
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) tz2[hh] = swz(8 * g + 4 * (hh ^ (g & 1)) + q + 1, p >> 1) + 8 * (p & 1);
+    // db of the segment's layers on MFMA: D = ones(16 x 32 pixels) x dzm(32 pixels x 16 o),
+    // one row per MFMA, every D row = the per-channel sum (fixed order)
+    f32x4 dacc[KSEG];
+    const bf16x8 ones = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
+    auto db_layer = [&](f32x4& a, int par) {
+      const unsigned char* zt = lds + L_Z + par * TILE + ROWB;
+      bf16x8 B[4];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) B[d] = tr2(zt + d * ROWB, tz2);
+#pragma unroll
+      for (int d = 0; d < H; ++d) {
+        if (d + 3 < H) B[(d + 3) & 3] = tr2(zt + (d + 3) * ROWB, tz2);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, B[d & 3], a, 0, 0, 0);
+      }
+    };
+    auto load_x = [&](int l, int n) {
+      const unsigned char* src = (const unsigned char*)(xs + l * x_stride + (long)n * IMG) + lane * 16;
+#pragma unroll
+      for (int j = 0; j < HS; ++j) st[j] = *(const u32x4v*)(src + j * ROW_G);
+    };
+    auto write_x = [&](int par) {
+      unsigned char* dst = lds + L_X + par * XT + 32 + lane * 16;
+#pragma unroll
+      for (int j = 0; j < HS; ++j) *(u32x4v*)(dst + j * ROWB) = st[j];
+    };
+    auto dma_x = [&](int l, int n, int par, int j0) {
       const unsigned char* xsrc = (const unsigned char*)(xs + l * x_stride + (long)n * IMG);
-      for (int j = 0; j < H; ++j) dma16(xsrc + j * ROW_G + lane * 16, lds + L_X + par * XT + j * ROWB + 32);
+      for (int j = j0; j < H; ++j) dma16(xsrc + j * ROW_G + lane * 16, lds + L_X + par * XT + j * ROWB + 32);
     };
     auto dma_m = [&](int l, int n, int par) {
       const uint8_t* msrc = masks + l * mask_stride + (long)n * MB;
@@ -511,30 +553,54 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
     int t = 0;
     for (int sg = 0; sg < nseg; ++sg) {
       const int ltop = L - 1 - sg * KSEG, kcount = min(KSEG, ltop + 1);
+#pragma unroll
+      for (int k = 0; k < KSEG; ++k) dacc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int n = b; n < N; n += P) {
+        // later images (clamped repeats past the segment's last image: harmless loads)
+        const int nn = n + P < N ? n + P : n, nnn = nn + P < N ? nn + P : nn;
         if (n == b) {
-          dma_x(ltop, n, t & 1);
+          dma_x(ltop, n, t & 1, 0);
           dma_m(ltop, n, t & 1);
           dma_m(max(ltop - 1, 0), n, (t + 1) & 1);
-          barrier_vm(0);
+          if (kcount > 1) load_x(ltop - 1, n);
+          else load_x(ltop, nn);
+          barrier_vmt<HS>();  // the DMAs landed; the staging loads keep flying
         }
         barrier_lds();  // dzm_ltop written
-        const int nn = n + P < N ? n + P : n;
         for (int k = 0; k < kcount; ++k) {
           const int l = ltop - k;
+          ASR_TRACE(2, t, 0);
+          write_x((t + 1) & 1);  // x of step k+1 (this image's next layer or the next image's top)
           if (k + 1 < kcount) {
-            dma_x(l - 1, n, (t + 1) & 1);
+#if ASR_DEEP_EXP != 6 && ASR_DEEP_EXP != 7
+            dma_x(l - 1, n, (t + 1) & 1, HS);
+#endif
             dma_m(max(l - 2, 0), n, t & 1);
-          } else {  // the next image's first layer (a clamped repeat after the segment's last image)
-            dma_x(ltop, nn, (t + 1) & 1);
+          } else {
+            dma_x(ltop, nn, (t + 1) & 1, HS);
             dma_m(ltop, nn, (t + 1) & 1);
             dma_m(max(ltop - 1, 0), nn, t & 1);
           }
+          const int k2 = k + 2;  // the step after next
+          if (k2 < kcount) load_x(ltop - k2, n);
+          else if (k2 - kcount < kcount) load_x(ltop - (k2 - kcount), nn);
+          else load_x(ltop, nnn);
+          static_for<0, KSEG>([&](auto kc) {
+            if (k == decltype(kc)::value) db_layer(dacc[decltype(kc)::value], t & 1);
+          });
+#if ASR_DEEP_EXP == 8
+          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // trace the DMA landing, not its issue
+#endif
+          ASR_TRACE(2, t, 1);
           ++t;
-          barrier_vm(0);
+          barrier_vmt<HS>();
         }
       }
       __syncthreads();
+      static_for<0, KSEG>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if (k < kcount && g == 0) slabs[((long)(ltop - k) * PS + b) * ES + 9 * C * C + lx] = h * dacc[k][0];
+      });
       for (int k = 0; k < kcount; ++k)  // padding slabs of the 32-slab reduction groups
         for (int j = P + b; j < PS; j += P) {
           float* zs = slabs + ((long)(ltop - k) * PS + j) * ES;
@@ -572,6 +638,12 @@ int deep16_forward(const void* x0, void* y0, long y_stride, uint8_t* mask0, long
   return ASR_OK;
 }
 
+#if ASR_DEEP_EXP == 8
+extern "C" int asr_debug_deep16_trace(void* dst, size_t bytes) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(deep::g_trace), bytes) == hipSuccess ? 0 : -1;
+}
+#endif
+
 int deep16_slab_rows(int N) {
   int cus = cu_count();
   if (cus <= 0) cus = 256;
@@ -592,9 +664,9 @@ int deep16_backward(void* dbufA, void* dbufB, const void* xs, long x_stride, con
   if (cus <= 0) cus = 256;
   const int P = std::max(1, std::min(N, cus));
   const int PS = deep16_slab_rows(N);
-  hipLaunchKernelGGL(deep::k_bwd16_fused, dim3(P), dim3(64 * deep::NWB), (size_t)deep::L_TOTAL, s, (bf16*)dbufA,
-                     (bf16*)dbufB, (const bf16*)xs, x_stride, masks, mask_stride, (const bf16*)wpack, h, two_gamma,
-                     N, L, slabs, PS);
+  auto kern = two_gamma != 0.f ? deep::k_bwd16_fused<true> : deep::k_bwd16_fused<false>;
+  hipLaunchKernelGGL(kern, dim3(P), dim3(64 * deep::NWB), (size_t)deep::L_TOTAL, s, (bf16*)dbufA, (bf16*)dbufB,
+                     (const bf16*)xs, x_stride, masks, mask_stride, (const bf16*)wpack, h, two_gamma, N, L, slabs, PS);
   ASR_LAUNCH_CHECK("k_bwd16_fused");
   *slab_rows = PS;
   *dx0_in_b = ((L + deep::KSEG - 1) / deep::KSEG) & 1;

@@ -89,12 +89,11 @@ def test_stack_many_images(rt):
 
 @pytest.mark.parametrize("N,L,gamma", [(3, 5, 0.0), (5, 13, -0.1), (300, 7, 0.0)])
 def test_stack_backward_matches_per_block_and_oracle(rt, N, L, gamma):
-    """The fused backward over the stack (dx resident in registers, weight
-    gradients accumulated per segment in registers) against the per-block
-    backward kernels run layer by layer (asr_conv_backward, the standard tap
-    order): the fused dgrad sums the 9 taps in its row-reuse order, so dx
-    differs by fp32 summation order before each bf16 rounding -- dx_0 within
-    rel-L2 1e-2 and 2^-6 of max|dx_0| per element; dtheta / dbias of the top
+    """The fused backward over the stack (dx resident in registers in fp32
+    within a segment, weight gradients accumulated per segment in registers)
+    against the per-block backward kernels run layer by layer
+    (asr_conv_backward: dx rounded to bf16 after every layer, the standard tap
+    order): dx_0 within rel-L2 1e-2 and 2^-6 of max|dx_0| per element; dtheta / dbias of the top
     layer (identical dzm) within 1e-5 of max|.|, lower layers within rel-L2
     1e-2; the top layer's dtheta / dbias also against the oracle on the GPU's
     bf16 inputs (1e-3 of max|.|, the bf16-network tolerance of
