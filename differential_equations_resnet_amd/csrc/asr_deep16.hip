@@ -279,8 +279,17 @@ constexpr int NWB = 8;                   // waves per backward workgroup
 constexpr int ES = 9 * C * C + C;        // slab floats per layer
 constexpr int XT = H * ROWB;             // x tile: 32 image rows x 34 columns
 constexpr int MB = IMG / 8;              // 2 KiB of relu bits per image
+// x tile rows [0, XS) reach LDS through wave 7's registers (loaded two steps
+// ahead, written one step ahead); rows [XS, 32) by LDS-DMA two steps ahead into
+// a rotation of three row blocks: the upper rows of the two x tiles and L_E.
+constexpr int XS = 22;
 constexpr int L_Z = 0, L_X = L_Z + 2 * TILE + ROWB, L_M = L_X + 2 * XT, L_TAB = L_M + 2 * MB;
-constexpr int L_TOTAL = L_TAB + 256 * 16;  // mask byte -> 8 x 0xffff/0 bf16 AND masks
+constexpr int L_E = L_TAB + 256 * 16;  // after the mask byte -> 8 x 0xffff/0 bf16 AND-mask table
+constexpr int L_TOTAL = L_E + (H - XS) * ROWB;
+__device__ __forceinline__ int xhi_base(int t) {  // LDS offset of image row XS of step t's x
+  const int r = t % 3;
+  return r == 2 ? L_E : L_X + r * XT + XS * ROWB;
+}
 static_assert(L_TOTAL <= 160 * 1024, "LDS budget");
 
 // f(integral_constant<int, k>) for k = K .. N-1: compile-time register-array
@@ -308,11 +317,33 @@ __device__ __forceinline__ void barrier_vmt() {  // barrier after all but the N 
 
 #if ASR_DEEP_EXP == 8  // development: per-step timestamps of block 0 (waves 0, 4, 7)
 __device__ unsigned long long g_trace[3][160][2];
-#define ASR_TRACE(role, t, which) \
-  if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (t) < 160) g_trace[role][t][which] = __builtin_amdgcn_s_memtime();
+#define ASR_TRACE(role, t, which)                                     \
+  if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (t) < 160) {      \
+    unsigned long long tt_ = __builtin_amdgcn_s_memtime();            \
+    unsigned lo_ = (unsigned)tt_, hi_ = (unsigned)(tt_ >> 32);        \
+    asm volatile("v_mov_b32 %0, %0\n\tv_mov_b32 %1, %1" : "+v"(lo_), "+v"(hi_)); \
+    g_trace[role][t][which] = ((unsigned long long)hi_ << 32) | lo_;  \
+  }
 #else
 #define ASR_TRACE(role, t, which)
 #endif
+
+// The workgroup's layer steps in order: segments sg, its images n = b, b+P, ..,
+// layers ltop(sg) - k.  Every prefetch (x two steps ahead, masks two steps
+// ahead, the next image's dx) follows this stream across image and segment
+// boundaries; past the last step it repeats the last one (harmless reloads).
+struct Pos {
+  int sg, n, k;
+};
+__device__ __forceinline__ int seg_top(int L, int sg) { return L - 1 - sg * KSEG; }
+__device__ __forceinline__ int seg_len(int L, int sg) { return min(KSEG, L - sg * KSEG); }
+__device__ __forceinline__ Pos pos_next(Pos s, int L, int N, int P, int b) {
+  if (s.k + 1 < seg_len(L, s.sg)) return {s.sg, s.n, s.k + 1};
+  if (s.n + P < N) return {s.sg, s.n + P, 0};
+  if ((s.sg + 1) * KSEG < L) return {s.sg + 1, b, 0};
+  return s;
+}
+__device__ __forceinline__ int pos_layer(Pos s, int L) { return seg_top(L, s.sg) - s.k; }
 
 template <bool GAMMA>
 __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ dbufA, bf16* __restrict__ dbufB,
@@ -324,8 +355,9 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, lx = lane & 15, q = lx >> 2, p = lx & 3;
   const int P = gridDim.x, b = blockIdx.x;
-  // dz tiles, their zero row and the x tiles (halos stay zero)
+  // dz tiles, their zero row, the x tiles and the third x row block (halos stay zero)
   for (int i = tid; i < L_M / 16; i += 64 * NWB) ((uint4*)lds)[i] = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < (L_TOTAL - L_E) / 16; i += 64 * NWB) ((uint4*)(lds + L_E))[i] = make_uint4(0, 0, 0, 0);
   if (tid < 256) {
     u32x4v e;
 #pragma unroll
@@ -348,19 +380,16 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
     unsigned wo[KS];
     wt_offsets(lane, wo);
     int t = 0;  // layer steps so far: buffer parity (identical count in every role)
+    f32x2 dxf[RPW][4];  // dx_{l+1} of the wave's pixels (regrouped chunks), fp32 between layers
+    bf16x8 dnx[RPW];    // dx at the segment top of the next image (bf16 in HBM)
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) dnx[j] = *(const bf16x8*)((const unsigned char*)dbufA + (long)b * IMG * 2 + oG + j * ROW_G);
+    barrier_lds();  // prologue: wave 7's DMA of the first x / masks
     for (int sg = 0; sg < nseg; ++sg) {
       const int ltop = L - 1 - sg * KSEG, kcount = min(KSEG, ltop + 1);
-      const unsigned char* din = (const unsigned char*)((sg & 1) ? dbufB : dbufA);
       unsigned char* dout = (unsigned char*)((sg & 1) ? dbufA : dbufB);
-      f32x2 dxf[RPW][4];  // dx_{l+1} of the wave's pixels (regrouped chunks), fp32 between layers
-      bf16x8 dnx[RPW];    // dx at the segment top of the next image (bf16 in HBM)
       for (int n = b; n < N; n += P) {
         const long img = (long)n * IMG * 2;
-        if (n == b) {  // the segment's first image: dx from HBM (later images: prefetched)
-#pragma unroll
-          for (int j = 0; j < RPW; ++j) dnx[j] = *(const bf16x8*)(din + img + oG + j * ROW_G);
-          barrier_lds();  // wave 7's DMA of x_ltop / masks
-        }
         // dzm_ltop = dx & mask_ltop into dz tile t
         {
           const unsigned char* mt = lds + L_M + (t & 1) * MB;
@@ -384,8 +413,9 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
           unsigned char* zn = lds + L_Z + ((t + 1) & 1) * TILE;
           const unsigned char* mn = lds + L_M + ((t + 1) & 1) * MB;  // mask_{l-1}
           load_wt(wpack + (long)max(l - 1, 0) * WSTRIDE, wo, An);      // branch-free prefetch
-          const int nn = n + P < N ? n + P : n;
-          const unsigned char* dnext = din + (long)nn * IMG * 2;
+          const Pos nx = pos_next({sg, n, k}, L, N, P, b);  // the next image's (or segment's) top
+          const unsigned char* dnext =
+              (const unsigned char*)((nx.sg & 1) ? dbufB : dbufA) + (long)nx.n * IMG * 2;
           Frag fr;
 #pragma unroll
           for (int R = 0; R < 3; ++R) fr.load(zt, bF, bG, R);
@@ -443,22 +473,25 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
     // one layer's weight gradient for tap column kx into a[ky] (ky = 0..2): the x
     // fragment of image row ir-1 feeds output rows ir - ky; reads run DEPTH rows
     // ahead of the MFMAs
-    auto wgrad_layer = [&](f32x4 (&a)[3], int par) {
+    auto wgrad_layer = [&](f32x4 (&a)[3], int tt) {
       constexpr int DEPTH = 2;
-      const unsigned char* xt = lds + L_X + par * XT + kx * 32 - ROWB;  // + ir*ROWB: image row ir-1
+      const int par = tt & 1;
+      const unsigned char* xt = lds + L_X + par * XT + kx * 32 - ROWB;  // + ir*ROWB: image row ir-1 < XS
+      const unsigned char* xh = lds + xhi_base(tt) - XS * ROWB + kx * 32 - ROWB;  // image rows >= XS
       const unsigned char* zt = lds + L_Z + par * TILE + ROWB;          // + d*ROWB: output row d
+      auto xrow = [&](int ir) { return (ir - 1 < XS ? xt : xh) + ir * ROWB; };
       bf16x8 Aq[DEPTH + 1], Bq[DEPTH + 1];
       const bf16x8 Bz = tr2(zt, tz2);
 #pragma unroll
       for (int d = 1; d <= DEPTH; ++d) {
-        Aq[d % (DEPTH + 1)] = tr2(xt + d * ROWB, tx2);
+        Aq[d % (DEPTH + 1)] = tr2(xrow(d), tx2);
         if (d < H) Bq[d % (DEPTH + 1)] = tr2(zt + d * ROWB, tz2);
       }
       bf16x8 Bm1 = Bz, Bm2 = Bz;
 #pragma unroll
       for (int ir = 1; ir <= H; ++ir) {
         if (ir + DEPTH <= H) {
-          Aq[(ir + DEPTH) % (DEPTH + 1)] = tr2(xt + (ir + DEPTH) * ROWB, tx2);
+          Aq[(ir + DEPTH) % (DEPTH + 1)] = tr2(xrow(ir + DEPTH), tx2);
           if (ir + DEPTH < H) Bq[(ir + DEPTH) % (DEPTH + 1)] = tr2(zt + (ir + DEPTH) * ROWB, tz2);
         }
         const bf16x8 Ax = Aq[ir % (DEPTH + 1)];
@@ -470,6 +503,7 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
       }
     };
     int t = 0;
+    barrier_lds();  // prologue
     for (int sg = 0; sg < nseg; ++sg) {
       const int ltop = L - 1 - sg * KSEG, kcount = min(KSEG, ltop + 1);
 #pragma unroll
@@ -477,7 +511,6 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
 #pragma unroll
         for (int e = 0; e < 3; ++e) acc[k][e] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int n = b; n < N; n += P) {
-        if (n == b) barrier_lds();
         barrier_lds();  // dzm_ltop written
         for (int k = 0; k < kcount; ++k) {
           if (wave == 4) ASR_TRACE(1, t, 0);
@@ -485,7 +518,7 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
 #if ASR_DEEP_EXP == 1 || ASR_DEEP_EXP == 3 || ASR_DEEP_EXP == 7
             if (two_gamma == 1234.5f)  // never: the wgrad MFMAs skipped at run time
 #endif
-            if (k == decltype(kc)::value) wgrad_layer(acc[decltype(kc)::value], t & 1);
+            if (k == decltype(kc)::value) wgrad_layer(acc[decltype(kc)::value], t);
           });
           if (wave == 4) ASR_TRACE(1, t, 1);
           ++t;
@@ -507,12 +540,13 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
     }
   } else {
     // -------------------------- x / mask staging wave (7) --------------------------
-    // x of the step after next, rows 0..HS-1: global loads into 64 VGPRs (a third
-    // x buffer, in registers), written to the free LDS x tile one step later, so
-    // those loads have about two layer steps to land; rows HS.. by LDS-DMA one
-    // step ahead; masks by LDS-DMA two layers ahead.  (Staging all 32 rows in
-    // registers trips a register-class error in the ROCm 7.2 compiler.)
-    constexpr int HS = 16;
+    // x of the step after next: rows 0..XS-1 by global loads into registers (a
+    // third x buffer), written to the free LDS x tile one step later; rows XS..
+    // by LDS-DMA into the rotating third row block; so every x load has about
+    // two layer steps to land.  Masks by LDS-DMA two steps ahead; db of each
+    // layer on MFMA.
+    constexpr int HS = XS;
+    const unsigned lb = lds_u32(lds);  // LDS byte address of the dynamic allocation
     u32x4v st[HS];
     unsigned tz2[2];  // dz tr-read lane offsets (as the wgrad waves)
 #pragma unroll
@@ -532,8 +566,8 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
         a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, B[d & 3], a, 0, 0, 0);
       }
     };
-    auto load_x = [&](int l, int n) {
-      const unsigned char* src = (const unsigned char*)(xs + l * x_stride + (long)n * IMG) + lane * 16;
+    auto load_x = [&](Pos s) {
+      const unsigned char* src = (const unsigned char*)(xs + pos_layer(s, L) * x_stride + (long)s.n * IMG) + lane * 16;
 #pragma unroll
       for (int j = 0; j < HS; ++j) st[j] = *(const u32x4v*)(src + j * ROW_G);
     };
@@ -542,58 +576,47 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
 #pragma unroll
       for (int j = 0; j < HS; ++j) *(u32x4v*)(dst + j * ROWB) = st[j];
     };
-    auto dma_x = [&](int l, int n, int par, int j0) {
-      const unsigned char* xsrc = (const unsigned char*)(xs + l * x_stride + (long)n * IMG);
-      for (int j = j0; j < H; ++j) dma16(xsrc + j * ROW_G + lane * 16, lds + L_X + par * XT + j * ROWB + 32);
+    auto dma_x = [&](Pos s, int j0, int tt) {  // rows j0.. of step tt's x (rows < XS: tile tt & 1)
+      const unsigned char* xsrc = (const unsigned char*)(xs + pos_layer(s, L) * x_stride + (long)s.n * IMG);
+      const unsigned hb = lb + xhi_base(tt) - XS * ROWB + 32, lo = lb + L_X + (tt & 1) * XT + 32;
+      for (int j = j0; j < H; ++j) dma16_at(xsrc + j * ROW_G + lane * 16, (j < XS ? lo : hb) + j * ROWB);
     };
-    auto dma_m = [&](int l, int n, int par) {
-      const uint8_t* msrc = masks + l * mask_stride + (long)n * MB;
-      for (int j = 0; j < 2; ++j) dma16(msrc + j * 1024 + lane * 16, lds + L_M + par * MB + j * 1024);
+    auto dma_m = [&](Pos s, int par) {
+      const uint8_t* msrc = masks + pos_layer(s, L) * mask_stride + (long)s.n * MB;
+      for (int j = 0; j < 2; ++j) dma16_at(msrc + j * 1024 + lane * 16, lb + L_M + par * MB + j * 1024);
     };
     int t = 0;
+    {  // prologue: the first step's x and masks, the next step's x and mask
+      const Pos p0 = {0, b, 0}, p1 = pos_next(p0, L, N, P, b);
+      dma_x(p0, 0, 0);
+      dma_m(p0, 0);
+      dma_m(p1, 1);
+      dma_x(p1, XS, 1);
+      load_x(p1);
+      barrier_vmt<HS + H - XS>();  // the first x and masks landed; the next x keeps flying
+    }
     for (int sg = 0; sg < nseg; ++sg) {
       const int ltop = L - 1 - sg * KSEG, kcount = min(KSEG, ltop + 1);
 #pragma unroll
       for (int k = 0; k < KSEG; ++k) dacc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int n = b; n < N; n += P) {
-        // later images (clamped repeats past the segment's last image: harmless loads)
-        const int nn = n + P < N ? n + P : n, nnn = nn + P < N ? nn + P : nn;
-        if (n == b) {
-          dma_x(ltop, n, t & 1, 0);
-          dma_m(ltop, n, t & 1);
-          dma_m(max(ltop - 1, 0), n, (t + 1) & 1);
-          if (kcount > 1) load_x(ltop - 1, n);
-          else load_x(ltop, nn);
-          barrier_vmt<HS>();  // the DMAs landed; the staging loads keep flying
-        }
         barrier_lds();  // dzm_ltop written
         for (int k = 0; k < kcount; ++k) {
-          const int l = ltop - k;
           ASR_TRACE(2, t, 0);
-          write_x((t + 1) & 1);  // x of step k+1 (this image's next layer or the next image's top)
-          if (k + 1 < kcount) {
-#if ASR_DEEP_EXP != 6 && ASR_DEEP_EXP != 7
-            dma_x(l - 1, n, (t + 1) & 1, HS);
-#endif
-            dma_m(max(l - 2, 0), n, t & 1);
-          } else {
-            dma_x(ltop, nn, (t + 1) & 1, HS);
-            dma_m(ltop, nn, (t + 1) & 1);
-            dma_m(max(ltop - 1, 0), nn, t & 1);
-          }
-          const int k2 = k + 2;  // the step after next
-          if (k2 < kcount) load_x(ltop - k2, n);
-          else if (k2 - kcount < kcount) load_x(ltop - (k2 - kcount), nn);
-          else load_x(ltop, nnn);
+          const Pos n1 = pos_next({sg, n, k}, L, N, P, b), n2 = pos_next(n1, L, N, P, b);
+          write_x((t + 1) & 1);  // x of the next step
+          dma_m(n2, t & 1);      // mask of the step after next (read by the next step's dgrad epilogue)
+          dma_x(n2, XS, t + 2);  // upper x rows of the step after next
+          load_x(n2);
           static_for<0, KSEG>([&](auto kc) {
             if (k == decltype(kc)::value) db_layer(dacc[decltype(kc)::value], t & 1);
           });
 #if ASR_DEEP_EXP == 8
-          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // trace the DMA landing, not its issue
+          asm volatile("s_waitcnt vmcnt(32)" ::: "memory");  // trace the mask DMA landing, not its issue
 #endif
           ASR_TRACE(2, t, 1);
           ++t;
-          barrier_vmt<HS>();
+          barrier_vmt<HS + H - XS>();  // the masks (and the previous step's x DMA) landed
         }
       }
       __syncthreads();

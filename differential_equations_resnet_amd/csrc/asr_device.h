@@ -46,6 +46,20 @@ __device__ __forceinline__ void dma16(const void* src, unsigned char* lds_wave_b
 #endif
 }
 
+// dma16 with the wave-uniform LDS byte address given directly (no generic ->
+// LDS pointer conversion, whose null check trips a ROCm 7.2 codegen bug in
+// register-tight kernels)
+__device__ __forceinline__ void dma16_at(const void* src, unsigned lds_addr) {
+  const unsigned l = __builtin_amdgcn_readfirstlane(lds_addr);
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off"
+      :
+      : "v"(src), "s"(l)
+      : "memory", "m0");
+}
+
 // Workgroup barrier that waits only for this wave's vector-memory ops OLDER
 // than its `n` youngest (vmcnt counts loads, stores and LDS-DMA in issue
 // order).  Used so that the barrier guarding an LDS-DMA'd buffer does not
