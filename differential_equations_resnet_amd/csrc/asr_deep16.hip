@@ -101,6 +101,13 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 pk_fma(float s, f32x2 ab, f32x2 cd) {
   return __builtin_elementwise_fma((f32x2){s, s}, ab, cd);
 }
+// 1 if v > 0 else 0 (v_med3_i32; in asm so that the compiler does not turn the
+// following shift into a compare + select per bit)
+__device__ __forceinline__ unsigned bit01(int v) {
+  unsigned r;
+  asm("v_med3_i32 %0, %1, 0, 1" : "=v"(r) : "v"(v));
+  return r;
+}
 // two fp32 -> packed bf16 pair (RNE, one v_cvt_pk_bf16_f32)
 __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
   const bf16x2 v = {(bf16)a, (bf16)b};
@@ -192,6 +199,8 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
       const int ln = min(l + 1, L - 1);
       float bn[4];
       // next layer's W^T fragments and bias (L2-resident) while this one runs
+      // (copied to A / bz at the layer end: alternating two register sets
+      // instead makes this kernel spill)
       load_wt(wpack + (long)ln * WSTRIDE, wo, An);
 #pragma unroll
       for (int e = 0; e < 4; ++e) bn[e] = bsrc[ln * bstr + 4 * g + e];
@@ -221,10 +230,9 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
         for (int d = 0; d < 4; ++d) {
           // relu on the bit pattern: a float is > 0 iff its bits are a positive int
           const int ra = max(__float_as_int(z[2 * d]), 0), rb = max(__float_as_int(z[2 * d + 1]), 0);
-          const f32x2 y2 = pk_fma(h, (f32x2){__int_as_float(ra), __int_as_float(rb)}, (f32x2){lo_f(xw[d]), hi_f(xw[d])});
-          yw[d] = pk_bf16(y2.x, y2.y);
-          bits |= min((unsigned)ra, 1u) << (2 * d);
-          bits |= min((unsigned)rb, 1u) << (2 * d + 1);
+          yw[d] = pk_bf16(fmaf(h, __int_as_float(ra), lo_f(xw[d])), fmaf(h, __int_as_float(rb), hi_f(xw[d])));
+          bits |= bit01(ra) << (2 * d);
+          bits |= bit01(rb) << (2 * d + 1);
         }
         const bf16x8 y = __builtin_bit_cast(bf16x8, yw);
         *(bf16x8*)(dst + oT + j * ROWB) = y;
@@ -316,7 +324,7 @@ __device__ __forceinline__ void barrier_vmt() {  // barrier after all but the N 
 }
 
 #if ASR_DEEP_EXP == 8  // development: per-step timestamps of block 0 (waves 0, 4, 7)
-__device__ unsigned long long g_trace[3][160][2];
+__device__ unsigned long long g_trace[3][160][4];
 #define ASR_TRACE(role, t, which)                                     \
   if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (t) < 160) {      \
     unsigned long long tt_ = __builtin_amdgcn_s_memtime();            \
@@ -401,11 +409,12 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
             for (int d = 0; d < 4; ++d) dxf[j][d] = (f32x2){lo_f(w[d]), hi_f(w[d])};
           }
         }
-        bf16x8 A[KS], An[KS];
-        load_wt(wpack + (long)ltop * WSTRIDE, wo, A);
+        bf16x8 A0[KS], A1[KS];
+        load_wt(wpack + (long)ltop * WSTRIDE, wo, A0);
         barrier_lds();
-        // one layer step; LAST: the image's last layer of the segment (dx out, next image's dx in)
-        auto step = [&](int k, auto last_c) {
+        // one layer step; LAST: the image's last layer of the segment (dx out, next
+        // image's dx in); A this layer's W^T, An receives the next layer's
+        auto step = [&](int k, auto last_c, bf16x8 (&A)[KS], bf16x8 (&An)[KS]) {
           constexpr bool LAST = decltype(last_c)::value;
           if (wave == 0) ASR_TRACE(0, t, 0);
           const int l = ltop - k;
@@ -447,14 +456,21 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
               dnx[j] = *(const bf16x8*)(dnext + oG + j * ROW_G);
             }
           }
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) A[ks] = An[ks];
           if (wave == 0) ASR_TRACE(0, t, 1);
           ++t;
           barrier_lds();  // dz_{l-1} complete, dz_l / x_l consumed
         };
-        for (int k = 0; k + 1 < kcount; ++k) step(k, std::false_type{});
-        step(kcount - 1, std::true_type{});
+        int k = 0;
+        for (; k + 2 < kcount; k += 2) {  // the two register sets alternate
+          step(k, std::false_type{}, A0, A1);
+          step(k + 1, std::false_type{}, A1, A0);
+        }
+        if (k + 1 < kcount) {
+          step(k, std::false_type{}, A0, A1);
+          step(k + 1, std::true_type{}, A1, A0);
+        } else {
+          step(k, std::true_type{}, A0, A1);
+        }
       }
       __syncthreads();  // segment end (slabs written by the wgrad waves and wave 7)
       __syncthreads();
@@ -543,8 +559,8 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
     // x of the step after next: rows 0..XS-1 by global loads into registers (a
     // third x buffer), written to the free LDS x tile one step later; rows XS..
     // by LDS-DMA into the rotating third row block; so every x load has about
-    // two layer steps to land.  Masks by LDS-DMA two steps ahead; db of each
-    // layer on MFMA.
+    // two layer steps to land.  Masks likewise through registers (three steps
+    // ahead of the dgrad epilogue that reads them); db of each layer on MFMA.
     constexpr int HS = XS;
     const unsigned lb = lds_u32(lds);  // LDS byte address of the dynamic allocation
     u32x4v st[HS];
@@ -581,19 +597,30 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
       const unsigned hb = lb + xhi_base(tt) - XS * ROWB + 32, lo = lb + L_X + (tt & 1) * XT + 32;
       for (int j = j0; j < H; ++j) dma16_at(xsrc + j * ROW_G + lane * 16, (j < XS ? lo : hb) + j * ROWB);
     };
+    u32x4v mst[2];  // a mask (2 KiB) staged in registers, as the x rows
+    auto load_m = [&](Pos s) {
+      const unsigned char* src = masks + pos_layer(s, L) * mask_stride + (long)s.n * MB + lane * 16;
+      mst[0] = *(const u32x4v*)src;
+      mst[1] = *(const u32x4v*)(src + 1024);
+    };
+    auto write_m = [&](int par) {
+      *(u32x4v*)(lds + L_M + par * MB + lane * 16) = mst[0];
+      *(u32x4v*)(lds + L_M + par * MB + 1024 + lane * 16) = mst[1];
+    };
     auto dma_m = [&](Pos s, int par) {
       const uint8_t* msrc = masks + pos_layer(s, L) * mask_stride + (long)s.n * MB;
       for (int j = 0; j < 2; ++j) dma16_at(msrc + j * 1024 + lane * 16, lb + L_M + par * MB + j * 1024);
     };
     int t = 0;
     {  // prologue: the first step's x and masks, the next step's x and mask
-      const Pos p0 = {0, b, 0}, p1 = pos_next(p0, L, N, P, b);
+      const Pos p0 = {0, b, 0}, p1 = pos_next(p0, L, N, P, b), p2 = pos_next(p1, L, N, P, b);
       dma_x(p0, 0, 0);
       dma_m(p0, 0);
       dma_m(p1, 1);
       dma_x(p1, XS, 1);
       load_x(p1);
-      barrier_vmt<HS + H - XS>();  // the first x and masks landed; the next x keeps flying
+      load_m(p2);
+      barrier_vmt<H + 2>();  // the first x and masks landed; the next ones keep flying
     }
     for (int sg = 0; sg < nseg; ++sg) {
       const int ltop = L - 1 - sg * KSEG, kcount = min(KSEG, ltop + 1);
@@ -603,20 +630,34 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
         barrier_lds();  // dzm_ltop written
         for (int k = 0; k < kcount; ++k) {
           ASR_TRACE(2, t, 0);
-          const Pos n1 = pos_next({sg, n, k}, L, N, P, b), n2 = pos_next(n1, L, N, P, b);
+          const Pos n1 = pos_next({sg, n, k}, L, N, P, b), n2 = pos_next(n1, L, N, P, b),
+                    n3 = pos_next(n2, L, N, P, b);
           write_x((t + 1) & 1);  // x of the next step
-          dma_m(n2, t & 1);      // mask of the step after next (read by the next step's dgrad epilogue)
+          write_m(t & 1);        // mask of the step after next (read by the next step's dgrad epilogue)
+#if ASR_DEEP_EXP == 8
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+          ASR_TRACE(2, t, 2);
           dma_x(n2, XS, t + 2);  // upper x rows of the step after next
           load_x(n2);
+          load_m(n3);
           static_for<0, KSEG>([&](auto kc) {
             if (k == decltype(kc)::value) db_layer(dacc[decltype(kc)::value], t & 1);
           });
 #if ASR_DEEP_EXP == 8
-          asm volatile("s_waitcnt vmcnt(32)" ::: "memory");  // trace the mask DMA landing, not its issue
+          {
+            float sink = dacc[0][0];
+            asm volatile("s_nop 0" : "+v"(sink));
+            dacc[0][0] = sink;
+          }
+#endif
+          ASR_TRACE(2, t, 3);
+#if ASR_DEEP_EXP == 8
+          asm volatile("s_waitcnt vmcnt(34)" ::: "memory");  // trace the x DMA landing, not its issue
 #endif
           ASR_TRACE(2, t, 1);
           ++t;
-          barrier_vmt<HS + H - XS>();  // the masks (and the previous step's x DMA) landed
+          barrier_vmt<H + 2>();  // the previous step's x DMA landed; this step's loads keep flying
         }
       }
       __syncthreads();

@@ -35,9 +35,10 @@ for _ in range(3):
     rt.block_stack_backward(dyL, x0, ys, masks, w, pm, h, 0.0)
 torch.cuda.synchronize()
 lib = ctypes.CDLL(path)
-buf = (ctypes.c_uint64 * (3 * 160 * 2))()
+buf = (ctypes.c_uint64 * (3 * 160 * 4))()
 assert lib.asr_debug_deep16_trace(buf, ctypes.sizeof(buf)) == 0
-tr = np.frombuffer(buf, np.uint64).reshape(3, 160, 2).astype(np.int64)
+tr4 = np.frombuffer(buf, np.uint64).reshape(3, 160, 4).astype(np.int64)
+tr = tr4[:, :, :2]
 t0 = tr[tr > 0].min()
 names = ["dgrad0", "wgrad4", "stage7"]
 print("step " + " ".join(f"{n + ' start':>13} {'busy':>6}" for n in names) + "   step_len")
@@ -55,3 +56,7 @@ for r in range(3):
 s = tr[0, 5:100, 0]
 s = s[s > 0]
 print("median step", int(np.median(np.diff(s))))
+v = tr4[2, 5:100]
+v = v[v[:, 0] > 0]
+print("stage7 median: start->written", int(np.median(v[:, 2] - v[:, 0])), " written->db done", int(np.median(v[:, 3] - v[:, 2])),
+      " db done->x DMA landed", int(np.median(v[:, 1] - v[:, 3])))
