@@ -196,6 +196,70 @@ def block_roofline(rt, lib, C, N, dtype_name, reps, h, integrator="euler"):
                 bytes_fwd=2 * P * esz, bytes_bwd=3 * P * esz)
 
 
+def stack_roofline(rt, N, L, reps, h):
+    """The deep C=16 path (asr_deep16.hip): all L Euler blocks fused in one
+    forward and one backward launch, timed at the workload shape on random
+    operands with HIP events on the launch stream (torch's current stream).
+
+    Algorithmic bytes per image (extended to the fused stack):
+    forward reads x_0 and writes every x_l and its relu mask (the backward
+    needs them): s·P + L·(s·P + P/8); backward reads every x_l and mask, dL/dx_L,
+    and writes dx_0: L·(s·P + P/8) + 2·s·P (P = 32·32·16, s = 2 B)."""
+    import torch
+    dev = torch.device("cuda")
+    C = 16
+    g = torch.Generator(device=dev).manual_seed(7)
+    pm = rt.param_map(C)
+    w = rt.theta_to_w(torch.randn(L * pm.n_theta, device=dev, generator=g) * 0.05, C, pm, 0.0, rt.ASR_BF16,
+                      layers=L)
+    bias = torch.randn(L, C, device=dev, generator=g) * 0.1
+    x0 = torch.randn(N, 32, 32, C, device=dev, generator=g).to(torch.bfloat16)
+    dyL = (torch.randn(N, 32, 32, C, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+    from differential_equations_resnet_amd import _lib
+    P = 32 * 32 * C
+    mb = rt.mask_bytes(N, 32, 32, C)
+    xs = torch.empty((L + 1, N, 32, 32, C), dtype=torch.bfloat16, device=dev)  # x_0, .., x_L: one stack
+    xs[0].copy_(x0)
+    masks = torch.empty((L, mb), dtype=torch.uint8, device=dev)
+    wsb = int(_lib.load().asr_block_stack_backward_workspace_bytes(N, 32, 32, C, L, rt.ASR_BF16))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    dx0 = torch.empty_like(x0)
+    dparams = torch.empty(L, pm.n_theta + C, dtype=torch.float32, device=dev)
+    _, theta_dst = pm.device(dev)
+    s = torch.cuda.current_stream().cuda_stream
+    per = w[0].numel()
+
+    def fwd():  # writes x_1 .. x_L behind x_0 and the L masks
+        _lib.call("asr_block_stack_forward", xs[0].data_ptr(), xs[1].data_ptr(), N * P, masks.data_ptr(), mb,
+                  w.data_ptr(), per, bias.data_ptr(), C, float(h), N, 32, 32, C, L, rt.ASR_BF16, 1, s)
+
+    def bwd():  # incl. the slab reduction and projection onto theta
+        _lib.call("asr_block_stack_backward", dyL.data_ptr(), xs.data_ptr(), N * P, masks.data_ptr(), mb,
+                  w.data_ptr(), per, theta_dst.data_ptr(), pm.n_theta, float(h), 0.0, N, 32, 32, C, L,
+                  rt.ASR_BF16, dx0.data_ptr(), dparams.data_ptr(), ws.data_ptr(), wsb, s)
+
+    fwd()
+    bwd()
+    torch.cuda.synchronize()
+
+    def timed(fn):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e-3
+
+    tf = timed(fwd)
+    tb = timed(bwd)
+    act = L * (2 * P + P // 8)
+    bytes_fwd, bytes_bwd = N * (2 * P + act), N * (act + 4 * P)
+    flops = 3 * 2 * 9 * C * C * 32 * 32 * N * L
+    return dict(t_fwd=tf, t_bwd=tb, t=tf + tb, bytes=bytes_fwd + bytes_bwd, flops=flops, bytes_fwd=bytes_fwd,
+                bytes_bwd=bytes_bwd)
+
+
 def cpu_baseline(threads):
     """The oracle's PyTorch-CPU restatements of the reference TF graph
     (oracle/torch_cpu_ref.py), timed on this box's host cores: the metric's
@@ -343,14 +407,20 @@ def main():
     value = N * world * args.steps / elapsed
 
     if rank == 0:
-        rb = block_roofline(rt, lib, C, N, dtype_name, args.block_reps, h, integrator)
+        deep = C == 16 and dtype_name == "bfloat16" and integrator == "euler"  # the fused-stack path
+        if deep:
+            rb = stack_roofline(rt, N, L, max(2, args.block_reps // 10), h)
+        else:
+            rb = block_roofline(rt, lib, C, N, dtype_name, args.block_reps, h, integrator)
         achieved = rb["bytes"] / rb["t"] / 1e9
         tflops = rb["flops"] / rb["t"] / 1e12
         peak_tf = BF16_PEAK_TFLOPS if dtype_name == "bfloat16" else F32_PEAK_TFLOPS
         traffic, traffic_src = traffic_record(args.config)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": ("RK2 block fwd+bwd (2x blk::k_fwd_pipe, blk::k_bwd2 stage 2 + blk::k_bwd2<XT> stage 1 on "
+                "kernel": ("fused stack of all L Euler blocks, fwd + bwd (deep::k_fwd16_fused, deep::k_bwd16_fused, "
+                           "k_reduce_slabs, k_project_layers)" if deep else
+                           "RK2 block fwd+bwd (2x blk::k_fwd_pipe, blk::k_bwd2 stage 2 + blk::k_bwd2<XT> stage 1 on "
                            "one slab set, k_reduce_slabs, k_project)" if integrator == "rk2" else
                            "Euler block fwd+bwd (blk::k_fwd_pipe, blk::k_bwd2 fused dgrad+wgrad, k_reduce_slabs, "
                            "k_project)"),
@@ -360,7 +430,10 @@ def main():
                 "kernels": {"fwd": {"avg_us": round(rb["t_fwd"] * 1e6, 2), "algorithmic_bytes": rb["bytes_fwd"],
                                     "frac": round(rb["bytes_fwd"] / rb["t_fwd"] / 1e9 / HBM_PEAK_GBS, 4)},
                             "bwd_with_reduction": {"avg_us": round(rb["t_bwd"] * 1e6, 2)}}}
-        if rb["t_bwd_kernel"] is not None:
+        if deep:
+            roof["kernels"]["bwd_with_reduction"]["algorithmic_bytes"] = rb["bytes_bwd"]
+            roof["kernels"]["bwd_with_reduction"]["frac"] = round(rb["bytes_bwd"] / rb["t_bwd"] / 1e9 / HBM_PEAK_GBS, 4)
+        elif rb["t_bwd_kernel"] is not None:
             roof["kernels"]["bwd"] = {"avg_us": round(rb["t_bwd_kernel"] * 1e6, 2),
                                       "algorithmic_bytes": rb["bytes_bwd"],
                                       "frac": round(rb["bytes_bwd"] / rb["t_bwd_kernel"] / 1e9 / HBM_PEAK_GBS, 4)}
