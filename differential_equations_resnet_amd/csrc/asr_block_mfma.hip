@@ -1931,7 +1931,7 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
 }
 
 // ===========================================================================
-// Stem weight gradient on MFMA (C=64, CIN=3, W=32, H % 8 == 0), from dz1 =
+// Stem weight gradient on MFMA (C = 16 or 64, CIN=3, W=32, H % 8 == 0), from dz1 =
 // dx1 * [x1 > 0] (written by the first block's backward, k_bwd2<..., RO>):
 //   dW1[kappa][o] = inv_std * sum_p (img[p + tap] - mean)[ci] * dz1[p][o]
 //   db1[o]        = sum_p dz1[p][o]
@@ -1944,11 +1944,11 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
 // double-buffered; both operands come from transposed LDS reads exactly as
 // in the blocks' weight gradient.  One slab [dW1 (27*C) | db1 (C)] per WG.
 // ===========================================================================
-template <typename Tin>
+template <int C, typename Tin>
 __global__ __launch_bounds__(256) void k_stem_wgrad_mfma(const Tin* __restrict__ img, const bf16* __restrict__ dz1,
                                                          int N, int H, float mean, float inv_std,
                                                          float* __restrict__ slabs) {
-  constexpr int C = 64, W = 32, CIN = 3, TW = W + 2, BRS = 8, KC = 9 * CIN;
+  constexpr int W = 32, CIN = 3, TW = W + 2, BRS = 8, KC = 9 * CIN, NT = C / 16;
   constexpr int IMROW = TW * 4 * 16, DZROW = TW * (C / 8) * 16, DZT = BRS * DZROW;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int IM = 0, DZ0 = H * IMROW, FT = DZ0 + 2 * DZT;  // im2col | 2 dz1 bands | staged image (fp32, halo)
@@ -1957,11 +1957,11 @@ __global__ __launch_bounds__(256) void k_stem_wgrad_mfma(const Tin* __restrict__
   const int g = lane >> 4, lx = lane & 15, tq = lx >> 2, tp = lx & 3;
   const int nbands = H / BRS;
   for (int i = tid; i < (H + 2) * TW * CIN; i += 256) ft[i] = 0.f;  // halo stays zero
-  f32x4 acc[2][4];
+  f32x4 acc[2][NT];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int n0 = blockIdx.x, items = ((N - n0 + (int)gridDim.x - 1) / (int)gridDim.x) * nbands;
   auto band_n = [&](int it) { return n0 + (it / nbands) * (int)gridDim.x; };
   auto dma_band = [&](int it, int buf) {
@@ -2007,7 +2007,7 @@ __global__ __launch_bounds__(256) void k_stem_wgrad_mfma(const Tin* __restrict__
     for (int k = 0; k < BRS / 4; ++k) {  // this wave's rows of the band
       const int r = wave + 4 * k, y = b * BRS + r;
       const int pb = 8 * g + tq;
-      bf16x8 A[2], B[4];
+      bf16x8 A[2], B[NT];
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         const int q = 2 * mt + (tp >> 1);
@@ -2015,14 +2015,14 @@ __global__ __launch_bounds__(256) void k_stem_wgrad_mfma(const Tin* __restrict__
                         lds + IM + toff<32>(y, pb + 5, q, TW) + 8 * (tp & 1));
       }
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
+      for (int nt = 0; nt < NT; ++nt) {
         const int q = 2 * nt + (tp >> 1);
         B[nt] = tr_pair(dzt + toff<C>(r, pb + 1, q, TW) + 8 * (tp & 1), dzt + toff<C>(r, pb + 5, q, TW) + 8 * (tp & 1));
       }
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
+        for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mt], B[nt], acc[mt][nt], 0, 0, 0);
     }
   }
@@ -2032,7 +2032,7 @@ __global__ __launch_bounds__(256) void k_stem_wgrad_mfma(const Tin* __restrict__
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
+    for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
       for (int e = 0; e < 4; ++e) red[(wave * 32 + 16 * mt + 4 * g + e) * C + 16 * nt + lx] = acc[mt][nt][e];
   __syncthreads();
@@ -2044,31 +2044,32 @@ __global__ __launch_bounds__(256) void k_stem_wgrad_mfma(const Tin* __restrict__
 }
 
 // ===========================================================================
-// Stem forward on MFMA (C=64, CIN=3, W=32): x1 = relu(conv3x3((v - mean) *
+// Stem forward on MFMA (C = 16 or 64, CIN=3, W=32): x1 = relu(conv3x3((v - mean) *
 // inv_std, W1) + b1), bf16 NHWC out (models/tfkeras_resnets.py:555-572).
-// M = o (4 tiles), K = kappa = tap*3 + ci (27, padded to 32: one k-step),
+// M = o (C/16 tiles), K = kappa = tap*3 + ci (27, padded to 32: one k-step),
 // N = 16 pixels.  B: lane (pixel lx, kappa 8g..8g+7) gathers its 8 patch
 // values from the image staged in LDS as fp32 v - mean (bf16-exact for u8
 // input with a half-integer mean); A = inv_std * W1^T split into bf16 hi +
 // lo parts held in registers (two MFMAs per tile: W1 to ~16 mantissa bits,
 // so the result matches the fp32 VALU kernel to accumulation-order noise).
-// Epilogue: + b1 (fp32), relu, bf16, 16-B stores (a 16-lane row swap between
-// o-tile pairs gives each lane 8 consecutive channels).
+// Epilogue: + b1 (fp32), relu, bf16, 16-B stores at C=64 (a 16-lane row swap
+// between o-tile pairs gives each lane 8 consecutive channels), 8-B stores at
+// C=16 (one o-tile: 16 pixels x 32 B contiguous per tile).
 // ===========================================================================
-template <typename Tin>
+template <int C, typename Tin>
 __global__ __launch_bounds__(256) void k_stem_fwd_mfma(const Tin* __restrict__ img, const float* __restrict__ w1,
                                                        const float* __restrict__ b1, int N, int H, float mean,
                                                        float inv_std, bf16* __restrict__ out) {
-  constexpr int C = 64, W = 32, CIN = 3, TW = W + 2, KC = 9 * CIN;
+  constexpr int W = 32, CIN = 3, TW = W + 2, KC = 9 * CIN, MT = C / 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   float* ft = (float*)lds;  // staged image (fp32 v - mean), zero halo
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, lx = lane & 15;
   for (int i = tid; i < (H + 2) * TW * CIN; i += 256) ft[i] = 0.f;  // halo stays zero
   // A fragments: lane (o = 16 mt + lx, kappa 8g..8g+7), hi and lo bf16 parts
-  bf16x8 Ah[4], Al[4];
+  bf16x8 Ah[MT], Al[MT];
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int kap = 8 * g + j;
@@ -2077,9 +2078,9 @@ __global__ __launch_bounds__(256) void k_stem_fwd_mfma(const Tin* __restrict__ i
       Ah[mt][j] = hi;
       Al[mt][j] = (bf16)(wv - (float)hi);
     }
-  float bz[4][4];
+  float bz[MT][4];
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int e = 0; e < 4; ++e) bz[mt][e] = b1 ? b1[16 * mt + 4 * g + e] : 0.f;
   // B operand: lane (pixel lx, kappa 8g..8g+7) read straight from the staged
@@ -2105,28 +2106,32 @@ __global__ __launch_bounds__(256) void k_stem_fwd_mfma(const Tin* __restrict__ i
       bf16x8 B;
 #pragma unroll
       for (int j = 0; j < 8; ++j) B[j] = (bf16)((8 * g + j < KC) ? pb[koff[j]] : 0.f);
-      f32x4 acc[4];
+      f32x4 acc[MT];
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
+      for (int mt = 0; mt < MT; ++mt) {
         acc[mt] = f32x4{bz[mt][0], bz[mt][1], bz[mt][2], bz[mt][3]};
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[mt], B, acc[mt], 0, 0, 0);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Al[mt], B, acc[mt], 0, 0, 0);
       }
       // lane (g, lx): channels 16 mt + 4g + e of pixel x0 + lx
-      u32x2 ov[4];
+      u32x2 ov[MT];
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
+      for (int mt = 0; mt < MT; ++mt) {
         bf16x4 o4;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaxf(acc[mt][e], 0.f);
         ov[mt] = *(const u32x2*)&o4;
       }
       bf16* orow = out + (((long)n * H + y) * W + x0 + lx) * C;
+      if constexpr (MT == 1) {
+        *(u32x2*)(orow + 4 * g) = ov[0];
+      } else {
 #pragma unroll
-      for (int mp = 0; mp < 2; ++mp) {  // o-tiles 2mp, 2mp+1 -> lane row g: channels 16(2mp + (g&1)) + 8(g>>1)
-        const auto s0 = __builtin_amdgcn_permlane16_swap(ov[2 * mp][0], ov[2 * mp + 1][0], false, false);
-        const auto s1 = __builtin_amdgcn_permlane16_swap(ov[2 * mp][1], ov[2 * mp + 1][1], false, false);
-        *(u32x4*)(orow + 16 * (2 * mp + (g & 1)) + 8 * (g >> 1)) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+        for (int mp = 0; mp < MT / 2; ++mp) {  // o-tiles 2mp, 2mp+1 -> lane row g: channels 16(2mp + (g&1)) + 8(g>>1)
+          const auto s0 = __builtin_amdgcn_permlane16_swap(ov[2 * mp][0], ov[2 * mp + 1][0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(ov[2 * mp][1], ov[2 * mp + 1][1], false, false);
+          *(u32x4*)(orow + 16 * (2 * mp + (g & 1)) + 8 * (g >> 1)) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+        }
       }
     }
   }
@@ -2251,9 +2256,13 @@ static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* ma
 // ---------------------------------------------------------------------------
 // stem weight gradient on MFMA (see k_stem_wgrad_mfma)
 // ---------------------------------------------------------------------------
+static size_t stem_wgrad_mfma_lds(int H, int C) {
+  return (size_t)H * 34 * 64 + 2 * 8 * 34 * (C / 8) * 16 + (size_t)(H + 2) * 34 * 3 * 4;
+}
+
 bool stem_wgrad_mfma_supported(int Cin, int H, int W, int C) {
-  const size_t lds = (size_t)H * 34 * 64 + 2 * 8 * 34 * 128 + (size_t)(H + 2) * 34 * 3 * 4;
-  return Cin == 3 && W == 32 && C == 64 && H % 8 == 0 && H >= 8 && lds <= 160 * 1024;
+  return Cin == 3 && W == 32 && (C == 64 || C == 16) && H % 8 == 0 && H >= 8 &&
+         stem_wgrad_mfma_lds(H, C) <= 160 * 1024;
 }
 
 int stem_wgrad_mfma(const void* img, int input_u8, const void* dz1, int N, int H, int W, int Cin, int C, float mean,
@@ -2263,21 +2272,26 @@ int stem_wgrad_mfma(const void* img, int input_u8, const void* dz1, int N, int H
   if (cus <= 0) cus = 256;
   const int grid = std::max(1, std::min(N, std::min(cus, kMaxBlockSlabs)));
   *nslabs = grid;
-  const size_t lds = (size_t)H * 34 * 64 + 2 * 8 * 34 * 128 + (size_t)(H + 2) * 34 * 3 * 4;
+  const size_t lds = std::max(stem_wgrad_mfma_lds(H, C), (size_t)4 * 32 * C * 4);  // (reduction area)
   const float m = use_norm ? mean : 0.f, is = use_norm ? inv_std : 1.f;
-  if (input_u8)
-    hipLaunchKernelGGL(blk::k_stem_wgrad_mfma<uint8_t>, dim3(grid), dim3(256), lds, s, (const uint8_t*)img,
-                       (const bf16*)dz1, N, H, m, is, slabs);
-  else
-    hipLaunchKernelGGL(blk::k_stem_wgrad_mfma<float>, dim3(grid), dim3(256), lds, s, (const float*)img,
-                       (const bf16*)dz1, N, H, m, is, slabs);
+#define ASR_STEMW(CC, TI)                                                                                   \
+  hipLaunchKernelGGL((blk::k_stem_wgrad_mfma<CC, TI>), dim3(grid), dim3(256), lds, s, (const TI*)img, \
+                     (const bf16*)dz1, N, H, m, is, slabs)
+  if (C == 64) {
+    if (input_u8) ASR_STEMW(64, uint8_t);
+    else ASR_STEMW(64, float);
+  } else {
+    if (input_u8) ASR_STEMW(16, uint8_t);
+    else ASR_STEMW(16, float);
+  }
+#undef ASR_STEMW
   ASR_LAUNCH_CHECK("k_stem_wgrad_mfma");
   return ASR_OK;
 }
 
 bool stem_fwd_mfma_supported(int Cin, int H, int W, int C) {
   const size_t lds = (size_t)(H + 2) * 34 * 3 * 4;
-  return Cin == 3 && W == 32 && C == 64 && H >= 1 && lds <= 160 * 1024;
+  return Cin == 3 && W == 32 && (C == 64 || C == 16) && H >= 1 && lds <= 160 * 1024;
 }
 
 int stem_fwd_mfma(const void* img, int input_u8, const float* w1, const float* b1, int N, int H, int W, int Cin, int C,
@@ -2288,12 +2302,17 @@ int stem_fwd_mfma(const void* img, int input_u8, const float* w1, const float* b
   const int grid = std::max(1, std::min(N, 4 * cus));
   const size_t lds = (size_t)(H + 2) * 34 * 3 * 4;
   const float m = use_norm ? mean : 0.f, is = use_norm ? inv_std : 1.f;
-  if (input_u8)
-    hipLaunchKernelGGL(blk::k_stem_fwd_mfma<uint8_t>, dim3(grid), dim3(256), lds, s, (const uint8_t*)img, w1, b1, N,
-                       H, m, is, (bf16*)out);
-  else
-    hipLaunchKernelGGL(blk::k_stem_fwd_mfma<float>, dim3(grid), dim3(256), lds, s, (const float*)img, w1, b1, N, H,
-                       m, is, (bf16*)out);
+#define ASR_STEMF(CC, TI)                                                                                     \
+  hipLaunchKernelGGL((blk::k_stem_fwd_mfma<CC, TI>), dim3(grid), dim3(256), lds, s, (const TI*)img, w1, b1, N, H, m, \
+                     is, (bf16*)out)
+  if (C == 64) {
+    if (input_u8) ASR_STEMF(64, uint8_t);
+    else ASR_STEMF(64, float);
+  } else {
+    if (input_u8) ASR_STEMF(16, uint8_t);
+    else ASR_STEMF(16, float);
+  }
+#undef ASR_STEMF
   ASR_LAUNCH_CHECK("k_stem_fwd_mfma");
   return ASR_OK;
 }

@@ -122,16 +122,18 @@ def test_network_fullsize_properties(rt, cfg):
     assert np.abs(gf - gm).max() <= 1e-4 * np.abs(gf).max()
 
 
-@pytest.mark.parametrize("N,u8", [(64, True), (512, True), (64, False)])
-def test_stem_wgrad_mfma_matches_fp32_path(rt, N, u8):
+@pytest.mark.parametrize("N,u8,C", [(64, True, 64), (512, True, 64), (64, False, 64), (64, True, 16), (512, True, 16),
+                                    (64, False, 16)])
+def test_stem_wgrad_mfma_matches_fp32_path(rt, N, u8, C):
     """The network's default bf16 path fuses the stem's relu' into the first
     block's backward (dx -> dz1) and computes the stem weight gradient on
     MFMA from bf16 (v - mean) (exact for u8 input and mean 127.5); with
     variant ASR_VARIANT_STEM_WGRAD_VALU it runs the fp32 VALU stem kernel from dx1 and x1.  The
     stem gradients agree to fp32 summation-order noise (u8) or bf16 rounding
     of the centred float input (1e-3 of max|g|); every other gradient and the
-    loss are bitwise unchanged."""
-    C, L = 64, 2
+    loss are bitwise unchanged.  At C=16 (the fused-stack network) dz1 comes
+    from k_relu_grad_bf16 before the MFMA kernel."""
+    L = 2
     from differential_equations_resnet_amd.netparams import init_net_params
     dev = torch.device("cuda")
     params = torch.from_numpy(init_net_params(C, L, 3, 10, seed=3) * 0.5).to(dev)
@@ -195,14 +197,14 @@ def test_folded_slab_reduction_matches_separate(rt, N):
         assert np.abs(ga - gb).max() <= 1e-5 * np.abs(gb).max(), (l, np.abs(ga - gb).max(), np.abs(gb).max())
 
 
-@pytest.mark.parametrize("N,u8", [(64, True), (512, True), (64, False)])
-def test_stem_fwd_mfma_matches_fp32_path(rt, N, u8):
+@pytest.mark.parametrize("N,u8,C", [(64, True, 64), (512, True, 64), (64, False, 64), (64, True, 16), (512, True, 16)])
+def test_stem_fwd_mfma_matches_fp32_path(rt, N, u8, C):
     """The bf16 network's stem forward runs on MFMA (im2col of bf16 (v - mean)
     from LDS, inv_std * W1 split into bf16 hi + lo); with variant
     ASR_VARIANT_STEM_FWD_VALU it runs the fp32 VALU stem kernel.  Same probabilities to bf16 noise
     propagated through the blocks (1e-3 absolute; the stem output itself is
     rounded to bf16 in both)."""
-    C, L = 64, 2
+    L = 2
     from differential_equations_resnet_amd.netparams import init_net_params
     dev = torch.device("cuda")
     params = torch.from_numpy(init_net_params(C, L, 3, 10, seed=4) * 0.5).to(dev)
