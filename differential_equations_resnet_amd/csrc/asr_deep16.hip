@@ -134,16 +134,19 @@ __device__ __forceinline__ void row_mfma(const bf16x8 (&A)[KS], const bf16x8 (&F
 // Row-reuse B fragments of the wave's 10 tile rows: F(R), G(R) for R = j..j+3
 // live in a ring of 4 (slot R & 3); row j's MFMAs read F(j..j+2), G(j), G(j+2)
 // while the fragments of tile row j+3 load.
-struct Frag {
-  bf16x8 F[4][2], G[4][2];
+// (NS = 3: tile row j+3 loads into row j's slots after row j's MFMAs issue)
+template <int NS = 4>
+struct FragT {
+  bf16x8 F[NS][2], G[NS][2];
   __device__ __forceinline__ void load(const unsigned char* tile, unsigned bF, unsigned bG, int R) {
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt) {
-      F[R & 3][pt] = *(const bf16x8*)(tile + bF + R * ROWB + pt * 512);
-      G[R & 3][pt] = *(const bf16x8*)(tile + bG + R * ROWB + pt * 512);
+      F[R % NS][pt] = *(const bf16x8*)(tile + bF + R * ROWB + pt * 512);
+      G[R % NS][pt] = *(const bf16x8*)(tile + bG + R * ROWB + pt * 512);
     }
   }
 };
+using Frag = FragT<4>;
 
 // x_{l+1} for l = 0 .. L-1 of every image the workgroup owns.
 //   x0:    [N,32,32,16] bf16 (the stem output)
@@ -282,8 +285,13 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
 // One barrier per layer.  LDS: 2 dz tiles (swizzled, zero halo) + zero row |
 // 2 x tiles (image rows, zero halo columns) | 2 x 2 KiB masks | db partials.
 // ---------------------------------------------------------------------------
-constexpr int KSEG = 12;                 // layers per segment (dW accumulators in registers)
-constexpr int NWB = 8;                   // waves per backward workgroup
+#ifndef ASR_DEEP_NDG
+#define ASR_DEEP_NDG 8
+#endif
+constexpr int NDG = ASR_DEEP_NDG;        // dgrad waves (image rows split among them)
+constexpr int RPB = H / NDG;             // image rows per dgrad wave
+constexpr int KSEG = NDG == 4 ? 12 : 8;  // layers per segment (dW accumulators in registers)
+constexpr int NWB = NDG + 4;             // waves per backward workgroup: dgrad, 3 wgrad, staging
 constexpr int ES = 9 * C * C + C;        // slab floats per layer
 constexpr int XT = H * ROWB;             // x tile: 32 image rows x 34 columns
 constexpr int MB = IMG / 8;              // 2 KiB of relu bits per image
@@ -292,7 +300,8 @@ constexpr int MB = IMG / 8;              // 2 KiB of relu bits per image
 // a rotation of three row blocks: the upper rows of the two x tiles and L_E.
 constexpr int XS = 22;
 constexpr int L_Z = 0, L_X = L_Z + 2 * TILE + ROWB, L_M = L_X + 2 * XT, L_TAB = L_M + 2 * MB;
-constexpr int L_E = L_TAB + 256 * 16;  // after the mask byte -> 8 x 0xffff/0 bf16 AND-mask table
+constexpr int L_DB = L_TAB + 16 * 8;   // after the mask nibble -> 4 x 0xffff/0 bf16 AND-mask table
+constexpr int L_E = L_DB + KSEG * C * 4;  // after the segment's db sums [KSEG][C]
 constexpr int L_TOTAL = L_E + (H - XS) * ROWB;
 __device__ __forceinline__ int xhi_base(int t) {  // LDS offset of image row XS of step t's x
   const int r = t % 3;
@@ -314,9 +323,12 @@ __device__ __forceinline__ bf16x8 tr2(const unsigned char* base, const unsigned 
   return tr_pair(base + o[0], base + o[1]);
 }
 
-// 8 bf16 ANDed with the relu bits of the lane's mask byte (table: 0xffff per set bit)
+// 8 bf16 ANDed with the relu bits of the lane's mask byte (table per nibble:
+// 0xffff per set bit; 16 entries of 8 B, so lanes of a read group share
+// entries by broadcast and never conflict)
 __device__ __forceinline__ u32x4v mask_bf16x8(const unsigned char* lds, u32x4v v, unsigned m) {
-  return v & *(const u32x4v*)(lds + L_TAB + m * 16);
+  const u32x2 lo = *(const u32x2*)(lds + L_TAB + (m & 15u) * 8), hi = *(const u32x2*)(lds + L_TAB + (m >> 4) * 8);
+  return v & u32x4v{lo[0], lo[1], hi[0], hi[1]};
 }
 template <int N>
 __device__ __forceinline__ void barrier_vmt() {  // barrier after all but the N youngest vector-memory ops
@@ -366,18 +378,18 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
   // dz tiles, their zero row, the x tiles and the third x row block (halos stay zero)
   for (int i = tid; i < L_M / 16; i += 64 * NWB) ((uint4*)lds)[i] = make_uint4(0, 0, 0, 0);
   for (int i = tid; i < (L_TOTAL - L_E) / 16; i += 64 * NWB) ((uint4*)(lds + L_E))[i] = make_uint4(0, 0, 0, 0);
-  if (tid < 256) {
-    u32x4v e;
+  if (tid < 16) {
+    u32x2 e;
 #pragma unroll
-    for (int d = 0; d < 4; ++d) e[d] = ((tid >> (2 * d)) & 1 ? 0xffffu : 0u) | ((tid >> (2 * d + 1)) & 1 ? 0xffff0000u : 0u);
-    *(u32x4v*)(lds + L_TAB + tid * 16) = e;
+    for (int d = 0; d < 2; ++d) e[d] = ((tid >> (2 * d)) & 1 ? 0xffffu : 0u) | ((tid >> (2 * d + 1)) & 1 ? 0xffff0000u : 0u);
+    *(u32x2*)(lds + L_TAB + tid * 8) = e;
   }
   __syncthreads();
   const int nseg = (L + KSEG - 1) / KSEG;
 
-  if (wave < 4) {
+  if (wave < NDG) {
     // ------------------------------ dgrad waves ------------------------------
-    const int r0 = wave * RPW;
+    const int r0 = wave * RPB;
     const float hs2g = h * two_gamma;
     const unsigned bF = (unsigned)(r0 * ROWB) + swz(lx + (g >> 1), g & 1);
     const unsigned bG = (unsigned)((r0 + (g >> 1)) * ROWB) + swz(lx + 2, g & 1);
@@ -388,10 +400,16 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
     unsigned wo[KS];
     wt_offsets(lane, wo);
     int t = 0;  // layer steps so far: buffer parity (identical count in every role)
-    f32x2 dxf[RPW][4];  // dx_{l+1} of the wave's pixels (regrouped chunks), fp32 between layers
-    bf16x8 dnx[RPW];    // dx at the segment top of the next image (bf16 in HBM)
+    // dx_{l+1} of the wave's pixels (regrouped chunks), fp32 between layers; at an
+    // image's segment top the bf16 dx from HBM sits raw in the first two pairs
+    f32x2 dxf[RPB][4];
+    auto raw_load = [&](int j, const unsigned char* src) {
+      const u32x4v v = *(const u32x4v*)src;
+      dxf[j][0] = (f32x2){__uint_as_float(v[0]), __uint_as_float(v[1])};
+      dxf[j][1] = (f32x2){__uint_as_float(v[2]), __uint_as_float(v[3])};
+    };
 #pragma unroll
-    for (int j = 0; j < RPW; ++j) dnx[j] = *(const bf16x8*)((const unsigned char*)dbufA + (long)b * IMG * 2 + oG + j * ROW_G);
+    for (int j = 0; j < RPB; ++j) raw_load(j, (const unsigned char*)dbufA + (long)b * IMG * 2 + oG + j * ROW_G);
     barrier_lds();  // prologue: wave 7's DMA of the first x / masks
     for (int sg = 0; sg < nseg; ++sg) {
       const int ltop = L - 1 - sg * KSEG, kcount = min(KSEG, ltop + 1);
@@ -402,8 +420,9 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
         {
           const unsigned char* mt = lds + L_M + (t & 1) * MB;
 #pragma unroll
-          for (int j = 0; j < RPW; ++j) {
-            const u32x4v w = __builtin_bit_cast(u32x4v, dnx[j]);
+          for (int j = 0; j < RPB; ++j) {
+            const u32x4v w = {__float_as_uint(dxf[j][0].x), __float_as_uint(dxf[j][0].y), __float_as_uint(dxf[j][1].x),
+                              __float_as_uint(dxf[j][1].y)};
             *(u32x4v*)(lds + L_Z + (t & 1) * TILE + oT + j * ROWB) = mask_bf16x8(lds, w, mt[oM + j * 64]);
 #pragma unroll
             for (int d = 0; d < 4; ++d) dxf[j][d] = (f32x2){lo_f(w[d]), hi_f(w[d])};
@@ -425,18 +444,20 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
           const Pos nx = pos_next({sg, n, k}, L, N, P, b);  // the next image's (or segment's) top
           const unsigned char* dnext =
               (const unsigned char*)((nx.sg & 1) ? dbufB : dbufA) + (long)nx.n * IMG * 2;
-          Frag fr;
+          constexpr int NS = NDG == 8 ? 3 : 4;  // 3 slots at 3 waves per SIMD (VGPR budget)
+          FragT<NS> fr;
 #pragma unroll
           for (int R = 0; R < 3; ++R) fr.load(zt, bF, bG, R);
 #pragma unroll
-          for (int j = 0; j < RPW; ++j) {
-            if (j + 3 <= RPW + 1) fr.load(zt, bF, bG, j + 3);
+          for (int j = 0; j < RPB; ++j) {
+            if (NS == 4 && j + 3 <= RPB + 1) fr.load(zt, bF, bG, j + 3);
             f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #if ASR_DEEP_EXP == 2 || ASR_DEEP_EXP == 3 || ASR_DEEP_EXP == 7
-            acc[0][0] = (float)fr.F[j & 3][0][0] + (float)fr.G[(j + 2) & 3][1][3];
+            acc[0][0] = (float)fr.F[j % NS][0][0] + (float)fr.G[(j + 2) % NS][1][3];
 #else
-            row_mfma(A, fr.F[j & 3], fr.F[(j + 1) & 3], fr.F[(j + 2) & 3], fr.G[j & 3], fr.G[(j + 2) & 3], acc);
+            row_mfma(A, fr.F[j % NS], fr.F[(j + 1) % NS], fr.F[(j + 2) % NS], fr.G[j % NS], fr.G[(j + 2) % NS], acc);
 #endif
+            if (NS == 3 && j + 3 <= RPB + 1) fr.load(zt, bF, bG, j + 3);
             u32x4v zw;
             if constexpr (GAMMA) zw = *(const u32x4v*)(zt + oT + j * ROWB);  // dzm_l of the lane's chunk
             float c[8];
@@ -453,7 +474,7 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
               *(u32x4v*)(zn + oT + j * ROWB) = mask_bf16x8(lds, ow, mn[oM + j * 64]);
             } else {
               *(u32x4v*)(dout + img + oG + j * ROW_G) = ow;
-              dnx[j] = *(const bf16x8*)(dnext + oG + j * ROW_G);
+              raw_load(j, dnext + oG + j * ROW_G);
             }
           }
           if (wave == 0) ASR_TRACE(0, t, 1);
@@ -475,9 +496,9 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
       __syncthreads();  // segment end (slabs written by the wgrad waves and wave 7)
       __syncthreads();
     }
-  } else if (wave < 7) {
+  } else if (wave < NDG + 3) {
     // ------------------------------ wgrad waves ------------------------------
-    const int kx = wave - 4;
+    const int kx = wave - NDG;
     unsigned tx2[2], tz2[2];  // tr-read lane offsets: pixel 8g + 4*(hh ^ (g&1)) + q, channels 4p..4p+3
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
@@ -529,14 +550,14 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
       for (int n = b; n < N; n += P) {
         barrier_lds();  // dzm_ltop written
         for (int k = 0; k < kcount; ++k) {
-          if (wave == 4) ASR_TRACE(1, t, 0);
+          if (wave == NDG) ASR_TRACE(1, t, 0);
           static_for<0, KSEG>([&](auto kc) {
 #if ASR_DEEP_EXP == 1 || ASR_DEEP_EXP == 3 || ASR_DEEP_EXP == 7
             if (two_gamma == 1234.5f)  // never: the wgrad MFMAs skipped at run time
 #endif
             if (k == decltype(kc)::value) wgrad_layer(acc[decltype(kc)::value], t);
           });
-          if (wave == 4) ASR_TRACE(1, t, 1);
+          if (wave == NDG) ASR_TRACE(1, t, 1);
           ++t;
           barrier_lds();
         }
@@ -567,9 +588,10 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
     unsigned tz2[2];  // dz tr-read lane offsets (as the wgrad waves)
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) tz2[hh] = swz(8 * g + 4 * (hh ^ (g & 1)) + q + 1, p >> 1) + 8 * (p & 1);
-    // db of the segment's layers on MFMA: D = ones(16 x 32 pixels) x dzm(32 pixels x 16 o),
-    // one row per MFMA, every D row = the per-channel sum (fixed order)
-    f32x4 dacc[KSEG];
+    // db on MFMA: D = ones(16 x 32 pixels) x dzm(32 pixels x 16 o), one row per
+    // MFMA, every D row = the per-channel sum (fixed order); added per image into
+    // the segment's db sums in LDS (one lane per channel: deterministic)
+    float* dbl = (float*)(lds + L_DB);
     const bf16x8 ones = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
     auto db_layer = [&](f32x4& a, int par) {
       const unsigned char* zt = lds + L_Z + par * TILE + ROWB;
@@ -624,8 +646,7 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
     }
     for (int sg = 0; sg < nseg; ++sg) {
       const int ltop = L - 1 - sg * KSEG, kcount = min(KSEG, ltop + 1);
-#pragma unroll
-      for (int k = 0; k < KSEG; ++k) dacc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int i = lane; i < KSEG * C; i += 64) dbl[i] = 0.f;
       for (int n = b; n < N; n += P) {
         barrier_lds();  // dzm_ltop written
         for (int k = 0; k < kcount; ++k) {
@@ -641,16 +662,11 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
           dma_x(n2, XS, t + 2);  // upper x rows of the step after next
           load_x(n2);
           load_m(n3);
-          static_for<0, KSEG>([&](auto kc) {
-            if (k == decltype(kc)::value) db_layer(dacc[decltype(kc)::value], t & 1);
-          });
-#if ASR_DEEP_EXP == 8
           {
-            float sink = dacc[0][0];
-            asm volatile("s_nop 0" : "+v"(sink));
-            dacc[0][0] = sink;
+            f32x4 a = {0.f, 0.f, 0.f, 0.f};
+            db_layer(a, t & 1);
+            if (g == 0) dbl[k * C + lx] += a[0];
           }
-#endif
           ASR_TRACE(2, t, 3);
 #if ASR_DEEP_EXP == 8
           asm volatile("s_waitcnt vmcnt(34)" ::: "memory");  // trace the x DMA landing, not its issue
@@ -661,10 +677,8 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
         }
       }
       __syncthreads();
-      static_for<0, KSEG>([&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        if (k < kcount && g == 0) slabs[((long)(ltop - k) * PS + b) * ES + 9 * C * C + lx] = h * dacc[k][0];
-      });
+      for (int k = 0; k < kcount; ++k)
+        if (g == 0) slabs[((long)(ltop - k) * PS + b) * ES + 9 * C * C + lx] = h * dbl[k * C + lx];
       for (int k = 0; k < kcount; ++k)  // padding slabs of the 32-slab reduction groups
         for (int j = P + b; j < PS; j += P) {
           float* zs = slabs + ((long)(ltop - k) * PS + j) * ES;
