@@ -108,6 +108,23 @@ __device__ __forceinline__ unsigned bit01(int v) {
   asm("v_med3_i32 %0, %1, 0, 1" : "=v"(r) : "v"(v));
   return r;
 }
+// f(integral_constant<int, k>) for k = K .. N-1: compile-time register-array
+// indices (a runtime index would put the array in scratch memory)
+template <int K, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (K < N) {
+    f(std::integral_constant<int, K>{});
+    static_for<K + 1, N>(f);
+  }
+}
+
+// (b << e) | acc in one v_lshl_or_b32
+template <int E>
+__device__ __forceinline__ unsigned lshl_or(unsigned b, unsigned acc) {
+  unsigned r;
+  asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "n"(E), "v"(acc));
+  return r;
+}
 // two fp32 -> packed bf16 pair (RNE, one v_cvt_pk_bf16_f32)
 __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
   const bf16x2 v = {(bf16)a, (bf16)b};
@@ -229,14 +246,14 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
         const u32x4v xw = __builtin_bit_cast(u32x4v, xr[j]);
         u32x4v yw;
         unsigned bits = 0;
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
+        static_for<0, 4>([&](auto dc) {
+          constexpr int d = decltype(dc)::value;
           // relu on the bit pattern: a float is > 0 iff its bits are a positive int
           const int ra = max(__float_as_int(z[2 * d]), 0), rb = max(__float_as_int(z[2 * d + 1]), 0);
           yw[d] = pk_bf16(fmaf(h, __int_as_float(ra), lo_f(xw[d])), fmaf(h, __int_as_float(rb), hi_f(xw[d])));
-          bits |= bit01(ra) << (2 * d);
-          bits |= bit01(rb) << (2 * d + 1);
-        }
+          bits = d == 0 ? bit01(ra) : lshl_or<2 * d>(bit01(ra), bits);
+          bits = lshl_or<2 * d + 1>(bit01(rb), bits);
+        });
         const bf16x8 y = __builtin_bit_cast(bf16x8, yw);
         *(bf16x8*)(dst + oT + j * ROWB) = y;
 #if ASR_DEEP_EXP != 4
@@ -308,16 +325,6 @@ __device__ __forceinline__ int xhi_base(int t) {  // LDS offset of image row XS 
   return r == 2 ? L_E : L_X + r * XT + XS * ROWB;
 }
 static_assert(L_TOTAL <= 160 * 1024, "LDS budget");
-
-// f(integral_constant<int, k>) for k = K .. N-1: compile-time register-array
-// indices (a runtime index would put the array in scratch memory)
-template <int K, int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (K < N) {
-    f(std::integral_constant<int, K>{});
-    static_for<K + 1, N>(f);
-  }
-}
 
 __device__ __forceinline__ bf16x8 tr2(const unsigned char* base, const unsigned (&o)[2]) {
   return tr_pair(base + o[0], base + o[1]);
