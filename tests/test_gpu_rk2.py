@@ -171,3 +171,32 @@ def test_rk2_model_lowering_matches_executor():
     spec = O.NetSpec(C=16, L=2, h=0.5, integrator="rk2")
     want, _ = O.net_forward(spec, [w.astype(np.float64) for w in m.get_weights()], imgs)
     assert_close(got, want, rtol=1e-5, atol=1e-6, what="rk2 model probs")
+
+
+def test_rk2_forward_multiband(rt):
+    """The RK2 second-stage forward (k_fwd_pipe<..., RESG>: residual read from
+    global memory, loads issued one band ahead of their use) over a persistent
+    run of several bands per workgroup: N=192 images of H=30 rows (8 bands
+    each, the last band ragged: 30 is not a multiple of the band height 4)
+    = 1536 items on a grid of at most 512 workgroups.  Every image's x_mid and
+    y against the oracle (stage 2 fed the GPU's own bf16 midpoint), bf16
+    tolerances as test_rk2_block_parity."""
+    N, H, W_, C = 192, 30, 32, 64
+    gamma, h = 0.0, 0.5
+    rng = np.random.default_rng(4242)
+    x_np = rng.standard_normal((N, H, W_, C)).astype(np.float32)
+    th = _theta(C, 21)
+    b = (rng.standard_normal(C) * 0.1).astype(np.float32)
+    dev = torch.device("cuda")
+    pm = rt.param_map(C)
+    w = rt.theta_to_w(torch.from_numpy(th).to(dev), C, pm, gamma, rt.ASR_BF16)
+    x = torch.from_numpy(x_np).to(dev).to(torch.bfloat16).contiguous()
+    y, xm, m1, m2 = rt.rk2_forward(x, w, torch.from_numpy(b).to(dev), h)
+    src, sign = O.param_map(C)
+    Wo = bf16_round(O.assemble_from_map(th.astype(np.float64), C, src, sign, gamma)).astype(np.float64)
+    xo = bf16_round(x_np).astype(np.float64)
+    xm_want = xo + 0.5 * h * np.maximum(O.conv2d_same(xo, Wo) + b, 0)
+    xm_gpu = xm.float().cpu().numpy().astype(np.float64)
+    y_want = xo + h * np.maximum(O.conv2d_same(xm_gpu, Wo) + b, 0)
+    assert_close(xm_gpu, xm_want, rtol=2 ** -8, atol=4e-3 * np.abs(xm_want).max(), what="multiband xmid")
+    assert_close(y.float().cpu().numpy(), y_want, rtol=2 ** -8, atol=4e-3 * np.abs(y_want).max(), what="multiband y")
