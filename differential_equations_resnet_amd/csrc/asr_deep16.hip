@@ -43,6 +43,9 @@ namespace deep {
 
 using namespace blk;
 
+#ifndef ASR_DEEP_NT
+#define ASR_DEEP_NT 1  // streaming (nt) stores of the forward: +6 % forward, -1 % backward (A/B r02k)
+#endif
 #ifndef ASR_DEEP_EXP
 #define ASR_DEEP_EXP 0  // development A/B only (tools/build_variants.sh): 0 = the product kernels
 #endif
@@ -257,8 +260,14 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
         const bf16x8 y = __builtin_bit_cast(bf16x8, yw);
         *(bf16x8*)(dst + oT + j * ROWB) = y;
 #if ASR_DEEP_EXP != 4
+#if ASR_DEEP_NT
+        // streaming stores: x_{l+1} and its mask are read back only by the backward
+        if (store) __builtin_nontemporal_store(yw, (u32x4v*)(yl + oG + j * ROW_G));
+        if (MASK) __builtin_nontemporal_store((uint8_t)bits, ml + oM + j * 64);
+#else
         if (store) *(bf16x8*)(yl + oG + j * ROW_G) = y;
         if (MASK) ml[oM + j * 64] = (uint8_t)bits;
+#endif
 #endif
         xr[j] = y;
       }
