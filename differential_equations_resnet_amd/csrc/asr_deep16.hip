@@ -43,6 +43,9 @@ namespace deep {
 
 using namespace blk;
 
+#ifndef ASR_DEEP_PRIO
+#define ASR_DEEP_PRIO 0  // development A/B: s_setprio 1 for the wgrad (1) / staging (2) waves
+#endif
 #ifndef ASR_DEEP_NT
 #define ASR_DEEP_NT 1  // streaming (nt) stores of the forward: +6 % forward, -1 % backward (A/B r02k)
 #endif
@@ -513,6 +516,9 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
       __syncthreads();
     }
   } else if (wave < NDG + 3) {
+#if ASR_DEEP_PRIO & 1
+    __builtin_amdgcn_s_setprio(1);
+#endif
     // ------------------------------ wgrad waves ------------------------------
     const int kx = wave - NDG;
     unsigned tx2[2], tz2[2];  // tr-read lane offsets: pixel 8g + 4*(hh ^ (g&1)) + q, channels 4p..4p+3
@@ -593,6 +599,9 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
     }
   } else {
     // -------------------------- x / mask staging wave (7) --------------------------
+#if ASR_DEEP_PRIO & 2
+    __builtin_amdgcn_s_setprio(1);
+#endif
     // x of the step after next: rows 0..XS-1 by global loads into registers (a
     // third x buffer), written to the free LDS x tile one step later; rows XS..
     // by LDS-DMA into the rotating third row block; so every x load has about

@@ -97,7 +97,7 @@ def test_stack_backward_matches_per_block_and_oracle(rt, N, L, gamma):
     layer (identical dzm) within 1e-5 of max|.|, lower layers within rel-L2
     1e-2; the top layer's dtheta / dbias also against the oracle on the GPU's
     bf16 inputs (1e-3 of max|.|, the bf16-network tolerance of
-    test_gpu_kernels.py).  L=13 covers a full 12-layer segment and a partial
+    test_gpu_kernels.py).  L=13 covers a full 8-layer segment (KSEG) and a partial
     one; N=300 several images per workgroup."""
     h = 8.0 / 30
     x0, w, bias, th, b, pm = _stack_inputs(rt, N, L, gamma, seed=7 * N + L)
