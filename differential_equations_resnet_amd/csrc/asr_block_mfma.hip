@@ -62,6 +62,9 @@
 #ifndef ASR_XT_EARLY
 #define ASR_XT_EARLY 1  // v2 backward, RK2 first stage: extra-term loads of row 0 before the dy DMA burst (0: after)
 #endif
+#ifndef ASR_FWD3
+#define ASR_FWD3 1  // C=64 forward (Euler without RK2 residual, plain conv): k_fwd3 at 3 WGs per CU (0: k_fwd_pipe)
+#endif
 #ifndef ASR_ABLATE
 #define ASR_ABLATE 0  // development only: fwd 1 no epilogue, 2 no MFMA, 3 no prefetch DMA;
                       // bwd 4 no convert, 5 no dgrad MFMA, 6 no wgrad MFMA, 7 no dgrad epilogue,
@@ -804,6 +807,123 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
     cur.next(nb);
     nx1.next(nb);
     nx2.next(nb);
+  }
+}
+
+// Forward, band form at three waves per SIMD (C = 64; 3 WGs of 4 waves per
+// CU, <= 168 VGPRs): no cross-band software pipeline.  Each wave runs its
+// o-tile's band conv, then the band's epilogue; the other two workgroups on
+// the CU keep the matrix pipe busy meanwhile.  The epilogue works on the
+// regrouped accumulators (v_permlane16_swap: lane (lx, g) owns channels
+// 16*ot + 8*(g>>1) + 0..7 of pixel lx + 16*(g&1)): the residual is one
+// ds_read_b128 of the band's LDS tile, y one 16-B store, the relu bits one
+// byte per lane (v_med3 + v_lshl_or, relu as an integer max on the bit
+// pattern).  MFMA accumulation order and rounding equal k_fwd_pipe's, so both
+// kernels give bitwise the same y and mask.
+template <int C, int W, int BR, int MODE, int WPE>
+__global__ __launch_bounds__(256, WPE) void k_fwd3(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                   uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
+                                                   const float* __restrict__ bias, float h, int N, int H) {
+  using G = Geo<C>;
+  constexpr int TW = W + 2, NQ = G::NQ, OT = C / 16, NW = 4, RB = BR;
+  static_assert(OT == NW && W == 32, "one 16-channel o-tile per wave, two pixel tiles");
+  using BD = Band<C, W, RB>;
+  constexpr int TILE = (BR + 2) * BD::ROWB;
+  constexpr bool EULER = MODE == FWD_EULER;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ot = wave, g = lane >> 4, lx = lane & 15;
+  const int o0 = 16 * ot + 4 * g;
+  const int px = lx + 16 * (g & 1), cg = 2 * ot + (g >> 1);  // after the regroup: pixel, 16-B channel chunk
+
+  bf16x8 A[G::KS];
+  load_A1<C>(wpack, ot, lane, A);
+  unsigned lo[3 * BD::NCB];
+  band_lane_offsets<C, W, RB>(g, lx, lo);
+  float bz[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) bz[e] = bias ? bias[o0 + e] : 0.f;
+  const unsigned lxr = (unsigned)toff<C>(1, px + 1, cg, TW);  // output row 0's residual chunk
+  const unsigned ly = (unsigned)(px * C + 8 * cg) * 2u, lm = (unsigned)(px * (C / 8) + cg);
+
+  zero_halo_cols<C, W>(lds, BR + 2, tid, 64 * NW);
+  zero_halo_cols<C, W>(lds + TILE, BR + 2, tid, 64 * NW);
+  const int nb = (H + BR - 1) / BR;
+  int i0, i1;
+  item_range(N * nb, &i0, &i1);
+  if (i0 >= i1) return;
+  ItemCursor cur(i0, nb), nxt(i0, nb);
+  nxt.next(nb);
+  {
+    const int yy = cur.b * BR;
+    dma_rows<C, W>(x, lds, cur.n, yy - 1, min(BR, H - yy) + 2, H, wave, NW, lane);
+  }
+  int nst = 0;  // vector-memory ops issued after the DMA the next barrier waits for
+  for (int it = i0; it < i1; ++it, cur.next(nb), nxt.next(nb)) {
+    const int buf = (it - i0) & 1;
+    barrier_vm(nst);  // band it landed; every wave is done with band it-1's tile
+    nst = 0;
+    if (it + 1 < i1) {
+      // the next band into the other buffer; its rows 0, 1 are this band's rows
+      // BR, BR+1 when it continues the image (copied inside LDS, the rest by DMA)
+      unsigned char* nt = lds + (buf ^ 1) * TILE;
+      const int yy = nxt.b * BR;
+      if (nxt.n == cur.n && nxt.b == cur.b + 1) {
+        dma_rows<C, W>(x, nt + 2 * BD::ROWB, nxt.n, yy + 1, min(BR, H - yy), H, wave, NW, lane);
+        const uint4* src = (const uint4*)(lds + buf * TILE + BR * BD::ROWB);
+        uint4* dst = (uint4*)nt;
+        constexpr int NCH = 2 * W * NQ;
+        for (int i = tid; i < NCH; i += 64 * NW) {
+          const int o = ((i / (W * NQ)) * TW + 1) * NQ + i % (W * NQ);
+          dst[o] = src[o];
+        }
+      } else {
+        dma_rows<C, W>(x, nt, nxt.n, yy - 1, min(BR, H - yy) + 2, H, wave, NW, lane);
+      }
+    }
+    const unsigned tb = lds_u32(lds + buf * TILE);
+    f32x4 acc[RB][2];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt) acc[r][pt] = f32x4{bz[0], bz[1], bz[2], bz[3]};
+    conv_band<C, W, RB>(tb, lo, A, acc);
+    u32x4 xr[RB];
+    if constexpr (EULER) {
+#pragma unroll
+      for (int r = 0; r < RB; ++r) xr[r] = lds_rd128(tb + lxr + (unsigned)(r * BD::ROWB));
+      lgkm_wait<0>();
+    }
+    const int y0 = cur.b * BR, rows = min(BR, H - y0);
+    const long rowb = ((long)cur.n * H + y0) * W;
+    unsigned char* yb = (unsigned char*)(y + rowb * C) + ly;
+    uint8_t* mb = mask ? mask + rowb * (C / 8) + lm : nullptr;
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      if (r >= rows) break;
+      float z[8];
+      regroup(acc[r][0], acc[r][1], z);
+      u32x4 yw;
+      if constexpr (EULER) {
+        unsigned bits = 0;
+        static_for<0, 4>([&](auto dc) {
+          constexpr int d = decltype(dc)::value;
+          const int ra = max(__float_as_int(z[2 * d]), 0), rb = max(__float_as_int(z[2 * d + 1]), 0);
+          yw[d] = pk_bf16(fmaf(h, __int_as_float(ra), lo_f(xr[r][d])), fmaf(h, __int_as_float(rb), hi_f(xr[r][d])));
+          bits = d == 0 ? bit01(ra) : lshl_or<2 * d>(bit01(ra), bits);
+          bits = lshl_or<2 * d + 1>(bit01(rb), bits);
+        });
+        if (mb) {
+          mb[r * W * (C / 8)] = (uint8_t)bits;
+          ++nst;
+        }
+      } else {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) yw[d] = pk_bf16(z[2 * d], z[2 * d + 1]);
+      }
+      *(u32x4*)(yb + r * W * C * 2) = yw;
+      ++nst;
+    }
   }
 }
 
@@ -2161,6 +2281,19 @@ static int launch_fwd_v(int mode, const void* x, const void* resid, void* y, uin
   if (cus <= 0) cus = 256;
   const int grid = (int)std::max<long>(1, std::min<long>(items, (long)cus * (8 / NW)));
   const size_t lds = 2 * (size_t)(BR + 2) * (W + 2) * C * 2;
+  if constexpr (C == 64 && W == 32 && BR == 4 && NW == 4) {
+    if (ASR_FWD3 && !resid) {
+      const int grid3 = (int)std::max<long>(1, std::min<long>(items, (long)cus * 3));
+      if (mode == blk::FWD_EULER)
+        hipLaunchKernelGGL((blk::k_fwd3<C, W, BR, blk::FWD_EULER, 3>), dim3(grid3), dim3(256), lds, s, (const bf16*)x,
+                           (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+      else
+        hipLaunchKernelGGL((blk::k_fwd3<C, W, BR, blk::FWD_CONV, 3>), dim3(grid3), dim3(256), lds, s, (const bf16*)x,
+                           (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+      ASR_LAUNCH_CHECK("k_fwd3");
+      return ASR_OK;
+    }
+  }
   if constexpr (C >= 32) {
     if (mode == blk::FWD_EULER && resid) {  // second RK2 stage: residual from the step input
       hipLaunchKernelGGL((blk::k_fwd_pipe<C, W, BR, blk::FWD_EULER, NW, true>), dim3(grid), dim3(64 * NW), lds, s,

@@ -87,55 +87,15 @@ __device__ __forceinline__ void load_wt(const bf16* __restrict__ w, const unsign
   for (int ks = 0; ks < KS; ++ks) A[ks] = *(const bf16x8*)(w + wo[ks]);
 }
 
-// The two pixel tiles' accumulators of one output row (D layout: lane (lx, g)
-// holds channels 4g..4g+3 of pixels lx and 16+lx) regrouped so that lane
-// (lx, g) holds channels 8(g>>1) + i, i = 0..7, of pixel lx + 16(g&1)
-// (v_permlane16_swap: odd rows of the first operand <-> even rows of the second).
-__device__ __forceinline__ void regroup(const f32x4& c0, const f32x4& c1, float (&z)[8]) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(c0[e]), __float_as_uint(c1[e]), false, false);
-    z[e] = __uint_as_float(s[0]);
-    z[4 + e] = __uint_as_float(s[1]);
-  }
-}
-__device__ __forceinline__ float lo_f(unsigned w) { return __uint_as_float(w << 16); }
-__device__ __forceinline__ float hi_f(unsigned w) { return __uint_as_float(w & 0xffff0000u); }
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-// (a, b) * s + (c, d) on one v_pk_fma_f32
-__device__ __forceinline__ f32x2 pk_fma(float s, f32x2 ab, f32x2 cd) {
-  return __builtin_elementwise_fma((f32x2){s, s}, ab, cd);
-}
-// 1 if v > 0 else 0 (v_med3_i32; in asm so that the compiler does not turn the
-// following shift into a compare + select per bit)
-__device__ __forceinline__ unsigned bit01(int v) {
-  unsigned r;
-  asm("v_med3_i32 %0, %1, 0, 1" : "=v"(r) : "v"(v));
-  return r;
-}
-// f(integral_constant<int, k>) for k = K .. N-1: compile-time register-array
-// indices (a runtime index would put the array in scratch memory)
-template <int K, int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (K < N) {
-    f(std::integral_constant<int, K>{});
-    static_for<K + 1, N>(f);
-  }
-}
-
-// (b << e) | acc in one v_lshl_or_b32
-template <int E>
-__device__ __forceinline__ unsigned lshl_or(unsigned b, unsigned acc) {
-  unsigned r;
-  asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "n"(E), "v"(acc));
-  return r;
-}
-// two fp32 -> packed bf16 pair (RNE, one v_cvt_pk_bf16_f32)
-__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
-  const bf16x2 v = {(bf16)a, (bf16)b};
-  return __builtin_bit_cast(unsigned, v);
-}
+using blk::bit01;
+using blk::f32x2;
+using blk::hi_f;
+using blk::lo_f;
+using blk::lshl_or;
+using blk::pk_bf16;
+using blk::pk_fma;
+using blk::regroup;
+using blk::static_for;
 
 // One output row of the implicit GEMM for both pixel tiles from the row-reuse
 // fragments (fixed accumulation order: init, k-steps 0..4).
