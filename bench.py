@@ -132,21 +132,23 @@ def block_roofline(rt, lib, C, N, dtype_name, reps, h, integrator="euler"):
     dth = torch.empty(pm.n_theta, device=dev)
     db = torch.empty(C, device=dev)
     w_src, theta_dst = pm.device(dev)
-    s = torch.cuda.current_stream().cuda_stream
+
+    def cs():  # the launch stream: torch's current one (a capture stream inside timed())
+        return torch.cuda.current_stream().cuda_stream
 
     def fwd():
         _lib.check(lib.asr_conv_forward(0, x.data_ptr(), y.data_ptr(), mask.data_ptr(), w.data_ptr(),
-                                        bias.data_ptr(), h, N, H, W, C, dt, s), "fwd")
+                                        bias.data_ptr(), h, N, H, W, C, dt, cs()), "fwd")
 
     def bwd_kernel():  # dx only: the fused dgrad + wgrad kernel alone (no slab reduction / projection)
         _lib.check(lib.asr_conv_backward(0, dy.data_ptr(), x.data_ptr(), mask.data_ptr(), w.data_ptr(),
                                          theta_dst.data_ptr(), pm.n_theta, h, 0.0, N, H, W, C, dt, dx.data_ptr(),
-                                         None, None, None, ws.data_ptr(), ws_bytes, s), "bwd")
+                                         None, None, None, ws.data_ptr(), ws_bytes, cs()), "bwd")
 
     def bwd():
         _lib.check(lib.asr_conv_backward(0, dy.data_ptr(), x.data_ptr(), mask.data_ptr(), w.data_ptr(),
                                          theta_dst.data_ptr(), pm.n_theta, h, 0.0, N, H, W, C, dt, dx.data_ptr(),
-                                         dth.data_ptr(), db.data_ptr(), None, ws.data_ptr(), ws_bytes, s), "bwd")
+                                         dth.data_ptr(), db.data_ptr(), None, ws.data_ptr(), ws_bytes, cs()), "bwd")
 
     if integrator == "rk2":
         xm = torch.empty_like(x)
@@ -156,31 +158,52 @@ def block_roofline(rt, lib, C, N, dtype_name, reps, h, integrator="euler"):
 
         def fwd():  # noqa: F811
             _lib.check(lib.asr_rk2_forward(x.data_ptr(), xm.data_ptr(), y.data_ptr(), mask.data_ptr(),
-                                           mask2.data_ptr(), w.data_ptr(), bias.data_ptr(), h, N, H, W, C, dt, s),
+                                           mask2.data_ptr(), w.data_ptr(), bias.data_ptr(), h, N, H, W, C, dt, cs()),
                        "rk2 fwd")
 
         def bwd():  # noqa: F811
             _lib.check(lib.asr_rk2_backward(dy.data_ptr(), x.data_ptr(), xm.data_ptr(), mask.data_ptr(),
                                             mask2.data_ptr(), w.data_ptr(), theta_dst.data_ptr(), pm.n_theta, h, 0.0,
                                             N, H, W, C, dt, dx.data_ptr(), dth.data_ptr(), db.data_ptr(), None,
-                                            ws.data_ptr(), ws_bytes, s), "rk2 bwd")
+                                            ws.data_ptr(), ws_bytes, cs()), "rk2 bwd")
         bwd_kernel = None
 
     for _ in range(10):
         fwd()
         bwd()
     torch.cuda.synchronize()
+    timing_mode = [None]
 
     def timed(fn):
-        # one event pair around `reps` back-to-back launches: the per-launch
-        # average then matches rocprofv3's kernel durations (events between
-        # every launch would add their own serialisation gaps)
+        # `reps` back-to-back launches captured in one HIP graph and replayed
+        # between two events on the replay stream: per-launch averages without
+        # the Python/ctypes launch path (at ~40 us per kernel that path, not the
+        # GPU, would set the pace); eager launches if capture is unavailable
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
-            fn()
-        e1.record()
-        torch.cuda.synchronize()
+        try:
+            gr = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                fn()
+            torch.cuda.current_stream().wait_stream(side)
+            with torch.cuda.graph(gr):
+                for _ in range(reps):
+                    fn()
+            gr.replay()
+            torch.cuda.synchronize()
+            e0.record()
+            gr.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            timing_mode[0] = "hip graph of %d launches, events around the replay" % reps
+        except Exception as ex:  # noqa: BLE001
+            timing_mode[0] = "eager launches (graph capture failed: %s)" % type(ex).__name__
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps * 1e-3
 
     tf = timed(fwd)
@@ -193,7 +216,7 @@ def block_roofline(rt, lib, C, N, dtype_name, reps, h, integrator="euler"):
     bytes_alg = (12 if stages == 2 else 5) * P * esz  # see the docstring
     flops = stages * 3 * 2 * 9 * C * C * N * H * W
     return dict(t_fwd=tf, t_bwd_kernel=tbk, t_bwd=tb, t=t_blk, bytes=bytes_alg, flops=flops,
-                bytes_fwd=2 * P * esz, bytes_bwd=3 * P * esz)
+                bytes_fwd=2 * P * esz, bytes_bwd=3 * P * esz, timing=timing_mode[0])
 
 
 def stack_roofline(rt, N, L, reps, h):
@@ -420,10 +443,13 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": ("fused stack of all L Euler blocks, fwd + bwd (deep::k_fwd16_fused, deep::k_bwd16_fused, "
                            "k_reduce_slabs, k_project_layers)" if deep else
-                           "RK2 block fwd+bwd (2x blk::k_fwd_pipe, blk::k_bwd2 stage 2 + blk::k_bwd2<XT> stage 1 on "
-                           "one slab set, k_reduce_slabs, k_project)" if integrator == "rk2" else
-                           "Euler block fwd+bwd (blk::k_fwd_pipe, blk::k_bwd2 fused dgrad+wgrad, k_reduce_slabs, "
+                           "RK2 block fwd+bwd (blk::k_fwd3 stage 1 + blk::k_fwd_pipe<RESG> stage 2, blk::k_bwd3 stage 2 "
+                           "+ blk::k_bwd3<XT> stage 1 on one slab set, k_reduce_slabs, k_project)"
+                           if integrator == "rk2" and C == 64 else
+                           "Euler block fwd+bwd (blk::k_fwd3, blk::k_bwd3 fused dgrad+wgrad, k_reduce_slabs, k_project)"
+                           if C == 64 else "block fwd+bwd (blk::k_fwd_pipe / k_fwd, blk::k_bwd, k_reduce_slabs, "
                            "k_project)"),
+                "timing": rb.get("timing") or "events around back-to-back launches",
                 "operands": "random (x, dy ~ N(0,1) in bf16, theta ~ N(0, 0.05^2))",
                 "algorithmic_bytes": rb["bytes"], "avg_us": round(rb["t"] * 1e6, 2),
                 "mfma_tflops": round(tflops, 1), "mfma_frac": round(tflops / peak_tf, 4),

@@ -65,6 +65,9 @@
 #ifndef ASR_FWD3
 #define ASR_FWD3 1  // C=64 forward (Euler without RK2 residual, plain conv): k_fwd3 at 3 WGs per CU (0: k_fwd_pipe)
 #endif
+#ifndef ASR_BWD3
+#define ASR_BWD3 1  // C=64 backward: k_bwd3 (12 waves, 3 per SIMD; 0: k_bwd2, 8 waves)
+#endif
 #ifndef ASR_ABLATE
 #define ASR_ABLATE 0  // development only: fwd 1 no epilogue, 2 no MFMA, 3 no prefetch DMA;
                       // bwd 4 no convert, 5 no dgrad MFMA, 6 no wgrad MFMA, 7 no dgrad epilogue,
@@ -102,6 +105,44 @@ __device__ unsigned long long g_stamps[512][2][kStampBands][kStampSlots];
 #endif
 
 enum { FWD_EULER = 0, FWD_CONV = 1, BWD_EULER = 2, BWD_CONV = 3 };
+
+// Diagnostic build only (-DASR_BLK_TRACE=1): s_memtime stamps per band of
+// workgroup 0 in k_fwd3 (kernel 0, wave 0) and k_bwd3 (kernel 1, role 0 =
+// dgrad wave 0, role 1 = wgrad wave 4), and the clock probe pair (s_memtime,
+// s_memrealtime) at the start and end of wave 0 in every workgroup; into
+// buffers nothing else reads (asr_debug_blk_trace).
+#ifndef ASR_BLK_TRACE
+#define ASR_BLK_TRACE 0
+#endif
+#if ASR_BLK_TRACE
+constexpr int kTrBands = 40, kTrSlots = 6;
+__device__ unsigned long long g_btrace[2][2][kTrBands][kTrSlots];
+__device__ unsigned long long g_bclock[2][1024][4];
+__device__ __forceinline__ void tr_store(unsigned long long* p, unsigned long long t) {
+  unsigned lo = (unsigned)t, hi = (unsigned)(t >> 32);
+  asm volatile("v_mov_b32 %0, %0\n\tv_mov_b32 %1, %1" : "+v"(lo), "+v"(hi));  // vector store
+  *p = ((unsigned long long)hi << 32) | lo;
+}
+#define ASR_BTR(kern, role, band, slot)                                                         \
+  do {                                                                                          \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (band) < kTrBands)                        \
+      tr_store(&g_btrace[kern][role][band][slot], __builtin_amdgcn_s_memtime());                \
+  } while (0)
+#define ASR_BCLK(kern, which)                                                                    \
+  do {                                                                                           \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) {                                                 \
+      tr_store(&g_bclock[kern][blockIdx.x][2 * (which)], __builtin_amdgcn_s_memtime());          \
+      tr_store(&g_bclock[kern][blockIdx.x][2 * (which) + 1], __builtin_amdgcn_s_memrealtime());  \
+    }                                                                                            \
+  } while (0)
+#else
+#define ASR_BTR(kern, role, band, slot) \
+  do {                                  \
+  } while (0)
+#define ASR_BCLK(kern, which) \
+  do {                        \
+  } while (0)
+#endif
 
 template <int C>
 struct Geo {
@@ -859,9 +900,12 @@ __global__ __launch_bounds__(256, WPE) void k_fwd3(const bf16* __restrict__ x, b
     dma_rows<C, W>(x, lds, cur.n, yy - 1, min(BR, H - yy) + 2, H, wave, NW, lane);
   }
   int nst = 0;  // vector-memory ops issued after the DMA the next barrier waits for
+  ASR_BCLK(0, 0);
   for (int it = i0; it < i1; ++it, cur.next(nb), nxt.next(nb)) {
     const int buf = (it - i0) & 1;
+    if (wave == 0) ASR_BTR(0, 0, it - i0, 0);
     barrier_vm(nst);  // band it landed; every wave is done with band it-1's tile
+    if (wave == 0) ASR_BTR(0, 0, it - i0, 1);
     nst = 0;
     if (it + 1 < i1) {
       // the next band into the other buffer; its rows 0, 1 are this band's rows
@@ -887,7 +931,9 @@ __global__ __launch_bounds__(256, WPE) void k_fwd3(const bf16* __restrict__ x, b
     for (int r = 0; r < RB; ++r)
 #pragma unroll
       for (int pt = 0; pt < 2; ++pt) acc[r][pt] = f32x4{bz[0], bz[1], bz[2], bz[3]};
+    if (wave == 0) ASR_BTR(0, 0, it - i0, 2);
     conv_band<C, W, RB>(tb, lo, A, acc);
+    if (wave == 0) ASR_BTR(0, 0, it - i0, 3);
     u32x4 xr[RB];
     if constexpr (EULER) {
 #pragma unroll
@@ -924,7 +970,9 @@ __global__ __launch_bounds__(256, WPE) void k_fwd3(const bf16* __restrict__ x, b
       *(u32x4*)(yb + r * W * C * 2) = yw;
       ++nst;
     }
+    if (wave == 0) ASR_BTR(0, 0, it - i0, 4);
   }
+  ASR_BCLK(0, 1);
 }
 
 // ===========================================================================
@@ -2051,6 +2099,426 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
 }
 
 // ===========================================================================
+// Backward v3 (C=64, W=32, BR=4): k_bwd2's band protocol (double-buffered
+// dy / x / dz tiles, the next band's dz converted by the dgrad waves from
+// their own dy rows, x DMA + halo copy by the wgrad waves, the previous
+// block's slab pass folded in) at three waves per SIMD (12 waves, <= 168
+// VGPRs):
+//   waves 0-3  dgrad, one 16-channel o-tile each over the whole band (the
+//              forward's band conv on the dz tile: A 72 VGPRs), epilogue on
+//              the regrouped accumulators (16-B dy / dz / x chunk reads, one
+//              16-B dx store per row, db over 8 channels per lane);
+//   waves 4-11 wgrad, m-tile group tg = (w-4)/2 (9 m-tiles) x o-tiles
+//              2*((w-4)&1) + 0..1: 72 accumulator VGPRs, 18 MFMAs per k-step.
+// dW accumulates in k_bwd2's order (bitwise the same slabs); dx sums the taps
+// in the band conv's order, db over the regrouped lanes.
+// ===========================================================================
+template <int C, int W, int BR, int MODE, bool RO, bool XT = false>
+__global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                 const uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
+                                                 float h, float two_gamma, int N, int H, bf16* __restrict__ dx,
+                                                 float* __restrict__ slabs, const float* __restrict__ pslabs, int pP,
+                                                 float* __restrict__ pgrp, int skip_dy,
+                                                 const bf16* __restrict__ extra = nullptr) {
+  using G = Geo<C>;
+  using L = Bwd2Lds<C, W, BR>;
+  using BD = Band<C, W, BR>;
+  constexpr int TW = W + 2, OT = G::OT, MTW = G::MTW, IPR = W / G::PPI, NQ = G::NQ;
+  constexpr bool EULER = MODE == BWD_EULER;
+  static_assert(C == 64 && W == 32 && BR == 4 && MTW == 9 && OT == 4, "v3 backward geometry");
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, lx = lane & 15;
+
+  for (int b = 0; b < 2; ++b) {
+    zero_halo_cols<C, W>(lds + L::DY + b * L::TILE, BR + 2, tid, 768);
+    zero_halo_cols<C, W>(lds + L::X + b * L::TILE, BR + 2, tid, 768);
+    zero_halo_cols<C, W>(lds + L::DZ + b * L::TILE, BR + 2, tid, 768);
+  }
+  if (ASR_V2_MASKTAB && EULER) {  // dword d of byte m's entry: 0xffff per set bit of (m >> 2d) & 3
+    unsigned* tab = (unsigned*)(lds + L::MTAB);
+    for (int i = tid; i < 1024; i += 768) {
+      const unsigned m = (unsigned)i >> 2, d = (unsigned)i & 3;
+      tab[i] = (((m >> (2 * d)) & 1u) ? 0xffffu : 0u) | (((m >> (2 * d + 1)) & 1u) ? 0xffff0000u : 0u);
+    }
+  }
+  const int nb = (H + BR - 1) / BR;
+  int i0, i1;
+  item_range(N * nb, &i0, &i1);
+  const unsigned loff = (unsigned)dma_lane_off<C, W>(lane) * 2u;
+  float* slab = slabs + (long)blockIdx.x * (9 * C * C + C);
+  const float hs = EULER ? h : 1.f;  // dz = hs * dzm (dzm = dy*mask in LDS)
+  const float hs2g = hs * two_gamma;
+  __syncthreads();  // halo columns zeroed before any convert / copy writes near them
+  ASR_BCLK(1, 0);
+
+  // pass 1 of the previous block's slab reduction (as k_bwd2), on the wgrad
+  // waves only: thread ft = tid - 256 owns one 16-B chunk of one group row
+  constexpr int ES = 9 * C * C + C, ECH = ES / 4;
+  const int ft = tid - 256;
+  const long fT = (long)((pP + 31) / 32) * ECH;
+  const long fc0 = (long)blockIdx.x * fT / gridDim.x, fc1 = (long)(blockIdx.x + 1) * fT / gridDim.x;
+  const bool fold = pP > 0 && ft >= 0 && fc0 + ft < fc1;
+  const int fg = fold ? (int)((fc0 + ft) / ECH) : 0;
+  const int fpe = min(pP, 32 * fg + 32);
+  int fp = 32 * fg;
+  unsigned foff = fold ? (unsigned)fp * ES + (unsigned)((fc0 + ft) % ECH) * 4 : 0u;
+  f32x4 facc = {0.f, 0.f, 0.f, 0.f}, fv[2];
+
+  if (wave < 4) {
+    // ---------------- dgrad waves ----------------
+    const int ot = wave;
+    bf16x8 A[G::KS];
+    load_A1<C>(wpack, ot, lane, A);
+    unsigned lo[3 * BD::NCB];
+    band_lane_offsets<C, W, BR>(g, lx, lo);
+    const int px = lx + 16 * (g & 1), cg = 2 * ot + (g >> 1);  // regrouped: pixel, 16-B channel chunk
+    const unsigned lch = (unsigned)toff<C>(1, px + 1, cg, TW);  // output row 0's chunk in a tile
+    const unsigned ldx = (unsigned)(px * C + 8 * cg) * 2u;
+    int nst = 0;
+    ItemCursor cur(i0, nb);
+    for (int it = i0; it < i1; ++it, cur.next(nb)) {
+      const int buf = (it - i0) & 1;
+      const int n = cur.n, y0 = cur.b * BR;
+      const int rows = min(BR, H - y0);
+      if (wave == 0) ASR_BTR(1, 0, it - i0, 0);
+      barrier_vm(nst);  // band it staged everywhere; band it-1 fully consumed
+      if (wave == 0) ASR_BTR(1, 0, it - i0, 1);
+      // XT: the extra dx term of the band's rows (in flight during the conv)
+      u32x4 exv[XT ? BR : 1];
+      if constexpr (XT) {
+        const bf16* eb = extra + ((long)n * H + y0) * W * C;
+#pragma unroll
+        for (int r = 0; r < BR; ++r) {
+          const int rr = min(r, rows - 1);
+          exv[r] = *(const u32x4*)((const unsigned char*)(eb + (long)rr * W * C) + ldx);
+        }
+      }
+      const unsigned dzt = lds_u32(lds + L::DZ + buf * L::TILE), dyt = lds_u32(lds + L::DY + buf * L::TILE);
+      const unsigned xt = lds_u32(lds + L::X + buf * L::TILE);
+      f32x4 acc[BR][2];
+#pragma unroll
+      for (int r = 0; r < BR; ++r) acc[r][0] = acc[r][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (wave == 0) ASR_BTR(1, 0, it - i0, 2);
+      conv_band<C, W, BR>(dzt, lo, A, acc);
+      if (wave == 0) ASR_BTR(1, 0, it - i0, 3);
+      // epilogue, LDS reads one row ahead: dy (the residual), dz only for the
+      // 2*gamma*dz term (gamma != 0), x for RO
+      const bool g2 = hs2g != 0.f;
+      bf16* drow = dx ? dx + ((long)n * H + y0) * W * C : nullptr;
+      u32x4 dyw[2], dzw[2], xw[2];
+      auto issue = [&](int r, int sl) {
+        const unsigned co = lch + (unsigned)(r * L::ROWB);
+        if (EULER) dyw[sl] = lds_rd128(dyt + co);
+        if (g2) dzw[sl] = lds_rd128(dzt + co);
+        if constexpr (RO) xw[sl] = lds_rd128(xt + co);
+      };
+      issue(0, 0);
+      int nld = 0;
+      static_for<0, BR>([&](auto rc) {
+        constexpr int r = decltype(rc)::value, sl = r & 1;
+        if (r < rows) {
+          if (r + 1 < rows) {
+            issue(r + 1, sl ^ 1);
+            // wait for row r's reads only (row r+1's still in flight)
+            if (g2) {
+              if (EULER) lgkm_wait<(RO ? 3 : 2)>();
+              else lgkm_wait<(RO ? 2 : 1)>();
+            } else if (EULER) lgkm_wait<(RO ? 2 : 1)>();
+            else if (RO) lgkm_wait<1>();
+          } else {
+            lgkm_wait<0>();
+          }
+          float z[8];
+          regroup(acc[r][0], acc[r][1], z);
+          u32x4 ow;
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            float v0, v1;
+            if constexpr (EULER) {
+              float r0 = skip_dy ? 0.f : lo_f(dyw[sl][d]), r1 = skip_dy ? 0.f : hi_f(dyw[sl][d]);
+              if constexpr (XT) {
+                r0 += lo_f(exv[r][d]);
+                r1 += hi_f(exv[r][d]);
+              }
+              v0 = fmaf(-hs, z[2 * d], r0);
+              v1 = fmaf(-hs, z[2 * d + 1], r1);
+              if (g2) {
+                v0 = fmaf(hs2g, lo_f(dzw[sl][d]), v0);
+                v1 = fmaf(hs2g, hi_f(dzw[sl][d]), v1);
+              }
+            } else {
+              v0 = -z[2 * d];
+              v1 = -z[2 * d + 1];
+              if (g2) {
+                v0 = fmaf(two_gamma, lo_f(dzw[sl][d]), v0);
+                v1 = fmaf(two_gamma, hi_f(dzw[sl][d]), v1);
+              }
+            }
+            ow[d] = pk_bf16(v0, v1);
+            if constexpr (RO) {  // bf16 x > 0: positive as a signed 16-bit integer
+              const unsigned xd = xw[sl][d];
+              ow[d] &= ((int)(short)(xd & 0xffffu) > 0 ? 0xffffu : 0u) | ((int)xd > 0xffff ? 0xffff0000u : 0u);
+            }
+          }
+          if (drow) {
+            *(u32x4*)((unsigned char*)(drow + (long)r * W * C) + ldx) = ow;
+            ++nld;
+          }
+        }
+      });
+      if (wave == 0) ASR_BTR(1, 0, it - i0, 4);
+      if (wave == 0) ASR_BTR(1, 0, it - i0, 5);
+      nst = nld;
+    }
+    barrier_vm(0);  // matches the wgrad waves' end-of-loop barrier
+  } else {
+    // ---------------- wgrad waves ----------------
+    const int w8 = __builtin_amdgcn_readfirstlane(wave) - 4;
+    const int tg = w8 >> 1, oq = 2 * (w8 & 1);  // m-tiles tg*9 .. +8, o-tiles oq, oq+1
+    const int tq = lx >> 2, tp = lx & 3;
+    f32x4 acc[MTW][2];
+#pragma unroll
+    for (int mi = 0; mi < MTW; ++mi) acc[mi][0] = acc[mi][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // per-lane byte offsets (tile row 0) of the transposed fragment reads:
+    // A = x at tap (ky, kx) of m-tile tg*9 + mi, B = dz of o-tile oq + oi (output row 0 = tile row 1)
+    // LDS byte addresses in the current band's buffer (row r's r * ROWB is an immediate)
+    unsigned offA[MTW][2], offB[2][2];
+    {
+      const unsigned xb0 = lds_u32(lds + L::X), zb0 = lds_u32(lds + L::DZ);
+      const int pb = 8 * g + tq;
+#pragma unroll
+      for (int mi = 0; mi < MTW; ++mi) {
+        const int mt = tg * MTW + mi;
+        const int tap = (16 * mt) / C, itile = ((16 * mt) % C) / 16;
+        const int ky = tap / 3, kx = tap % 3, q = 2 * itile + (tp >> 1);
+        offA[mi][0] = xb0 + (unsigned)(toff<C>(ky, pb + kx, q, TW) + 8 * (tp & 1));
+        offA[mi][1] = xb0 + (unsigned)(toff<C>(ky, pb + 4 + kx, q, TW) + 8 * (tp & 1));
+      }
+#pragma unroll
+      for (int oi = 0; oi < 2; ++oi) {
+        const int q = 2 * (oq + oi) + (tp >> 1);
+        offB[oi][0] = zb0 + (unsigned)(toff<C>(1, pb + 1, q, TW) + 8 * (tp & 1));
+        offB[oi][1] = zb0 + (unsigned)(toff<C>(1, pb + 5, q, TW) + 8 * (tp & 1));
+      }
+      // opaque to the compiler: kept in VGPRs, not recomputed per band
+#pragma unroll
+      for (int mi = 0; mi < MTW; ++mi) asm volatile("" : "+v"(offA[mi][0]), "+v"(offA[mi][1]));
+      asm volatile("" : "+v"(offB[0][0]), "+v"(offB[0][1]), "+v"(offB[1][0]), "+v"(offB[1][1]));
+    }
+    // the next band's dz: wgrad wave w8 owns tile row 2 + w8 (w8 < 4) of a band that
+    // continues the image, row w8 (w8 < 6) of one that starts an image; it DMAs
+    // that row's dy, loads its mask dwords and converts it (its own vmcnt covers both)
+    auto own_row = [&](bool reuse) { return reuse ? (w8 < 4 ? 2 + w8 : -1) : (w8 < 6 ? w8 : -1); };
+    auto stage_own = [&](const ItemCursor& c, int row, int nbuf, unsigned& mwv) {
+      if (row < 0) return;
+      if constexpr (EULER) mwv = bwd2_mask_word<C, W>(mask, c.n, c.b * BR, row, H, lane);
+      for (int j = 0; j < IPR; ++j)
+        dma_row_instr<C, W>(dy, lds + L::DY + nbuf * L::TILE + row * L::ROWB, c.n, c.b * BR - 1 + row, j, H, loff);
+    };
+    // dz = dy & mask of the own row (lane = pixel lane&31, chunks 4*(lane>>5) + j),
+    // two chunks at a time, compiler-visible LDS accesses (this role's live state
+    // leaves little room: a spilled inline-asm read result would be garbage)
+    auto convert_own = [&](int row, int nbuf, unsigned mwv) {
+      if (row < 0) return;
+      const unsigned base = lds_u32(lds);
+      const int cpx = lane & 31, hh = lane >> 5;
+#pragma unroll
+      for (int jj = 0; jj < 4; jj += 2) {
+        u32x4 v[2], mt[2];
+        unsigned off[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          off[j] = (unsigned)toff<C>(row, cpx + 1, 4 * hh + jj + j, TW) + (unsigned)(nbuf * L::TILE);
+          v[j] = lds_ld128(base + L::DY + off[j]);
+          if (EULER && ASR_V2_MASKTAB) mt[j] = lds_ld128(base + L::MTAB + __builtin_amdgcn_ubfe(mwv, 8 * (jj + j), 8) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          u32x4 z = v[j];
+          if constexpr (EULER && ASR_V2_MASKTAB) {
+            z &= mt[j];
+          } else if constexpr (EULER) {
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+              const unsigned lo = (unsigned)__builtin_amdgcn_sbfe((int)mwv, 8 * (jj + j) + 2 * d, 1);
+              const unsigned hi = (unsigned)__builtin_amdgcn_sbfe((int)mwv, 8 * (jj + j) + 2 * d + 1, 1);
+              z[d] &= __builtin_amdgcn_perm(hi, lo, 0x07060100u);
+            }
+          }
+          lds_st128(base + L::DZ + off[j], z);
+        }
+      }
+    };
+    // db on MFMA (tile group 3): ones(16 x 32) x dz^T, every row of the result = db
+    bf16x8 ones;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
+    f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    const bool dbw = tg == 3;
+    if (i0 < i1) {  // prologue: dy rows (own) and x rows of band i0, its dz converted
+      const ItemCursor c0(i0, nb);
+      unsigned mw0 = 0u;
+      const int row0 = own_row(false);
+      stage_own(c0, row0, 0, mw0);
+      for (int j = w8; j < (BR + 2) * IPR; j += 8) dma_row_instr<C, W>(x, lds + L::X, c0.n, c0.b * BR - 1, j, H, loff);
+      // (the band loop's x DMA runs on waves w8 >= 4 only: waves 0-3 DMA the own dy rows)
+      vm_wait(0);
+      convert_own(row0, 0, mw0);
+    }
+    ItemCursor cur(i0, nb), nxt(i0, nb);
+    nxt.next(nb);
+    for (int it = i0; it < i1; ++it, cur.next(nb), nxt.next(nb)) {
+      const int buf = (it - i0) & 1;
+      const int y0 = cur.b * BR;
+      const int rows = min(BR, H - y0);
+      if (wave == 4) ASR_BTR(1, 1, it - i0, 0);
+      barrier_vm(0);  // this wave's x rows of band it landed
+      if (wave == 4) ASR_BTR(1, 1, it - i0, 1);
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if (fold && fp + q < fpe) fv[q] = *(const f32x4*)(pslabs + foff + (unsigned)q * ES);
+      const bool more = it + 1 < i1;
+      const int orow = more ? own_row(nxt.n == cur.n) : -1;
+      unsigned mwv = 0u;
+      stage_own(nxt, orow, buf ^ 1, mwv);
+      // x rows of band it+1 (rows 2.. when it continues this band's image)
+      const int xr0 = nxt.n == cur.n ? 2 : 0;
+      if (it + 1 < i1) {
+        unsigned char* xn = lds + L::X + (buf ^ 1) * L::TILE + xr0 * L::ROWB;
+        const int xy = nxt.b * BR - 1 + xr0;
+        for (int j = w8 - 4; j < (BR + 2 - xr0) * IPR; j += 4)
+          if (j >= 0) dma_row_instr<C, W>(x, xn, nxt.n, xy, j, H, loff);
+      }
+      bf16x8 Bf[2], Ar[3];
+      if (wave == 4) ASR_BTR(1, 1, it - i0, 2);
+      // A fragments two m-tiles ahead (ring of 3), as k_bwd2
+      auto mfma_band = [&](auto bo) {
+        constexpr int BO = decltype(bo)::value;
+        Ar[0] = tr_pair_at<BO>(offA[0][0], offA[0][1]);
+        static_for<0, BR>([&](auto rc) {
+          constexpr int r = decltype(rc)::value, RO_ = BO + r * L::ROWB;
+          __builtin_amdgcn_sched_barrier(0);  // no hoisting of later rows' reads (register pressure)
+          if (r < rows) {
+            const bool mr = r + 1 < rows;
+#pragma unroll
+            for (int oi = 0; oi < 2; ++oi) Bf[oi] = tr_pair_at<RO_>(offB[oi][0], offB[oi][1]);
+            Ar[1] = tr_pair_at<RO_>(offA[1][0], offA[1][1]);
+            static_for<0, MTW>([&](auto mc) {
+              constexpr int mi = decltype(mc)::value;
+              if constexpr (mi + 2 < MTW) Ar[(mi + 2) % 3] = tr_pair_at<RO_>(offA[mi + 2][0], offA[mi + 2][1]);
+              else if constexpr (mi + 2 == MTW && r + 1 < BR) {
+                if (mr) Ar[0] = tr_pair_at<RO_ + L::ROWB>(offA[0][0], offA[0][1]);  // MTW % 3 == 0: slot 0 again
+              }
+#pragma unroll
+              for (int oi = 0; oi < 2; ++oi)
+                acc[mi][oi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ar[mi % 3], Bf[oi], acc[mi][oi], 0, 0, 0);
+            });
+            if (dbw) {
+#pragma unroll
+              for (int oi = 0; oi < 2; ++oi)
+                accb[oi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, Bf[oi], accb[oi], 0, 0, 0);
+            }
+          }
+        });
+      };
+      if (it > i0) {  // the offsets follow the buffer (in place: no second register set)
+        const unsigned dlt = buf ? (unsigned)L::TILE : (unsigned)-L::TILE;
+#pragma unroll
+        for (int mi = 0; mi < MTW; ++mi) offA[mi][0] += dlt, offA[mi][1] += dlt;
+#pragma unroll
+        for (int oi = 0; oi < 2; ++oi) offB[oi][0] += dlt, offB[oi][1] += dlt;
+      }
+      mfma_band(std::integral_constant<int, 0>{});
+      if (more) {
+        vm_wait(0);  // own dy row and mask dwords of band it+1 (x DMA and fold loads too: long landed)
+        convert_own(orow, buf ^ 1, mwv);
+      }
+      if (wave == 4) ASR_BTR(1, 1, it - i0, 3);
+      // halo rows of a band that continues this band's image: dz rows BR, BR+1
+      // -> 0, 1 (masked), x rows BR, BR+1 -> 0, 1, dy row BR+1 -> 1; 5 x 256
+      // chunks over the 512 wgrad threads
+      if (it + 1 < i1 && nxt.n == cur.n) {
+        const unsigned base = lds_u32(lds);
+        const int nbf = buf ^ 1;
+        u32x4 cv[3];
+        unsigned dst[3];
+        int nc = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int c = ft + 512 * k;
+          if (c < 5 * 256) {
+            const int which = c >> 8;
+            const unsigned o = (unsigned)((c & 255) + NQ) * 16u;
+            const unsigned sreg = which < 2 ? L::DZ : which < 4 ? L::X : L::DY;
+            const int srow = which == 4 ? BR + 1 : BR + (which & 1);
+            const int drow = which == 4 ? 1 : (which & 1);
+            cv[k] = lds_rd128(base + sreg + buf * L::TILE + srow * L::ROWB + o);
+            dst[k] = base + sreg + nbf * L::TILE + drow * L::ROWB + o;
+            nc = k + 1;
+          }
+        }
+        lgkm_wait<0>();
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          if (k < nc) lds_wr128(dst[k], cv[k]);
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if (fold && fp < fpe) {
+          facc += fv[q];
+          ++fp;
+          foff += ES;
+        }
+      if (wave == 4) ASR_BTR(1, 1, it - i0, 4);
+    }
+    barrier_vm(0);  // all items consumed: LDS reusable
+    if (dbw && g == 0) {
+      float* dbl = (float*)lds + 12288;  // [C]
+#pragma unroll
+      for (int oi = 0; oi < 2; ++oi) dbl[16 * (oq + oi) + lx] = hs * accb[oi][0];
+    }
+    constexpr int MC = XT ? 3 : MTW;
+#pragma unroll
+    for (int m0 = 0; m0 < MTW; m0 += MC) {
+      float prev[XT ? MC : 1][2][4];
+      if constexpr (XT) {
+#pragma unroll
+        for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+          for (int oi = 0; oi < 2; ++oi)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              prev[mi][oi][e] = slab[(long)(16 * (tg * MTW + m0 + mi) + 4 * g + e) * C + 16 * (oq + oi) + lx];
+      }
+#pragma unroll
+      for (int mi = 0; mi < MC; ++mi)
+#pragma unroll
+        for (int oi = 0; oi < 2; ++oi)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int m = 16 * (tg * MTW + m0 + mi) + 4 * g + e;
+            float v = hs * acc[m0 + mi][oi][e];
+            if constexpr (XT) v += prev[mi][oi][e];
+            slab[(long)m * C + 16 * (oq + oi) + lx] = v;
+          }
+    }
+  }
+  __syncthreads();
+  if (tid < C) {
+    const float* dbl = (const float*)lds + 12288;
+    float s = dbl[tid];
+    if constexpr (XT) s += slab[9 * C * C + tid];
+    slab[9 * C * C + tid] = s;
+  }
+  if (fold) {  // slabs the bands did not cover (a WG with fewer than 16 bands)
+    for (; fp < fpe; ++fp, foff += ES) facc += *(const f32x4*)(pslabs + foff);
+    *(f32x4*)(pgrp + (long)fg * ES + (foff - (unsigned)fpe * ES)) = facc;
+  }
+  ASR_BCLK(1, 1);
+}
+
+// ===========================================================================
 // Stem weight gradient on MFMA (C = 16 or 64, CIN=3, W=32, H % 8 == 0), from dz1 =
 // dx1 * [x1 > 0] (written by the first block's backward, k_bwd2<..., RO>):
 //   dW1[kappa][o] = inv_std * sum_p (img[p + tap] - mean)[ci] * dz1[p][o]
@@ -2265,6 +2733,15 @@ __global__ __launch_bounds__(256) void k_stem_fwd_mfma(const Tin* __restrict__ i
 constexpr int kBwdBR = 4;
 constexpr int kMaxBlockSlabs = 512;
 
+#if ASR_BLK_TRACE
+}  // namespace asr
+extern "C" int asr_debug_blk_trace(void* trace, size_t tbytes, void* clock, size_t cbytes) {
+  if (hipMemcpyFromSymbol(trace, HIP_SYMBOL(asr::blk::g_btrace), tbytes) != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(clock, HIP_SYMBOL(asr::blk::g_bclock), cbytes) == hipSuccess ? 0 : -1;
+}
+namespace asr {
+#endif
+
 static int persistent_grid(long items) {
   int cus = cu_count();
   if (cus <= 0) cus = 256;
@@ -2351,6 +2828,22 @@ static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* ma
       // the folded pass gives each thread one 16-B chunk: at most 512 per WG
       const long fchunks = (long)((fold_P + 31) / 32) * ((9 * C * C + C) / 4);
       if ((fchunks + grid - 1) / grid > 512) fold_P = 0;
+      if (ASR_BWD3) {
+#define ASR_LAUNCH_BWD3(M, RO, XT)                                                                            \
+  hipLaunchKernelGGL((blk::k_bwd3<C, W, kBwdBR, M, RO, XT>), dim3(grid), dim3(768), lds2, s, (const bf16*)dy,    \
+                     (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs, fold_slabs, fold_P, \
+                     fold_grp, skip_dy, (const bf16*)extra)
+        if (xt2) ASR_LAUNCH_BWD3(blk::BWD_EULER, false, true);
+        else if (mode == blk::BWD_EULER && relu_dx) {
+          ASR_LAUNCH_BWD3(blk::BWD_EULER, true, false);
+          if (relu_done) *relu_done = 1;
+        } else if (mode == blk::BWD_EULER) ASR_LAUNCH_BWD3(blk::BWD_EULER, false, false);
+        else ASR_LAUNCH_BWD3(blk::BWD_CONV, false, false);
+#undef ASR_LAUNCH_BWD3
+        ASR_LAUNCH_CHECK("k_bwd3");
+        if (fold_done) *fold_done = fold_P > 0;
+        return ASR_OK;
+      }
       if (xt2) {
         hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_EULER, false, true>), dim3(grid), dim3(512), lds2, s,
                            (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs,

@@ -145,6 +145,27 @@ __device__ __forceinline__ int strided_count(int total, int wave, int nw) {
   return total > wave ? (total - wave + nw - 1) / nw : 0;
 }
 
+// compiler-visible 16-B LDS load / store at an LDS byte address (integer -> LDS
+// pointer, no generic cast): hipcc places the lgkmcnt waits itself, so spilling
+// or copying the result is safe
+__device__ __forceinline__ u32x4 lds_ld128(unsigned a) {
+  return *(const __attribute__((address_space(3))) u32x4*)(size_t)a;
+}
+__device__ __forceinline__ void lds_st128(unsigned a, u32x4 v) {
+  *(__attribute__((address_space(3))) u32x4*)(size_t)a = v;
+}
+
+// tr_pair from LDS byte addresses (+ a compile-time offset the compiler folds
+// into the instruction's offset field); integer -> LDS pointer, no generic cast
+template <int OFF>
+__device__ __forceinline__ bf16x8 tr_pair_at(unsigned a0, unsigned a1) {
+  typedef __attribute__((address_space(3))) s16x4* lp;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(size_t)(a0 + OFF));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(size_t)(a1 + OFF));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return *(bf16x8*)&c;
+}
 __device__ __forceinline__ bf16x8 tr_pair(const unsigned char* p0, const unsigned char* p1) {
   const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ASR_LDS s16x4*)p0);
   const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ASR_LDS s16x4*)p1);
