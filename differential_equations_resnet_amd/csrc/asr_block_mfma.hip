@@ -68,6 +68,9 @@
 #ifndef ASR_BWD3
 #define ASR_BWD3 1  // C=64 backward: k_bwd3 (12 waves, 3 per SIMD; 0: k_bwd2, 8 waves)
 #endif
+#ifndef ASR_BWD3_DMA0
+#define ASR_BWD3_DMA0 9  // k_bwd3 wgrad waves: DMA pieces issued right after the barrier, the rest one per row (A/B: spreading them lengthened the MFMA phase as much as it saved)
+#endif
 #ifndef ASR_ABLATE
 #define ASR_ABLATE 0  // development only: fwd 1 no epilogue, 2 no MFMA, 3 no prefetch DMA;
                       // bwd 4 no convert, 5 no dgrad MFMA, 6 no wgrad MFMA, 7 no dgrad epilogue,
@@ -2110,8 +2113,8 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
 //              16-B dx store per row, db over 8 channels per lane);
 //   waves 4-11 wgrad, m-tile group tg = (w-4)/2 (9 m-tiles) x o-tiles
 //              2*((w-4)&1) + 0..1: 72 accumulator VGPRs, 18 MFMAs per k-step.
-// dW accumulates in k_bwd2's order (bitwise the same slabs); dx sums the taps
-// in the band conv's order, db over the regrouped lanes.
+// dW sums the pixels of a row in a bank-conflict-free permutation, dx the taps
+// in the band conv's order, db on MFMA.
 // ===========================================================================
 template <int C, int W, int BR, int MODE, bool RO, bool XT = false>
 __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, const bf16* __restrict__ x,
@@ -2203,70 +2206,83 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
       conv_band<C, W, BR>(dzt, lo, A, acc);
       if (wave == 0) ASR_BTR(1, 0, it - i0, 3);
       // epilogue, LDS reads one row ahead: dy (the residual), dz only for the
-      // 2*gamma*dz term (gamma != 0), x for RO
-      const bool g2 = hs2g != 0.f;
+      // 2*gamma*dz term (gamma != 0), x for RO; the flags are compile-time in
+      // each instantiation (a runtime flag costs selects on every element)
       bf16* drow = dx ? dx + ((long)n * H + y0) * W * C : nullptr;
-      u32x4 dyw[2], dzw[2], xw[2];
-      auto issue = [&](int r, int sl) {
-        const unsigned co = lch + (unsigned)(r * L::ROWB);
-        if (EULER) dyw[sl] = lds_rd128(dyt + co);
-        if (g2) dzw[sl] = lds_rd128(dzt + co);
-        if constexpr (RO) xw[sl] = lds_rd128(xt + co);
-      };
-      issue(0, 0);
       int nld = 0;
-      static_for<0, BR>([&](auto rc) {
-        constexpr int r = decltype(rc)::value, sl = r & 1;
-        if (r < rows) {
-          if (r + 1 < rows) {
-            issue(r + 1, sl ^ 1);
-            // wait for row r's reads only (row r+1's still in flight)
-            if (g2) {
-              if (EULER) lgkm_wait<(RO ? 3 : 2)>();
-              else lgkm_wait<(RO ? 2 : 1)>();
-            } else if (EULER) lgkm_wait<(RO ? 2 : 1)>();
-            else if (RO) lgkm_wait<1>();
-          } else {
-            lgkm_wait<0>();
-          }
-          float z[8];
-          regroup(acc[r][0], acc[r][1], z);
-          u32x4 ow;
+      auto epilogue = [&](auto g2c, auto skc) {
+        constexpr bool G2 = decltype(g2c)::value, SKIP = decltype(skc)::value;
+        constexpr bool RDY = EULER && !SKIP;
+        constexpr int NR = (RDY ? 1 : 0) + (G2 ? 1 : 0) + (RO ? 1 : 0);  // LDS reads per row
+        u32x4 dyw[2], dzw[2], xw[2];
+        auto issue = [&](int r, int sl) {
+          const unsigned co = lch + (unsigned)(r * L::ROWB);
+          if constexpr (RDY) dyw[sl] = lds_rd128(dyt + co);
+          if constexpr (G2) dzw[sl] = lds_rd128(dzt + co);
+          if constexpr (RO) xw[sl] = lds_rd128(xt + co);
+        };
+        if constexpr (NR > 0) issue(0, 0);
+        static_for<0, BR>([&](auto rc) {
+          constexpr int r = decltype(rc)::value, sl = r & 1;
+          if (r < rows) {
+            if constexpr (NR > 0) {
+              if (r + 1 < rows) {
+                issue(r + 1, sl ^ 1);
+                lgkm_wait<NR>();  // row r's reads (row r+1's still in flight)
+              } else {
+                lgkm_wait<0>();
+              }
+            }
+            float z[8];
+            regroup(acc[r][0], acc[r][1], z);
+            u32x4 ow;
 #pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            float v0, v1;
-            if constexpr (EULER) {
-              float r0 = skip_dy ? 0.f : lo_f(dyw[sl][d]), r1 = skip_dy ? 0.f : hi_f(dyw[sl][d]);
-              if constexpr (XT) {
-                r0 += lo_f(exv[r][d]);
-                r1 += hi_f(exv[r][d]);
+            for (int d = 0; d < 4; ++d) {
+              float v0, v1;
+              if constexpr (EULER) {
+                float r0 = 0.f, r1 = 0.f;
+                if constexpr (RDY) r0 = lo_f(dyw[sl][d]), r1 = hi_f(dyw[sl][d]);
+                if constexpr (XT) {
+                  r0 += lo_f(exv[r][d]);
+                  r1 += hi_f(exv[r][d]);
+                }
+                v0 = fmaf(-hs, z[2 * d], r0);
+                v1 = fmaf(-hs, z[2 * d + 1], r1);
+                if constexpr (G2) {
+                  v0 = fmaf(hs2g, lo_f(dzw[sl][d]), v0);
+                  v1 = fmaf(hs2g, hi_f(dzw[sl][d]), v1);
+                }
+              } else {
+                v0 = -z[2 * d];
+                v1 = -z[2 * d + 1];
+                if constexpr (G2) {
+                  v0 = fmaf(two_gamma, lo_f(dzw[sl][d]), v0);
+                  v1 = fmaf(two_gamma, hi_f(dzw[sl][d]), v1);
+                }
               }
-              v0 = fmaf(-hs, z[2 * d], r0);
-              v1 = fmaf(-hs, z[2 * d + 1], r1);
-              if (g2) {
-                v0 = fmaf(hs2g, lo_f(dzw[sl][d]), v0);
-                v1 = fmaf(hs2g, hi_f(dzw[sl][d]), v1);
-              }
-            } else {
-              v0 = -z[2 * d];
-              v1 = -z[2 * d + 1];
-              if (g2) {
-                v0 = fmaf(two_gamma, lo_f(dzw[sl][d]), v0);
-                v1 = fmaf(two_gamma, hi_f(dzw[sl][d]), v1);
+              ow[d] = pk_bf16(v0, v1);
+              if constexpr (RO) {  // bf16 x > 0: positive as a signed 16-bit integer
+                const unsigned xd = xw[sl][d];
+                ow[d] &= ((int)(short)(xd & 0xffffu) > 0 ? 0xffffu : 0u) | ((int)xd > 0xffff ? 0xffff0000u : 0u);
               }
             }
-            ow[d] = pk_bf16(v0, v1);
-            if constexpr (RO) {  // bf16 x > 0: positive as a signed 16-bit integer
-              const unsigned xd = xw[sl][d];
-              ow[d] &= ((int)(short)(xd & 0xffffu) > 0 ? 0xffffu : 0u) | ((int)xd > 0xffff ? 0xffff0000u : 0u);
+            if (drow) {
+              *(u32x4*)((unsigned char*)(drow + (long)r * W * C) + ldx) = ow;
+              ++nld;
             }
           }
-          if (drow) {
-            *(u32x4*)((unsigned char*)(drow + (long)r * W * C) + ldx) = ow;
-            ++nld;
-          }
-        }
-      });
+        });
+      };
+      using T_ = std::true_type;
+      using F_ = std::false_type;
+      const bool g2 = hs2g != 0.f;
+      if (EULER && skip_dy) {
+        if (g2) epilogue(T_{}, T_{});
+        else epilogue(F_{}, T_{});
+      } else {
+        if (g2) epilogue(T_{}, F_{});
+        else epilogue(F_{}, F_{});
+      }
       if (wave == 0) ASR_BTR(1, 0, it - i0, 4);
       if (wave == 0) ASR_BTR(1, 0, it - i0, 5);
       nst = nld;
@@ -2282,24 +2298,29 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
     for (int mi = 0; mi < MTW; ++mi) acc[mi][0] = acc[mi][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     // per-lane byte offsets (tile row 0) of the transposed fragment reads:
     // A = x at tap (ky, kx) of m-tile tg*9 + mi, B = dz of o-tile oq + oi (output row 0 = tile row 1)
-    // LDS byte addresses in the current band's buffer (row r's r * ROWB is an immediate)
+    // LDS byte addresses in the current band's buffer (row r's r * ROWB is an immediate).
+    // K = the row's 32 pixels, lane group g reading pixels 4g + tq and 4g + 16 + tq
+    // (any pixel permutation shared by A and B gives the same GEMM): each 32-lane
+    // half then reads 8 consecutive tile columns, whose swizzled 8-B pieces cover
+    // the 64 banks once (pixels 8g + tq, 8g + 4 + tq, as k_bwd2 reads them, put
+    // columns c and c + 8 on the same banks: every read 2-way)
     unsigned offA[MTW][2], offB[2][2];
     {
       const unsigned xb0 = lds_u32(lds + L::X), zb0 = lds_u32(lds + L::DZ);
-      const int pb = 8 * g + tq;
+      const int pb = 4 * g + tq;
 #pragma unroll
       for (int mi = 0; mi < MTW; ++mi) {
         const int mt = tg * MTW + mi;
         const int tap = (16 * mt) / C, itile = ((16 * mt) % C) / 16;
         const int ky = tap / 3, kx = tap % 3, q = 2 * itile + (tp >> 1);
         offA[mi][0] = xb0 + (unsigned)(toff<C>(ky, pb + kx, q, TW) + 8 * (tp & 1));
-        offA[mi][1] = xb0 + (unsigned)(toff<C>(ky, pb + 4 + kx, q, TW) + 8 * (tp & 1));
+        offA[mi][1] = xb0 + (unsigned)(toff<C>(ky, pb + 16 + kx, q, TW) + 8 * (tp & 1));
       }
 #pragma unroll
       for (int oi = 0; oi < 2; ++oi) {
         const int q = 2 * (oq + oi) + (tp >> 1);
         offB[oi][0] = zb0 + (unsigned)(toff<C>(1, pb + 1, q, TW) + 8 * (tp & 1));
-        offB[oi][1] = zb0 + (unsigned)(toff<C>(1, pb + 5, q, TW) + 8 * (tp & 1));
+        offB[oi][1] = zb0 + (unsigned)(toff<C>(1, pb + 17, q, TW) + 8 * (tp & 1));
       }
       // opaque to the compiler: kept in VGPRs, not recomputed per band
 #pragma unroll
@@ -2381,15 +2402,29 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
       const bool more = it + 1 < i1;
       const int orow = more ? own_row(nxt.n == cur.n) : -1;
       unsigned mwv = 0u;
-      stage_own(nxt, orow, buf ^ 1, mwv);
-      // x rows of band it+1 (rows 2.. when it continues this band's image)
-      const int xr0 = nxt.n == cur.n ? 2 : 0;
-      if (it + 1 < i1) {
-        unsigned char* xn = lds + L::X + (buf ^ 1) * L::TILE + xr0 * L::ROWB;
-        const int xy = nxt.b * BR - 1 + xr0;
-        for (int j = w8 - 4; j < (BR + 2 - xr0) * IPR; j += 4)
-          if (j >= 0) dma_row_instr<C, W>(x, xn, nxt.n, xy, j, H, loff);
+      // the next band's DMA pieces of this wave: own dy row (waves 0-3, or 0-5 when
+      // the next band starts an image), x rows (waves 4-7; rows 2.. when it
+      // continues this band's image); issued ASR_BWD3_DMA0 at once, the rest one
+      // after each of the first rows' MFMAs (a piece among MFMAs issues cheaper)
+      if constexpr (EULER) {
+        if (orow >= 0) mwv = bwd2_mask_word<C, W>(mask, nxt.n, nxt.b * BR, orow, H, lane);
       }
+      const int xr0 = nxt.n == cur.n ? 2 : 0;
+      const int ndy = orow >= 0 ? IPR : 0;
+      const int nx = (more && w8 >= 4) ? ((BR + 2 - xr0) * IPR - (w8 - 4) + 3) / 4 : 0;
+      const int npc = ndy + nx;
+      int ipc = 0;
+      auto piece = [&]() {
+        if (ipc < ndy) {
+          dma_row_instr<C, W>(dy, lds + L::DY + (buf ^ 1) * L::TILE + orow * L::ROWB, nxt.n, nxt.b * BR - 1 + orow,
+                              ipc, H, loff);
+        } else {
+          dma_row_instr<C, W>(x, lds + L::X + (buf ^ 1) * L::TILE + xr0 * L::ROWB, nxt.n, nxt.b * BR - 1 + xr0,
+                              (w8 - 4) + 4 * (ipc - ndy), H, loff);
+        }
+        ++ipc;
+      };
+      while (ipc < npc && ipc < ASR_BWD3_DMA0) piece();
       bf16x8 Bf[2], Ar[3];
       if (wave == 4) ASR_BTR(1, 1, it - i0, 2);
       // A fragments two m-tiles ahead (ring of 3), as k_bwd2
@@ -2419,6 +2454,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
               for (int oi = 0; oi < 2; ++oi)
                 accb[oi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, Bf[oi], accb[oi], 0, 0, 0);
             }
+            if (r < BR - 1 && ipc < npc) piece();
           }
         });
       };
@@ -2430,6 +2466,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
         for (int oi = 0; oi < 2; ++oi) offB[oi][0] += dlt, offB[oi][1] += dlt;
       }
       mfma_band(std::integral_constant<int, 0>{});
+      while (ipc < npc) piece();
       if (more) {
         vm_wait(0);  // own dy row and mask dwords of band it+1 (x DMA and fold loads too: long landed)
         convert_own(orow, buf ^ 1, mwv);
