@@ -215,8 +215,10 @@ def block_roofline(rt, lib, C, N, dtype_name, reps, h, integrator="euler"):
     stages = 2 if integrator == "rk2" else 1
     bytes_alg = (12 if stages == 2 else 5) * P * esz  # see the docstring
     flops = stages * 3 * 2 * 9 * C * C * N * H * W
+    # per pass: Euler fwd 2 (x, y), bwd 3 (dy, x, dx); RK2 fwd 5, bwd 7 (docstring)
+    fb, bb = (5, 7) if stages == 2 else (2, 3)
     return dict(t_fwd=tf, t_bwd_kernel=tbk, t_bwd=tb, t=t_blk, bytes=bytes_alg, flops=flops,
-                bytes_fwd=2 * P * esz, bytes_bwd=3 * P * esz, timing=timing_mode[0])
+                bytes_fwd=fb * P * esz, bytes_bwd=bb * P * esz, timing=timing_mode[0])
 
 
 def stack_roofline(rt, N, L, reps, h):
@@ -456,7 +458,7 @@ def main():
                 "kernels": {"fwd": {"avg_us": round(rb["t_fwd"] * 1e6, 2), "algorithmic_bytes": rb["bytes_fwd"],
                                     "frac": round(rb["bytes_fwd"] / rb["t_fwd"] / 1e9 / HBM_PEAK_GBS, 4)},
                             "bwd_with_reduction": {"avg_us": round(rb["t_bwd"] * 1e6, 2)}}}
-        if deep:
+        if deep or integrator == "rk2":
             roof["kernels"]["bwd_with_reduction"]["algorithmic_bytes"] = rb["bytes_bwd"]
             roof["kernels"]["bwd_with_reduction"]["frac"] = round(rb["bytes_bwd"] / rb["t_bwd"] / 1e9 / HBM_PEAK_GBS, 4)
         elif rb["t_bwd_kernel"] is not None:

@@ -864,10 +864,13 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
 // byte per lane (v_med3 + v_lshl_or, relu as an integer max on the bit
 // pattern).  MFMA accumulation order and rounding equal k_fwd_pipe's, so both
 // kernels give bitwise the same y and mask.
-template <int C, int W, int BR, int MODE, int WPE>
-__global__ __launch_bounds__(256, WPE) void k_fwd3(const bf16* __restrict__ x, bf16* __restrict__ y,
-                                                   uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
-                                                   const float* __restrict__ bias, float h, int N, int H) {
+// RESG (second RK2 stage): the residual is `resid` (the step input), not the
+// conv input x: 16-B global loads in the regrouped layout, issued before the conv.
+template <int C, int W, int BR, int MODE, int WPE, bool RESG = false>
+__global__ __launch_bounds__(256, WPE) void k_fwd3(const bf16* __restrict__ x, const bf16* __restrict__ resid,
+                                                   bf16* __restrict__ y, uint8_t* __restrict__ mask,
+                                                   const bf16* __restrict__ wpack, const float* __restrict__ bias,
+                                                   float h, int N, int H) {
   using G = Geo<C>;
   constexpr int TW = W + 2, NQ = G::NQ, OT = C / 16, NW = 4, RB = BR;
   static_assert(OT == NW && W == 32, "one 16-channel o-tile per wave, two pixel tiles");
@@ -929,6 +932,13 @@ __global__ __launch_bounds__(256, WPE) void k_fwd3(const bf16* __restrict__ x, b
       }
     }
     const unsigned tb = lds_u32(lds + buf * TILE);
+    u32x4 xr[RB];
+    if constexpr (RESG) {  // rows past the image end re-read its last row (never stored)
+      const int y0 = cur.b * BR, rows = min(BR, H - y0);
+      const unsigned char* rb = (const unsigned char*)(resid + ((long)cur.n * H + y0) * W * C) + ly;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) xr[r] = *(const u32x4*)(rb + (long)min(r, rows - 1) * W * C * 2);
+    }
     f32x4 acc[RB][2];
 #pragma unroll
     for (int r = 0; r < RB; ++r)
@@ -937,8 +947,7 @@ __global__ __launch_bounds__(256, WPE) void k_fwd3(const bf16* __restrict__ x, b
     if (wave == 0) ASR_BTR(0, 0, it - i0, 2);
     conv_band<C, W, RB>(tb, lo, A, acc);
     if (wave == 0) ASR_BTR(0, 0, it - i0, 3);
-    u32x4 xr[RB];
-    if constexpr (EULER) {
+    if constexpr (EULER && !RESG) {
 #pragma unroll
       for (int r = 0; r < RB; ++r) xr[r] = lds_rd128(tb + lxr + (unsigned)(r * BD::ROWB));
       lgkm_wait<0>();
@@ -2796,14 +2805,17 @@ static int launch_fwd_v(int mode, const void* x, const void* resid, void* y, uin
   const int grid = (int)std::max<long>(1, std::min<long>(items, (long)cus * (8 / NW)));
   const size_t lds = 2 * (size_t)(BR + 2) * (W + 2) * C * 2;
   if constexpr (C == 64 && W == 32 && BR == 4 && NW == 4) {
-    if (ASR_FWD3 && !resid) {
+    if (ASR_FWD3 && (!resid || mode == blk::FWD_EULER)) {
       const int grid3 = (int)std::max<long>(1, std::min<long>(items, (long)cus * 3));
-      if (mode == blk::FWD_EULER)
+      if (mode == blk::FWD_EULER && resid)
+        hipLaunchKernelGGL((blk::k_fwd3<C, W, BR, blk::FWD_EULER, 3, true>), dim3(grid3), dim3(256), lds, s,
+                           (const bf16*)x, (const bf16*)resid, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+      else if (mode == blk::FWD_EULER)
         hipLaunchKernelGGL((blk::k_fwd3<C, W, BR, blk::FWD_EULER, 3>), dim3(grid3), dim3(256), lds, s, (const bf16*)x,
-                           (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+                           nullptr, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
       else
         hipLaunchKernelGGL((blk::k_fwd3<C, W, BR, blk::FWD_CONV, 3>), dim3(grid3), dim3(256), lds, s, (const bf16*)x,
-                           (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
+                           nullptr, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
       ASR_LAUNCH_CHECK("k_fwd3");
       return ASR_OK;
     }
