@@ -37,6 +37,8 @@ ASR_INTEGRATOR_RK2 = 1
 ASR_VARIANT_NO_FOLD = 1
 ASR_VARIANT_STEM_FWD_VALU = 2
 ASR_VARIANT_STEM_WGRAD_VALU = 4
+ASR_VARIANT_PER_BLOCK_FWD = 8
+ASR_VARIANT_PER_BLOCK_BWD = 16
 ASR_DIST_UNIQUE_ID_BYTES = 128
 
 

@@ -46,6 +46,16 @@ bool stem_fwd_mfma_supported(int Cin, int H, int W, int C);
 static bool mfma_supported(int C, int W) { return (C == 16 || C == 32 || C == 64) && W == 32; }
 // asr_deep16.hip
 bool deep16_supported(int H, int W, int C);
+bool block_stack_fwd_supported(int N, int H, int W, int C);
+bool block_stack_bwd_supported(int N, int H, int W, int C);
+int block_stack_bwd_grid(int N);
+int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride, const uint8_t* masks,
+                         long mask_stride, const void* w, long w_stride, float h, float two_gamma, int N, int H, int W,
+                         int C, int L, int ro0, float* slabs, long slab_stride, float* grp, long grp_stride,
+                         unsigned* done, int* lfold_out, hipStream_t s);
+int block_stack_fwd_mfma(const void* x0, void* ys, long y_stride, uint8_t* masks, long mask_stride, const void* w,
+                         long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C, int L,
+                         hipStream_t s);
 int deep16_forward(const void* x0, void* y0, long y_stride, uint8_t* mask0, long mask_stride, const void* wpack,
                    const float* bias, long bias_stride, float h, int N, int L, bool store_all, hipStream_t s);
 size_t deep16_slab_bytes(int N, int L);
@@ -309,6 +319,9 @@ struct NetLayout {
   bool fast_stem;
   bool deep;          // C=16 stack path: one fused launch forward, one backward (asr_deep16.hip)
   size_t deep_slabs;  // its weight-gradient slabs [L][rows][E+C]
+  bool stack_bwd;     // C=64 Euler bf16: all blocks' backward in one k_bwd3_stack launch
+  int stack_grid;     // its workgroups
+  size_t theta_dst_tm, stack_slabs, stack_done;  // tile-major projection map, [L][grid][E+C] slabs, counters
 };
 
 static int net_check(const asr_net_config* c) {
@@ -322,7 +335,8 @@ static int net_check(const asr_net_config* c) {
     return fail(ASR_E_ARG, "the 3by3 parametrisation is always antisymmetric");
   if (c->integrator != ASR_INTEGRATOR_EULER && c->integrator != ASR_INTEGRATOR_RK2)
     return fail(ASR_E_ARG, "bad integrator %d", c->integrator);
-  if (c->variant & ~(ASR_VARIANT_NO_FOLD | ASR_VARIANT_STEM_FWD_VALU | ASR_VARIANT_STEM_WGRAD_VALU))
+  if (c->variant & ~(ASR_VARIANT_NO_FOLD | ASR_VARIANT_STEM_FWD_VALU | ASR_VARIANT_STEM_WGRAD_VALU | ASR_VARIANT_PER_BLOCK_FWD |
+                    ASR_VARIANT_PER_BLOCK_BWD))
     return fail(ASR_E_ARG, "bad variant bits 0x%x", c->variant);
   if (c->dtype == ASR_BF16 && !mfma_supported(c->C, c->W))
     return fail(ASR_E_UNSUPPORTED, "bf16 network needs C in {16,32,64} and W == 32 (C=%d W=%d)", c->C, c->W);
@@ -350,6 +364,8 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.mask_bytes = asr_mask_bytes(c->N, c->H, c->W, C);
   L.fast_stem = stem_supported(c->Cin, c->H, c->W, C);
   L.deep = c->dtype == ASR_BF16 && !L.rk2 && deep16_supported(c->H, c->W, C);
+  L.stack_bwd = c->dtype == ASR_BF16 && !L.rk2 && block_stack_bwd_supported(c->N, c->H, c->W, C);
+  L.stack_grid = L.stack_bwd ? block_stack_bwd_grid(c->N) : 0;
   size_t off = 0;
   auto take = [&](size_t bytes) {
     size_t o = off;
@@ -380,6 +396,9 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.grp_stride = (long)reduce_groups(L.stages * kMaxSlabsApi) * (L.E + C);
   L.grp = take((size_t)c->L * L.grp_stride * 4);
   L.deep_slabs = take(L.deep ? deep16_slab_bytes(c->N, c->L) : 0);
+  L.theta_dst_tm = take(L.stack_bwd ? (size_t)L.ntheta * 2 * 4 : 0);
+  L.stack_slabs = take(L.stack_bwd ? (size_t)c->L * L.stack_grid * (L.E + C) * 4 : 0);
+  L.stack_done = take(L.stack_bwd ? (size_t)(c->L + 4) * 4 : 0);
   L.probs = take((size_t)c->N * K * 4);
   L.loss_per = take((size_t)c->N * 4);
   L.dlogits = take((size_t)c->N * K * 4);
@@ -430,6 +449,11 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
     return deep16_forward(act(0), act(training ? 1 : c->L), L.P, training ? (uint8_t*)(ws + L.masks) : nullptr,
                           L.mask_bytes, ws + L.wbuf, params + L.off_blk + L.ntheta, L.blk_stride, c->h, N, c->L,
                           training, s);
+  }
+  if (bf && training && !L.rk2 && block_stack_fwd_supported(N, H, W, C) && !(c->variant & ASR_VARIANT_PER_BLOCK_FWD)) {
+    // C=64: all L blocks in one launch (whole images per workgroup)
+    return block_stack_fwd_mfma(act(0), act(1), (long)L.P, (uint8_t*)(ws + L.masks), (long)L.mask_bytes, ws + L.wbuf,
+                                (long)L.wstride, params + L.off_blk + L.ntheta, L.blk_stride, c->h, N, H, W, C, c->L, s);
   }
   for (int l = 0; l < c->L; ++l) {
     const float* bias = params + L.off_blk + (long)l * L.blk_stride + L.ntheta;
@@ -494,6 +518,9 @@ int asr_block_stack_forward(const void* x0, void* ys, long y_stride, uint8_t* ma
   if (dtype != ASR_F32 && dtype != ASR_BF16) return fail(ASR_E_ARG, "asr_block_stack_forward: bad dtype");
   const size_t es = dtype == ASR_BF16 ? 2 : 4;
   if (!store_all && L > 1) return fail(ASR_E_UNSUPPORTED, "asr_block_stack_forward: store_all=0 needs the fused path");
+  if (dtype == ASR_BF16 && block_stack_fwd_supported(N, H, W, C))
+    return block_stack_fwd_mfma(x0, ys, L > 1 ? y_stride : (long)N * H * W * C, masks, mask_stride, w, w_stride, bias,
+                                bias_stride, h, N, H, W, C, L, s);
   for (int l = 0; l < L; ++l) {
     const void* xi = l == 0 ? x0 : (const unsigned char*)ys + (size_t)(l - 1) * y_stride * es;
     void* yo = (unsigned char*)ys + (size_t)l * y_stride * es;
@@ -677,6 +704,17 @@ int asr_net_prepare(const asr_net_config* cfg, void* ws, size_t ws_bytes) {
   ASR_TRY(hip_check(hipMemcpy(b + L.w_src, w_src.data(), w_src.size() * 4, hipMemcpyHostToDevice), "hipMemcpy"));
   ASR_TRY(hip_check(hipMemcpy(b + L.theta_dst, theta_dst.data(), theta_dst.size() * 4, hipMemcpyHostToDevice),
                     "hipMemcpy"));
+  if (L.stack_bwd) {  // the same map into k_bwd3_stack's tile-major dW slabs
+    const int C = cfg->C;
+    std::vector<int32_t> tm(theta_dst);
+    for (auto& v : tm) {
+      if (v < 0) continue;
+      const long e = v >> 1, m = e / C, o = e % C;
+      const long et = (((m / 16) * (C / 16) + o / 16) * 64 + 16 * ((m % 16) / 4) + o % 16) * 4 + m % 4;
+      v = (int32_t)((et << 1) | (v & 1));
+    }
+    ASR_TRY(hip_check(hipMemcpy(b + L.theta_dst_tm, tm.data(), tm.size() * 4, hipMemcpyHostToDevice), "hipMemcpy"));
+  }
   return ASR_OK;
 }
 
@@ -738,7 +776,26 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
     ASR_TRY(project_layers((float*)(b + L.grp), (long)G * (L.E + C), G, L.E, C, theta_dst, L.ntheta, cfg->L,
                            grads + L.off_blk, L.blk_stride, s));
   }
-  for (int l = L.deep ? -1 : cfg->L - 1; l >= 0; --l) {
+  const bool stacked = L.stack_bwd && !(cfg->variant & ASR_VARIANT_PER_BLOCK_BWD);
+  if (stacked) {  // C=64: all L blocks in one launch, tile-major slabs
+    const int grid = L.stack_grid;
+    const long ES = L.E + C, sst = (long)grid * ES;
+    float* slabs = (float*)(b + L.stack_slabs);
+    float* grp = (float*)(b + L.grp);
+    const int ro0 = L.fast_stem && !stem_v1;
+    int lfold = cfg->L;
+    ASR_TRY(block_stack_bwd_mfma(dcur, dnext, act(0), L.P, (const uint8_t*)(b + L.masks), L.mask_bytes,
+                                 b + (L.sep_bwd ? L.wbuf_bwd : L.wbuf), L.wstride, cfg->h,
+                                 L.sep_bwd ? 0.f : 2.f * cfg->gamma, N, H, W, C, cfg->L, ro0, slabs, sst, grp,
+                                 L.grp_stride, (unsigned*)(b + L.stack_done), &lfold, s));
+    for (int l = std::min(lfold, cfg->L) - 1; l >= 0; --l)  // blocks below lfold: pass 1 after the launch
+      ASR_TRY(reduce_slabs_to_groups(slabs + (long)l * sst, grid, ES, grp + (long)l * L.grp_stride, s));
+    if (cfg->L & 1) std::swap(dcur, dnext);
+    dz1_fused = ro0;
+    ASR_TRY(project_layers(grp, L.grp_stride, reduce_groups(grid), L.E, C, (const int32_t*)(b + L.theta_dst_tm),
+                           L.ntheta, cfg->L, grads + L.off_blk, L.blk_stride, s));
+  }
+  for (int l = (L.deep || stacked) ? -1 : cfg->L - 1; l >= 0; --l) {
     const unsigned char* wl = b + (L.sep_bwd ? L.wbuf_bwd : L.wbuf) + (size_t)l * L.wstride * L.act_bytes;
     const uint8_t* mask = (const uint8_t*)(b + L.masks) + (size_t)l * L.mask_bytes;
     const float gam = L.sep_bwd ? 0.f : cfg->gamma;
@@ -769,7 +826,7 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   }
   if (pend_P > 0) ASR_TRY(reduce_slabs_to_groups(pend_slabs, pend_P, L.E + C, pend_grp, s));
   // pass 2 of every block's weight-gradient reduction + projection onto theta, one launch
-  if (!L.deep)
+  if (!L.deep && !stacked)
     ASR_TRY(project_layers((float*)(b + L.grp), L.grp_stride, reduce_groups(nsl_blk), L.E, C, theta_dst, L.ntheta,
                            cfg->L, grads + L.off_blk, L.blk_stride, s));
   // stem: dz1 = dx1 * [x1 > 0]; conv1 weight/bias gradient from the normalised input

@@ -65,6 +65,15 @@
 #ifndef ASR_FWD3
 #define ASR_FWD3 1  // C=64 forward (Euler without RK2 residual, plain conv): k_fwd3 at 3 WGs per CU (0: k_fwd_pipe)
 #endif
+#ifndef ASR_FWD3_WGS
+#define ASR_FWD3_WGS 3  // k_fwd3 workgroups per CU (grid = min(bands, WGS x CUs))
+#endif
+#ifndef ASR_FWD_STACK
+#define ASR_FWD_STACK 1  // C=64 network forward: all blocks in one k_fwd3_stack launch (0: one k_fwd3 per block)
+#endif
+#ifndef ASR_BWD_STACK
+#define ASR_BWD_STACK 1  // C=64 network backward: all blocks in one k_bwd3_stack launch (0: one k_bwd3 per block)
+#endif
 #ifndef ASR_BWD3
 #define ASR_BWD3 1  // C=64 backward: k_bwd3 (12 waves, 3 per SIMD; 0: k_bwd2, 8 waves)
 #endif
@@ -985,6 +994,144 @@ __global__ __launch_bounds__(256, WPE) void k_fwd3(const bf16* __restrict__ x, c
     if (wave == 0) ASR_BTR(0, 0, it - i0, 4);
   }
   ASR_BCLK(0, 1);
+}
+
+// ===========================================================================
+// Stack forward (C=64, W=32, BR=4, Euler): all L blocks of a network in ONE
+// launch.  The images do not interact (3x3 SAME conv per image, no batch
+// statistics), so a workgroup owns a contiguous run of whole images and walks
+// (layer, image, band) items: block l+1 of an image reads only what this
+// workgroup wrote for block l, and no workgroup ever waits for another.  The
+// per-band protocol is k_fwd3's (band conv + regrouped epilogue, next band's
+// rows by LDS-DMA into the other buffer, halo rows copied within an image).
+// Replaces L launches of k_fwd3: no per-launch fill and drain, and no tail of
+// workgroups with one band more than the rest (whole images per workgroup).
+// Ordering: the DMA of item it+1 is issued after the barrier of item it, when
+// every wave's stores of items <= it-1 have been waited for (barrier_vm counts
+// only the previous item's stores as still in flight), so the first band of
+// block l+1 (it reads rows -1..4 of block l's output, written by the first
+// two bands of the image) needs >= 4 bands per workgroup and block: the host
+// checks nb >= 4.  Activations are distinct buffers per block, written once
+// in this launch, so no L1 line of them can be stale.
+// ===========================================================================
+template <int C, int W, int BR>
+__global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ x0, bf16* __restrict__ ys,
+                                                       long y_stride, uint8_t* __restrict__ masks, long mask_stride,
+                                                       const bf16* __restrict__ wpack, long w_stride,
+                                                       const float* __restrict__ bias, long bias_stride, float h,
+                                                       int N, int H, int L) {
+  using G = Geo<C>;
+  constexpr int TW = W + 2, NQ = G::NQ, OT = C / 16, NW = 4, RB = BR;
+  static_assert(OT == NW && W == 32, "one 16-channel o-tile per wave, two pixel tiles");
+  using BD = Band<C, W, RB>;
+  constexpr int TILE = (BR + 2) * BD::ROWB;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ot = wave, g = lane >> 4, lx = lane & 15;
+  const int o0 = 16 * ot + 4 * g;
+  const int px = lx + 16 * (g & 1), cg = 2 * ot + (g >> 1);
+
+  // whole images per workgroup
+  const int n0 = (int)((long)blockIdx.x * N / gridDim.x), n1 = (int)((long)(blockIdx.x + 1) * N / gridDim.x);
+  if (n0 >= n1) return;
+  const int nb = (H + BR - 1) / BR, per = (n1 - n0) * nb;  // items per block
+  auto src_of = [&](int l) -> const bf16* { return l == 0 ? x0 : ys + (long)(l - 1) * y_stride; };
+
+  bf16x8 A[G::KS];
+  load_A1<C>(wpack, ot, lane, A);
+  unsigned lo[3 * BD::NCB];
+  band_lane_offsets<C, W, RB>(g, lx, lo);
+  float bz[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) bz[e] = bias ? bias[o0 + e] : 0.f;
+  const unsigned lxr = (unsigned)toff<C>(1, px + 1, cg, TW);
+  const unsigned ly = (unsigned)(px * C + 8 * cg) * 2u, lm = (unsigned)(px * (C / 8) + cg);
+
+  zero_halo_cols<C, W>(lds, BR + 2, tid, 64 * NW);
+  zero_halo_cols<C, W>(lds + TILE, BR + 2, tid, 64 * NW);
+  // cursor over (block l, image n, band b)
+  int cl = 0, cn = n0, cb = 0;
+  int xl = 0, xn = n0, xb = 0;  // next item
+  auto adv = [&](int& l, int& n, int& b) {
+    if (++b == nb) {
+      b = 0;
+      if (++n == n1) {
+        n = n0;
+        ++l;
+      }
+    }
+  };
+  adv(xl, xn, xb);
+  dma_rows<C, W>(x0, lds, cn, -1, min(BR, H) + 2, H, wave, NW, lane);
+  int nst = 0;
+  const int total = L * per;
+  for (int it = 0; it < total; ++it) {
+    const int buf = it & 1;
+    barrier_vm(nst);  // band it landed; every wave is done with band it-1's tile
+    nst = 0;
+    if (it + 1 < total) {
+      unsigned char* nt = lds + (buf ^ 1) * TILE;
+      const int yy = xb * BR;
+      const bf16* xs = src_of(xl);
+      if (xl == cl && xn == cn && xb == cb + 1) {
+        dma_rows<C, W>(xs, nt + 2 * BD::ROWB, xn, yy + 1, min(BR, H - yy), H, wave, NW, lane);
+        const uint4* src = (const uint4*)(lds + buf * TILE + BR * BD::ROWB);
+        uint4* dst = (uint4*)nt;
+        constexpr int NCH = 2 * W * NQ;
+        for (int i = tid; i < NCH; i += 64 * NW) {
+          const int o = ((i / (W * NQ)) * TW + 1) * NQ + i % (W * NQ);
+          dst[o] = src[o];
+        }
+      } else {
+        dma_rows<C, W>(xs, nt, xn, yy - 1, min(BR, H - yy) + 2, H, wave, NW, lane);
+      }
+    }
+    const unsigned tb = lds_u32(lds + buf * TILE);
+    f32x4 acc[RB][2];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt) acc[r][pt] = f32x4{bz[0], bz[1], bz[2], bz[3]};
+    conv_band<C, W, RB>(tb, lo, A, acc);
+    u32x4 xr[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) xr[r] = lds_rd128(tb + lxr + (unsigned)(r * BD::ROWB));
+    const int l = cl;
+    if (xl != cl && it + 1 < total) {  // the next item starts block l+1: its W and bias (L2 hits)
+      load_A1<C>(wpack + (long)xl * w_stride, ot, lane, A);
+      const float* bl = bias ? bias + (long)xl * bias_stride : nullptr;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bz[e] = bl ? bl[o0 + e] : 0.f;
+    }
+    lgkm_wait<0>();
+    const int y0 = cb * BR, rows = min(BR, H - y0);
+    const long rowb = ((long)cn * H + y0) * W;
+    unsigned char* yb = (unsigned char*)(ys + (long)l * y_stride + rowb * C) + ly;
+    uint8_t* mb = masks ? masks + (long)l * mask_stride + rowb * (C / 8) + lm : nullptr;
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      if (r >= rows) break;
+      float z[8];
+      regroup(acc[r][0], acc[r][1], z);
+      u32x4 yw;
+      unsigned bits = 0;
+      static_for<0, 4>([&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        const int ra = max(__float_as_int(z[2 * d]), 0), rb = max(__float_as_int(z[2 * d + 1]), 0);
+        yw[d] = pk_bf16(fmaf(h, __int_as_float(ra), lo_f(xr[r][d])), fmaf(h, __int_as_float(rb), hi_f(xr[r][d])));
+        bits = d == 0 ? bit01(ra) : lshl_or<2 * d>(bit01(ra), bits);
+        bits = lshl_or<2 * d + 1>(bit01(rb), bits);
+      });
+      if (mb) {
+        mb[r * W * (C / 8)] = (uint8_t)bits;
+        ++nst;
+      }
+      *(u32x4*)(yb + r * W * C * 2) = yw;
+      ++nst;
+    }
+    cl = xl, cn = xn, cb = xb;
+    adv(xl, xn, xb);
+  }
 }
 
 // ===========================================================================
@@ -2565,6 +2712,443 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
 }
 
 // ===========================================================================
+// Stack backward (C=64, W=32, BR=4, Euler): the backward of all L blocks in
+// ONE launch, k_bwd3's band protocol and roles on (block, image, band) items,
+// blocks last to first.  A workgroup owns whole images (as k_fwd3_stack), so
+// block l-1 of an image reads only the dx this workgroup wrote for block l
+// (ping-pong buffers dbuf[0/1]: block L-1 reads dbuf[0]); the only exchange
+// between workgroups is the weight-gradient reduction:
+//   * at the end of its items of block l, every wgrad wave stores its dW
+//     tiles as sc1 (write-through) 16-B stores in the tile-major slab layout
+//       slab[((mt * 4 + ot) * 64 + lane) * 4 + e] = dW[16 mt + 4 (lane>>4) + e][16 ot + (lane&15)]
+//     (db after the 9C^2 block); the next band barrier drains them (vmcnt(0))
+//     and one lane adds 1 to done[l] (relaxed, agent scope: the Guideline-16
+//     write-through publish);
+//   * pass 1 of block l's reduction (32-slab group sums, as k_bwd3's fold) is
+//     folded into this workgroup's bands of block l-2: one lane polls done[l]
+//     == gridDim.x before the first of them (bounded; a timeout sets *tmo) and
+//     fences acquire at agent scope, and the band barrier orders that before
+//     every slab load.  Blocks below lfold (>= 2; L when a workgroup would
+//     own more than 512 chunks of the group rows, one per wgrad thread) are
+//     reduced after the launch.
+// The grid must be co-resident (one 768-thread workgroup per CU, grid <= CUs):
+// the host sizes it so.  At the switch to block l-1 the dgrad waves load its W
+// after their last conv of block l; block 0 applies the stem's relu' to dx
+// when ro0 (k_bwd3<..., RO>).
+// ===========================================================================
+typedef __attribute__((address_space(1))) unsigned gu32;  // global agent-scope words (never flat)
+typedef __attribute__((address_space(1))) float gf32;
+
+template <int C, int W, int BR>
+__global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0, bf16* __restrict__ dbuf1,
+                                                       const bf16* __restrict__ xs, long x_stride,
+                                                       const uint8_t* __restrict__ masks, long mask_stride,
+                                                       const bf16* __restrict__ wpack, long w_stride, float h,
+                                                       float two_gamma, int N, int H, int L, int ro0,
+                                                       float* __restrict__ slabs, long slab_stride,
+                                                       float* __restrict__ grp, long grp_stride,
+                                                       unsigned* __restrict__ done, unsigned* __restrict__ tmo,
+                                                       int lfold) {
+  using G = Geo<C>;
+  using LL = Bwd2Lds<C, W, BR>;
+  using BD = Band<C, W, BR>;
+  constexpr int TW = W + 2, OT = G::OT, MTW = G::MTW, IPR = W / G::PPI, NQ = G::NQ;
+  static_assert(C == 64 && W == 32 && BR == 4 && MTW == 9 && OT == 4, "v3 backward geometry");
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, lx = lane & 15;
+
+  for (int b = 0; b < 2; ++b) {
+    zero_halo_cols<C, W>(lds + LL::DY + b * LL::TILE, BR + 2, tid, 768);
+    zero_halo_cols<C, W>(lds + LL::X + b * LL::TILE, BR + 2, tid, 768);
+    zero_halo_cols<C, W>(lds + LL::DZ + b * LL::TILE, BR + 2, tid, 768);
+  }
+  if (ASR_V2_MASKTAB) {
+    unsigned* tab = (unsigned*)(lds + LL::MTAB);
+    for (int i = tid; i < 1024; i += 768) {
+      const unsigned m = (unsigned)i >> 2, d = (unsigned)i & 3;
+      tab[i] = (((m >> (2 * d)) & 1u) ? 0xffffu : 0u) | (((m >> (2 * d + 1)) & 1u) ? 0xffff0000u : 0u);
+    }
+  }
+  const int n0 = (int)((long)blockIdx.x * N / gridDim.x), n1 = (int)((long)(blockIdx.x + 1) * N / gridDim.x);
+  const int nb = (H + BR - 1) / BR, per = (n1 - n0) * nb, total = L * per;
+  const unsigned loff = (unsigned)dma_lane_off<C, W>(lane) * 2u;
+  const float hs = h, hs2g = h * two_gamma;
+  // block l reads dy from dbuf[(L-1-l) & 1] and writes dx to the other one
+  auto dy_of = [&](int l) -> bf16* { return ((L - 1 - l) & 1) ? dbuf1 : dbuf0; };
+  auto dx_of = [&](int l) -> bf16* { return ((L - 1 - l) & 1) ? dbuf0 : dbuf1; };
+  auto x_of = [&](int l) -> const bf16* { return xs + (long)l * x_stride; };
+  auto mask_of = [&](int l) -> const uint8_t* { return masks + (long)l * mask_stride; };
+  // (block, image, band) cursor, blocks last to first
+  struct Cur {
+    int l, n, b;
+  };
+  auto adv = [&](Cur& c) {
+    if (++c.b == nb) {
+      c.b = 0;
+      if (++c.n == n1) {
+        c.n = n0;
+        --c.l;
+      }
+    }
+  };
+  __syncthreads();
+  if (n0 >= n1) return;  // (uniform per workgroup: never with grid <= N)
+
+  constexpr int ES = 9 * C * C + C, ECH = ES / 4;
+  if (wave < 4) {
+    // ---------------- dgrad waves ----------------
+    const int ot = wave;
+    bf16x8 A[G::KS];
+    load_A1<C>(wpack + (long)(L - 1) * w_stride, ot, lane, A);
+    unsigned lo[3 * BD::NCB];
+    band_lane_offsets<C, W, BR>(g, lx, lo);
+    const int px = lx + 16 * (g & 1), cg = 2 * ot + (g >> 1);
+    const unsigned lch = (unsigned)toff<C>(1, px + 1, cg, TW);
+    const unsigned ldx = (unsigned)(px * C + 8 * cg) * 2u;
+    int nst = 0;
+    Cur cur{L - 1, n0, 0};
+    for (int it = 0; it < total; ++it) {
+      const int buf = it & 1;
+      const int n = cur.n, y0 = cur.b * BR, l = cur.l;
+      const int rows = min(BR, H - y0);
+      barrier_vm(nst);  // item it staged everywhere; item it-1 fully consumed
+      const unsigned dzt = lds_u32(lds + LL::DZ + buf * LL::TILE), dyt = lds_u32(lds + LL::DY + buf * LL::TILE);
+      const unsigned xt = lds_u32(lds + LL::X + buf * LL::TILE);
+      f32x4 acc[BR][2];
+#pragma unroll
+      for (int r = 0; r < BR; ++r) acc[r][0] = acc[r][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      conv_band<C, W, BR>(dzt, lo, A, acc);
+      const bool last_of_block = cur.b == nb - 1 && n == n1 - 1;
+      if (last_of_block && l > 0) load_A1<C>(wpack + (long)(l - 1) * w_stride, ot, lane, A);
+      bf16* drow = dx_of(l) + ((long)n * H + y0) * W * C;
+      int nld = 0;
+      auto epilogue = [&](auto g2c, auto roc) {
+        constexpr bool G2 = decltype(g2c)::value, RO = decltype(roc)::value;
+        constexpr int NR = 1 + (G2 ? 1 : 0) + (RO ? 1 : 0);  // LDS reads per row
+        u32x4 dyw[2], dzw[2], xw[2];
+        auto issue = [&](int r, int sl) {
+          const unsigned co = lch + (unsigned)(r * LL::ROWB);
+          dyw[sl] = lds_rd128(dyt + co);
+          if constexpr (G2) dzw[sl] = lds_rd128(dzt + co);
+          if constexpr (RO) xw[sl] = lds_rd128(xt + co);
+        };
+        issue(0, 0);
+        static_for<0, BR>([&](auto rc) {
+          constexpr int r = decltype(rc)::value, sl = r & 1;
+          if (r < rows) {
+            if (r + 1 < rows) {
+              issue(r + 1, sl ^ 1);
+              lgkm_wait<NR>();
+            } else {
+              lgkm_wait<0>();
+            }
+            float z[8];
+            regroup(acc[r][0], acc[r][1], z);
+            u32x4 ow;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+              float v0 = fmaf(-hs, z[2 * d], lo_f(dyw[sl][d]));
+              float v1 = fmaf(-hs, z[2 * d + 1], hi_f(dyw[sl][d]));
+              if constexpr (G2) {
+                v0 = fmaf(hs2g, lo_f(dzw[sl][d]), v0);
+                v1 = fmaf(hs2g, hi_f(dzw[sl][d]), v1);
+              }
+              ow[d] = pk_bf16(v0, v1);
+              if constexpr (RO) {
+                const unsigned xd = xw[sl][d];
+                ow[d] &= ((int)(short)(xd & 0xffffu) > 0 ? 0xffffu : 0u) | ((int)xd > 0xffff ? 0xffff0000u : 0u);
+              }
+            }
+            *(u32x4*)((unsigned char*)(drow + (long)r * W * C) + ldx) = ow;
+            ++nld;
+          }
+        });
+      };
+      using T_ = std::true_type;
+      using F_ = std::false_type;
+      const bool g2 = hs2g != 0.f, ro = ro0 && l == 0;
+      if (ro) {
+        if (g2) epilogue(T_{}, T_{});
+        else epilogue(F_{}, T_{});
+      } else {
+        if (g2) epilogue(T_{}, F_{});
+        else epilogue(F_{}, F_{});
+      }
+      nst = nld;
+      adv(cur);
+    }
+    barrier_vm(0);  // matches the wgrad waves' end-of-loop barrier
+  } else {
+    // ---------------- wgrad waves ----------------
+    const int w8 = __builtin_amdgcn_readfirstlane(wave) - 4;
+    const int tg = w8 >> 1, oq = 2 * (w8 & 1);
+    const int tq = lx >> 2, tp = lx & 3;
+    const int ft = tid - 256;
+    f32x4 acc[MTW][2];
+#pragma unroll
+    for (int mi = 0; mi < MTW; ++mi) acc[mi][0] = acc[mi][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    unsigned offA[MTW][2], offB[2][2];
+    {
+      const unsigned xb0 = lds_u32(lds + LL::X), zb0 = lds_u32(lds + LL::DZ);
+      const int pb = 4 * g + tq;
+#pragma unroll
+      for (int mi = 0; mi < MTW; ++mi) {
+        const int mt = tg * MTW + mi;
+        const int tap = (16 * mt) / C, itile = ((16 * mt) % C) / 16;
+        const int ky = tap / 3, kx = tap % 3, q = 2 * itile + (tp >> 1);
+        offA[mi][0] = xb0 + (unsigned)(toff<C>(ky, pb + kx, q, TW) + 8 * (tp & 1));
+        offA[mi][1] = xb0 + (unsigned)(toff<C>(ky, pb + 16 + kx, q, TW) + 8 * (tp & 1));
+      }
+#pragma unroll
+      for (int oi = 0; oi < 2; ++oi) {
+        const int q = 2 * (oq + oi) + (tp >> 1);
+        offB[oi][0] = zb0 + (unsigned)(toff<C>(1, pb + 1, q, TW) + 8 * (tp & 1));
+        offB[oi][1] = zb0 + (unsigned)(toff<C>(1, pb + 17, q, TW) + 8 * (tp & 1));
+      }
+#pragma unroll
+      for (int mi = 0; mi < MTW; ++mi) asm volatile("" : "+v"(offA[mi][0]), "+v"(offA[mi][1]));
+      asm volatile("" : "+v"(offB[0][0]), "+v"(offB[0][1]), "+v"(offB[1][0]), "+v"(offB[1][1]));
+    }
+    auto own_row = [&](bool reuse) { return reuse ? (w8 < 4 ? 2 + w8 : -1) : (w8 < 6 ? w8 : -1); };
+    auto stage_own = [&](const Cur& c, int row, int nbuf, unsigned& mwv) {
+      if (row < 0) return;
+      mwv = bwd2_mask_word<C, W>(mask_of(c.l), c.n, c.b * BR, row, H, lane);
+      for (int j = 0; j < IPR; ++j)
+        dma_row_instr<C, W>(dy_of(c.l), lds + LL::DY + nbuf * LL::TILE + row * LL::ROWB, c.n, c.b * BR - 1 + row, j,
+                            H, loff);
+    };
+    auto convert_own = [&](int row, int nbuf, unsigned mwv) {
+      if (row < 0) return;
+      const unsigned base = lds_u32(lds);
+      const int cpx = lane & 31, hh = lane >> 5;
+#pragma unroll
+      for (int jj = 0; jj < 4; jj += 2) {
+        u32x4 v[2], mt[2];
+        unsigned off[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          off[j] = (unsigned)toff<C>(row, cpx + 1, 4 * hh + jj + j, TW) + (unsigned)(nbuf * LL::TILE);
+          v[j] = lds_ld128(base + LL::DY + off[j]);
+          if (ASR_V2_MASKTAB) mt[j] = lds_ld128(base + LL::MTAB + __builtin_amdgcn_ubfe(mwv, 8 * (jj + j), 8) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          u32x4 z = v[j];
+          if constexpr (ASR_V2_MASKTAB) {
+            z &= mt[j];
+          } else {
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+              const unsigned lo = (unsigned)__builtin_amdgcn_sbfe((int)mwv, 8 * (jj + j) + 2 * d, 1);
+              const unsigned hi = (unsigned)__builtin_amdgcn_sbfe((int)mwv, 8 * (jj + j) + 2 * d + 1, 1);
+              z[d] &= __builtin_amdgcn_perm(hi, lo, 0x07060100u);
+            }
+          }
+          lds_st128(base + LL::DZ + off[j], z);
+        }
+      }
+    };
+    bf16x8 ones;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
+    f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    const bool dbw = tg == 3;
+    // fold state (pass 1 of block l+2's reduction while on block l)
+    const long fT = (long)((gridDim.x + 31) / 32) * ECH;
+    const long fc0 = (long)blockIdx.x * fT / gridDim.x, fc1 = (long)(blockIdx.x + 1) * fT / gridDim.x;
+    const bool fmine = ft >= 0 && fc0 + ft < fc1;
+    const int fg = fmine ? (int)((fc0 + ft) / ECH) : 0;
+    const int fpe = min((int)gridDim.x, 32 * fg + 32);
+    const unsigned fch = fmine ? (unsigned)((fc0 + ft) % ECH) * 4 : 0u;
+    bool fold = false;
+    int fp = 0;
+    unsigned foff = 0u;
+    const float* pslabs = slabs;
+    f32x4 facc = {0.f, 0.f, 0.f, 0.f}, fv[2];
+    auto fold_begin = [&](int l) {  // block l's slabs (published: done[l] == grid, acquired)
+      fold = fmine;
+      fp = 32 * fg;
+      foff = (unsigned)fp * ES + fch;
+      pslabs = slabs + (long)l * slab_stride;
+      facc = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    auto fold_end = [&](int l) {
+      if (fold) {
+        for (; fp < fpe; ++fp, foff += ES) facc += *(const f32x4*)(pslabs + foff);
+        *(f32x4*)(grp + (long)l * grp_stride + (long)fg * ES + fch) = facc;
+      }
+      fold = false;
+    };
+    {  // prologue: own dy rows and x rows of item 0, its dz converted
+      const Cur c0{L - 1, n0, 0};
+      unsigned mw0 = 0u;
+      const int row0 = own_row(false);
+      stage_own(c0, row0, 0, mw0);
+      for (int j = w8; j < (BR + 2) * IPR; j += 8)
+        dma_row_instr<C, W>(x_of(c0.l), lds + LL::X, c0.n, c0.b * BR - 1, j, H, loff);
+      vm_wait(0);
+      convert_own(row0, 0, mw0);
+    }
+    Cur cur{L - 1, n0, 0}, nxt{L - 1, n0, 0};
+    adv(nxt);
+    for (int it = 0; it < total; ++it) {
+      const int buf = it & 1;
+      const int y0 = cur.b * BR, l = cur.l;
+      const int rows = min(BR, H - y0);
+      const bool first_of_block = cur.b == 0 && cur.n == n0;
+      if (first_of_block && l + 2 < L && l + 2 >= lfold && w8 == 0 && lane == 0) {
+        // block l+2's slabs: every workgroup published them (bounded poll)
+        unsigned spins = 0;
+        while (__hip_atomic_load((gu32*)(done + l + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > (1u << 24)) {
+            __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+      barrier_vm(0);  // this wave's x rows of item it landed (and its slab stores drained)
+      if (first_of_block && l + 1 < L && l + 1 >= lfold && w8 == 0 && lane == 0)
+        __hip_atomic_fetch_add((gu32*)(done + l + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // published
+      if (first_of_block && l + 2 < L && l + 2 >= lfold) fold_begin(l + 2);
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if (fold && fp + q < fpe) fv[q] = *(const f32x4*)(pslabs + foff + (unsigned)q * ES);
+      const bool more = it + 1 < total;
+      const bool cont = more && nxt.l == cur.l && nxt.n == cur.n;
+      const int orow = more ? own_row(cont) : -1;
+      unsigned mwv = 0u;
+      if (orow >= 0) mwv = bwd2_mask_word<C, W>(mask_of(nxt.l), nxt.n, nxt.b * BR, orow, H, lane);
+      const int xr0 = cont ? 2 : 0;
+      const int ndy = orow >= 0 ? IPR : 0;
+      const int nx = (more && w8 >= 4) ? ((BR + 2 - xr0) * IPR - (w8 - 4) + 3) / 4 : 0;
+      const int npc = ndy + nx;
+      int ipc = 0;
+      const bf16* nxdy = dy_of(nxt.l);
+      const bf16* nxx = x_of(nxt.l);
+      auto piece = [&]() {
+        if (ipc < ndy) {
+          dma_row_instr<C, W>(nxdy, lds + LL::DY + (buf ^ 1) * LL::TILE + orow * LL::ROWB, nxt.n,
+                              nxt.b * BR - 1 + orow, ipc, H, loff);
+        } else {
+          dma_row_instr<C, W>(nxx, lds + LL::X + (buf ^ 1) * LL::TILE + xr0 * LL::ROWB, nxt.n, nxt.b * BR - 1 + xr0,
+                              (w8 - 4) + 4 * (ipc - ndy), H, loff);
+        }
+        ++ipc;
+      };
+      while (ipc < npc && ipc < ASR_BWD3_DMA0) piece();
+      bf16x8 Bf[2], Ar[3];
+      auto mfma_band = [&](auto bo) {
+        constexpr int BO = decltype(bo)::value;
+        Ar[0] = tr_pair_at<BO>(offA[0][0], offA[0][1]);
+        static_for<0, BR>([&](auto rc) {
+          constexpr int r = decltype(rc)::value, RO_ = BO + r * LL::ROWB;
+          __builtin_amdgcn_sched_barrier(0);
+          if (r < rows) {
+            const bool mr = r + 1 < rows;
+#pragma unroll
+            for (int oi = 0; oi < 2; ++oi) Bf[oi] = tr_pair_at<RO_>(offB[oi][0], offB[oi][1]);
+            Ar[1] = tr_pair_at<RO_>(offA[1][0], offA[1][1]);
+            static_for<0, MTW>([&](auto mc) {
+              constexpr int mi = decltype(mc)::value;
+              if constexpr (mi + 2 < MTW) Ar[(mi + 2) % 3] = tr_pair_at<RO_>(offA[mi + 2][0], offA[mi + 2][1]);
+              else if constexpr (mi + 2 == MTW && r + 1 < BR) {
+                if (mr) Ar[0] = tr_pair_at<RO_ + LL::ROWB>(offA[0][0], offA[0][1]);
+              }
+#pragma unroll
+              for (int oi = 0; oi < 2; ++oi)
+                acc[mi][oi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ar[mi % 3], Bf[oi], acc[mi][oi], 0, 0, 0);
+            });
+            if (dbw) {
+#pragma unroll
+              for (int oi = 0; oi < 2; ++oi)
+                accb[oi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, Bf[oi], accb[oi], 0, 0, 0);
+            }
+            if (r < BR - 1 && ipc < npc) piece();
+          }
+        });
+      };
+      if (it > 0) {
+        const unsigned dlt = buf ? (unsigned)LL::TILE : (unsigned)-LL::TILE;
+#pragma unroll
+        for (int mi = 0; mi < MTW; ++mi) offA[mi][0] += dlt, offA[mi][1] += dlt;
+#pragma unroll
+        for (int oi = 0; oi < 2; ++oi) offB[oi][0] += dlt, offB[oi][1] += dlt;
+      }
+      mfma_band(std::integral_constant<int, 0>{});
+      while (ipc < npc) piece();
+      if (more) {
+        vm_wait(0);
+        convert_own(orow, buf ^ 1, mwv);
+      }
+      if (cont) {  // halo rows of the next band of this image
+        const unsigned base = lds_u32(lds);
+        const int nbf = buf ^ 1;
+        u32x4 cv[3];
+        unsigned dst[3];
+        int nc = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int c = ft + 512 * k;
+          if (c < 5 * 256) {
+            const int which = c >> 8;
+            const unsigned o = (unsigned)((c & 255) + NQ) * 16u;
+            const unsigned sreg = which < 2 ? LL::DZ : which < 4 ? LL::X : LL::DY;
+            const int srow = which == 4 ? BR + 1 : BR + (which & 1);
+            const int drow = which == 4 ? 1 : (which & 1);
+            cv[k] = lds_rd128(base + sreg + buf * LL::TILE + srow * LL::ROWB + o);
+            dst[k] = base + sreg + nbf * LL::TILE + drow * LL::ROWB + o;
+            nc = k + 1;
+          }
+        }
+        lgkm_wait<0>();
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          if (k < nc) lds_wr128(dst[k], cv[k]);
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if (fold && fp < fpe) {
+          facc += fv[q];
+          ++fp;
+          foff += ES;
+        }
+      const bool last_of_block = cur.b == nb - 1 && cur.n == n1 - 1;
+      if (last_of_block) {
+        if (l + 2 < L && l + 2 >= lfold) fold_end(l + 2);
+        // publish block l's dW tiles and db (write-through; drained at the next band barrier)
+        float* slab = slabs + (long)l * slab_stride + (long)blockIdx.x * ES;
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, ES * 4, 0x00020000);
+#pragma unroll
+        for (int mi = 0; mi < MTW; ++mi)
+#pragma unroll
+          for (int oi = 0; oi < 2; ++oi) {
+            const int mt = tg * MTW + mi;
+            f32x4 v = acc[mi][oi] * hs;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs,
+                                                   (((mt * 4 + oq + oi) * 64 + lane) * 4) * 4, 0, 16);
+            acc[mi][oi] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        if (dbw) {
+          if (g == 0) {
+#pragma unroll
+            for (int oi = 0; oi < 2; ++oi)
+              __hip_atomic_store((gf32*)(slab + 9 * C * C + 16 * (oq + oi) + lx), hs * accb[oi][0], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+          }
+          accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      cur = nxt;
+      adv(nxt);
+    }
+    barrier_vm(0);
+  }
+}
+
+// ===========================================================================
 // Stem weight gradient on MFMA (C = 16 or 64, CIN=3, W=32, H % 8 == 0), from dz1 =
 // dx1 * [x1 > 0] (written by the first block's backward, k_bwd2<..., RO>):
 //   dW1[kappa][o] = inv_std * sum_p (img[p + tap] - mean)[ci] * dz1[p][o]
@@ -2777,6 +3361,7 @@ __global__ __launch_bounds__(256) void k_stem_fwd_mfma(const Tin* __restrict__ i
 // host launchers
 // ---------------------------------------------------------------------------
 constexpr int kBwdBR = 4;
+constexpr int kFwdBR = 4;  // k_fwd3 / k_fwd3_stack row band
 constexpr int kMaxBlockSlabs = 512;
 
 #if ASR_BLK_TRACE
@@ -2806,7 +3391,7 @@ static int launch_fwd_v(int mode, const void* x, const void* resid, void* y, uin
   const size_t lds = 2 * (size_t)(BR + 2) * (W + 2) * C * 2;
   if constexpr (C == 64 && W == 32 && BR == 4 && NW == 4) {
     if (ASR_FWD3 && (!resid || mode == blk::FWD_EULER)) {
-      const int grid3 = (int)std::max<long>(1, std::min<long>(items, (long)cus * 3));
+      const int grid3 = (int)std::max<long>(1, std::min<long>(items, (long)cus * ASR_FWD3_WGS));
       if (mode == blk::FWD_EULER && resid)
         hipLaunchKernelGGL((blk::k_fwd3<C, W, BR, blk::FWD_EULER, 3, true>), dim3(grid3), dim3(256), lds, s,
                            (const bf16*)x, (const bf16*)resid, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);
@@ -3001,6 +3586,66 @@ int block_fwd_mfma(int mode, const void* x, const void* resid, void* y, uint8_t*
     case 64: return launch_fwd<64, 32>(mode, x, resid, y, mask, w, bias, h, N, H, s);
   }
   return fail(ASR_E_UNSUPPORTED, "bf16 block: C=%d not supported (16, 32, 64)", C);
+}
+
+bool block_stack_fwd_supported(int N, int H, int W, int C) {
+  return ASR_FWD_STACK && C == 64 && W == 32 && N >= 1 && (H + kFwdBR - 1) / kFwdBR >= 4;
+}
+
+// all L Euler blocks in one launch (k_fwd3_stack); x_l of block l >= 1 is
+// ys + (l-1)*y_stride, its output ys + l*y_stride (elements)
+int block_stack_fwd_mfma(const void* x0, void* ys, long y_stride, uint8_t* masks, long mask_stride, const void* w,
+                         long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C, int L,
+                         hipStream_t s) {
+  if (!block_stack_fwd_supported(N, H, W, C) || L < 1)
+    return fail(ASR_E_UNSUPPORTED, "stack forward: needs C=64, W=32, >= 4 row bands per image (C=%d W=%d H=%d)", C, W, H);
+  if (y_stride < (long)N * H * W * C) return fail(ASR_E_ARG, "stack forward: y_stride smaller than one activation");
+  int cus = cu_count();
+  if (cus <= 0) cus = 256;
+  const int grid = std::max(1, std::min(N, 2 * cus));
+  const size_t lds = 2 * (size_t)(kFwdBR + 2) * (W + 2) * C * 2;
+  hipLaunchKernelGGL((blk::k_fwd3_stack<64, 32, kFwdBR>), dim3(grid), dim3(256), lds, s, (const bf16*)x0, (bf16*)ys,
+                     y_stride, masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, H, L);
+  ASR_LAUNCH_CHECK("k_fwd3_stack");
+  return ASR_OK;
+}
+
+bool block_stack_bwd_supported(int N, int H, int W, int C) {
+  return ASR_BWD_STACK && C == 64 && W == 32 && N >= 1 && (H + kBwdBR - 1) / kBwdBR >= 4;
+}
+
+// workgroups of k_bwd3_stack: one per CU at most (the in-launch slab
+// hand-off needs every workgroup resident), whole images each
+int block_stack_bwd_grid(int N) {
+  int cus = cu_count();
+  if (cus <= 0) cus = 256;
+  return std::max(1, std::min(N, std::min(cus, kMaxBlockSlabs)));
+}
+
+// the backward of L Euler blocks in one launch (k_bwd3_stack).  dbuf0 holds
+// dL/dx_L on entry; block 0's dx ends in dbuf[L & 1].  Block l's slabs (grid
+// of them, tile-major dW) at slabs + l*slab_stride; blocks >= 2 leave as
+// 32-slab group sums at grp + l*grp_stride, blocks 1 and 0 as slabs.  done:
+// L + 4 zeroed words (counters + timeout flag), reset here.
+int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride, const uint8_t* masks,
+                         long mask_stride, const void* w, long w_stride, float h, float two_gamma, int N, int H, int W,
+                         int C, int L, int ro0, float* slabs, long slab_stride, float* grp, long grp_stride,
+                         unsigned* done, int* lfold_out, hipStream_t s) {
+  if (!block_stack_bwd_supported(N, H, W, C) || L < 1)
+    return fail(ASR_E_UNSUPPORTED, "stack backward: needs C=64, W=32, >= 4 row bands per image (C=%d W=%d H=%d)", C, W, H);
+  const int grid = block_stack_bwd_grid(N);
+  if (slab_stride < (long)grid * (9L * C * C + C)) return fail(ASR_E_ARG, "stack backward: slab_stride too small");
+  // in-kernel pass 1 needs <= 512 group-row chunks per workgroup (one per wgrad thread)
+  const long fchunks = (long)((grid + 31) / 32) * ((9L * C * C + C) / 4);
+  const int lfold = (fchunks + grid - 1) / grid <= 512 ? 2 : L;
+  if (lfold_out) *lfold_out = lfold;
+  ASR_TRY(hip_check(hipMemsetAsync(done, 0, align_up((size_t)(L + 4) * 4, 16), s), "hipMemsetAsync"));
+  using L2 = blk::Bwd2Lds<64, 32, kBwdBR>;
+  hipLaunchKernelGGL((blk::k_bwd3_stack<64, 32, kBwdBR>), dim3(grid), dim3(768), (size_t)L2::TOTAL, s, (bf16*)dbuf0,
+                     (bf16*)dbuf1, (const bf16*)xs, x_stride, masks, mask_stride, (const bf16*)w, w_stride, h, two_gamma,
+                     N, H, L, ro0, slabs, slab_stride, grp, grp_stride, done, done + L + 2, lfold);
+  ASR_LAUNCH_CHECK("k_bwd3_stack");
+  return ASR_OK;
 }
 
 int block_bwd_mfma(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,

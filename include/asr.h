@@ -234,6 +234,12 @@ typedef struct asr_net_config {
 #define ASR_VARIANT_STEM_WGRAD_VALU 4 /* stem weight gradient on the fp32 VALU
                                         kernel from dx1 and x1 (relu' not fused
                                         into the first block's backward)       */
+#define ASR_VARIANT_PER_BLOCK_FWD 8 /* C=64 bf16 training forward: one k_fwd3
+                                       launch per block instead of the single
+                                       all-blocks k_fwd3_stack launch         */
+#define ASR_VARIANT_PER_BLOCK_BWD 16 /* C=64 bf16 Euler backward: one k_bwd3 launch
+                                        per block (slab pass folded into the
+                                        next one) instead of k_bwd3_stack     */
 
 long asr_net_param_count(const asr_net_config* cfg);
 size_t asr_net_workspace_bytes(const asr_net_config* cfg);

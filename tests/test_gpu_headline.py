@@ -3,10 +3,14 @@ configs[1]: the C=64 Euler bf16 network) against the fp64 oracle, and the
 reference-held conv KAT run through the C ABI itself.
 
 The bf16 network runs with the production kernel set (variant 0): the MFMA
-stem forward (k_stem_fwd_mfma), the pipelined block forward (k_fwd_pipe),
-the fused backward with the stem's relu' folded into the first block
-(k_bwd2<..., RO>), the slab reduction folded into the next block's backward,
-and the MFMA stem weight gradient (k_stem_wgrad_mfma).  It is compared with
+stem forward (k_stem_fwd_mfma), the band-conv block forward (k_fwd3, three
+workgroups per CU), the 12-wave fused backward with the stem's relu' folded
+into the first block (k_bwd3<..., RO>), the slab reduction folded into the
+next block's backward, and the MFMA stem weight gradient (k_stem_wgrad_mfma).
+The N=192 case gives every persistent workgroup several row bands (fwd: 1536
+bands over 768 workgroups, bwd: 6 bands per workgroup), so the band pipeline,
+the halo-row copies and the per-workgroup dW accumulation across bands are
+all compared with the oracle, not only the single-band path.  It is compared with
 the fp64 oracle (oracle.net_forward / net_backward, a restatement of
 tfkeras_resnets.py:547-597, training.py:295) on the same fp32 parameters and
 uint8 images.
@@ -32,7 +36,8 @@ torch = pytest.importorskip("torch")
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.mark.parametrize("C,N,L,h,seed", [(64, 8, 3, 8.0 / 30, 0), (64, 16, 4, 0.25, 1), (16, 8, 3, 8.0 / 30, 2)])
+@pytest.mark.parametrize("C,N,L,h,seed", [(64, 8, 3, 8.0 / 30, 0), (64, 16, 4, 0.25, 1), (16, 8, 3, 8.0 / 30, 2),
+                                          (64, 192, 2, 8.0 / 30, 3)])
 def test_euler_bf16_network_matches_oracle(C, N, L, h, seed):
     from differential_equations_resnet_amd.runtime import NetExecutor
     spec = O.NetSpec(C=C, L=L, h=h)

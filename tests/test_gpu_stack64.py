@@ -1,0 +1,131 @@
+"""GPU parity of the C=64 stack forward (k_fwd3_stack: all L Euler blocks of
+the headline network in one launch, whole images per workgroup), reached
+through asr_block_stack_forward and the network executor's training forward.
+
+Checks:
+  * a stack of L blocks equals L single-block calls (asr_conv_forward ->
+    k_fwd3, the same band conv and epilogue) bitwise, relu masks included,
+    for N = 1, N not a multiple of the grid and N above it (two images per
+    workgroup), with and without bias;
+  * every layer against the oracle's Euler step on the GPU's own bf16 input
+    of that layer (models/tfkeras_resnets.py:69-92 via conv2d_same): 2^-8
+    relative + 4e-3 * max|ref|;
+  * the network's training step with the stack forward equals the one with
+    per-block forward launches (ASR_VARIANT_PER_BLOCK_FWD) bitwise: loss and
+    every gradient.
+"""
+import numpy as np
+import pytest
+
+from helpers import assert_close, bf16_round
+from oracle import asr_oracle as O
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def rt():
+    from differential_equations_resnet_amd import runtime
+    runtime.require_gpu()
+    return runtime
+
+
+@pytest.mark.parametrize("N,L,with_bias", [(1, 3, True), (5, 4, False), (300, 3, True), (600, 2, True)])
+def test_stack64_equals_single_blocks(rt, N, L, with_bias):
+    C, H, W, h = 64, 32, 32, 8.0 / 30
+    rng = np.random.default_rng(N * 7 + L)
+    dev = torch.device("cuda")
+    pm = rt.param_map(C)
+    th = np.concatenate([O.flatten(O.init_theta_3by3(C, rng, np.float64)) for _ in range(L)]).astype(np.float32)
+    w = rt.theta_to_w(torch.from_numpy(th).to(dev), C, pm, 0.0, rt.ASR_BF16, layers=L)
+    b = (rng.standard_normal((L, C)) * 0.1).astype(np.float32)
+    bias = torch.from_numpy(b).to(dev) if with_bias else None
+    x0 = torch.from_numpy(rng.standard_normal((N, H, W, C)).astype(np.float32)).to(dev).to(torch.bfloat16)
+    ys, masks = rt.block_stack_forward(x0, w, bias, h)
+    x = x0
+    for l in range(L):
+        m = torch.zeros(rt.mask_bytes(N, H, W, C), dtype=torch.uint8, device=dev)
+        y = rt.conv_forward(rt.ASR_MODE_EULER, x, w[l:l + 1], bias[l].contiguous() if bias is not None else None, h, m)
+        assert torch.equal(y, ys[l]), f"layer {l}: stack != single block"
+        assert torch.equal(m, masks[l]), f"layer {l}: mask differs"
+        x = y
+    # oracle on a few images (all of them when N is small)
+    src, sign = O.param_map(C)
+    th = th.reshape(L, -1)
+    pick = np.arange(N) if N <= 5 else np.array([0, N // 2, N - 1])
+    xin = x0[pick].float().cpu().numpy().astype(np.float64)
+    for l in range(L):
+        Wl = bf16_round(O.assemble_from_map(th[l].astype(np.float64), C, src, sign, 0.0)).astype(np.float64)
+        z = O.conv2d_same(xin, Wl) + (b[l] if with_bias else 0.0)
+        want = xin + h * np.maximum(z, 0)
+        got = ys[l][pick].float().cpu().numpy()
+        assert_close(got, want, rtol=2 ** -8, atol=4e-3 * np.abs(want).max(), what=f"layer {l}")
+        xin = got.astype(np.float64)
+
+
+@pytest.mark.parametrize("N", [1, 8, 192, 512])
+def test_network_stack_forward_equals_per_block(rt, N):
+    C, L = 64, 4
+    from differential_equations_resnet_amd.netparams import init_net_params
+    dev = torch.device("cuda")
+    params = torch.from_numpy(init_net_params(C, L, 3, 10, seed=3) * 0.5).to(dev)
+    rng = np.random.default_rng(21)
+    imgs = torch.from_numpy(rng.integers(0, 256, (N, 32, 32, 3), dtype=np.uint8)).to(dev)
+    tgt = torch.from_numpy(np.eye(10, dtype=np.float32)[rng.integers(0, 10, N)]).to(dev)
+    ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / L, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
+                        dtype="bfloat16", input_u8=True, device=dev)
+    loss, g = ex.forward_backward(params, imgs, tgt)
+    loss, g = loss.clone(), g.clone()
+    ex.variant = rt.ASR_VARIANT_PER_BLOCK_FWD
+    loss1, g1 = ex.forward_backward(params, imgs, tgt)
+    ex.variant = 0
+    torch.cuda.synchronize()
+    assert torch.equal(loss, loss1)
+    assert torch.equal(g, g1)
+    assert np.isfinite(loss.item()) and g.abs().max().item() > 0
+
+
+@pytest.mark.parametrize("N,L,gamma,kind,anti", [(512, 4, 0.0, "3by3", True), (192, 5, 0.0, "3by3", True),
+                                                 (8, 3, -0.1, "3by3", True), (1, 2, 0.0, "3by3", True),
+                                                 (24, 1, 0.0, "3by3", True), (64, 4, 0.0, "general", False)])
+def test_network_stack_backward_equals_per_block(rt, N, L, gamma, kind, anti):
+    """k_bwd3_stack (all blocks' backward in one launch, slabs published
+    write-through and pass 1 of block l's reduction folded into block l-2's
+    bands behind a counter) against one k_bwd3 launch per block
+    (ASR_VARIANT_PER_BLOCK_BWD).  dx is the same arithmetic, so the loss, the
+    stem gradient (from dz1) and the head gradients are bitwise equal; the
+    block gradients sum the same per-workgroup partials, possibly in another
+    workgroup order: 1e-5 of max|g| per block."""
+    C = 64
+    from differential_equations_resnet_amd.netparams import init_net_params
+    dev = torch.device("cuda")
+    pk = {"3by3": rt.ASR_PARAM_3BY3, "general": rt.ASR_PARAM_GENERAL}[kind]
+    ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / max(L, 4), gamma, subtract_mean=127.5, divide_by_stddev=127.5,
+                        dtype="bfloat16", input_u8=True, device=dev, param_kind=pk, antisymmetric=anti)
+    rng = np.random.default_rng(N + 100 * L)
+    if kind == "3by3":
+        params = torch.from_numpy(init_net_params(C, L, 3, 10, seed=4) * 0.5).to(dev)
+    else:
+        params = torch.from_numpy((rng.standard_normal(ex.n_params) * 0.02).astype(np.float32)).to(dev)
+    imgs = torch.from_numpy(rng.integers(0, 256, (N, 32, 32, 3), dtype=np.uint8)).to(dev)
+    tgt = torch.from_numpy(np.eye(10, dtype=np.float32)[rng.integers(0, 10, N)]).to(dev)
+    loss, g = ex.forward_backward(params, imgs, tgt)
+    loss, g = loss.clone(), g.clone()
+    loss2, g2 = ex.forward_backward(params, imgs, tgt)
+    assert torch.equal(g, g2), "stack backward is not deterministic"
+    ex.variant = rt.ASR_VARIANT_PER_BLOCK_BWD
+    loss1, g1 = ex.forward_backward(params, imgs, tgt)
+    ex.variant = 0
+    torch.cuda.synchronize()
+    assert torch.equal(loss, loss1)
+    a, b = g.cpu().numpy(), g1.cpu().numpy()
+    n_blk = (ex.n_params - (9 * 3 * C + C) - (C * 10 + 10)) // L
+    stem, head = 9 * 3 * C + C, C * 10 + 10
+    assert np.array_equal(a[:stem], b[:stem]), np.abs(a[:stem] - b[:stem]).max()
+    assert np.array_equal(a[-head:], b[-head:])
+    for l in range(L):
+        o = stem + l * n_blk
+        ga, gb = a[o:o + n_blk], b[o:o + n_blk]
+        assert np.abs(gb).max() > 0
+        assert np.abs(ga - gb).max() <= 1e-5 * np.abs(gb).max(), (l, np.abs(ga - gb).max(), np.abs(gb).max())

@@ -57,6 +57,9 @@ for k, name in ((0, "k_fwd3"), (1, "k_bwd3")):
     print(f"{name}: workgroups {len(c)}, in-kernel clock median {np.median(ghz):.3f} GHz "
           f"(min {ghz.min():.3f}, max {ghz.max():.3f}); wave-0 cycles median {int(np.median(cyc))}, "
           f"max {int(cyc.max())}; wall median {np.median((c[:, 3] - c[:, 1]) / 100):.1f} us")
+    st, en = (c[:, 1] - c[:, 1].min()) / 100, (c[:, 3] - c[:, 1].min()) / 100
+    q = lambda v: " ".join(f"{x:.1f}" for x in np.percentile(v, [0, 10, 50, 90, 100]))  # noqa: E731
+    print(f"   start us (p0 p10 p50 p90 p100): {q(st)};  end us: {q(en)};  span {en.max():.1f} us")
 
 
 def phases(t, names):
@@ -74,3 +77,12 @@ print("k_bwd3 dgrad wave 0:")
 phases(tr[1, 0, :, :6], ["barrier", "mask+dma", "conv", "epilogue", "convert"])
 print("k_bwd3 wgrad wave 4:")
 phases(tr[1, 1, :, :5], ["barrier", "fold+xdma", "mfma", "halo+fold"])
+# workgroup 0: cycles from its clock stamp to the first band, and from the last band to its end stamp
+for k, role, last, name in ((0, 0, 4, "k_fwd3 wave 0"), (1, 0, 5, "k_bwd3 dgrad wave 0"), (1, 1, 4, "k_bwd3 wgrad wave 4")):
+    t = tr[k, role]
+    nbnd = int((t[:, 0] > 0).sum())
+    if nbnd:
+        pre = t[0, 0] - ck[k, 0, 0]
+        post = ck[k, 0, 2] - t[nbnd - 1, last]
+        print(f"{name}: {nbnd} bands; prologue {pre} cycles, after the last band {post} cycles, "
+              f"first band {t[1, 0] - t[0, 0] if nbnd > 1 else 0}, last band {t[nbnd - 1, last] - t[nbnd - 1, 0]}")
