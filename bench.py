@@ -221,18 +221,21 @@ def block_roofline(rt, lib, C, N, dtype_name, reps, h, integrator="euler"):
                 bytes_fwd=fb * P * esz, bytes_bwd=bb * P * esz, timing=timing_mode[0])
 
 
-def stack_roofline(rt, N, L, reps, h):
-    """The deep C=16 path (asr_deep16.hip): all L Euler blocks fused in one
-    forward and one backward launch, timed at the workload shape on random
+def stack_roofline(rt, N, L, reps, h, C=16):
+    """The network's block path at the workload shape: all L Euler blocks in
+    one forward and one backward launch (C=16: asr_deep16.hip, every image
+    resident in LDS; C=64: k_fwd3_stack / k_bwd3_stack, whole images per
+    workgroup), through asr_block_stack_forward / _backward, timed on random
     operands with HIP events on the launch stream (torch's current stream).
 
-    Algorithmic bytes per image (extended to the fused stack):
-    forward reads x_0 and writes every x_l and its relu mask (the backward
-    needs them): s·P + L·(s·P + P/8); backward reads every x_l and mask, dL/dx_L,
-    and writes dx_0: L·(s·P + P/8) + 2·s·P (P = 32·32·16, s = 2 B)."""
+    Algorithmic bytes per image.  C=16, extended to the fused
+    stack: forward reads x_0 and writes every x_l and its relu mask (the
+    backward needs them): s·P + L·(s·P + P/8); backward reads every x_l and
+    mask, dL/dx_L, and writes dx_0: L·(s·P + P/8) + 2·s·P (P = 32·32·16, s = 2 B).
+    C=64: the survey's per-block unit 5·P·s (forward x, y; backward dy, x, dx),
+    times L: x_l is re-read from HBM by every block there."""
     import torch
     dev = torch.device("cuda")
-    C = 16
     g = torch.Generator(device=dev).manual_seed(7)
     pm = rt.param_map(C)
     w = rt.theta_to_w(torch.randn(L * pm.n_theta, device=dev, generator=g) * 0.05, C, pm, 0.0, rt.ASR_BF16,
@@ -278,8 +281,11 @@ def stack_roofline(rt, N, L, reps, h):
 
     tf = timed(fwd)
     tb = timed(bwd)
-    act = L * (2 * P + P // 8)
-    bytes_fwd, bytes_bwd = N * (2 * P + act), N * (act + 4 * P)
+    if C == 16:
+        act = L * (2 * P + P // 8)
+        bytes_fwd, bytes_bwd = N * (2 * P + act), N * (act + 4 * P)
+    else:
+        bytes_fwd, bytes_bwd = N * L * 2 * 2 * P, N * L * 3 * 2 * P
     flops = 3 * 2 * 9 * C * C * 32 * 32 * N * L
     return dict(t_fwd=tf, t_bwd=tb, t=tf + tb, bytes=bytes_fwd + bytes_bwd, flops=flops, bytes_fwd=bytes_fwd,
                 bytes_bwd=bytes_bwd)
@@ -432,9 +438,10 @@ def main():
     value = N * world * args.steps / elapsed
 
     if rank == 0:
-        deep = C == 16 and dtype_name == "bfloat16" and integrator == "euler"  # the fused-stack path
+        # the network's fused-stack paths (C=16 LDS-resident, C=64 whole images per workgroup)
+        deep = C in (16, 64) and dtype_name == "bfloat16" and integrator == "euler"
         if deep:
-            rb = stack_roofline(rt, N, L, max(2, args.block_reps // 10), h)
+            rb = stack_roofline(rt, N, L, max(2, args.block_reps // 10), h, C)
         else:
             rb = block_roofline(rt, lib, C, N, dtype_name, args.block_reps, h, integrator)
         achieved = rb["bytes"] / rb["t"] / 1e9
@@ -444,7 +451,10 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": ("fused stack of all L Euler blocks, fwd + bwd (deep::k_fwd16_fused, deep::k_bwd16_fused, "
-                           "k_reduce_slabs, k_project_layers)" if deep else
+                           "k_reduce_slabs, k_project_layers)" if deep and C == 16 else
+                           "all L Euler blocks in one forward and one backward launch (blk::k_fwd3_stack, "
+                           "blk::k_bwd3_stack with pass 1 of the slab reduction in-launch; k_reduce_slabs for "
+                           "blocks 0-1, k_sum_groups, k_project_layers)" if deep else
                            "RK2 block fwd+bwd (blk::k_fwd3 stage 1 + blk::k_fwd_pipe<RESG> stage 2, blk::k_bwd3 stage 2 "
                            "+ blk::k_bwd3<XT> stage 1 on one slab set, k_reduce_slabs, k_project)"
                            if integrator == "rk2" and C == 64 else

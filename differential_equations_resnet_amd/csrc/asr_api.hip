@@ -49,6 +49,7 @@ bool deep16_supported(int H, int W, int C);
 bool block_stack_fwd_supported(int N, int H, int W, int C);
 bool block_stack_bwd_supported(int N, int H, int W, int C);
 int block_stack_bwd_grid(int N);
+int theta_dst_tile_major(const int32_t* in, long n, int C, int32_t* out, hipStream_t s);
 int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride, const uint8_t* masks,
                          long mask_stride, const void* w, long w_stride, float h, float two_gamma, int N, int H, int W,
                          int C, int L, int ro0, float* slabs, long slab_stride, float* grp, long grp_stride,
@@ -534,14 +535,17 @@ int asr_block_stack_forward(const void* x0, void* ys, long y_stride, uint8_t* ma
 // workspace of asr_block_stack_backward: two dx buffers, then either the
 // fused path's slabs + group rows or one per-block backward workspace
 struct StackWs {
-  size_t da, db, slabs, grp, blk, total;
-  bool deep;
+  size_t da, db, slabs, grp, blk, done, tdst, total;
+  bool deep, stack64;
+  int grid;
 };
 static StackWs stack_ws_layout(int N, int H, int W, int C, int L, int dtype) {
   StackWs w{};
   const size_t act = align_up((size_t)N * H * W * C * (dtype == ASR_BF16 ? 2 : 4), 256);
   const long ES = 9L * C * C + C;
   w.deep = dtype == ASR_BF16 && deep16_supported(H, W, C);
+  w.stack64 = dtype == ASR_BF16 && !w.deep && block_stack_bwd_supported(N, H, W, C);
+  w.grid = w.stack64 ? block_stack_bwd_grid(N) : 0;
   size_t off = 0;
   w.da = off;
   off += act;
@@ -552,6 +556,15 @@ static StackWs stack_ws_layout(int N, int H, int W, int C, int L, int dtype) {
     off += align_up(deep16_slab_bytes(N, L), 256);
     w.grp = off;
     off += align_up((size_t)L * reduce_groups(kMaxSlabsApi) * ES * 4, 256);
+  } else if (w.stack64) {  // slabs [L][grid][ES] (tile-major dW), group rows, counters, tile-major theta map
+    w.slabs = off;
+    off += align_up((size_t)L * w.grid * ES * 4, 256);
+    w.grp = off;
+    off += align_up((size_t)L * reduce_groups(w.grid) * ES * 4, 256);
+    w.done = off;
+    off += align_up((size_t)(L + 4) * 4, 256);
+    w.tdst = off;
+    off += align_up((size_t)2 * 9 * C * C * 4, 256);
   } else {
     w.blk = off;
     off += bwd_ws_layout(N, H, W, C, dtype).total;
@@ -596,6 +609,27 @@ int asr_block_stack_backward(const void* dyL, const void* xs, long x_stride, con
       ASR_TRY(reduce_slabs_to_groups(slabs, L * rows, E + C, (float*)(base + Lw.grp), s));
       ASR_TRY(project_layers((float*)(base + Lw.grp), (long)G * (E + C), G, E, C, theta_dst, n_theta, L, dparams,
                              n_theta + C, s));
+    }
+    return ASR_OK;
+  }
+  if (Lw.stack64) {
+    if (n_theta > 9L * C * C) return fail(ASR_E_ARG, "asr_block_stack_backward: n_theta > 9*C*C");
+    ASR_TRY(hip_check(hipMemcpyAsync(base + Lw.da, dyL, act, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync"));
+    float* slabs = (float*)(base + Lw.slabs);
+    float* grp = (float*)(base + Lw.grp);
+    const long ES = E + C, sst = (long)Lw.grid * ES, gst = (long)reduce_groups(Lw.grid) * ES;
+    int lfold = L;
+    ASR_TRY(block_stack_bwd_mfma(base + Lw.da, base + Lw.db, xs, x_stride, masks, mask_stride, w, w_stride, h,
+                                 2.f * gamma, N, H, W, C, L, 0, slabs, sst, grp, gst, (unsigned*)(base + Lw.done),
+                                 &lfold, s));
+    ASR_TRY(hip_check(hipMemcpyAsync(dx0, base + ((L & 1) ? Lw.db : Lw.da), act, hipMemcpyDeviceToDevice, s),
+                      "hipMemcpyAsync"));
+    if (dparams) {
+      for (int l = std::min(lfold, L) - 1; l >= 0; --l)
+        ASR_TRY(reduce_slabs_to_groups(slabs + (long)l * sst, Lw.grid, ES, grp + (long)l * gst, s));
+      int32_t* tm = (int32_t*)(base + Lw.tdst);
+      ASR_TRY(theta_dst_tile_major(theta_dst, 2 * n_theta, C, tm, s));
+      ASR_TRY(project_layers(grp, gst, reduce_groups(Lw.grid), E, C, tm, n_theta, L, dparams, n_theta + C, s));
     }
     return ASR_OK;
   }

@@ -430,6 +430,28 @@ __global__ void k_sum_groups(float* __restrict__ grp, long grp_stride, int G, lo
   rg[e] = (a[0] + a[1]) + (a[2] + a[3]);
 }
 
+// theta_dst entries (e<<1)|neg with e = m*C + o (dW row-major) -> the same
+// entries into the tile-major dW of k_bwd3_stack's slabs:
+// ((m/16 * C/16 + o/16) * 64 + 16*((m%16)/4) + o%16) * 4 + m%4
+__global__ void k_theta_dst_tile(const int32_t* __restrict__ in, long n, int C, int32_t* __restrict__ out) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t v = in[i];
+  if (v < 0) {
+    out[i] = v;
+    return;
+  }
+  const long e = v >> 1, m = e / C, o = e % C;
+  const long et = (((m / 16) * (C / 16) + o / 16) * 64 + 16 * ((m % 16) / 4) + o % 16) * 4 + m % 4;
+  out[i] = (int32_t)((et << 1) | (v & 1));
+}
+
+int theta_dst_tile_major(const int32_t* in, long n, int C, int32_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_theta_dst_tile, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, n, C, out);
+  ASR_LAUNCH_CHECK("k_theta_dst_tile");
+  return ASR_OK;
+}
+
 int project_layers(float* grp, long grp_stride, int G, long E, int Cb, const int32_t* theta_dst, long n_theta,
                    int L, float* out, long out_stride, hipStream_t s) {
   const long n = n_theta + Cb;

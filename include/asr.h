@@ -149,7 +149,9 @@ long asr_mask_bytes(int N, int H, int W, int C);
  * written, to ys.  w: layer l's asr_theta_to_w output at w + l*w_stride
  * elements; bias: layer l's at bias + l*bias_stride (may be NULL).  bf16 at
  * C=16, H=W=32 runs all L steps in one launch with every image resident in
- * LDS; other shapes run the per-block kernels in sequence. */
+ * LDS; bf16 at C=64, W=32 (store_all) runs all L steps in one launch with
+ * whole images per workgroup; other shapes run the per-block kernels in
+ * sequence. */
 int asr_block_stack_forward(const void* x0, void* ys, long y_stride, uint8_t* masks, long mask_stride,
                             const void* w, long w_stride, const float* bias, long bias_stride, float h,
                             int N, int H, int W, int C, int L, int dtype, int store_all, asr_stream_t stream);
@@ -160,7 +162,9 @@ int asr_block_stack_forward(const void* x0, void* ys, long y_stride, uint8_t* ma
  * dL/dx_0; dparams (may be NULL) layer l's [dtheta (n_theta) | dbias (C)] at
  * dparams + l*(n_theta + C), projected through theta_dst.  bf16 at C=16,
  * H=W=32 runs one fused launch with dx resident in LDS (w_stride must be
- * asr_wpack_elems(16)); other shapes run asr_conv_backward per block. */
+ * asr_wpack_elems(16)); bf16 at C=64, W=32 runs one launch over all blocks
+ * (whole images per workgroup, weight-gradient slabs reduced in-launch);
+ * other shapes run asr_conv_backward per block. */
 size_t asr_block_stack_backward_workspace_bytes(int N, int H, int W, int C, int L, int dtype);
 int asr_block_stack_backward(const void* dyL, const void* xs, long x_stride, const uint8_t* masks, long mask_stride,
                              const void* w, long w_stride, const int32_t* theta_dst, long n_theta, float h,

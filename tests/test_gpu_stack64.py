@@ -129,3 +129,45 @@ def test_network_stack_backward_equals_per_block(rt, N, L, gamma, kind, anti):
         ga, gb = a[o:o + n_blk], b[o:o + n_blk]
         assert np.abs(gb).max() > 0
         assert np.abs(ga - gb).max() <= 1e-5 * np.abs(gb).max(), (l, np.abs(ga - gb).max(), np.abs(gb).max())
+
+
+@pytest.mark.parametrize("N,L,gamma", [(3, 4, 0.0), (7, 3, -0.1), (300, 5, 0.0), (512, 4, 0.0)])
+def test_stack64_backward_abi_matches_per_block_and_oracle(rt, N, L, gamma):
+    """asr_block_stack_backward at C=64 (k_bwd3_stack) against asr_conv_backward
+    block by block (k_bwd3): dx_0 bitwise (the same dgrad arithmetic per
+    element), dtheta / dbias within 1e-5 of max|.| per layer (the same
+    per-workgroup partial sums, another workgroup order when the band split
+    differs); the top layer also against the oracle on the GPU's bf16 operands
+    (1e-3 of max|.|, N <= 64).  N=512 folds pass 1 of blocks >= 2 in-launch; N=3, 7
+    reduce every block after the launch (a workgroup would own > 512 chunks)."""
+    from helpers import decode_mask
+    C, h = 64, 8.0 / 30
+    rng = np.random.default_rng(N * 3 + L)
+    dev = torch.device("cuda")
+    pm = rt.param_map(C)
+    th = np.concatenate([O.flatten(O.init_theta_3by3(C, rng, np.float64)) for _ in range(L)]).astype(np.float32)
+    w = rt.theta_to_w(torch.from_numpy(th).to(dev), C, pm, gamma, rt.ASR_BF16, layers=L)
+    bias = torch.from_numpy((rng.standard_normal((L, C)) * 0.1).astype(np.float32)).to(dev)
+    x0 = torch.from_numpy(rng.standard_normal((N, 32, 32, C)).astype(np.float32)).to(dev).to(torch.bfloat16)
+    ys, masks = rt.block_stack_forward(x0, w, bias, h)
+    dyL = torch.from_numpy((rng.standard_normal((N, 32, 32, C)) * 0.1).astype(np.float32)).to(dev).to(torch.bfloat16)
+    dx0, dp = rt.block_stack_backward(dyL, x0, ys, masks, w, pm, h, gamma)
+    dy = dyL
+    for l in range(L - 1, -1, -1):
+        xl = x0 if l == 0 else ys[l - 1]
+        dx, dth, db, _ = rt.conv_backward(rt.ASR_MODE_EULER, dy, xl.contiguous(), masks[l], w[l:l + 1], pm, h, gamma)
+        for got, want, what in ((dp[l, :pm.n_theta], dth, "dtheta"), (dp[l, pm.n_theta:], db, "dbias")):
+            a, bb = got.cpu().numpy().astype(np.float64), want.cpu().numpy().astype(np.float64)
+            assert np.abs(a - bb).max() <= 1e-5 * max(np.abs(bb).max(), 1e-30), (l, what, np.abs(a - bb).max())
+        if l == L - 1 and N <= 64:  # (the fp64 oracle's wgrad at N=300+ would take minutes)
+            xo = xl.float().cpu().numpy().astype(np.float64)
+            mk = decode_mask(masks[l].cpu().numpy(), N, 32, 32, C)
+            dzm = bf16_round(dyL.float().cpu().numpy() * mk).astype(np.float64)
+            dW_want = h * O.conv2d_backprop_filter(xo, dzm)
+            src, sign = O.param_map(C)
+            dth_want = O.project_dW(dW_want, src, sign, pm.n_theta)
+            db_want = h * dzm.sum(axis=(0, 1, 2))
+            assert np.abs(dp[l, :pm.n_theta].cpu().numpy() - dth_want).max() <= 1e-3 * np.abs(dth_want).max()
+            assert np.abs(dp[l, pm.n_theta:].cpu().numpy() - db_want).max() <= 1e-3 * np.abs(db_want).max()
+        dy = dx
+    assert torch.equal(dx0, dy)

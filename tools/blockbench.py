@@ -15,6 +15,7 @@ ap.add_argument("--N", type=int, default=512)
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--what", default="fwd,bwd")
 ap.add_argument("--lib", default=None, help="development: another build of libasr (A/B timing)")
+ap.add_argument("--stack", type=int, default=0, help="run L blocks through asr_block_stack_forward/backward instead")
 a = ap.parse_args()
 lib = _lib.load(path=a.lib)
 dev = rt.require_gpu()
@@ -39,6 +40,16 @@ whats = a.what.split(",")
 # one forward first: the backward reads its relu mask (random operands, ~half set)
 _lib.check(lib.asr_conv_forward(0, x.data_ptr(), y.data_ptr(), mask.data_ptr(), w.data_ptr(), bias.data_ptr(),
                                 0.25, N, H, W, C, 1, s))
+if a.stack:  # the network's path: all L blocks in one forward and one backward launch
+    L = a.stack
+    w = rt.theta_to_w(torch.randn(L * pm.n_theta, device=dev, generator=g) * 0.05, C, pm, 0.0, rt.ASR_BF16, layers=L)
+    biasL = torch.zeros(L, C, device=dev)
+    for _ in range(a.reps):
+        ys, masks = rt.block_stack_forward(x, w, biasL, 0.25)
+        rt.block_stack_backward(dy, x, ys, masks, w, pm, 0.25, 0.0)
+    torch.cuda.synchronize()
+    print("done")
+    sys.exit(0)
 for _ in range(a.reps):
     if "fwd" in whats:
         _lib.check(lib.asr_conv_forward(0, x.data_ptr(), y.data_ptr(), mask.data_ptr(), w.data_ptr(), bias.data_ptr(),

@@ -9,4 +9,4 @@ cat gpurun_out/bench_$TAG.json
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1 || { echo PROF FAILED; tail -20 gpurun_out/prof_$TAG.log; exit 1; }
 python3 tools/kstats.py gpurun_out/prof_$TAG/run_kernel_stats.csv 14
-bash tools/traffic.sh $TAG c2 --reps 10
+TRAFFIC_BLOCKS=30 bash tools/traffic.sh $TAG c2 --reps 3 --stack 30

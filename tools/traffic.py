@@ -2,7 +2,9 @@
 tools/traffic.sh, corrected as MI355X_MICROARCH.md § HBM prescribes:
 FETCH_SIZE (KiB) counts half the bytes of 16-B/lane streaming reads on
 gfx950 -> x2; WRITE_SIZE (KiB) is exact for 16-B/lane stores.
-usage: traffic.py PMC_DIR CONFIG OUT_JSON [ROUND_TAG]"""
+usage: traffic.py PMC_DIR CONFIG OUT_JSON [ROUND_TAG [BLOCKS]]
+BLOCKS > 1: the passes ran blockbench --stack BLOCKS (all blocks in one
+forward and one backward launch); per-block bytes = per-launch bytes / BLOCKS."""
 import csv
 import glob
 import json
@@ -12,6 +14,7 @@ from collections import defaultdict
 
 root, config, out = sys.argv[1], sys.argv[2], sys.argv[3]
 tag = sys.argv[4] if len(sys.argv) > 4 else "?"
+blocks = int(sys.argv[5]) if len(sys.argv) > 5 else 1
 vals = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
@@ -37,9 +40,12 @@ for k, cs in vals.items():
     fetch = sum(cs["FETCH_SIZE"]) / max(len(cs["FETCH_SIZE"]), 1) * 1024 * 2 if "FETCH_SIZE" in cs else 0.0
     write = sum(cs["WRITE_SIZE"]) / max(len(cs["WRITE_SIZE"]), 1) * 1024 if "WRITE_SIZE" in cs else 0.0
     per[short] = {"read_bytes": round(fetch), "write_bytes": round(write), "launches": len(cs.get("FETCH_SIZE", []))}
-total = sum(v["read_bytes"] + v["write_bytes"] for v in per.values())
-res = {"config": config, "round": tag, "hbm_bytes_per_block": total, "per_kernel": per,
+total = sum(v["read_bytes"] + v["write_bytes"] for v in per.values()) / blocks
+res = {"config": config, "round": tag, "hbm_bytes_per_block": round(total), "per_kernel": per,
+       "blocks_per_launch": blocks,
        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over tools/blockbench.py "
-                 "(one fwd + one bwd per rep); FETCH_SIZE x2 (gfx950 16B/lane read correction), KiB->B"}
+                 + (f"--stack {blocks} (one stack fwd + one stack bwd per rep; per-launch bytes / {blocks})"
+                    if blocks > 1 else "(one fwd + one bwd per rep)")
+                 + "; FETCH_SIZE x2 (gfx950 16B/lane read correction), KiB->B"}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
