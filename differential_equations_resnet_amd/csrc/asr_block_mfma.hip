@@ -74,6 +74,9 @@
 #ifndef ASR_BWD_STACK
 #define ASR_BWD_STACK 1  // C=64 network backward: all blocks in one k_bwd3_stack launch (0: one k_bwd3 per block)
 #endif
+#ifndef ASR_STACK_ABLATE
+#define ASR_STACK_ABLATE 0  // development only: k_bwd3_stack 1 = no slab stores at block ends (wrong dW; timing)
+#endif
 #ifndef ASR_BWD3
 #define ASR_BWD3 1  // C=64 backward: k_bwd3 (12 waves, 3 per SIMD; 0: k_bwd2, 8 waves)
 #endif
@@ -1065,9 +1068,12 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
   dma_rows<C, W>(x0, lds, cn, -1, min(BR, H) + 2, H, wave, NW, lane);
   int nst = 0;
   const int total = L * per;
+  ASR_BCLK(0, 0);
   for (int it = 0; it < total; ++it) {
     const int buf = it & 1;
+    if (wave == 0) ASR_BTR(0, 0, it, 0);
     barrier_vm(nst);  // band it landed; every wave is done with band it-1's tile
+    if (wave == 0) ASR_BTR(0, 0, it, 1);
     nst = 0;
     if (it + 1 < total) {
       unsigned char* nt = lds + (buf ^ 1) * TILE;
@@ -1086,6 +1092,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
         dma_rows<C, W>(xs, nt, xn, yy - 1, min(BR, H - yy) + 2, H, wave, NW, lane);
       }
     }
+    if (wave == 0) ASR_BTR(0, 0, it, 2);
     const unsigned tb = lds_u32(lds + buf * TILE);
     f32x4 acc[RB][2];
 #pragma unroll
@@ -1093,6 +1100,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
 #pragma unroll
       for (int pt = 0; pt < 2; ++pt) acc[r][pt] = f32x4{bz[0], bz[1], bz[2], bz[3]};
     conv_band<C, W, RB>(tb, lo, A, acc);
+    if (wave == 0) ASR_BTR(0, 0, it, 3);
     u32x4 xr[RB];
 #pragma unroll
     for (int r = 0; r < RB; ++r) xr[r] = lds_rd128(tb + lxr + (unsigned)(r * BD::ROWB));
@@ -1129,9 +1137,11 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
       *(u32x4*)(yb + r * W * C * 2) = yw;
       ++nst;
     }
+    if (wave == 0) ASR_BTR(0, 0, it, 4);
     cl = xl, cn = xn, cb = xb;
     adv(xl, xn, xb);
   }
+  ASR_BCLK(0, 1);
 }
 
 // ===========================================================================
@@ -2794,6 +2804,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
   };
   __syncthreads();
   if (n0 >= n1) return;  // (uniform per workgroup: never with grid <= N)
+  ASR_BCLK(1, 0);
 
   constexpr int ES = 9 * C * C + C, ECH = ES / 4;
   if (wave < 4) {
@@ -2812,13 +2823,16 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       const int buf = it & 1;
       const int n = cur.n, y0 = cur.b * BR, l = cur.l;
       const int rows = min(BR, H - y0);
+      if (wave == 0) ASR_BTR(1, 0, it, 0);
       barrier_vm(nst);  // item it staged everywhere; item it-1 fully consumed
+      if (wave == 0) ASR_BTR(1, 0, it, 1);
       const unsigned dzt = lds_u32(lds + LL::DZ + buf * LL::TILE), dyt = lds_u32(lds + LL::DY + buf * LL::TILE);
       const unsigned xt = lds_u32(lds + LL::X + buf * LL::TILE);
       f32x4 acc[BR][2];
 #pragma unroll
       for (int r = 0; r < BR; ++r) acc[r][0] = acc[r][1] = f32x4{0.f, 0.f, 0.f, 0.f};
       conv_band<C, W, BR>(dzt, lo, A, acc);
+      if (wave == 0) ASR_BTR(1, 0, it, 2);
       const bool last_of_block = cur.b == nb - 1 && n == n1 - 1;
       if (last_of_block && l > 0) load_A1<C>(wpack + (long)(l - 1) * w_stride, ot, lane, A);
       bf16* drow = dx_of(l) + ((long)n * H + y0) * W * C;
@@ -2876,6 +2890,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         else epilogue(F_{}, F_{});
       }
       nst = nld;
+      if (wave == 0) ASR_BTR(1, 0, it, 3);
       adv(cur);
     }
     barrier_vm(0);  // matches the wgrad waves' end-of-loop barrier
@@ -2997,6 +3012,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       const int y0 = cur.b * BR, l = cur.l;
       const int rows = min(BR, H - y0);
       const bool first_of_block = cur.b == 0 && cur.n == n0;
+      if (wave == 4) ASR_BTR(1, 1, it, 0);
       if (first_of_block && l + 2 < L && l + 2 >= lfold && w8 == 0 && lane == 0) {
         // block l+2's slabs: every workgroup published them (bounded poll)
         unsigned spins = 0;
@@ -3010,6 +3026,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
       barrier_vm(0);  // this wave's x rows of item it landed (and its slab stores drained)
+      if (wave == 4) ASR_BTR(1, 1, it, 1);
       if (first_of_block && l + 1 < L && l + 1 >= lfold && w8 == 0 && lane == 0)
         __hip_atomic_fetch_add((gu32*)(done + l + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // published
       if (first_of_block && l + 2 < L && l + 2 >= lfold) fold_begin(l + 2);
@@ -3039,6 +3056,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         ++ipc;
       };
       while (ipc < npc && ipc < ASR_BWD3_DMA0) piece();
+      if (wave == 4) ASR_BTR(1, 1, it, 2);
       bf16x8 Bf[2], Ar[3];
       auto mfma_band = [&](auto bo) {
         constexpr int BO = decltype(bo)::value;
@@ -3079,10 +3097,12 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       }
       mfma_band(std::integral_constant<int, 0>{});
       while (ipc < npc) piece();
+      if (wave == 4) ASR_BTR(1, 1, it, 3);
       if (more) {
         vm_wait(0);
         convert_own(orow, buf ^ 1, mwv);
       }
+      if (wave == 4) ASR_BTR(1, 1, it, 4);
       if (cont) {  // halo rows of the next band of this image
         const unsigned base = lds_u32(lds);
         const int nbf = buf ^ 1;
@@ -3116,7 +3136,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
           foff += ES;
         }
       const bool last_of_block = cur.b == nb - 1 && cur.n == n1 - 1;
-      if (last_of_block) {
+      if (last_of_block && (!(ASR_STACK_ABLATE & 1) || hs == -1.f)) {  // (ablation: never, but kept live)
         if (l + 2 < L && l + 2 >= lfold) fold_end(l + 2);
         // publish block l's dW tiles and db (write-through; drained at the next band barrier)
         float* slab = slabs + (long)l * slab_stride + (long)blockIdx.x * ES;
@@ -3141,11 +3161,13 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
           accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
+      if (wave == 4) ASR_BTR(1, 1, it, 5);
       cur = nxt;
       adv(nxt);
     }
     barrier_vm(0);
   }
+  ASR_BCLK(1, 1);
 }
 
 // ===========================================================================

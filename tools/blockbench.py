@@ -37,9 +37,6 @@ db = torch.empty(C, device=dev)
 _, tdst = pm.device(dev)
 s = torch.cuda.current_stream().cuda_stream
 whats = a.what.split(",")
-# one forward first: the backward reads its relu mask (random operands, ~half set)
-_lib.check(lib.asr_conv_forward(0, x.data_ptr(), y.data_ptr(), mask.data_ptr(), w.data_ptr(), bias.data_ptr(),
-                                0.25, N, H, W, C, 1, s))
 if a.stack:  # the network's path: all L blocks in one forward and one backward launch
     L = a.stack
     w = rt.theta_to_w(torch.randn(L * pm.n_theta, device=dev, generator=g) * 0.05, C, pm, 0.0, rt.ASR_BF16, layers=L)
@@ -50,6 +47,9 @@ if a.stack:  # the network's path: all L blocks in one forward and one backward 
     torch.cuda.synchronize()
     print("done")
     sys.exit(0)
+# one forward first: the backward reads its relu mask (random operands, ~half set)
+_lib.check(lib.asr_conv_forward(0, x.data_ptr(), y.data_ptr(), mask.data_ptr(), w.data_ptr(), bias.data_ptr(),
+                                0.25, N, H, W, C, 1, s))
 for _ in range(a.reps):
     if "fwd" in whats:
         _lib.check(lib.asr_conv_forward(0, x.data_ptr(), y.data_ptr(), mask.data_ptr(), w.data_ptr(), bias.data_ptr(),
