@@ -71,6 +71,9 @@
 #ifndef ASR_FWD_STACK
 #define ASR_FWD_STACK 1  // C=64 network forward: all blocks in one k_fwd3_stack launch (0: one k_fwd3 per block)
 #endif
+#ifndef ASR_FSTACK_HOOK
+#define ASR_FSTACK_HOOK 0  // k_fwd3_stack: next band's DMA pieces + residual reads as conv hooks (0: burst after the barrier)
+#endif
 #ifndef ASR_BWD_STACK
 #define ASR_BWD_STACK 1  // C=64 network backward: all blocks in one k_bwd3_stack launch (0: one k_bwd3 per block)
 #endif
@@ -1052,6 +1055,8 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
 
   zero_halo_cols<C, W>(lds, BR + 2, tid, 64 * NW);
   zero_halo_cols<C, W>(lds + TILE, BR + 2, tid, 64 * NW);
+  constexpr int IPR = W / G::PPI, NPW = ((BR + 2) * IPR + NW - 1) / NW;  // DMA pieces per row, per wave (max)
+  const unsigned loff = (unsigned)dma_lane_off<C, W>(lane) * 2u;
   // cursor over (block l, image n, band b)
   int cl = 0, cn = n0, cb = 0;
   int xl = 0, xn = n0, xb = 0;  // next item
@@ -1075,12 +1080,17 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
     barrier_vm(nst);  // band it landed; every wave is done with band it-1's tile
     if (wave == 0) ASR_BTR(0, 0, it, 1);
     nst = 0;
+    // the next band into the other buffer: rows 0, 1 are this band's rows BR, BR+1
+    // when it continues the image (copied inside LDS), the rest by DMA
+    unsigned char* ntile = lds;
+    const bf16* nxs = x0;
+    int ngy0 = 0, nrows = 0;
     if (it + 1 < total) {
       unsigned char* nt = lds + (buf ^ 1) * TILE;
       const int yy = xb * BR;
-      const bf16* xs = src_of(xl);
+      nxs = src_of(xl);
       if (xl == cl && xn == cn && xb == cb + 1) {
-        dma_rows<C, W>(xs, nt + 2 * BD::ROWB, xn, yy + 1, min(BR, H - yy), H, wave, NW, lane);
+        ntile = nt + 2 * BD::ROWB, ngy0 = yy + 1, nrows = min(BR, H - yy);
         const uint4* src = (const uint4*)(lds + buf * TILE + BR * BD::ROWB);
         uint4* dst = (uint4*)nt;
         constexpr int NCH = 2 * W * NQ;
@@ -1089,8 +1099,11 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
           dst[o] = src[o];
         }
       } else {
-        dma_rows<C, W>(xs, nt, xn, yy - 1, min(BR, H - yy) + 2, H, wave, NW, lane);
+        ntile = nt, ngy0 = yy - 1, nrows = min(BR, H - yy) + 2;
       }
+#if !ASR_FSTACK_HOOK
+      for (int j = wave; j < nrows * IPR; j += NW) dma_row_instr<C, W>(nxs, ntile, xn, ngy0, j, H, loff);
+#endif
     }
     if (wave == 0) ASR_BTR(0, 0, it, 2);
     const unsigned tb = lds_u32(lds + buf * TILE);
@@ -1099,11 +1112,28 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
     for (int r = 0; r < RB; ++r)
 #pragma unroll
       for (int pt = 0; pt < 2; ++pt) acc[r][pt] = f32x4{bz[0], bz[1], bz[2], bz[3]};
+    u32x4 xr[RB];
+#if ASR_FSTACK_HOOK
+    // the DMA pieces of this wave (j = wave + 4u) and the residual reads issued among
+    // the conv's MFMAs (a piece issues cheaper there than in a burst after the barrier)
+    auto hook = [&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      if constexpr (u < NPW) {
+        const int j = wave + NW * u;
+        if (j < nrows * IPR) dma_row_instr<C, W>(nxs, ntile, xn, ngy0, j, H, loff);
+      } else {
+#pragma unroll
+        for (int r = 0; r < RB; ++r) xr[r] = lds_rd128(tb + lxr + (unsigned)(r * BD::ROWB));
+      }
+    };
+    conv_band<C, W, RB, NPW + 1>(tb, lo, A, acc, hook);
+    if (wave == 0) ASR_BTR(0, 0, it, 3);
+#else
     conv_band<C, W, RB>(tb, lo, A, acc);
     if (wave == 0) ASR_BTR(0, 0, it, 3);
-    u32x4 xr[RB];
 #pragma unroll
     for (int r = 0; r < RB; ++r) xr[r] = lds_rd128(tb + lxr + (unsigned)(r * BD::ROWB));
+#endif
     const int l = cl;
     if (xl != cl && it + 1 < total) {  // the next item starts block l+1: its W and bias (L2 hits)
       load_A1<C>(wpack + (long)xl * w_stride, ot, lane, A);

@@ -1,9 +1,10 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_stack64.py > gpurun_out/t_st.log 2>&1; rc=$?
-tail -3 gpurun_out/t_st.log
-[ $rc -eq 0 ] || { grep -B5 -A40 "Error\|FAILED\|assert" gpurun_out/t_st.log | head -80; exit 1; }
-timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_headline.py tests/test_gpu_fullsize.py tests/test_gpu_network.py tests/test_gpu_api.py > gpurun_out/t_fs.log 2>&1; rc=$?
-tail -3 gpurun_out/t_fs.log
-[ $rc -eq 0 ] || { grep -B5 -A40 "Error\|FAILED\|assert" gpurun_out/t_fs.log | head -80; exit 1; }
-bash tools/netab.sh c2 "base fwd both base fwd both"
+for v in cur fh; do
+  cp build_abl_$v.so differential_equations_resnet_amd/libasr.so
+  timeout -k 10 200 python3 -u -m pytest -x -q --timeout 60 --timeout-method thread tests/test_gpu_stack64.py tests/test_gpu_headline.py > gpurun_out/t_$v.log 2>&1 || { echo "$v FAILED"; tail -30 gpurun_out/t_$v.log; exit 1; }
+  echo "$v: $(tail -1 gpurun_out/t_$v.log)"
+done
+bash tools/netab.sh c2 "cur fh cur fh" || exit 1
+cp build_abl_cur.so differential_equations_resnet_amd/libasr.so
+TRAFFIC_BLOCKS=30 bash tools/traffic.sh r02o c2 --reps 3 --stack 30 || exit 1
