@@ -1776,6 +1776,7 @@ __device__ __forceinline__ unsigned bwd2_mask_word(const uint8_t* __restrict__ m
 // image: dz rows BR, BR+1 -> rows 0, 1 (already masked), x rows BR, BR+1 ->
 // rows 0, 1, dy row BR+1 -> row 1 (the residual's first interior row) of
 // the next buffers.  Interior columns, physical chunk slots (the swizzle
+#if !ASR_BWD3  // k_bwd2 (8-wave C=64 backward, round 1): built only as the A/B arm of k_bwd3
 // depends on the column only).  t in [0, 256).
 template <int C, int W, int BR>
 __device__ __forceinline__ void bwd2_copy_halo(unsigned char* lds, int buf, int t) {
@@ -2296,6 +2297,8 @@ __global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const
     *(f32x4*)(pgrp + (long)fg * ES + (foff - (unsigned)fpe * ES)) = facc;
   }
 }
+
+#endif  // !ASR_BWD3
 
 // ===========================================================================
 // Backward v3 (C=64, W=32, BR=4): k_bwd2's band protocol (double-buffered
@@ -3530,6 +3533,7 @@ static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* ma
         if (fold_done) *fold_done = fold_P > 0;
         return ASR_OK;
       }
+#if !ASR_BWD3
       if (xt2) {
         hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_EULER, false, true>), dim3(grid), dim3(512), lds2, s,
                            (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs,
@@ -3551,6 +3555,8 @@ static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* ma
       ASR_LAUNCH_CHECK("k_bwd2");
       if (fold_done) *fold_done = fold_P > 0;
       return ASR_OK;
+#endif
+
     }
   }
   if (mode == blk::BWD_EULER) {

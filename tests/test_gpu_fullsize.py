@@ -92,9 +92,12 @@ def test_block_fullsize(rt, N, C, integrator):
                      what="y")
 
 
-@pytest.mark.parametrize("cfg", ["c2", "c3", "c5"])
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c3_64", "c5"])
 def test_network_fullsize_properties(rt, cfg):
-    C, L, N, integ = {"c2": (64, 30, 512, "euler"), "c3": (16, 108, 1024, "euler"), "c5": (64, 30, 512, "rk2")}[cfg]
+    """c3_64 is BASELINE C3's "(and 64)" variant: C=64, 108 blocks, N=1024 (the stacked C=64 kernels with
+    four images per workgroup and 108 in-launch slab hand-offs)."""
+    C, L, N, integ = {"c2": (64, 30, 512, "euler"), "c3": (16, 108, 1024, "euler"), "c3_64": (64, 108, 1024, "euler"),
+                      "c5": (64, 30, 512, "rk2")}[cfg]
     from differential_equations_resnet_amd.netparams import init_net_params
     h = 8.0 / L
     dev = torch.device("cuda")
