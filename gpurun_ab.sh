@@ -1,10 +1,10 @@
 set -o pipefail
 mkdir -p gpurun_out
-for v in cur fh; do
-  cp build_abl_$v.so differential_equations_resnet_amd/libasr.so
-  timeout -k 10 200 python3 -u -m pytest -x -q --timeout 60 --timeout-method thread tests/test_gpu_stack64.py tests/test_gpu_headline.py > gpurun_out/t_$v.log 2>&1 || { echo "$v FAILED"; tail -30 gpurun_out/t_$v.log; exit 1; }
-  echo "$v: $(tail -1 gpurun_out/t_$v.log)"
+bash tools/round_evidence.sh r02p || exit 1
+export TMPDIR=/tmp
+for cfg in c5 c3 c3_64; do
+  timeout -k 10 400 python3 bench.py --config $cfg --no-cpu-baseline > gpurun_out/bench_r02p_$cfg.json 2> gpurun_out/bench_r02p_$cfg.err || { echo "bench $cfg failed"; tail -5 gpurun_out/bench_r02p_$cfg.err; exit 1; }
+  python3 -c "import json; d=json.load(open('gpurun_out/bench_r02p_$cfg.json')); print('$cfg', d['value'], d['ms_per_step'], d['roofline']['frac'])"
 done
-bash tools/netab.sh c2 "cur fh cur fh" || exit 1
-cp build_abl_cur.so differential_equations_resnet_amd/libasr.so
-TRAFFIC_BLOCKS=30 bash tools/traffic.sh r02o c2 --reps 3 --stack 30 || exit 1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r02p_c5 -o run --output-format csv -- python3 bench.py --config c5 --no-cpu-baseline > gpurun_out/prof_r02p_c5.log 2>&1 || { echo PROF c5 FAILED; exit 1; }
+python3 tools/kstats.py gpurun_out/prof_r02p_c5/run_kernel_stats.csv 8
