@@ -48,6 +48,9 @@ static bool mfma_supported(int C, int W) { return (C == 16 || C == 32 || C == 64
 bool deep16_supported(int H, int W, int C);
 bool block_stack_fwd_supported(int N, int H, int W, int C);
 bool block_stack_bwd_supported(int N, int H, int W, int C);
+int block_stack_fwd_rk2_mfma(const void* x0, void* ys, void* xm, long y_stride, uint8_t* masks, uint8_t* masks2,
+                             long mask_stride, const void* w, long w_stride, const float* bias, long bias_stride,
+                             float h, int N, int H, int W, int C, int L, hipStream_t s);
 int block_stack_bwd_grid(int N);
 int theta_dst_tile_major(const int32_t* in, long n, int C, int32_t* out, hipStream_t s);
 int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride, const uint8_t* masks,
@@ -450,6 +453,13 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
     return deep16_forward(act(0), act(training ? 1 : c->L), L.P, training ? (uint8_t*)(ws + L.masks) : nullptr,
                           L.mask_bytes, ws + L.wbuf, params + L.off_blk + L.ntheta, L.blk_stride, c->h, N, c->L,
                           training, s);
+  }
+  if (bf && training && L.rk2 && block_stack_fwd_supported(N, H, W, C) && !(c->variant & ASR_VARIANT_PER_BLOCK_FWD)) {
+    // C=64 RK2: all 2L stages in one launch
+    uint8_t* m1 = (uint8_t*)(ws + L.masks);
+    return block_stack_fwd_rk2_mfma(act(0), act(1), ws + L.xmids, (long)L.P, m1, m1 + (size_t)c->L * L.mask_bytes,
+                                    (long)L.mask_bytes, ws + L.wbuf, (long)L.wstride, params + L.off_blk + L.ntheta,
+                                    L.blk_stride, c->h, N, H, W, C, c->L, s);
   }
   if (bf && training && !L.rk2 && block_stack_fwd_supported(N, H, W, C) && !(c->variant & ASR_VARIANT_PER_BLOCK_FWD)) {
     // C=64: all L blocks in one launch (whole images per workgroup)

@@ -1020,12 +1020,16 @@ __global__ __launch_bounds__(256, WPE) void k_fwd3(const bf16* __restrict__ x, c
 // checks nb >= 4.  Activations are distinct buffers per block, written once
 // in this launch, so no L1 line of them can be stale.
 // ===========================================================================
-template <int C, int W, int BR>
+// RK2 (BASELINE config 5): 2L stages, stage 2l = the first (x_l -> xmid_l, h/2,
+// mask1), stage 2l+1 the second (xmid_l -> x_{l+1}, h, mask2) with the residual
+// x_l from global memory (16-B loads in the regrouped layout, as k_fwd3<..., RESG>).
+template <int C, int W, int BR, bool RK2 = false>
 __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ x0, bf16* __restrict__ ys,
                                                        long y_stride, uint8_t* __restrict__ masks, long mask_stride,
                                                        const bf16* __restrict__ wpack, long w_stride,
                                                        const float* __restrict__ bias, long bias_stride, float h,
-                                                       int N, int H, int L) {
+                                                       int N, int H, int L, bf16* __restrict__ xm = nullptr,
+                                                       uint8_t* __restrict__ masks2 = nullptr) {
   using G = Geo<C>;
   constexpr int TW = W + 2, NQ = G::NQ, OT = C / 16, NW = 4, RB = BR;
   static_assert(OT == NW && W == 32, "one 16-channel o-tile per wave, two pixel tiles");
@@ -1041,7 +1045,21 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
   const int n0 = (int)((long)blockIdx.x * N / gridDim.x), n1 = (int)((long)(blockIdx.x + 1) * N / gridDim.x);
   if (n0 >= n1) return;
   const int nb = (H + BR - 1) / BR, per = (n1 - n0) * nb;  // items per block
-  auto src_of = [&](int l) -> const bf16* { return l == 0 ? x0 : ys + (long)(l - 1) * y_stride; };
+  // items walk stages (blocks, or RK2 half steps): block, input, output, mask, step of stage st
+  auto blk_of = [&](int st) { return RK2 ? st >> 1 : st; };
+  auto xin_of = [&](int l) -> const bf16* { return l == 0 ? x0 : ys + (long)(l - 1) * y_stride; };
+  auto src_of = [&](int st) -> const bf16* {
+    if constexpr (RK2) return (st & 1) ? xm + (long)(st >> 1) * y_stride : xin_of(st >> 1);
+    else return xin_of(st);
+  };
+  auto out_of = [&](int st) -> bf16* {
+    if constexpr (RK2) return ((st & 1) ? ys : xm) + (long)(st >> 1) * y_stride;
+    else return ys + (long)st * y_stride;
+  };
+  auto mask_of = [&](int st) -> uint8_t* {
+    uint8_t* m = (RK2 && (st & 1)) ? masks2 : masks;
+    return m ? m + (long)blk_of(st) * mask_stride : nullptr;
+  };
 
   bf16x8 A[G::KS];
   load_A1<C>(wpack, ot, lane, A);
@@ -1072,7 +1090,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
   adv(xl, xn, xb);
   dma_rows<C, W>(x0, lds, cn, -1, min(BR, H) + 2, H, wave, NW, lane);
   int nst = 0;
-  const int total = L * per;
+  const int total = (RK2 ? 2 : 1) * L * per;
   ASR_BCLK(0, 0);
   for (int it = 0; it < total; ++it) {
     const int buf = it & 1;
@@ -1113,6 +1131,13 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
 #pragma unroll
       for (int pt = 0; pt < 2; ++pt) acc[r][pt] = f32x4{bz[0], bz[1], bz[2], bz[3]};
     u32x4 xr[RB];
+    const bool resg = RK2 && (cl & 1);  // second RK2 stage: residual x_l from global memory
+    if (resg) {  // rows past the image end re-read its last row (never stored)
+      const int y0 = cb * BR, rows = min(BR, H - y0);
+      const unsigned char* rb = (const unsigned char*)(xin_of(cl >> 1) + ((long)cn * H + y0) * W * C) + ly;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) xr[r] = *(const u32x4*)(rb + (long)min(r, rows - 1) * W * C * 2);
+    }
 #if ASR_FSTACK_HOOK
     // the DMA pieces of this wave (j = wave + 4u) and the residual reads issued among
     // the conv's MFMAs (a piece issues cheaper there than in a burst after the barrier)
@@ -1121,7 +1146,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
       if constexpr (u < NPW) {
         const int j = wave + NW * u;
         if (j < nrows * IPR) dma_row_instr<C, W>(nxs, ntile, xn, ngy0, j, H, loff);
-      } else {
+      } else if (!resg) {
 #pragma unroll
         for (int r = 0; r < RB; ++r) xr[r] = lds_rd128(tb + lxr + (unsigned)(r * BD::ROWB));
       }
@@ -1131,21 +1156,25 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
 #else
     conv_band<C, W, RB>(tb, lo, A, acc);
     if (wave == 0) ASR_BTR(0, 0, it, 3);
+    if (!resg) {
 #pragma unroll
-    for (int r = 0; r < RB; ++r) xr[r] = lds_rd128(tb + lxr + (unsigned)(r * BD::ROWB));
+      for (int r = 0; r < RB; ++r) xr[r] = lds_rd128(tb + lxr + (unsigned)(r * BD::ROWB));
+    }
 #endif
     const int l = cl;
-    if (xl != cl && it + 1 < total) {  // the next item starts block l+1: its W and bias (L2 hits)
-      load_A1<C>(wpack + (long)xl * w_stride, ot, lane, A);
-      const float* bl = bias ? bias + (long)xl * bias_stride : nullptr;
+    if (blk_of(xl) != blk_of(cl) && it + 1 < total) {  // the next item starts block l+1: its W and bias (L2 hits)
+      load_A1<C>(wpack + (long)blk_of(xl) * w_stride, ot, lane, A);
+      const float* bl = bias ? bias + (long)blk_of(xl) * bias_stride : nullptr;
 #pragma unroll
       for (int e = 0; e < 4; ++e) bz[e] = bl ? bl[o0 + e] : 0.f;
     }
     lgkm_wait<0>();
     const int y0 = cb * BR, rows = min(BR, H - y0);
     const long rowb = ((long)cn * H + y0) * W;
-    unsigned char* yb = (unsigned char*)(ys + (long)l * y_stride + rowb * C) + ly;
-    uint8_t* mb = masks ? masks + (long)l * mask_stride + rowb * (C / 8) + lm : nullptr;
+    unsigned char* yb = (unsigned char*)(out_of(l) + rowb * C) + ly;
+    uint8_t* mb = mask_of(l);
+    if (mb) mb += rowb * (C / 8) + lm;
+    const float hst = (RK2 && !(l & 1)) ? 0.5f * h : h;
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
       if (r >= rows) break;
@@ -1156,7 +1185,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
       static_for<0, 4>([&](auto dc) {
         constexpr int d = decltype(dc)::value;
         const int ra = max(__float_as_int(z[2 * d]), 0), rb = max(__float_as_int(z[2 * d + 1]), 0);
-        yw[d] = pk_bf16(fmaf(h, __int_as_float(ra), lo_f(xr[r][d])), fmaf(h, __int_as_float(rb), hi_f(xr[r][d])));
+        yw[d] = pk_bf16(fmaf(hst, __int_as_float(ra), lo_f(xr[r][d])), fmaf(hst, __int_as_float(rb), hi_f(xr[r][d])));
         bits = d == 0 ? bit01(ra) : lshl_or<2 * d>(bit01(ra), bits);
         bits = lshl_or<2 * d + 1>(bit01(rb), bits);
       });
@@ -3646,6 +3675,12 @@ int block_fwd_mfma(int mode, const void* x, const void* resid, void* y, uint8_t*
   return fail(ASR_E_UNSUPPORTED, "bf16 block: C=%d not supported (16, 32, 64)", C);
 }
 
+// RK2: 2L stages in one launch (k_fwd3_stack<..., RK2>): x_l -> xmid_l (xm + l*y_stride,
+// mask1 at masks + l*mask_stride) -> x_{l+1} (mask2 at masks2 + l*mask_stride)
+int block_stack_fwd_rk2_mfma(const void* x0, void* ys, void* xm, long y_stride, uint8_t* masks, uint8_t* masks2,
+                             long mask_stride, const void* w, long w_stride, const float* bias, long bias_stride,
+                             float h, int N, int H, int W, int C, int L, hipStream_t s);
+
 bool block_stack_fwd_supported(int N, int H, int W, int C) {
   return ASR_FWD_STACK && C == 64 && W == 32 && N >= 1 && (H + kFwdBR - 1) / kFwdBR >= 4;
 }
@@ -3703,6 +3738,23 @@ int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride
                      (bf16*)dbuf1, (const bf16*)xs, x_stride, masks, mask_stride, (const bf16*)w, w_stride, h, two_gamma,
                      N, H, L, ro0, slabs, slab_stride, grp, grp_stride, done, done + L + 2, lfold);
   ASR_LAUNCH_CHECK("k_bwd3_stack");
+  return ASR_OK;
+}
+
+int block_stack_fwd_rk2_mfma(const void* x0, void* ys, void* xm, long y_stride, uint8_t* masks, uint8_t* masks2,
+                             long mask_stride, const void* w, long w_stride, const float* bias, long bias_stride,
+                             float h, int N, int H, int W, int C, int L, hipStream_t s) {
+  if (!block_stack_fwd_supported(N, H, W, C) || L < 1 || !xm)
+    return fail(ASR_E_UNSUPPORTED, "RK2 stack forward: needs C=64, W=32, >= 4 row bands per image");
+  if (y_stride < (long)N * H * W * C) return fail(ASR_E_ARG, "RK2 stack forward: y_stride smaller than one activation");
+  int cus = cu_count();
+  if (cus <= 0) cus = 256;
+  const int grid = std::max(1, std::min(N, 2 * cus));
+  const size_t lds = 2 * (size_t)(kFwdBR + 2) * (W + 2) * C * 2;
+  hipLaunchKernelGGL((blk::k_fwd3_stack<64, 32, kFwdBR, true>), dim3(grid), dim3(256), lds, s, (const bf16*)x0,
+                     (bf16*)ys, y_stride, masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, H, L,
+                     (bf16*)xm, masks2);
+  ASR_LAUNCH_CHECK("k_fwd3_stack<RK2>");
   return ASR_OK;
 }
 

@@ -171,3 +171,29 @@ def test_stack64_backward_abi_matches_per_block_and_oracle(rt, N, L, gamma):
             assert np.abs(dp[l, pm.n_theta:].cpu().numpy() - db_want).max() <= 1e-3 * np.abs(db_want).max()
         dy = dx
     assert torch.equal(dx0, dy)
+
+
+@pytest.mark.parametrize("N,L", [(1, 2), (8, 3), (192, 2)])
+def test_network_rk2_stack_forward_equals_per_block(rt, N, L):
+    """RK2 (BASELINE config 5): all 2L half steps in one k_fwd3_stack<..., RK2> launch
+    (second stage with the residual x_l from global memory) against the per-block
+    asr_rk2 kernels (ASR_VARIANT_PER_BLOCK_FWD): the same band conv and epilogue,
+    so the loss and every gradient are bitwise equal."""
+    C = 64
+    from differential_equations_resnet_amd.netparams import init_net_params
+    dev = torch.device("cuda")
+    params = torch.from_numpy(init_net_params(C, L, 3, 10, seed=8) * 0.5).to(dev)
+    rng = np.random.default_rng(N + L)
+    imgs = torch.from_numpy(rng.integers(0, 256, (N, 32, 32, 3), dtype=np.uint8)).to(dev)
+    tgt = torch.from_numpy(np.eye(10, dtype=np.float32)[rng.integers(0, 10, N)]).to(dev)
+    ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / max(L, 4), 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
+                        dtype="bfloat16", input_u8=True, device=dev, integrator="rk2")
+    loss, g = ex.forward_backward(params, imgs, tgt)
+    loss, g = loss.clone(), g.clone()
+    ex.variant = rt.ASR_VARIANT_PER_BLOCK_FWD
+    loss1, g1 = ex.forward_backward(params, imgs, tgt)
+    ex.variant = 0
+    torch.cuda.synchronize()
+    assert torch.equal(loss, loss1)
+    assert torch.equal(g, g1)
+    assert np.isfinite(loss.item()) and g.abs().max().item() > 0
