@@ -56,7 +56,8 @@ int theta_dst_tile_major(const int32_t* in, long n, int C, int32_t* out, hipStre
 int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride, const uint8_t* masks,
                          long mask_stride, const void* w, long w_stride, float h, float two_gamma, int N, int H, int W,
                          int C, int L, int ro0, float* slabs, long slab_stride, float* grp, long grp_stride,
-                         unsigned* done, int* lfold_out, hipStream_t s);
+                         unsigned* done, int* lfold_out, hipStream_t s, const void* xm = nullptr,
+                         const uint8_t* masks2 = nullptr, void* gbuf = nullptr);
 int block_stack_fwd_mfma(const void* x0, void* ys, long y_stride, uint8_t* masks, long mask_stride, const void* w,
                          long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C, int L,
                          hipStream_t s);
@@ -368,7 +369,7 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.mask_bytes = asr_mask_bytes(c->N, c->H, c->W, C);
   L.fast_stem = stem_supported(c->Cin, c->H, c->W, C);
   L.deep = c->dtype == ASR_BF16 && !L.rk2 && deep16_supported(c->H, c->W, C);
-  L.stack_bwd = c->dtype == ASR_BF16 && !L.rk2 && block_stack_bwd_supported(c->N, c->H, c->W, C);
+  L.stack_bwd = c->dtype == ASR_BF16 && block_stack_bwd_supported(c->N, c->H, c->W, C);
   L.stack_grid = L.stack_bwd ? block_stack_bwd_grid(c->N) : 0;
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -826,12 +827,15 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
     const long ES = L.E + C, sst = (long)grid * ES;
     float* slabs = (float*)(b + L.stack_slabs);
     float* grp = (float*)(b + L.grp);
-    const int ro0 = L.fast_stem && !stem_v1;
+    // (RK2: the first block's first stage has the extra term, so the stem's relu' runs separately)
+    const int ro0 = L.fast_stem && !stem_v1 && !L.rk2;
     int lfold = cfg->L;
-    ASR_TRY(block_stack_bwd_mfma(dcur, dnext, act(0), L.P, (const uint8_t*)(b + L.masks), L.mask_bytes,
-                                 b + (L.sep_bwd ? L.wbuf_bwd : L.wbuf), L.wstride, cfg->h,
-                                 L.sep_bwd ? 0.f : 2.f * cfg->gamma, N, H, W, C, cfg->L, ro0, slabs, sst, grp,
-                                 L.grp_stride, (unsigned*)(b + L.stack_done), &lfold, s));
+    const uint8_t* m1 = (const uint8_t*)(b + L.masks);
+    ASR_TRY(block_stack_bwd_mfma(dcur, dnext, act(0), L.P, m1, L.mask_bytes, b + (L.sep_bwd ? L.wbuf_bwd : L.wbuf),
+                                 L.wstride, cfg->h, L.sep_bwd ? 0.f : 2.f * cfg->gamma, N, H, W, C, cfg->L, ro0, slabs,
+                                 sst, grp, L.grp_stride, (unsigned*)(b + L.stack_done), &lfold, s,
+                                 L.rk2 ? b + L.xmids : nullptr, L.rk2 ? m1 + (size_t)cfg->L * L.mask_bytes : nullptr,
+                                 L.rk2 ? b + L.dxg : nullptr));
     for (int l = std::min(lfold, cfg->L) - 1; l >= 0; --l)  // blocks below lfold: pass 1 after the launch
       ASR_TRY(reduce_slabs_to_groups(slabs + (long)l * sst, grid, ES, grp + (long)l * L.grp_stride, s));
     if (cfg->L & 1) std::swap(dcur, dnext);

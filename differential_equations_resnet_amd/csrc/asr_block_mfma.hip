@@ -2811,7 +2811,12 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
 typedef __attribute__((address_space(1))) unsigned gu32;  // global agent-scope words (never flat)
 typedef __attribute__((address_space(1))) float gf32;
 
-template <int C, int W, int BR>
+// RK2 (config 5): items walk 2L stages, per block l its second stage first
+// (dy = dL/dx_{l+1}, x = xmid_l, mask2, h, no +dy residual: out g = A^T dz2 into
+// gbuf) then its first (dy = g, x = x_l, mask1, h/2, plus the extra term
+// dL/dx_{l+1} by 16-B global loads: out dx_l).  Both stages accumulate one dW:
+// at the stage switch acc *= 2 (exact), and the block's slab is (h/2) acc.
+template <int C, int W, int BR, bool RK2 = false>
 __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0, bf16* __restrict__ dbuf1,
                                                        const bf16* __restrict__ xs, long x_stride,
                                                        const uint8_t* __restrict__ masks, long mask_stride,
@@ -2820,7 +2825,9 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
                                                        float* __restrict__ slabs, long slab_stride,
                                                        float* __restrict__ grp, long grp_stride,
                                                        unsigned* __restrict__ done, unsigned* __restrict__ tmo,
-                                                       int lfold) {
+                                                       int lfold, const bf16* __restrict__ xm = nullptr,
+                                                       const uint8_t* __restrict__ masks2 = nullptr,
+                                                       bf16* __restrict__ gbuf = nullptr) {
   using G = Geo<C>;
   using LL = Bwd2Lds<C, W, BR>;
   using BD = Band<C, W, BR>;
@@ -2843,14 +2850,31 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
     }
   }
   const int n0 = (int)((long)blockIdx.x * N / gridDim.x), n1 = (int)((long)(blockIdx.x + 1) * N / gridDim.x);
-  const int nb = (H + BR - 1) / BR, per = (n1 - n0) * nb, total = L * per;
+  // cursor index l is a STAGE: the block itself (Euler) or 2*block + (1: second RK2 stage, 0: first)
+  constexpr int SPB = RK2 ? 2 : 1;
+  const int nb = (H + BR - 1) / BR, per = (n1 - n0) * nb, total = SPB * L * per;
   const unsigned loff = (unsigned)dma_lane_off<C, W>(lane) * 2u;
-  const float hs = h, hs2g = h * two_gamma;
-  // block l reads dy from dbuf[(L-1-l) & 1] and writes dx to the other one
-  auto dy_of = [&](int l) -> bf16* { return ((L - 1 - l) & 1) ? dbuf1 : dbuf0; };
-  auto dx_of = [&](int l) -> bf16* { return ((L - 1 - l) & 1) ? dbuf0 : dbuf1; };
-  auto x_of = [&](int l) -> const bf16* { return xs + (long)l * x_stride; };
-  auto mask_of = [&](int l) -> const uint8_t* { return masks + (long)l * mask_stride; };
+  auto blk_of = [&](int st) { return RK2 ? st >> 1 : st; };
+  auto s1_of = [&](int st) { return RK2 && !(st & 1); };  // first RK2 stage: h/2, extra term
+  // block l reads dL/dx_{l+1} from dbuf[(L-1-l) & 1] and writes dL/dx_l to the other one
+  auto din_of = [&](int l) -> bf16* { return ((L - 1 - l) & 1) ? dbuf1 : dbuf0; };
+  auto dout_of = [&](int l) -> bf16* { return ((L - 1 - l) & 1) ? dbuf0 : dbuf1; };
+  auto dy_of = [&](int st) -> bf16* {
+    if constexpr (RK2) return (st & 1) ? din_of(st >> 1) : gbuf;
+    else return din_of(st);
+  };
+  auto dx_of = [&](int st) -> bf16* {
+    if constexpr (RK2) return (st & 1) ? gbuf : dout_of(st >> 1);
+    else return dout_of(st);
+  };
+  auto x_of = [&](int st) -> const bf16* {
+    if constexpr (RK2) return ((st & 1) ? xm : xs) + (long)(st >> 1) * x_stride;
+    else return xs + (long)st * x_stride;
+  };
+  auto mask_of = [&](int st) -> const uint8_t* {
+    if constexpr (RK2) return ((st & 1) ? masks2 : masks) + (long)(st >> 1) * mask_stride;
+    else return masks + (long)st * mask_stride;
+  };
   // (block, image, band) cursor, blocks last to first
   struct Cur {
     int l, n, b;
@@ -2880,7 +2904,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
     const unsigned lch = (unsigned)toff<C>(1, px + 1, cg, TW);
     const unsigned ldx = (unsigned)(px * C + 8 * cg) * 2u;
     int nst = 0;
-    Cur cur{L - 1, n0, 0};
+    Cur cur{SPB * L - 1, n0, 0};
     for (int it = 0; it < total; ++it) {
       const int buf = it & 1;
       const int n = cur.n, y0 = cur.b * BR, l = cur.l;
@@ -2890,42 +2914,64 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       if (wave == 0) ASR_BTR(1, 0, it, 1);
       const unsigned dzt = lds_u32(lds + LL::DZ + buf * LL::TILE), dyt = lds_u32(lds + LL::DY + buf * LL::TILE);
       const unsigned xt = lds_u32(lds + LL::X + buf * LL::TILE);
+      const bool s1 = s1_of(l);
+      const float hs = s1 ? 0.5f * h : h, hs2g = hs * two_gamma;
+      // RK2 first stage: the extra dx term dL/dx_{l+1} of the band's rows (in flight during the conv)
+      u32x4 exv[RK2 ? BR : 1];
+      if (RK2 && s1) {
+        const bf16* eb = din_of(blk_of(l)) + ((long)n * H + y0) * W * C;
+#pragma unroll
+        for (int r = 0; r < (RK2 ? BR : 1); ++r)
+          exv[r] = *(const u32x4*)((const unsigned char*)(eb + (long)min(r, rows - 1) * W * C) + ldx);
+      }
       f32x4 acc[BR][2];
 #pragma unroll
       for (int r = 0; r < BR; ++r) acc[r][0] = acc[r][1] = f32x4{0.f, 0.f, 0.f, 0.f};
       conv_band<C, W, BR>(dzt, lo, A, acc);
       if (wave == 0) ASR_BTR(1, 0, it, 2);
-      const bool last_of_block = cur.b == nb - 1 && n == n1 - 1;
-      if (last_of_block && l > 0) load_A1<C>(wpack + (long)(l - 1) * w_stride, ot, lane, A);
+      const bool last_of_stage = cur.b == nb - 1 && n == n1 - 1;
+      if (last_of_stage && blk_of(l) > 0 && (!RK2 || s1))
+        load_A1<C>(wpack + (long)(blk_of(l) - 1) * w_stride, ot, lane, A);
       bf16* drow = dx_of(l) + ((long)n * H + y0) * W * C;
       int nld = 0;
-      auto epilogue = [&](auto g2c, auto roc) {
+      auto epilogue = [&](auto g2c, auto roc, auto kc) {
+        // KIND 0: Euler (+dy), 1: second RK2 stage (no +dy), 2: first RK2 stage (+dy +extra)
         constexpr bool G2 = decltype(g2c)::value, RO = decltype(roc)::value;
-        constexpr int NR = 1 + (G2 ? 1 : 0) + (RO ? 1 : 0);  // LDS reads per row
+        constexpr int KIND = decltype(kc)::value;
+        constexpr bool RDY = KIND != 1;
+        constexpr int NR = (RDY ? 1 : 0) + (G2 ? 1 : 0) + (RO ? 1 : 0);  // LDS reads per row
         u32x4 dyw[2], dzw[2], xw[2];
         auto issue = [&](int r, int sl) {
           const unsigned co = lch + (unsigned)(r * LL::ROWB);
-          dyw[sl] = lds_rd128(dyt + co);
+          if constexpr (RDY) dyw[sl] = lds_rd128(dyt + co);
           if constexpr (G2) dzw[sl] = lds_rd128(dzt + co);
           if constexpr (RO) xw[sl] = lds_rd128(xt + co);
         };
-        issue(0, 0);
+        if constexpr (NR > 0) issue(0, 0);
         static_for<0, BR>([&](auto rc) {
           constexpr int r = decltype(rc)::value, sl = r & 1;
           if (r < rows) {
-            if (r + 1 < rows) {
-              issue(r + 1, sl ^ 1);
-              lgkm_wait<NR>();
-            } else {
-              lgkm_wait<0>();
+            if constexpr (NR > 0) {
+              if (r + 1 < rows) {
+                issue(r + 1, sl ^ 1);
+                lgkm_wait<NR>();
+              } else {
+                lgkm_wait<0>();
+              }
             }
             float z[8];
             regroup(acc[r][0], acc[r][1], z);
             u32x4 ow;
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
-              float v0 = fmaf(-hs, z[2 * d], lo_f(dyw[sl][d]));
-              float v1 = fmaf(-hs, z[2 * d + 1], hi_f(dyw[sl][d]));
+              float r0 = 0.f, r1 = 0.f;
+              if constexpr (RDY) r0 = lo_f(dyw[sl][d]), r1 = hi_f(dyw[sl][d]);
+              if constexpr (KIND == 2) {
+                r0 += lo_f(exv[RK2 ? r : 0][d]);
+                r1 += hi_f(exv[RK2 ? r : 0][d]);
+              }
+              float v0 = fmaf(-hs, z[2 * d], r0);
+              float v1 = fmaf(-hs, z[2 * d + 1], r1);
               if constexpr (G2) {
                 v0 = fmaf(hs2g, lo_f(dzw[sl][d]), v0);
                 v1 = fmaf(hs2g, hi_f(dzw[sl][d]), v1);
@@ -2943,13 +2989,27 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       };
       using T_ = std::true_type;
       using F_ = std::false_type;
-      const bool g2 = hs2g != 0.f, ro = ro0 && l == 0;
-      if (ro) {
-        if (g2) epilogue(T_{}, T_{});
-        else epilogue(F_{}, T_{});
+      using K0 = std::integral_constant<int, 0>;
+      using K1 = std::integral_constant<int, 1>;
+      using K2 = std::integral_constant<int, 2>;
+      const bool g2 = hs2g != 0.f;
+      if constexpr (RK2) {
+        if (s1) {
+          if (g2) epilogue(T_{}, F_{}, K2{});
+          else epilogue(F_{}, F_{}, K2{});
+        } else {
+          if (g2) epilogue(T_{}, F_{}, K1{});
+          else epilogue(F_{}, F_{}, K1{});
+        }
       } else {
-        if (g2) epilogue(T_{}, F_{});
-        else epilogue(F_{}, F_{});
+        const bool ro = ro0 && l == 0;
+        if (ro) {
+          if (g2) epilogue(T_{}, T_{}, K0{});
+          else epilogue(F_{}, T_{}, K0{});
+        } else {
+          if (g2) epilogue(T_{}, F_{}, K0{});
+          else epilogue(F_{}, F_{}, K0{});
+        }
       }
       nst = nld;
       if (wave == 0) ASR_BTR(1, 0, it, 3);
@@ -3057,8 +3117,9 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       }
       fold = false;
     };
+    const float hsb = RK2 ? 0.5f * h : h;  // the slab scale (RK2: acc doubled at the stage switch)
     {  // prologue: own dy rows and x rows of item 0, its dz converted
-      const Cur c0{L - 1, n0, 0};
+      const Cur c0{SPB * L - 1, n0, 0};
       unsigned mw0 = 0u;
       const int row0 = own_row(false);
       stage_own(c0, row0, 0, mw0);
@@ -3067,13 +3128,13 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       vm_wait(0);
       convert_own(row0, 0, mw0);
     }
-    Cur cur{L - 1, n0, 0}, nxt{L - 1, n0, 0};
+    Cur cur{SPB * L - 1, n0, 0}, nxt{SPB * L - 1, n0, 0};
     adv(nxt);
     for (int it = 0; it < total; ++it) {
       const int buf = it & 1;
-      const int y0 = cur.b * BR, l = cur.l;
+      const int y0 = cur.b * BR, l = blk_of(cur.l);  // (l: the block)
       const int rows = min(BR, H - y0);
-      const bool first_of_block = cur.b == 0 && cur.n == n0;
+      const bool first_of_block = cur.b == 0 && cur.n == n0 && (!RK2 || (cur.l & 1));
       if (wave == 4) ASR_BTR(1, 1, it, 0);
       if (first_of_block && l + 2 < L && l + 2 >= lfold && w8 == 0 && lane == 0) {
         // block l+2's slabs: every workgroup published them (bounded poll)
@@ -3197,8 +3258,14 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
           ++fp;
           foff += ES;
         }
-      const bool last_of_block = cur.b == nb - 1 && cur.n == n1 - 1;
-      if (last_of_block && (!(ASR_STACK_ABLATE & 1) || hs == -1.f)) {  // (ablation: never, but kept live)
+      const bool last_of_stage = cur.b == nb - 1 && cur.n == n1 - 1;
+      const bool last_of_block = last_of_stage && !(RK2 && (cur.l & 1));
+      if (RK2 && last_of_stage && (cur.l & 1)) {  // second -> first RK2 stage of the block: acc *= 2 (exact)
+#pragma unroll
+        for (int mi = 0; mi < MTW; ++mi) acc[mi][0] *= 2.f, acc[mi][1] *= 2.f;
+        accb[0] *= 2.f, accb[1] *= 2.f;
+      }
+      if (last_of_block && (!(ASR_STACK_ABLATE & 1) || hsb == -1.f)) {  // (ablation: never, but kept live)
         if (l + 2 < L && l + 2 >= lfold) fold_end(l + 2);
         // publish block l's dW tiles and db (write-through; drained at the next band barrier)
         float* slab = slabs + (long)l * slab_stride + (long)blockIdx.x * ES;
@@ -3208,7 +3275,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
 #pragma unroll
           for (int oi = 0; oi < 2; ++oi) {
             const int mt = tg * MTW + mi;
-            f32x4 v = acc[mi][oi] * hs;
+            f32x4 v = acc[mi][oi] * hsb;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs,
                                                    (((mt * 4 + oq + oi) * 64 + lane) * 4) * 4, 0, 16);
             acc[mi][oi] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -3217,7 +3284,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
           if (g == 0) {
 #pragma unroll
             for (int oi = 0; oi < 2; ++oi)
-              __hip_atomic_store((gf32*)(slab + 9 * C * C + 16 * (oq + oi) + lx), hs * accb[oi][0], __ATOMIC_RELAXED,
+              __hip_atomic_store((gf32*)(slab + 9 * C * C + 16 * (oq + oi) + lx), hsb * accb[oi][0], __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
           }
           accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -3723,7 +3790,8 @@ int block_stack_bwd_grid(int N) {
 int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride, const uint8_t* masks,
                          long mask_stride, const void* w, long w_stride, float h, float two_gamma, int N, int H, int W,
                          int C, int L, int ro0, float* slabs, long slab_stride, float* grp, long grp_stride,
-                         unsigned* done, int* lfold_out, hipStream_t s) {
+                         unsigned* done, int* lfold_out, hipStream_t s, const void* xm, const uint8_t* masks2,
+                         void* gbuf) {
   if (!block_stack_bwd_supported(N, H, W, C) || L < 1)
     return fail(ASR_E_UNSUPPORTED, "stack backward: needs C=64, W=32, >= 4 row bands per image (C=%d W=%d H=%d)", C, W, H);
   const int grid = block_stack_bwd_grid(N);
@@ -3734,9 +3802,18 @@ int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride
   if (lfold_out) *lfold_out = lfold;
   ASR_TRY(hip_check(hipMemsetAsync(done, 0, align_up((size_t)(L + 4) * 4, 16), s), "hipMemsetAsync"));
   using L2 = blk::Bwd2Lds<64, 32, kBwdBR>;
-  hipLaunchKernelGGL((blk::k_bwd3_stack<64, 32, kBwdBR>), dim3(grid), dim3(768), (size_t)L2::TOTAL, s, (bf16*)dbuf0,
-                     (bf16*)dbuf1, (const bf16*)xs, x_stride, masks, mask_stride, (const bf16*)w, w_stride, h, two_gamma,
-                     N, H, L, ro0, slabs, slab_stride, grp, grp_stride, done, done + L + 2, lfold);
+  if (xm) {  // RK2: both stages of every block (x_mid stack at xm, stride x_stride; masks2; g scratch)
+    if (!masks2 || !gbuf) return fail(ASR_E_ARG, "stack backward (RK2): masks2 and the g buffer are required");
+    hipLaunchKernelGGL((blk::k_bwd3_stack<64, 32, kBwdBR, true>), dim3(grid), dim3(768), (size_t)L2::TOTAL, s,
+                       (bf16*)dbuf0, (bf16*)dbuf1, (const bf16*)xs, x_stride, masks, mask_stride, (const bf16*)w,
+                       w_stride, h, two_gamma, N, H, L, 0, slabs, slab_stride, grp, grp_stride, done, done + L + 2,
+                       lfold, (const bf16*)xm, masks2, (bf16*)gbuf);
+  } else {
+    hipLaunchKernelGGL((blk::k_bwd3_stack<64, 32, kBwdBR>), dim3(grid), dim3(768), (size_t)L2::TOTAL, s,
+                       (bf16*)dbuf0, (bf16*)dbuf1, (const bf16*)xs, x_stride, masks, mask_stride, (const bf16*)w,
+                       w_stride, h, two_gamma, N, H, L, ro0, slabs, slab_stride, grp, grp_stride, done, done + L + 2,
+                       lfold);
+  }
   ASR_LAUNCH_CHECK("k_bwd3_stack");
   return ASR_OK;
 }

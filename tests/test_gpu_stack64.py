@@ -197,3 +197,42 @@ def test_network_rk2_stack_forward_equals_per_block(rt, N, L):
     assert torch.equal(loss, loss1)
     assert torch.equal(g, g1)
     assert np.isfinite(loss.item()) and g.abs().max().item() > 0
+
+
+@pytest.mark.parametrize("N,L,gamma", [(512, 4, 0.0), (8, 3, -0.1), (1, 2, 0.0), (192, 5, 0.0)])
+def test_network_rk2_stack_backward_equals_per_block(rt, N, L, gamma):
+    """RK2 backward of all blocks in one k_bwd3_stack<..., RK2> launch (per block:
+    the second stage without the +dy residual into g, then the first stage with
+    h/2 and the extra term; one dW accumulation per block, doubled at the stage
+    switch, slab = (h/2) acc) against two k_bwd3 launches per block
+    (ASR_VARIANT_PER_BLOCK_BWD; the first stage adds onto the second's slab).
+    dx is the same arithmetic: loss, stem and head gradients bitwise; block
+    gradients sum the same products in another order: 1e-5 of max|g| per block."""
+    C = 64
+    from differential_equations_resnet_amd.netparams import init_net_params
+    dev = torch.device("cuda")
+    ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / max(L, 4), gamma, subtract_mean=127.5, divide_by_stddev=127.5,
+                        dtype="bfloat16", input_u8=True, device=dev, integrator="rk2")
+    params = torch.from_numpy(init_net_params(C, L, 3, 10, seed=6) * 0.5).to(dev)
+    rng = np.random.default_rng(N + 7 * L)
+    imgs = torch.from_numpy(rng.integers(0, 256, (N, 32, 32, 3), dtype=np.uint8)).to(dev)
+    tgt = torch.from_numpy(np.eye(10, dtype=np.float32)[rng.integers(0, 10, N)]).to(dev)
+    loss, g = ex.forward_backward(params, imgs, tgt)
+    loss, g = loss.clone(), g.clone()
+    loss2, g2 = ex.forward_backward(params, imgs, tgt)
+    assert torch.equal(g, g2), "RK2 stack backward is not deterministic"
+    ex.variant = rt.ASR_VARIANT_PER_BLOCK_BWD
+    loss1, g1 = ex.forward_backward(params, imgs, tgt)
+    ex.variant = 0
+    torch.cuda.synchronize()
+    assert torch.equal(loss, loss1)
+    a, b = g.cpu().numpy(), g1.cpu().numpy()
+    n_blk = (ex.n_params - (9 * 3 * C + C) - (C * 10 + 10)) // L
+    stem, head = 9 * 3 * C + C, C * 10 + 10
+    assert np.array_equal(a[:stem], b[:stem]), np.abs(a[:stem] - b[:stem]).max()
+    assert np.array_equal(a[-head:], b[-head:])
+    for l in range(L):
+        o = stem + l * n_blk
+        ga, gb = a[o:o + n_blk], b[o:o + n_blk]
+        assert np.abs(gb).max() > 0
+        assert np.abs(ga - gb).max() <= 1e-5 * np.abs(gb).max(), (l, np.abs(ga - gb).max(), np.abs(gb).max())
