@@ -432,6 +432,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     elapsed = distributed.max_over_ranks(elapsed)
+    ex.check_status()  # blocking, after the timed region: the stacked backward's slab hand-off completed
     final_loss = float(loss.item())
     live = distributed.max_over_ranks(-live_fraction())  # min over ranks
     live = -live

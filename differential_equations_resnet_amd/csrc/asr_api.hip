@@ -778,6 +778,20 @@ int asr_net_forward(const asr_net_config* cfg, const float* params, const void* 
   return ASR_OK;
 }
 
+int asr_net_check_status(const asr_net_config* cfg, const void* ws, size_t ws_bytes, asr_stream_t stream) {
+  ASR_TRY(net_check(cfg));
+  const NetLayout L = net_layout(cfg);
+  if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_net_check_status: workspace too small");
+  if (!L.stack_bwd) return ASR_OK;
+  ASR_TRY(hip_check(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize"));
+  unsigned tmo = 0;  // done[L + 2]: the stack backward's timeout word
+  ASR_TRY(hip_check(hipMemcpy(&tmo, (const unsigned char*)ws + L.stack_done + (size_t)(cfg->L + 2) * 4, 4,
+                              hipMemcpyDeviceToHost),
+                    "hipMemcpy"));
+  if (tmo) return fail(ASR_E_DEVICE, "stacked backward: a workgroup timed out waiting for the slab hand-off");
+  return ASR_OK;
+}
+
 int asr_net_forward_backward(const asr_net_config* cfg, const float* params, const void* images, const float* targets,
                              float* grads, float* loss, float* probs, void* ws, size_t ws_bytes,
                              asr_stream_t stream) {

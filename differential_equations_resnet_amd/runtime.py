@@ -346,6 +346,11 @@ class NetExecutor:
         """Select ASR_VARIANT_* kernel compositions for later calls (tests)."""
         self.cfg.variant = int(bits)
 
+    def check_status(self):
+        """Blocking: raises if the last forward_backward's in-launch slab hand-off
+        (the C=64 stacked backward) timed out (asr_net_check_status)."""
+        _lib.call("asr_net_check_status", ct.byref(self.cfg), _p(self.ws), self.ws_bytes, _stream())
+
     def forward_backward(self, params, images, targets, want_probs=False):
         self._check_inputs(params, images)
         if tuple(targets.shape) != (self.cfg.N, self.cfg.num_classes) or targets.dtype != torch.float32:

@@ -258,6 +258,11 @@ int asr_net_forward(const asr_net_config* cfg, const float* params, const void* 
 int asr_net_forward_backward(const asr_net_config* cfg, const float* params, const void* images,
                              const float* targets, float* grads, float* loss, float* probs,
                              void* ws, size_t ws_bytes, asr_stream_t stream);
+/* Host, blocking (synchronises the stream): ASR_OK, or ASR_E_DEVICE when the
+ * last asr_net_forward_backward on this workspace stopped waiting for another
+ * workgroup's weight-gradient slabs (the bounded in-launch hand-off of the
+ * C=64 stacked backward timed out: its block gradients are then incomplete). */
+int asr_net_check_status(const asr_net_config* cfg, const void* ws, size_t ws_bytes, asr_stream_t stream);
 
 /* tf.train.AdamOptimizer.apply_gradients (training.py:300-301), TF1
  * epsilon-hat form; step is the 1-based update count; g is multiplied by

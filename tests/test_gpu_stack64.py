@@ -113,6 +113,7 @@ def test_network_stack_backward_equals_per_block(rt, N, L, gamma, kind, anti):
     loss, g = ex.forward_backward(params, imgs, tgt)
     loss, g = loss.clone(), g.clone()
     loss2, g2 = ex.forward_backward(params, imgs, tgt)
+    ex.check_status()  # the in-launch slab hand-off did not time out
     assert torch.equal(g, g2), "stack backward is not deterministic"
     ex.variant = rt.ASR_VARIANT_PER_BLOCK_BWD
     loss1, g1 = ex.forward_backward(params, imgs, tgt)
@@ -220,6 +221,7 @@ def test_network_rk2_stack_backward_equals_per_block(rt, N, L, gamma):
     loss, g = ex.forward_backward(params, imgs, tgt)
     loss, g = loss.clone(), g.clone()
     loss2, g2 = ex.forward_backward(params, imgs, tgt)
+    ex.check_status()
     assert torch.equal(g, g2), "RK2 stack backward is not deterministic"
     ex.variant = rt.ASR_VARIANT_PER_BLOCK_BWD
     loss1, g1 = ex.forward_backward(params, imgs, tgt)
