@@ -221,7 +221,7 @@ def block_roofline(rt, lib, C, N, dtype_name, reps, h, integrator="euler"):
                 bytes_fwd=fb * P * esz, bytes_bwd=bb * P * esz, timing=timing_mode[0])
 
 
-def stack_roofline(rt, N, L, reps, h, C=16):
+def stack_roofline(rt, N, L, reps, h, C=16, rk2=False):
     """The network's block path at the workload shape: all L Euler blocks in
     one forward and one backward launch (C=16: asr_deep16.hip, every image
     resident in LDS; C=64: k_fwd3_stack / k_bwd3_stack, whole images per
@@ -233,7 +233,9 @@ def stack_roofline(rt, N, L, reps, h, C=16):
     backward needs them): s·P + L·(s·P + P/8); backward reads every x_l and
     mask, dL/dx_L, and writes dx_0: L·(s·P + P/8) + 2·s·P (P = 32·32·16, s = 2 B).
     C=64: the survey's per-block unit 5·P·s (forward x, y; backward dy, x, dx),
-    times L: x_l is re-read from HBM by every block there."""
+    times L: x_l is re-read from HBM by every block there.  RK2 (config 5,
+    asr_rk2_stack_forward / _backward): the RK2 block unit 12·P·s (forward 5
+    passes: x, x_mid written and read, x again as the residual, y; backward 7)."""
     import torch
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(7)
@@ -257,14 +259,31 @@ def stack_roofline(rt, N, L, reps, h, C=16):
     s = torch.cuda.current_stream().cuda_stream
     per = w[0].numel()
 
-    def fwd():  # writes x_1 .. x_L behind x_0 and the L masks
-        _lib.call("asr_block_stack_forward", xs[0].data_ptr(), xs[1].data_ptr(), N * P, masks.data_ptr(), mb,
-                  w.data_ptr(), per, bias.data_ptr(), C, float(h), N, 32, 32, C, L, rt.ASR_BF16, 1, s)
+    if rk2:
+        xm = torch.empty((L, N, 32, 32, C), dtype=torch.bfloat16, device=dev)
+        masks2 = torch.empty((L, mb), dtype=torch.uint8, device=dev)
+        wsb = int(_lib.load().asr_rk2_stack_backward_workspace_bytes(N, 32, 32, C, L, rt.ASR_BF16))
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
 
-    def bwd():  # incl. the slab reduction and projection onto theta
-        _lib.call("asr_block_stack_backward", dyL.data_ptr(), xs.data_ptr(), N * P, masks.data_ptr(), mb,
-                  w.data_ptr(), per, theta_dst.data_ptr(), pm.n_theta, float(h), 0.0, N, 32, 32, C, L,
-                  rt.ASR_BF16, dx0.data_ptr(), dparams.data_ptr(), ws.data_ptr(), wsb, s)
+        def fwd():  # x_1 .. x_L behind x_0, the L x_mid and both masks of every block
+            _lib.call("asr_rk2_stack_forward", xs[0].data_ptr(), xs[1].data_ptr(), xm.data_ptr(), N * P,
+                      masks.data_ptr(), masks2.data_ptr(), mb, w.data_ptr(), per, bias.data_ptr(), C, float(h), N, 32,
+                      32, C, L, rt.ASR_BF16, s)
+
+        def bwd():
+            _lib.call("asr_rk2_stack_backward", dyL.data_ptr(), xs.data_ptr(), xm.data_ptr(), N * P,
+                      masks.data_ptr(), masks2.data_ptr(), mb, w.data_ptr(), per, theta_dst.data_ptr(), pm.n_theta,
+                      float(h), 0.0, N, 32, 32, C, L, rt.ASR_BF16, dx0.data_ptr(), dparams.data_ptr(), ws.data_ptr(),
+                      wsb, s)
+    else:
+        def fwd():  # writes x_1 .. x_L behind x_0 and the L masks
+            _lib.call("asr_block_stack_forward", xs[0].data_ptr(), xs[1].data_ptr(), N * P, masks.data_ptr(), mb,
+                      w.data_ptr(), per, bias.data_ptr(), C, float(h), N, 32, 32, C, L, rt.ASR_BF16, 1, s)
+
+        def bwd():  # incl. the slab reduction and projection onto theta
+            _lib.call("asr_block_stack_backward", dyL.data_ptr(), xs.data_ptr(), N * P, masks.data_ptr(), mb,
+                      w.data_ptr(), per, theta_dst.data_ptr(), pm.n_theta, float(h), 0.0, N, 32, 32, C, L,
+                      rt.ASR_BF16, dx0.data_ptr(), dparams.data_ptr(), ws.data_ptr(), wsb, s)
 
     fwd()
     bwd()
@@ -284,9 +303,11 @@ def stack_roofline(rt, N, L, reps, h, C=16):
     if C == 16:
         act = L * (2 * P + P // 8)
         bytes_fwd, bytes_bwd = N * (2 * P + act), N * (act + 4 * P)
+    elif rk2:
+        bytes_fwd, bytes_bwd = N * L * 5 * 2 * P, N * L * 7 * 2 * P
     else:
         bytes_fwd, bytes_bwd = N * L * 2 * 2 * P, N * L * 3 * 2 * P
-    flops = 3 * 2 * 9 * C * C * 32 * 32 * N * L
+    flops = (2 if rk2 else 1) * 3 * 2 * 9 * C * C * 32 * 32 * N * L
     return dict(t_fwd=tf, t_bwd=tb, t=tf + tb, bytes=bytes_fwd + bytes_bwd, flops=flops, bytes_fwd=bytes_fwd,
                 bytes_bwd=bytes_bwd)
 
@@ -440,9 +461,10 @@ def main():
 
     if rank == 0:
         # the network's fused-stack paths (C=16 LDS-resident, C=64 whole images per workgroup)
-        deep = C in (16, 64) and dtype_name == "bfloat16" and integrator == "euler"
+        deep = dtype_name == "bfloat16" and ((C in (16, 64) and integrator == "euler") or
+                                             (C == 64 and integrator == "rk2"))
         if deep:
-            rb = stack_roofline(rt, N, L, max(2, args.block_reps // 10), h, C)
+            rb = stack_roofline(rt, N, L, max(2, args.block_reps // 10), h, C, rk2=integrator == "rk2")
         else:
             rb = block_roofline(rt, lib, C, N, dtype_name, args.block_reps, h, integrator)
         achieved = rb["bytes"] / rb["t"] / 1e9
@@ -453,6 +475,9 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": ("fused stack of all L Euler blocks, fwd + bwd (deep::k_fwd16_fused, deep::k_bwd16_fused, "
                            "k_reduce_slabs, k_project_layers)" if deep and C == 16 else
+                           "all L RK2 blocks (2L stages) in one forward and one backward launch "
+                           "(blk::k_fwd3_stack<RK2>, blk::k_bwd3_stack<RK2>; k_reduce_slabs for blocks 0-1, "
+                           "k_sum_groups, k_project_layers)" if deep and integrator == "rk2" else
                            "all L Euler blocks in one forward and one backward launch (blk::k_fwd3_stack, "
                            "blk::k_bwd3_stack with pass 1 of the slab reduction in-launch; k_reduce_slabs for "
                            "blocks 0-1, k_sum_groups, k_project_layers)" if deep else

@@ -94,6 +94,10 @@ SIGNATURES = [
     ("asr_net_forward", _I, [ct.POINTER(NetConfig), _P, _P, _P, _P, _S, _P]),
     ("asr_net_forward_backward", _I, [ct.POINTER(NetConfig), _P, _P, _P, _P, _P, _P, _P, _S, _P]),
     ("asr_net_check_status", _I, [ct.POINTER(NetConfig), _P, _S, _P]),
+    ("asr_rk2_stack_forward", _I, [_P, _P, _P, _L, _P, _P, _L, _P, _L, _P, _L, _F, _I, _I, _I, _I, _I, _I, _P]),
+    ("asr_rk2_stack_backward_workspace_bytes", _S, [_I, _I, _I, _I, _I, _I]),
+    ("asr_rk2_stack_backward", _I, [_P, _P, _P, _L, _P, _P, _L, _P, _L, _P, _L, _F, _F, _I, _I, _I, _I, _I, _I, _P,
+                                    _P, _P, _S, _P]),
     ("asr_adam_update", _I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _L, _F, _P]),
     ("asr_segment_sq_norms", _I, [_P, _P, _I, _P, _P]),
     ("asr_batch_metrics", _I, [_P, _P, _P, _I, _I, _P, _P]),

@@ -546,15 +546,15 @@ int asr_block_stack_forward(const void* x0, void* ys, long y_stride, uint8_t* ma
 // workspace of asr_block_stack_backward: two dx buffers, then either the
 // fused path's slabs + group rows or one per-block backward workspace
 struct StackWs {
-  size_t da, db, slabs, grp, blk, done, tdst, total;
+  size_t da, db, slabs, grp, blk, done, tdst, g, total;
   bool deep, stack64;
   int grid;
 };
-static StackWs stack_ws_layout(int N, int H, int W, int C, int L, int dtype) {
+static StackWs stack_ws_layout(int N, int H, int W, int C, int L, int dtype, bool rk2 = false) {
   StackWs w{};
   const size_t act = align_up((size_t)N * H * W * C * (dtype == ASR_BF16 ? 2 : 4), 256);
   const long ES = 9L * C * C + C;
-  w.deep = dtype == ASR_BF16 && deep16_supported(H, W, C);
+  w.deep = !rk2 && dtype == ASR_BF16 && deep16_supported(H, W, C);
   w.stack64 = dtype == ASR_BF16 && !w.deep && block_stack_bwd_supported(N, H, W, C);
   w.grid = w.stack64 ? block_stack_bwd_grid(N) : 0;
   size_t off = 0;
@@ -576,6 +576,10 @@ static StackWs stack_ws_layout(int N, int H, int W, int C, int L, int dtype) {
     off += align_up((size_t)(L + 4) * 4, 256);
     w.tdst = off;
     off += align_up((size_t)2 * 9 * C * C * 4, 256);
+    if (rk2) {  // the gradient reaching x_mid between a block's two stages
+      w.g = off;
+      off += act;
+    }
   } else {
     w.blk = off;
     off += bwd_ws_layout(N, H, W, C, dtype).total;
@@ -654,6 +658,60 @@ int asr_block_stack_backward(const void* dyL, const void* xs, long x_stride, con
                                theta_dst, n_theta, h, gamma, N, H, W, C, dtype, dnext, dp, dp ? dp + n_theta : nullptr,
                                nullptr, base + Lw.blk, s));
     dcur = dnext;
+  }
+  return ASR_OK;
+}
+
+int asr_rk2_stack_forward(const void* x0, void* ys, void* xmids, long y_stride, uint8_t* masks1, uint8_t* masks2,
+                          long mask_stride, const void* w, long w_stride, const float* bias, long bias_stride, float h,
+                          int N, int H, int W, int C, int L, int dtype, asr_stream_t stream) {
+  ASR_TRY(check_shape(N, H, W, C));
+  if (!x0 || !ys || !xmids || !w || L < 1) return fail(ASR_E_ARG, "asr_rk2_stack_forward: null pointer or L < 1");
+  if (dtype != ASR_BF16 || !block_stack_fwd_supported(N, H, W, C))
+    return fail(ASR_E_UNSUPPORTED, "asr_rk2_stack_forward: bf16, C=64, W=32 only (C=%d W=%d)", C, W);
+  if ((masks1 == nullptr) != (masks2 == nullptr)) return fail(ASR_E_ARG, "asr_rk2_stack_forward: masks1/masks2");
+  return block_stack_fwd_rk2_mfma(x0, ys, xmids, y_stride, masks1, masks2, mask_stride, w, w_stride, bias,
+                                  bias_stride, h, N, H, W, C, L, (hipStream_t)stream);
+}
+
+size_t asr_rk2_stack_backward_workspace_bytes(int N, int H, int W, int C, int L, int dtype) {
+  if (check_shape(N, H, W, C) != ASR_OK || L < 1) return 0;
+  const StackWs w = stack_ws_layout(N, H, W, C, L, dtype, true);
+  return w.stack64 ? w.total : 0;
+}
+
+int asr_rk2_stack_backward(const void* dyL, const void* xs, const void* xmids, long x_stride, const uint8_t* masks1,
+                           const uint8_t* masks2, long mask_stride, const void* w, long w_stride,
+                           const int32_t* theta_dst, long n_theta, float h, float gamma, int N, int H, int W, int C,
+                           int L, int dtype, void* dx0, float* dparams, void* ws, size_t ws_bytes,
+                           asr_stream_t stream) {
+  ASR_TRY(check_shape(N, H, W, C));
+  if (!dyL || !xs || !xmids || !masks1 || !masks2 || !w || !dx0 || L < 1)
+    return fail(ASR_E_ARG, "asr_rk2_stack_backward: null pointer");
+  if (dparams && !theta_dst) return fail(ASR_E_ARG, "asr_rk2_stack_backward: theta_dst needed for dparams");
+  const StackWs Lw = stack_ws_layout(N, H, W, C, L, dtype, true);
+  if (!Lw.stack64) return fail(ASR_E_UNSUPPORTED, "asr_rk2_stack_backward: bf16, C=64, W=32 only (C=%d W=%d)", C, W);
+  if (!ws || ws_bytes < Lw.total) return fail(ASR_E_WORKSPACE, "asr_rk2_stack_backward: workspace too small");
+  if (n_theta > 9L * C * C) return fail(ASR_E_ARG, "asr_rk2_stack_backward: n_theta > 9*C*C");
+  hipStream_t s = (hipStream_t)stream;
+  unsigned char* base = (unsigned char*)ws;
+  const size_t act = (size_t)N * H * W * C * 2;
+  const long E = 9L * C * C, ES = E + C, sst = (long)Lw.grid * ES, gst = (long)reduce_groups(Lw.grid) * ES;
+  ASR_TRY(hip_check(hipMemcpyAsync(base + Lw.da, dyL, act, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync"));
+  float* slabs = (float*)(base + Lw.slabs);
+  float* grp = (float*)(base + Lw.grp);
+  int lfold = L;
+  ASR_TRY(block_stack_bwd_mfma(base + Lw.da, base + Lw.db, xs, x_stride, masks1, mask_stride, w, w_stride, h,
+                               2.f * gamma, N, H, W, C, L, 0, slabs, sst, grp, gst, (unsigned*)(base + Lw.done),
+                               &lfold, s, xmids, masks2, base + Lw.g));
+  ASR_TRY(hip_check(hipMemcpyAsync(dx0, base + ((L & 1) ? Lw.db : Lw.da), act, hipMemcpyDeviceToDevice, s),
+                    "hipMemcpyAsync"));
+  if (dparams) {
+    for (int l = std::min(lfold, L) - 1; l >= 0; --l)
+      ASR_TRY(reduce_slabs_to_groups(slabs + (long)l * sst, Lw.grid, ES, grp + (long)l * gst, s));
+    int32_t* tm = (int32_t*)(base + Lw.tdst);
+    ASR_TRY(theta_dst_tile_major(theta_dst, 2 * n_theta, C, tm, s));
+    ASR_TRY(project_layers(grp, gst, reduce_groups(Lw.grid), E, C, tm, n_theta, L, dparams, n_theta + C, s));
   }
   return ASR_OK;
 }

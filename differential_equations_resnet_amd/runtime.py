@@ -289,6 +289,45 @@ def rk2_backward(dy, x, xmid, mask1, mask2, w, pmap: ParamMap, h: float, gamma: 
     return dx, dth, db, dw
 
 
+def rk2_stack_forward(x0: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, h: float):
+    """L RK2 blocks in one call (asr_rk2_stack_forward; bf16, C=64): returns
+    (ys [L,N,H,W,C] with ys[l] = x_{l+1}, xmids [L,N,H,W,C], masks1, masks2 [L, mask_bytes])."""
+    N, H, W, C = x0.shape
+    L = int(w.shape[0])
+    if not x0.is_contiguous():
+        raise ValueError("x0 must be contiguous NHWC")
+    P = N * H * W * C
+    ys = torch.empty((L, N, H, W, C), dtype=x0.dtype, device=x0.device)
+    xm = torch.empty_like(ys)
+    mb = mask_bytes(N, H, W, C)
+    m1 = torch.zeros(L, mb, dtype=torch.uint8, device=x0.device)
+    m2 = torch.zeros(L, mb, dtype=torch.uint8, device=x0.device)
+    if bias is not None and (tuple(bias.shape) != (L, C) or bias.dtype != torch.float32 or not bias.is_contiguous()):
+        raise ValueError(f"bias must be contiguous float32 [{L}, {C}]")
+    _lib.call("asr_rk2_stack_forward", _p(x0), _p(ys), _p(xm), P, _p(m1), _p(m2), mb, _p(w), w[0].numel(), _p(bias),
+              C, float(h), N, H, W, C, L, dtype_code(x0.dtype), _stream())
+    return ys, xm, m1, m2
+
+
+def rk2_stack_backward(dyL, x0, ys, xmids, masks1, masks2, w, pmap: ParamMap, h: float, gamma: float):
+    """Backward of rk2_stack_forward (asr_rk2_stack_backward): (dx0, dparams [L, n_theta + C])."""
+    L = int(w.shape[0])
+    N, H, W, C = x0.shape
+    dt = dtype_code(x0.dtype)
+    xs = (torch.cat([x0.unsqueeze(0), ys[:L - 1]]) if L > 1 else x0.unsqueeze(0)).contiguous()
+    P = N * H * W * C
+    mb = mask_bytes(N, H, W, C)
+    wsb = int(_lib.load().asr_rk2_stack_backward_workspace_bytes(N, H, W, C, L, dt))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=x0.device)
+    dx0 = torch.empty_like(x0)
+    dparams = torch.empty(L, pmap.n_theta + C, dtype=torch.float32, device=x0.device)
+    _, theta_dst = pmap.device(x0.device)
+    _lib.call("asr_rk2_stack_backward", _p(dyL), _p(xs), _p(xmids), P, _p(masks1), _p(masks2), mb, _p(w),
+              w[0].numel(), _p(theta_dst), pmap.n_theta, float(h), float(gamma), N, H, W, C, L, dt, _p(dx0),
+              _p(dparams), _p(ws), wsb, _stream())
+    return dx0, dparams
+
+
 def adam_update(params, grads, m, v, lr, beta1, beta2, eps, step, grad_scale=1.0):
     _lib.call("asr_adam_update", _p(params), _p(grads), _p(m), _p(v), params.numel(), float(lr), float(beta1),
               float(beta2), float(eps), int(step), float(grad_scale), _stream())

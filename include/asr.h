@@ -203,6 +203,27 @@ int asr_rk2_backward(const void* dy, const void* x, const void* xmid, const uint
                      float* dtheta, float* dbias, float* dw_hwio, void* ws, size_t ws_bytes,
                      asr_stream_t stream);
 
+/* A stack of L RK2 blocks in one call (config 5's network path): block l reads
+ * x_l (x0 for l = 0), writes x_mid_l to xmids + l*y_stride and x_{l+1} to
+ * ys + l*y_stride elements, mask1 / mask2 of block l to masks1 / masks2 +
+ * l*mask_stride bytes; w, bias as asr_block_stack_forward.  bf16 at C=64,
+ * W=32 (>= 4 row bands per image) runs all 2L stages in one launch; other
+ * shapes return ASR_E_UNSUPPORTED. */
+int asr_rk2_stack_forward(const void* x0, void* ys, void* xmids, long y_stride, uint8_t* masks1, uint8_t* masks2,
+                          long mask_stride, const void* w, long w_stride, const float* bias, long bias_stride, float h,
+                          int N, int H, int W, int C, int L, int dtype, asr_stream_t stream);
+
+/* Backward of asr_rk2_stack_forward: dyL = dL/dx_L; x_l at xs + l*x_stride
+ * (x_0 first), x_mid_l at xmids + l*x_stride; dx0, dparams as
+ * asr_block_stack_backward.  One launch over all blocks' two stages (bf16,
+ * C=64, W=32). */
+size_t asr_rk2_stack_backward_workspace_bytes(int N, int H, int W, int C, int L, int dtype);
+int asr_rk2_stack_backward(const void* dyL, const void* xs, const void* xmids, long x_stride, const uint8_t* masks1,
+                           const uint8_t* masks2, long mask_stride, const void* w, long w_stride,
+                           const int32_t* theta_dst, long n_theta, float h, float gamma, int N, int H, int W, int C,
+                           int L, int dtype, void* dx0, float* dparams, void* ws, size_t ws_bytes,
+                           asr_stream_t stream);
+
 /* ------------------------------------------------------------------------
  * Whole single-block network (get_single_block_resnet_build_function,
  * tfkeras_resnets.py:511-604, antisymmetric, num_stages=2, strides (1,1),

@@ -238,3 +238,38 @@ def test_network_rk2_stack_backward_equals_per_block(rt, N, L, gamma):
         ga, gb = a[o:o + n_blk], b[o:o + n_blk]
         assert np.abs(gb).max() > 0
         assert np.abs(ga - gb).max() <= 1e-5 * np.abs(gb).max(), (l, np.abs(ga - gb).max(), np.abs(gb).max())
+
+
+@pytest.mark.parametrize("N,L,gamma", [(3, 3, 0.0), (300, 2, -0.1), (512, 4, 0.0)])
+def test_rk2_stack_abi_matches_per_block(rt, N, L, gamma):
+    """asr_rk2_stack_forward / _backward (config 5's stacks through the C ABI)
+    against asr_rk2_forward / asr_rk2_backward block by block: x_mid, x_{l+1}
+    and both relu masks bitwise; dx_0 bitwise; dtheta / dbias within 1e-5 of
+    max|.| per block (one dW accumulation per block vs the per-block path's
+    slab read-modify-write)."""
+    C, h = 64, 8.0 / 30
+    rng = np.random.default_rng(N * 5 + L)
+    dev = torch.device("cuda")
+    pm = rt.param_map(C)
+    th = np.concatenate([O.flatten(O.init_theta_3by3(C, rng, np.float64)) for _ in range(L)]).astype(np.float32)
+    w = rt.theta_to_w(torch.from_numpy(th).to(dev), C, pm, gamma, rt.ASR_BF16, layers=L)
+    bias = torch.from_numpy((rng.standard_normal((L, C)) * 0.1).astype(np.float32)).to(dev)
+    x0 = torch.from_numpy(rng.standard_normal((N, 32, 32, C)).astype(np.float32)).to(dev).to(torch.bfloat16)
+    ys, xm, m1, m2 = rt.rk2_stack_forward(x0, w, bias, h)
+    x = x0
+    for l in range(L):
+        y, xmid, a1, a2 = rt.rk2_forward(x, w[l:l + 1], bias[l].contiguous(), h)
+        assert torch.equal(xmid, xm[l]) and torch.equal(y, ys[l]), f"block {l}: stack != per-block"
+        assert torch.equal(a1, m1[l]) and torch.equal(a2, m2[l]), f"block {l}: masks differ"
+        x = y
+    dyL = torch.from_numpy((rng.standard_normal((N, 32, 32, C)) * 0.1).astype(np.float32)).to(dev).to(torch.bfloat16)
+    dx0, dp = rt.rk2_stack_backward(dyL, x0, ys, xm, m1, m2, w, pm, h, gamma)
+    dy = dyL
+    for l in range(L - 1, -1, -1):
+        xl = x0 if l == 0 else ys[l - 1]
+        dx, dth, db, _ = rt.rk2_backward(dy, xl.contiguous(), xm[l].contiguous(), m1[l], m2[l], w[l:l + 1], pm, h, gamma)
+        for got, want, what in ((dp[l, :pm.n_theta], dth, "dtheta"), (dp[l, pm.n_theta:], db, "dbias")):
+            a, bb = got.cpu().numpy().astype(np.float64), want.cpu().numpy().astype(np.float64)
+            assert np.abs(a - bb).max() <= 1e-5 * max(np.abs(bb).max(), 1e-30), (l, what, np.abs(a - bb).max())
+        dy = dx
+    assert torch.equal(dx0, dy)
