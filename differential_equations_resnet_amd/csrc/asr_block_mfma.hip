@@ -84,7 +84,7 @@
 #define ASR_BWD3 1  // C=64 backward: k_bwd3 (12 waves, 3 per SIMD; 0: k_bwd2, 8 waves)
 #endif
 #ifndef ASR_BWD3_DMA0
-#define ASR_BWD3_DMA0 9  // k_bwd3 wgrad waves: DMA pieces issued right after the barrier, the rest one per row (A/B: spreading them lengthened the MFMA phase as much as it saved)
+#define ASR_BWD3_DMA0 16  // k_bwd3 wgrad waves: DMA pieces issued right after the barrier, the rest one per row (A/B: spreading them lengthened the MFMA phase as much as it saved; the stacks: all at once 16 vs 9 +0.3-0.5 %, 4 -0.7 %)
 #endif
 #ifndef ASR_ABLATE
 #define ASR_ABLATE 0  // development only: fwd 1 no epilogue, 2 no MFMA, 3 no prefetch DMA;
