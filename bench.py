@@ -68,6 +68,7 @@ def parse():
     ap.add_argument("--block-reps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this process may run on")
+    ap.add_argument("--lib", default=None, help="development A/B only: load this libasr build instead of the in-tree one")
     return ap.parse_args()
 
 
@@ -402,6 +403,8 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     torch.cuda.set_device(local)
+    if args.lib:
+        _lib.load(path=os.path.abspath(args.lib))
     dev = rt.require_gpu()
     distributed.init_from_env(device=dev)  # RCCL communicator through asr_dist_init (world > 1)
     lib = _lib.load()

@@ -41,26 +41,11 @@
 #ifndef ASR_V2_MASKTAB
 #define ASR_V2_MASKTAB 1  // v2 backward convert: relu-mask expansion from a 4 KiB LDS table (0: bit ops)
 #endif
-#ifndef ASR_V2_XHOOK
-#define ASR_V2_XHOOK 0  // v2 backward: wgrad waves issue the x prefetch one per k-step (0: before the k-steps)
-#endif
-#ifndef ASR_V2_SPREAD
-#define ASR_V2_SPREAD 0  // v2 backward: dgrad waves issue one dy DMA every N conv k-steps (0: one burst after the barrier)
-#endif
-#ifndef ASR_V2_ST16
-#define ASR_V2_ST16 1  // v2 backward: dx as 16-B stores (row swap between the two o-tiles)
-#endif
 #ifndef ASR_FWD_ST16
 #define ASR_FWD_ST16 1  // forward pipe: y as 16-B stores (row swap between the two pixel tiles)
 #endif
 #ifndef ASR_FWD_REUSE
 #define ASR_FWD_REUSE 1  // forward pipe: halo rows of a band continuing the previous band's image copied in LDS
-#endif
-#ifndef ASR_V2_WPIPE
-#define ASR_V2_WPIPE 1  // v2 backward: wgrad k-steps software-pipelined across m-tiles and k-steps
-#endif
-#ifndef ASR_XT_EARLY
-#define ASR_XT_EARLY 1  // v2 backward, RK2 first stage: extra-term loads of row 0 before the dy DMA burst (0: after)
 #endif
 #ifndef ASR_FWD3
 #define ASR_FWD3 1  // C=64 forward (Euler without RK2 residual, plain conv): k_fwd3 at 3 WGs per CU (0: k_fwd_pipe)
@@ -71,26 +56,11 @@
 #ifndef ASR_FWD_STACK
 #define ASR_FWD_STACK 1  // C=64 network forward: all blocks in one k_fwd3_stack launch (0: one k_fwd3 per block)
 #endif
-#ifndef ASR_FSTACK_HOOK
-#define ASR_FSTACK_HOOK 0  // k_fwd3_stack: next band's DMA pieces + residual reads as conv hooks (0: burst after the barrier)
-#endif
 #ifndef ASR_BWD_STACK
 #define ASR_BWD_STACK 1  // C=64 network backward: all blocks in one k_bwd3_stack launch (0: one k_bwd3 per block)
 #endif
-#ifndef ASR_STACK_ABLATE
-#define ASR_STACK_ABLATE 0  // development only: k_bwd3_stack 1 = no slab stores at block ends (wrong dW; timing)
-#endif
-#ifndef ASR_BWD3
-#define ASR_BWD3 1  // C=64 backward: k_bwd3 (12 waves, 3 per SIMD; 0: k_bwd2, 8 waves)
-#endif
 #ifndef ASR_BWD3_DMA0
 #define ASR_BWD3_DMA0 16  // k_bwd3 wgrad waves: DMA pieces issued right after the barrier, the rest one per row (A/B: spreading them lengthened the MFMA phase as much as it saved; the stacks: all at once 16 vs 9 +0.3-0.5 %, 4 -0.7 %)
-#endif
-#ifndef ASR_ABLATE
-#define ASR_ABLATE 0  // development only: fwd 1 no epilogue, 2 no MFMA, 3 no prefetch DMA;
-                      // bwd 4 no convert, 5 no dgrad MFMA, 6 no wgrad MFMA, 7 no dgrad epilogue,
-                      // 8 no prefetch DMA, 9 wgrad fragments from registers (no LDS reads),
-                      // 10 dgrad waves do not wait for the prefetch at the band barrier
 #endif
 
 namespace asr {
@@ -536,7 +506,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(const bf16* __restrict__ x, con
     unsigned char* tile = lds + buf * TILE;
     barrier_vm(nst);  // this item's DMA has landed; the other buffer is free
     nst = 0;
-    if (ASR_ABLATE != 3 && it + 1 < i1) {
+    if (it + 1 < i1) {
       const int y1 = nxt.b * BR;
       dma_rows<C, W>(x, lds + (buf ^ 1) * TILE, nxt.n, y1 - 1, min(BR, H - y1) + 2, H, wave, NW, lane);
     }
@@ -548,21 +518,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(const bf16* __restrict__ x, con
       for (int t = 0; t < OTW; ++t)
 #pragma unroll
         for (int pt = 0; pt < PT; ++pt) acc[t][pt] = f32x4{bz[t][0], bz[t][1], bz[t][2], bz[t][3]};
-      if (ASR_ABLATE != 2) {
-        conv_row<C, W>(tile, r, A, boff, acc);
-      } else {
-#pragma unroll
-        for (int t = 0; t < OTW; ++t)
-#pragma unroll
-          for (int pt = 0; pt < PT; ++pt) acc[t][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      if (ASR_ABLATE == 1) {
-#pragma unroll
-        for (int t = 0; t < OTW; ++t)
-#pragma unroll
-          for (int pt = 0; pt < PT; ++pt) asm volatile("" ::"v"(acc[t][pt]));
-        continue;
-      }
+      conv_row<C, W>(tile, r, A, boff, acc);
       const int gy = y0 + r;
       nst += PT * (OTW + ((EULER && mask) ? 1 : 0));
 #pragma unroll
@@ -1073,7 +1029,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
 
   zero_halo_cols<C, W>(lds, BR + 2, tid, 64 * NW);
   zero_halo_cols<C, W>(lds + TILE, BR + 2, tid, 64 * NW);
-  constexpr int IPR = W / G::PPI, NPW = ((BR + 2) * IPR + NW - 1) / NW;  // DMA pieces per row, per wave (max)
+  constexpr int IPR = W / G::PPI;  // DMA pieces per row
   const unsigned loff = (unsigned)dma_lane_off<C, W>(lane) * 2u;
   // cursor over (block l, image n, band b)
   int cl = 0, cn = n0, cb = 0;
@@ -1119,9 +1075,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
       } else {
         ntile = nt, ngy0 = yy - 1, nrows = min(BR, H - yy) + 2;
       }
-#if !ASR_FSTACK_HOOK
       for (int j = wave; j < nrows * IPR; j += NW) dma_row_instr<C, W>(nxs, ntile, xn, ngy0, j, H, loff);
-#endif
     }
     if (wave == 0) ASR_BTR(0, 0, it, 2);
     const unsigned tb = lds_u32(lds + buf * TILE);
@@ -1138,29 +1092,12 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
 #pragma unroll
       for (int r = 0; r < RB; ++r) xr[r] = *(const u32x4*)(rb + (long)min(r, rows - 1) * W * C * 2);
     }
-#if ASR_FSTACK_HOOK
-    // the DMA pieces of this wave (j = wave + 4u) and the residual reads issued among
-    // the conv's MFMAs (a piece issues cheaper there than in a burst after the barrier)
-    auto hook = [&](auto uc) {
-      constexpr int u = decltype(uc)::value;
-      if constexpr (u < NPW) {
-        const int j = wave + NW * u;
-        if (j < nrows * IPR) dma_row_instr<C, W>(nxs, ntile, xn, ngy0, j, H, loff);
-      } else if (!resg) {
-#pragma unroll
-        for (int r = 0; r < RB; ++r) xr[r] = lds_rd128(tb + lxr + (unsigned)(r * BD::ROWB));
-      }
-    };
-    conv_band<C, W, RB, NPW + 1>(tb, lo, A, acc, hook);
-    if (wave == 0) ASR_BTR(0, 0, it, 3);
-#else
     conv_band<C, W, RB>(tb, lo, A, acc);
     if (wave == 0) ASR_BTR(0, 0, it, 3);
     if (!resg) {
 #pragma unroll
       for (int r = 0; r < RB; ++r) xr[r] = lds_rd128(tb + lxr + (unsigned)(r * BD::ROWB));
     }
-#endif
     const int l = cl;
     if (blk_of(xl) != blk_of(cl) && it + 1 < total) {  // the next item starts block l+1: its W and bias (L2 hits)
       load_A1<C>(wpack + (long)blk_of(xl) * w_stride, ot, lane, A);
@@ -1454,8 +1391,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
       const int n = cur.n, y0 = cur.b * BR;
       const int rows = min(BR, H - y0);
       ASR_STAMP(it - i0, 0);
-      if (ASR_ABLATE == 10) barrier_lds();
-      else barrier_vm(nst);  // item's DMA landed; previous item fully consumed
+      barrier_vm(nst);  // item's DMA landed; previous item fully consumed
       ASR_STAMP(it - i0, 1);
       nst = 0;
       // prefetch of band it+1: dy rows, x rows, mask chunks as one stream of
@@ -1465,7 +1401,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
       int nd = 0;  // prefetch instructions this wave issued
       const bool reuse = it + 1 < i1 && nxt.n == cur.n;
       BwdPrefetch<C, W, BR, EULER> pf;
-      pf.init(nxt, ASR_ABLATE != 8 && it + 1 < i1, reuse, lds, buf ^ 1, H);
+      pf.init(nxt, it + 1 < i1, reuse, lds, buf ^ 1, H);
       const int dsplit = (pf.end * ASR_BWD_DGRAD_DMA_PCT) / 100;  // dgrad waves: [0, dsplit)
       int du = wv4;                                               // wave-uniform stream cursor
       const int dend = dsplit;
@@ -1481,7 +1417,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
         while (du < dend) dma_one();
       bool ex_wait = has_extra;
       if (reuse) bwd_halo_copy<C, W, BR, EULER>(lds, buf, tid, 512);
-      if (ASR_ABLATE != 4) bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, tid, 512);
+      bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, tid, 512);
       ASR_STAMP(it - i0, 2);
       barrier_lds();  // dz ready
       ASR_STAMP(it - i0, 3);
@@ -1496,26 +1432,12 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
         for (int t = 0; t < OTW; ++t)
 #pragma unroll
           for (int pt = 0; pt < PT; ++pt) acc[t][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (ASR_ABLATE != 5) {
-          if (ASR_BWD_DMA_HOOK && k == 0) {
-            conv_row<C, W>(dzt, r, A, boff, acc, dma_one);
-            while (du < dend) dma_one();
-            ASR_STAMP(it - i0, 4);
-          } else {
-            conv_row<C, W>(dzt, r, A, boff, acc);
-          }
+        if (ASR_BWD_DMA_HOOK && k == 0) {
+          conv_row<C, W>(dzt, r, A, boff, acc, dma_one);
+          while (du < dend) dma_one();
+          ASR_STAMP(it - i0, 4);
         } else {
-#pragma unroll
-          for (int t = 0; t < OTW; ++t)
-#pragma unroll
-            for (int pt = 0; pt < PT; ++pt) acc[t][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        if (ASR_ABLATE == 7) {
-#pragma unroll
-          for (int t = 0; t < OTW; ++t)
-#pragma unroll
-            for (int pt = 0; pt < PT; ++pt) asm volatile("" ::"v"(acc[t][pt]));
-          continue;
+          conv_row<C, W>(dzt, r, A, boff, acc);
         }
         const int gy = y0 + r;
         if (dx) nst += PT * OTW;
@@ -1637,7 +1559,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
       // its MFMAs
       const bool reuse = it + 1 < i1 && nxt.n == cur.n;
       BwdPrefetch<C, W, BR, EULER> pf;
-      pf.init(nxt, ASR_ABLATE != 8 && it + 1 < i1, reuse, lds, buf ^ 1, H);
+      pf.init(nxt, it + 1 < i1, reuse, lds, buf ^ 1, H);
       int du = (pf.end * ASR_BWD_DGRAD_DMA_PCT) / 100 + wv8 - 4;  // wgrad waves: [dsplit, end)
       const int dend = pf.end;
       auto dma_one = [&]() {
@@ -1647,7 +1569,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
         }
       };
       if (reuse) bwd_halo_copy<C, W, BR, EULER>(lds, buf, tid, 512);
-      if (ASR_ABLATE != 4) bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, tid, 512);
+      bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, tid, 512);
       ASR_STAMP(it - i0, 2);
       barrier_lds();
       ASR_STAMP(it - i0, 3);
@@ -1655,16 +1577,10 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
       ASR_STAMP(it - i0, 4);
       const unsigned char* dzt = lds + L::DZ;
       const unsigned char* xt = lds + L::X + buf * L::TILE;
-      for (int kk = kg; kk < (ASR_ABLATE == 6 ? 0 : rows * KPR); kk += G::KSPLIT) {
+      for (int kk = kg; kk < rows * KPR; kk += G::KSPLIT) {
         const int r = kk / KPR, kb = kk % KPR;
         const int pb = 32 * kb + 8 * g + tq;
         auto loadA = [&](int mi) {
-          if (ASR_ABLATE == 9) {
-            bf16x8 v;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = (bf16)(float)(lane + mi + kk + e);
-            return v;
-          }
           const int mt = tg * MTW + mi;
           const int tap = (16 * mt) / C, itile = ((16 * mt) % C) / 16;
           const int ky = tap / 3, kx = tap % 3;
@@ -1678,9 +1594,6 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
           const int q = 2 * ot + (tp >> 1);
           Bf[ot] = tr_pair(dzt + toff<C>(r + 1, pb + 1, q, TW) + 8 * (tp & 1),
                            dzt + toff<C>(r + 1, pb + 5, q, TW) + 8 * (tp & 1));
-          if (ASR_ABLATE == 9)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) Bf[ot][e] = (bf16)(float)(lane + ot + kk + e);
         }
         bf16x8 Ac = loadA(0), An;
 #pragma unroll
@@ -1801,536 +1714,9 @@ __device__ __forceinline__ unsigned bwd2_mask_word(const uint8_t* __restrict__ m
   return *(const unsigned*)(mask + ((long)n * H + gy) * (W * C / 8) + (2 * (lane & 31) + (lane >> 5)) * 4);
 }
 
-// wgrad waves, after band it's MFMAs, when band it+1 continues band it's
-// image: dz rows BR, BR+1 -> rows 0, 1 (already masked), x rows BR, BR+1 ->
-// rows 0, 1, dy row BR+1 -> row 1 (the residual's first interior row) of
-// the next buffers.  Interior columns, physical chunk slots (the swizzle
-#if !ASR_BWD3  // k_bwd2 (8-wave C=64 backward, round 1): built only as the A/B arm of k_bwd3
-// depends on the column only).  t in [0, 256).
-template <int C, int W, int BR>
-__device__ __forceinline__ void bwd2_copy_halo(unsigned char* lds, int buf, int t) {
-  using L = Bwd2Lds<C, W, BR>;
-  constexpr int NQ = C / 8, ROWB = L::ROWB;
-  static_assert(W * NQ == 256, "one interior row = 256 chunks");
-  const unsigned base = lds_u32(lds);
-  const int nb = buf ^ 1;
-  const unsigned o = (unsigned)(t + NQ) * 16u;
-  u32x4 cv[5];
-  cv[0] = lds_rd128(base + L::DZ + buf * L::TILE + BR * ROWB + o);
-  cv[1] = lds_rd128(base + L::DZ + buf * L::TILE + (BR + 1) * ROWB + o);
-  cv[2] = lds_rd128(base + L::X + buf * L::TILE + BR * ROWB + o);
-  cv[3] = lds_rd128(base + L::X + buf * L::TILE + (BR + 1) * ROWB + o);
-  cv[4] = lds_rd128(base + L::DY + buf * L::TILE + (BR + 1) * ROWB + o);
-  lgkm_wait<0>();
-  lds_wr128(base + L::DZ + nb * L::TILE + o, cv[0]);
-  lds_wr128(base + L::DZ + nb * L::TILE + ROWB + o, cv[1]);
-  lds_wr128(base + L::X + nb * L::TILE + o, cv[2]);
-  lds_wr128(base + L::X + nb * L::TILE + ROWB + o, cv[3]);
-  lds_wr128(base + L::DY + nb * L::TILE + ROWB + o, cv[4]);
-}
-
-// dgrad waves: convert the wave's own rows of the next band (buffer nb):
-// lane = (pixel lane&31, chunks 4h..4h+3, h = lane>>5), mask dword mw[k]
-template <int C, int W, int BR, bool EULER>
-__device__ __forceinline__ void bwd2_convert_own(unsigned char* lds, int nb, const Bwd2Own& own,
-                                                 const unsigned (&mw)[2], int lane) {
-  using L = Bwd2Lds<C, W, BR>;
-  constexpr int TW = W + 2;
-  static_assert(C == 64 && W == 32 && BR == 4, "v2 backward geometry");
-  const unsigned base = lds_u32(lds);
-  const int px = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {  // one row at a time (the second only on a band that starts an image)
-    if (k == 1 && own.rb < 0) break;
-    const int r = own.row(k);
-    u32x4 v[4], mt[4];
-    unsigned off[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      off[j] = (unsigned)toff<C>(r, px + 1, 4 * h + j, TW);
-      v[j] = lds_rd128(base + L::DY + nb * L::TILE + off[j]);
-      if (EULER && ASR_V2_MASKTAB) mt[j] = lds_rd128(base + L::MTAB + __builtin_amdgcn_ubfe(mw[k], 8 * j, 8) * 16);
-    }
-    lgkm_wait<0>();
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      u32x4 z = v[j];
-      if constexpr (EULER && ASR_V2_MASKTAB) {
-        z &= mt[j];
-      } else if constexpr (EULER) {
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {  // element pair (2d, 2d+1) of chunk 4h+j: mask bits 8j+2d, 8j+2d+1
-          const unsigned lo = (unsigned)__builtin_amdgcn_sbfe((int)mw[k], 8 * j + 2 * d, 1);
-          const unsigned hi = (unsigned)__builtin_amdgcn_sbfe((int)mw[k], 8 * j + 2 * d + 1, 1);
-          z[d] &= __builtin_amdgcn_perm(hi, lo, 0x07060100u);
-        }
-      }
-      lds_wr128(base + L::DZ + nb * L::TILE + off[j], z);
-    }
-  }
-}
-
-// RO: dx *= [x > 0] (x = this block's input; the network's first block, so
-// that dx is the stem's dz1 = dx1 * relu'(x1) directly)
-// XT (RK2 first stage): dx gets the extra term `extra` (the step's outer dy,
-// read from global memory in the epilogue, issued before the row's conv) and
-// the slabs are added onto the ones this WG's slot holds (the second stage's).
-template <int C, int W, int BR, int MODE, bool RO, bool XT = false>
-__global__ __launch_bounds__(512) void k_bwd2(const bf16* __restrict__ dy, const bf16* __restrict__ x,
-                                              const uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
-                                              float h, float two_gamma, int N, int H, bf16* __restrict__ dx,
-                                              float* __restrict__ slabs, const float* __restrict__ pslabs, int pP,
-                                              float* __restrict__ pgrp, int skip_dy,
-                                              const bf16* __restrict__ extra = nullptr) {
-  using G = Geo<C>;
-  using L = Bwd2Lds<C, W, BR>;
-  constexpr int TW = W + 2, PT = W / 16, OTW = G::OTW, OT = G::OT, MTW = G::MTW, IPR = W / G::PPI;
-  constexpr int KPR = W / 32;
-  constexpr bool EULER = MODE == BWD_EULER;
-  static_assert(C == 64 && W == 32 && BR == 4 && G::KSPLIT == 1 && G::OSPLIT == 2 && MTW % 3 == 0, "v2 backward geometry");
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int g = lane >> 4, lx = lane & 15;
-
-  for (int b = 0; b < 2; ++b) {
-    zero_halo_cols<C, W>(lds + L::DY + b * L::TILE, BR + 2, tid, 512);
-    zero_halo_cols<C, W>(lds + L::X + b * L::TILE, BR + 2, tid, 512);
-    zero_halo_cols<C, W>(lds + L::DZ + b * L::TILE, BR + 2, tid, 512);
-  }
-  if (ASR_V2_MASKTAB && EULER) {  // dword d of byte m's entry: 0xffff per set bit of (m >> 2d) & 3
-    unsigned* tab = (unsigned*)(lds + L::MTAB);
-    for (int i = tid; i < 1024; i += 512) {
-      const unsigned m = (unsigned)i >> 2, d = (unsigned)i & 3;
-      tab[i] = (((m >> (2 * d)) & 1u) ? 0xffffu : 0u) | (((m >> (2 * d + 1)) & 1u) ? 0xffff0000u : 0u);
-    }
-  }
-  const int nb = (H + BR - 1) / BR;
-  int i0, i1;
-  item_range(N * nb, &i0, &i1);
-  const unsigned loff = (unsigned)dma_lane_off<C, W>(lane) * 2u;
-  float* slab = slabs + (long)blockIdx.x * (9 * C * C + C);
-  const float hs = EULER ? h : 1.f;  // dz = hs * dzm (dzm = dy*mask in LDS)
-  const float hs2g = hs * two_gamma;
-  __syncthreads();  // halo columns zeroed before any convert / copy writes near them
-
-  // Pass 1 of the previous (deeper) block's slab reduction, folded in: the
-  // pP slabs at pslabs -> ceil(pP/32) group rows at pgrp, as k_reduce_slabs
-  // (each output 16-B chunk summed over its group's slabs in slab order by
-  // one thread: deterministic), two slab loads per band and thread, issued
-  // after the band barrier and added at the band's end.
-  constexpr int ES = 9 * C * C + C, ECH = ES / 4;
-  static_assert(ES % 4 == 0, "16-B slab chunks");
-  const long fT = (long)((pP + 31) / 32) * ECH;
-  const long fc0 = (long)blockIdx.x * fT / gridDim.x, fc1 = (long)(blockIdx.x + 1) * fT / gridDim.x;
-  const bool fold = pP > 0 && fc0 + tid < fc1;
-  const int fg = fold ? (int)((fc0 + tid) / ECH) : 0;
-  const int fpe = min(pP, 32 * fg + 32);
-  int fp = 32 * fg;
-  unsigned foff = fold ? (unsigned)fp * ES + (unsigned)((fc0 + tid) % ECH) * 4 : 0u;  // < 2^32: pP <= 512
-  f32x4 facc = {0.f, 0.f, 0.f, 0.f}, fv[2];
-  auto fold_issue = [&](auto NQ) {  // loads of the next NQ slabs
-#pragma unroll
-    for (int q = 0; q < decltype(NQ)::value; ++q)
-      if (fold && fp + q < fpe) fv[q] = *(const f32x4*)(pslabs + foff + (unsigned)q * ES);
-  };
-  auto fold_acc = [&](auto NQ) {
-#pragma unroll
-    for (int q = 0; q < decltype(NQ)::value; ++q)
-      if (fold && fp < fpe) {
-        facc += fv[q];
-        ++fp;
-        foff += ES;
-      }
-  };
-  using One = std::integral_constant<int, 1>;
-  using Two = std::integral_constant<int, 2>;
-
-  if (wave < 4) {
-    // ---------------- dgrad waves ----------------
-    constexpr int RS = 4 / G::OSPLIT;
-    const int oh = wave % G::OSPLIT, rg = wave / G::OSPLIT;
-    const int wv4 = __builtin_amdgcn_readfirstlane(wave);
-    bf16x8 A[OTW][G::KS];
-    load_A<C>(wpack, oh, lane, A);
-    Frag<C, W> boff;
-    boff.init(g, lx);
-    float dbacc[OTW][4];
-#pragma unroll
-    for (int t = 0; t < OTW; ++t)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) dbacc[t][e] = 0.f;
-    const unsigned lex = (unsigned)(2 * (lx * C + 16 * oh * OTW + 4 * g));  // XT: extra-term lane byte offset
-    int nst = 0;
-    // prologue: own rows of band i0 (a band with no predecessor: all BR+2 rows)
-    if (i0 < i1) {
-      const ItemCursor c0(i0, nb);
-      const Bwd2Own own(false, wv4);
-      unsigned mw[2] = {0u, 0u};
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        if (k == 1 && own.rb < 0) break;
-        const int r = own.row(k);
-        if constexpr (EULER) mw[k] = bwd2_mask_word<C, W>(mask, c0.n, c0.b * BR, r, H, lane);
-        for (int j = 0; j < IPR; ++j)
-          dma_row_instr<C, W>(dy, lds + L::DY + r * L::ROWB, c0.n, c0.b * BR - 1 + r, j, H, loff);
-      }
-      vm_wait(0);
-      bwd2_convert_own<C, W, BR, EULER>(lds, 0, own, mw, lane);
-    }
-    ItemCursor cur(i0, nb), nxt(i0, nb);
-    nxt.next(nb);
-    for (int it = i0; it < i1; ++it, cur.next(nb), nxt.next(nb)) {
-      const int buf = (it - i0) & 1;
-      const int n = cur.n, y0 = cur.b * BR;
-      const int rows = min(BR, H - y0);
-      ASR_STAMP(it - i0, 0);
-      barrier_vm(nst);  // band it staged everywhere; band it-1 fully consumed
-      ASR_STAMP(it - i0, 1);
-      nst = 0;
-      fold_issue(One{});  // dgrad: one slab load in flight at a time (registers)
-      const bool more = it + 1 < i1;
-      const bool reuse = more && nxt.n == cur.n;
-      const Bwd2Own own(reuse, wv4);
-      const int y1 = nxt.b * BR;
-      // mask dwords of the own rows of band it+1 (registers until the convert)
-      unsigned mw[2] = {0u, 0u};
-      if (EULER && more) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          if (k == 1 && own.rb < 0) break;
-          mw[k] = bwd2_mask_word<C, W>(mask, nxt.n, y1, own.row(k), H, lane);
-        }
-      }
-      // dy DMA of the own rows of band it+1, one instruction per k-step of
-      // the first dgrad row
-      const int dend = more ? own.count() * IPR : 0;
-      int du = 0, kstep = 0;
-      unsigned char* dyn = lds + L::DY + (buf ^ 1) * L::TILE;
-      auto dma_now = [&]() {
-        if (du < dend) {
-          const int r = own.row(du / IPR);
-          dma_row_instr<C, W>(dy, dyn + r * L::ROWB, nxt.n, y1 - 1 + r, du % IPR, H, loff);
-          ++du;
-        }
-      };
-      auto dma_one = [&]() {  // conv k-step hook: one DMA every ASR_V2_SPREAD k-steps
-        if (ASR_V2_SPREAD > 0 && kstep++ % (ASR_V2_SPREAD > 0 ? ASR_V2_SPREAD : 1) == 0) dma_now();
-      };
-      // XT: the extra term of own row k (wave-uniform row base in SGPRs + the
-      // lane's 32-bit offset + immediates).  Row 0's loads go out before the
-      // dy DMA burst, so waiting for them (in-order vmcnt) does not wait for
-      // it; row 1's before its conv (both rows' early: 10 spilled VGPRs).
-      u32x2 exv[2][XT ? PT : 1][OTW];
-      auto ex_load = [&](int k) {
-        if constexpr (XT) {
-          const int ur = __builtin_amdgcn_readfirstlane((n * H + y0 + rg + k * RS) * W);
-          const unsigned char* erow = (const unsigned char*)(extra + (long)ur * C);
-#pragma unroll
-          for (int pt = 0; pt < PT; ++pt)
-#pragma unroll
-            for (int t = 0; t < OTW; ++t)
-              exv[k][pt][t] = *(const u32x2*)(erow + lex + (unsigned)(2 * (16 * pt * C + 16 * t)));
-        }
-      };
-      if (XT && ASR_XT_EARLY && rg < rows) ex_load(0);
-      if (ASR_V2_SPREAD == 0)
-        while (du < dend) dma_now();  // one burst after the barrier
-      if (XT && !ASR_XT_EARLY && rg < rows) ex_load(0);
-      const unsigned char* dzt = lds + L::DZ + buf * L::TILE;
-      const unsigned char* dyt = lds + L::DY + buf * L::TILE;
-      int nstores = 0;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int r = rg + k * RS;
-        if (r >= rows) break;
-        f32x4 acc[OTW][PT];
-#pragma unroll
-        for (int t = 0; t < OTW; ++t)
-#pragma unroll
-          for (int pt = 0; pt < PT; ++pt) acc[t][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (k == 0) {
-          conv_row<C, W>(dzt, r, A, boff, acc, dma_one);
-          while (du < dend) dma_now();
-        } else {
-          if constexpr (XT) ex_load(1);
-          conv_row<C, W>(dzt, r, A, boff, acc);
-        }
-        ASR_STAMP(it - i0, 2 + k);
-        const int gy = y0 + r;
-        if (dx) nstores += ASR_V2_ST16 ? PT : PT * OTW;
-        u32x2 dzv[PT][OTW], dyv[PT][OTW], xv[RO ? PT : 1][OTW];
-#pragma unroll
-        for (int pt = 0; pt < PT; ++pt)
-#pragma unroll
-          for (int t = 0; t < OTW; ++t) {
-            const int px = 16 * pt + lx, o0 = 16 * (oh * OTW + t) + 4 * g;
-            const int co = toff<C>(r + 1, px + 1, o0 >> 3, TW) + (o0 & 4) * 2;
-            dzv[pt][t] = lds_rd64(lds_u32(dzt + co));
-            if (EULER) dyv[pt][t] = lds_rd64(lds_u32(dyt + co));
-            if constexpr (RO) xv[pt][t] = lds_rd64(lds_u32(lds + L::X + buf * L::TILE + co));
-          }
-        lgkm_wait<0>();
-        const bool g2 = hs2g != 0.f;  // wave-uniform: the 2*gamma*dz term (0 in the network: gamma is in W)
-#pragma unroll
-        for (int pt = 0; pt < PT; ++pt) {
-          const int px = 16 * pt + lx;
-          u32x2 ov[OTW];
-#pragma unroll
-          for (int t = 0; t < OTW; ++t) {
-            const bf16x4 dzr = *(const bf16x4*)&dzv[pt][t];
-            float dzf[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              dzf[e] = (float)dzr[e];
-              dbacc[t][e] += dzf[e];
-            }
-            bf16x4 o4;
-            if constexpr (EULER) {
-              const bf16x4 dyr = *(const bf16x4*)&dyv[pt][t];
-              float res[4];  // the +dy residual (none in the second RK2 stage)
-#pragma unroll
-              for (int e = 0; e < 4; ++e) res[e] = skip_dy ? 0.f : (float)dyr[e];
-              if constexpr (XT) {
-                const bf16x4 exr = *(const bf16x4*)&exv[k][pt][t];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) res[e] += (float)exr[e];
-              }
-              if (g2) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(hs2g, dzf[e], fmaf(-hs, acc[t][pt][e], res[e]));
-              } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(-hs, acc[t][pt][e], res[e]);
-              }
-            } else {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) o4[e] = (bf16)fmaf(two_gamma, dzf[e], -acc[t][pt][e]);
-            }
-            ov[t] = *(const u32x2*)&o4;
-            if constexpr (RO) {  // bf16 x > 0: positive as a signed 16-bit integer
-#pragma unroll
-              for (int d = 0; d < 2; ++d) {
-                const unsigned xw = xv[pt][t][d];
-                const unsigned keep = ((int)(short)(xw & 0xffffu) > 0 ? 0xffffu : 0u) | ((int)xw > 0xffff ? 0xffff0000u : 0u);
-                ov[t][d] &= keep;
-              }
-            }
-          }
-          if (!dx) continue;
-          bf16* drow = dx + (((long)n * H + gy) * W + px) * C;
-          if (ASR_V2_ST16) {
-            // 16-B stores: swap 16-lane rows between the two o-tiles, so lane
-            // row g holds 8 consecutive channels 16*(2oh + (g&1)) + 8*(g>>1)
-            const auto s0 = __builtin_amdgcn_permlane16_swap(ov[0][0], ov[1][0], false, false);
-            const auto s1 = __builtin_amdgcn_permlane16_swap(ov[0][1], ov[1][1], false, false);
-            *(u32x4*)(drow + 16 * (oh * OTW + (g & 1)) + 8 * (g >> 1)) = u32x4{s0[0], s1[0], s0[1], s1[1]};
-          } else {
-#pragma unroll
-            for (int t = 0; t < OTW; ++t) *(u32x2*)(drow + 16 * (oh * OTW + t) + 4 * g) = ov[t];
-          }
-        }
-        ASR_STAMP(it - i0, 4 + k);
-        if (k == 0) {  // second slab of this band
-          fold_acc(One{});
-          fold_issue(One{});
-        }
-      }
-      while (du < dend) dma_now();  // a wave without rows in this band
-      fold_acc(One{});
-      if (more) {
-        vm_wait(nstores);  // own dy rows and mask dwords of band it+1 (older than this band's stores)
-        bwd2_convert_own<C, W, BR, EULER>(lds, buf ^ 1, own, mw, lane);
-      }
-      nst = nstores;
-      ASR_STAMP(it - i0, 6);
-    }
-    // reduce db over the 16 pixel lanes, then over the row-group waves (LDS)
-#pragma unroll
-    for (int t = 0; t < OTW; ++t)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float v = dbacc[t][e];
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 8);
-        dbacc[t][e] = v;
-      }
-    barrier_vm(0);  // matches the wgrad waves' end-of-loop barrier
-    float* dbl = (float*)lds + 12288;  // [RS][C]
-    if (lx == 0) {
-#pragma unroll
-      for (int t = 0; t < OTW; ++t)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dbl[rg * C + 16 * (oh * OTW + t) + 4 * g + e] = hs * dbacc[t][e];
-    }
-  } else {
-    // ---------------- wgrad waves ----------------
-    const int w4 = wave - 4;
-    const int tg = w4;  // KSPLIT == 1: one m-tile group per wave, all k-steps
-    const int tq = lx >> 2, tp = lx & 3;
-    const int wv8 = __builtin_amdgcn_readfirstlane(wave) - 4;
-    f32x4 acc[MTW][OT];
-#pragma unroll
-    for (int mi = 0; mi < MTW; ++mi)
-#pragma unroll
-      for (int ot = 0; ot < OT; ++ot) acc[mi][ot] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (i0 < i1) {  // prologue: x rows of band i0
-      const ItemCursor c0(i0, nb);
-      for (int j = wv8; j < (BR + 2) * IPR; j += 4)
-        dma_row_instr<C, W>(x, lds + L::X, c0.n, c0.b * BR - 1, j, H, loff);
-    }
-    ItemCursor cur(i0, nb), nxt(i0, nb);
-    nxt.next(nb);
-    for (int it = i0; it < i1; ++it, cur.next(nb), nxt.next(nb)) {
-      const int buf = (it - i0) & 1;
-      const int y0 = cur.b * BR;
-      const int rows = min(BR, H - y0);
-      ASR_STAMP(it - i0, 0);
-      barrier_vm(0);  // this wave's x rows of band it landed
-      ASR_STAMP(it - i0, 1);
-      fold_issue(Two{});
-      // x rows of band it+1 (rows 2.. when it continues this band's image)
-      const int xr0 = nxt.n == cur.n ? 2 : 0;
-      unsigned char* xn = lds + L::X + (buf ^ 1) * L::TILE + xr0 * L::ROWB;
-      const int xy = nxt.b * BR - 1 + xr0;
-      const int xend = it + 1 < i1 ? (BR + 2 - xr0) * IPR : 0;
-      int xj = wv8;
-      auto xdma = [&]() {
-        if (xj < xend) {
-          dma_row_instr<C, W>(x, xn, nxt.n, xy, xj, H, loff);
-          xj += 4;
-        }
-      };
-      if (!ASR_V2_XHOOK)
-        while (xj < xend) xdma();
-      ASR_STAMP(it - i0, 2);
-      const unsigned char* dzt = lds + L::DZ + buf * L::TILE;
-      const unsigned char* xt = lds + L::X + buf * L::TILE;
-#if ASR_V2_WPIPE
-      // A fragments two m-tiles ahead (a ring of 3; the next k-step's first
-      // one during this one's last m-tiles), so an MFMA group does not wait a
-      // whole LDS latency for its A
-      const int nkk = rows * KPR;
-      auto loadA = [&](int kk, int mi) {
-        const int r = kk / KPR, kb = kk % KPR;
-        const int pb = 32 * kb + 8 * g + tq;
-        const int mt = tg * MTW + mi;
-        const int tap = (16 * mt) / C, itile = ((16 * mt) % C) / 16;
-        const int ky = tap / 3, kx = tap % 3;
-        const int q = 2 * itile + (tp >> 1);
-        return tr_pair(xt + toff<C>(r + ky, pb + kx, q, TW) + 8 * (tp & 1),
-                       xt + toff<C>(r + ky, pb + 4 + kx, q, TW) + 8 * (tp & 1));
-      };
-      auto loadB = [&](int kk, bf16x8 (&B)[OT]) {
-        const int r = kk / KPR, kb = kk % KPR;
-        const int pb = 32 * kb + 8 * g + tq;
-#pragma unroll
-        for (int ot = 0; ot < OT; ++ot) {
-          const int q = 2 * ot + (tp >> 1);
-          B[ot] = tr_pair(dzt + toff<C>(r + 1, pb + 1, q, TW) + 8 * (tp & 1),
-                          dzt + toff<C>(r + 1, pb + 5, q, TW) + 8 * (tp & 1));
-        }
-      };
-      bf16x8 Bf[OT], Ar[3];
-      if (nkk > 0) Ar[0] = loadA(0, 0);
-      for (int kk = 0; kk < nkk; ++kk) {
-        const bool more = kk + 1 < nkk;
-        loadB(kk, Bf);
-        Ar[1] = loadA(kk, 1);
-#pragma unroll
-        for (int mi = 0; mi < MTW; ++mi) {
-          if (mi + 2 < MTW) Ar[(mi + 2) % 3] = loadA(kk, mi + 2);
-          else if (mi + 2 == MTW && more) Ar[0] = loadA(kk + 1, 0);  // MTW % 3 == 0: slot 0 again
-#pragma unroll
-          for (int ot = 0; ot < OT; ++ot)
-            acc[mi][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ar[mi % 3], Bf[ot], acc[mi][ot], 0, 0, 0);
-        }
-        if (ASR_V2_XHOOK) xdma();
-      }
-#else
-      for (int kk = 0; kk < rows * KPR; ++kk) {
-        const int r = kk / KPR, kb = kk % KPR;
-        const int pb = 32 * kb + 8 * g + tq;
-        auto loadA = [&](int mi) {
-          const int mt = tg * MTW + mi;
-          const int tap = (16 * mt) / C, itile = ((16 * mt) % C) / 16;
-          const int ky = tap / 3, kx = tap % 3;
-          const int q = 2 * itile + (tp >> 1);
-          return tr_pair(xt + toff<C>(r + ky, pb + kx, q, TW) + 8 * (tp & 1),
-                         xt + toff<C>(r + ky, pb + 4 + kx, q, TW) + 8 * (tp & 1));
-        };
-        bf16x8 Bf[OT];
-#pragma unroll
-        for (int ot = 0; ot < OT; ++ot) {
-          const int q = 2 * ot + (tp >> 1);
-          Bf[ot] = tr_pair(dzt + toff<C>(r + 1, pb + 1, q, TW) + 8 * (tp & 1),
-                           dzt + toff<C>(r + 1, pb + 5, q, TW) + 8 * (tp & 1));
-        }
-        bf16x8 Ac = loadA(0), An;
-#pragma unroll
-        for (int mi = 0; mi < MTW; ++mi) {
-          if (mi + 1 < MTW) An = loadA(mi + 1);
-#pragma unroll
-          for (int ot = 0; ot < OT; ++ot)
-            acc[mi][ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ac, Bf[ot], acc[mi][ot], 0, 0, 0);
-          if (mi + 1 < MTW) Ac = An;
-        }
-        if (ASR_V2_XHOOK) xdma();
-      }
-#endif
-      while (xj < xend) xdma();
-      if (it + 1 < i1 && nxt.n == cur.n) bwd2_copy_halo<C, W, BR>(lds, buf, tid - 256);
-      fold_acc(Two{});
-      ASR_STAMP(it - i0, 3);
-    }
-    barrier_vm(0);  // all items consumed: LDS reusable
-    // XT: the old values of MC m-tiles loaded before their first store (one
-    // latency per chunk: the compiler keeps load/store pairs to the slab in order)
-    constexpr int MC = XT ? (MTW % 3 == 0 ? 3 : 1) : MTW;
-#pragma unroll
-    for (int m0 = 0; m0 < MTW; m0 += MC) {
-      float prev[XT ? MC : 1][OT][4];
-      if constexpr (XT) {
-#pragma unroll
-        for (int mi = 0; mi < MC; ++mi)
-#pragma unroll
-          for (int ot = 0; ot < OT; ++ot)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              prev[mi][ot][e] = slab[(long)(16 * (tg * MTW + m0 + mi) + 4 * g + e) * C + 16 * ot + lx];
-      }
-#pragma unroll
-      for (int mi = 0; mi < MC; ++mi)
-#pragma unroll
-        for (int ot = 0; ot < OT; ++ot)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int m = 16 * (tg * MTW + m0 + mi) + 4 * g + e;
-            float v = hs * acc[m0 + mi][ot][e];
-            if constexpr (XT) v += prev[mi][ot][e];
-            slab[(long)m * C + 16 * ot + lx] = v;
-          }
-    }
-  }
-  __syncthreads();
-  if (tid < C) {
-    const float* dbl = (const float*)lds + 12288;
-    float s = 0.f;
-    for (int q = 0; q < 4 / G::OSPLIT; ++q) s += dbl[q * C + tid];
-    if constexpr (XT) s += slab[9 * C * C + tid];
-    slab[9 * C * C + tid] = s;
-  }
-  if (fold) {  // slabs the bands did not cover (a WG with fewer than 16 bands)
-    for (; fp < fpe; ++fp, foff += ES) facc += *(const f32x4*)(pslabs + foff);
-    *(f32x4*)(pgrp + (long)fg * ES + (foff - (unsigned)fpe * ES)) = facc;
-  }
-}
-
-#endif  // !ASR_BWD3
 
 // ===========================================================================
-// Backward v3 (C=64, W=32, BR=4): k_bwd2's band protocol (double-buffered
+// Backward v3 (C=64, W=32, BR=4): the round-1 v2 backward's band protocol (double-buffered
 // dy / x / dz tiles, the next band's dz converted by the dgrad waves from
 // their own dy rows, x DMA + halo copy by the wgrad waves, the previous
 // block's slab pass folded in) at three waves per SIMD (12 waves, <= 168
@@ -2383,7 +1769,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
   __syncthreads();  // halo columns zeroed before any convert / copy writes near them
   ASR_BCLK(1, 0);
 
-  // pass 1 of the previous block's slab reduction (as k_bwd2), on the wgrad
+  // pass 1 of the previous block's slab reduction (as in the round-1 v2 backward), on the wgrad
   // waves only: thread ft = tid - 256 owns one 16-B chunk of one group row
   constexpr int ES = 9 * C * C + C, ECH = ES / 4;
   const int ft = tid - 256;
@@ -2530,7 +1916,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
     // K = the row's 32 pixels, lane group g reading pixels 4g + tq and 4g + 16 + tq
     // (any pixel permutation shared by A and B gives the same GEMM): each 32-lane
     // half then reads 8 consecutive tile columns, whose swizzled 8-B pieces cover
-    // the 64 banks once (pixels 8g + tq, 8g + 4 + tq, as k_bwd2 reads them, put
+    // the 64 banks once (pixels 8g + tq, 8g + 4 + tq, as the round-1 v2 backward read them, put
     // columns c and c + 8 on the same banks: every read 2-way)
     unsigned offA[MTW][2], offB[2][2];
     {
@@ -2655,7 +2041,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
       while (ipc < npc && ipc < ASR_BWD3_DMA0) piece();
       bf16x8 Bf[2], Ar[3];
       if (wave == 4) ASR_BTR(1, 1, it - i0, 2);
-      // A fragments two m-tiles ahead (ring of 3), as k_bwd2
+      // A fragments two m-tiles ahead (ring of 3), as in the round-1 v2 backward
       auto mfma_band = [&](auto bo) {
         constexpr int BO = decltype(bo)::value;
         Ar[0] = tr_pair_at<BO>(offA[0][0], offA[0][1]);
@@ -3265,7 +2651,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         for (int mi = 0; mi < MTW; ++mi) acc[mi][0] *= 2.f, acc[mi][1] *= 2.f;
         accb[0] *= 2.f, accb[1] *= 2.f;
       }
-      if (last_of_block && (!(ASR_STACK_ABLATE & 1) || hsb == -1.f)) {  // (ablation: never, but kept live)
+      if (last_of_block) {
         if (l + 2 < L && l + 2 >= lfold) fold_end(l + 2);
         // publish block l's dW tiles and db (write-through; drained at the next band barrier)
         float* slab = slabs + (long)l * slab_stride + (long)blockIdx.x * ES;
@@ -3301,7 +2687,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
 
 // ===========================================================================
 // Stem weight gradient on MFMA (C = 16 or 64, CIN=3, W=32, H % 8 == 0), from dz1 =
-// dx1 * [x1 > 0] (written by the first block's backward, k_bwd2<..., RO>):
+// dx1 * [x1 > 0] (written by the first block's backward, k_bwd3<..., RO> or k_bwd3_stack with ro0):
 //   dW1[kappa][o] = inv_std * sum_p (img[p + tap] - mean)[ci] * dz1[p][o]
 //   db1[o]        = sum_p dz1[p][o]
 // (models/tfkeras_resnets.py:555-572: input normalisation, then the 3x3 SAME
@@ -3613,46 +2999,20 @@ static int launch_bwd(int mode, const void* dy, const void* x, const uint8_t* ma
       // the folded pass gives each thread one 16-B chunk: at most 512 per WG
       const long fchunks = (long)((fold_P + 31) / 32) * ((9 * C * C + C) / 4);
       if ((fchunks + grid - 1) / grid > 512) fold_P = 0;
-      if (ASR_BWD3) {
 #define ASR_LAUNCH_BWD3(M, RO, XT)                                                                            \
   hipLaunchKernelGGL((blk::k_bwd3<C, W, kBwdBR, M, RO, XT>), dim3(grid), dim3(768), lds2, s, (const bf16*)dy,    \
                      (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs, fold_slabs, fold_P, \
                      fold_grp, skip_dy, (const bf16*)extra)
-        if (xt2) ASR_LAUNCH_BWD3(blk::BWD_EULER, false, true);
-        else if (mode == blk::BWD_EULER && relu_dx) {
-          ASR_LAUNCH_BWD3(blk::BWD_EULER, true, false);
-          if (relu_done) *relu_done = 1;
-        } else if (mode == blk::BWD_EULER) ASR_LAUNCH_BWD3(blk::BWD_EULER, false, false);
-        else ASR_LAUNCH_BWD3(blk::BWD_CONV, false, false);
-#undef ASR_LAUNCH_BWD3
-        ASR_LAUNCH_CHECK("k_bwd3");
-        if (fold_done) *fold_done = fold_P > 0;
-        return ASR_OK;
-      }
-#if !ASR_BWD3
-      if (xt2) {
-        hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_EULER, false, true>), dim3(grid), dim3(512), lds2, s,
-                           (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs,
-                           fold_slabs, fold_P, fold_grp, skip_dy, (const bf16*)extra);
-      } else if (mode == blk::BWD_EULER && relu_dx) {
-        hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_EULER, true>), dim3(grid), dim3(512), lds2, s,
-                           (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs,
-                           fold_slabs, fold_P, fold_grp, skip_dy);
+      if (xt2) ASR_LAUNCH_BWD3(blk::BWD_EULER, false, true);
+      else if (mode == blk::BWD_EULER && relu_dx) {
+        ASR_LAUNCH_BWD3(blk::BWD_EULER, true, false);
         if (relu_done) *relu_done = 1;
-      } else if (mode == blk::BWD_EULER) {
-        hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_EULER, false>), dim3(grid), dim3(512), lds2, s,
-                           (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs,
-                           fold_slabs, fold_P, fold_grp, skip_dy);
-      } else {
-        hipLaunchKernelGGL((blk::k_bwd2<C, W, kBwdBR, blk::BWD_CONV, false>), dim3(grid), dim3(512), lds2, s,
-                           (const bf16*)dy, (const bf16*)x, mask, (const bf16*)w, h, two_gamma, N, H, (bf16*)dx, slabs,
-                           fold_slabs, fold_P, fold_grp, skip_dy);
-      }
-      ASR_LAUNCH_CHECK("k_bwd2");
+      } else if (mode == blk::BWD_EULER) ASR_LAUNCH_BWD3(blk::BWD_EULER, false, false);
+      else ASR_LAUNCH_BWD3(blk::BWD_CONV, false, false);
+#undef ASR_LAUNCH_BWD3
+      ASR_LAUNCH_CHECK("k_bwd3");
       if (fold_done) *fold_done = fold_P > 0;
       return ASR_OK;
-#endif
-
     }
   }
   if (mode == blk::BWD_EULER) {

@@ -43,14 +43,11 @@ namespace deep {
 
 using namespace blk;
 
-#ifndef ASR_DEEP_PRIO
-#define ASR_DEEP_PRIO 0  // development A/B: s_setprio 1 for the wgrad (1) / staging (2) waves
-#endif
 #ifndef ASR_DEEP_NT
 #define ASR_DEEP_NT 1  // streaming (nt) stores of the forward: +6 % forward, -1 % backward (A/B r02k)
 #endif
-#ifndef ASR_DEEP_EXP
-#define ASR_DEEP_EXP 0  // development A/B only (tools/build_variants.sh): 0 = the product kernels
+#ifndef ASR_DEEP_TRACE
+#define ASR_DEEP_TRACE 0  // diagnostic build only: per-step s_memtime stamps of workgroup 0 (tools/tracebench.py)
 #endif
 
 constexpr int C = 16, W = 32, H = 32, TW = W + 2;
@@ -200,11 +197,7 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
       for (int j = 0; j < RPW; ++j) {
         if (j + 3 <= RPW + 1) fr.load(src, bF, bG, j + 3);
         f32x4 acc[2] = {{bz[0], bz[1], bz[2], bz[3]}, {bz[0], bz[1], bz[2], bz[3]}};
-#if ASR_DEEP_EXP == 5
-        acc[0][0] += (float)fr.F[j & 3][0][0] + (float)fr.G[(j + 2) & 3][1][3];
-#else
         row_mfma(A, fr.F[j & 3], fr.F[(j + 1) & 3], fr.F[(j + 2) & 3], fr.G[j & 3], fr.G[(j + 2) & 3], acc);
-#endif
         // epilogue on the regrouped chunk: y = x + h * relu(z) (fp32, one rounding),
         // relu bits as TF's ReluGrad (z > 0)
         float z[8];
@@ -222,7 +215,6 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
         });
         const bf16x8 y = __builtin_bit_cast(bf16x8, yw);
         *(bf16x8*)(dst + oT + j * ROWB) = y;
-#if ASR_DEEP_EXP != 4
 #if ASR_DEEP_NT
         // streaming stores: x_{l+1} and its mask are read back only by the backward
         if (store) __builtin_nontemporal_store(yw, (u32x4v*)(yl + oG + j * ROW_G));
@@ -230,7 +222,6 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
 #else
         if (store) *(bf16x8*)(yl + oG + j * ROW_G) = y;
         if (MASK) ml[oM + j * 64] = (uint8_t)bits;
-#endif
 #endif
         xr[j] = y;
       }
@@ -314,7 +305,7 @@ __device__ __forceinline__ void barrier_vmt() {  // barrier after all but the N 
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
 }
 
-#if ASR_DEEP_EXP == 8  // development: per-step timestamps of block 0 (waves 0, 4, 7)
+#if ASR_DEEP_TRACE  // diagnostic: per-step timestamps of workgroup 0 (waves 0, 4, 7)
 __device__ unsigned long long g_trace[3][160][4];
 #define ASR_TRACE(role, t, which)                                     \
   if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (t) < 160) {      \
@@ -431,11 +422,7 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
           for (int j = 0; j < RPB; ++j) {
             if (NS == 4 && j + 3 <= RPB + 1) fr.load(zt, bF, bG, j + 3);
             f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#if ASR_DEEP_EXP == 2 || ASR_DEEP_EXP == 3 || ASR_DEEP_EXP == 7
-            acc[0][0] = (float)fr.F[j % NS][0][0] + (float)fr.G[(j + 2) % NS][1][3];
-#else
             row_mfma(A, fr.F[j % NS], fr.F[(j + 1) % NS], fr.F[(j + 2) % NS], fr.G[j % NS], fr.G[(j + 2) % NS], acc);
-#endif
             if (NS == 3 && j + 3 <= RPB + 1) fr.load(zt, bF, bG, j + 3);
             u32x4v zw;
             if constexpr (GAMMA) zw = *(const u32x4v*)(zt + oT + j * ROWB);  // dzm_l of the lane's chunk
@@ -476,9 +463,6 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
       __syncthreads();
     }
   } else if (wave < NDG + 3) {
-#if ASR_DEEP_PRIO & 1
-    __builtin_amdgcn_s_setprio(1);
-#endif
     // ------------------------------ wgrad waves ------------------------------
     const int kx = wave - NDG;
     unsigned tx2[2], tz2[2];  // tr-read lane offsets: pixel 8g + 4*(hh ^ (g&1)) + q, channels 4p..4p+3
@@ -534,9 +518,6 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
         for (int k = 0; k < kcount; ++k) {
           if (wave == NDG) ASR_TRACE(1, t, 0);
           static_for<0, KSEG>([&](auto kc) {
-#if ASR_DEEP_EXP == 1 || ASR_DEEP_EXP == 3 || ASR_DEEP_EXP == 7
-            if (two_gamma == 1234.5f)  // never: the wgrad MFMAs skipped at run time
-#endif
             if (k == decltype(kc)::value) wgrad_layer(acc[decltype(kc)::value], t);
           });
           if (wave == NDG) ASR_TRACE(1, t, 1);
@@ -559,9 +540,6 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
     }
   } else {
     // -------------------------- x / mask staging wave (7) --------------------------
-#if ASR_DEEP_PRIO & 2
-    __builtin_amdgcn_s_setprio(1);
-#endif
     // x of the step after next: rows 0..XS-1 by global loads into registers (a
     // third x buffer), written to the free LDS x tile one step later; rows XS..
     // by LDS-DMA into the rotating third row block; so every x load has about
@@ -640,7 +618,7 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
                     n3 = pos_next(n2, L, N, P, b);
           write_x((t + 1) & 1);  // x of the next step
           write_m(t & 1);        // mask of the step after next (read by the next step's dgrad epilogue)
-#if ASR_DEEP_EXP == 8
+#if ASR_DEEP_TRACE
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
           ASR_TRACE(2, t, 2);
@@ -653,7 +631,7 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
             if (g == 0) dbl[k * C + lx] += a[0];
           }
           ASR_TRACE(2, t, 3);
-#if ASR_DEEP_EXP == 8
+#if ASR_DEEP_TRACE
           asm volatile("s_waitcnt vmcnt(34)" ::: "memory");  // trace the x DMA landing, not its issue
 #endif
           ASR_TRACE(2, t, 1);
@@ -701,7 +679,7 @@ int deep16_forward(const void* x0, void* y0, long y_stride, uint8_t* mask0, long
   return ASR_OK;
 }
 
-#if ASR_DEEP_EXP == 8
+#if ASR_DEEP_TRACE
 extern "C" int asr_debug_deep16_trace(void* dst, size_t bytes) {
   return hipMemcpyFromSymbol(dst, HIP_SYMBOL(deep::g_trace), bytes) == hipSuccess ? 0 : -1;
 }

@@ -11,9 +11,6 @@
 
 #include "asr_common.h"
 
-#ifndef ASR_ABLATE
-#define ASR_ABLATE 0  // development only: stem wgrad 11 no FMA loop, 12 no dx1/x1 loads
-#endif
 
 namespace asr {
 
@@ -162,10 +159,7 @@ __global__ __launch_bounds__(256) void k_stem_wgrad(const Tin* __restrict__ img,
         const int p = p0 + u * PL;
         const int pc = p < H * W ? p : 0;
         float dv[4], av[4];
-        if (ASR_ABLATE == 12) {
-#pragma unroll
-          for (int v = 0; v < 4; ++v) dv[v] = (float)(pc + v), av[v] = 1.f;
-        } else if constexpr (sizeof(T) == 2) {
+        if constexpr (sizeof(T) == 2) {
           const bf16x4 d4 = *(const bf16x4*)(d + (long)pc * C), a4 = *(const bf16x4*)(a + (long)pc * C);
 #pragma unroll
           for (int v = 0; v < 4; ++v) dv[v] = (float)d4[v], av[v] = (float)a4[v];
@@ -179,10 +173,9 @@ __global__ __launch_bounds__(256) void k_stem_wgrad(const Tin* __restrict__ img,
         for (int v = 0; v < 4; ++v) g4[v] = (p < H * W && av[v] > 0.f) ? dv[v] : 0.f;
         gv[u][0] = f32x2{g4[0], g4[1]};
         gv[u][1] = f32x2{g4[2], g4[3]};
-        if (ASR_ABLATE == 11) acc[u][0] += gv[u][0] + gv[u][1];
       }
 #pragma unroll
-      for (int u = 0; u < (ASR_ABLATE == 11 ? 0 : U); ++u) {
+      for (int u = 0; u < U; ++u) {
         const int p = p0 + u * PL;
         const int pc = p < H * W ? p : 0;
         const int x = pc % W, y = pc / W;

@@ -1,6 +1,6 @@
 """development: per-step timestamps of the fused C=16 backward (block 0:
 dgrad wave 0, wgrad wave 4, staging wave 7) from a build with
--DASR_DEEP_EXP=8 (tools/build_variants.sh e8 "-DASR_DEEP_EXP=8").
+-DASR_DEEP_TRACE=1 (tools/build_variants.sh e8 "-DASR_DEEP_TRACE=1").
 usage: python tools/tracebench.py build_abl_e8.so [--N 1024 --L 108]"""
 import argparse
 import ctypes
