@@ -9,6 +9,8 @@ import os
 import shutil
 import subprocess
 import sys
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
@@ -33,23 +35,35 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile every HIP source for gfx950 into one shared library."""
+def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -> str:
+    """Compile every HIP source for gfx950 (one object per source, in
+    parallel) and link them into one shared library."""
     if not force and not _stale():
         return LIB
-    objs = []
     cc = hipcc()
     flags = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-unused-function",
              "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
-    tmp = LIB + ".tmp"
-    cmd = [cc] + flags + ["-shared", "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    res = subprocess.run(cmd, capture_output=True, text=True)
-    if res.returncode != 0:
-        raise RuntimeError("hipcc failed building libasr.so:\n" + res.stdout + res.stderr)
-    os.replace(tmp, LIB)
-    del objs
+    jobs = jobs or max(1, min(len(SOURCES), os.cpu_count() or 1, 8))
+    with tempfile.TemporaryDirectory(prefix="asr_build_") as tmpdir:
+        def compile_one(src):
+            obj = os.path.join(tmpdir, os.path.splitext(src)[0] + ".o")
+            cmd = [cc] + flags + ["-c", "-o", obj, os.path.join(CSRC, src)]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            res = subprocess.run(cmd, capture_output=True, text=True)
+            if res.returncode != 0:
+                raise RuntimeError(f"hipcc failed on {src}:\n" + res.stdout + res.stderr)
+            return obj
+        with ThreadPoolExecutor(jobs) as pool:
+            objs = list(pool.map(compile_one, SOURCES))
+        tmp = LIB + ".tmp"
+        cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError("linking libasr.so failed:\n" + res.stdout + res.stderr)
+        os.replace(tmp, LIB)
     return LIB
 
 

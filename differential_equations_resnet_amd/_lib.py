@@ -29,7 +29,7 @@ ASR_BF16 = 1
 ASR_PARAM_3BY3 = 0
 ASR_PARAM_GENERAL = 1
 ASR_PARAM_REGULAR = 2
-ABI_VERSION = 4
+ABI_VERSION = 5
 ASR_MODE_EULER = 0
 ASR_MODE_CONV = 1
 ASR_INTEGRATOR_EULER = 0
@@ -39,6 +39,8 @@ ASR_VARIANT_STEM_FWD_VALU = 2
 ASR_VARIANT_STEM_WGRAD_VALU = 4
 ASR_VARIANT_PER_BLOCK_FWD = 8
 ASR_VARIANT_PER_BLOCK_BWD = 16
+ASR_VARIANT_INFERENCE = 32
+ASR_VARIANT_TIMED = 64
 ASR_DIST_UNIQUE_ID_BYTES = 128
 
 
@@ -94,6 +96,9 @@ SIGNATURES = [
     ("asr_net_forward", _I, [ct.POINTER(NetConfig), _P, _P, _P, _P, _S, _P]),
     ("asr_net_forward_backward", _I, [ct.POINTER(NetConfig), _P, _P, _P, _P, _P, _P, _P, _S, _P]),
     ("asr_net_check_status", _I, [ct.POINTER(NetConfig), _P, _S, _P]),
+    ("asr_net_kernel_times", _I, [_P]),
+    ("asr_stack_status", _I, [_I]),
+    ("asr_debug_stack_backward", _I, [_I]),
     ("asr_rk2_stack_forward", _I, [_P, _P, _P, _L, _P, _P, _L, _P, _L, _P, _L, _F, _I, _I, _I, _I, _I, _I, _P]),
     ("asr_rk2_stack_backward_workspace_bytes", _S, [_I, _I, _I, _I, _I, _I]),
     ("asr_rk2_stack_backward", _I, [_P, _P, _P, _L, _P, _P, _L, _P, _L, _P, _L, _F, _F, _I, _I, _I, _I, _I, _I, _P,

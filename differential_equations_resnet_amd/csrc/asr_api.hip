@@ -60,7 +60,7 @@ int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride
                          const uint8_t* masks2 = nullptr, void* gbuf = nullptr);
 int block_stack_fwd_mfma(const void* x0, void* ys, long y_stride, uint8_t* masks, long mask_stride, const void* w,
                          long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C, int L,
-                         hipStream_t s);
+                         hipStream_t s, int slots = 0);
 int deep16_forward(const void* x0, void* y0, long y_stride, uint8_t* mask0, long mask_stride, const void* wpack,
                    const float* bias, long bias_stride, float h, int N, int L, bool store_all, hipStream_t s);
 size_t deep16_slab_bytes(int N, int L);
@@ -324,6 +324,7 @@ struct NetLayout {
   bool fast_stem;
   bool deep;          // C=16 stack path: one fused launch forward, one backward (asr_deep16.hip)
   size_t deep_slabs;  // its weight-gradient slabs [L][rows][E+C]
+  bool inference;     // ASR_VARIANT_INFERENCE: forward-only workspace (3 activation slots, no backward buffers)
   bool stack_bwd;     // C=64 Euler bf16: all blocks' backward in one k_bwd3_stack launch
   int stack_grid;     // its workgroups
   size_t theta_dst_tm, stack_slabs, stack_done;  // tile-major projection map, [L][grid][E+C] slabs, counters
@@ -341,7 +342,7 @@ static int net_check(const asr_net_config* c) {
   if (c->integrator != ASR_INTEGRATOR_EULER && c->integrator != ASR_INTEGRATOR_RK2)
     return fail(ASR_E_ARG, "bad integrator %d", c->integrator);
   if (c->variant & ~(ASR_VARIANT_NO_FOLD | ASR_VARIANT_STEM_FWD_VALU | ASR_VARIANT_STEM_WGRAD_VALU | ASR_VARIANT_PER_BLOCK_FWD |
-                    ASR_VARIANT_PER_BLOCK_BWD))
+                    ASR_VARIANT_PER_BLOCK_BWD | ASR_VARIANT_INFERENCE | ASR_VARIANT_TIMED))
     return fail(ASR_E_ARG, "bad variant bits 0x%x", c->variant);
   if (c->dtype == ASR_BF16 && !mfma_supported(c->C, c->W))
     return fail(ASR_E_UNSUPPORTED, "bf16 network needs C in {16,32,64} and W == 32 (C=%d W=%d)", c->C, c->W);
@@ -368,8 +369,10 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.nparams = L.off_fcb + K;
   L.mask_bytes = asr_mask_bytes(c->N, c->H, c->W, C);
   L.fast_stem = stem_supported(c->Cin, c->H, c->W, C);
+  L.inference = (c->variant & ASR_VARIANT_INFERENCE) != 0;
+  const bool tr = !L.inference;  // training buffers
   L.deep = c->dtype == ASR_BF16 && !L.rk2 && deep16_supported(c->H, c->W, C);
-  L.stack_bwd = c->dtype == ASR_BF16 && block_stack_bwd_supported(c->N, c->H, c->W, C);
+  L.stack_bwd = tr && c->dtype == ASR_BF16 && block_stack_bwd_supported(c->N, c->H, c->W, C);
   L.stack_grid = L.stack_bwd ? block_stack_bwd_grid(c->N) : 0;
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -378,42 +381,74 @@ static NetLayout net_layout(const asr_net_config* c) {
     return o;
   };
   L.w_src = take((size_t)L.E * 4);
-  L.w_src_bwd = take(L.sep_bwd ? (size_t)L.E * 4 : 0);
+  L.w_src_bwd = take(L.sep_bwd && tr ? (size_t)L.E * 4 : 0);
   L.theta_dst = take((size_t)L.ntheta * 2 * 4);
   L.wbuf = take((size_t)c->L * L.wstride * L.act_bytes);
-  L.wbuf_bwd = take(L.sep_bwd ? (size_t)c->L * L.wstride * L.act_bytes : 0);
+  L.wbuf_bwd = take(L.sep_bwd && tr ? (size_t)c->L * L.wstride * L.act_bytes : 0);
   L.x0 = take(L.fast_stem ? 0 : (size_t)c->N * c->H * c->W * c->Cin * 4);
-  L.acts = take((size_t)(c->L + 1) * L.P * L.act_bytes);
-  L.xmids = take(L.rk2 ? (size_t)c->L * L.P * L.act_bytes : 0);
-  L.masks = take((size_t)L.stages * c->L * L.mask_bytes);  // RK2: mask1 of every block, then mask2
-  L.dxa = take((size_t)L.P * L.act_bytes);
-  L.dxb = take((size_t)L.P * L.act_bytes);
-  L.dxg = take(L.rk2 ? (size_t)L.P * L.act_bytes : 0);
+  // training keeps x_0 .. x_L for the backward; inference ping-pongs (x_0 + 2 slots)
+  L.acts = take((size_t)(tr ? c->L + 1 : 3) * L.P * L.act_bytes);
+  L.xmids = take(L.rk2 ? (size_t)(tr ? c->L : 1) * L.P * L.act_bytes : 0);
+  L.masks = take(tr ? (size_t)L.stages * c->L * L.mask_bytes : 0);  // RK2: mask1 of every block, then mask2
+  L.dxa = take(tr ? (size_t)L.P * L.act_bytes : 0);
+  L.dxb = take(tr ? (size_t)L.P * L.act_bytes : 0);
+  L.dxg = take(L.rk2 && tr ? (size_t)L.P * L.act_bytes : 0);
   // per-block backward workspace (asr_conv_backward layout), reused by the stem
   const BwdWs bw = bwd_ws_layout(c->N, c->H, c->W, C, c->dtype, L.stages);
   const long E1 = 9L * c->Cin * C;
   const size_t stem_ws = align_up((size_t)L.P * 4, 256) + align_up((size_t)kMaxSlabsApi * (E1 + C) * 4, 256) +
                          align_up(reduce_ws_bytes(kMaxSlabsApi, E1 + C), 256);
-  L.bwdws = take(std::max(bw.total, stem_ws));
+  L.bwdws = take(tr ? std::max(bw.total, stem_ws) : 0);
   // odd Euler blocks' slabs (even ones use the backward workspace's): a
   // block's slabs stay readable while the next block's kernel reduces them
-  L.slabs2 = take((size_t)L.stages * kMaxSlabsApi * (L.E + C) * 4);  // every other block's slabs
+  L.slabs2 = take(tr ? (size_t)L.stages * kMaxSlabsApi * (L.E + C) * 4 : 0);  // every other block's slabs
   L.grp_stride = (long)reduce_groups(L.stages * kMaxSlabsApi) * (L.E + C);
-  L.grp = take((size_t)c->L * L.grp_stride * 4);
-  L.deep_slabs = take(L.deep ? deep16_slab_bytes(c->N, c->L) : 0);
+  L.grp = take(tr ? (size_t)c->L * L.grp_stride * 4 : 0);
+  L.deep_slabs = take(L.deep && tr ? deep16_slab_bytes(c->N, c->L) : 0);
   L.theta_dst_tm = take(L.stack_bwd ? (size_t)L.ntheta * 2 * 4 : 0);
   L.stack_slabs = take(L.stack_bwd ? (size_t)c->L * L.stack_grid * (L.E + C) * 4 : 0);
   L.stack_done = take(L.stack_bwd ? (size_t)(c->L + 4) * 4 : 0);
   L.probs = take((size_t)c->N * K * 4);
-  L.loss_per = take((size_t)c->N * 4);
-  L.dlogits = take((size_t)c->N * K * 4);
-  L.gap = take((size_t)c->N * C * 4);
+  L.loss_per = take(tr ? (size_t)c->N * 4 : 0);
+  L.dlogits = take(tr ? (size_t)c->N * K * 4 : 0);
+  L.gap = take(tr ? (size_t)c->N * C * 4 : 0);
   L.total = off;
   return L;
 }
 
+// ASR_VARIANT_TIMED: HIP events around the block launches of the last timed
+// asr_net_forward / asr_net_forward_backward (asr_net_kernel_times): 0-1 the
+// blocks' forward, 2-3 the stacked backward kernel, 3-4 its post-launch slab
+// reductions and the projection onto theta.  Measurement only.
+static hipEvent_t g_tev[5];
+static bool g_tev_made = false;
+static unsigned g_tev_rec = 0;  // bit i: event i recorded by the last timed call
+
+static int timed_event(const asr_net_config* c, int i, hipStream_t s) {
+  if (!(c->variant & ASR_VARIANT_TIMED)) return ASR_OK;
+  if (!g_tev_made) {
+    for (auto& e : g_tev) ASR_TRY(hip_check(hipEventCreate(&e), "hipEventCreate"));
+    g_tev_made = true;
+  }
+  if (i == 0) g_tev_rec = 0;
+  ASR_TRY(hip_check(hipEventRecord(g_tev[i], s), "hipEventRecord"));
+  g_tev_rec |= 1u << i;
+  return ASR_OK;
+}
+
+// x_L of a forward: training keeps every activation (slot L); evaluation
+// ping-pongs (the C=64 stack over slots 1-2 of the inference layout, the
+// per-block kernels over slots 0-1)
+static unsigned char* net_xL(const asr_net_config* c, const NetLayout& L, unsigned char* ws, bool training,
+                             bool stack_fwd) {
+  const size_t a = (size_t)L.P * L.act_bytes;
+  if (training) return ws + L.acts + (size_t)c->L * a;
+  if (stack_fwd) return ws + L.acts + (size_t)(1 + (c->L - 1) % 2) * a;
+  return ws + L.acts + (size_t)(c->L & 1) * a;
+}
+
 static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const float* params, const void* images,
-                            bool training, unsigned char* ws, hipStream_t s) {
+                            bool training, unsigned char* ws, hipStream_t s, unsigned char** xL_out = nullptr) {
   const int C = c->C, N = c->N, H = c->H, W = c->W;
   const bool bf = c->dtype == ASR_BF16;
   const float inv_std = c->use_norm ? 1.f / c->divide_by_stddev : 1.f;
@@ -423,11 +458,13 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
   if (training && L.sep_bwd)
     ASR_TRY(asr_theta_to_w(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src_bwd), 0.f,
                            ws + L.wbuf_bwd, L.wstride, c->dtype, s));
+  if (training && L.inference) return fail(ASR_E_ARG, "an ASR_VARIANT_INFERENCE workspace has no training buffers");
   unsigned char* acts = ws + L.acts;
   auto act = [&](int i) -> unsigned char* {
     const int slot = training ? i : (i & 1);
     return acts + (size_t)slot * L.P * L.act_bytes;
   };
+  if (xL_out) *xL_out = net_xL(c, L, ws, training, false);
   // 2. normalisation + conv1 + relu (tfkeras_resnets.py:555-572)
   if (L.fast_stem && bf && stem_fwd_mfma_supported(c->Cin, H, W, C) && !(c->variant & ASR_VARIANT_STEM_FWD_VALU)) {
     ASR_TRY(stem_fwd_mfma(images, c->input_u8, params + L.off_c1k, params + L.off_c1b, N, H, W, c->Cin, C,
@@ -450,22 +487,36 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
                      W, c->Cin, C, bf ? 1 : 0, s));
   }
   // 3. L Euler blocks (tfkeras_resnets.py:579-582 -> :28-94), or RK2 blocks
+  ASR_TRY(timed_event(c, 0, s));
   if (L.deep) {  // C=16: all L steps in one launch, images resident in LDS
-    return deep16_forward(act(0), act(training ? 1 : c->L), L.P, training ? (uint8_t*)(ws + L.masks) : nullptr,
-                          L.mask_bytes, ws + L.wbuf, params + L.off_blk + L.ntheta, L.blk_stride, c->h, N, c->L,
-                          training, s);
+    ASR_TRY(deep16_forward(act(0), act(training ? 1 : c->L), L.P, training ? (uint8_t*)(ws + L.masks) : nullptr,
+                           L.mask_bytes, ws + L.wbuf, params + L.off_blk + L.ntheta, L.blk_stride, c->h, N, c->L,
+                           training, s));
+    return timed_event(c, 1, s);
   }
   if (bf && training && L.rk2 && block_stack_fwd_supported(N, H, W, C) && !(c->variant & ASR_VARIANT_PER_BLOCK_FWD)) {
     // C=64 RK2: all 2L stages in one launch
     uint8_t* m1 = (uint8_t*)(ws + L.masks);
-    return block_stack_fwd_rk2_mfma(act(0), act(1), ws + L.xmids, (long)L.P, m1, m1 + (size_t)c->L * L.mask_bytes,
-                                    (long)L.mask_bytes, ws + L.wbuf, (long)L.wstride, params + L.off_blk + L.ntheta,
-                                    L.blk_stride, c->h, N, H, W, C, c->L, s);
+    ASR_TRY(block_stack_fwd_rk2_mfma(act(0), act(1), ws + L.xmids, (long)L.P, m1, m1 + (size_t)c->L * L.mask_bytes,
+                                     (long)L.mask_bytes, ws + L.wbuf, (long)L.wstride, params + L.off_blk + L.ntheta,
+                                     L.blk_stride, c->h, N, H, W, C, c->L, s));
+    return timed_event(c, 1, s);
   }
-  if (bf && training && !L.rk2 && block_stack_fwd_supported(N, H, W, C) && !(c->variant & ASR_VARIANT_PER_BLOCK_FWD)) {
-    // C=64: all L blocks in one launch (whole images per workgroup)
-    return block_stack_fwd_mfma(act(0), act(1), (long)L.P, (uint8_t*)(ws + L.masks), (long)L.mask_bytes, ws + L.wbuf,
-                                (long)L.wstride, params + L.off_blk + L.ntheta, L.blk_stride, c->h, N, H, W, C, c->L, s);
+  if (bf && !L.rk2 && (training || L.inference) && block_stack_fwd_supported(N, H, W, C) &&
+      !(c->variant & ASR_VARIANT_PER_BLOCK_FWD)) {
+    // C=64: all L blocks in one launch (whole images per workgroup); inference
+    // ping-pongs x_l between slots 1 and 2 with no relu masks
+    if (training) {
+      ASR_TRY(block_stack_fwd_mfma(act(0), act(1), (long)L.P, (uint8_t*)(ws + L.masks), (long)L.mask_bytes,
+                                   ws + L.wbuf, (long)L.wstride, params + L.off_blk + L.ntheta, L.blk_stride, c->h, N,
+                                   H, W, C, c->L, s));
+    } else {
+      ASR_TRY(block_stack_fwd_mfma(acts, acts + (size_t)L.P * L.act_bytes, (long)L.P, nullptr, 0, ws + L.wbuf,
+                                   (long)L.wstride, params + L.off_blk + L.ntheta, L.blk_stride, c->h, N, H, W, C,
+                                   c->L, s, 2));
+      if (xL_out) *xL_out = net_xL(c, L, ws, false, true);
+    }
+    return timed_event(c, 1, s);
   }
   for (int l = 0; l < c->L; ++l) {
     const float* bias = params + L.off_blk + (long)l * L.blk_stride + L.ntheta;
@@ -482,7 +533,7 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
                        0, s));
     }
   }
-  return ASR_OK;
+  return timed_event(c, 1, s);
 }
 
 }  // namespace asr
@@ -799,7 +850,7 @@ int asr_net_prepare(const asr_net_config* cfg, void* ws, size_t ws_bytes) {
   std::vector<int32_t> w_src((size_t)L.E), theta_dst((size_t)L.ntheta * 2);
   ASR_TRY(param_map(cfg->C, cfg->param_kind, cfg->antisymmetric, w_src.data(), theta_dst.data()));
   unsigned char* b = (unsigned char*)ws;
-  if (L.sep_bwd) {
+  if (L.sep_bwd && !L.inference) {
     std::vector<int32_t> w_bwd((size_t)L.E);
     ASR_TRY(param_map_transpose(cfg->C, w_src.data(), w_bwd.data()));
     ASR_TRY(hip_check(hipMemcpy(b + L.w_src_bwd, w_bwd.data(), w_bwd.size() * 4, hipMemcpyHostToDevice), "hipMemcpy"));
@@ -829,8 +880,8 @@ int asr_net_forward(const asr_net_config* cfg, const float* params, const void* 
   if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_net_forward: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   unsigned char* b = (unsigned char*)ws;
-  ASR_TRY(net_forward_impl(cfg, L, params, images, false, b, s));
-  const unsigned char* xL = b + L.acts + (size_t)(cfg->L & 1) * L.P * L.act_bytes;
+  unsigned char* xL = nullptr;
+  ASR_TRY(net_forward_impl(cfg, L, params, images, false, b, s, &xL));
   ASR_TRY(head(xL, cfg->dtype == ASR_BF16, params + L.off_fck, params + L.off_fcb, nullptr, cfg->N, cfg->H * cfg->W,
                cfg->C, cfg->num_classes, probs, nullptr, nullptr, nullptr, nullptr, s));
   return ASR_OK;
@@ -842,11 +893,22 @@ int asr_net_check_status(const asr_net_config* cfg, const void* ws, size_t ws_by
   if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_net_check_status: workspace too small");
   if (!L.stack_bwd) return ASR_OK;
   ASR_TRY(hip_check(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize"));
-  unsigned tmo = 0;  // done[L + 2]: the stack backward's timeout word
-  ASR_TRY(hip_check(hipMemcpy(&tmo, (const unsigned char*)ws + L.stack_done + (size_t)(cfg->L + 2) * 4, 4,
-                              hipMemcpyDeviceToHost),
-                    "hipMemcpy"));
-  if (tmo) return fail(ASR_E_DEVICE, "stacked backward: a workgroup timed out waiting for the slab hand-off");
+  return stack_status_check();  // the process-wide sticky hand-off status
+}
+
+int asr_net_kernel_times(float* us) {
+  if (!us) return fail(ASR_E_ARG, "asr_net_kernel_times: null output");
+  if (!(g_tev_rec & 3u)) return fail(ASR_E_ARG, "asr_net_kernel_times: no ASR_VARIANT_TIMED call recorded");
+  for (int i = 0; i < 3; ++i) us[i] = -1.f;
+  for (int i = 0; i < 3; ++i) {
+    const int a = i == 0 ? 0 : i + 1, e = a + 1;
+    if ((g_tev_rec >> a & 1u) && (g_tev_rec >> e & 1u)) {
+      ASR_TRY(hip_check(hipEventSynchronize(g_tev[e]), "hipEventSynchronize"));
+      float ms = 0.f;
+      ASR_TRY(hip_check(hipEventElapsedTime(&ms, g_tev[a], g_tev[e]), "hipEventElapsedTime"));
+      us[i] = ms * 1e3f;
+    }
+  }
   return ASR_OK;
 }
 
@@ -861,6 +923,8 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   unsigned char* b = (unsigned char*)ws;
   const int C = cfg->C, N = cfg->N, H = cfg->H, W = cfg->W, K = cfg->num_classes;
   const bool bf = cfg->dtype == ASR_BF16;
+  const bool stacked = L.stack_bwd && !(cfg->variant & ASR_VARIANT_PER_BLOCK_BWD);
+  if (stacked) ASR_TRY(stack_status_check());  // a previous stacked backward timed out: refuse (sticky)
   ASR_TRY(net_forward_impl(cfg, L, params, images, true, b, s));
   auto act = [&](int i) { return b + L.acts + (size_t)i * L.P * L.act_bytes; };
   // head: probabilities, per-image loss, dlogits, dL/dx_L
@@ -881,19 +945,21 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   float* pend_grp = nullptr;
   const bool fold_on = !(cfg->variant & ASR_VARIANT_NO_FOLD);               // else the reduction as separate launches
   const bool stem_v1 = (cfg->variant & ASR_VARIANT_STEM_WGRAD_VALU) != 0;  // fp32 VALU stem wgrad
+  ASR_TRY(timed_event(cfg, 2, s));  // (measurement) the blocks' backward starts
   if (L.deep) {  // C=16: all L blocks in one launch (dx resident in LDS), one slab set per layer
     int rows = 0, in_b = 0;
     float* slabs = (float*)(b + L.deep_slabs);
     ASR_TRY(deep16_backward(dcur, dnext, act(0), L.P, (const uint8_t*)(b + L.masks), L.mask_bytes,
                             b + (L.sep_bwd ? L.wbuf_bwd : L.wbuf), cfg->h, L.sep_bwd ? 0.f : 2.f * cfg->gamma, N,
                             cfg->L, slabs, &rows, &in_b, s));
+    ASR_TRY(timed_event(cfg, 3, s));
     if (in_b) std::swap(dcur, dnext);
     const int G = reduce_groups(rows);
     ASR_TRY(reduce_slabs_to_groups(slabs, cfg->L * rows, L.E + C, (float*)(b + L.grp), s));
     ASR_TRY(project_layers((float*)(b + L.grp), (long)G * (L.E + C), G, L.E, C, theta_dst, L.ntheta, cfg->L,
                            grads + L.off_blk, L.blk_stride, s));
+    ASR_TRY(timed_event(cfg, 4, s));
   }
-  const bool stacked = L.stack_bwd && !(cfg->variant & ASR_VARIANT_PER_BLOCK_BWD);
   if (stacked) {  // C=64: all L blocks in one launch, tile-major slabs
     const int grid = L.stack_grid;
     const long ES = L.E + C, sst = (long)grid * ES;
@@ -908,12 +974,14 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
                                  sst, grp, L.grp_stride, (unsigned*)(b + L.stack_done), &lfold, s,
                                  L.rk2 ? b + L.xmids : nullptr, L.rk2 ? m1 + (size_t)cfg->L * L.mask_bytes : nullptr,
                                  L.rk2 ? b + L.dxg : nullptr));
+    ASR_TRY(timed_event(cfg, 3, s));
     for (int l = std::min(lfold, cfg->L) - 1; l >= 0; --l)  // blocks below lfold: pass 1 after the launch
       ASR_TRY(reduce_slabs_to_groups(slabs + (long)l * sst, grid, ES, grp + (long)l * L.grp_stride, s));
     if (cfg->L & 1) std::swap(dcur, dnext);
     dz1_fused = ro0;
     ASR_TRY(project_layers(grp, L.grp_stride, reduce_groups(grid), L.E, C, (const int32_t*)(b + L.theta_dst_tm),
                            L.ntheta, cfg->L, grads + L.off_blk, L.blk_stride, s));
+    ASR_TRY(timed_event(cfg, 4, s));
   }
   for (int l = (L.deep || stacked) ? -1 : cfg->L - 1; l >= 0; --l) {
     const unsigned char* wl = b + (L.sep_bwd ? L.wbuf_bwd : L.wbuf) + (size_t)l * L.wstride * L.act_bytes;
@@ -946,9 +1014,12 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   }
   if (pend_P > 0) ASR_TRY(reduce_slabs_to_groups(pend_slabs, pend_P, L.E + C, pend_grp, s));
   // pass 2 of every block's weight-gradient reduction + projection onto theta, one launch
-  if (!L.deep && !stacked)
+  if (!L.deep && !stacked) {
+    ASR_TRY(timed_event(cfg, 3, s));  // (per-block kernels: their slab passes ride inside)
     ASR_TRY(project_layers((float*)(b + L.grp), L.grp_stride, reduce_groups(nsl_blk), L.E, C, theta_dst, L.ntheta,
                            cfg->L, grads + L.off_blk, L.blk_stride, s));
+    ASR_TRY(timed_event(cfg, 4, s));
+  }
   // stem: dz1 = dx1 * [x1 > 0]; conv1 weight/bias gradient from the normalised input
   const long E1 = 9L * cfg->Cin * C;
   unsigned char* sw = b + L.bwdws;

@@ -47,17 +47,8 @@
 #ifndef ASR_FWD_REUSE
 #define ASR_FWD_REUSE 1  // forward pipe: halo rows of a band continuing the previous band's image copied in LDS
 #endif
-#ifndef ASR_FWD3
-#define ASR_FWD3 1  // C=64 forward (Euler without RK2 residual, plain conv): k_fwd3 at 3 WGs per CU (0: k_fwd_pipe)
-#endif
 #ifndef ASR_FWD3_WGS
 #define ASR_FWD3_WGS 3  // k_fwd3 workgroups per CU (grid = min(bands, WGS x CUs))
-#endif
-#ifndef ASR_FWD_STACK
-#define ASR_FWD_STACK 1  // C=64 network forward: all blocks in one k_fwd3_stack launch (0: one k_fwd3 per block)
-#endif
-#ifndef ASR_BWD_STACK
-#define ASR_BWD_STACK 1  // C=64 network backward: all blocks in one k_bwd3_stack launch (0: one k_bwd3 per block)
 #endif
 #ifndef ASR_BWD3_DMA0
 #define ASR_BWD3_DMA0 16  // k_bwd3 wgrad waves: DMA pieces issued right after the barrier, the rest one per row (A/B: spreading them lengthened the MFMA phase as much as it saved; the stacks: all at once 16 vs 9 +0.3-0.5 %, 4 -0.7 %)
@@ -973,8 +964,11 @@ __global__ __launch_bounds__(256, WPE) void k_fwd3(const bf16* __restrict__ x, c
 // only the previous item's stores as still in flight), so the first band of
 // block l+1 (it reads rows -1..4 of block l's output, written by the first
 // two bands of the image) needs >= 4 bands per workgroup and block: the host
-// checks nb >= 4.  Activations are distinct buffers per block, written once
-// in this launch, so no L1 line of them can be stale.
+// checks nb >= 4.  Training: activations are distinct buffers per block,
+// written once in this launch.  Inference (slots = 2): x_{l+1} goes to slot
+// l % 2 of ys, so block l+1 overwrites x_l; a workgroup finishes every item of
+// block l (whole images, its own) before it writes block l+1, and its own
+// stores and DMA reads meet in its CU's L1, so no line can be stale either.
 // ===========================================================================
 // RK2 (BASELINE config 5): 2L stages, stage 2l = the first (x_l -> xmid_l, h/2,
 // mask1), stage 2l+1 the second (xmid_l -> x_{l+1}, h, mask2) with the residual
@@ -984,7 +978,8 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
                                                        long y_stride, uint8_t* __restrict__ masks, long mask_stride,
                                                        const bf16* __restrict__ wpack, long w_stride,
                                                        const float* __restrict__ bias, long bias_stride, float h,
-                                                       int N, int H, int L, bf16* __restrict__ xm = nullptr,
+                                                       int N, int H, int L, int slots,
+                                                       bf16* __restrict__ xm = nullptr,
                                                        uint8_t* __restrict__ masks2 = nullptr) {
   using G = Geo<C>;
   constexpr int TW = W + 2, NQ = G::NQ, OT = C / 16, NW = 4, RB = BR;
@@ -1003,14 +998,16 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
   const int nb = (H + BR - 1) / BR, per = (n1 - n0) * nb;  // items per block
   // items walk stages (blocks, or RK2 half steps): block, input, output, mask, step of stage st
   auto blk_of = [&](int st) { return RK2 ? st >> 1 : st; };
-  auto xin_of = [&](int l) -> const bf16* { return l == 0 ? x0 : ys + (long)(l - 1) * y_stride; };
+  // slots: 0 = one buffer per block (training), 2 = ping-pong (inference; Euler only)
+  auto slot_of = [&](int l) -> long { return slots > 0 ? (long)(l % slots) : (long)l; };
+  auto xin_of = [&](int l) -> const bf16* { return l == 0 ? x0 : ys + slot_of(l - 1) * y_stride; };
   auto src_of = [&](int st) -> const bf16* {
     if constexpr (RK2) return (st & 1) ? xm + (long)(st >> 1) * y_stride : xin_of(st >> 1);
     else return xin_of(st);
   };
   auto out_of = [&](int st) -> bf16* {
     if constexpr (RK2) return ((st & 1) ? ys : xm) + (long)(st >> 1) * y_stride;
-    else return ys + (long)st * y_stride;
+    else return ys + slot_of(st) * y_stride;
   };
   auto mask_of = [&](int st) -> uint8_t* {
     uint8_t* m = (RK2 && (st & 1)) ? masks2 : masks;
@@ -2184,17 +2181,25 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
 //     write-through publish);
 //   * pass 1 of block l's reduction (32-slab group sums, as k_bwd3's fold) is
 //     folded into this workgroup's bands of block l-2: one lane polls done[l]
-//     == gridDim.x before the first of them (bounded; a timeout sets *tmo) and
+//     == gridDim.x before the first of them (bounded by kStackSpinLimit sleeps; a
+//     timeout stores 1 into the process-wide mapped status word *tmo, which the
+//     host keeps as a sticky ASR_E_DEVICE, see stack_status_check) and
 //     fences acquire at agent scope, and the band barrier orders that before
 //     every slab load.  Blocks below lfold (>= 2; L when a workgroup would
 //     own more than 512 chunks of the group rows, one per wgrad thread) are
 //     reduced after the launch.
 // The grid must be co-resident (one 768-thread workgroup per CU, grid <= CUs):
-// the host sizes it so.  At the switch to block l-1 the dgrad waves load its W
+// the host sizes it so and uses the stacked path only when the occupancy
+// query keeps at least one workgroup resident per CU.  At the switch to block l-1 the dgrad waves load its W
 // after their last conv of block l; block 0 applies the stem's relu' to dx
 // when ro0 (k_bwd3<..., RO>).
 // ===========================================================================
 typedef __attribute__((address_space(1))) unsigned gu32;  // global agent-scope words (never flat)
+// bound of the stacked backward's slab wait, in polls of one relaxed L2 load
+// + s_sleep 2 (0.3-0.6 s: thousands of times the skew between workgroups of
+// one launch).  A compile-time constant: a run-time bound cost the kernel a
+// spilled register (tests/test_isa.py)
+constexpr unsigned kStackSpinLimit = 1u << 21;
 typedef __attribute__((address_space(1))) float gf32;
 
 // RK2 (config 5): items walk 2L stages, per block l its second stage first
@@ -2527,7 +2532,8 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         unsigned spins = 0;
         while (__hip_atomic_load((gu32*)(done + l + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
           __builtin_amdgcn_s_sleep(2);
-          if (++spins > (1u << 24)) {
+          if (++spins > kStackSpinLimit) {
+            // (fine-grained host memory: the store bypasses L2; the end-of-kernel release makes it host-visible)
             __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
           }
@@ -2927,7 +2933,7 @@ static int launch_fwd_v(int mode, const void* x, const void* resid, void* y, uin
   const int grid = (int)std::max<long>(1, std::min<long>(items, (long)cus * (8 / NW)));
   const size_t lds = 2 * (size_t)(BR + 2) * (W + 2) * C * 2;
   if constexpr (C == 64 && W == 32 && BR == 4 && NW == 4) {
-    if (ASR_FWD3 && (!resid || mode == blk::FWD_EULER)) {
+    if (!resid || mode == blk::FWD_EULER) {
       const int grid3 = (int)std::max<long>(1, std::min<long>(items, (long)cus * ASR_FWD3_WGS));
       if (mode == blk::FWD_EULER && resid)
         hipLaunchKernelGGL((blk::k_fwd3<C, W, BR, blk::FWD_EULER, 3, true>), dim3(grid3), dim3(256), lds, s,
@@ -3109,29 +3115,55 @@ int block_stack_fwd_rk2_mfma(const void* x0, void* ys, void* xm, long y_stride, 
                              float h, int N, int H, int W, int C, int L, hipStream_t s);
 
 bool block_stack_fwd_supported(int N, int H, int W, int C) {
-  return ASR_FWD_STACK && C == 64 && W == 32 && N >= 1 && (H + kFwdBR - 1) / kFwdBR >= 4;
+  return C == 64 && W == 32 && N >= 1 && (H + kFwdBR - 1) / kFwdBR >= 4;
 }
 
 // all L Euler blocks in one launch (k_fwd3_stack); x_l of block l >= 1 is
 // ys + (l-1)*y_stride, its output ys + l*y_stride (elements)
 int block_stack_fwd_mfma(const void* x0, void* ys, long y_stride, uint8_t* masks, long mask_stride, const void* w,
                          long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C, int L,
-                         hipStream_t s) {
+                         hipStream_t s, int slots) {
   if (!block_stack_fwd_supported(N, H, W, C) || L < 1)
     return fail(ASR_E_UNSUPPORTED, "stack forward: needs C=64, W=32, >= 4 row bands per image (C=%d W=%d H=%d)", C, W, H);
   if (y_stride < (long)N * H * W * C) return fail(ASR_E_ARG, "stack forward: y_stride smaller than one activation");
+  if (slots != 0 && slots != 2) return fail(ASR_E_ARG, "stack forward: slots must be 0 or 2");
   int cus = cu_count();
   if (cus <= 0) cus = 256;
   const int grid = std::max(1, std::min(N, 2 * cus));
   const size_t lds = 2 * (size_t)(kFwdBR + 2) * (W + 2) * C * 2;
   hipLaunchKernelGGL((blk::k_fwd3_stack<64, 32, kFwdBR>), dim3(grid), dim3(256), lds, s, (const bf16*)x0, (bf16*)ys,
-                     y_stride, masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, H, L);
+                     y_stride, masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, H, L, slots);
   ASR_LAUNCH_CHECK("k_fwd3_stack");
   return ASR_OK;
 }
 
+// test knobs (asr_debug_stack_backward): a forced grid (0: one workgroup per
+// CU) and the bound of the slab hand-off's wait (0: the default)
+static int g_stack_grid_override = 0;
+
+// k_bwd3_stack workgroups the device keeps resident per CU (both
+// instantiations; cached per device): the in-launch hand-off needs the whole
+// grid resident, so the stacked path is used only when this is >= 1
+static int stack_bwd_resident_per_cu() {
+  static int dev_cached = -1, per = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (dev != dev_cached) {
+    using L2 = blk::Bwd2Lds<64, 32, kBwdBR>;
+    int a = 0, b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, blk::k_bwd3_stack<64, 32, kBwdBR, false>, 768,
+                                                     (size_t)L2::TOTAL) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, blk::k_bwd3_stack<64, 32, kBwdBR, true>, 768,
+                                                     (size_t)L2::TOTAL) != hipSuccess)
+      return 0;
+    per = std::min(a, b);
+    dev_cached = dev;
+  }
+  return per;
+}
+
 bool block_stack_bwd_supported(int N, int H, int W, int C) {
-  return ASR_BWD_STACK && C == 64 && W == 32 && N >= 1 && (H + kBwdBR - 1) / kBwdBR >= 4;
+  return C == 64 && W == 32 && N >= 1 && (H + kBwdBR - 1) / kBwdBR >= 4 && stack_bwd_resident_per_cu() >= 1;
 }
 
 // workgroups of k_bwd3_stack: one per CU at most (the in-launch slab
@@ -3139,14 +3171,16 @@ bool block_stack_bwd_supported(int N, int H, int W, int C) {
 int block_stack_bwd_grid(int N) {
   int cus = cu_count();
   if (cus <= 0) cus = 256;
-  return std::max(1, std::min(N, std::min(cus, kMaxBlockSlabs)));
+  const int cap = g_stack_grid_override > 0 ? g_stack_grid_override : cus;
+  return std::max(1, std::min(N, std::min(cap, kMaxBlockSlabs)));
 }
 
 // the backward of L Euler blocks in one launch (k_bwd3_stack).  dbuf0 holds
 // dL/dx_L on entry; block 0's dx ends in dbuf[L & 1].  Block l's slabs (grid
 // of them, tile-major dW) at slabs + l*slab_stride; blocks >= 2 leave as
 // 32-slab group sums at grp + l*grp_stride, blocks 1 and 0 as slabs.  done:
-// L + 4 zeroed words (counters + timeout flag), reset here.
+// L + 4 words (the per-block publish counters), zeroed here.  Refused while
+// the sticky hand-off status is set (a previous launch timed out).
 int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride, const uint8_t* masks,
                          long mask_stride, const void* w, long w_stride, float h, float two_gamma, int N, int H, int W,
                          int C, int L, int ro0, float* slabs, long slab_stride, float* grp, long grp_stride,
@@ -3160,18 +3194,21 @@ int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride
   const long fchunks = (long)((grid + 31) / 32) * ((9L * C * C + C) / 4);
   const int lfold = (fchunks + grid - 1) / grid <= 512 ? 2 : L;
   if (lfold_out) *lfold_out = lfold;
+  ASR_TRY(stack_status_check());
+  unsigned* tmo = stack_status_device();
+  if (!tmo) return ASR_E_HIP;
   ASR_TRY(hip_check(hipMemsetAsync(done, 0, align_up((size_t)(L + 4) * 4, 16), s), "hipMemsetAsync"));
   using L2 = blk::Bwd2Lds<64, 32, kBwdBR>;
   if (xm) {  // RK2: both stages of every block (x_mid stack at xm, stride x_stride; masks2; g scratch)
     if (!masks2 || !gbuf) return fail(ASR_E_ARG, "stack backward (RK2): masks2 and the g buffer are required");
     hipLaunchKernelGGL((blk::k_bwd3_stack<64, 32, kBwdBR, true>), dim3(grid), dim3(768), (size_t)L2::TOTAL, s,
                        (bf16*)dbuf0, (bf16*)dbuf1, (const bf16*)xs, x_stride, masks, mask_stride, (const bf16*)w,
-                       w_stride, h, two_gamma, N, H, L, 0, slabs, slab_stride, grp, grp_stride, done, done + L + 2,
+                       w_stride, h, two_gamma, N, H, L, 0, slabs, slab_stride, grp, grp_stride, done, tmo,
                        lfold, (const bf16*)xm, masks2, (bf16*)gbuf);
   } else {
     hipLaunchKernelGGL((blk::k_bwd3_stack<64, 32, kBwdBR>), dim3(grid), dim3(768), (size_t)L2::TOTAL, s,
                        (bf16*)dbuf0, (bf16*)dbuf1, (const bf16*)xs, x_stride, masks, mask_stride, (const bf16*)w,
-                       w_stride, h, two_gamma, N, H, L, ro0, slabs, slab_stride, grp, grp_stride, done, done + L + 2,
+                       w_stride, h, two_gamma, N, H, L, ro0, slabs, slab_stride, grp, grp_stride, done, tmo,
                        lfold);
   }
   ASR_LAUNCH_CHECK("k_bwd3_stack");
@@ -3189,7 +3226,7 @@ int block_stack_fwd_rk2_mfma(const void* x0, void* ys, void* xm, long y_stride, 
   const int grid = std::max(1, std::min(N, 2 * cus));
   const size_t lds = 2 * (size_t)(kFwdBR + 2) * (W + 2) * C * 2;
   hipLaunchKernelGGL((blk::k_fwd3_stack<64, 32, kFwdBR, true>), dim3(grid), dim3(256), lds, s, (const bf16*)x0,
-                     (bf16*)ys, y_stride, masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, H, L,
+                     (bf16*)ys, y_stride, masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, H, L, 0,
                      (bf16*)xm, masks2);
   ASR_LAUNCH_CHECK("k_fwd3_stack<RK2>");
   return ASR_OK;
@@ -3218,6 +3255,16 @@ int block_bwd_mfma(int mode, const void* dy, const void* x, const uint8_t* mask,
 }
 
 }  // namespace asr
+
+// test knob: force the stacked backward's grid (a grid larger than the
+// resident capacity makes the in-launch hand-off time out); 0 restores the
+// default (one workgroup per CU)
+extern "C" int asr_debug_stack_backward(int grid) {
+  if (grid < 0 || grid > asr::kMaxBlockSlabs)
+    return asr::fail(ASR_E_ARG, "asr_debug_stack_backward: grid must be in 0..%d", asr::kMaxBlockSlabs);
+  asr::g_stack_grid_override = grid;
+  return ASR_OK;
+}
 
 #if ASR_STAMP_BUILD
 extern "C" int asr_debug_stamps(void* host, size_t bytes) {

@@ -257,8 +257,10 @@ class NativeModel:
         self._host_stale = True
 
     # -- execution ---------------------------------------------------------------
-    def executor(self, batch_size: int, dtype, input_u8: bool):
-        key = (int(batch_size), dtype, bool(input_u8))
+    def executor(self, batch_size: int, dtype, input_u8: bool, inference: bool = False):
+        """The executor for (batch, dtype, input kind); inference=True gives the
+        forward-only one (bounded workspace: x_0 + two activation slots)."""
+        key = (int(batch_size), dtype, bool(input_u8), bool(inference))
         ex = self._executors.get(key)
         if ex is None:
             p = self.plan
@@ -266,7 +268,7 @@ class NativeModel:
                                       subtract_mean=p.subtract_mean, divide_by_stddev=p.divide_by_stddev,
                                       dtype=dtype, input_u8=input_u8, device=self.device,
                                       param_kind=p.param_kind, antisymmetric=p.antisymmetric,
-                                      integrator=p.integrator)
+                                      integrator=p.integrator, inference=inference)
             if ex.n_params != self.n_params:
                 raise _lib.AsrError(f"executor expects {ex.n_params} parameters, model has {self.n_params}")
             self._executors[key] = ex
@@ -313,26 +315,31 @@ class NativeView:
     def matches(self, batch_size, dtype):
         return self.batch_size == int(batch_size) and self.dtype == dtype
 
-    def executor(self, input_u8: bool):
-        return self.state.executor(self.batch_size, self.dtype, input_u8)
+    def executor(self, input_u8: bool, inference: bool = False):
+        return self.state.executor(self.batch_size, self.dtype, input_u8, inference)
 
     def predict(self, x):
         """Softmax outputs [n, K] (numpy) for n images, in batches of
-        batch_size (the last batch is zero-padded)."""
+        batch_size (the last batch is zero-padded), on the forward-only
+        executor: device memory is one batch of images plus the inference
+        workspace, whatever n is (host arrays are copied batch by batch)."""
         torch = self._torch
-        x = self._images(x)
+        if isinstance(x, np.ndarray):
+            x = torch.from_numpy(np.ascontiguousarray(x))
+        if x.dtype not in (torch.uint8, torch.float32):
+            x = x.float()
         n = int(x.shape[0])
-        ex = self.executor(x.dtype == torch.uint8)
-        out = []
+        ex = self.executor(x.dtype == torch.uint8, inference=True)
+        out = np.empty((n, ex.cfg.num_classes), dtype=np.float32)
         B = self.batch_size
+        buf = torch.zeros((B,) + tuple(x.shape[1:]), dtype=x.dtype, device=self.device)
         for i in range(0, n, B):
-            chunk = x[i:i + B]
-            if chunk.shape[0] < B:
-                pad = torch.zeros((B,) + tuple(chunk.shape[1:]), dtype=chunk.dtype, device=chunk.device)
-                pad[:chunk.shape[0]] = chunk
-                chunk = pad
-            out.append(ex.forward(self.params, chunk)[: min(B, n - i)].clone())
-        return torch.cat(out).cpu().numpy()
+            m = min(B, n - i)
+            buf[:m].copy_(x[i:i + m])
+            if m < B:
+                buf[m:].zero_()
+            out[i:i + m] = ex.forward(self.params, buf)[:m].cpu().numpy()
+        return out
 
     def forward_backward(self, images, targets, want_probs=False):
         """(loss, grads, probs): loss [1] and grads [n_params] are views of

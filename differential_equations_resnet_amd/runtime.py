@@ -15,12 +15,21 @@ from . import _lib
 from ._lib import (ASR_BF16, ASR_F32, ASR_INTEGRATOR_EULER, ASR_INTEGRATOR_RK2, ASR_MODE_CONV, ASR_MODE_EULER,
                    ASR_PARAM_3BY3, ASR_PARAM_GENERAL, ASR_PARAM_REGULAR, ASR_VARIANT_NO_FOLD, ASR_VARIANT_STEM_FWD_VALU,
                    ASR_VARIANT_STEM_WGRAD_VALU, ASR_VARIANT_PER_BLOCK_FWD,
-                   ASR_VARIANT_PER_BLOCK_BWD, NetConfig)
+                   ASR_VARIANT_PER_BLOCK_BWD, ASR_VARIANT_INFERENCE, ASR_VARIANT_TIMED, NetConfig)
 
 __all__ = [
     "require_gpu", "dtype_code", "torch_dtype", "ParamMap", "param_map", "theta_count", "theta_to_w",
-    "conv_forward", "block_stack_forward", "block_stack_backward", "conv_backward", "rk2_forward", "rk2_backward", "integrator_code", "NetExecutor", "adam_update",
+    "conv_forward", "block_stack_forward", "block_stack_backward", "conv_backward", "rk2_forward", "rk2_backward",
+    "integrator_code", "NetExecutor", "adam_update", "stack_status",
 ]
+
+
+def stack_status(reset: bool = False) -> bool:
+    """Non-blocking: True when a C=64 stacked backward of this process timed
+    out waiting for another workgroup's weight-gradient slabs (sticky; every
+    later stacked backward refuses to run until reset).  reset clears it."""
+    rc = _lib.load().asr_stack_status(int(bool(reset)))
+    return rc == _lib.ASR_E_DEVICE
 
 
 def integrator_code(integrator) -> int:
@@ -337,11 +346,14 @@ class NetExecutor:
     """Native executor of the single-block antisymmetric ResNet
     (asr_net_* in include/asr.h).  Owns the device workspace; parameters,
     gradients and Adam moments are flat float32 buffers in Keras
-    get_weights() order."""
+    get_weights() order.  inference=True builds the forward-only workspace
+    (ASR_VARIANT_INFERENCE: x_0 and two ping-pong activation slots)."""
 
     def __init__(self, N, H, W, Cin, C, L, num_classes, h, gamma=0.0, subtract_mean=None, divide_by_stddev=None,
                  dtype="bfloat16", input_u8=True, device=None, param_kind=ASR_PARAM_3BY3, antisymmetric=True,
-                 integrator="euler", variant=0):
+                 integrator="euler", variant=0, inference=False):
+        if inference:
+            variant |= ASR_VARIANT_INFERENCE
         self.device = device or require_gpu()
         use_norm = subtract_mean is not None or divide_by_stddev is not None
         self.cfg = NetConfig(int(N), int(H), int(W), int(Cin), int(C), int(L), int(num_classes), float(h),
@@ -358,7 +370,8 @@ class NetExecutor:
             _lib.check(_lib.ASR_E_ARG, "asr_net_workspace_bytes")
         self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
         _lib.call("asr_net_prepare", ct.byref(self.cfg), _p(self.ws), self.ws_bytes)
-        self.grads = torch.zeros(self.n_params, dtype=torch.float32, device=self.device)
+        self.inference = bool(inference)
+        self.grads = None if inference else torch.zeros(self.n_params, dtype=torch.float32, device=self.device)
         self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.probs = torch.zeros(N, num_classes, dtype=torch.float32, device=self.device)
 
@@ -386,11 +399,26 @@ class NetExecutor:
         self.cfg.variant = int(bits)
 
     def check_status(self):
-        """Blocking: raises if the last forward_backward's in-launch slab hand-off
-        (the C=64 stacked backward) timed out (asr_net_check_status)."""
+        """Blocking: raises AsrError if a stacked backward of this process
+        (the C=64 in-launch slab hand-off) timed out (asr_net_check_status;
+        sticky, see stack_status)."""
         _lib.call("asr_net_check_status", ct.byref(self.cfg), _p(self.ws), self.ws_bytes, _stream())
 
+    @staticmethod
+    def kernel_times() -> dict:
+        """Blocking: device microseconds of the block launches of the last
+        call made with ASR_VARIANT_TIMED (asr_net_kernel_times): "fwd" the
+        blocks' forward, "bwd" the blocks' backward kernels (the one stack
+        launch where one runs), "bwd_reduce" the weight-gradient reductions
+        left after them + the projection (None where that call ran no such
+        part)."""
+        out = (ct.c_float * 3)()
+        _lib.call("asr_net_kernel_times", ct.cast(out, ct.c_void_p))
+        return {k: (float(v) if v >= 0 else None) for k, v in zip(("fwd", "bwd", "bwd_reduce"), out)}
+
     def forward_backward(self, params, images, targets, want_probs=False):
+        if self.inference:
+            raise ValueError("an inference executor has no backward")
         self._check_inputs(params, images)
         if tuple(targets.shape) != (self.cfg.N, self.cfg.num_classes) or targets.dtype != torch.float32:
             raise ValueError("targets must be float32 one-hot [N, num_classes]")

@@ -252,6 +252,15 @@ class Training:
         self.variables_updated = True
         return norms
 
+    def _check_device_status(self):
+        """Once per epoch, after a synchronising read: the C=64 stacked
+        backward's in-launch slab hand-off never timed out (a timeout means
+        incomplete block gradients; the status is sticky, runtime.stack_status)."""
+        from .. import _lib, runtime
+        if runtime.stack_status():
+            raise _lib.AsrError("stacked backward: a workgroup timed out waiting for the weight-gradient hand-off; "
+                                "the block gradients of at least one step were incomplete")
+
     def train(self, epochs, steps_per_epoch, learning_rate_schedule, eval_dataset="train", eval_frequency=5,
               eval_steps=None, save_during_training=False, save_dir=None, save_best_only=True, save_tags=["default"],
               save_name="", save_frequency=5, saver="train_saver", monitor="loss", summaries_frequency=10):
@@ -285,7 +294,8 @@ class Training:
                         self.csv_file_train.flush()
                     tr.set_postfix(dict(zip(self.metric_names + ["global_step"], vals + [self.g_step])))
                 lr = learning_rate_schedule(self.g_step)
-            self.training_loss = self._metric_values()[0]
+            self.training_loss = self._metric_values()[0]  # (reads the device metrics: synchronises)
+            self._check_device_status()
             evaluated = eval_frequency is not None and epoch % eval_frequency == 0
             if evaluated:
                 desc = "Evaluation on training dataset" if eval_dataset == "train" else \
@@ -334,7 +344,7 @@ class Training:
             images = self.native._images(images)
             labels = self._targets(labels)
             if ex_u8 is None:
-                ex_u8 = self.native.executor(images.dtype == self._torch.uint8)
+                ex_u8 = self.native.executor(images.dtype == self._torch.uint8, inference=True)
             probs = ex_u8.forward(self.native.params, images)
             runtime.batch_metrics(probs, labels, None, self._accum)
         self.metric_values = self._metric_values()

@@ -265,6 +265,12 @@ typedef struct asr_net_config {
 #define ASR_VARIANT_PER_BLOCK_BWD 16 /* C=64 bf16 Euler backward: one k_bwd3 launch
                                         per block (slab pass folded into the
                                         next one) instead of k_bwd3_stack     */
+#define ASR_VARIANT_INFERENCE 32  /* forward-only workspace: x_0 and two ping-pong
+                                     activation slots, no masks / backward
+                                     buffers (asr_net_forward only; the C=64 bf16
+                                     blocks run as one k_fwd3_stack launch)     */
+#define ASR_VARIANT_TIMED 64      /* record HIP events around the block launches
+                                     (measurement; asr_net_kernel_times)       */
 
 long asr_net_param_count(const asr_net_config* cfg);
 size_t asr_net_workspace_bytes(const asr_net_config* cfg);
@@ -279,11 +285,36 @@ int asr_net_forward(const asr_net_config* cfg, const float* params, const void* 
 int asr_net_forward_backward(const asr_net_config* cfg, const float* params, const void* images,
                              const float* targets, float* grads, float* loss, float* probs,
                              void* ws, size_t ws_bytes, asr_stream_t stream);
-/* Host, blocking (synchronises the stream): ASR_OK, or ASR_E_DEVICE when the
- * last asr_net_forward_backward on this workspace stopped waiting for another
- * workgroup's weight-gradient slabs (the bounded in-launch hand-off of the
- * C=64 stacked backward timed out: its block gradients are then incomplete). */
+/* Host, blocking (synchronises the stream): ASR_OK, or ASR_E_DEVICE when a
+ * stacked backward of this process stopped waiting for another workgroup's
+ * weight-gradient slabs (the bounded in-launch hand-off of the C=64 stacked
+ * backward timed out: its block gradients were incomplete).  The status is
+ * sticky (see asr_stack_status). */
 int asr_net_check_status(const asr_net_config* cfg, const void* ws, size_t ws_bytes, asr_stream_t stream);
+
+/* Host, blocking: device times in microseconds of the last asr_net_forward /
+ * asr_net_forward_backward called with ASR_VARIANT_TIMED: us[0] the L blocks'
+ * forward (the single stack launch where one runs), us[1] the L blocks'
+ * backward kernels (the single stack launch k_bwd3_stack / k_bwd16_fused
+ * where one runs), us[2] the weight-gradient reductions left after them and
+ * the projection onto theta; -1 for a part that call did not run. */
+int asr_net_kernel_times(float* us);
+
+/* Host, non-blocking: the process-wide status of the C=64 stacked backward's
+ * in-launch slab hand-off (k_bwd3_stack).  A workgroup whose bounded wait runs
+ * out sets it from the device (a pinned, mapped host word); it stays set, and
+ * asr_net_forward_backward / asr_block_stack_backward / asr_rk2_stack_backward
+ * return ASR_E_DEVICE without launching while it is set.  Returns ASR_OK or
+ * ASR_E_DEVICE as it stands (launches still in flight may set it later:
+ * synchronise first for a final answer); reset != 0 then clears it.  The grid
+ * of the stacked backward is one workgroup per CU and the path is used only
+ * when the occupancy query keeps one resident per CU. */
+int asr_stack_status(int reset);
+/* Test knob: force the stacked backward's grid (0: one workgroup per CU;
+ * larger than the resident capacity makes the hand-off time out after its
+ * bounded wait, 0.3-0.6 s).  Workspace sizes depend on the grid: query them
+ * after setting it. */
+int asr_debug_stack_backward(int grid);
 
 /* tf.train.AdamOptimizer.apply_gradients (training.py:300-301), TF1
  * epsilon-hat form; step is the 1-based update count; g is multiplied by

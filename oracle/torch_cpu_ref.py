@@ -15,7 +15,9 @@ reference slow:
     (…3By3.py:168-169, models/tfkeras_resnets.py:89-92);
   * loss = mean Keras categorical cross-entropy on softmax probabilities
     (training/training.py:295), TF1 Adam with epsilon 1e-7 (training.py:300-301).
-Everything is float32, like the reference.
+Everything is float32, like the reference (dtype=torch.float64 gives the
+same graph in double precision: the full-size fp32 parity check of BASELINE
+C1 in tests/test_gpu_fullsize.py).
 
 RefNet(..., assembly="vectorised") replaces the per-step op-by-op assembly by
 one gather W = sign * theta[src] (the closed form W = P - P* + gamma*I of
@@ -85,7 +87,8 @@ def conv2d_nhwc_same(x, w_hwio):
 class RefNet:
     """antisymmetric single-block ResNet (tfkeras_resnets.py:547-597) in float32."""
 
-    def __init__(self, params_np, C, L, h, gamma=0.0, num_classes=10, mean=127.5, std=127.5, assembly="reference"):
+    def __init__(self, params_np, C, L, h, gamma=0.0, num_classes=10, mean=127.5, std=127.5, assembly="reference",
+                 dtype=torch.float32):
         if assembly not in ("reference", "vectorised"):
             raise ValueError(assembly)
         self.C, self.L, self.h, self.gamma, self.K = C, L, h, gamma, num_classes
@@ -94,10 +97,11 @@ class RefNet:
             from .asr_oracle import param_map
             src, sign = param_map(C)
             self._src = torch.from_numpy(np.maximum(src, 0))
-            self._sign = torch.from_numpy(sign.astype(np.float32))
+            self._sign = torch.from_numpy(sign.astype(np.float32)).to(dtype)
             self._is_gamma = torch.from_numpy(src < 0)
         self.mean, self.std = mean, std
-        self.params = [torch.tensor(np.asarray(p, dtype=np.float32), requires_grad=True) for p in params_np]
+        self.dtype = dtype
+        self.params = [torch.tensor(np.asarray(p), dtype=dtype, requires_grad=True) for p in params_np]
         self.m = [torch.zeros_like(p) for p in self.params]
         self.v = [torch.zeros_like(p) for p in self.params]
         self.t = 0
@@ -113,7 +117,7 @@ class RefNet:
 
     def forward(self, images_u8):
         c1k, c1b, blocks, fck, fcb = self._split()
-        x = torch.as_tensor(images_u8).float()
+        x = torch.as_tensor(images_u8).to(self.dtype)
         x = x - self.mean
         x = x / self.std
         x = conv2d_nhwc_same(x.contiguous(), c1k) + c1b
@@ -121,7 +125,7 @@ class RefNet:
         for theta, b in blocks:
             if self.assembly == "vectorised":
                 flat = torch.cat([t.reshape(-1) for t in theta])
-                W = torch.where(self._is_gamma, torch.full((), self.gamma), self._sign * flat[self._src])
+                W = torch.where(self._is_gamma, torch.full((), self.gamma, dtype=self.dtype), self._sign * flat[self._src])
                 W = W.view(3, 3, self.C, self.C)
             else:
                 a, bb, c, d = theta[:4]
@@ -142,9 +146,19 @@ class RefNet:
         out = torch.clamp(out, 1e-7, 1.0 - 1e-7)
         return -(onehot * torch.log(out)).sum(dim=-1)
 
+    def loss_and_grads(self, images_u8, onehot):
+        """(probs, batch-mean loss, gradients in Keras weight order) without
+        an optimizer step."""
+        probs = self.forward(images_u8)
+        loss = self.keras_cce(probs, torch.as_tensor(onehot, dtype=self.dtype)).mean()
+        for p in self.params:
+            p.grad = None
+        loss.backward()
+        return (probs.detach().numpy(), float(loss.detach()), [p.grad.detach().numpy().copy() for p in self.params])
+
     def train_step(self, images_u8, onehot, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-7):
         probs = self.forward(images_u8)
-        loss = self.keras_cce(probs, torch.as_tensor(onehot, dtype=torch.float32)).mean()
+        loss = self.keras_cce(probs, torch.as_tensor(onehot, dtype=self.dtype)).mean()
         for p in self.params:
             p.grad = None
         loss.backward()

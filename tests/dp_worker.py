@@ -4,7 +4,13 @@ this rank's slice of a fixed global batch, the gradient all-reduce through
 the package's distributed layer (backend from argv), one Adam step with
 grad_scale 1/world; results to <outdir>/r<rank>.npz.
 
-usage: python -m torch.distributed.run --nproc-per-node 2 ... tests/dp_worker.py OUTDIR BACKEND
+usage: python -m torch.distributed.run --nproc-per-node 2 ... tests/dp_worker.py OUTDIR BACKEND [CASE]
+
+CASE "small" (default): fp32, C=16, L=2, 4 images per rank (the per-block
+fp32 kernels).  CASE "c2": BASELINE C4's per-rank composition at a reduced
+depth: bf16, C=64, L=3, 192 images per rank, so every rank runs the stacked
+kernels (k_fwd3_stack / k_bwd3_stack, several images per workgroup, the
+in-launch slab fold) before the all-reduce.
 """
 import os
 import sys
@@ -14,7 +20,16 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-C, L, B, H = 16, 2, 4, 0.5  # per-rank batch B
+CASES = {  # C, L, per-rank batch B, h, activation dtype
+    "small": (16, 2, 4, 0.5, "float32"),
+    "c2": (64, 3, 192, 8.0 / 30, "bfloat16"),
+}
+C, L, B, H, DTYPE = CASES["small"]
+
+
+def use_case(name):
+    global C, L, B, H, DTYPE
+    C, L, B, H, DTYPE = CASES[name]
 
 
 def global_batch(world):
@@ -31,6 +46,7 @@ def params0(seed):
 
 def main():
     outdir, backend = sys.argv[1], sys.argv[2]
+    use_case(sys.argv[3] if len(sys.argv) > 3 else "small")
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     if backend == "rccl" and os.environ.get("ASR_TEST_SPLIT_HOSTID"):
         # two ranks on ONE device: RCCL refuses a duplicate GPU within a host,
@@ -47,7 +63,7 @@ def main():
     imgs, onehot = global_batch(world)
     sl = slice(rank * B, (rank + 1) * B)
     ex = rt.NetExecutor(B, 32, 32, 3, C, L, 10, H, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
-                        dtype="float32", input_u8=True, device=dev)
+                        dtype=DTYPE, input_u8=True, device=dev)
     loss, grads = ex.forward_backward(params, torch.from_numpy(imgs[sl]).to(dev), torch.from_numpy(onehot[sl]).to(dev))
     p_before = params.cpu().numpy()
     distributed.allreduce_grads(grads)

@@ -150,3 +150,31 @@ def test_transposed_operator_map(lib, kind, anti):
         assert rc == 0
         Wb = (th[wb >> 1] * np.where(wb & 1, -1.0, 1.0)).reshape(3, 3, C, C)
         assert np.array_equal(Wb, want)
+
+
+def test_status_and_measurement_entry_points_without_gpu(lib):
+    """The sticky stacked-backward status reads clean before any launch;
+    kernel times need a recorded ASR_VARIANT_TIMED call; the test knob
+    checks its range (no kernel launches here)."""
+    from differential_equations_resnet_amd import _lib
+    assert lib.asr_stack_status(0) == 0 and lib.asr_stack_status(1) == 0
+    out = (ct.c_float * 3)()
+    assert lib.asr_net_kernel_times(ct.cast(out, ct.c_void_p)) == _lib.ASR_E_ARG
+    assert lib.asr_debug_stack_backward(-1) == _lib.ASR_E_ARG
+    assert lib.asr_debug_stack_backward(513) == _lib.ASR_E_ARG
+    assert lib.asr_debug_stack_backward(0) == 0
+
+
+def test_inference_workspace_is_bounded(lib):
+    """ASR_VARIANT_INFERENCE: x_0 + two activation slots instead of L+1
+    activations, masks and backward buffers; unknown variant bits fail."""
+    from differential_equations_resnet_amd import _lib
+    for C, L, dt in ((64, 30, 1), (16, 18, 0), (16, 108, 1)):
+        tr = _lib.NetConfig(512, 32, 32, 3, C, L, 10, 8 / L, 0.0, 127.5, 127.5, 1, dt, 1, 0, 1, 0, 0)
+        inf = _lib.NetConfig(512, 32, 32, 3, C, L, 10, 8 / L, 0.0, 127.5, 127.5, 1, dt, 1, 0, 1, 0,
+                             _lib.ASR_VARIANT_INFERENCE)
+        a, b = lib.asr_net_workspace_bytes(ct.byref(tr)), lib.asr_net_workspace_bytes(ct.byref(inf))
+        act = 512 * 32 * 32 * C * (2 if dt else 4)
+        assert 0 < b < a and b < 3 * act + 64 * 2 ** 20, (C, L, a, b)
+    bad = _lib.NetConfig(512, 32, 32, 3, 64, 30, 10, 0.1, 0.0, 127.5, 127.5, 1, 1, 1, 0, 1, 0, 1 << 12)
+    assert lib.asr_net_workspace_bytes(ct.byref(bad)) == 0

@@ -40,7 +40,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _launch(outdir, backend, extra_env=None, timeout=90):
+def _launch(outdir, backend, extra_env=None, timeout=90, case="small"):
     """Run the two ranks in their own process group; on a hang the whole
     group (launcher and ranks) is killed."""
     env = dict(os.environ)
@@ -48,7 +48,7 @@ def _launch(outdir, backend, extra_env=None, timeout=90):
     env.update(extra_env or {})
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(HERE, "dp_worker.py"),
-           str(outdir), backend]
+           str(outdir), backend, case]
     p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
                          start_new_session=True)
     try:
@@ -60,8 +60,9 @@ def _launch(outdir, backend, extra_env=None, timeout=90):
     return p.returncode, out
 
 
-def _check(outdir):
+def _check(outdir, case="small"):
     from differential_equations_resnet_amd import runtime as rt
+    W.use_case(case)
     r = [np.load(os.path.join(outdir, f"r{i}.npz")) for i in range(2)]
     np.testing.assert_array_equal(r[0]["p0"], r[1]["p0"])  # broadcast from rank 0
     np.testing.assert_array_equal(r[0]["p0"], W.params0(100))
@@ -72,11 +73,12 @@ def _check(outdir):
     dev = rt.require_gpu()
     imgs, onehot = W.global_batch(2)
     ex = rt.NetExecutor(2 * W.B, 32, 32, 3, W.C, W.L, 10, W.H, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
-                        dtype="float32", input_u8=True, device=dev)
+                        dtype=W.DTYPE, input_u8=True, device=dev)
     p = torch.from_numpy(r[0]["p0"]).to(dev)
     loss, g = ex.forward_backward(p, torch.from_numpy(imgs).to(dev), torch.from_numpy(onehot).to(dev))
     g_full = g.cpu().numpy()
     g_mean = r[0]["g"] / 2
+    assert np.abs(g_full).max() > 0 and np.isfinite(g_mean).all()
     assert np.abs(g_mean - g_full).max() <= 1e-5 * np.abs(g_full).max(), np.abs(g_mean - g_full).max()
     assert abs(0.5 * (float(r[0]["loss"][0]) + float(r[1]["loss"][0])) - loss.item()) <= 1e-5 * loss.item()
     m = torch.zeros_like(p)
@@ -91,10 +93,50 @@ def test_two_ranks_gloo_native(tmp_path):
     _check(tmp_path)
 
 
+RCCL_ONE_DEVICE = {"ASR_TEST_SPLIT_HOSTID": "1", "NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1"}
+
+
 def test_two_ranks_rccl_c_abi(tmp_path):
-    rc, out = _launch(tmp_path, "rccl", {"ASR_TEST_SPLIT_HOSTID": "1", "NCCL_SOCKET_IFNAME": "lo",
-                                         "NCCL_IB_DISABLE": "1"})
-    if rc != 0 and "Duplicate GPU" in out:
-        pytest.skip("RCCL refuses two ranks on one device even with split host ids")
+    rc, out = _launch(tmp_path, "rccl", RCCL_ONE_DEVICE)
     assert rc == 0, out[-3000:]
     _check(tmp_path)
+
+
+@pytest.mark.parametrize("backend", ["gloo", "rccl"])
+def test_two_ranks_c2_composition(tmp_path, backend):
+    """BASELINE C4's per-rank composition (bf16, C=64, stacked kernels with
+    several images per workgroup and the in-launch slab fold; L=3) on two
+    ranks: the all-reduced gradient is the single-rank gradient of the
+    concatenated batch (the 384-image reference runs a different workgroup
+    split, so the sums differ only in fp32 order: 1e-5 of max)."""
+    rc, out = _launch(tmp_path, backend, RCCL_ONE_DEVICE if backend == "rccl" else None, timeout=150, case="c2")
+    assert rc == 0, out[-3000:]
+    _check(tmp_path, "c2")
+
+
+def test_bench_two_ranks_one_device(tmp_path):
+    """bench.py's multi-rank branch (RCCL communicator, parameter broadcast,
+    per-step all-reduce, max-over-ranks timing, rank-0 JSON line) at the
+    metric's workload, both ranks on cuda:0 (--share-device: each rank claims
+    its own RCCL host id; the 8-GPU scaling run is the driver's)."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.update({"NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1"})
+    cmd = [sys.executable, os.path.join(os.path.dirname(HERE), "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--no-cpu-baseline", "--share-device", "--block-reps", "2"]
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                         start_new_session=True)
+    try:
+        out, _ = p.communicate(timeout=240)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, _ = p.communicate()
+        pytest.fail("bench --gpus 2 hung:\n" + out[-3000:])
+    assert p.returncode == 0, out[-3000:]
+    import json
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out[-3000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 1024 and d["config"]["parallelism"] == "dp2"
+    assert d["config"]["collective"] == "asr_dist_allreduce_sum (RCCL)"
+    assert d["value"] > 0 and d["config"]["live_gradient_fraction"] >= 0.9

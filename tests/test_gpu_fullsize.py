@@ -1,5 +1,11 @@
-"""GPU checks at BASELINE.json's full sizes (configs[1] C2: N=512, C=64;
-configs[2] C3: N=1024, C=16, 108 blocks; configs[4] C5: RK2 at the C2 shape).
+"""GPU checks at BASELINE.json's full sizes (configs[0] C1: N=128, C=16, 18
+blocks, fp32; configs[1] C2: N=512, C=64; configs[2] C3: N=1024, C=16, 108
+blocks; configs[4] C5: RK2 at the C2 shape).
+
+C1 is small enough for a direct comparison: the whole fp32 network (loss,
+probabilities, every gradient) against the op-by-op restatement of the
+reference graph in float64 (oracle/torch_cpu_ref.py, dtype=float64), with the
+fp32 tolerances of test_gpu_network.py.
 
 The fp64 oracle cannot run a whole batch at these sizes in seconds, so parity
 is checked through properties that do not depend on the size:
@@ -92,12 +98,56 @@ def test_block_fullsize(rt, N, C, integrator):
                      what="y")
 
 
-@pytest.mark.parametrize("cfg", ["c2", "c3", "c3_64", "c5"])
+def _c1_case():
+    """BASELINE C1 (get_single_block_resnet_build_function(blocks_per_stage=[18],
+    filters_per_block=[16]), h = 8/18, batch 128, fp32) with the bench's
+    non-saturating init scale (block thetas and biases x0.5, fc x0.1)."""
+    C, L, N = 16, 18, 128
+    spec = O.NetSpec(C=C, L=L, h=8.0 / L)
+    rng = np.random.default_rng(2024)
+    params = O.init_params(spec, rng, np.float64, bias_std=0.05)
+    params = [p * (0.1 if i == len(params) - 2 else 0.5 if 2 <= i < len(params) - 2 else 1.0)
+              for i, p in enumerate(params)]
+    params = [p.astype(np.float32).astype(np.float64) for p in params]
+    imgs = rng.integers(0, 256, (N, 32, 32, 3)).astype(np.uint8)
+    onehot = np.eye(10)[rng.integers(0, 10, N)]
+    return spec, params, imgs, onehot
+
+
+def test_c1_fullsize_fp32_vs_reference_graph(rt):
+    """BASELINE C1 at its own size on the GPU's fp32 path vs the reference
+    graph restated op by op in float64 (vectorised kernel assembly, autograd):
+    probabilities rtol 1e-5 (atol 1e-6), loss 1e-5 relative, every gradient
+    within 1e-4 of its tensor's max |reference| (test_gpu_network.py)."""
+    from oracle.torch_cpu_ref import RefNet
+    spec, params, imgs, onehot = _c1_case()
+    N = imgs.shape[0]
+    ex = rt.NetExecutor(N, 32, 32, 3, spec.C, spec.L, 10, spec.h, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
+                        dtype="float32", input_u8=True)
+    flat = torch.from_numpy(O.flatten(params).astype(np.float32)).cuda()
+    x = torch.from_numpy(imgs).cuda()
+    loss, grads = ex.forward_backward(flat, x, torch.from_numpy(onehot.astype(np.float32)).cuda(), want_probs=True)
+    probs_gpu = ex.probs.cpu().numpy().astype(np.float64)
+    g_gpu = O.unflatten(grads.cpu().numpy().astype(np.float64), [p.shape for p in params])
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    ref = RefNet(params, spec.C, spec.L, spec.h, assembly="vectorised", dtype=torch.float64)
+    probs, want_loss, g_want = ref.loss_and_grads(imgs, onehot)
+    live = ((probs[np.arange(N), onehot.argmax(1)] > 1e-7) & (probs[np.arange(N), onehot.argmax(1)] < 1 - 1e-7))
+    assert live.mean() > 0.9  # the gradient is not clipped away (Keras CE clip)
+    assert_close(probs_gpu, probs, rtol=1e-5, atol=1e-6, what="probs")
+    assert abs(loss.item() - want_loss) <= 1e-5 * abs(want_loss)
+    for i, (a, b) in enumerate(zip(g_gpu, g_want)):
+        assert_close(a, b, rtol=0, atol=1e-4 * max(np.abs(b).max(), 1e-12), what=f"grad[{i}] {b.shape}")
+
+
+@pytest.mark.parametrize("cfg", ["c1", "c2", "c3", "c3_64", "c5"])
 def test_network_fullsize_properties(rt, cfg):
     """c3_64 is BASELINE C3's "(and 64)" variant: C=64, 108 blocks, N=1024 (the stacked C=64 kernels with
-    four images per workgroup and 108 in-launch slab hand-offs)."""
-    C, L, N, integ = {"c2": (64, 30, 512, "euler"), "c3": (16, 108, 1024, "euler"), "c3_64": (64, 108, 1024, "euler"),
-                      "c5": (64, 30, 512, "rk2")}[cfg]
+    four images per workgroup and 108 in-launch slab hand-offs).  c1 is BASELINE C1 (fp32, C=16, 18 blocks,
+    batch 128) on the fp32 kernels."""
+    C, L, N, integ = {"c1": (16, 18, 128, "euler"), "c2": (64, 30, 512, "euler"), "c3": (16, 108, 1024, "euler"),
+                      "c3_64": (64, 108, 1024, "euler"), "c5": (64, 30, 512, "rk2")}[cfg]
+    dtype = "float32" if cfg == "c1" else "bfloat16"
     from differential_equations_resnet_amd.netparams import init_net_params
     h = 8.0 / L
     dev = torch.device("cuda")
@@ -108,7 +158,7 @@ def test_network_fullsize_properties(rt, cfg):
 
     def ex(n):
         return rt.NetExecutor(n, 32, 32, 3, C, L, 10, h, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
-                              dtype="bfloat16", input_u8=True, device=dev, integrator=integ)
+                              dtype=dtype, input_u8=True, device=dev, integrator=integ)
     full, half = ex(N), ex(N // 2)
     loss, g = full.forward_backward(params, imgs, tgt)
     loss, g = loss.clone(), g.clone()

@@ -39,7 +39,8 @@ def _executor(spec, N, dtype):
 
 @pytest.mark.parametrize("gamma,kind,anti,C,W", [(0.0, "3by3", True, 16, 32), (-0.05, "3by3", True, 16, 32),
                                                    (-0.05, "general", True, 6, 9), (0.0, "general", False, 5, 7),
-                                                   (0.0, "regular", False, 16, 32)])
+                                                   (0.0, "regular", False, 16, 32), (0.0, "3by3", True, 64, 32),
+                                                   (-0.05, "3by3", True, 64, 32)])
 def test_network_fp32_parity(gamma, kind, anti, C, W):
     spec, params, imgs, onehot = _setup(gamma=gamma, kind=kind, antisymmetric=anti, C=C, W=W, H=W)
     N = imgs.shape[0]

@@ -273,3 +273,101 @@ def test_rk2_stack_abi_matches_per_block(rt, N, L, gamma):
             assert np.abs(a - bb).max() <= 1e-5 * max(np.abs(bb).max(), 1e-30), (l, what, np.abs(a - bb).max())
         dy = dx
     assert torch.equal(dx0, dy)
+
+
+def _net_case(rt, N, C, L, seed=5):
+    from differential_equations_resnet_amd.netparams import init_net_params
+    dev = torch.device("cuda")
+    params = torch.from_numpy(init_net_params(C, L, 3, 10, seed=seed) * 0.5).to(dev)
+    rng = np.random.default_rng(seed)
+    imgs = torch.from_numpy(rng.integers(0, 256, (N, 32, 32, 3), dtype=np.uint8)).to(dev)
+    tgt = torch.from_numpy(np.eye(10, dtype=np.float32)[rng.integers(0, 10, N)]).to(dev)
+    return dev, params, imgs, tgt
+
+
+def test_stack_handoff_timeout_is_sticky(rt):
+    """The stacked backward's bounded wait for other workgroups' slabs: a grid
+    of twice the resident capacity (asr_debug_stack_backward; one 768-thread
+    workgroup fits per CU) leaves half the workgroups queued behind the
+    waiting ones, so the wait runs out.  That must surface as an error, and
+    stay one: asr_net_check_status raises, the status word stays set, and
+    the next stacked forward_backward refuses to run until it is cleared;
+    after the reset the default grid runs clean."""
+    from differential_equations_resnet_amd import _lib
+    lib = _lib.load()
+    cus = lib.asr_device_cu_count()
+    N, C, L = min(2 * cus, 512), 64, 3
+    if N <= cus:
+        pytest.skip("needs a grid larger than the CU count within 512 workgroups")
+    dev, params, imgs, tgt = _net_case(rt, N, C, L)
+    assert not rt.stack_status()
+    try:
+        _lib.check(lib.asr_debug_stack_backward(N), "asr_debug_stack_backward")
+        ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / L, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
+                            dtype="bfloat16", input_u8=True, device=dev)
+        ex.forward_backward(params, imgs, tgt)
+        with pytest.raises(_lib.AsrError, match="timed out"):
+            ex.check_status()
+        assert rt.stack_status()  # sticky
+        with pytest.raises(_lib.AsrError, match="sticky"):
+            ex.forward_backward(params, imgs, tgt)
+    finally:
+        lib.asr_debug_stack_backward(0)
+        rt.stack_status(reset=True)
+    assert not rt.stack_status()
+    ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / L, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
+                        dtype="bfloat16", input_u8=True, device=dev)
+    loss, g = ex.forward_backward(params, imgs, tgt)
+    ex.check_status()
+    assert np.isfinite(loss.item()) and g.abs().max().item() > 0
+
+
+@pytest.mark.parametrize("C,L,dtype", [(64, 5, "bfloat16"), (64, 4, "bfloat16"), (16, 5, "bfloat16"),
+                                       (16, 3, "float32")])
+def test_inference_executor_matches_training_forward(rt, C, L, dtype):
+    """The forward-only workspace (ASR_VARIANT_INFERENCE: x_0 + two ping-pong
+    slots; at C=64 bf16 one k_fwd3_stack launch with slots=2 and no masks)
+    gives the training forward's probabilities bitwise (the same kernels'
+    arithmetic), for both parities of L, at a fraction of the memory."""
+    N = 96
+    dev, params, imgs, tgt = _net_case(rt, N, C, L, seed=11)
+    kw = dict(subtract_mean=127.5, divide_by_stddev=127.5, dtype=dtype, input_u8=True, device=dev)
+    tr = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / L, 0.0, **kw)
+    inf = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / L, 0.0, inference=True, **kw)
+    assert inf.ws_bytes < 0.5 * tr.ws_bytes
+    tr.forward_backward(params, imgs, tgt, want_probs=True)
+    p_train = tr.probs.clone()
+    p_eval = tr.forward(params, imgs).clone()  # evaluation on the training workspace (per-block kernels)
+    p_inf = inf.forward(params, imgs).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(p_inf, p_train)
+    assert torch.equal(p_eval, p_train)
+    with pytest.raises(ValueError):
+        inf.forward_backward(params, imgs, tgt)
+
+
+def test_kernel_times_of_the_network_step(rt):
+    """ASR_VARIANT_TIMED records events around the block launches of the
+    training step and of an inference forward; the times are positive and
+    the stack kernels account for most of the step."""
+    import time
+    N, C, L = 512, 64, 6
+    dev, params, imgs, tgt = _net_case(rt, N, C, L, seed=2)
+    kw = dict(subtract_mean=127.5, divide_by_stddev=127.5, dtype="bfloat16", input_u8=True, device=dev)
+    ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / L, 0.0, **kw)
+    ex.forward_backward(params, imgs, tgt)
+    ex.variant = rt.ASR_VARIANT_TIMED
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ex.forward_backward(params, imgs, tgt)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) * 1e6
+    kt = ex.kernel_times()
+    ex.variant = 0
+    assert kt["fwd"] > 0 and kt["bwd"] > 0 and kt["bwd_reduce"] > 0
+    assert kt["fwd"] + kt["bwd"] + kt["bwd_reduce"] < wall
+    assert kt["bwd"] > kt["fwd"]
+    inf = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / L, 0.0, inference=True, variant=rt.ASR_VARIANT_TIMED, **kw)
+    inf.forward(params, imgs)
+    kt2 = inf.kernel_times()
+    assert kt2["fwd"] > 0 and kt2["bwd"] is None
