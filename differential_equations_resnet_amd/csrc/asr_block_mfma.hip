@@ -50,6 +50,15 @@
 #ifndef ASR_FWD3_WGS
 #define ASR_FWD3_WGS 3  // k_fwd3 workgroups per CU (grid = min(bands, WGS x CUs))
 #endif
+#ifndef ASR_FSTACK_STAGGER
+#define ASR_FSTACK_STAGGER 0  // A/B: k_fwd3_stack workgroups of the grid's second half start this many s_sleep-64 units late
+#endif
+#ifndef ASR_BWD_DPRIO
+#define ASR_BWD_DPRIO 0  // A/B: k_bwd3_stack dgrad waves at s_setprio(N)
+#endif
+#ifndef ASR_SLAB_DEFER
+#define ASR_SLAB_DEFER 0  // A/B: k_bwd3_stack slab stores not drained at the next band barrier (signalled one band later)
+#endif
 #ifndef ASR_BWD3_DMA0
 #define ASR_BWD3_DMA0 16  // k_bwd3 wgrad waves: DMA pieces issued right after the barrier, the rest one per row (A/B: spreading them lengthened the MFMA phase as much as it saved; the stacks: all at once 16 vs 9 +0.3-0.5 %, 4 -0.7 %)
 #endif
@@ -1041,6 +1050,8 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
     }
   };
   adv(xl, xn, xb);
+  if (ASR_FSTACK_STAGGER && blockIdx.x >= gridDim.x / 2)
+    for (int i = 0; i < ASR_FSTACK_STAGGER; ++i) __builtin_amdgcn_s_sleep(1);
   dma_rows<C, W>(x0, lds, cn, -1, min(BR, H) + 2, H, wave, NW, lane);
   int nst = 0;
   const int total = (RK2 ? 2 : 1) * L * per;
@@ -2286,6 +2297,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
   constexpr int ES = 9 * C * C + C, ECH = ES / 4;
   if (wave < 4) {
     // ---------------- dgrad waves ----------------
+    if (ASR_BWD_DPRIO) __builtin_amdgcn_s_setprio(ASR_BWD_DPRIO);
     const int ot = wave;
     bf16x8 A[G::KS];
     load_A1<C>(wpack + (long)(L - 1) * w_stride, ot, lane, A);
@@ -2521,11 +2533,17 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
     }
     Cur cur{SPB * L - 1, n0, 0}, nxt{SPB * L - 1, n0, 0};
     adv(nxt);
+    int nslab = 0;            // (ASR_SLAB_DEFER) slab stores of the previous item, still draining
+    bool prev_first = false;  // (ASR_SLAB_DEFER) the previous item was its block's first
     for (int it = 0; it < total; ++it) {
       const int buf = it & 1;
       const int y0 = cur.b * BR, l = blk_of(cur.l);  // (l: the block)
       const int rows = min(BR, H - y0);
       const bool first_of_block = cur.b == 0 && cur.n == n0 && (!RK2 || (cur.l & 1));
+      // block l+1's slabs are complete in memory: every wgrad wave has waited for them (the barrier at the
+      // top of this item; deferred: the vm_wait(0) of the block's first item, behind this item's barrier)
+      const bool signal = ASR_SLAB_DEFER ? prev_first : first_of_block;
+      prev_first = first_of_block;
       if (wave == 4) ASR_BTR(1, 1, it, 0);
       if (first_of_block && l + 2 < L && l + 2 >= lfold && w8 == 0 && lane == 0) {
         // block l+2's slabs: every workgroup published them (bounded poll)
@@ -2540,9 +2558,11 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
-      barrier_vm(0);  // this wave's x rows of item it landed (and its slab stores drained)
+      if (ASR_SLAB_DEFER) barrier_vm(nslab);  // (x rows of item it landed in item it-1; slab stores keep flying)
+      else barrier_vm(0);  // this wave's x rows of item it landed (and its slab stores drained)
+      nslab = 0;
       if (wave == 4) ASR_BTR(1, 1, it, 1);
-      if (first_of_block && l + 1 < L && l + 1 >= lfold && w8 == 0 && lane == 0)
+      if (signal && l + 1 < L && l + 1 >= lfold && w8 == 0 && lane == 0)
         __hip_atomic_fetch_add((gu32*)(done + l + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // published
       if (first_of_block && l + 2 < L && l + 2 >= lfold) fold_begin(l + 2);
 #pragma unroll
@@ -2681,6 +2701,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
           }
           accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
+        nslab = 2 * MTW + (dbw ? 2 : 0);
       }
       if (wave == 4) ASR_BTR(1, 1, it, 5);
       cur = nxt;
