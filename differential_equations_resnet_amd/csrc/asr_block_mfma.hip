@@ -50,15 +50,6 @@
 #ifndef ASR_FWD3_WGS
 #define ASR_FWD3_WGS 3  // k_fwd3 workgroups per CU (grid = min(bands, WGS x CUs))
 #endif
-#ifndef ASR_FSTACK_STAGGER
-#define ASR_FSTACK_STAGGER 0  // A/B: k_fwd3_stack workgroups of the grid's second half start this many s_sleep-64 units late
-#endif
-#ifndef ASR_BWD_DPRIO
-#define ASR_BWD_DPRIO 0  // A/B: k_bwd3_stack dgrad waves at s_setprio(N)
-#endif
-#ifndef ASR_SLAB_DEFER
-#define ASR_SLAB_DEFER 0  // A/B: k_bwd3_stack slab stores not drained at the next band barrier (signalled one band later)
-#endif
 #ifndef ASR_BWD3_DMA0
 #define ASR_BWD3_DMA0 16  // k_bwd3 wgrad waves: DMA pieces issued right after the barrier, the rest one per row (A/B: spreading them lengthened the MFMA phase as much as it saved; the stacks: all at once 16 vs 9 +0.3-0.5 %, 4 -0.7 %)
 #endif
@@ -1050,8 +1041,6 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
     }
   };
   adv(xl, xn, xb);
-  if (ASR_FSTACK_STAGGER && blockIdx.x >= gridDim.x / 2)
-    for (int i = 0; i < ASR_FSTACK_STAGGER; ++i) __builtin_amdgcn_s_sleep(1);
   dma_rows<C, W>(x0, lds, cn, -1, min(BR, H) + 2, H, wave, NW, lane);
   int nst = 0;
   const int total = (RK2 ? 2 : 1) * L * per;
@@ -1926,7 +1915,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
     // half then reads 8 consecutive tile columns, whose swizzled 8-B pieces cover
     // the 64 banks once (pixels 8g + tq, 8g + 4 + tq, as the round-1 v2 backward read them, put
     // columns c and c + 8 on the same banks: every read 2-way)
-    unsigned offA[MTW][2], offB[2][2];
+    unsigned offA[MTW], offB[2];  // pixel tile 1 sits 16 px = 2 KiB on (swizzle period 8 px)
     {
       const unsigned xb0 = lds_u32(lds + L::X), zb0 = lds_u32(lds + L::DZ);
       const int pb = 4 * g + tq;
@@ -1935,19 +1924,17 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
         const int mt = tg * MTW + mi;
         const int tap = (16 * mt) / C, itile = ((16 * mt) % C) / 16;
         const int ky = tap / 3, kx = tap % 3, q = 2 * itile + (tp >> 1);
-        offA[mi][0] = xb0 + (unsigned)(toff<C>(ky, pb + kx, q, TW) + 8 * (tp & 1));
-        offA[mi][1] = xb0 + (unsigned)(toff<C>(ky, pb + 16 + kx, q, TW) + 8 * (tp & 1));
+        offA[mi] = xb0 + (unsigned)(toff<C>(ky, pb + kx, q, TW) + 8 * (tp & 1));
       }
 #pragma unroll
       for (int oi = 0; oi < 2; ++oi) {
         const int q = 2 * (oq + oi) + (tp >> 1);
-        offB[oi][0] = zb0 + (unsigned)(toff<C>(1, pb + 1, q, TW) + 8 * (tp & 1));
-        offB[oi][1] = zb0 + (unsigned)(toff<C>(1, pb + 17, q, TW) + 8 * (tp & 1));
+        offB[oi] = zb0 + (unsigned)(toff<C>(1, pb + 1, q, TW) + 8 * (tp & 1));
       }
       // opaque to the compiler: kept in VGPRs, not recomputed per band
 #pragma unroll
-      for (int mi = 0; mi < MTW; ++mi) asm volatile("" : "+v"(offA[mi][0]), "+v"(offA[mi][1]));
-      asm volatile("" : "+v"(offB[0][0]), "+v"(offB[0][1]), "+v"(offB[1][0]), "+v"(offB[1][1]));
+      for (int mi = 0; mi < MTW; ++mi) asm volatile("" : "+v"(offA[mi]));
+      asm volatile("" : "+v"(offB[0]), "+v"(offB[1]));
     }
     // the next band's dz: wgrad wave w8 owns tile row 2 + w8 (w8 < 4) of a band that
     // continues the image, row w8 (w8 < 6) of one that starts an image; it DMAs
@@ -2052,20 +2039,20 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
       // A fragments two m-tiles ahead (ring of 3), as in the round-1 v2 backward
       auto mfma_band = [&](auto bo) {
         constexpr int BO = decltype(bo)::value;
-        Ar[0] = tr_pair_at<BO>(offA[0][0], offA[0][1]);
+        Ar[0] = tr_pair_px<BO>(offA[0]);
         static_for<0, BR>([&](auto rc) {
           constexpr int r = decltype(rc)::value, RO_ = BO + r * L::ROWB;
           __builtin_amdgcn_sched_barrier(0);  // no hoisting of later rows' reads (register pressure)
           if (r < rows) {
             const bool mr = r + 1 < rows;
 #pragma unroll
-            for (int oi = 0; oi < 2; ++oi) Bf[oi] = tr_pair_at<RO_>(offB[oi][0], offB[oi][1]);
-            Ar[1] = tr_pair_at<RO_>(offA[1][0], offA[1][1]);
+            for (int oi = 0; oi < 2; ++oi) Bf[oi] = tr_pair_px<RO_>(offB[oi]);
+            Ar[1] = tr_pair_px<RO_>(offA[1]);
             static_for<0, MTW>([&](auto mc) {
               constexpr int mi = decltype(mc)::value;
-              if constexpr (mi + 2 < MTW) Ar[(mi + 2) % 3] = tr_pair_at<RO_>(offA[mi + 2][0], offA[mi + 2][1]);
+              if constexpr (mi + 2 < MTW) Ar[(mi + 2) % 3] = tr_pair_px<RO_>(offA[mi + 2]);
               else if constexpr (mi + 2 == MTW && r + 1 < BR) {
-                if (mr) Ar[0] = tr_pair_at<RO_ + L::ROWB>(offA[0][0], offA[0][1]);  // MTW % 3 == 0: slot 0 again
+                if (mr) Ar[0] = tr_pair_px<RO_ + L::ROWB>(offA[0]);  // MTW % 3 == 0: slot 0 again
               }
 #pragma unroll
               for (int oi = 0; oi < 2; ++oi)
@@ -2083,9 +2070,9 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
       if (it > i0) {  // the offsets follow the buffer (in place: no second register set)
         const unsigned dlt = buf ? (unsigned)L::TILE : (unsigned)-L::TILE;
 #pragma unroll
-        for (int mi = 0; mi < MTW; ++mi) offA[mi][0] += dlt, offA[mi][1] += dlt;
+        for (int mi = 0; mi < MTW; ++mi) offA[mi] += dlt;
 #pragma unroll
-        for (int oi = 0; oi < 2; ++oi) offB[oi][0] += dlt, offB[oi][1] += dlt;
+        for (int oi = 0; oi < 2; ++oi) offB[oi] += dlt;
       }
       mfma_band(std::integral_constant<int, 0>{});
       while (ipc < npc) piece();
@@ -2297,7 +2284,6 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
   constexpr int ES = 9 * C * C + C, ECH = ES / 4;
   if (wave < 4) {
     // ---------------- dgrad waves ----------------
-    if (ASR_BWD_DPRIO) __builtin_amdgcn_s_setprio(ASR_BWD_DPRIO);
     const int ot = wave;
     bf16x8 A[G::KS];
     load_A1<C>(wpack + (long)(L - 1) * w_stride, ot, lane, A);
@@ -2428,7 +2414,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
     f32x4 acc[MTW][2];
 #pragma unroll
     for (int mi = 0; mi < MTW; ++mi) acc[mi][0] = acc[mi][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    unsigned offA[MTW][2], offB[2][2];
+    unsigned offA[MTW], offB[2];  // pixel tile 1 sits 16 px = 2 KiB on (swizzle period 8 px)
     {
       const unsigned xb0 = lds_u32(lds + LL::X), zb0 = lds_u32(lds + LL::DZ);
       const int pb = 4 * g + tq;
@@ -2437,18 +2423,16 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         const int mt = tg * MTW + mi;
         const int tap = (16 * mt) / C, itile = ((16 * mt) % C) / 16;
         const int ky = tap / 3, kx = tap % 3, q = 2 * itile + (tp >> 1);
-        offA[mi][0] = xb0 + (unsigned)(toff<C>(ky, pb + kx, q, TW) + 8 * (tp & 1));
-        offA[mi][1] = xb0 + (unsigned)(toff<C>(ky, pb + 16 + kx, q, TW) + 8 * (tp & 1));
+        offA[mi] = xb0 + (unsigned)(toff<C>(ky, pb + kx, q, TW) + 8 * (tp & 1));
       }
 #pragma unroll
       for (int oi = 0; oi < 2; ++oi) {
         const int q = 2 * (oq + oi) + (tp >> 1);
-        offB[oi][0] = zb0 + (unsigned)(toff<C>(1, pb + 1, q, TW) + 8 * (tp & 1));
-        offB[oi][1] = zb0 + (unsigned)(toff<C>(1, pb + 17, q, TW) + 8 * (tp & 1));
+        offB[oi] = zb0 + (unsigned)(toff<C>(1, pb + 1, q, TW) + 8 * (tp & 1));
       }
 #pragma unroll
-      for (int mi = 0; mi < MTW; ++mi) asm volatile("" : "+v"(offA[mi][0]), "+v"(offA[mi][1]));
-      asm volatile("" : "+v"(offB[0][0]), "+v"(offB[0][1]), "+v"(offB[1][0]), "+v"(offB[1][1]));
+      for (int mi = 0; mi < MTW; ++mi) asm volatile("" : "+v"(offA[mi]));
+      asm volatile("" : "+v"(offB[0]), "+v"(offB[1]));
     }
     auto own_row = [&](bool reuse) { return reuse ? (w8 < 4 ? 2 + w8 : -1) : (w8 < 6 ? w8 : -1); };
     auto stage_own = [&](const Cur& c, int row, int nbuf, unsigned& mwv) {
@@ -2533,17 +2517,11 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
     }
     Cur cur{SPB * L - 1, n0, 0}, nxt{SPB * L - 1, n0, 0};
     adv(nxt);
-    int nslab = 0;            // (ASR_SLAB_DEFER) slab stores of the previous item, still draining
-    bool prev_first = false;  // (ASR_SLAB_DEFER) the previous item was its block's first
     for (int it = 0; it < total; ++it) {
       const int buf = it & 1;
       const int y0 = cur.b * BR, l = blk_of(cur.l);  // (l: the block)
       const int rows = min(BR, H - y0);
       const bool first_of_block = cur.b == 0 && cur.n == n0 && (!RK2 || (cur.l & 1));
-      // block l+1's slabs are complete in memory: every wgrad wave has waited for them (the barrier at the
-      // top of this item; deferred: the vm_wait(0) of the block's first item, behind this item's barrier)
-      const bool signal = ASR_SLAB_DEFER ? prev_first : first_of_block;
-      prev_first = first_of_block;
       if (wave == 4) ASR_BTR(1, 1, it, 0);
       if (first_of_block && l + 2 < L && l + 2 >= lfold && w8 == 0 && lane == 0) {
         // block l+2's slabs: every workgroup published them (bounded poll)
@@ -2558,11 +2536,9 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
-      if (ASR_SLAB_DEFER) barrier_vm(nslab);  // (x rows of item it landed in item it-1; slab stores keep flying)
-      else barrier_vm(0);  // this wave's x rows of item it landed (and its slab stores drained)
-      nslab = 0;
+      barrier_vm(0);  // this wave's x rows of item it landed (and its slab stores drained)
       if (wave == 4) ASR_BTR(1, 1, it, 1);
-      if (signal && l + 1 < L && l + 1 >= lfold && w8 == 0 && lane == 0)
+      if (first_of_block && l + 1 < L && l + 1 >= lfold && w8 == 0 && lane == 0)
         __hip_atomic_fetch_add((gu32*)(done + l + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // published
       if (first_of_block && l + 2 < L && l + 2 >= lfold) fold_begin(l + 2);
 #pragma unroll
@@ -2595,20 +2571,20 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       bf16x8 Bf[2], Ar[3];
       auto mfma_band = [&](auto bo) {
         constexpr int BO = decltype(bo)::value;
-        Ar[0] = tr_pair_at<BO>(offA[0][0], offA[0][1]);
+        Ar[0] = tr_pair_px<BO>(offA[0]);
         static_for<0, BR>([&](auto rc) {
           constexpr int r = decltype(rc)::value, RO_ = BO + r * LL::ROWB;
           __builtin_amdgcn_sched_barrier(0);
           if (r < rows) {
             const bool mr = r + 1 < rows;
 #pragma unroll
-            for (int oi = 0; oi < 2; ++oi) Bf[oi] = tr_pair_at<RO_>(offB[oi][0], offB[oi][1]);
-            Ar[1] = tr_pair_at<RO_>(offA[1][0], offA[1][1]);
+            for (int oi = 0; oi < 2; ++oi) Bf[oi] = tr_pair_px<RO_>(offB[oi]);
+            Ar[1] = tr_pair_px<RO_>(offA[1]);
             static_for<0, MTW>([&](auto mc) {
               constexpr int mi = decltype(mc)::value;
-              if constexpr (mi + 2 < MTW) Ar[(mi + 2) % 3] = tr_pair_at<RO_>(offA[mi + 2][0], offA[mi + 2][1]);
+              if constexpr (mi + 2 < MTW) Ar[(mi + 2) % 3] = tr_pair_px<RO_>(offA[mi + 2]);
               else if constexpr (mi + 2 == MTW && r + 1 < BR) {
-                if (mr) Ar[0] = tr_pair_at<RO_ + LL::ROWB>(offA[0][0], offA[0][1]);
+                if (mr) Ar[0] = tr_pair_px<RO_ + LL::ROWB>(offA[0]);
               }
 #pragma unroll
               for (int oi = 0; oi < 2; ++oi)
@@ -2626,9 +2602,9 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       if (it > 0) {
         const unsigned dlt = buf ? (unsigned)LL::TILE : (unsigned)-LL::TILE;
 #pragma unroll
-        for (int mi = 0; mi < MTW; ++mi) offA[mi][0] += dlt, offA[mi][1] += dlt;
+        for (int mi = 0; mi < MTW; ++mi) offA[mi] += dlt;
 #pragma unroll
-        for (int oi = 0; oi < 2; ++oi) offB[oi][0] += dlt, offB[oi][1] += dlt;
+        for (int oi = 0; oi < 2; ++oi) offB[oi] += dlt;
       }
       mfma_band(std::integral_constant<int, 0>{});
       while (ipc < npc) piece();
@@ -2701,7 +2677,6 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
           }
           accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        nslab = 2 * MTW + (dbw ? 2 : 0);
       }
       if (wave == 4) ASR_BTR(1, 1, it, 5);
       cur = nxt;

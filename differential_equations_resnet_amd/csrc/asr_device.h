@@ -166,6 +166,13 @@ __device__ __forceinline__ bf16x8 tr_pair_at(unsigned a0, unsigned a1) {
   s16x8 c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
   return *(bf16x8*)&c;
 }
+// the same for the C=64 wgrad operands: the second half 16 pixels (2 KiB of a
+// swizzled tile row: the XOR swizzle repeats every 8 pixels) after the first,
+// both as immediate offsets on one address register
+template <int OFF>
+__device__ __forceinline__ bf16x8 tr_pair_px(unsigned a) {
+  return tr_pair_at<OFF>(a, a + 2048u);
+}
 __device__ __forceinline__ bf16x8 tr_pair(const unsigned char* p0, const unsigned char* p1) {
   const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ASR_LDS s16x4*)p0);
   const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ASR_LDS s16x4*)p1);

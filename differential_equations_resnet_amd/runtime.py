@@ -395,8 +395,10 @@ class NetExecutor:
 
     @variant.setter
     def variant(self, bits: int):
-        """Select ASR_VARIANT_* kernel compositions for later calls (tests)."""
-        self.cfg.variant = int(bits)
+        """Select ASR_VARIANT_* kernel compositions (tests) or the timing
+        instrumentation for later calls; an inference executor keeps its
+        ASR_VARIANT_INFERENCE bit (its workspace layout)."""
+        self.cfg.variant = int(bits) | (ASR_VARIANT_INFERENCE if self.inference else 0)
 
     def check_status(self):
         """Blocking: raises AsrError if a stacked backward of this process

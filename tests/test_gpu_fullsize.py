@@ -117,8 +117,14 @@ def _c1_case():
 def test_c1_fullsize_fp32_vs_reference_graph(rt):
     """BASELINE C1 at its own size on the GPU's fp32 path vs the reference
     graph restated op by op in float64 (vectorised kernel assembly, autograd):
-    probabilities rtol 1e-5 (atol 1e-6), loss 1e-5 relative, every gradient
-    within 1e-4 of its tensor's max |reference| (test_gpu_network.py)."""
+    probabilities rtol 1e-5 (atol 1e-6), loss 1e-5 relative (test_gpu_network.py's fp32 bounds).
+    Gradients, per SURVEY §8c group (conv1 kernel, conv1 bias, each block's merged theta, each block's
+    bias, fc kernel, fc bias; scale = the group's max |fp64 value|): the GPU's largest deviation from
+    fp64 must be within max(1e-4 * scale, 2x the deviation of the same graph restated op by op in
+    FLOAT32 (per-step slice/concat assembly, i.e. the reference's own precision)), and never above
+    1e-3 * scale.  At 18 blocks and 131k pixels per weight gradient the fp32 reference graph itself
+    deviates from fp64 by up to ~3e-4 of a group's max, so a fixed 1e-4 would ask the GPU to be more
+    exact than the reference."""
     from oracle.torch_cpu_ref import RefNet
     spec, params, imgs, onehot = _c1_case()
     N = imgs.shape[0]
@@ -132,12 +138,24 @@ def test_c1_fullsize_fp32_vs_reference_graph(rt):
     torch.set_num_threads(min(16, torch.get_num_threads()))
     ref = RefNet(params, spec.C, spec.L, spec.h, assembly="vectorised", dtype=torch.float64)
     probs, want_loss, g_want = ref.loss_and_grads(imgs, onehot)
+    _, _, g_ref32 = RefNet(params, spec.C, spec.L, spec.h, assembly="reference",
+                           dtype=torch.float32).loss_and_grads(imgs, onehot)
     live = ((probs[np.arange(N), onehot.argmax(1)] > 1e-7) & (probs[np.arange(N), onehot.argmax(1)] < 1 - 1e-7))
     assert live.mean() > 0.9  # the gradient is not clipped away (Keras CE clip)
     assert_close(probs_gpu, probs, rtol=1e-5, atol=1e-6, what="probs")
     assert abs(loss.item() - want_loss) <= 1e-5 * abs(want_loss)
-    for i, (a, b) in enumerate(zip(g_gpu, g_want)):
-        assert_close(a, b, rtol=0, atol=1e-4 * max(np.abs(b).max(), 1e-12), what=f"grad[{i}] {b.shape}")
+    nt = len(spec.theta_shapes())
+    groups = [[0], [1]] + [g for l in range(spec.L) for g in ([2 + l * (nt + 1) + j for j in range(nt)],
+                                                              [2 + l * (nt + 1) + nt])] + [[len(params) - 2],
+                                                                                           [len(params) - 1]]
+    assert sorted(i for g in groups for i in g) == list(range(len(params)))
+    for g in groups:
+        scale = max(np.abs(g_want[i]).max() for i in g)
+        ref_err = max(np.abs(g_ref32[i] - g_want[i]).max() for i in g)
+        tol = min(max(1e-4 * scale, 2 * ref_err), 1e-3 * scale)
+        for i in g:
+            assert_close(g_gpu[i], g_want[i], rtol=0, atol=tol, what=f"grad[{i}] {g_want[i].shape} (group tol {tol:.3g}, "
+                                                                       f"fp32 reference graph err {ref_err:.3g})")
 
 
 @pytest.mark.parametrize("cfg", ["c1", "c2", "c3", "c3_64", "c5"])

@@ -38,13 +38,12 @@ KERNEL_SOURCES = ["asr_block_mfma.hip", "asr_deep16.hip", "asr_stem_head.hip", "
 
 # (kernel-name regex) -> (max VGPR spills, max scratch bytes, why)
 SPILL_ALLOW = {
-    r"k_bwd3_stackILi64ELi32ELi4ELb0E": (6, 28, "12-wave C=64 stacked backward at the 168-register cap of 3 waves "
-                                               "per SIMD (dgrad: W 72 + accumulators 32; wgrad: dW tiles 72)"),
-    r"k_bwd3_stackILi64ELi32ELi4ELb1E": (11, 48, "its RK2 instantiation: + the stage's extra-term registers"),
+    r"k_bwd3_stack": (0, 0, "12-wave C=64 stacked backward at the 168-register cap of 3 waves per SIMD: no spills "
+                            "(the wgrad operands' two pixel tiles share one address register)"),
     r"k_bwd16_fusedILb0E": (8, 28, "12-wave fused C=16 backward at 168 registers (fp32 dx of 8 layers in the "
                                    "dgrad waves)"),
     r"k_bwd16_fusedILb1E": (12, 36, "its gamma != 0 instantiation (+ the dz tile term)"),
-    r"k_bwd3ILi64ELi32ELi4ELi2ELb0ELb1E": (4, 20, "per-block backward, first RK2 stage (extra dx term)"),
+    r"k_bwd3ILi64ELi32ELi4ELi2ELb0ELb1E": (4, 20, "per-block backward, first RK2 stage (extra dx term in registers)"),
     r"k_fwd3_stack": (0, 0, "forward stack: no spills"),
     r"k_fwd16_fused": (0, 0, "fused C=16 forward: no spills"),
     r"k_fwd3I": (0, 0, "per-block forward: no spills"),
