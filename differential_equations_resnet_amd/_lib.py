@@ -41,6 +41,7 @@ ASR_VARIANT_PER_BLOCK_FWD = 8
 ASR_VARIANT_PER_BLOCK_BWD = 16
 ASR_VARIANT_INFERENCE = 32
 ASR_VARIANT_TIMED = 64
+ASR_VARIANT_FULL_DXL = 128
 ASR_DIST_UNIQUE_ID_BYTES = 128
 
 

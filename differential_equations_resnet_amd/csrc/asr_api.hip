@@ -57,7 +57,7 @@ int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride
                          long mask_stride, const void* w, long w_stride, float h, float two_gamma, int N, int H, int W,
                          int C, int L, int ro0, float* slabs, long slab_stride, float* grp, long grp_stride,
                          unsigned* done, int* lfold_out, hipStream_t s, const void* xm = nullptr,
-                         const uint8_t* masks2 = nullptr, void* gbuf = nullptr);
+                         const uint8_t* masks2 = nullptr, void* gbuf = nullptr, const void* gtop = nullptr);
 int block_stack_fwd_mfma(const void* x0, void* ys, long y_stride, uint8_t* masks, long mask_stride, const void* w,
                          long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C, int L,
                          hipStream_t s, int slots = 0);
@@ -83,7 +83,8 @@ int stem_forward(const void* img, int input_u8, const float* w1, const float* b1
 int stem_wgrad(const void* img, int input_u8, const void* dx1, const void* x1, int act_bf16, int N, int H, int W,
                int Cin, int C, float mean, float inv_std, int use_norm, float* slabs, int* nslabs, hipStream_t s);
 int head(const void* xL, int act_bf16, const float* fck, const float* fcb, const float* targets, int N, int HW, int C,
-         int K, float* probs, float* loss_per, float* dlogits, float* gap, void* dxL, hipStream_t s);
+         int K, float* probs, float* loss_per, float* dlogits, float* gap, void* dxL, hipStream_t s,
+         void* growL = nullptr);
 int head_param_grads(const float* gap, const float* dlogits, int N, int C, int K, float* dfck, float* dfcb,
                      const float* loss_per, float* loss_out, hipStream_t s);
 
@@ -328,6 +329,7 @@ struct NetLayout {
   bool stack_bwd;     // C=64 Euler bf16: all blocks' backward in one k_bwd3_stack launch
   int stack_grid;     // its workgroups
   size_t theta_dst_tm, stack_slabs, stack_done;  // tile-major projection map, [L][grid][E+C] slabs, counters
+  size_t grow;        // stacked Euler backward: dL/dx_L as one bf16 row per image (the GAP gradient) [N][C]
 };
 
 static int net_check(const asr_net_config* c) {
@@ -342,7 +344,7 @@ static int net_check(const asr_net_config* c) {
   if (c->integrator != ASR_INTEGRATOR_EULER && c->integrator != ASR_INTEGRATOR_RK2)
     return fail(ASR_E_ARG, "bad integrator %d", c->integrator);
   if (c->variant & ~(ASR_VARIANT_NO_FOLD | ASR_VARIANT_STEM_FWD_VALU | ASR_VARIANT_STEM_WGRAD_VALU | ASR_VARIANT_PER_BLOCK_FWD |
-                    ASR_VARIANT_PER_BLOCK_BWD | ASR_VARIANT_INFERENCE | ASR_VARIANT_TIMED))
+                    ASR_VARIANT_PER_BLOCK_BWD | ASR_VARIANT_INFERENCE | ASR_VARIANT_TIMED | ASR_VARIANT_FULL_DXL))
     return fail(ASR_E_ARG, "bad variant bits 0x%x", c->variant);
   if (c->dtype == ASR_BF16 && !mfma_supported(c->C, c->W))
     return fail(ASR_E_UNSUPPORTED, "bf16 network needs C in {16,32,64} and W == 32 (C=%d W=%d)", c->C, c->W);
@@ -408,6 +410,7 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.theta_dst_tm = take(L.stack_bwd ? (size_t)L.ntheta * 2 * 4 : 0);
   L.stack_slabs = take(L.stack_bwd ? (size_t)c->L * L.stack_grid * (L.E + C) * 4 : 0);
   L.stack_done = take(L.stack_bwd ? (size_t)(c->L + 4) * 4 : 0);
+  L.grow = take(L.stack_bwd && !L.rk2 ? (size_t)c->N * C * 2 : 0);
   L.probs = take((size_t)c->N * K * 4);
   L.loss_per = take(tr ? (size_t)c->N * 4 : 0);
   L.dlogits = take(tr ? (size_t)c->N * K * 4 : 0);
@@ -931,8 +934,12 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   unsigned char* dcur = b + L.dxa;
   unsigned char* dnext = b + L.dxb;
   float* probs_ws = probs ? probs : (float*)(b + L.probs);
+  // the stacked Euler backward stages its top block's dy from one row per image (the GAP gradient is
+  // constant over the pixels): the head writes N x C values instead of the full dL/dx_L tensor
+  const bool grow = stacked && !L.rk2 && !(cfg->variant & ASR_VARIANT_FULL_DXL);
   ASR_TRY(head(act(cfg->L), bf, params + L.off_fck, params + L.off_fcb, targets, N, H * W, C, K, probs_ws,
-               (float*)(b + L.loss_per), (float*)(b + L.dlogits), (float*)(b + L.gap), dcur, s));
+               (float*)(b + L.loss_per), (float*)(b + L.dlogits), (float*)(b + L.gap), grow ? nullptr : dcur, s,
+               grow ? b + L.grow : nullptr));
   ASR_TRY(head_param_grads((const float*)(b + L.gap), (const float*)(b + L.dlogits), N, C, K, grads + L.off_fck,
                            grads + L.off_fcb, (const float*)(b + L.loss_per), loss, s));
   // blocks, last to first
@@ -973,7 +980,7 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
                                  L.wstride, cfg->h, L.sep_bwd ? 0.f : 2.f * cfg->gamma, N, H, W, C, cfg->L, ro0, slabs,
                                  sst, grp, L.grp_stride, (unsigned*)(b + L.stack_done), &lfold, s,
                                  L.rk2 ? b + L.xmids : nullptr, L.rk2 ? m1 + (size_t)cfg->L * L.mask_bytes : nullptr,
-                                 L.rk2 ? b + L.dxg : nullptr));
+                                 L.rk2 ? b + L.dxg : nullptr, grow ? b + L.grow : nullptr));
     ASR_TRY(timed_event(cfg, 3, s));
     for (int l = std::min(lfold, cfg->L) - 1; l >= 0; --l)  // blocks below lfold: pass 1 after the launch
       ASR_TRY(reduce_slabs_to_groups(slabs + (long)l * sst, grid, ES, grp + (long)l * L.grp_stride, s));

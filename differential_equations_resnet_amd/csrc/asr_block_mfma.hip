@@ -2216,7 +2216,8 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
                                                        unsigned* __restrict__ done, unsigned* __restrict__ tmo,
                                                        int lfold, const bf16* __restrict__ xm = nullptr,
                                                        const uint8_t* __restrict__ masks2 = nullptr,
-                                                       bf16* __restrict__ gbuf = nullptr) {
+                                                       bf16* __restrict__ gbuf = nullptr,
+                                                       const bf16* __restrict__ gtop = nullptr) {
   using G = Geo<C>;
   using LL = Bwd2Lds<C, W, BR>;
   using BD = Band<C, W, BR>;
@@ -2435,9 +2436,25 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       asm volatile("" : "+v"(offB[0]), "+v"(offB[1]));
     }
     auto own_row = [&](bool reuse) { return reuse ? (w8 < 4 ? 2 + w8 : -1) : (w8 < 6 ? w8 : -1); };
+    // gtop (Euler): the top block's dy = dL/dx_L is the GAP gradient, one row per image constant over the
+    // pixels (tfkeras_resnets.py:595-597); its tile rows are written from that row (zeros outside the
+    // image, as the DMA's zero page) instead of read from a full tensor
+    auto synth = [&](const Cur& c) { return !RK2 && gtop != nullptr && c.l == L - 1; };
+    auto synth_row = [&](const Cur& c, int row, int nbuf) {
+      const int gy = c.b * BR - 1 + row, q = lane & 7, p0 = lane >> 3;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if ((unsigned)gy < (unsigned)H) v = *(const u32x4*)(gtop + (long)c.n * C + 8 * q);
+      const unsigned rb = lds_u32(lds + LL::DY + nbuf * LL::TILE + row * LL::ROWB);
+#pragma unroll
+      for (int k = 0; k < W / 8; ++k) lds_st128(rb + (unsigned)toff<C>(0, p0 + 8 * k + 1, q, TW), v);
+    };
     auto stage_own = [&](const Cur& c, int row, int nbuf, unsigned& mwv) {
       if (row < 0) return;
       mwv = bwd2_mask_word<C, W>(mask_of(c.l), c.n, c.b * BR, row, H, lane);
+      if (synth(c)) {
+        synth_row(c, row, nbuf);
+        return;
+      }
       for (int j = 0; j < IPR; ++j)
         dma_row_instr<C, W>(dy_of(c.l), lds + LL::DY + nbuf * LL::TILE + row * LL::ROWB, c.n, c.b * BR - 1 + row, j,
                             H, loff);
@@ -2550,7 +2567,9 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       unsigned mwv = 0u;
       if (orow >= 0) mwv = bwd2_mask_word<C, W>(mask_of(nxt.l), nxt.n, nxt.b * BR, orow, H, lane);
       const int xr0 = cont ? 2 : 0;
-      const int ndy = orow >= 0 ? IPR : 0;
+      const bool syn = orow >= 0 && synth(nxt);
+      if (syn) synth_row(nxt, orow, buf ^ 1);
+      const int ndy = orow >= 0 && !syn ? IPR : 0;
       const int nx = (more && w8 >= 4) ? ((BR + 2 - xr0) * IPR - (w8 - 4) + 3) / 4 : 0;
       const int npc = ndy + nx;
       int ipc = 0;
@@ -3172,7 +3191,8 @@ int block_stack_bwd_grid(int N) {
 }
 
 // the backward of L Euler blocks in one launch (k_bwd3_stack).  dbuf0 holds
-// dL/dx_L on entry; block 0's dx ends in dbuf[L & 1].  Block l's slabs (grid
+// dL/dx_L on entry, or gtop (Euler) its per-image row (the head's GAP
+// gradient, bf16 [N][C]): then dbuf0 is not read.  Block 0's dx ends in dbuf[L & 1].  Block l's slabs (grid
 // of them, tile-major dW) at slabs + l*slab_stride; blocks >= 2 leave as
 // 32-slab group sums at grp + l*grp_stride, blocks 1 and 0 as slabs.  done:
 // L + 4 words (the per-block publish counters), zeroed here.  Refused while
@@ -3181,7 +3201,7 @@ int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride
                          long mask_stride, const void* w, long w_stride, float h, float two_gamma, int N, int H, int W,
                          int C, int L, int ro0, float* slabs, long slab_stride, float* grp, long grp_stride,
                          unsigned* done, int* lfold_out, hipStream_t s, const void* xm, const uint8_t* masks2,
-                         void* gbuf) {
+                         void* gbuf, const void* gtop) {
   if (!block_stack_bwd_supported(N, H, W, C) || L < 1)
     return fail(ASR_E_UNSUPPORTED, "stack backward: needs C=64, W=32, >= 4 row bands per image (C=%d W=%d H=%d)", C, W, H);
   const int grid = block_stack_bwd_grid(N);
@@ -3205,7 +3225,7 @@ int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride
     hipLaunchKernelGGL((blk::k_bwd3_stack<64, 32, kBwdBR>), dim3(grid), dim3(768), (size_t)L2::TOTAL, s,
                        (bf16*)dbuf0, (bf16*)dbuf1, (const bf16*)xs, x_stride, masks, mask_stride, (const bf16*)w,
                        w_stride, h, two_gamma, N, H, L, ro0, slabs, slab_stride, grp, grp_stride, done, tmo,
-                       lfold);
+                       lfold, nullptr, nullptr, nullptr, (const bf16*)gtop);
   }
   ASR_LAUNCH_CHECK("k_bwd3_stack");
   return ASR_OK;

@@ -224,13 +224,17 @@ __global__ __launch_bounds__(256) void k_stem_wgrad(const Tin* __restrict__ img,
 // GAP -> Dense(K) -> softmax [-> Keras CE loss and its gradient] per image.
 // (TF 1.12 keras.backend.categorical_crossentropy: renormalise, clip
 // [1e-7, 1-1e-7], -sum t*log q; the clip gradient passes on the closed
-// interval.)  dxL[n,p,c] = (dlogits . fc[c,:]) / (H*W) for every pixel.
+// interval.)  dxL[n,p,c] = (dlogits . fc[c,:]) / (H*W) for every pixel; or,
+// with growL, only that per-(image, channel) row (the GAP gradient is
+// constant over the pixels, models/tfkeras_resnets.py:595-597): the C=64
+// stacked backward stages its top block's dy from it instead of reading a
+// full tensor.
 template <typename T, int VEC>
 __global__ __launch_bounds__(256) void k_head(const T* __restrict__ xL, const float* __restrict__ fck,
                                               const float* __restrict__ fcb, const float* __restrict__ targets,
                                               int HW, int C, int K, float inv_n, float* __restrict__ probs,
                                               float* __restrict__ loss_per, float* __restrict__ dlogits,
-                                              float* __restrict__ gap, T* __restrict__ dxL) {
+                                              float* __restrict__ gap, T* __restrict__ dxL, T* __restrict__ growL) {
   __shared__ float red[256 * VEC];
   __shared__ float gs[256];
   __shared__ float lg[256];
@@ -324,7 +328,13 @@ __global__ __launch_bounds__(256) void k_head(const T* __restrict__ xL, const fl
     }
   }
   __syncthreads();
-  if (targets && dxL) {
+  if (targets && growL) {
+    if (tid < C) {
+      float a = 0.f;
+      for (int k = 0; k < K; ++k) a = fmaf(dl[k], fck[(long)tid * K + k], a);
+      growL[(long)n * C + tid] = from_f32<T>(a / (float)HW);
+    }
+  } else if (targets && dxL) {
     if (tid < C) {
       float a = 0.f;
       for (int k = 0; k < K; ++k) a = fmaf(dl[k], fck[(long)tid * K + k], a);
@@ -453,23 +463,23 @@ int stem_wgrad(const void* img, int input_u8, const void* dx1, const void* x1, i
 }
 
 int head(const void* xL, int act_bf16, const float* fck, const float* fcb, const float* targets, int N, int HW, int C,
-         int K, float* probs, float* loss_per, float* dlogits, float* gap, void* dxL, hipStream_t s) {
+         int K, float* probs, float* loss_per, float* dlogits, float* gap, void* dxL, hipStream_t s, void* growL) {
   if (C > 256 || K > 256) return fail(ASR_E_UNSUPPORTED, "head: C and num_classes must be <= 256");
   const float inv_n = 1.f / (float)N;
   if (act_bf16) {
     if (C % 8 == 0)
       hipLaunchKernelGGL((k_head<bf16, 8>), dim3(N), dim3(256), 0, s, (const bf16*)xL, fck, fcb, targets, HW, C, K,
-                         inv_n, probs, loss_per, dlogits, gap, (bf16*)dxL);
+                         inv_n, probs, loss_per, dlogits, gap, (bf16*)dxL, (bf16*)growL);
     else
       hipLaunchKernelGGL((k_head<bf16, 1>), dim3(N), dim3(256), 0, s, (const bf16*)xL, fck, fcb, targets, HW, C, K,
-                         inv_n, probs, loss_per, dlogits, gap, (bf16*)dxL);
+                         inv_n, probs, loss_per, dlogits, gap, (bf16*)dxL, (bf16*)growL);
   } else {
     if (C % 4 == 0)
       hipLaunchKernelGGL((k_head<float, 4>), dim3(N), dim3(256), 0, s, (const float*)xL, fck, fcb, targets, HW, C,
-                         K, inv_n, probs, loss_per, dlogits, gap, (float*)dxL);
+                         K, inv_n, probs, loss_per, dlogits, gap, (float*)dxL, (float*)growL);
     else
       hipLaunchKernelGGL((k_head<float, 1>), dim3(N), dim3(256), 0, s, (const float*)xL, fck, fcb, targets, HW, C,
-                         K, inv_n, probs, loss_per, dlogits, gap, (float*)dxL);
+                         K, inv_n, probs, loss_per, dlogits, gap, (float*)dxL, (float*)growL);
   }
   ASR_LAUNCH_CHECK("k_head");
   return ASR_OK;

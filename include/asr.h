@@ -271,6 +271,11 @@ typedef struct asr_net_config {
                                      blocks run as one k_fwd3_stack launch)     */
 #define ASR_VARIANT_TIMED 64      /* record HIP events around the block launches
                                      (measurement; asr_net_kernel_times)       */
+#define ASR_VARIANT_FULL_DXL 128  /* C=64 bf16 Euler stacked backward: the head
+                                     writes dL/dx_L as a full [N,H,W,C] tensor
+                                     that the top block reads, instead of the
+                                     per-image row it is constant over
+                                     (cross-check of the synthesised dy)        */
 
 long asr_net_param_count(const asr_net_config* cfg);
 size_t asr_net_workspace_bytes(const asr_net_config* cfg);

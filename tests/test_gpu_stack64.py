@@ -371,3 +371,26 @@ def test_kernel_times_of_the_network_step(rt):
     inf.forward(params, imgs)
     kt2 = inf.kernel_times()
     assert kt2["fwd"] > 0 and kt2["bwd"] is None
+
+
+@pytest.mark.parametrize("N,L", [(1, 3), (192, 4), (512, 5)])
+def test_synthesised_top_dy_equals_full_tensor(rt, N, L):
+    """The stacked Euler backward stages its top block's dy = dL/dx_L from the
+    head's one row per image (the GAP gradient is constant over the pixels,
+    models/tfkeras_resnets.py:595-597) instead of reading the full
+    [N,H,W,C] tensor the head writes with ASR_VARIANT_FULL_DXL: the same
+    bf16 values in the same LDS rows, so the loss and every gradient are
+    bitwise equal."""
+    C = 64
+    dev, params, imgs, tgt = _net_case(rt, N, C, L, seed=9)
+    ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / L, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
+                        dtype="bfloat16", input_u8=True, device=dev)
+    loss, g = ex.forward_backward(params, imgs, tgt)
+    loss, g = loss.clone(), g.clone()
+    ex.variant = rt.ASR_VARIANT_FULL_DXL
+    loss1, g1 = ex.forward_backward(params, imgs, tgt)
+    ex.variant = 0
+    torch.cuda.synchronize()
+    assert torch.equal(loss, loss1)
+    assert torch.equal(g, g1)
+    assert g.abs().max().item() > 0
