@@ -50,9 +50,6 @@
 #ifndef ASR_FWD3_WGS
 #define ASR_FWD3_WGS 3  // k_fwd3 workgroups per CU (grid = min(bands, WGS x CUs))
 #endif
-#ifndef ASR_FSTACK_PIPE
-#define ASR_FSTACK_PIPE 1  // Euler forward stack with the previous band's epilogue among this band's MFMAs (0: after them)
-#endif
 #ifndef ASR_BWD3_DMA0
 #define ASR_BWD3_DMA0 16  // k_bwd3 wgrad waves: DMA pieces issued right after the barrier, the rest one per row (A/B: spreading them lengthened the MFMA phase as much as it saved; the stacks: all at once 16 vs 9 +0.3-0.5 %, 4 -0.7 %)
 #endif
@@ -976,13 +973,7 @@ __global__ __launch_bounds__(256, WPE) void k_fwd3(const bf16* __restrict__ x, c
 // RK2 (BASELINE config 5): 2L stages, stage 2l = the first (x_l -> xmid_l, h/2,
 // mask1), stage 2l+1 the second (xmid_l -> x_{l+1}, h, mask2) with the residual
 // x_l from global memory (16-B loads in the regrouped layout, as k_fwd3<..., RESG>).
-// PIPE (Euler): the epilogue of band it-1 runs in pieces among band it's MFMAs
-// (two pieces per output row, conv_band hooks), so a wave keeps the matrix
-// pipe busy through its own epilogue; the accumulators and residual rows of
-// two bands are live (about 200 of the 256 registers two waves per SIMD
-// allow).  A band's stores then complete one band later, so the first band of
-// block l+1 needs >= 5 bands per image (the host checks).
-template <int C, int W, int BR, bool RK2 = false, bool PIPE = false>
+template <int C, int W, int BR, bool RK2 = false>
 __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ x0, bf16* __restrict__ ys,
                                                        long y_stride, uint8_t* __restrict__ masks, long mask_stride,
                                                        const bf16* __restrict__ wpack, long w_stride,
@@ -1054,106 +1045,6 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
   int nst = 0;
   const int total = (RK2 ? 2 : 1) * L * per;
   ASR_BCLK(0, 0);
-  if constexpr (PIPE) {
-    static_assert(!RK2, "the pipelined forward stack is the Euler one");
-    constexpr int PPR = 2, NU = PPR * RB;  // epilogue pieces per output row, per band
-    f32x4 accA[RB][2], accB[RB][2];
-    u32x4 xrA[RB], xrB[RB];
-    // the band whose epilogue is pending (P): output row pointers and its row count
-    unsigned char* ybP = nullptr;
-    uint8_t* mbP = nullptr;
-    int rowsP = 0;
-    float ez[8];
-    u32x4 eyw;
-    unsigned ebits = 0;
-    // piece ph of output row r of band P: regroup + channel pairs 0-1, then pairs 2-3 + the stores
-    auto piece = [&](auto uc, const f32x4 (&accP)[RB][2], const u32x4 (&xrP)[RB]) {
-      constexpr int u = decltype(uc)::value, r = u / PPR, ph = u % PPR;
-      if (r >= rowsP) return;
-      constexpr int d0 = ph * 2;
-      if constexpr (ph == 0) regroup(accP[r][0], accP[r][1], ez);
-      static_for<d0, d0 + 2>([&](auto dc) {
-        constexpr int d = decltype(dc)::value;
-        const int ra = max(__float_as_int(ez[2 * d]), 0), rb = max(__float_as_int(ez[2 * d + 1]), 0);
-        eyw[d] = pk_bf16(fmaf(h, __int_as_float(ra), lo_f(xrP[r][d])), fmaf(h, __int_as_float(rb), hi_f(xrP[r][d])));
-        ebits = d == 0 ? bit01(ra) : lshl_or<2 * d>(bit01(ra), ebits);
-        ebits = lshl_or<2 * d + 1>(bit01(rb), ebits);
-      });
-      if constexpr (ph == PPR - 1) {
-        if (mbP) {
-          mbP[r * W * (C / 8)] = (uint8_t)ebits;
-          ++nst;
-        }
-        *(u32x4*)(ybP + r * W * C * 2) = eyw;
-        ++nst;
-      }
-    };
-    // band `it` into accC (its residual rows into xrC) with the pending band's epilogue among its MFMAs
-    auto step = [&](int it, f32x4 (&accC)[RB][2], u32x4 (&xrC)[RB], const f32x4 (&accP)[RB][2],
-                    const u32x4 (&xrP)[RB]) {
-      const int buf = it & 1;
-      if (wave == 0) ASR_BTR(0, 0, it, 0);
-      barrier_vm(nst);  // band it landed; every wave is done with band it-1's tile
-      if (wave == 0) ASR_BTR(0, 0, it, 1);
-      nst = 0;
-      if (it + 1 < total) {
-        unsigned char* nt = lds + (buf ^ 1) * TILE;
-        unsigned char* ntile;
-        const int yy = xb * BR;
-        int ngy0, nrows;
-        if (xl == cl && xn == cn && xb == cb + 1) {
-          ntile = nt + 2 * BD::ROWB, ngy0 = yy + 1, nrows = min(BR, H - yy);
-          const uint4* src = (const uint4*)(lds + buf * TILE + BR * BD::ROWB);
-          uint4* dst = (uint4*)nt;
-          constexpr int NCH = 2 * W * NQ;
-          for (int i = tid; i < NCH; i += 64 * NW) {
-            const int o = ((i / (W * NQ)) * TW + 1) * NQ + i % (W * NQ);
-            dst[o] = src[o];
-          }
-        } else {
-          ntile = nt, ngy0 = yy - 1, nrows = min(BR, H - yy) + 2;
-        }
-        const bf16* nxs = src_of(xl);
-        for (int j = wave; j < nrows * IPR; j += NW) dma_row_instr<C, W>(nxs, ntile, xn, ngy0, j, H, loff);
-      }
-      if (wave == 0) ASR_BTR(0, 0, it, 2);
-      const unsigned tb = lds_u32(lds + buf * TILE);
-#pragma unroll
-      for (int r = 0; r < RB; ++r)
-#pragma unroll
-        for (int pt = 0; pt < 2; ++pt) accC[r][pt] = f32x4{bz[0], bz[1], bz[2], bz[3]};
-      auto hook = [&](auto uc) { piece(uc, accP, xrP); };
-      conv_band<C, W, RB, NU>(tb, lo, A, accC, hook);
-      if (wave == 0) ASR_BTR(0, 0, it, 3);
-      // this band's residual rows: retired by the next conv_band's first lgkmcnt(0), before any piece reads them
-#pragma unroll
-      for (int r = 0; r < RB; ++r) xrC[r] = lds_rd128(tb + lxr + (unsigned)(r * BD::ROWB));
-      const int y0 = cb * BR;
-      rowsP = min(BR, H - y0);
-      const long rowb = ((long)cn * H + y0) * W;
-      ybP = (unsigned char*)(out_of(cl) + rowb * C) + ly;
-      mbP = mask_of(cl);
-      if (mbP) mbP += rowb * (C / 8) + lm;
-      if (xl != cl && it + 1 < total) {  // the next item starts block l+1: its W and bias (L2 hits)
-        load_A1<C>(wpack + (long)xl * w_stride, ot, lane, A);
-        const float* bl = bias ? bias + (long)xl * bias_stride : nullptr;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bz[e] = bl ? bl[o0 + e] : 0.f;
-      }
-      if (wave == 0) ASR_BTR(0, 0, it, 4);
-      cl = xl, cn = xn, cb = xb;
-      adv(xl, xn, xb);
-    };
-    for (int it = 0; it < total; it += 2) {
-      step(it, accA, xrA, accB, xrB);
-      if (it + 1 < total) step(it + 1, accB, xrB, accA, xrA);
-    }
-    lgkm_wait<0>();
-    if ((total - 1) & 1) static_for<0, NU>([&](auto uc) { piece(uc, accB, xrB); });
-    else static_for<0, NU>([&](auto uc) { piece(uc, accA, xrA); });
-    ASR_BCLK(0, 1);
-    return;
-  }
   for (int it = 0; it < total; ++it) {
     const int buf = it & 1;
     if (wave == 0) ASR_BTR(0, 0, it, 0);
@@ -3255,13 +3146,8 @@ int block_stack_fwd_mfma(const void* x0, void* ys, long y_stride, uint8_t* masks
   if (cus <= 0) cus = 256;
   const int grid = std::max(1, std::min(N, 2 * cus));
   const size_t lds = 2 * (size_t)(kFwdBR + 2) * (W + 2) * C * 2;
-  if (ASR_FSTACK_PIPE && (H + kFwdBR - 1) / kFwdBR >= 5)  // (a band's stores land one band later)
-    hipLaunchKernelGGL((blk::k_fwd3_stack<64, 32, kFwdBR, false, true>), dim3(grid), dim3(256), lds, s,
-                       (const bf16*)x0, (bf16*)ys, y_stride, masks, mask_stride, (const bf16*)w, w_stride, bias,
-                       bias_stride, h, N, H, L, slots);
-  else
-    hipLaunchKernelGGL((blk::k_fwd3_stack<64, 32, kFwdBR>), dim3(grid), dim3(256), lds, s, (const bf16*)x0, (bf16*)ys,
-                       y_stride, masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, H, L, slots);
+  hipLaunchKernelGGL((blk::k_fwd3_stack<64, 32, kFwdBR>), dim3(grid), dim3(256), lds, s, (const bf16*)x0, (bf16*)ys,
+                     y_stride, masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, H, L, slots);
   ASR_LAUNCH_CHECK("k_fwd3_stack");
   return ASR_OK;
 }
