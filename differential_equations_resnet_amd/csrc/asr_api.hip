@@ -577,8 +577,11 @@ int asr_block_stack_forward(const void* x0, void* ys, long y_stride, uint8_t* ma
   if (store_all && L > 1 && y_stride < (long)N * H * W * C)
     return fail(ASR_E_ARG, "asr_block_stack_forward: y_stride smaller than one activation");
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == ASR_BF16 && deep16_supported(H, W, C))
+  if (dtype == ASR_BF16 && deep16_supported(H, W, C)) {
+    if (L > 1 && w_stride != (long)asr_wpack_elems(C))
+      return fail(ASR_E_ARG, "asr_block_stack_forward: w_stride must be asr_wpack_elems(C) on the fused path");
     return deep16_forward(x0, ys, y_stride, masks, mask_stride, w, bias, bias_stride, h, N, L, store_all != 0, s);
+  }
   if (dtype == ASR_BF16 && !mfma_supported(C, W))
     return fail(ASR_E_UNSUPPORTED, "bf16 conv needs C in {16,32,64} and W == 32 (C=%d W=%d)", C, W);
   if (dtype != ASR_F32 && dtype != ASR_BF16) return fail(ASR_E_ARG, "asr_block_stack_forward: bad dtype");

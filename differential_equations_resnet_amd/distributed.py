@@ -28,7 +28,7 @@ import os
 __all__ = ["init_from_env", "is_initialized", "rank", "world_size", "device_backend", "broadcast_params",
            "allreduce_grads", "max_over_ranks", "barrier", "shutdown"]
 
-_state = {"backend": None}
+_state = {"backend": None, "ctrl": None}
 
 
 def _dist():
@@ -60,7 +60,14 @@ def init_from_env(backend: str | None = None, device=None):
     GPU device) or "gloo".  No-op for WORLD_SIZE 1."""
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world <= 1 or is_initialized():
+    if is_initialized():
+        # The caller made the default group.  The control plane all-reduces
+        # host float64 tensors, so it needs a gloo group of its own when the
+        # default one is nccl (collective: every rank calls this).
+        if _dist().get_backend() != "gloo" and _state["ctrl"] is None:
+            _state["ctrl"] = _dist().new_group(backend="gloo")
+        return
+    if world <= 1:
         return
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     on_gpu = device is not None and torch.device(device).type == "cuda"
@@ -132,7 +139,7 @@ def max_over_ranks(value: float, device=None) -> float:
     if not (is_initialized() and world_size() > 1):
         return float(value)
     t = torch.tensor([value], dtype=torch.float64)
-    _dist().all_reduce(t, op=_dist().ReduceOp.MAX)
+    _dist().all_reduce(t, op=_dist().ReduceOp.MAX, group=_state["ctrl"])
     return float(t.item())
 
 
@@ -141,7 +148,7 @@ def sum_over_ranks(values):
     import torch
     t = torch.tensor(list(values), dtype=torch.float64)
     if is_initialized() and world_size() > 1:
-        _dist().all_reduce(t)
+        _dist().all_reduce(t, group=_state["ctrl"])
     return t.tolist()
 
 
@@ -162,3 +169,4 @@ def shutdown():
             _lib.call("asr_dist_finalize")
         _dist().destroy_process_group()
     _state["backend"] = None
+    _state["ctrl"] = None

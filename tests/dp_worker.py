@@ -5,6 +5,8 @@ the package's distributed layer (backend from argv), one Adam step with
 grad_scale 1/world; results to <outdir>/r<rank>.npz.
 
 usage: python -m torch.distributed.run --nproc-per-node 2 ... tests/dp_worker.py OUTDIR BACKEND [CASE]
+BACKEND: "gloo", "rccl" (asr_dist_*), or "user_nccl" (the caller initialised
+torch.distributed with nccl before the package's init_from_env).
 
 CASE "small" (default): fp32, C=16, L=2, 4 images per rank (the per-block
 fp32 kernels).  CASE "c2": BASELINE C4's per-rank composition at a reduced
@@ -48,7 +50,7 @@ def main():
     outdir, backend = sys.argv[1], sys.argv[2]
     use_case(sys.argv[3] if len(sys.argv) > 3 else "small")
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    if backend == "rccl" and os.environ.get("ASR_TEST_SPLIT_HOSTID"):
+    if backend in ("rccl", "user_nccl") and os.environ.get("ASR_TEST_SPLIT_HOSTID"):
         # two ranks on ONE device: RCCL refuses a duplicate GPU within a host,
         # so each rank claims its own host id and the ranks talk over sockets
         os.environ["NCCL_HOSTID"] = f"asr-dp-test-{rank}"
@@ -56,8 +58,17 @@ def main():
     from differential_equations_resnet_amd import distributed, runtime as rt
     torch.cuda.set_device(0)
     dev = rt.require_gpu()
-    distributed.init_from_env(backend=backend, device=dev)
-    assert distributed.world_size() == world and distributed.device_backend() == backend
+    if backend == "user_nccl":
+        # the caller owns an nccl default group; the package adds a gloo group
+        # for its host-side control plane and leaves the device collectives
+        # to the default group
+        torch.distributed.init_process_group("nccl", rank=rank, world_size=world)
+        distributed.init_from_env(device=dev)
+        assert distributed.device_backend() is None
+    else:
+        distributed.init_from_env(backend=backend, device=dev)
+        assert distributed.device_backend() == backend
+    assert distributed.world_size() == world
     params = torch.from_numpy(params0(100 + rank)).to(dev)  # differs per rank until the broadcast
     distributed.broadcast_params(params, 0)
     imgs, onehot = global_batch(world)

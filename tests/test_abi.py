@@ -178,3 +178,16 @@ def test_inference_workspace_is_bounded(lib):
         assert 0 < b < a and b < 3 * act + 64 * 2 ** 20, (C, L, a, b)
     bad = _lib.NetConfig(512, 32, 32, 3, 64, 30, 10, 0.1, 0.0, 127.5, 127.5, 1, 1, 1, 0, 1, 0, 1 << 12)
     assert lib.asr_net_workspace_bytes(ct.byref(bad)) == 0
+
+
+def test_fused_c16_forward_checks_weight_stride(lib):
+    """The fused C=16 stack reads packed per-layer weights back to back, so
+    asr_block_stack_forward refuses any other w_stride (as the backward
+    does) before launching anything."""
+    from differential_equations_resnet_amd import _lib
+    C, N, L = 16, 2, 3
+    fake = ct.c_void_p(16)  # never dereferenced: the check comes first
+    act = N * 32 * 32 * C
+    rc = lib.asr_block_stack_forward(fake, fake, act, None, 0, fake, lib.asr_wpack_elems(C) + 8, None, 0,
+                                     ct.c_float(0.1), N, 32, 32, C, L, _lib.ASR_BF16, 1, None)
+    assert rc == _lib.ASR_E_ARG

@@ -102,6 +102,16 @@ def test_two_ranks_rccl_c_abi(tmp_path):
     _check(tmp_path)
 
 
+def test_two_ranks_user_nccl_default_group(tmp_path):
+    """A caller that initialised torch.distributed with nccl itself: the
+    package's host-side control plane (max_over_ranks / sum_over_ranks on
+    float64 CPU tensors) runs on a gloo group of its own, the gradient
+    all-reduce on the caller's group."""
+    rc, out = _launch(tmp_path, "user_nccl", RCCL_ONE_DEVICE)
+    assert rc == 0, out[-3000:]
+    _check(tmp_path)
+
+
 @pytest.mark.parametrize("backend", ["gloo", "rccl"])
 def test_two_ranks_c2_composition(tmp_path, backend):
     """BASELINE C4's per-rank composition (bf16, C=64, stacked kernels with
