@@ -50,8 +50,8 @@
 #ifndef ASR_FWD3_WGS
 #define ASR_FWD3_WGS 3  // k_fwd3 workgroups per CU (grid = min(bands, WGS x CUs))
 #endif
-#ifndef ASR_FWD32
-#define ASR_FWD32 0  // A/B: the Euler forward stack on v_mfma_f32_32x32x16_bf16 (k_fwd32_stack)
+#ifndef ASR_BWD_SKEW
+#define ASR_BWD_SKEW 0  // A/B: odd k_bwd3_stack workgroups start this many ~8k-cycle sleeps late (splits the slab bursts)
 #endif
 #ifndef ASR_BWD3_DMA0
 #define ASR_BWD3_DMA0 16  // k_bwd3 wgrad waves: DMA pieces issued right after the barrier, the rest one per row (A/B: spreading them lengthened the MFMA phase as much as it saved; the stacks: all at once 16 vs 9 +0.3-0.5 %, 4 -0.7 %)
@@ -422,6 +422,37 @@ __device__ __forceinline__ void load_A1(const bf16* __restrict__ wpack, int ot, 
 #pragma unroll
   for (int ks = 0; ks < Geo<C>::KS; ++ks)
     A[ks] = *(const bf16x8*)(wpack + (((long)ot * Geo<C>::KS + ks) * 64 + lane) * 8);
+}
+
+// load_A1 / the 4 bias values of lane group g by untracked loads (see
+// gload128_untracked): for the stacks' per-block reloads, whose results the
+// next item's barrier_vm retires.  Unconditional loads into the registers the
+// values live in (a null bias reads the zero page): a conditional load would
+// make hipcc merge the two values with copies that read the registers before
+// the load retires.
+template <int C, int KS0 = 0>
+__device__ __forceinline__ void load_A1_untracked_at(const unsigned char* base, unsigned voff, bf16x8 (&A)[Geo<C>::KS]) {
+  if constexpr (KS0 < Geo<C>::KS) {
+    u32x4 v = __builtin_bit_cast(u32x4, A[KS0]);
+    gload128_untracked<(KS0 % 4) * 1024>(v, base + (KS0 / 4) * 4096, voff);
+    A[KS0] = __builtin_bit_cast(bf16x8, v);
+    load_A1_untracked_at<C, KS0 + 1>(base, voff, A);
+  }
+}
+template <int C>
+__device__ __forceinline__ void load_A1_untracked(const bf16* __restrict__ wpack, int ot, int lane,
+                                                  bf16x8 (&A)[Geo<C>::KS]) {
+  const auto* base = (const unsigned char*)uniform_ptr((const unsigned char*)wpack + (long)ot * Geo<C>::KS * 1024);
+  load_A1_untracked_at<C>(base, (unsigned)lane * 16u, A);
+}
+// b: the wave's 16 bias values (wave-uniform); lane group g reads 4 of them
+__device__ __forceinline__ void load_bias4_untracked(const float* __restrict__ b, int g, float (&bz)[4]) {
+  const void* base = uniform_ptr(b ? (const void*)b : (const void*)g_zero_page);
+  const unsigned voff = (unsigned)g * 16u;
+  gload32_untracked<0>(bz[0], base, voff);
+  gload32_untracked<4>(bz[1], base, voff);
+  gload32_untracked<8>(bz[2], base, voff);
+  gload32_untracked<12>(bz[3], base, voff);
 }
 
 template <int C>
@@ -1017,13 +1048,15 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
     return m ? m + (long)blk_of(st) * mask_stride : nullptr;
   };
 
-  bf16x8 A[G::KS];
-  load_A1<C>(wpack, ot, lane, A);
+  // A and the bias by untracked loads, here and at every block switch: the
+  // next item's barrier_vm retires them (tracked, hipcc would wait vmcnt(0)
+  // before each band's first MFMA, i.e. for the next band's DMA as well)
+  bf16x8 A[G::KS] = {};
+  load_A1_untracked<C>(wpack, ot, lane, A);
   unsigned lo[3 * BD::NCB];
   band_lane_offsets<C, W, RB>(g, lx, lo);
-  float bz[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) bz[e] = bias ? bias[o0 + e] : 0.f;
+  float bz[4] = {0.f, 0.f, 0.f, 0.f};
+  load_bias4_untracked(bias ? bias + 16 * ot : nullptr, g, bz);
   const unsigned lxr = (unsigned)toff<C>(1, px + 1, cg, TW);
   const unsigned ly = (unsigned)(px * C + 8 * cg) * 2u, lm = (unsigned)(px * (C / 8) + cg);
 
@@ -1075,7 +1108,8 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
       } else {
         ntile = nt, ngy0 = yy - 1, nrows = min(BR, H - yy) + 2;
       }
-      for (int j = wave; j < nrows * IPR; j += NW) dma_row_instr<C, W>(nxs, ntile, xn, ngy0, j, H, loff);
+      for (int j = __builtin_amdgcn_readfirstlane(wave); j < nrows * IPR; j += NW)
+        dma_row_instr<C, W>(nxs, ntile, xn, ngy0, j, H, loff);
     }
     if (wave == 0) ASR_BTR(0, 0, it, 2);
     const unsigned tb = lds_u32(lds + buf * TILE);
@@ -1100,10 +1134,11 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
     }
     const int l = cl;
     if (blk_of(xl) != blk_of(cl) && it + 1 < total) {  // the next item starts block l+1: its W and bias (L2 hits)
-      load_A1<C>(wpack + (long)blk_of(xl) * w_stride, ot, lane, A);
-      const float* bl = bias ? bias + (long)blk_of(xl) * bias_stride : nullptr;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bz[e] = bl ? bl[o0 + e] : 0.f;
+      load_A1_untracked<C>(wpack + (long)blk_of(xl) * w_stride, ot, lane, A);
+      load_bias4_untracked(bias ? bias + (long)blk_of(xl) * bias_stride + 16 * ot : nullptr, g, bz);
+#ifdef ASR_RELOAD_WAIT
+      vm_wait(0);
+#endif
     }
     lgkm_wait<0>();
     const int y0 = cb * BR, rows = min(BR, H - y0);
@@ -1138,215 +1173,6 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
     adv(xl, xn, xb);
   }
   ASR_BCLK(0, 1);
-}
-
-// ===========================================================================
-// Stack forward on v_mfma_f32_32x32x16_bf16 (C=64, W=32, BR=4, Euler; the
-// ASR_FWD32 A/B arm of k_fwd3_stack).  A 32x32x16 MFMA takes 32 cycles and
-// holds the SIMD's vector issue for 8 of them, so per FLOP it leaves three
-// times the free issue cycles of 16x16x32 (8 of 16) for the epilogue's VALU,
-// which is what bounds the 16x16x32 stack (3.1 VALU per MFMA).
-//   D[o][p] = sum_kappa W^T[o][kappa] X[p][kappa], M = 32 output channels
-//   (o-half T), N = the 32 pixels of one output row, K = 16 per MFMA (kappa =
-//   16 ks + k, tap = ks / 4, channel 16 (ks % 4) + k): 36 k-steps per row.
-// Wave w: o-half T = w & 1, output rows 2R, 2R+1 (R = w >> 1) of the band; A
-// (W^T of its 32 channels, 36 x 4 VGPRs) stays in registers.  The B fragment
-// of input row ir, tap column kx, channel quarter c4 (lane: pixel lane % 32,
-// channels 16 c4 + 8 (lane / 32) + 0..7: one 16-B read) feeds the rows
-// 2R..2R+1 that use it (1.5 MFMAs per read).  D rows reach a lane as o =
-// 8 (r / 4) + 4 (lane / 32) + r % 4; v_permlane32_swap of register groups
-// (0,1) and (2,3) gives each lane two 8-channel chunks of its pixel (chunks
-// 4T + h and 4T + 2 + h, h = lane / 32), stored as 16 B each with a mask byte.
-// Tile layout, DMA, halo copy and ordering: as k_fwd3_stack.
-// ===========================================================================
-template <int C, int W, int BR>
-__global__ __launch_bounds__(256, 2) void k_fwd32_stack(const bf16* __restrict__ x0, bf16* __restrict__ ys,
-                                                        long y_stride, uint8_t* __restrict__ masks, long mask_stride,
-                                                        const bf16* __restrict__ wpack, long w_stride,
-                                                        const float* __restrict__ bias, long bias_stride, float h,
-                                                        int N, int H, int L, int slots) {
-  using G = Geo<C>;
-  constexpr int TW = W + 2, NQ = G::NQ, NW = 4, KS16 = 9 * C / 16;
-  static_assert(C == 64 && W == 32 && BR == 4, "32x32x16 stack geometry");
-  using BD = Band<C, W, BR>;
-  constexpr int TILE = (BR + 2) * BD::ROWB;
-  typedef float f32x16 __attribute__((ext_vector_type(16)));
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int T = wave & 1, R = wave >> 1;
-  const int p = lane & 31, hh = lane >> 5;
-
-  const int n0 = (int)((long)blockIdx.x * N / gridDim.x), n1 = (int)((long)(blockIdx.x + 1) * N / gridDim.x);
-  if (n0 >= n1) return;
-  const int nb = (H + BR - 1) / BR, per = (n1 - n0) * nb;
-  auto slot_of = [&](int l) -> long { return slots > 0 ? (long)(l % slots) : (long)l; };
-  auto src_of = [&](int l) -> const bf16* { return l == 0 ? x0 : ys + slot_of(l - 1) * y_stride; };
-  auto out_of = [&](int l) -> bf16* { return ys + slot_of(l) * y_stride; };
-
-  // A fragments of k-step ks from the 16x16x32 pack (asr_theta_to_w): o = 32T + lane % 32,
-  // kappa = 16 ks + 8 (lane / 32) + j  ->  o-tile 2T + p / 16, 32-deep step ks / 2, lane' below
-  bf16x8 A[KS16];
-  auto load_A = [&](const bf16* wp) {
-    const int ot = 2 * T + (p >> 4);
-#pragma unroll
-    for (int ks = 0; ks < KS16; ++ks) {
-      const int lp = (p & 15) + 16 * (2 * (ks & 1) + hh);
-      A[ks] = *(const bf16x8*)(wp + (((long)ot * G::KS + ks / 2) * 64 + lp) * 8);
-    }
-  };
-  load_A(wpack);
-  // the blocks' biases in LDS behind the two tiles, block l in slot l & 1 (64 floats each,
-  // written by wave 0 one block ahead; read at every band's accumulator init: the lane's D rows
-  // o = 32T + 8 (r / 4) + 4 hh + r % 4 are four 16-B chunks)
-  float* bias_lds = (float*)(lds + 2 * TILE);
-  auto stage_bias = [&](const float* bl, int slot) {
-    if (wave == 0) bias_lds[64 * slot + lane] = bl ? bl[lane] : 0.f;
-  };
-  stage_bias(bias, 0);
-  const unsigned lbz = lds_u32(lds + 2 * TILE) + (unsigned)((32 * T + 4 * hh) * 4);
-  // B lane offsets (bytes within a tile row) of tap column kx, channel quarter c4
-  unsigned bo[12];
-#pragma unroll
-  for (int kx = 0; kx < 3; ++kx)
-#pragma unroll
-    for (int c4 = 0; c4 < 4; ++c4) bo[kx * 4 + c4] = (unsigned)toff<C>(0, p + kx, 2 * c4 + hh, TW);
-  // epilogue: the lane's two 8-channel chunks of pixel p (residual at tile row r + 1, column p + 1)
-  const int ca = 4 * T + hh, cbk = 4 * T + 2 + hh;
-  const unsigned lra = (unsigned)toff<C>(1, p + 1, ca, TW), lrb = (unsigned)toff<C>(1, p + 1, cbk, TW);
-
-  zero_halo_cols<C, W>(lds, BR + 2, tid, 64 * NW);
-  zero_halo_cols<C, W>(lds + TILE, BR + 2, tid, 64 * NW);
-  constexpr int IPR = W / G::PPI;
-  const unsigned loff = (unsigned)dma_lane_off<C, W>(lane) * 2u;
-  int cl = 0, cn = n0, cb = 0;
-  int xl = 0, xn = n0, xb = 0;
-  auto adv = [&](int& l, int& n, int& b) {
-    if (++b == nb) {
-      b = 0;
-      if (++n == n1) {
-        n = n0;
-        ++l;
-      }
-    }
-  };
-  adv(xl, xn, xb);
-  dma_rows<C, W>(x0, lds, cn, -1, min(BR, H) + 2, H, wave, NW, lane);
-  int nst = 0;
-  const int total = L * per;
-  for (int it = 0; it < total; ++it) {
-    const int buf = it & 1;
-    barrier_vm(nst);  // band it landed; every wave is done with band it-1's tile
-    nst = 0;
-    if (it + 1 < total) {
-      unsigned char* nt = lds + (buf ^ 1) * TILE;
-      unsigned char* ntile;
-      const int yy = xb * BR;
-      int ngy0, nrows;
-      if (xl == cl && xn == cn && xb == cb + 1) {
-        ntile = nt + 2 * BD::ROWB, ngy0 = yy + 1, nrows = min(BR, H - yy);
-        const uint4* src = (const uint4*)(lds + buf * TILE + BR * BD::ROWB);
-        uint4* dst = (uint4*)nt;
-        constexpr int NCH = 2 * W * NQ;
-        for (int i = tid; i < NCH; i += 64 * NW) {
-          const int o = ((i / (W * NQ)) * TW + 1) * NQ + i % (W * NQ);
-          dst[o] = src[o];
-        }
-      } else {
-        ntile = nt, ngy0 = yy - 1, nrows = min(BR, H - yy) + 2;
-      }
-      const bf16* nxs = src_of(xl);
-      for (int j = wave; j < nrows * IPR; j += NW) dma_row_instr<C, W>(nxs, ntile, xn, ngy0, j, H, loff);
-    }
-    // rows 2R, 2R+1: input tile rows 2R .. 2R+3; stages s = (kx, c4) major, input row minor
-    const unsigned tb = lds_u32(lds + buf * TILE) + (unsigned)(2 * R * BD::ROWB);
-    f32x16 acc[2];
-    {
-      u32x4 bv[4];
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) bv[g4] = lds_ld128(lbz + (unsigned)((cl & 1) * 256 + g4 * 32));
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[q][r] = __uint_as_float(bv[r / 4][r % 4]);
-    }
-    constexpr int NS = 12 * 4;
-    bf16x8 Bf[3];
-    lgkm_wait<0>();
-    static_for<0, 2>([&](auto sc) {
-      constexpr int S = decltype(sc)::value;
-      Bf[S] = ds_read128<(S % 4) * BD::ROWB>(tb + bo[S / 4]);
-    });
-    static_for<0, NS>([&](auto sc) {
-      constexpr int S = decltype(sc)::value, kc = S / 4, ir = S % 4, kx = kc / 4, c4 = kc % 4;
-      lgkm_wait<(S + 1 < NS) ? 1 : 0>();
-      // output row ro = ir - ky of this wave's pair (ro in {0, 1})
-      static_for<0, 3>([&](auto kyc) {
-        constexpr int ky = decltype(kyc)::value, ro = ir - ky;
-        if constexpr (ro >= 0 && ro < 2)
-          acc[ro] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[(ky * 3 + kx) * 4 + c4], Bf[S % 3], acc[ro], 0, 0, 0);
-      });
-      if constexpr (S + 2 < NS) {
-        constexpr int S2 = S + 2;
-        Bf[S2 % 3] = ds_read128<(S2 % 4) * BD::ROWB>(tb + bo[S2 / 4]);
-      }
-    });
-    // residual chunks of this wave's two rows (tile rows 2R+1, 2R+2)
-    u32x4 xra[2], xrb[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const unsigned rb = lds_u32(lds + buf * TILE) + (unsigned)((2 * R + q) * BD::ROWB);
-      xra[q] = lds_rd128(rb + lra);
-      xrb[q] = lds_rd128(rb + lrb);
-    }
-    const int l = cl;
-    if (xl != cl && it + 1 < total) {  // the next item starts block l+1: its W and bias (L2 hits)
-      load_A(wpack + (long)xl * w_stride);
-      stage_bias(bias ? bias + (long)xl * bias_stride : nullptr, xl & 1);  // read after the next band barrier
-    }
-    lgkm_wait<0>();
-    const int y0 = cb * BR, rows = min(BR, H - y0);
-    const long rowb = ((long)cn * H + y0 + 2 * R) * W + p;
-    unsigned char* yb = (unsigned char*)(out_of(l) + rowb * C);
-    uint8_t* mb = masks ? masks + (long)l * mask_stride + rowb * (C / 8) : nullptr;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (2 * R + q >= rows) break;
-      // two 8-channel chunks per lane: swap register groups (0,1) and (2,3) between the lane halves
-      float za[8], zb[8];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const auto s0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[q][j]), __float_as_uint(acc[q][4 + j]),
-                                                         false, false);
-        za[j] = __uint_as_float(s0[0]);
-        za[4 + j] = __uint_as_float(s0[1]);
-        const auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[q][8 + j]),
-                                                         __float_as_uint(acc[q][12 + j]), false, false);
-        zb[j] = __uint_as_float(s1[0]);
-        zb[4 + j] = __uint_as_float(s1[1]);
-      }
-      auto chunk = [&](const float (&z)[8], const u32x4& xr, int c) {
-        u32x4 yw;
-        unsigned bits = 0;
-        static_for<0, 4>([&](auto dc) {
-          constexpr int d = decltype(dc)::value;
-          const int ra = max(__float_as_int(z[2 * d]), 0), rb = max(__float_as_int(z[2 * d + 1]), 0);
-          yw[d] = pk_bf16(fmaf(h, __int_as_float(ra), lo_f(xr[d])), fmaf(h, __int_as_float(rb), hi_f(xr[d])));
-          bits = d == 0 ? bit01(ra) : lshl_or<2 * d>(bit01(ra), bits);
-          bits = lshl_or<2 * d + 1>(bit01(rb), bits);
-        });
-        if (mb) {
-          mb[q * W * (C / 8) + c] = (uint8_t)bits;
-          ++nst;
-        }
-        *(u32x4*)(yb + ((long)q * W * C + 8 * c) * 2) = yw;
-        ++nst;
-      };
-      chunk(za, xra[q], ca);
-      chunk(zb, xrb[q], cbk);
-    }
-    cl = xl, cn = xn, cb = xb;
-    adv(xl, xn, xb);
-  }
 }
 
 // ===========================================================================
@@ -2492,14 +2318,19 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
   };
   __syncthreads();
   if (n0 >= n1) return;  // (uniform per workgroup: never with grid <= N)
+  if (ASR_BWD_SKEW && (blockIdx.x & 1))
+    for (int i = 0; i < ASR_BWD_SKEW; ++i) __builtin_amdgcn_s_sleep(127);
   ASR_BCLK(1, 0);
 
   constexpr int ES = 9 * C * C + C, ECH = ES / 4;
   if (wave < 4) {
     // ---------------- dgrad waves ----------------
     const int ot = wave;
-    bf16x8 A[G::KS];
-    load_A1<C>(wpack + (long)(L - 1) * w_stride, ot, lane, A);
+    // W by untracked loads, here and at each block switch: the next item's
+    // barrier_vm retires them (a tracked reload made hipcc wait vmcnt(0) before
+    // every band's first MFMA, i.e. for the previous band's dx stores)
+    bf16x8 A[G::KS] = {};
+    load_A1_untracked<C>(wpack + (long)(L - 1) * w_stride, ot, lane, A);
     unsigned lo[3 * BD::NCB];
     band_lane_offsets<C, W, BR>(g, lx, lo);
     const int px = lx + 16 * (g & 1), cg = 2 * ot + (g >> 1);
@@ -2533,7 +2364,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       if (wave == 0) ASR_BTR(1, 0, it, 2);
       const bool last_of_stage = cur.b == nb - 1 && n == n1 - 1;
       if (last_of_stage && blk_of(l) > 0 && (!RK2 || s1))
-        load_A1<C>(wpack + (long)(blk_of(l) - 1) * w_stride, ot, lane, A);
+        load_A1_untracked<C>(wpack + (long)(blk_of(l) - 1) * w_stride, ot, lane, A);
       bf16* drow = dx_of(l) + ((long)n * H + y0) * W * C;
       int nld = 0;
       auto epilogue = [&](auto g2c, auto roc, auto kc) {
@@ -3358,14 +3189,9 @@ int block_stack_fwd_mfma(const void* x0, void* ys, long y_stride, uint8_t* masks
   if (cus <= 0) cus = 256;
   const int grid = std::max(1, std::min(N, 2 * cus));
   const size_t lds = 2 * (size_t)(kFwdBR + 2) * (W + 2) * C * 2;
-  if (ASR_FWD32)
-    hipLaunchKernelGGL((blk::k_fwd32_stack<64, 32, kFwdBR>), dim3(grid), dim3(256), lds + 512, s, (const bf16*)x0,
-                       (bf16*)ys, y_stride, masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, H, L,
-                       slots);
-  else
-    hipLaunchKernelGGL((blk::k_fwd3_stack<64, 32, kFwdBR>), dim3(grid), dim3(256), lds, s, (const bf16*)x0,
-                       (bf16*)ys, y_stride, masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, H,
-                       L, slots);
+  hipLaunchKernelGGL((blk::k_fwd3_stack<64, 32, kFwdBR>), dim3(grid), dim3(256), lds, s, (const bf16*)x0,
+                     (bf16*)ys, y_stride, masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, H, L,
+                     slots);
   ASR_LAUNCH_CHECK("k_fwd3_stack");
   return ASR_OK;
 }

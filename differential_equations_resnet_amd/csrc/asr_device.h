@@ -60,21 +60,36 @@ __device__ __forceinline__ void dma16_at(const void* src, unsigned lds_addr) {
       : "memory", "m0");
 }
 
-// Workgroup barrier that waits only for this wave's vector-memory ops OLDER
-// than its `n` youngest (vmcnt counts loads, stores and LDS-DMA in issue
-// order).  Used so that the barrier guarding an LDS-DMA'd buffer does not
-// also wait for the global stores issued after that DMA.
-__device__ __forceinline__ void barrier_vm(int n) {
-#define ASR_BVM(k) \
-  case k: asm volatile("s_waitcnt vmcnt(" #k ") lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
-  switch (n) {
-    ASR_BVM(1) ASR_BVM(2) ASR_BVM(3) ASR_BVM(4) ASR_BVM(5) ASR_BVM(6) ASR_BVM(7) ASR_BVM(8)
-    ASR_BVM(9) ASR_BVM(10) ASR_BVM(11) ASR_BVM(12) ASR_BVM(13) ASR_BVM(14) ASR_BVM(15) ASR_BVM(16)
-    ASR_BVM(17) ASR_BVM(18) ASR_BVM(19) ASR_BVM(20) ASR_BVM(21) ASR_BVM(22) ASR_BVM(23) ASR_BVM(24)
-    default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
-  }
-#undef ASR_BVM
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+// 16-B / 4-B global loads the compiler does not track: it inserts no wait
+// before their results are used.  For operands reloaded inside a loop whose
+// next iteration starts with a counted barrier_vm that retires them (every
+// vector-memory op older than the stores issued after them): with tracked
+// loads hipcc waits vmcnt(0) before the first use, which also waits for the
+// LDS-DMA of the next band issued since.  "+v": the result lands in the
+// registers the value already lives in (tests/test_isa.py checks that no
+// instruction reads them before the wait).
+// Wave-uniform base (SGPRs) + 32-bit lane offset + immediate (< 4 KiB).  The
+// base usually comes from v_readfirstlane (a VALU write of an SGPR), which a
+// VMEM instruction may read only 5 wait states later; hipcc does not insert
+// them in front of inline asm, so the asm does (s_nop 4).
+template <int IMM>
+__device__ __forceinline__ void gload128_untracked(u32x4& v, const void* sbase, unsigned voff) {
+  static_assert(IMM >= 0 && IMM < 4096, "global immediate offset range");
+  asm volatile("s_nop 4\n\tglobal_load_dwordx4 %0, %1, %2 offset:%3" : "+v"(v) : "v"(voff), "s"(sbase), "i"(IMM) : "memory");
 }
+template <int IMM>
+__device__ __forceinline__ void gload32_untracked(float& v, const void* sbase, unsigned voff) {
+  static_assert(IMM >= 0 && IMM < 4096, "global immediate offset range");
+  asm volatile("s_nop 4\n\tglobal_load_dword %0, %1, %2 offset:%3" : "+v"(v) : "v"(voff), "s"(sbase), "i"(IMM) : "memory");
+}
+// a pointer made wave-uniform (SGPRs)
+__device__ __forceinline__ const void* uniform_ptr(const void* p) {
+  const unsigned long long a = (unsigned long long)(uintptr_t)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return (const void*)(uintptr_t)(((unsigned long long)hi << 32) | lo);
+}
+
 // barrier for LDS data only (in-flight DMA and stores keep flying)
 __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
@@ -102,7 +117,6 @@ __device__ __forceinline__ void lgkm_wait() {
 // outstanding (it cannot tell the DMA's destination buffer apart), which
 // would serialise the next band's prefetch with this band's work.  The
 // caller waits lgkmcnt itself (lgkm_wait) before using a read result.
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u32x4 lds_rd128(unsigned addr) {
   u32x4 v;
@@ -129,7 +143,7 @@ __device__ __forceinline__ void lds_wr128(unsigned addr, u32x4 v) {
 __device__ __forceinline__ void vm_wait(int n) {
 #define ASR_VMW(k) \
   case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-  switch (n) {
+  switch (__builtin_amdgcn_readfirstlane(n)) {
     ASR_VMW(1) ASR_VMW(2) ASR_VMW(3) ASR_VMW(4) ASR_VMW(5) ASR_VMW(6) ASR_VMW(7) ASR_VMW(8)
     ASR_VMW(9) ASR_VMW(10) ASR_VMW(11) ASR_VMW(12) ASR_VMW(13) ASR_VMW(14) ASR_VMW(15) ASR_VMW(16)
     ASR_VMW(17) ASR_VMW(18) ASR_VMW(19) ASR_VMW(20) ASR_VMW(21) ASR_VMW(22) ASR_VMW(23) ASR_VMW(24)
@@ -139,6 +153,14 @@ __device__ __forceinline__ void vm_wait(int n) {
       break;
   }
 #undef ASR_VMW
+}
+// Workgroup barrier that waits only for this wave's vector-memory ops OLDER
+// than its `n` youngest (vmcnt counts loads, stores and LDS-DMA in issue
+// order).  Used so that the barrier guarding an LDS-DMA'd buffer does not
+// also wait for the global stores issued after that DMA.
+__device__ __forceinline__ void barrier_vm(int n) {
+  vm_wait(n);  // the counted wait, then one barrier every path reaches
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 // instructions one wave issues in a `for (j = wave; j < total; j += nw)` loop
 __device__ __forceinline__ int strided_count(int total, int wave, int nw) {

@@ -8,6 +8,12 @@ LDS reads and LDS-DMA, which the compiler cannot see:
     (tools/asm_lds_audit.py) models lgkmcnt as an in-order queue per basic
     block; it must find nothing in any product source, and it must flag a
     kernel that reintroduces the hazard (self-test below);
+  * the same for the untracked global loads (gload128_untracked /
+    gload32_untracked: the stacks' per-block weight and bias reloads, which
+    the next item's barrier_vm retires): tools/asm_vmem_audit.py walks the
+    control-flow graph from each such load and flags any instruction that
+    touches its registers before a retiring vmcnt wait or barrier_vm's
+    barrier (self-test below);
   * register spills: a compiler-inserted scratch access only ever adds
     vector-memory ops, which makes a counted `vmcnt(n)` wait MORE conservative
     (it retires the oldest ops first), never less; but a spill is also where
@@ -29,6 +35,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "differential_equations_resnet_amd", "csrc")
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import asm_lds_audit  # noqa: E402
+import asm_vmem_audit  # noqa: E402
 
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 pytestmark = pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
@@ -105,6 +112,39 @@ extern "C" __global__ void k(unsigned* out, unsigned a) {
         src.write_text(tmpl.replace("WAIT", wait))
         asm = _compile(str(src), str(src) + ".s")
         bad, _ = asm_lds_audit.audit(open(asm).read())
+        assert (bad > 0) == want_bad, (wait, bad)
+
+
+def test_asm_vmem_audit_clean(asm_files):
+    n_loads = 0
+    for f in asm_files:
+        text = open(f).read()
+        n_loads += len(re.findall(r"global_load_dword\w* v", text.split(".end_amdgpu_metadata")[0]))
+        bad, findings = asm_vmem_audit.audit(text)
+        assert bad == 0, f"{os.path.basename(f)}: " + "\n".join(findings[:10])
+    assert n_loads > 0
+
+
+def test_asm_vmem_audit_catches_early_use(tmp_path):
+    """An untracked global load whose result is used before any vmcnt wait is
+    flagged; with the wait (or a barrier_vm-style wait + barrier) first it is not."""
+    tmpl = r'''
+#include <hip/hip_runtime.h>
+extern "C" __global__ void k(float* out, const float* p) {
+  float v = 0.f;
+  asm volatile("global_load_dword %0, %1, off" : "+v"(v) : "v"(p + threadIdx.x) : "memory");
+  WAIT
+  out[threadIdx.x] = v * 2.f;
+}
+'''
+    cases = (("", True), ('asm volatile("s_waitcnt vmcnt(0)" ::: "memory");', False),
+             ('asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory");',
+              False))
+    for i, (wait, want_bad) in enumerate(cases):
+        src = tmp_path / ("v%d.hip" % i)
+        src.write_text(tmpl.replace("WAIT", wait))
+        asm = _compile(str(src), str(src) + ".s")
+        bad, _ = asm_vmem_audit.audit(open(asm).read())
         assert (bad > 0) == want_bad, (wait, bad)
 
 

@@ -1,4 +1,4 @@
-"""Development check of a forward-stack variant build (e.g. ASR_FWD32=1) that
+"""Development check of a forward-stack variant build that
 is not bitwise equal to the per-block kernels: every layer of
 asr_block_stack_forward against the oracle's Euler step on the variant's own
 bf16 input of that layer (2^-8 relative + 4e-3 * max|ref|, as
