@@ -50,9 +50,6 @@
 #ifndef ASR_FWD3_WGS
 #define ASR_FWD3_WGS 3  // k_fwd3 workgroups per CU (grid = min(bands, WGS x CUs))
 #endif
-#ifndef ASR_BWD_SKEW
-#define ASR_BWD_SKEW 0  // A/B: odd k_bwd3_stack workgroups start this many ~8k-cycle sleeps late (splits the slab bursts)
-#endif
 #ifndef ASR_BWD3_DMA0
 #define ASR_BWD3_DMA0 16  // k_bwd3 wgrad waves: DMA pieces issued right after the barrier, the rest one per row (A/B: spreading them lengthened the MFMA phase as much as it saved; the stacks: all at once 16 vs 9 +0.3-0.5 %, 4 -0.7 %)
 #endif
@@ -1136,9 +1133,6 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
     if (blk_of(xl) != blk_of(cl) && it + 1 < total) {  // the next item starts block l+1: its W and bias (L2 hits)
       load_A1_untracked<C>(wpack + (long)blk_of(xl) * w_stride, ot, lane, A);
       load_bias4_untracked(bias ? bias + (long)blk_of(xl) * bias_stride + 16 * ot : nullptr, g, bz);
-#ifdef ASR_RELOAD_WAIT
-      vm_wait(0);
-#endif
     }
     lgkm_wait<0>();
     const int y0 = cb * BR, rows = min(BR, H - y0);
@@ -2318,8 +2312,6 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
   };
   __syncthreads();
   if (n0 >= n1) return;  // (uniform per workgroup: never with grid <= N)
-  if (ASR_BWD_SKEW && (blockIdx.x & 1))
-    for (int i = 0; i < ASR_BWD_SKEW; ++i) __builtin_amdgcn_s_sleep(127);
   ASR_BCLK(1, 0);
 
   constexpr int ES = 9 * C * C + C, ECH = ES / 4;
