@@ -3,13 +3,15 @@ of asr_device.h: gload128_untracked / gload32_untracked) must not be read or
 written by any instruction until an s_waitcnt vmcnt retires the load.  Walks
 the control-flow graph of each function from every such load (fall-through
 and branch targets, loop back-edges included), counting the vector-memory
-ops issued after the load on each path (vmcnt retires in issue order, so
-s_waitcnt vmcnt(k) retires it once k or more younger ops were issued); a
-barrier_vm's s_barrier also ends the walk: barrier_vm = vm_wait(n) (a
-switch of counted waits) + one asm barrier, so every path into that barrier
-passed a wait whose count is the stores issued since (kept by the source:
-the protocol that guards the LDS-DMA'd tiles, checked by the GPU parity
-tests).  Any instruction on a path before that which mentions one of
+ops issued after the load on each path (vmcnt retires in issue order, so a
+compiler s_waitcnt vmcnt(k) retires it once k or more younger ops were
+issued).  The kernels' own counted waits (vm_wait / barrier_vm: asm
+s_waitcnt whose count is the ops the source issued since, the protocol that
+guards the LDS-DMA'd tiles and is checked by the GPU parity tests) end the
+walk as well; the audit proves that every path reaches one of them before
+anything touches the registers.  Guards of the structurized switch inside
+vm_wait are tracked (see _flags_after), so paths that skip every case are
+not taken.  Any instruction on a path before that which mentions one of
 the registers is a finding: the compiler copied, spilled or reused them.  Used by tests/test_isa.py; as a script it scans one .s file."""
 import re
 import sys
@@ -51,6 +53,51 @@ def _parse(func_text):
     return ins, labels
 
 
+# The backend structurizes a switch into guarded blocks whose guards are SGPR
+# flags (s_mov_b64 s[a:b], -1 / 0; s_and(n2)_b64 vcc, exec, s[a:b];
+# s_cbranch_vcc(n)z): tracking those constants keeps the walk off paths that
+# skip every case of a counted-wait switch, which cannot execute.
+def _flags_after(flags, op, body):
+    d = dict(flags)
+    args = [a.strip() for a in body.split(None, 1)[1].split(",")] if " " in body else []
+    dst = args[0] if args else ""
+    if op in ("s_and_b64", "s_andn2_b64") and dst == "vcc" and len(args) == 3 and args[1] == "exec":
+        v = d.get(args[2])
+        d.pop("vcc", None)
+        if v is not None:
+            d["vcc"] = (v != 0) if op == "s_and_b64" else (v == 0)
+        return frozenset(d.items())
+    if op.startswith("v_cmp") or dst == "vcc" or dst.startswith("vcc"):
+        d.pop("vcc", None)
+    if op.startswith("s_") and dst.startswith("s["):
+        lo, hi = (int(t) for t in re.match(r"s\[(\d+):(\d+)\]", dst).groups())
+        for key in [key for key in d if key.startswith("s[")]:
+            a0, a1 = (int(t) for t in re.match(r"s\[(\d+):(\d+)\]", key).groups())
+            if not (a1 < lo or a0 > hi):
+                d.pop(key)
+        if op == "s_mov_b64" and len(args) == 2 and args[1] in ("-1", "0"):
+            d[dst] = int(args[1])
+    elif op.startswith("s_") and re.match(r"s(\d+)$", dst):
+        r = int(dst[1:])
+        for key in [key for key in d if key.startswith("s[")]:
+            a0, a1 = (int(t) for t in re.match(r"s\[(\d+):(\d+)\]", key).groups())
+            if a0 <= r <= a1:
+                d.pop(key)
+    return frozenset(d.items())
+
+
+def _branch_known(flags, op):
+    """True / False when the branch direction follows from a known vcc, else None."""
+    v = dict(flags).get("vcc")
+    if v is None:
+        return None
+    if op == "s_cbranch_vccz":
+        return not v
+    if op == "s_cbranch_vccnz":
+        return bool(v)
+    return None
+
+
 def audit(src):
     funcs = re.split(r"\n(?=_Z[\w]+:|[A-Za-z_]\w*:\s+; @)", src)
     bad, findings = 0, []
@@ -64,18 +111,16 @@ def audit(src):
             lo = int(m.group(2))
             regs = set(range(lo, int(m.group(3) or lo) + 1))
             seen = set()
-            stack = [(i + 1, 0)]
+            stack = [(i + 1, 0, frozenset())]
             while stack:
-                k, younger = stack.pop()
-                if k >= len(ins) or (k, younger) in seen:
+                k, younger, flags = stack.pop()
+                if k >= len(ins) or (k, younger, flags) in seen:
                     continue
-                seen.add((k, younger))
+                seen.add((k, younger, flags))
                 op2, body2, _ = ins[k]
                 w = re.search(r"s_waitcnt.*vmcnt\((\d+)\)", body2)
-                if w and younger >= int(w.group(1)):
-                    continue  # retired on this path
-                if op2 == "s_barrier" and ins[k][2]:
-                    continue  # barrier_vm: its counted wait precedes this barrier on every path
+                if w and (younger >= int(w.group(1)) or ins[k][2]):
+                    continue  # retired on this path, or a counted asm wait (vm_wait / barrier_vm)
                 if not w and _regs(body2.split(None, 1)[1] if " " in body2 else "") & regs:
                     bad += 1
                     findings.append(f"{name}: '{body[:50]}' result touched by '{body2[:60]}' before a retiring wait")
@@ -83,13 +128,15 @@ def audit(src):
                 if op2 == "s_endpgm":
                     continue
                 y = min(younger + (1 if op2.startswith(VMEM) else 0), 64)
+                fl = _flags_after(flags, op2, body2)
                 if op2 == "s_branch" or op2.startswith("s_cbranch"):
                     tgt = body2.split()[-1]
-                    if tgt in labels:
-                        stack.append((labels[tgt], y))
-                    if op2 == "s_branch":
+                    taken = _branch_known(flags, op2)
+                    if tgt in labels and taken is not False:
+                        stack.append((labels[tgt], y, fl))
+                    if op2 == "s_branch" or taken is True:
                         continue
-                stack.append((k + 1, y))
+                stack.append((k + 1, y, fl))
     return bad, findings
 
 
