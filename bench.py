@@ -470,6 +470,10 @@ def main():
     h = 8.0 / L  # final_time 8 (experiments_antisymmetric_resnet_v6.ipynb cell 1)
     ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, h, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
                         dtype=dtype_name, input_u8=True, device=dev, integrator=integrator, inference=not train)
+    # ranks sharing one device (test only) cannot keep both stacked backward grids resident:
+    # no in-launch slab hand-off then (ASR_VARIANT_NO_FOLD), so no workgroup waits for another
+    base_variant = rt.ASR_VARIANT_NO_FOLD if args.share_device else 0
+    ex.variant = base_variant
     params = torch.from_numpy(bench_params(C, L)).to(dev)
     distributed.broadcast_params(params, 0)
     m = torch.zeros_like(params)
@@ -521,12 +525,12 @@ def main():
         ex.check_status()  # blocking: the stacked backward's slab hand-off never timed out
 
     # the timed step's own block kernels: events inside instrumented steps (all ranks take part)
-    ex.variant = rt.ASR_VARIANT_TIMED
+    ex.variant = rt.ASR_VARIANT_TIMED | base_variant
     kts = []
     for _ in range(max(1, args.timed_steps)):
         step()
         kts.append(ex.kernel_times())
-    ex.variant = 0
+    ex.variant = base_variant
     if train:
         ex.check_status()
 

@@ -57,7 +57,8 @@ int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride
                          long mask_stride, const void* w, long w_stride, float h, float two_gamma, int N, int H, int W,
                          int C, int L, int ro0, float* slabs, long slab_stride, float* grp, long grp_stride,
                          unsigned* done, int* lfold_out, hipStream_t s, const void* xm = nullptr,
-                         const uint8_t* masks2 = nullptr, void* gbuf = nullptr, const void* gtop = nullptr);
+                         const uint8_t* masks2 = nullptr, void* gbuf = nullptr, const void* gtop = nullptr,
+                         int fold = 1);
 int block_stack_fwd_mfma(const void* x0, void* ys, long y_stride, uint8_t* masks, long mask_stride, const void* w,
                          long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C, int L,
                          hipStream_t s, int slots = 0);
@@ -983,7 +984,7 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
                                  L.wstride, cfg->h, L.sep_bwd ? 0.f : 2.f * cfg->gamma, N, H, W, C, cfg->L, ro0, slabs,
                                  sst, grp, L.grp_stride, (unsigned*)(b + L.stack_done), &lfold, s,
                                  L.rk2 ? b + L.xmids : nullptr, L.rk2 ? m1 + (size_t)cfg->L * L.mask_bytes : nullptr,
-                                 L.rk2 ? b + L.dxg : nullptr, grow ? b + L.grow : nullptr));
+                                 L.rk2 ? b + L.dxg : nullptr, grow ? b + L.grow : nullptr, fold_on ? 1 : 0));
     ASR_TRY(timed_event(cfg, 3, s));
     for (int l = std::min(lfold, cfg->L) - 1; l >= 0; --l)  // blocks below lfold: pass 1 after the launch
       ASR_TRY(reduce_slabs_to_groups(slabs + (long)l * sst, grid, ES, grp + (long)l * L.grp_stride, s));

@@ -1864,18 +1864,21 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
           if constexpr (G2) dzw[sl] = lds_rd128(dzt + co);
           if constexpr (RO) xw[sl] = lds_rd128(xt + co);
         };
+        // reads of all BR tile rows on a compile-time schedule (rows past the image
+        // read tile rows that exist and are not used), each retired before the row
+        // guard: no branch between a read and its wait (see k_bwd3_stack)
         if constexpr (NR > 0) issue(0, 0);
         static_for<0, BR>([&](auto rc) {
           constexpr int r = decltype(rc)::value, sl = r & 1;
-          if (r < rows) {
-            if constexpr (NR > 0) {
-              if (r + 1 < rows) {
-                issue(r + 1, sl ^ 1);
-                lgkm_wait<NR>();  // row r's reads (row r+1's still in flight)
-              } else {
-                lgkm_wait<0>();
-              }
+          if constexpr (NR > 0) {
+            if constexpr (r + 1 < BR) {
+              issue(r + 1, sl ^ 1);
+              lgkm_wait<NR>();  // row r's reads (row r+1's still in flight)
+            } else {
+              lgkm_wait<0>();
             }
+          }
+          if (r < rows) {
             float z[8];
             regroup(acc[r][0], acc[r][1], z);
             u32x4 ow;
@@ -2372,18 +2375,22 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
           if constexpr (G2) dzw[sl] = lds_rd128(dzt + co);
           if constexpr (RO) xw[sl] = lds_rd128(xt + co);
         };
+        // the reads run on a compile-time schedule, each retired before the row guard,
+        // so no branch sits between a read and the wait that retires it: with the
+        // reads inside the guard hipcc merged a read's register at the join with a copy
+        // placed before that wait (stale dy rows under LDS contention, tools/asm_lds_audit.py)
         if constexpr (NR > 0) issue(0, 0);
         static_for<0, BR>([&](auto rc) {
           constexpr int r = decltype(rc)::value, sl = r & 1;
-          if (r < rows) {
-            if constexpr (NR > 0) {
-              if (r + 1 < rows) {
-                issue(r + 1, sl ^ 1);
-                lgkm_wait<NR>();
-              } else {
-                lgkm_wait<0>();
-              }
+          if constexpr (NR > 0) {
+            if constexpr (r + 1 < BR) {
+              issue(r + 1, sl ^ 1);
+              lgkm_wait<NR>();
+            } else {
+              lgkm_wait<0>();
             }
+          }
+          if (r < rows) {
             float z[8];
             regroup(acc[r][0], acc[r][1], z);
             u32x4 ow;
@@ -3237,14 +3244,16 @@ int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride
                          long mask_stride, const void* w, long w_stride, float h, float two_gamma, int N, int H, int W,
                          int C, int L, int ro0, float* slabs, long slab_stride, float* grp, long grp_stride,
                          unsigned* done, int* lfold_out, hipStream_t s, const void* xm, const uint8_t* masks2,
-                         void* gbuf, const void* gtop) {
+                         void* gbuf, const void* gtop, int fold) {
   if (!block_stack_bwd_supported(N, H, W, C) || L < 1)
     return fail(ASR_E_UNSUPPORTED, "stack backward: needs C=64, W=32, >= 4 row bands per image (C=%d W=%d H=%d)", C, W, H);
   const int grid = block_stack_bwd_grid(N);
   if (slab_stride < (long)grid * (9L * C * C + C)) return fail(ASR_E_ARG, "stack backward: slab_stride too small");
   // in-kernel pass 1 needs <= 512 group-row chunks per workgroup (one per wgrad thread)
   const long fchunks = (long)((grid + 31) / 32) * ((9L * C * C + C) / 4);
-  const int lfold = (fchunks + grid - 1) / grid <= 512 ? 2 : L;
+  // fold = 0: no in-launch pass 1, so no workgroup ever waits for another (no
+  // co-residency needed: e.g. several processes sharing one device)
+  const int lfold = fold && (fchunks + grid - 1) / grid <= 512 ? 2 : L;
   if (lfold_out) *lfold_out = lfold;
   ASR_TRY(stack_status_check());
   unsigned* tmo = stack_status_device();

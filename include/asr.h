@@ -254,7 +254,10 @@ typedef struct asr_net_config {
 /* asr_net_config.variant bits (all 0 in production) */
 #define ASR_VARIANT_NO_FOLD 1      /* reduce every block's weight-gradient slabs in
                                       its own launch instead of folding the pass
-                                      into the next block's backward kernel      */
+                                      into the next block's backward kernel; the
+                                      C=64 stacked backward then has no in-launch
+                                      hand-off, so it needs no co-resident grid
+                                      (use it when processes share one device)   */
 #define ASR_VARIANT_STEM_FWD_VALU 2 /* bf16 stem forward on the fp32 VALU kernel  */
 #define ASR_VARIANT_STEM_WGRAD_VALU 4 /* stem weight gradient on the fp32 VALU
                                         kernel from dx1 and x1 (relu' not fused

@@ -75,6 +75,10 @@ def main():
     sl = slice(rank * B, (rank + 1) * B)
     ex = rt.NetExecutor(B, 32, 32, 3, C, L, 10, H, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
                         dtype=DTYPE, input_u8=True, device=dev)
+    # both ranks share the box's one device: the stacked backward's in-launch slab
+    # hand-off needs its whole grid resident, which two concurrent launches cannot
+    # guarantee, so the ranks reduce the slabs after the launch (ASR_VARIANT_NO_FOLD)
+    ex.variant = rt.ASR_VARIANT_NO_FOLD
     loss, grads = ex.forward_backward(params, torch.from_numpy(imgs[sl]).to(dev), torch.from_numpy(onehot[sl]).to(dev))
     p_before = params.cpu().numpy()
     distributed.allreduce_grads(grads)

@@ -115,6 +115,27 @@ extern "C" __global__ void k(unsigned* out, unsigned a) {
         assert (bad > 0) == want_bad, (wait, bad)
 
 
+def test_asm_lds_audit_follows_branches():
+    """The round-3 stacked-backward bug: an asm LDS read issued before a branch,
+    its register copied after the join, its wait later.  The audit carries the
+    pending read across the branch and the label, and flags the copy."""
+    asm = """_Z1kv:                                   ; @_Z1kv
+\t;;#ASMSTART
+\tds_read_b128 v[114:117], v114
+\t;;#ASMEND
+\ts_cbranch_scc1 .LBB0_2
+\ts_nop 0
+.LBB0_2:
+\tv_mov_b64_e32 v[110:111], v[114:115]
+\ts_waitcnt lgkmcnt(0)
+\ts_endpgm
+"""
+    bad, findings = asm_lds_audit.audit(asm)
+    assert bad >= 1, findings
+    assert asm_lds_audit.audit(asm.replace("\ts_nop 0\n", "\ts_waitcnt lgkmcnt(0)\n").replace(
+        "\ts_cbranch_scc1 .LBB0_2\n", "\ts_waitcnt lgkmcnt(0)\n\ts_cbranch_scc1 .LBB0_2\n"))[0] == 0
+
+
 def test_asm_vmem_audit_clean(asm_files):
     n_loads = 0
     for f in asm_files:
