@@ -86,6 +86,8 @@ def parse():
     ap.add_argument("--share-device", action="store_true",
                     help="test only: every rank on cuda:0 with its own RCCL host id (multi-rank rehearsal on one GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-random-leg", action="store_true",
+                    help="skip the random-operand leg (profiling passes of the network's own kernels only)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this process may run on")
     ap.add_argument("--lib", default=None, help="development A/B only: load this libasr build instead of the in-tree one")
     return ap.parse_args()
@@ -408,6 +410,33 @@ def traffic_record(config):
     return d.get("hbm_bytes_per_block"), f"profiles/traffic_{config}.json ({d.get('round', '?')})"
 
 
+def co_bound(config, flops, bytes_blk, t_blk, train, dtype_name):
+    """The MFMA side of the co-bound, at the clock the chip holds: the held
+    clock of the block kernels comes from the committed PMC pass over the same
+    bench command (profiles/clock_<config>.json, tools/clock.py:
+    GRBM_GUI_ACTIVE / 8 XCDs / kernel time, time-weighted over the forward and
+    backward kernels).  mfma_frac_held_clock = achieved FLOP/s / (1024 SIMDs x
+    FLOP/clk/SIMD x that clock); hbm_frac_at_mfma_ceiling = the HBM fraction
+    these algorithmic bytes would reach if the MFMA pipes were busy 100 % of
+    that time (the ceiling of `frac` for this FLOP count).  None without the
+    file or for an fp32 line."""
+    path = os.path.join(HERE, "profiles", f"clock_{config}.json")
+    if dtype_name != "bfloat16" or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    ghz = d.get("clock_ghz_train" if train else "clock_ghz_fwd")
+    if not ghz:
+        return None
+    flop_per_clk = 1024 * 1024  # 1024 SIMDs x 1024 bf16 FLOP/clk (v_mfma_f32_16x16x32_bf16: 16384 FLOP / 16 clk)
+    peak = flop_per_clk * ghz * 1e9
+    t_mfma = flops / peak
+    return {"mfma_frac_held_clock": round(flops / t_blk / peak, 4), "held_clock_ghz": round(ghz, 3),
+            "mfma_peak_held_clock_tflops": round(peak / 1e12, 1),
+            "hbm_frac_at_mfma_ceiling": round(bytes_blk / t_mfma / 1e9 / HBM_PEAK_GBS, 4),
+            "clock_source": f"profiles/clock_{config}.json ({d.get('round', '?')})"}
+
+
 def algorithmic_bytes(C, L, N, esz, integrator, deep):
     """Per-step algorithmic bytes of the blocks' forward and backward (SURVEY
     §8d; see stack_roofline / block_roofline for the per-config units)."""
@@ -470,10 +499,13 @@ def main():
     h = 8.0 / L  # final_time 8 (experiments_antisymmetric_resnet_v6.ipynb cell 1)
     ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, h, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
                         dtype=dtype_name, input_u8=True, device=dev, integrator=integrator, inference=not train)
-    # ranks sharing one device (test only) cannot keep both stacked backward grids resident:
-    # no in-launch slab hand-off then (ASR_VARIANT_NO_FOLD), so no workgroup waits for another
-    base_variant = rt.ASR_VARIANT_NO_FOLD if args.share_device else 0
+    # ranks sharing one device (test only) cannot keep both stacked backward grids resident: their
+    # in-launch slab hand-offs degrade (bounded waits, the flagged blocks reduced after the launch;
+    # counted in degraded_handoffs) -- slower, the same gradients
+    base_variant = 0
     ex.variant = base_variant
+    if train:
+        rt.stack_status(reset=True)
     params = torch.from_numpy(bench_params(C, L)).to(dev)
     distributed.broadcast_params(params, 0)
     m = torch.zeros_like(params)
@@ -522,7 +554,7 @@ def main():
     final_loss = float(out.item()) if train else None
     live = -distributed.max_over_ranks(-live_fraction()) if train else None  # min over ranks
     if train:
-        ex.check_status()  # blocking: the stacked backward's slab hand-off never timed out
+        ex.check_status()  # blocking: every launch completed
 
     # the timed step's own block kernels: events inside instrumented steps (all ranks take part)
     ex.variant = rt.ASR_VARIANT_TIMED | base_variant
@@ -531,8 +563,10 @@ def main():
         step()
         kts.append(ex.kernel_times())
     ex.variant = base_variant
+    degraded = None
     if train:
         ex.check_status()
+        degraded = rt.stack_status(reset=True)  # hand-offs of the timed + instrumented steps that degraded
 
     if rank == 0:
         def avg(key):
@@ -584,15 +618,21 @@ def main():
             if t_red is not None:
                 roof["kernels"]["bwd_reduce"] = {"avg_us": round(t_red * 1e6, 2)}
             # secondary: the same kernels through the layer/stack ABI on random operands
-            if stacked or deep:
+            if args.no_random_leg:
+                rb = None
+            elif stacked or deep:
                 rb = stack_roofline(rt, N, L, max(2, args.block_reps // 10), h, C, rk2=integrator == "rk2")
             else:
                 rb = block_roofline(rt, lib, C, N, dtype_name, args.block_reps, h, integrator)
-            roof["random_operand_leg"] = {
-                "avg_us": round(rb["t"] * 1e6, 2), "algorithmic_bytes": rb["bytes"],
-                "frac": round(rb["bytes"] / rb["t"] / 1e9 / HBM_PEAK_GBS, 4),
-                "fwd_us": round(rb["t_fwd"] * 1e6, 2), "bwd_with_reduction_us": round(rb["t_bwd"] * 1e6, 2),
-                "operands": "random (x, dy ~ N(0,1) in bf16, theta ~ N(0, 0.05^2)) through the stack / layer ABI"}
+            if rb is not None:
+                roof["random_operand_leg"] = {
+                    "avg_us": round(rb["t"] * 1e6, 2), "algorithmic_bytes": rb["bytes"],
+                    "frac": round(rb["bytes"] / rb["t"] / 1e9 / HBM_PEAK_GBS, 4),
+                    "fwd_us": round(rb["t_fwd"] * 1e6, 2), "bwd_with_reduction_us": round(rb["t_bwd"] * 1e6, 2),
+                    "operands": "random (x, dy ~ N(0,1) in bf16, theta ~ N(0, 0.05^2)) through the stack / layer ABI"}
+        co = co_bound(args.config, flops, bytes_blk, t_blk, train, dtype_name)
+        if co:
+            roof.update(co)
         cpu = None
         if world == 1 and not args.no_cpu_baseline and integrator == "euler":
             threads = args.cpu_threads or host_threads()
@@ -615,7 +655,8 @@ def main():
                        "collective": "asr_dist_allreduce_sum (RCCL)" if world > 1 and train else None,
                        "initial_loss": None if initial_loss is None else round(initial_loss, 4),
                        "final_loss": None if final_loss is None else round(final_loss, 4),
-                       "live_gradient_fraction": None if live is None else round(live, 4)},
+                       "live_gradient_fraction": None if live is None else round(live, 4),
+                       "degraded_handoffs": degraded},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -29,7 +29,7 @@ ASR_BF16 = 1
 ASR_PARAM_3BY3 = 0
 ASR_PARAM_GENERAL = 1
 ASR_PARAM_REGULAR = 2
-ABI_VERSION = 5
+ABI_VERSION = 6
 ASR_MODE_EULER = 0
 ASR_MODE_CONV = 1
 ASR_INTEGRATOR_EULER = 0

@@ -53,6 +53,9 @@ int block_stack_fwd_rk2_mfma(const void* x0, void* ys, void* xm, long y_stride, 
                              float h, int N, int H, int W, int C, int L, hipStream_t s);
 int block_stack_bwd_grid(int N);
 int theta_dst_tile_major(const int32_t* in, long n, int C, int32_t* out, hipStream_t s);
+int stack_done_words(int L);
+int stack_bwd_reduce_rest(const float* slabs, long slab_stride, int grid, long ES, float* grp, long grp_stride, int L,
+                          int lfold, const unsigned* done, hipStream_t s);
 int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride, const uint8_t* masks,
                          long mask_stride, const void* w, long w_stride, float h, float two_gamma, int N, int H, int W,
                          int C, int L, int ro0, float* slabs, long slab_stride, float* grp, long grp_stride,
@@ -410,7 +413,7 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.deep_slabs = take(L.deep && tr ? deep16_slab_bytes(c->N, c->L) : 0);
   L.theta_dst_tm = take(L.stack_bwd ? (size_t)L.ntheta * 2 * 4 : 0);
   L.stack_slabs = take(L.stack_bwd ? (size_t)c->L * L.stack_grid * (L.E + C) * 4 : 0);
-  L.stack_done = take(L.stack_bwd ? (size_t)(c->L + 4) * 4 : 0);
+  L.stack_done = take(L.stack_bwd ? (size_t)stack_done_words(c->L) * 4 : 0);
   L.grow = take(L.stack_bwd && !L.rk2 ? (size_t)c->N * C * 2 : 0);
   L.probs = take((size_t)c->N * K * 4);
   L.loss_per = take(tr ? (size_t)c->N * 4 : 0);
@@ -423,20 +426,35 @@ static NetLayout net_layout(const asr_net_config* c) {
 // ASR_VARIANT_TIMED: HIP events around the block launches of the last timed
 // asr_net_forward / asr_net_forward_backward (asr_net_kernel_times): 0-1 the
 // blocks' forward, 2-3 the stacked backward kernel, 3-4 its post-launch slab
-// reductions and the projection onto theta.  Measurement only.
-static hipEvent_t g_tev[5];
-static bool g_tev_made = false;
-static unsigned g_tev_rec = 0;  // bit i: event i recorded by the last timed call
+// reductions and the projection onto theta.  Measurement only.  The events are
+// kept per device (created on that device at its first timed call); on one
+// device, timed calls from several host threads at once overwrite each
+// other's times (one timing thread per device).
+constexpr int kMaxTimedDevices = 64;
+struct TimedEvents {
+  hipEvent_t ev[5];
+  bool made;
+  unsigned rec;  // bit i: event i recorded by the last timed call on this device
+};
+static TimedEvents g_tev[kMaxTimedDevices];
+
+static TimedEvents* timed_events_here() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxTimedDevices) return nullptr;
+  return &g_tev[dev];
+}
 
 static int timed_event(const asr_net_config* c, int i, hipStream_t s) {
   if (!(c->variant & ASR_VARIANT_TIMED)) return ASR_OK;
-  if (!g_tev_made) {
-    for (auto& e : g_tev) ASR_TRY(hip_check(hipEventCreate(&e), "hipEventCreate"));
-    g_tev_made = true;
+  TimedEvents* t = timed_events_here();
+  if (!t) return fail(ASR_E_HIP, "ASR_VARIANT_TIMED: no current device (or device id >= %d)", kMaxTimedDevices);
+  if (!t->made) {
+    for (auto& e : t->ev) ASR_TRY(hip_check(hipEventCreate(&e), "hipEventCreate"));
+    t->made = true;
   }
-  if (i == 0) g_tev_rec = 0;
-  ASR_TRY(hip_check(hipEventRecord(g_tev[i], s), "hipEventRecord"));
-  g_tev_rec |= 1u << i;
+  if (i == 0) t->rec = 0;
+  ASR_TRY(hip_check(hipEventRecord(t->ev[i], s), "hipEventRecord"));
+  t->rec |= 1u << i;
   return ASR_OK;
 }
 
@@ -456,13 +474,13 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
   const int C = c->C, N = c->N, H = c->H, W = c->W;
   const bool bf = c->dtype == ASR_BF16;
   const float inv_std = c->use_norm ? 1.f / c->divide_by_stddev : 1.f;
+  if (training && L.inference) return fail(ASR_E_ARG, "an ASR_VARIANT_INFERENCE workspace has no training buffers");
   // 1. materialise W for all L blocks (one launch)
   ASR_TRY(asr_theta_to_w(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src), c->gamma,
                          ws + L.wbuf, L.wstride, c->dtype, s));
   if (training && L.sep_bwd)
     ASR_TRY(asr_theta_to_w(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src_bwd), 0.f,
                            ws + L.wbuf_bwd, L.wstride, c->dtype, s));
-  if (training && L.inference) return fail(ASR_E_ARG, "an ASR_VARIANT_INFERENCE workspace has no training buffers");
   unsigned char* acts = ws + L.acts;
   auto act = [&](int i) -> unsigned char* {
     const int slot = training ? i : (i & 1);
@@ -631,7 +649,7 @@ static StackWs stack_ws_layout(int N, int H, int W, int C, int L, int dtype, boo
     w.grp = off;
     off += align_up((size_t)L * reduce_groups(w.grid) * ES * 4, 256);
     w.done = off;
-    off += align_up((size_t)(L + 4) * 4, 256);
+    off += align_up((size_t)stack_done_words(L) * 4, 256);
     w.tdst = off;
     off += align_up((size_t)2 * 9 * C * C * 4, 256);
     if (rk2) {  // the gradient reaching x_mid between a block's two stages
@@ -698,8 +716,7 @@ int asr_block_stack_backward(const void* dyL, const void* xs, long x_stride, con
     ASR_TRY(hip_check(hipMemcpyAsync(dx0, base + ((L & 1) ? Lw.db : Lw.da), act, hipMemcpyDeviceToDevice, s),
                       "hipMemcpyAsync"));
     if (dparams) {
-      for (int l = std::min(lfold, L) - 1; l >= 0; --l)
-        ASR_TRY(reduce_slabs_to_groups(slabs + (long)l * sst, Lw.grid, ES, grp + (long)l * gst, s));
+      ASR_TRY(stack_bwd_reduce_rest(slabs, sst, Lw.grid, ES, grp, gst, L, lfold, (const unsigned*)(base + Lw.done), s));
       int32_t* tm = (int32_t*)(base + Lw.tdst);
       ASR_TRY(theta_dst_tile_major(theta_dst, 2 * n_theta, C, tm, s));
       ASR_TRY(project_layers(grp, gst, reduce_groups(Lw.grid), E, C, tm, n_theta, L, dparams, n_theta + C, s));
@@ -765,8 +782,7 @@ int asr_rk2_stack_backward(const void* dyL, const void* xs, const void* xmids, l
   ASR_TRY(hip_check(hipMemcpyAsync(dx0, base + ((L & 1) ? Lw.db : Lw.da), act, hipMemcpyDeviceToDevice, s),
                     "hipMemcpyAsync"));
   if (dparams) {
-    for (int l = std::min(lfold, L) - 1; l >= 0; --l)
-      ASR_TRY(reduce_slabs_to_groups(slabs + (long)l * sst, Lw.grid, ES, grp + (long)l * gst, s));
+    ASR_TRY(stack_bwd_reduce_rest(slabs, sst, Lw.grid, ES, grp, gst, L, lfold, (const unsigned*)(base + Lw.done), s));
     int32_t* tm = (int32_t*)(base + Lw.tdst);
     ASR_TRY(theta_dst_tile_major(theta_dst, 2 * n_theta, C, tm, s));
     ASR_TRY(project_layers(grp, gst, reduce_groups(Lw.grid), E, C, tm, n_theta, L, dparams, n_theta + C, s));
@@ -898,21 +914,22 @@ int asr_net_check_status(const asr_net_config* cfg, const void* ws, size_t ws_by
   ASR_TRY(net_check(cfg));
   const NetLayout L = net_layout(cfg);
   if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_net_check_status: workspace too small");
-  if (!L.stack_bwd) return ASR_OK;
   ASR_TRY(hip_check(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize"));
-  return stack_status_check();  // the process-wide sticky hand-off status
+  return hip_check(hipGetLastError(), "asr_net_check_status");
 }
 
 int asr_net_kernel_times(float* us) {
   if (!us) return fail(ASR_E_ARG, "asr_net_kernel_times: null output");
-  if (!(g_tev_rec & 3u)) return fail(ASR_E_ARG, "asr_net_kernel_times: no ASR_VARIANT_TIMED call recorded");
+  const TimedEvents* t = timed_events_here();
+  if (!t || !t->made || !(t->rec & 3u))
+    return fail(ASR_E_ARG, "asr_net_kernel_times: no ASR_VARIANT_TIMED call recorded on the current device");
   for (int i = 0; i < 3; ++i) us[i] = -1.f;
   for (int i = 0; i < 3; ++i) {
     const int a = i == 0 ? 0 : i + 1, e = a + 1;
-    if ((g_tev_rec >> a & 1u) && (g_tev_rec >> e & 1u)) {
-      ASR_TRY(hip_check(hipEventSynchronize(g_tev[e]), "hipEventSynchronize"));
+    if ((t->rec >> a & 1u) && (t->rec >> e & 1u)) {
+      ASR_TRY(hip_check(hipEventSynchronize(t->ev[e]), "hipEventSynchronize"));
       float ms = 0.f;
-      ASR_TRY(hip_check(hipEventElapsedTime(&ms, g_tev[a], g_tev[e]), "hipEventElapsedTime"));
+      ASR_TRY(hip_check(hipEventElapsedTime(&ms, t->ev[a], t->ev[e]), "hipEventElapsedTime"));
       us[i] = ms * 1e3f;
     }
   }
@@ -926,12 +943,15 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   const NetLayout L = net_layout(cfg);
   if (!params || !images || !targets || !grads || !loss) return fail(ASR_E_ARG, "asr_net_forward_backward: null");
   if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_net_forward_backward: workspace too small");
+  // before any launch: an inference layout has no backward buffers (its maps for the
+  // transposed operator and the training activations are absent)
+  if (L.inference)
+    return fail(ASR_E_ARG, "asr_net_forward_backward: an ASR_VARIANT_INFERENCE workspace has no training buffers");
   hipStream_t s = (hipStream_t)stream;
   unsigned char* b = (unsigned char*)ws;
   const int C = cfg->C, N = cfg->N, H = cfg->H, W = cfg->W, K = cfg->num_classes;
   const bool bf = cfg->dtype == ASR_BF16;
   const bool stacked = L.stack_bwd && !(cfg->variant & ASR_VARIANT_PER_BLOCK_BWD);
-  if (stacked) ASR_TRY(stack_status_check());  // a previous stacked backward timed out: refuse (sticky)
   ASR_TRY(net_forward_impl(cfg, L, params, images, true, b, s));
   auto act = [&](int i) { return b + L.acts + (size_t)i * L.P * L.act_bytes; };
   // head: probabilities, per-image loss, dlogits, dL/dx_L
@@ -986,8 +1006,10 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
                                  L.rk2 ? b + L.xmids : nullptr, L.rk2 ? m1 + (size_t)cfg->L * L.mask_bytes : nullptr,
                                  L.rk2 ? b + L.dxg : nullptr, grow ? b + L.grow : nullptr, fold_on ? 1 : 0));
     ASR_TRY(timed_event(cfg, 3, s));
-    for (int l = std::min(lfold, cfg->L) - 1; l >= 0; --l)  // blocks below lfold: pass 1 after the launch
-      ASR_TRY(reduce_slabs_to_groups(slabs + (long)l * sst, grid, ES, grp + (long)l * L.grp_stride, s));
+    // pass 1 of the blocks below lfold, and of any block whose in-launch fold was
+    // flagged (a workgroup's wait ran out), before the projection reads them
+    ASR_TRY(stack_bwd_reduce_rest(slabs, sst, grid, ES, grp, L.grp_stride, cfg->L, lfold,
+                                  (const unsigned*)(b + L.stack_done), s));
     if (cfg->L & 1) std::swap(dcur, dnext);
     dz1_fused = ro0;
     ASR_TRY(project_layers(grp, L.grp_stride, reduce_groups(grid), L.E, C, (const int32_t*)(b + L.theta_dst_tm),

@@ -2214,25 +2214,37 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
 //     write-through publish);
 //   * pass 1 of block l's reduction (32-slab group sums, as k_bwd3's fold) is
 //     folded into this workgroup's bands of block l-2: one lane polls done[l]
-//     == gridDim.x before the first of them (bounded by kStackSpinLimit sleeps; a
-//     timeout stores 1 into the process-wide mapped status word *tmo, which the
-//     host keeps as a sticky ASR_E_DEVICE, see stack_status_check) and
-//     fences acquire at agent scope, and the band barrier orders that before
-//     every slab load.  Blocks below lfold (>= 2; L when a workgroup would
-//     own more than 512 chunks of the group rows, one per wgrad thread) are
-//     reduced after the launch.
-// The grid must be co-resident (one 768-thread workgroup per CU, grid <= CUs):
-// the host sizes it so and uses the stacked path only when the occupancy
-// query keeps at least one workgroup resident per CU.  At the switch to block l-1 the dgrad waves load its W
+//     == gridDim.x before the first of them and fences acquire at agent scope,
+//     and the band barrier orders that before every slab load.  Blocks below
+//     lfold (>= 2; L when a workgroup would own more than 512 chunks of the
+//     group rows, one per wgrad thread) are reduced after the launch.
+//   * the poll is bounded (kStackSpinLimit sleeps, ~1-2 ms): a missed hand-off
+//     costs speed, never correctness.  A workgroup whose wait runs out sets
+//     skipf[l] (its share of block l's group rows may be built from slabs not
+//     yet published), counts the event in g_stack_degraded (asr_stack_status),
+//     and stops waiting for the rest of the launch (a word in LDS): every later
+//     block it folds is flagged too.  After the launch, stack_bwd_reduce_rest
+//     recomputes the group rows of every flagged block from its slabs, which
+//     are all published by then (same stream), before the projection reads them.
+// Co-residency of the grid (one 768-thread workgroup per CU, grid <= CUs; the
+// stacked path is used only when the occupancy query keeps one resident per
+// CU) is therefore a speed matter: a grid that is not (another kernel or
+// process on the device) degrades to the post-launch reduction of the blocks
+// whose wait ran out.  At the switch to block l-1 the dgrad waves load its W
 // after their last conv of block l; block 0 applies the stem's relu' to dx
 // when ro0 (k_bwd3<..., RO>).
 // ===========================================================================
 typedef __attribute__((address_space(1))) unsigned gu32;  // global agent-scope words (never flat)
 // bound of the stacked backward's slab wait, in polls of one relaxed L2 load
-// + s_sleep 2 (0.3-0.6 s: thousands of times the skew between workgroups of
-// one launch).  A compile-time constant: a run-time bound cost the kernel a
-// spilled register (tests/test_isa.py)
-constexpr unsigned kStackSpinLimit = 1u << 21;
+// + s_sleep 2 (~1-2 ms: about one whole launch, far above the skew between
+// resident workgroups, which stay within a block of each other).  A
+// compile-time constant: a run-time bound cost the kernel a spilled register
+// (tests/test_isa.py)
+constexpr unsigned kStackSpinLimit = 1u << 13;
+// waits of k_bwd3_stack workgroups that ran out since the last reset
+// (asr_stack_status): each one means a slower launch (post-launch reduction of
+// the flagged blocks), not a wrong gradient
+__device__ unsigned g_stack_degraded = 0u;
 typedef __attribute__((address_space(1))) float gf32;
 
 // RK2 (config 5): items walk 2L stages, per block l its second stage first
@@ -2248,7 +2260,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
                                                        float two_gamma, int N, int H, int L, int ro0,
                                                        float* __restrict__ slabs, long slab_stride,
                                                        float* __restrict__ grp, long grp_stride,
-                                                       unsigned* __restrict__ done, unsigned* __restrict__ tmo,
+                                                       unsigned* __restrict__ done, unsigned* __restrict__ skipf,
                                                        int lfold, const bf16* __restrict__ xm = nullptr,
                                                        const uint8_t* __restrict__ masks2 = nullptr,
                                                        bf16* __restrict__ gbuf = nullptr,
@@ -2274,6 +2286,8 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       tab[i] = (((m >> (2 * d)) & 1u) ? 0xffffu : 0u) | (((m >> (2 * d + 1)) & 1u) ? 0xffff0000u : 0u);
     }
   }
+  unsigned* late = (unsigned*)(lds + LL::TOTAL);  // a slab wait of this workgroup ran out: stop waiting
+  if (tid == 0) *late = 0u;
   const int n0 = (int)((long)blockIdx.x * N / gridDim.x), n1 = (int)((long)(blockIdx.x + 1) * N / gridDim.x);
   // cursor index l is a STAGE: the block itself (Euler) or 2*block + (1: second RK2 stage, 0: first)
   constexpr int SPB = RK2 ? 2 : 1;
@@ -2583,16 +2597,23 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       const bool first_of_block = cur.b == 0 && cur.n == n0 && (!RK2 || (cur.l & 1));
       if (wave == 4) ASR_BTR(1, 1, it, 0);
       if (first_of_block && l + 2 < L && l + 2 >= lfold && w8 == 0 && lane == 0) {
-        // block l+2's slabs: every workgroup published them (bounded poll)
-        unsigned spins = 0;
-        while (__hip_atomic_load((gu32*)(done + l + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
-          __builtin_amdgcn_s_sleep(2);
-          if (++spins > kStackSpinLimit) {
-            // (fine-grained host memory: the store bypasses L2; the end-of-kernel release makes it host-visible)
-            __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
+        // block l+2's slabs: every workgroup published them (bounded poll); once a
+        // wait of this workgroup ran out, every later block it folds is flagged
+        // for the post-launch reduction instead (stack_bwd_reduce_rest)
+        bool ran_out = *(volatile unsigned*)late != 0u;
+        if (!ran_out) {
+          unsigned spins = 0;
+          while (__hip_atomic_load((gu32*)(done + l + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > kStackSpinLimit) {
+              ran_out = true;
+              *(volatile unsigned*)late = 1u;
+              __hip_atomic_fetch_add((gu32*)&g_stack_degraded, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
           }
         }
+        if (ran_out) __hip_atomic_store((gu32*)(skipf + l + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
       barrier_vm(0);  // this wave's x rows of item it landed (and its slab stores drained)
@@ -3199,20 +3220,22 @@ int block_stack_fwd_mfma(const void* x0, void* ys, long y_stride, uint8_t* masks
 // CU) and the bound of the slab hand-off's wait (0: the default)
 static int g_stack_grid_override = 0;
 
+// dynamic LDS of k_bwd3_stack: the v2 tiles + mask table, then its "late" word
+static size_t stack_bwd_lds() { return (size_t)blk::Bwd2Lds<64, 32, kBwdBR>::TOTAL + 16; }
+
 // k_bwd3_stack workgroups the device keeps resident per CU (both
-// instantiations; cached per device): the in-launch hand-off needs the whole
-// grid resident, so the stacked path is used only when this is >= 1
+// instantiations; cached per device): the in-launch hand-off is fast only with
+// the whole grid resident, so the stacked path is used only when this is >= 1
 static int stack_bwd_resident_per_cu() {
   static int dev_cached = -1, per = 0;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (dev != dev_cached) {
-    using L2 = blk::Bwd2Lds<64, 32, kBwdBR>;
     int a = 0, b = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, blk::k_bwd3_stack<64, 32, kBwdBR, false>, 768,
-                                                     (size_t)L2::TOTAL) != hipSuccess ||
+                                                     stack_bwd_lds()) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, blk::k_bwd3_stack<64, 32, kBwdBR, true>, 768,
-                                                     (size_t)L2::TOTAL) != hipSuccess)
+                                                     stack_bwd_lds()) != hipSuccess)
       return 0;
     per = std::min(a, b);
     dev_cached = dev;
@@ -3233,13 +3256,16 @@ int block_stack_bwd_grid(int N) {
   return std::max(1, std::min(N, std::min(cap, kMaxBlockSlabs)));
 }
 
+int stack_done_words(int L) { return 2 * L + 4; }
+
 // the backward of L Euler blocks in one launch (k_bwd3_stack).  dbuf0 holds
 // dL/dx_L on entry, or gtop (Euler) its per-image row (the head's GAP
 // gradient, bf16 [N][C]): then dbuf0 is not read.  Block 0's dx ends in dbuf[L & 1].  Block l's slabs (grid
-// of them, tile-major dW) at slabs + l*slab_stride; blocks >= 2 leave as
-// 32-slab group sums at grp + l*grp_stride, blocks 1 and 0 as slabs.  done:
-// L + 4 words (the per-block publish counters), zeroed here.  Refused while
-// the sticky hand-off status is set (a previous launch timed out).
+// of them, tile-major dW) at slabs + l*slab_stride; blocks >= lfold leave as
+// 32-slab group sums at grp + l*grp_stride (unless flagged), the rest as slabs:
+// stack_bwd_reduce_rest finishes both.  done: stack_done_words(L) words, zeroed
+// here: the per-block publish counters [0, L+4) and the per-block flags
+// [L+4, 2L+4) of folds whose wait ran out.
 int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride, const uint8_t* masks,
                          long mask_stride, const void* w, long w_stride, float h, float two_gamma, int N, int H, int W,
                          int C, int L, int ro0, float* slabs, long slab_stride, float* grp, long grp_stride,
@@ -3255,24 +3281,59 @@ int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride
   // co-residency needed: e.g. several processes sharing one device)
   const int lfold = fold && (fchunks + grid - 1) / grid <= 512 ? 2 : L;
   if (lfold_out) *lfold_out = lfold;
-  ASR_TRY(stack_status_check());
-  unsigned* tmo = stack_status_device();
-  if (!tmo) return ASR_E_HIP;
-  ASR_TRY(hip_check(hipMemsetAsync(done, 0, align_up((size_t)(L + 4) * 4, 16), s), "hipMemsetAsync"));
-  using L2 = blk::Bwd2Lds<64, 32, kBwdBR>;
+  ASR_TRY(hip_check(hipMemsetAsync(done, 0, (size_t)stack_done_words(L) * 4, s), "hipMemsetAsync"));
+  unsigned* skipf = done + L + 4;
+  const size_t lds = stack_bwd_lds();
   if (xm) {  // RK2: both stages of every block (x_mid stack at xm, stride x_stride; masks2; g scratch)
     if (!masks2 || !gbuf) return fail(ASR_E_ARG, "stack backward (RK2): masks2 and the g buffer are required");
-    hipLaunchKernelGGL((blk::k_bwd3_stack<64, 32, kBwdBR, true>), dim3(grid), dim3(768), (size_t)L2::TOTAL, s,
+    hipLaunchKernelGGL((blk::k_bwd3_stack<64, 32, kBwdBR, true>), dim3(grid), dim3(768), lds, s,
                        (bf16*)dbuf0, (bf16*)dbuf1, (const bf16*)xs, x_stride, masks, mask_stride, (const bf16*)w,
-                       w_stride, h, two_gamma, N, H, L, 0, slabs, slab_stride, grp, grp_stride, done, tmo,
+                       w_stride, h, two_gamma, N, H, L, 0, slabs, slab_stride, grp, grp_stride, done, skipf,
                        lfold, (const bf16*)xm, masks2, (bf16*)gbuf);
   } else {
-    hipLaunchKernelGGL((blk::k_bwd3_stack<64, 32, kBwdBR>), dim3(grid), dim3(768), (size_t)L2::TOTAL, s,
+    hipLaunchKernelGGL((blk::k_bwd3_stack<64, 32, kBwdBR>), dim3(grid), dim3(768), lds, s,
                        (bf16*)dbuf0, (bf16*)dbuf1, (const bf16*)xs, x_stride, masks, mask_stride, (const bf16*)w,
-                       w_stride, h, two_gamma, N, H, L, ro0, slabs, slab_stride, grp, grp_stride, done, tmo,
+                       w_stride, h, two_gamma, N, H, L, ro0, slabs, slab_stride, grp, grp_stride, done, skipf,
                        lfold, nullptr, nullptr, nullptr, (const bf16*)gtop);
   }
   ASR_LAUNCH_CHECK("k_bwd3_stack");
+  return ASR_OK;
+}
+
+// Pass 1 of the stacked backward's weight-gradient reduction left after the
+// launch: blocks below lfold always, blocks at or above it only where a fold's
+// wait ran out (flags[l] != 0: their group rows are recomputed from the slabs,
+// all published by now).  Same sums in the same order as k_reduce_slabs and
+// the in-launch fold (32-slab groups): deterministic either way.
+__global__ __launch_bounds__(256) void k_reduce_slabs_flagged(const float* __restrict__ slabs, long slab_stride, long ES,
+                                                              int P, float* __restrict__ grp, long grp_stride, int L,
+                                                              int lfold, const unsigned* __restrict__ flags) {
+  const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int g = blockIdx.y;
+  const int p0 = 32 * g, p1 = min(P, p0 + 32);
+  for (int l = 0; l < L; ++l) {
+    if (l >= lfold && flags[l] == 0u) continue;
+    if (e >= ES) continue;
+    const float* in = slabs + (long)l * slab_stride;
+    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+    int p = p0;
+    for (; p + 3 < p1; p += 4) {
+      acc0 += in[(long)p * ES + e];
+      acc1 += in[(long)(p + 1) * ES + e];
+      acc2 += in[(long)(p + 2) * ES + e];
+      acc3 += in[(long)(p + 3) * ES + e];
+    }
+    for (; p < p1; ++p) acc0 += in[(long)p * ES + e];
+    grp[(long)l * grp_stride + (long)g * ES + e] = (acc0 + acc1) + (acc2 + acc3);
+  }
+}
+
+int stack_bwd_reduce_rest(const float* slabs, long slab_stride, int grid, long ES, float* grp, long grp_stride, int L,
+                          int lfold, const unsigned* done, hipStream_t s) {
+  const int G = (grid + 31) / 32;
+  hipLaunchKernelGGL(k_reduce_slabs_flagged, dim3((unsigned)((ES + 255) / 256), G), dim3(256), 0, s, slabs,
+                     slab_stride, ES, grid, grp, grp_stride, L, lfold, done + L + 4);
+  ASR_LAUNCH_CHECK("k_reduce_slabs_flagged");
   return ASR_OK;
 }
 
@@ -3318,13 +3379,28 @@ int block_bwd_mfma(int mode, const void* dy, const void* x, const uint8_t* mask,
 }  // namespace asr
 
 // test knob: force the stacked backward's grid (a grid larger than the
-// resident capacity makes the in-launch hand-off time out); 0 restores the
-// default (one workgroup per CU)
+// resident capacity makes the in-launch hand-off run out and degrade to the
+// post-launch reduction); 0 restores the default (one workgroup per CU)
 extern "C" int asr_debug_stack_backward(int grid) {
   if (grid < 0 || grid > asr::kMaxBlockSlabs)
     return asr::fail(ASR_E_ARG, "asr_debug_stack_backward: grid must be in 0..%d", asr::kMaxBlockSlabs);
   asr::g_stack_grid_override = grid;
   return ASR_OK;
+}
+
+// host, blocking: waits of stacked-backward workgroups that ran out since the
+// last reset (each one a slower launch, never a wrong gradient); reset != 0
+// then clears the count
+extern "C" int asr_stack_status(int reset) {
+  unsigned n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(asr::blk::g_stack_degraded), sizeof(n)) != hipSuccess)
+    return asr::fail(ASR_E_HIP, "asr_stack_status: hipMemcpyFromSymbol failed");
+  if (reset) {
+    const unsigned z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(asr::blk::g_stack_degraded), &z, sizeof(z)) != hipSuccess)
+      return asr::fail(ASR_E_HIP, "asr_stack_status: hipMemcpyToSymbol failed");
+  }
+  return (int)std::min<unsigned>(n, 0x7fffffffu);
 }
 
 #if ASR_STAMP_BUILD

@@ -35,12 +35,6 @@ inline int hip_check(hipError_t e, const char* what) {
 
 int cu_count();
 
-// the stacked backward's sticky hand-off status (asr_theta.hip): the device
-// address of the process-wide mapped word (nullptr + error set on failure),
-// and ASR_OK / ASR_E_DEVICE from its host copy (non-blocking)
-unsigned* stack_status_device();
-int stack_status_check();
-
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 // ---- device helpers --------------------------------------------------------

@@ -51,42 +51,6 @@ int cu_count() {
   return cus;
 }
 
-// Process-wide status word of the stacked backward's in-launch hand-off
-// (k_bwd3_stack): pinned, mapped host memory, so that the host reads it
-// without synchronising.  A workgroup whose bounded wait for another
-// workgroup's weight-gradient slabs runs out stores 1 into it;
-// it stays set until asr_stack_status(1) clears it, and every entry point that
-// launches a stacked backward refuses to run while it is set.
-static unsigned* g_status_host = nullptr;
-static unsigned* g_status_dev = nullptr;
-
-unsigned* stack_status_device() {
-  if (!g_status_dev) {
-    void* h = nullptr;
-    if (hipHostMalloc(&h, 256, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess) {
-      fail(ASR_E_HIP, "hipHostMalloc (stack status word) failed");
-      return nullptr;
-    }
-    void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
-      fail(ASR_E_HIP, "hipHostGetDevicePointer (stack status word) failed");
-      return nullptr;
-    }
-    *(volatile unsigned*)h = 0u;
-    g_status_host = (unsigned*)h;
-    g_status_dev = (unsigned*)d;
-  }
-  return g_status_dev;
-}
-
-int stack_status_check() {
-  if (g_status_host && *(volatile unsigned*)g_status_host)
-    return fail(ASR_E_DEVICE,
-                "stacked backward: a workgroup timed out waiting for another workgroup's weight-gradient slabs "
-                "(its block gradients were incomplete); sticky until asr_stack_status(1)");
-  return ASR_OK;
-}
-
 // ---------------------------------------------------------------------------
 // host: element maps
 // ---------------------------------------------------------------------------
@@ -334,13 +298,8 @@ using namespace asr;
 extern "C" {
 
 const char* asr_last_error(void) { return g_err; }
-int asr_abi_version(void) { return 5; }
+int asr_abi_version(void) { return 6; }
 
-int asr_stack_status(int reset) {
-  const int rc = stack_status_check();
-  if (reset && g_status_host) *(volatile unsigned*)g_status_host = 0u;
-  return rc;
-}
 int asr_device_cu_count(void) { return cu_count(); }
 
 long asr_theta_count(int C, int kind, int antisymmetric) { return theta_count(C, kind, antisymmetric); }

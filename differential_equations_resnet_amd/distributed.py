@@ -28,7 +28,7 @@ import os
 __all__ = ["init_from_env", "is_initialized", "rank", "world_size", "device_backend", "broadcast_params",
            "allreduce_grads", "max_over_ranks", "barrier", "shutdown"]
 
-_state = {"backend": None, "ctrl": None}
+_state = {"backend": None, "ctrl": None, "owns_default": False}
 
 
 def _dist():
@@ -76,6 +76,7 @@ def init_from_env(backend: str | None = None, device=None):
         raise ValueError(f"unknown device collective backend {backend!r} ('rccl' or 'gloo')")
     r = int(os.environ["RANK"])
     _dist().init_process_group("gloo", rank=r, world_size=world)  # host control plane
+    _state["owns_default"] = True  # shutdown() may tear the default group down
     if backend == "rccl":
         if not on_gpu:
             raise ValueError("the rccl backend needs a GPU device")
@@ -162,11 +163,18 @@ def barrier(device_sync: bool = True):
 
 
 def shutdown():
+    """Finalise the RCCL communicator and destroy the groups this package
+    created: the default group only when init_from_env made it (a caller that
+    owns its default group keeps it; only the gloo control group goes)."""
     if is_initialized():
         _dist().barrier()
         if _state["backend"] == "rccl":
             from . import _lib
             _lib.call("asr_dist_finalize")
-        _dist().destroy_process_group()
+        if _state["owns_default"]:
+            _dist().destroy_process_group()
+        elif _state["ctrl"] is not None:
+            _dist().destroy_process_group(_state["ctrl"])
     _state["backend"] = None
     _state["ctrl"] = None
+    _state["owns_default"] = False

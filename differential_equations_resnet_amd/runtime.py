@@ -25,12 +25,16 @@ __all__ = [
 ]
 
 
-def stack_status(reset: bool = False) -> bool:
-    """Non-blocking: True when a C=64 stacked backward of this process timed
-    out waiting for another workgroup's weight-gradient slabs (sticky; every
-    later stacked backward refuses to run until reset).  reset clears it."""
-    rc = _lib.load().asr_stack_status(int(bool(reset)))
-    return rc == _lib.ASR_E_DEVICE
+def stack_status(reset: bool = False) -> int:
+    """Blocking: how many in-launch slab hand-offs of the C=64 stacked
+    backward degraded since the last reset (asr_stack_status): a workgroup's
+    bounded wait for the other workgroups' slabs ran out, so the flagged
+    blocks were reduced after the launch instead: slower, the same gradients.
+    reset clears the count after reading it."""
+    rc = int(_lib.load().asr_stack_status(int(bool(reset))))
+    if rc < 0:
+        _lib.check(rc, "asr_stack_status")
+    return rc
 
 
 def integrator_code(integrator) -> int:
@@ -402,9 +406,9 @@ class NetExecutor:
         self.cfg.variant = int(bits) | (ASR_VARIANT_INFERENCE if self.inference else 0)
 
     def check_status(self):
-        """Blocking: raises AsrError if a stacked backward of this process
-        (the C=64 in-launch slab hand-off) timed out (asr_net_check_status;
-        sticky, see stack_status)."""
+        """Blocking: synchronises the stream and raises AsrError when a launch
+        failed (asr_net_check_status).  A degraded slab hand-off is not an
+        error (it costs speed): see stack_status."""
         _lib.call("asr_net_check_status", ct.byref(self.cfg), _p(self.ws), self.ws_bytes, _stream())
 
     @staticmethod

@@ -253,13 +253,14 @@ class Training:
         return norms
 
     def _check_device_status(self):
-        """Once per epoch, after a synchronising read: the C=64 stacked
-        backward's in-launch slab hand-off never timed out (a timeout means
-        incomplete block gradients; the status is sticky, runtime.stack_status)."""
-        from .. import _lib, runtime
-        if runtime.stack_status():
-            raise _lib.AsrError("stacked backward: a workgroup timed out waiting for the weight-gradient hand-off; "
-                                "the block gradients of at least one step were incomplete")
+        """Once per epoch, after a synchronising read: launches completed, and
+        the count of degraded in-launch slab hand-offs of the C=64 stacked
+        backward (runtime.stack_status: a speed event, the gradients are
+        exact) is kept in self.degraded_handoffs."""
+        from .. import runtime
+        if self.native is not None and hasattr(self.native, "check_status"):
+            self.native.check_status()
+        self.degraded_handoffs = getattr(self, "degraded_handoffs", 0) + runtime.stack_status(reset=True)
 
     def train(self, epochs, steps_per_epoch, learning_rate_schedule, eval_dataset="train", eval_frequency=5,
               eval_steps=None, save_during_training=False, save_dir=None, save_best_only=True, save_tags=["default"],

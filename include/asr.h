@@ -256,8 +256,8 @@ typedef struct asr_net_config {
                                       its own launch instead of folding the pass
                                       into the next block's backward kernel; the
                                       C=64 stacked backward then has no in-launch
-                                      hand-off, so it needs no co-resident grid
-                                      (use it when processes share one device)   */
+                                      hand-off (a cross-check arm: without it a
+                                      missed hand-off degrades gracefully)       */
 #define ASR_VARIANT_STEM_FWD_VALU 2 /* bf16 stem forward on the fp32 VALU kernel  */
 #define ASR_VARIANT_STEM_WGRAD_VALU 4 /* stem weight gradient on the fp32 VALU
                                         kernel from dx1 and x1 (relu' not fused
@@ -293,11 +293,10 @@ int asr_net_forward(const asr_net_config* cfg, const float* params, const void* 
 int asr_net_forward_backward(const asr_net_config* cfg, const float* params, const void* images,
                              const float* targets, float* grads, float* loss, float* probs,
                              void* ws, size_t ws_bytes, asr_stream_t stream);
-/* Host, blocking (synchronises the stream): ASR_OK, or ASR_E_DEVICE when a
- * stacked backward of this process stopped waiting for another workgroup's
- * weight-gradient slabs (the bounded in-launch hand-off of the C=64 stacked
- * backward timed out: its block gradients were incomplete).  The status is
- * sticky (see asr_stack_status). */
+/* Host, blocking (synchronises the stream): ASR_OK, or ASR_E_HIP with the
+ * runtime's error when a launch of this thread failed.  (Since ABI 6 a missed
+ * in-launch hand-off of the C=64 stacked backward is not an error: it costs
+ * speed, see asr_stack_status.) */
 int asr_net_check_status(const asr_net_config* cfg, const void* ws, size_t ws_bytes, asr_stream_t stream);
 
 /* Host, blocking: device times in microseconds of the last asr_net_forward /
@@ -308,20 +307,21 @@ int asr_net_check_status(const asr_net_config* cfg, const void* ws, size_t ws_by
  * the projection onto theta; -1 for a part that call did not run. */
 int asr_net_kernel_times(float* us);
 
-/* Host, non-blocking: the process-wide status of the C=64 stacked backward's
- * in-launch slab hand-off (k_bwd3_stack).  A workgroup whose bounded wait runs
- * out sets it from the device (a pinned, mapped host word); it stays set, and
- * asr_net_forward_backward / asr_block_stack_backward / asr_rk2_stack_backward
- * return ASR_E_DEVICE without launching while it is set.  Returns ASR_OK or
- * ASR_E_DEVICE as it stands (launches still in flight may set it later:
- * synchronise first for a final answer); reset != 0 then clears it.  The grid
- * of the stacked backward is one workgroup per CU and the path is used only
- * when the occupancy query keeps one resident per CU. */
+/* Host, blocking (a device-to-host copy on the current device): the number of
+ * degraded in-launch slab hand-offs of the C=64 stacked backward (k_bwd3_stack)
+ * since the last reset, >= 0 (or a negative error code).  A workgroup whose
+ * bounded wait (~1-2 ms) for the other workgroups' weight-gradient slabs of a
+ * block runs out flags that block and stops waiting for the rest of its
+ * launch; the flagged blocks' slab reduction is then recomputed after the
+ * launch, on the same stream, before the projection: the gradients are those
+ * of the full hand-off, only slower (e.g. a grid that is not co-resident
+ * because another kernel or process shares the device).  reset != 0 clears
+ * the count after reading it. */
 int asr_stack_status(int reset);
 /* Test knob: force the stacked backward's grid (0: one workgroup per CU;
- * larger than the resident capacity makes the hand-off time out after its
- * bounded wait, 0.3-0.6 s).  Workspace sizes depend on the grid: query them
- * after setting it. */
+ * larger than the resident capacity makes hand-offs run out and degrade, see
+ * asr_stack_status).  Workspace sizes depend on the grid: query them after
+ * setting it. */
 int asr_debug_stack_backward(int grid);
 
 /* tf.train.AdamOptimizer.apply_gradients (training.py:300-301), TF1

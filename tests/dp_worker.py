@@ -12,7 +12,11 @@ CASE "small" (default): fp32, C=16, L=2, 4 images per rank (the per-block
 fp32 kernels).  CASE "c2": BASELINE C4's per-rank composition at a reduced
 depth: bf16, C=64, L=3, 192 images per rank, so every rank runs the stacked
 kernels (k_fwd3_stack / k_bwd3_stack, several images per workgroup, the
-in-launch slab fold) before the all-reduce.
+in-launch slab fold: the production variant 0) before the all-reduce.  Both
+ranks share the box's one device, so their two stacked-backward grids cannot
+both be resident: the in-launch hand-off then degrades (bounded waits, the
+flagged blocks reduced after the launch; the count is saved as `degraded`),
+which must not change the gradients.
 """
 import os
 import sys
@@ -75,10 +79,9 @@ def main():
     sl = slice(rank * B, (rank + 1) * B)
     ex = rt.NetExecutor(B, 32, 32, 3, C, L, 10, H, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
                         dtype=DTYPE, input_u8=True, device=dev)
-    # both ranks share the box's one device: the stacked backward's in-launch slab
-    # hand-off needs its whole grid resident, which two concurrent launches cannot
-    # guarantee, so the ranks reduce the slabs after the launch (ASR_VARIANT_NO_FOLD)
-    ex.variant = rt.ASR_VARIANT_NO_FOLD
+    # the production composition (variant 0, in-launch slab fold): ranks sharing one
+    # device degrade the hand-off gracefully (rt.stack_status counts it)
+    rt.stack_status(reset=True)
     loss, grads = ex.forward_backward(params, torch.from_numpy(imgs[sl]).to(dev), torch.from_numpy(onehot[sl]).to(dev))
     p_before = params.cpu().numpy()
     distributed.allreduce_grads(grads)
@@ -87,7 +90,7 @@ def main():
     rt.adam_update(params, grads, m, v, 1e-3, 0.9, 0.999, 1e-7, 1, 1.0 / world)
     distributed.barrier()
     np.savez(os.path.join(outdir, f"r{rank}.npz"), g=grads.cpu().numpy(), p0=p_before, p1=params.cpu().numpy(),
-             loss=loss.cpu().numpy(), t=distributed.max_over_ranks(1.0 + rank))
+             loss=loss.cpu().numpy(), t=distributed.max_over_ranks(1.0 + rank), degraded=rt.stack_status(reset=True))
     distributed.shutdown()
 
 

@@ -113,7 +113,7 @@ def test_network_stack_backward_equals_per_block(rt, N, L, gamma, kind, anti):
     loss, g = ex.forward_backward(params, imgs, tgt)
     loss, g = loss.clone(), g.clone()
     loss2, g2 = ex.forward_backward(params, imgs, tgt)
-    ex.check_status()  # the in-launch slab hand-off did not time out
+    ex.check_status()
     assert torch.equal(g, g2), "stack backward is not deterministic"
     ex.variant = rt.ASR_VARIANT_PER_BLOCK_BWD
     loss1, g1 = ex.forward_backward(params, imgs, tgt)
@@ -285,41 +285,62 @@ def _net_case(rt, N, C, L, seed=5):
     return dev, params, imgs, tgt
 
 
-def test_stack_handoff_timeout_is_sticky(rt):
-    """The stacked backward's bounded wait for other workgroups' slabs: a grid
-    of twice the resident capacity (asr_debug_stack_backward; one 768-thread
-    workgroup fits per CU) leaves half the workgroups queued behind the
-    waiting ones, so the wait runs out.  That must surface as an error, and
-    stay one: asr_net_check_status raises, the status word stays set, and
-    the next stacked forward_backward refuses to run until it is cleared;
-    after the reset the default grid runs clean."""
+def test_stack_handoff_degrades_gracefully(rt):
+    """The stacked backward's bounded wait for the other workgroups' slabs: a
+    grid of twice the resident capacity (asr_debug_stack_backward; one
+    768-thread workgroup fits per CU) leaves half the workgroups queued behind
+    the waiting ones, so the resident ones' waits run out.  That must cost
+    speed, never correctness: each such workgroup flags the blocks it folds
+    and stops waiting, the flagged blocks are reduced after the launch from the
+    published slabs, and asr_stack_status counts the degraded waits (no error).
+    Every block >= 2 is flagged here (the first wait runs out, then every later
+    fold of those workgroups is flagged), so the gradients equal the same grid
+    with no in-launch fold (ASR_VARIANT_NO_FOLD: the same post-launch sums)
+    bitwise, and the per-block path within 1e-5 of max|g| per block."""
     from differential_equations_resnet_amd import _lib
     lib = _lib.load()
     cus = lib.asr_device_cu_count()
-    N, C, L = min(2 * cus, 512), 64, 3
+    N, C, L = min(2 * cus, 512), 64, 5
     if N <= cus:
         pytest.skip("needs a grid larger than the CU count within 512 workgroups")
     dev, params, imgs, tgt = _net_case(rt, N, C, L)
-    assert not rt.stack_status()
+    rt.stack_status(reset=True)
     try:
         _lib.check(lib.asr_debug_stack_backward(N), "asr_debug_stack_backward")
         ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / L, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
                             dtype="bfloat16", input_u8=True, device=dev)
-        ex.forward_backward(params, imgs, tgt)
-        with pytest.raises(_lib.AsrError, match="timed out"):
-            ex.check_status()
-        assert rt.stack_status()  # sticky
-        with pytest.raises(_lib.AsrError, match="sticky"):
-            ex.forward_backward(params, imgs, tgt)
+        loss, g = ex.forward_backward(params, imgs, tgt)
+        loss, g = loss.clone(), g.clone()
+        ex.check_status()  # no error
+        degraded = rt.stack_status(reset=True)
+        assert degraded >= 1, "the over-size grid should have run out of its hand-off waits"
+        ex.variant = rt.ASR_VARIANT_NO_FOLD
+        loss0, g0 = ex.forward_backward(params, imgs, tgt)
+        ex.check_status()
+        assert rt.stack_status(reset=True) == 0  # no in-launch hand-off: nothing to degrade
+        assert torch.equal(loss, loss0)
+        assert torch.equal(g, g0), (g - g0).abs().max().item()
     finally:
         lib.asr_debug_stack_backward(0)
         rt.stack_status(reset=True)
-    assert not rt.stack_status()
+    ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / L, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
+                        dtype="bfloat16", input_u8=True, device=dev, variant=rt.ASR_VARIANT_PER_BLOCK_BWD)
+    loss1, g1 = ex.forward_backward(params, imgs, tgt)
+    torch.cuda.synchronize()
+    assert torch.equal(loss, loss1)
+    a, b = g.cpu().numpy(), g1.cpu().numpy()
+    n_blk = (ex.n_params - (9 * 3 * C + C) - (C * 10 + 10)) // L
+    stem = 9 * 3 * C + C
+    for l in range(L):
+        o = stem + l * n_blk
+        ga, gb = a[o:o + n_blk], b[o:o + n_blk]
+        assert np.abs(ga - gb).max() <= 1e-5 * np.abs(gb).max(), (l, np.abs(ga - gb).max(), np.abs(gb).max())
     ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / L, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
                         dtype="bfloat16", input_u8=True, device=dev)
-    loss, g = ex.forward_backward(params, imgs, tgt)
+    loss2, g2 = ex.forward_backward(params, imgs, tgt)
     ex.check_status()
-    assert np.isfinite(loss.item()) and g.abs().max().item() > 0
+    assert rt.stack_status() == 0  # the default grid is resident: no degraded wait
+    assert np.isfinite(loss2.item()) and g2.abs().max().item() > 0
 
 
 @pytest.mark.parametrize("C,L,dtype", [(64, 5, "bfloat16"), (64, 4, "bfloat16"), (16, 5, "bfloat16"),
