@@ -1,4 +1,6 @@
-// fp32 path of the 3x3 conv / Euler block: exact fp32 FMA chains on the VALU.
+// fp32 path of the 3x3 conv / Euler block: fp32 MFMA (v_mfma_f32_16x16x4_f32)
+// for the network's blocks (C in {16, 32, 64}, W = 32), exact fp32 FMA chains
+// on the VALU for every other shape.
 //
 // This is the reference-precision path (the reference computes everything in
 // fp32, layers/tfkeras_layer_Conv2DAntisymmetric3By3.py:157-171), used for the
@@ -147,6 +149,266 @@ __global__ void k_db_f32(const float* __restrict__ dz, long rows, int W, int C, 
   slabs[(long)blockIdx.x * (E + C) + E + o] = acc;
 }
 
+// ===========================================================================
+// fp32 on the matrix cores: v_mfma_f32_16x16x4_f32 (fp32 operands, fp32
+// accumulation: the reference's precision, …3By3.py:157-171) for the 3x3
+// SAME conv / Euler block with C_in = C_out = C in {16, 32, 64}, W = 32.
+//
+// Forward / dgrad (k_conv32): implicit GEMM D[o][px] = sum_kappa W^T[o][kappa]
+// X[kappa][px], kappa = (tap, i).  A workgroup (4 waves) owns a band of BR = 4
+// output rows of one image: the BR + 2 input rows (zero rows outside the
+// image, zero halo columns) are staged in LDS once, every wave keeps its
+// o-tile's A = W^T fragments in registers for the launch (9C/4 VGPRs) and
+// walks its rows (C=16: one row per wave; C=64: one o-tile per wave, all 4
+// rows).  K-step s of channel group q at a tap gives lane (lx, g) the
+// channel 16q + 4g + s, so one 16-B LDS read per lane (the pixel's channels
+// 16q+4g .. +3) feeds four MFMAs.  The accumulator lane (lx, g) holds
+// channels 4g .. 4g+3 of pixel lx: the residual / dy / dz operands and the
+// output are 16-B accesses, and the relu-mask nibbles of a pixel's 16
+// channels are merged across the 4 lane groups into one 16-bit store (every
+// bit written: no memset, no atomics).
+// Weight gradient (k_wgrad32): D[i][o] = sum_px x[px + tap][i] dz[px][o] per
+// tap, K = 4 pixels per MFMA (one fp32 per lane from LDS for each operand).
+// 12 waves: (tap row ky, o-tile, row split); each holds the 3 taps of its row
+// x C/16 i-tiles of its o-tile in accumulators over a persistent run of
+// bands, the row-split partials are summed through LDS at the end and the
+// workgroup writes one [dW | db] slab (db on MFMA: ones x dz in the ky = 1
+// waves), reduced by the same two-pass k_reduce_slabs / projection as the
+// bf16 path.
+// ===========================================================================
+template <int C>
+struct F32Band {
+  static constexpr int OT = C / 16, W = 32, TW = W + 2, BR = 4, ROWF = TW * C, TILEF = (BR + 2) * ROWF;
+  static constexpr int RSTEP = 4 / OT;  // rows between a wave's rows (forward / dgrad)
+  static constexpr int RS = 4 / OT;     // wgrad row split: 3 * OT * RS = 12 waves
+  static constexpr int DZF = BR * W * C;
+};
+
+// stage rows y0-1 .. y0+BR of image n into tile (zeros outside the image and
+// in the two halo columns), float4 per thread
+template <int C>
+__device__ __forceinline__ void f32_stage_rows(const float* __restrict__ src, float* tile, int n, int y0, int H,
+                                               int tid, int nthreads) {
+  using G = F32Band<C>;
+  constexpr int C4 = C / 4, NCH = (G::BR + 2) * G::TW * C4;
+  for (int i = tid; i < NCH; i += nthreads) {
+    const int r = i / (G::TW * C4), rem = i % (G::TW * C4), col = rem / C4, c4 = rem % C4;
+    const int gy = y0 - 1 + r, gx = col - 1;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)G::W)
+      v = *(const f32x4*)(src + (((long)n * H + gy) * G::W + gx) * C + 4 * c4);
+    *(f32x4*)(tile + (r * G::TW + col) * C + 4 * c4) = v;
+  }
+}
+
+template <int C, int MODE>
+__global__ __launch_bounds__(256) void k_conv32(const float* __restrict__ xin, float* __restrict__ out,
+                                                uint8_t* __restrict__ mask, const float* __restrict__ w,
+                                                const float* __restrict__ bias, float h, float two_gamma,
+                                                const float* __restrict__ dy, const float* __restrict__ extra, int N,
+                                                int H) {
+  using G = F32Band<C>;
+  constexpr int OT = G::OT, TW = G::TW, BR = G::BR;
+  __shared__ __attribute__((aligned(16))) float tile[G::TILEF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
+  const int ot = wave % OT, rw = wave / OT;
+  const int nb = (H + BR - 1) / BR;
+  const int n = blockIdx.x / nb, y0 = (blockIdx.x % nb) * BR;
+  if (n >= N) return;
+  // A = W^T of o-tile ot (HWIO W): A[t][q][s] = W[t][16q + 4g + s][16 ot + lx]
+  float A[9][OT][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int q = 0; q < OT; ++q)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) A[t][q][s] = w[((long)t * C + 16 * q + 4 * g + s) * C + 16 * ot + lx];
+  f32x4 bz = {0.f, 0.f, 0.f, 0.f};
+  if (MODE <= F_RELU && bias) bz = *(const f32x4*)(bias + 16 * ot + 4 * g);
+  f32_stage_rows<C>(xin, tile, n, y0, H, tid, 256);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < OT; ++k) {
+    const int r = rw + k * G::RSTEP;
+    if (y0 + r >= H) break;  // (wave-uniform)
+    f32x4 acc[2] = {bz, bz};
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int q = 0; q < OT; ++q) {
+          const f32x4 bv = *(const f32x4*)(tile + ((r + t / 3) * TW + 16 * pt + lx + t % 3) * C + 16 * q + 4 * g);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc[pt] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[t][q][s], bv[s], acc[pt], 0, 0, 0);
+        }
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt) {
+      const int px = 16 * pt + lx;
+      const long pix = ((long)n * H + y0 + r) * G::W + px;
+      const long oi = pix * C + 16 * ot + 4 * g;  // this lane's 4 channels
+      const f32x4 ctr = *(const f32x4*)(tile + ((r + 1) * TW + px + 1) * C + 16 * ot + 4 * g);  // x or dz at the pixel
+      f32x4 v;
+      if constexpr (MODE == F_EULER) {
+        const f32x4 res = extra ? *(const f32x4*)(extra + oi) : ctr;
+        unsigned nib = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float z = acc[pt][j];
+          nib |= (z > 0.f ? 1u : 0u) << j;
+          v[j] = res[j] + h * fmaxf(z, 0.f);
+        }
+        if (mask) {  // the pixel's 16 channels of this o-tile: 4 nibbles, one 16-bit store
+          unsigned m = nib << (4 * g);
+          m |= (unsigned)__shfl_xor((int)m, 16, 64);
+          m |= (unsigned)__shfl_xor((int)m, 32, 64);
+          if (g == 0) *(uint16_t*)(mask + (pix * C + 16 * ot) / 8) = (uint16_t)m;
+        }
+      } else if constexpr (MODE == F_CONV) {
+        v = acc[pt];
+      } else {  // B_EULER / B_CONV: the tile holds dz; dx = [dy] - A dz + 2 gamma dz [+ extra]
+        f32x4 d0 = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (MODE == B_EULER) d0 = *(const f32x4*)(dy + oi);
+        if (extra) d0 += *(const f32x4*)(extra + oi);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = d0[j] - acc[pt][j] + two_gamma * ctr[j];
+      }
+      *(f32x4*)(out + oi) = v;
+    }
+  }
+}
+
+template <int C>
+__global__ __launch_bounds__(768) void k_wgrad32(const float* __restrict__ x, const float* __restrict__ dz, int N,
+                                                 int H, float* __restrict__ slabs) {
+  using G = F32Band<C>;
+  constexpr int OT = G::OT, TW = G::TW, BR = G::BR, RS = G::RS, E = 9 * C * C;
+  extern __shared__ __attribute__((aligned(16))) float lds32[];
+  float* xt = lds32;               // [BR+2][TW][C]
+  float* dzt = lds32 + G::TILEF;   // [BR][W][C]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
+  const int ky = wave / (OT * RS), ot = (wave / RS) % OT, rs = wave % RS;
+  const int nb = (H + BR - 1) / BR;
+  const long items = (long)N * nb;
+  const long i0 = (long)blockIdx.x * items / gridDim.x, i1 = (long)(blockIdx.x + 1) * items / gridDim.x;
+  f32x4 acc[3][OT], accb = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+    for (int it = 0; it < OT; ++it) acc[kx][it] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (long item = i0; item < i1; ++item) {
+    const int n = (int)(item / nb), y0 = (int)(item % nb) * BR;
+    const int rows = min(BR, H - y0);
+    __syncthreads();  // the previous item's tiles consumed
+    f32_stage_rows<C>(x, xt, n, y0, H, tid, 768);
+    for (int i = tid; i < BR * G::W * C / 4; i += 768) {
+      const int r = i / (G::W * C / 4);
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (r < rows) v = *(const f32x4*)(dz + ((long)n * H + y0) * G::W * C + 4 * i);
+      *(f32x4*)(dzt + 4 * i) = v;
+    }
+    __syncthreads();
+    for (int r = rs; r < rows; r += RS) {
+#pragma unroll
+      for (int s = 0; s < G::W / 4; ++s) {
+        const int p = 4 * s + g;  // this lane's pixel (k index) of the step
+        const float bv = dzt[(r * G::W + p) * C + 16 * ot + lx];
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+          for (int it = 0; it < OT; ++it) {
+            const float av = xt[((r + ky) * TW + p + kx) * C + 16 * it + lx];
+            acc[kx][it] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[kx][it], 0, 0, 0);
+          }
+        if (ky == 1) accb = __builtin_amdgcn_mfma_f32_16x16x4f32(1.f, bv, accb, 0, 0, 0);
+      }
+    }
+  }
+  // sum the RS row-split partials through LDS (fixed order), one slab per workgroup
+  constexpr int PW = (3 * OT + 1) * 256;  // floats per wave: its tiles, then db
+  if constexpr (RS > 1) {
+    __syncthreads();  // (the last item's tiles consumed)
+    if (rs != 0) {
+      float* mine = lds32 + wave * PW;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+        for (int it = 0; it < OT; ++it) *(f32x4*)(mine + ((kx * OT + it) * 64 + lane) * 4) = acc[kx][it];
+      *(f32x4*)(mine + (3 * OT * 64 + lane) * 4) = accb;
+    }
+    __syncthreads();
+    if (rs == 0) {
+#pragma unroll
+      for (int q = 1; q < RS; ++q) {
+        const float* th = lds32 + (wave + q) * PW;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+          for (int it = 0; it < OT; ++it) acc[kx][it] += *(const f32x4*)(th + ((kx * OT + it) * 64 + lane) * 4);
+        accb += *(const f32x4*)(th + (3 * OT * 64 + lane) * 4);
+      }
+    }
+  }
+  if (rs == 0) {
+    float* slab = slabs + (long)blockIdx.x * (E + C);
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+      for (int it = 0; it < OT; ++it)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          slab[((long)(3 * ky + kx) * C + 16 * it + 4 * g + j) * C + 16 * ot + lx] = acc[kx][it][j];
+    // db: the ky = 1 waves' ones x dz (every row of that product is the column sum)
+    if (ky == 1 && g == 0) slab[E + 16 * ot + lx] = accb[0];
+  }
+}
+
+template <int C>
+static size_t wgrad32_lds() {
+  using G = F32Band<C>;
+  const size_t stage = (size_t)(G::TILEF + G::DZF) * 4;
+  const size_t red = G::RS > 1 ? (size_t)12 * (3 * G::OT + 1) * 256 * 4 : 0;
+  return std::max(stage, red);
+}
+
+static bool conv32_supported(int W, int Ci, int Co) { return W == 32 && Ci == Co && (Ci == 16 || Ci == 32 || Ci == 64); }
+
+template <int C, int MODE>
+static int launch_conv32(const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
+                         float two_gamma, const float* dy, const float* extra, int N, int H, hipStream_t s) {
+  const long blocks = (long)N * ((H + 3) / 4);
+  if (blocks > 0x7fffffffL) return fail(ASR_E_ARG, "conv f32: problem too large");
+  hipLaunchKernelGGL((k_conv32<C, MODE>), dim3((unsigned)blocks), dim3(256), 0, s, (const float*)xin, (float*)out,
+                     mask, w, bias, h, two_gamma, dy, extra, N, H);
+  ASR_LAUNCH_CHECK("k_conv32");
+  return ASR_OK;
+}
+
+template <int MODE>
+static int conv32_dispatch(int C, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias,
+                           float h, float two_gamma, const float* dy, const float* extra, int N, int H, hipStream_t s) {
+  switch (C) {
+    case 16: return launch_conv32<16, MODE>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+    case 32: return launch_conv32<32, MODE>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+    case 64: return launch_conv32<64, MODE>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+  }
+  return fail(ASR_E_UNSUPPORTED, "conv f32 (MFMA): C=%d", C);
+}
+
+template <int C>
+static int launch_wgrad32(const float* x, const float* dz, int N, int H, float* slabs, int* nslabs, hipStream_t s) {
+  const long items = (long)N * ((H + 3) / 4);
+  int cus = cu_count();
+  if (cus <= 0) cus = 256;
+  const size_t lds = wgrad32_lds<C>();
+  const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
+  const int grid = (int)std::max<long>(1, std::min<long>({items, (long)per_cu * cus, 512L}));
+  hipLaunchKernelGGL((k_wgrad32<C>), dim3(grid), dim3(768), lds, s, x, dz, N, H, slabs);
+  ASR_LAUNCH_CHECK("k_wgrad32");
+  *nslabs = grid;
+  return ASR_OK;
+}
+
 template <typename Tin, typename Tout, int MODE>
 static int launch_conv_f32(const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
                            float two_gamma, const float* dy, const float* extra, int N, int H, int W, int Ci, int Co,
@@ -167,6 +429,14 @@ static int launch_conv_f32(const void* xin, void* out, uint8_t* mask, const floa
 int conv_f32(int fmode, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
              float two_gamma, const float* dy, int N, int H, int W, int Ci, int Co, int out_bf16, hipStream_t s,
              const float* extra) {
+  if (conv32_supported(W, Ci, Co) && fmode != F_RELU) {  // the network's blocks: fp32 MFMA
+    switch (fmode) {
+      case F_EULER: return conv32_dispatch<F_EULER>(Ci, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+      case F_CONV: return conv32_dispatch<F_CONV>(Ci, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+      case B_EULER: return conv32_dispatch<B_EULER>(Ci, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+      case B_CONV: return conv32_dispatch<B_CONV>(Ci, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+    }
+  }
   switch (fmode) {
     case F_EULER:
       return launch_conv_f32<float, float, F_EULER>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, W, Ci, Co, s);
@@ -208,6 +478,13 @@ int wgrad_f32_chunks(int N, int H) {
 
 int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, int Ci, int Co, float* slabs,
               int* nslabs, hipStream_t s) {
+  if (!x_bf16 && conv32_supported(W, Ci, Co)) {  // the network's blocks: fp32 MFMA, db included
+    switch (Ci) {
+      case 16: return launch_wgrad32<16>((const float*)x, dz, N, H, slabs, nslabs, s);
+      case 32: return launch_wgrad32<32>((const float*)x, dz, N, H, slabs, nslabs, s);
+      case 64: return launch_wgrad32<64>((const float*)x, dz, N, H, slabs, nslabs, s);
+    }
+  }
   const long R = (long)N * H;
   const int chunks = wgrad_f32_chunks(N, H);
   const int rpc = (int)((R + chunks - 1) / chunks);

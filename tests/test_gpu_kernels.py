@@ -78,7 +78,7 @@ def _oracle_W(th, C, gamma, bf):
 
 
 SHAPES_BF16 = [(2, 32, 32, 16), (2, 32, 32, 32), (2, 32, 32, 64), (1, 11, 32, 64), (3, 5, 32, 16)]
-SHAPES_F32 = [(2, 32, 32, 16), (1, 7, 13, 5), (2, 9, 32, 64), (1, 3, 3, 1)]
+SHAPES_F32 = [(2, 32, 32, 16), (1, 7, 13, 5), (2, 9, 32, 64), (1, 3, 3, 1), (2, 32, 32, 32), (3, 6, 32, 16)]
 
 
 @pytest.mark.parametrize("dtype_name,shape", [("f32", s) for s in SHAPES_F32] + [("bf16", s) for s in SHAPES_BF16])
