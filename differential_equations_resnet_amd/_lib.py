@@ -42,6 +42,7 @@ ASR_VARIANT_PER_BLOCK_BWD = 16
 ASR_VARIANT_INFERENCE = 32
 ASR_VARIANT_TIMED = 64
 ASR_VARIANT_FULL_DXL = 128
+ASR_VARIANT_FULL_SLABS = 256
 ASR_DIST_UNIQUE_ID_BYTES = 128
 
 
@@ -77,6 +78,7 @@ SIGNATURES = [
     ("asr_param_map", _I, [_I, _I, _I, _P, _P]),
     ("asr_param_is_antisymmetric", _I, [_I, _I]),
     ("asr_param_map_transpose", _I, [_I, _P, _P]),
+    ("asr_param_map_pair", _I, [_I, _P, ct.c_long, _P]),
     ("asr_wpack_elems", _L, [_I]),
     ("asr_theta_to_w", _I, [_P, _L, _I, _I, _P, _F, _P, _L, _I, _P]),
     ("asr_conv_forward", _I, [_I, _P, _P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P]),

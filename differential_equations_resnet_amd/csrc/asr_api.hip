@@ -61,7 +61,10 @@ int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride
                          int C, int L, int ro0, float* slabs, long slab_stride, float* grp, long grp_stride,
                          unsigned* done, int* lfold_out, hipStream_t s, const void* xm = nullptr,
                          const uint8_t* masks2 = nullptr, void* gbuf = nullptr, const void* gtop = nullptr,
-                         int fold = 1);
+                         int fold = 1, int pair = 0);
+long stack_slab_floats(int C, int pair);
+int theta_dst_pair(const int32_t* in, long n_theta, int C, int32_t* out, hipStream_t s);
+int theta_dst_pair_host(const int32_t* in, long n_theta, int C, int32_t* out);
 int block_stack_fwd_mfma(const void* x0, void* ys, long y_stride, uint8_t* masks, long mask_stride, const void* w,
                          long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C, int L,
                          hipStream_t s, int slots = 0);
@@ -331,8 +334,10 @@ struct NetLayout {
   size_t deep_slabs;  // its weight-gradient slabs [L][rows][E+C]
   bool inference;     // ASR_VARIANT_INFERENCE: forward-only workspace (3 activation slots, no backward buffers)
   bool stack_bwd;     // C=64 Euler bf16: all blocks' backward in one k_bwd3_stack launch
+  bool stack_pair;    // ... with pair-local slabs (antisymmetric operator: the 74 D tiles, not dW)
   int stack_grid;     // its workgroups
   size_t theta_dst_tm, stack_slabs, stack_done;  // tile-major projection map, [L][grid][E+C] slabs, counters
+  size_t theta_dst_pr;  // the pull-back from the pair-local slabs (stack_pair)
   size_t grow;        // stacked Euler backward: dL/dx_L as one bf16 row per image (the GAP gradient) [N][C]
 };
 
@@ -348,7 +353,8 @@ static int net_check(const asr_net_config* c) {
   if (c->integrator != ASR_INTEGRATOR_EULER && c->integrator != ASR_INTEGRATOR_RK2)
     return fail(ASR_E_ARG, "bad integrator %d", c->integrator);
   if (c->variant & ~(ASR_VARIANT_NO_FOLD | ASR_VARIANT_STEM_FWD_VALU | ASR_VARIANT_STEM_WGRAD_VALU | ASR_VARIANT_PER_BLOCK_FWD |
-                    ASR_VARIANT_PER_BLOCK_BWD | ASR_VARIANT_INFERENCE | ASR_VARIANT_TIMED | ASR_VARIANT_FULL_DXL))
+                    ASR_VARIANT_PER_BLOCK_BWD | ASR_VARIANT_INFERENCE | ASR_VARIANT_TIMED | ASR_VARIANT_FULL_DXL |
+                    ASR_VARIANT_FULL_SLABS))
     return fail(ASR_E_ARG, "bad variant bits 0x%x", c->variant);
   if (c->dtype == ASR_BF16 && !mfma_supported(c->C, c->W))
     return fail(ASR_E_UNSUPPORTED, "bf16 network needs C in {16,32,64} and W == 32 (C=%d W=%d)", c->C, c->W);
@@ -380,6 +386,7 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.deep = c->dtype == ASR_BF16 && !L.rk2 && deep16_supported(c->H, c->W, C);
   L.stack_bwd = tr && c->dtype == ASR_BF16 && block_stack_bwd_supported(c->N, c->H, c->W, C);
   L.stack_grid = L.stack_bwd ? block_stack_bwd_grid(c->N) : 0;
+  L.stack_pair = L.stack_bwd && !L.sep_bwd;
   size_t off = 0;
   auto take = [&](size_t bytes) {
     size_t o = off;
@@ -412,6 +419,7 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.grp = take(tr ? (size_t)c->L * L.grp_stride * 4 : 0);
   L.deep_slabs = take(L.deep && tr ? deep16_slab_bytes(c->N, c->L) : 0);
   L.theta_dst_tm = take(L.stack_bwd ? (size_t)L.ntheta * 2 * 4 : 0);
+  L.theta_dst_pr = take(L.stack_pair ? (size_t)L.ntheta * 2 * 4 : 0);
   L.stack_slabs = take(L.stack_bwd ? (size_t)c->L * L.stack_grid * (L.E + C) * 4 : 0);
   L.stack_done = take(L.stack_bwd ? (size_t)stack_done_words(c->L) * 4 : 0);
   L.grow = take(L.stack_bwd && !L.rk2 ? (size_t)c->N * C * 2 : 0);
@@ -708,18 +716,19 @@ int asr_block_stack_backward(const void* dyL, const void* xs, long x_stride, con
     ASR_TRY(hip_check(hipMemcpyAsync(base + Lw.da, dyL, act, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync"));
     float* slabs = (float*)(base + Lw.slabs);
     float* grp = (float*)(base + Lw.grp);
-    const long ES = E + C, sst = (long)Lw.grid * ES, gst = (long)reduce_groups(Lw.grid) * ES;
+    // the stack ABI's operator is antisymmetric (its dgrad is A^T = -A + 2 gamma I): pair-local slabs
+    const long ES = stack_slab_floats(C, 1), sst = (long)Lw.grid * ES, gst = (long)reduce_groups(Lw.grid) * ES;
     int lfold = L;
     ASR_TRY(block_stack_bwd_mfma(base + Lw.da, base + Lw.db, xs, x_stride, masks, mask_stride, w, w_stride, h,
                                  2.f * gamma, N, H, W, C, L, 0, slabs, sst, grp, gst, (unsigned*)(base + Lw.done),
-                                 &lfold, s));
+                                 &lfold, s, nullptr, nullptr, nullptr, nullptr, 1, 1));
     ASR_TRY(hip_check(hipMemcpyAsync(dx0, base + ((L & 1) ? Lw.db : Lw.da), act, hipMemcpyDeviceToDevice, s),
                       "hipMemcpyAsync"));
     if (dparams) {
       ASR_TRY(stack_bwd_reduce_rest(slabs, sst, Lw.grid, ES, grp, gst, L, lfold, (const unsigned*)(base + Lw.done), s));
       int32_t* tm = (int32_t*)(base + Lw.tdst);
-      ASR_TRY(theta_dst_tile_major(theta_dst, 2 * n_theta, C, tm, s));
-      ASR_TRY(project_layers(grp, gst, reduce_groups(Lw.grid), E, C, tm, n_theta, L, dparams, n_theta + C, s));
+      ASR_TRY(theta_dst_pair(theta_dst, n_theta, C, tm, s));
+      ASR_TRY(project_layers(grp, gst, reduce_groups(Lw.grid), ES - C, C, tm, n_theta, L, dparams, n_theta + C, s));
     }
     return ASR_OK;
   }
@@ -771,21 +780,21 @@ int asr_rk2_stack_backward(const void* dyL, const void* xs, const void* xmids, l
   hipStream_t s = (hipStream_t)stream;
   unsigned char* base = (unsigned char*)ws;
   const size_t act = (size_t)N * H * W * C * 2;
-  const long E = 9L * C * C, ES = E + C, sst = (long)Lw.grid * ES, gst = (long)reduce_groups(Lw.grid) * ES;
+  const long ES = stack_slab_floats(C, 1), sst = (long)Lw.grid * ES, gst = (long)reduce_groups(Lw.grid) * ES;
   ASR_TRY(hip_check(hipMemcpyAsync(base + Lw.da, dyL, act, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync"));
   float* slabs = (float*)(base + Lw.slabs);
   float* grp = (float*)(base + Lw.grp);
   int lfold = L;
   ASR_TRY(block_stack_bwd_mfma(base + Lw.da, base + Lw.db, xs, x_stride, masks1, mask_stride, w, w_stride, h,
                                2.f * gamma, N, H, W, C, L, 0, slabs, sst, grp, gst, (unsigned*)(base + Lw.done),
-                               &lfold, s, xmids, masks2, base + Lw.g));
+                               &lfold, s, xmids, masks2, base + Lw.g, nullptr, 1, 1));
   ASR_TRY(hip_check(hipMemcpyAsync(dx0, base + ((L & 1) ? Lw.db : Lw.da), act, hipMemcpyDeviceToDevice, s),
                     "hipMemcpyAsync"));
   if (dparams) {
     ASR_TRY(stack_bwd_reduce_rest(slabs, sst, Lw.grid, ES, grp, gst, L, lfold, (const unsigned*)(base + Lw.done), s));
     int32_t* tm = (int32_t*)(base + Lw.tdst);
-    ASR_TRY(theta_dst_tile_major(theta_dst, 2 * n_theta, C, tm, s));
-    ASR_TRY(project_layers(grp, gst, reduce_groups(Lw.grid), E, C, tm, n_theta, L, dparams, n_theta + C, s));
+    ASR_TRY(theta_dst_pair(theta_dst, n_theta, C, tm, s));
+    ASR_TRY(project_layers(grp, gst, reduce_groups(Lw.grid), ES - C, C, tm, n_theta, L, dparams, n_theta + C, s));
   }
   return ASR_OK;
 }
@@ -881,7 +890,12 @@ int asr_net_prepare(const asr_net_config* cfg, void* ws, size_t ws_bytes) {
   ASR_TRY(hip_check(hipMemcpy(b + L.w_src, w_src.data(), w_src.size() * 4, hipMemcpyHostToDevice), "hipMemcpy"));
   ASR_TRY(hip_check(hipMemcpy(b + L.theta_dst, theta_dst.data(), theta_dst.size() * 4, hipMemcpyHostToDevice),
                     "hipMemcpy"));
-  if (L.stack_bwd) {  // the same map into k_bwd3_stack's tile-major dW slabs
+  if (L.stack_pair) {  // the same pull-back from k_bwd3_stack's pair-local D slabs
+    std::vector<int32_t> pr(theta_dst.size());
+    ASR_TRY(theta_dst_pair_host(theta_dst.data(), L.ntheta, cfg->C, pr.data()));
+    ASR_TRY(hip_check(hipMemcpy(b + L.theta_dst_pr, pr.data(), pr.size() * 4, hipMemcpyHostToDevice), "hipMemcpy"));
+  }
+  if (L.stack_bwd) {  // the same map into k_bwd3_stack's tile-major dW slabs (ASR_VARIANT_FULL_SLABS)
     const int C = cfg->C;
     std::vector<int32_t> tm(theta_dst);
     for (auto& v : tm) {
@@ -993,7 +1007,8 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   }
   if (stacked) {  // C=64: all L blocks in one launch, tile-major slabs
     const int grid = L.stack_grid;
-    const long ES = L.E + C, sst = (long)grid * ES;
+    const bool pair = L.stack_pair && !(cfg->variant & ASR_VARIANT_FULL_SLABS);
+    const long ES = stack_slab_floats(C, pair ? 1 : 0), sst = (long)grid * ES;
     float* slabs = (float*)(b + L.stack_slabs);
     float* grp = (float*)(b + L.grp);
     // (RK2: the first block's first stage has the extra term, so the stem's relu' runs separately)
@@ -1004,7 +1019,8 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
                                  L.wstride, cfg->h, L.sep_bwd ? 0.f : 2.f * cfg->gamma, N, H, W, C, cfg->L, ro0, slabs,
                                  sst, grp, L.grp_stride, (unsigned*)(b + L.stack_done), &lfold, s,
                                  L.rk2 ? b + L.xmids : nullptr, L.rk2 ? m1 + (size_t)cfg->L * L.mask_bytes : nullptr,
-                                 L.rk2 ? b + L.dxg : nullptr, grow ? b + L.grow : nullptr, fold_on ? 1 : 0));
+                                 L.rk2 ? b + L.dxg : nullptr, grow ? b + L.grow : nullptr, fold_on ? 1 : 0,
+                                 pair ? 1 : 0));
     ASR_TRY(timed_event(cfg, 3, s));
     // pass 1 of the blocks below lfold, and of any block whose in-launch fold was
     // flagged (a workgroup's wait ran out), before the projection reads them
@@ -1012,8 +1028,9 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
                                   (const unsigned*)(b + L.stack_done), s));
     if (cfg->L & 1) std::swap(dcur, dnext);
     dz1_fused = ro0;
-    ASR_TRY(project_layers(grp, L.grp_stride, reduce_groups(grid), L.E, C, (const int32_t*)(b + L.theta_dst_tm),
-                           L.ntheta, cfg->L, grads + L.off_blk, L.blk_stride, s));
+    ASR_TRY(project_layers(grp, L.grp_stride, reduce_groups(grid), ES - C, C,
+                           (const int32_t*)(b + (pair ? L.theta_dst_pr : L.theta_dst_tm)), L.ntheta, cfg->L,
+                           grads + L.off_blk, L.blk_stride, s));
     ASR_TRY(timed_event(cfg, 4, s));
   }
   for (int l = (L.deep || stacked) ? -1 : cfg->L - 1; l >= 0; --l) {

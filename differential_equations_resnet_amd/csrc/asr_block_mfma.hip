@@ -2247,12 +2247,59 @@ constexpr unsigned kStackSpinLimit = 1u << 13;
 __device__ unsigned g_stack_degraded = 0u;
 typedef __attribute__((address_space(1))) float gf32;
 
+// Pair-local weight-gradient tiling of k_bwd3_stack<..., PAIR> (C = 64, an
+// antisymmetric operator: W[8-t][o][i] = -W[t][i][o] for tap t = 3ky+kx,
+// …3By3.py:115-141, 277-293).  Every theta then pulls back
+// D(t,i,o) = dW[t][i][o] - dW[8-t][o][i] (one entry, a sign), so the slab
+// stores D, not dW: 74 16x16 tiles instead of 144 (half the publish burst
+// and half the fold's reads).  Wave w8 = 2p + h of the 8 wgrad waves owns tap
+// pair (p, 8-p) for input tiles a = 0..3 and output tiles b in {2h, 2h+1}:
+// X = dW[p] tiles (A = x(p, a), B = dz(b)) and the transposed dW[8-p] tiles
+// (A = dz(a), B = x(8-p, b): the same fragments in the other operand slot
+// give the transpose), D = X - Y^T in registers; plus 2 MFMAs of tap 4:
+// waves p < 3 one cross pair (a', b') of tiles (D likewise), waves p = 3 the
+// two self tiles of their b-set (raw, and transposed for the odd one; the
+// projection forms X - X^T there).  perm(0..3) orders the tiles a wave walks
+// (its b-set first) so that every accumulator and register index is
+// compile-time: acc[a][b] / acc[4+a][b] hold tiles (perm(a), perm(b)).
+using PairSlab = PairSlabLayout;  // (asr_common.h: the layout and the projection's pair_encode)
+struct PairRole {
+  // one wave-uniform word (the wgrad role sits at the SGPR limit): bits 0-7 perm(0..3),
+  // 8-9 t, 10 self, 11 (s1 == 2), 12-14 k4
+  unsigned w;
+  __device__ __forceinline__ explicit PairRole(int w8) {
+    const int t = w8 >> 1, h = w8 & 1, self = t == 3;
+    // tap-4 cross pair k4 = (a', b') with b' in the wave's b-set {2h, 2h+1}
+    const int k4 = 3 * h + t;
+    const int ap = pair_tap4_a(k4), bp = pair_tap4_b(k4);
+    const int b0 = self ? 2 * h : bp, b1 = (4 * h + 1) - b0;  // the b-set, b0 first
+    // perm(2): a' when a' is outside the b-set (the tap-4 transposed product reads dz(perm(s1)))
+    const int o0 = h ? 0 : 2, o1 = h ? 1 : 3;  // the two tiles outside the b-set
+    const bool ain = !self && (ap >> 1) == h;
+    const int p2 = (!self && !ain) ? ap : o0, p3 = (p2 == o0) ? o1 : o0;
+    const int s2 = (self || ain) ? 0 : 1;
+    w = (unsigned)(b0 | (b1 << 2) | (p2 << 4) | (p3 << 6) | (t << 8) | (self << 10) | (s2 << 11) | (k4 << 12));
+  }
+  __device__ __forceinline__ int perm(int k) const { return (w >> (2 * k)) & 3; }
+  __device__ __forceinline__ int t() const { return (w >> 8) & 3; }
+  __device__ __forceinline__ bool self() const { return (w >> 10) & 1; }
+  __device__ __forceinline__ bool s1_is_2() const { return (w >> 11) & 1; }
+  __device__ __forceinline__ int k4() const { return (int)(w >> 12) & 7; }
+  // tap-4 fragments: x(4, u0) (phase 2, with dz(perm 0)), x(4, v1) (phase 1, with dz(perm s1))
+  __device__ __forceinline__ int u0() const { return self() ? perm(0) : pair_tap4_a(k4()); }
+  __device__ __forceinline__ int v1() const { return self() ? perm(1) : pair_tap4_b(k4()); }
+  // LDS address bits of tile perm(k) relative to tile 0 (wave-uniform: one v_xor per read)
+  __device__ __forceinline__ unsigned sh(int k) const { return (unsigned)perm(k) << 5; }
+  // slab tile of acc[a][b] (D of tap t, input tile perm(a), output tile perm(b))
+  __device__ __forceinline__ int tile(int a, int b) const { return t() * 16 + perm(a) * 4 + perm(b); }
+};
+
 // RK2 (config 5): items walk 2L stages, per block l its second stage first
 // (dy = dL/dx_{l+1}, x = xmid_l, mask2, h, no +dy residual: out g = A^T dz2 into
 // gbuf) then its first (dy = g, x = x_l, mask1, h/2, plus the extra term
 // dL/dx_{l+1} by 16-B global loads: out dx_l).  Both stages accumulate one dW:
 // at the stage switch acc *= 2 (exact), and the block's slab is (h/2) acc.
-template <int C, int W, int BR, bool RK2 = false>
+template <int C, int W, int BR, bool RK2 = false, bool PAIR = false>
 __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0, bf16* __restrict__ dbuf1,
                                                        const bf16* __restrict__ xs, long x_stride,
                                                        const uint8_t* __restrict__ masks, long mask_stride,
@@ -2331,7 +2378,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
   if (n0 >= n1) return;  // (uniform per workgroup: never with grid <= N)
   ASR_BCLK(1, 0);
 
-  constexpr int ES = 9 * C * C + C, ECH = ES / 4;
+  constexpr int ES = PAIR ? PairSlab::ES : 9 * C * C + C, ECH = ES / 4;
   if (wave < 4) {
     // ---------------- dgrad waves ----------------
     const int ot = wave;
@@ -2471,25 +2518,47 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
     f32x4 acc[MTW][2];
 #pragma unroll
     for (int mi = 0; mi < MTW; ++mi) acc[mi][0] = acc[mi][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    unsigned offA[MTW], offB[2];  // pixel tile 1 sits 16 px = 2 KiB on (swizzle period 8 px)
+    // operand addresses: the full-dW tiling (PAIR false) reads 9 x fragments (offA) and 2 dz
+    // fragments (offB) per row; the pair-local tiling (PairRole) 8 x and 4 dz fragments
+    constexpr int NOA = PAIR ? 5 : MTW, NOB = PAIR ? 1 : 2;
+    unsigned offA[NOA], offB[NOB];  // pixel tile 1 sits 16 px = 2 KiB on (swizzle period 8 px)
+    const PairRole pr(w8);
     {
       const unsigned xb0 = lds_u32(lds + LL::X), zb0 = lds_u32(lds + LL::DZ);
       const int pb = 4 * g + tq;
-#pragma unroll
-      for (int mi = 0; mi < MTW; ++mi) {
-        const int mt = tg * MTW + mi;
-        const int tap = (16 * mt) / C, itile = ((16 * mt) % C) / 16;
+      auto xoff = [&](int tap, int itile) {
         const int ky = tap / 3, kx = tap % 3, q = 2 * itile + (tp >> 1);
-        offA[mi] = xb0 + (unsigned)(toff<C>(ky, pb + kx, q, TW) + 8 * (tp & 1));
-      }
+        return xb0 + (unsigned)(toff<C>(ky, pb + kx, q, TW) + 8 * (tp & 1));
+      };
+      auto zoff = [&](int otile) {
+        return zb0 + (unsigned)(toff<C>(1, pb + 1, 2 * otile + (tp >> 1), TW) + 8 * (tp & 1));
+      };
+      if constexpr (PAIR) {
+        // offA: x(t, tile 0), x(8-t, perm[0]), x(8-t, perm[1]), x(4, u0), x(4, v1); offB: dz(tile 0).
+        // A 16-channel tile's fragment address differs from tile 0's only in address bits 5-6
+        // (the chunk index 2*tile + h, XOR-swizzled by the column: (tile ^ (col&7)>>1) << 5; the
+        // buffer bases and the tile-buffer step keep those bits clear), so x(t, a) and dz(a) are
+        // read at offA[0] ^ (a << 5), offB[0] ^ (a << 5): one register each instead of four
+        offA[0] = xoff(pr.t(), 0);
+        offA[1] = xoff(8 - pr.t(), pr.perm(0));
+        offA[2] = xoff(8 - pr.t(), pr.perm(1));
+        offA[3] = xoff(4, pr.u0());
+        offA[4] = xoff(4, pr.v1());
+        offB[0] = zoff(0);
+      } else {
 #pragma unroll
-      for (int oi = 0; oi < 2; ++oi) {
-        const int q = 2 * (oq + oi) + (tp >> 1);
-        offB[oi] = zb0 + (unsigned)(toff<C>(1, pb + 1, q, TW) + 8 * (tp & 1));
-      }
+        for (int mi = 0; mi < MTW; ++mi) {
+          const int mt = tg * MTW + mi;
+          offA[mi] = xoff((16 * mt) / C, ((16 * mt) % C) / 16);
+        }
 #pragma unroll
-      for (int mi = 0; mi < MTW; ++mi) asm volatile("" : "+v"(offA[mi]));
-      asm volatile("" : "+v"(offB[0]), "+v"(offB[1]));
+        for (int oi = 0; oi < 2; ++oi) offB[oi] = zoff(oq + oi);
+      }
+      // opaque to the compiler: kept in VGPRs, not recomputed per band
+#pragma unroll
+      for (int k = 0; k < NOA; ++k) asm volatile("" : "+v"(offA[k]));
+#pragma unroll
+      for (int k = 0; k < NOB; ++k) asm volatile("" : "+v"(offB[k]));
     }
     auto own_row = [&](bool reuse) { return reuse ? (w8 < 4 ? 2 + w8 : -1) : (w8 < 6 ? w8 : -1); };
     // gtop (Euler): the top block's dy = dL/dx_L is the GAP gradient, one row per image constant over the
@@ -2499,7 +2568,10 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
     auto synth_row = [&](const Cur& c, int row, int nbuf) {
       const int gy = c.b * BR - 1 + row, q = lane & 7, p0 = lane >> 3;
       u32x4 v = {0u, 0u, 0u, 0u};
-      if ((unsigned)gy < (unsigned)H) v = *(const u32x4*)(gtop + (long)c.n * C + 8 * q);
+      if ((unsigned)gy < (unsigned)H) {  // (buffer load: a 32-bit lane offset, no 64-bit per-lane pointer kept live)
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(gtop + (long)c.n * C), 0, C * 2, 0x00020000);
+        v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * q, 0, 0));
+      }
       const unsigned rb = lds_u32(lds + LL::DY + nbuf * LL::TILE + row * LL::ROWB);
 #pragma unroll
       for (int k = 0; k < W / 8; ++k) lds_st128(rb + (unsigned)toff<C>(0, p0 + 8 * k + 1, q, TW), v);
@@ -2550,7 +2622,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
 #pragma unroll
     for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
     f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-    const bool dbw = tg == 3;
+    const bool dbw = PAIR ? pr.self() : tg == 3;
     // fold state (pass 1 of block l+2's reduction while on block l)
     const long fT = (long)((gridDim.x + 31) / 32) * ECH;
     const long fc0 = (long)blockIdx.x * fT / gridDim.x, fc1 = (long)(blockIdx.x + 1) * fT / gridDim.x;
@@ -2573,7 +2645,8 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
     auto fold_end = [&](int l) {
       if (fold) {
         for (; fp < fpe; ++fp, foff += ES) facc += *(const f32x4*)(pslabs + foff);
-        *(f32x4*)(grp + (long)l * grp_stride + (long)fg * ES + fch) = facc;
+        // (the group row's offset from live values: foff - fpe*ES is this thread's chunk)
+        *(f32x4*)(grp + (long)l * grp_stride + ((unsigned)fg * ES + (foff - (unsigned)fpe * ES))) = facc;
       }
       fold = false;
     };
@@ -2651,7 +2724,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       while (ipc < npc && ipc < ASR_BWD3_DMA0) piece();
       if (wave == 4) ASR_BTR(1, 1, it, 2);
       bf16x8 Bf[2], Ar[3];
-      auto mfma_band = [&](auto bo) {
+      auto mfma_band_full = [&](auto bo) {
         constexpr int BO = decltype(bo)::value;
         Ar[0] = tr_pair_px<BO>(offA[0]);
         static_for<0, BR>([&](auto rc) {
@@ -2681,12 +2754,61 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
           }
         });
       };
+      // pair-local tiling (PairRole): per row, phase 1 the transposed products of tap 8-t
+      // (A = dz(perm[a]), B = x(8-t, perm[b]): acc[4 + a][b] = dW[8-t]^T tiles) and the
+      // tap-4 partner's, phase 2 the direct products of tap t (A = x(t, perm[a]),
+      // B = dz(perm[b]): acc[a][b]) and the tap-4 tile; D = acc[a][b] - acc[4 + a][b]
+      // leaves at the block's end
+      auto mfma_band_pair = [&](auto bo) {
+        constexpr int BO = decltype(bo)::value;
+        static_for<0, BR>([&](auto rc) {
+          constexpr int r = decltype(rc)::value, RO_ = BO + r * LL::ROWB;
+          __builtin_amdgcn_sched_barrier(0);
+          if (r < rows) {
+            const bf16x8 x8a = tr_pair_px<RO_>(offA[1]), x8b = tr_pair_px<RO_>(offA[2]);
+            bf16x8 dz[4];
+            dz[0] = tr_pair_px<RO_>(offB[0] ^ pr.sh(0));
+            dz[1] = tr_pair_px<RO_>(offB[0] ^ pr.sh(1));
+            const bf16x8 x4v = tr_pair_px<RO_>(offA[4]);
+            static_for<0, 4>([&](auto ac) {
+              constexpr int a = decltype(ac)::value;
+              if constexpr (a >= 2) dz[a] = tr_pair_px<RO_>(offB[0] ^ pr.sh(a));
+              acc[4 + a][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dz[a], x8a, acc[4 + a][0], 0, 0, 0);
+              acc[4 + a][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dz[a], x8b, acc[4 + a][1], 0, 0, 0);
+              if constexpr (a == 2) {  // tap-4 transposed product: dz(perm[s1]) x x(4, v1)
+                const bf16x8 sel = pr.s1_is_2() ? dz[2] : dz[1];
+                acc[8][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, x4v, acc[8][1], 0, 0, 0);
+              }
+            });
+            bf16x8 xa[2];
+            xa[0] = tr_pair_px<RO_>(offA[0] ^ pr.sh(0));
+            static_for<0, 4>([&](auto ac) {
+              constexpr int a = decltype(ac)::value;
+              if constexpr (a + 1 < 4) xa[(a + 1) & 1] = tr_pair_px<RO_>(offA[0] ^ pr.sh(a + 1));
+              else xa[0] = tr_pair_px<RO_>(offA[3]);  // x(4, u0)
+              acc[a][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[a & 1], dz[0], acc[a][0], 0, 0, 0);
+              acc[a][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[a & 1], dz[1], acc[a][1], 0, 0, 0);
+            });
+            acc[8][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[0], dz[0], acc[8][0], 0, 0, 0);
+            if (dbw) {
+#pragma unroll
+              for (int oi = 0; oi < 2; ++oi)
+                accb[oi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, dz[oi], accb[oi], 0, 0, 0);
+            }
+            if (r < BR - 1 && ipc < npc) piece();
+          }
+        });
+      };
+      auto mfma_band = [&](auto bo) {
+        if constexpr (PAIR) mfma_band_pair(bo);
+        else mfma_band_full(bo);
+      };
       if (it > 0) {
         const unsigned dlt = buf ? (unsigned)LL::TILE : (unsigned)-LL::TILE;
 #pragma unroll
-        for (int mi = 0; mi < MTW; ++mi) offA[mi] += dlt;
+        for (int k = 0; k < NOA; ++k) offA[k] += dlt;
 #pragma unroll
-        for (int oi = 0; oi < 2; ++oi) offB[oi] += dlt;
+        for (int k = 0; k < NOB; ++k) offB[k] += dlt;
       }
       mfma_band(std::integral_constant<int, 0>{});
       while (ipc < npc) piece();
@@ -2697,11 +2819,11 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       }
       if (wave == 4) ASR_BTR(1, 1, it, 4);
       if (cont) {  // halo rows of the next band of this image
+        // compiler-visible LDS accesses: the item's DMAs were retired by the vm_wait(0)
+        // before the convert (cont implies more), so hipcc's own waits cost nothing
+        // here, and a copied or spilled read result stays correct
         const unsigned base = lds_u32(lds);
         const int nbf = buf ^ 1;
-        u32x4 cv[3];
-        unsigned dst[3];
-        int nc = 0;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           const int c = ft + 512 * k;
@@ -2711,15 +2833,10 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
             const unsigned sreg = which < 2 ? LL::DZ : which < 4 ? LL::X : LL::DY;
             const int srow = which == 4 ? BR + 1 : BR + (which & 1);
             const int drow = which == 4 ? 1 : (which & 1);
-            cv[k] = lds_rd128(base + sreg + buf * LL::TILE + srow * LL::ROWB + o);
-            dst[k] = base + sreg + nbf * LL::TILE + drow * LL::ROWB + o;
-            nc = k + 1;
+            lds_st128(base + sreg + nbf * LL::TILE + drow * LL::ROWB + o,
+                      lds_ld128(base + sreg + buf * LL::TILE + srow * LL::ROWB + o));
           }
         }
-        lgkm_wait<0>();
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-          if (k < nc) lds_wr128(dst[k], cv[k]);
       }
 #pragma unroll
       for (int q = 0; q < 2; ++q)
@@ -2740,22 +2857,40 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         // publish block l's dW tiles and db (write-through; drained at the next band barrier)
         float* slab = slabs + (long)l * slab_stride + (long)blockIdx.x * ES;
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, ES * 4, 0x00020000);
+        auto put = [&](int tile, f32x4 v) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, ((tile * 64 + lane) * 4) * 4, 0, 16);
+        };
+        if constexpr (PAIR) {  // D = X - Y^T per pair tile: 8 (+1 or 2 tap-4) tiles of the 74
 #pragma unroll
-        for (int mi = 0; mi < MTW; ++mi)
+          for (int a = 0; a < 4; ++a)
 #pragma unroll
-          for (int oi = 0; oi < 2; ++oi) {
-            const int mt = tg * MTW + mi;
-            f32x4 v = acc[mi][oi] * hsb;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs,
-                                                   (((mt * 4 + oq + oi) * 64 + lane) * 4) * 4, 0, 16);
-            acc[mi][oi] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int b = 0; b < 2; ++b) put(pr.tile(a, b), (acc[a][b] - acc[4 + a][b]) * hsb);
+          if (pr.self()) {
+            put(PairSlab::kSelf + pr.perm(0), acc[8][0] * hsb);  // raw X(4, c, c), c even
+            put(PairSlab::kSelf + pr.perm(1), acc[8][1] * hsb);  // X(4, c, c)^T, c odd
+          } else {
+            put(PairSlab::kTap4 + pr.k4(), (acc[8][0] - acc[8][1]) * hsb);
           }
+#pragma unroll
+          for (int mi = 0; mi < MTW; ++mi) acc[mi][0] = acc[mi][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        } else {
+#pragma unroll
+          for (int mi = 0; mi < MTW; ++mi)
+#pragma unroll
+            for (int oi = 0; oi < 2; ++oi) {
+              const int mt = tg * MTW + mi;
+              put(mt * 4 + oq + oi, acc[mi][oi] * hsb);
+              acc[mi][oi] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
         if (dbw) {
           if (g == 0) {
 #pragma unroll
-            for (int oi = 0; oi < 2; ++oi)
-              __hip_atomic_store((gf32*)(slab + 9 * C * C + 16 * (oq + oi) + lx), hsb * accb[oi][0], __ATOMIC_RELAXED,
+            for (int oi = 0; oi < 2; ++oi) {
+              const int ob = PAIR ? pr.perm(oi) : oq + oi;
+              __hip_atomic_store((gf32*)(slab + (ES - C) + 16 * ob + lx), hsb * accb[oi][0], __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
+            }
           }
           accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
@@ -3231,13 +3366,17 @@ static int stack_bwd_resident_per_cu() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (dev != dev_cached) {
-    int a = 0, b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, blk::k_bwd3_stack<64, 32, kBwdBR, false>, 768,
+    int a = 0, b = 0, c = 0, d = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, blk::k_bwd3_stack<64, 32, kBwdBR, false, false>, 768,
                                                      stack_bwd_lds()) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, blk::k_bwd3_stack<64, 32, kBwdBR, true>, 768,
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, blk::k_bwd3_stack<64, 32, kBwdBR, true, false>, 768,
+                                                     stack_bwd_lds()) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&c, blk::k_bwd3_stack<64, 32, kBwdBR, false, true>, 768,
+                                                     stack_bwd_lds()) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&d, blk::k_bwd3_stack<64, 32, kBwdBR, true, true>, 768,
                                                      stack_bwd_lds()) != hipSuccess)
       return 0;
-    per = std::min(a, b);
+    per = std::min(std::min(a, b), std::min(c, d));
     dev_cached = dev;
   }
   return per;
@@ -3258,6 +3397,9 @@ int block_stack_bwd_grid(int N) {
 
 int stack_done_words(int L) { return 2 * L + 4; }
 
+// floats per slab of k_bwd3_stack: the full dW (9C^2 + C) or, pair-local, the 74 D tiles + db
+long stack_slab_floats(int C, int pair) { return pair ? (long)PairSlabLayout::ES : 9L * C * C + C; }
+
 // the backward of L Euler blocks in one launch (k_bwd3_stack).  dbuf0 holds
 // dL/dx_L on entry, or gtop (Euler) its per-image row (the head's GAP
 // gradient, bf16 [N][C]): then dbuf0 is not read.  Block 0's dx ends in dbuf[L & 1].  Block l's slabs (grid
@@ -3270,13 +3412,14 @@ int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride
                          long mask_stride, const void* w, long w_stride, float h, float two_gamma, int N, int H, int W,
                          int C, int L, int ro0, float* slabs, long slab_stride, float* grp, long grp_stride,
                          unsigned* done, int* lfold_out, hipStream_t s, const void* xm, const uint8_t* masks2,
-                         void* gbuf, const void* gtop, int fold) {
+                         void* gbuf, const void* gtop, int fold, int pair) {
   if (!block_stack_bwd_supported(N, H, W, C) || L < 1)
     return fail(ASR_E_UNSUPPORTED, "stack backward: needs C=64, W=32, >= 4 row bands per image (C=%d W=%d H=%d)", C, W, H);
   const int grid = block_stack_bwd_grid(N);
-  if (slab_stride < (long)grid * (9L * C * C + C)) return fail(ASR_E_ARG, "stack backward: slab_stride too small");
+  const long ES = stack_slab_floats(C, pair);
+  if (slab_stride < (long)grid * ES) return fail(ASR_E_ARG, "stack backward: slab_stride too small");
   // in-kernel pass 1 needs <= 512 group-row chunks per workgroup (one per wgrad thread)
-  const long fchunks = (long)((grid + 31) / 32) * ((9L * C * C + C) / 4);
+  const long fchunks = (long)((grid + 31) / 32) * (ES / 4);
   // fold = 0: no in-launch pass 1, so no workgroup ever waits for another (no
   // co-residency needed: e.g. several processes sharing one device)
   const int lfold = fold && (fchunks + grid - 1) / grid <= 512 ? 2 : L;
@@ -3284,18 +3427,21 @@ int block_stack_bwd_mfma(void* dbuf0, void* dbuf1, const void* xs, long x_stride
   ASR_TRY(hip_check(hipMemsetAsync(done, 0, (size_t)stack_done_words(L) * 4, s), "hipMemsetAsync"));
   unsigned* skipf = done + L + 4;
   const size_t lds = stack_bwd_lds();
+#define ASR_STACK_BWD(RK, PR)                                                                                   \
+  hipLaunchKernelGGL((blk::k_bwd3_stack<64, 32, kBwdBR, RK, PR>), dim3(grid), dim3(768), lds, s, (bf16*)dbuf0,         \
+                     (bf16*)dbuf1, (const bf16*)xs, x_stride, masks, mask_stride, (const bf16*)w, w_stride, h,         \
+                     two_gamma, N, H, L, RK ? 0 : ro0, slabs, slab_stride, grp, grp_stride, done, skipf, lfold,        \
+                     RK ? (const bf16*)xm : nullptr, RK ? masks2 : nullptr, RK ? (bf16*)gbuf : nullptr,                \
+                     RK ? nullptr : (const bf16*)gtop)
   if (xm) {  // RK2: both stages of every block (x_mid stack at xm, stride x_stride; masks2; g scratch)
     if (!masks2 || !gbuf) return fail(ASR_E_ARG, "stack backward (RK2): masks2 and the g buffer are required");
-    hipLaunchKernelGGL((blk::k_bwd3_stack<64, 32, kBwdBR, true>), dim3(grid), dim3(768), lds, s,
-                       (bf16*)dbuf0, (bf16*)dbuf1, (const bf16*)xs, x_stride, masks, mask_stride, (const bf16*)w,
-                       w_stride, h, two_gamma, N, H, L, 0, slabs, slab_stride, grp, grp_stride, done, skipf,
-                       lfold, (const bf16*)xm, masks2, (bf16*)gbuf);
+    if (pair) ASR_STACK_BWD(true, true);
+    else ASR_STACK_BWD(true, false);
   } else {
-    hipLaunchKernelGGL((blk::k_bwd3_stack<64, 32, kBwdBR>), dim3(grid), dim3(768), lds, s,
-                       (bf16*)dbuf0, (bf16*)dbuf1, (const bf16*)xs, x_stride, masks, mask_stride, (const bf16*)w,
-                       w_stride, h, two_gamma, N, H, L, ro0, slabs, slab_stride, grp, grp_stride, done, skipf,
-                       lfold, nullptr, nullptr, nullptr, (const bf16*)gtop);
+    if (pair) ASR_STACK_BWD(false, true);
+    else ASR_STACK_BWD(false, false);
   }
+#undef ASR_STACK_BWD
   ASR_LAUNCH_CHECK("k_bwd3_stack");
   return ASR_OK;
 }

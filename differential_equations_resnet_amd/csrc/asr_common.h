@@ -37,6 +37,54 @@ int cu_count();
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// Slab layout of the pair-local C=64 stacked backward (k_bwd3_stack<..., PAIR>,
+// asr_block_mfma.hip): for an antisymmetric operator every theta pulls back
+// D(t,i,o) = dW[t][i][o] - dW[8-t][o][i] (tap t = 3ky+kx), and the slab holds
+// 74 16x16 fp32 tiles of D, element (r, c) of tile T at T*256 + ((r/4)*16 + c)*4 + r%4:
+//   T = 16p + 4a + b (p < 4):  D(p, 16a + r, 16b + c)
+//   T = 64 + k (tap-4 cross pairs (a', b') = kPairTap4A/B[k]):  D(4, 16a' + r, 16b' + c)
+//   T = 70 + c (tap-4 self tiles): X = dW[4] tile (c, c), raw for even c, transposed for odd c
+// then db [64].  pair_encode turns one entry (e = (t*C + i)*C + o, neg) of a theta's
+// (e, mirror(e)) pair into 1 or 2 (slab index << 1 | neg) entries.
+struct PairSlabLayout {
+  static constexpr int kTap4 = 64, kSelf = 70, kTiles = 74, E = kTiles * 256, ES = E + 64;
+};
+__host__ __device__ inline int pair_slab_index(int T, int r, int c) { return T * 256 + ((r >> 2) * 16 + c) * 4 + (r & 3); }
+// tap-4 cross pairs (a', b'), k = 3h + p for the waves (p < 3, h) of k_bwd3_stack<PAIR>
+__host__ __device__ inline int pair_tap4_a(int k) { return k < 3 ? (k == 0 ? 1 : k == 1 ? 2 : 3) : (k == 3 ? 3 : k == 4 ? 1 : 0); }
+__host__ __device__ inline int pair_tap4_b(int k) { return k < 3 ? (k == 2 ? 1 : 0) : (k == 5 ? 3 : 2); }
+__host__ __device__ inline int pair_encode(long e, int neg, int C, int32_t* out) {
+  const int t = (int)(e / ((long)C * C)), i = (int)((e / C) % C), o = (int)(e % C);
+  if (t < 4) {
+    out[0] = (pair_slab_index(t * 16 + (i >> 4) * 4 + (o >> 4), i & 15, o & 15) << 1) | neg;
+    return 1;
+  }
+  if (t > 4) {  // D(t, i, o) = -D(8-t, o, i)
+    out[0] = (pair_slab_index((8 - t) * 16 + (o >> 4) * 4 + (i >> 4), o & 15, i & 15) << 1) | (neg ^ 1);
+    return 1;
+  }
+  const int a = i >> 4, b = o >> 4;
+  if (a != b) {
+    for (int k = 0; k < 6; ++k) {
+      if (pair_tap4_a(k) == a && pair_tap4_b(k) == b) {
+        out[0] = (pair_slab_index(PairSlabLayout::kTap4 + k, i & 15, o & 15) << 1) | neg;
+        return 1;
+      }
+      if (pair_tap4_a(k) == b && pair_tap4_b(k) == a) {  // D(4, i, o) = -D(4, o, i)
+        out[0] = (pair_slab_index(PairSlabLayout::kTap4 + k, o & 15, i & 15) << 1) | (neg ^ 1);
+        return 1;
+      }
+    }
+    return 0;
+  }
+  // self tile: D = X[i][o] - X[o][i]; stored raw (a even) or transposed (a odd)
+  const int T = PairSlabLayout::kSelf + a, ri = i & 15, ro = o & 15;
+  const bool tr = (a & 1) != 0;
+  out[0] = (pair_slab_index(T, tr ? ro : ri, tr ? ri : ro) << 1) | neg;
+  out[1] = (pair_slab_index(T, tr ? ri : ro, tr ? ro : ri) << 1) | (neg ^ 1);
+  return 2;
+}
+
 // ---- device helpers --------------------------------------------------------
 
 __device__ __forceinline__ float to_f32(float v) { return v; }

@@ -291,6 +291,8 @@ __global__ void k_project(const float* __restrict__ red_groups, int G, long E, c
   if (dbias && t < Cb) dbias[t] = red_at(E + t);
 }
 
+int theta_dst_pair_host(const int32_t* in, long n_theta, int C, int32_t* out);  // (below)
+
 }  // namespace asr
 
 using namespace asr;
@@ -312,6 +314,12 @@ int asr_param_is_antisymmetric(int kind, int antisymmetric) { return param_is_an
 
 int asr_param_map_transpose(int C, const int32_t* w_src, int32_t* w_src_bwd) {
   return param_map_transpose(C, w_src, w_src_bwd);
+}
+
+int asr_param_map_pair(int C, const int32_t* theta_dst, long n_theta, int32_t* theta_dst_pair) {
+  if (C != 64 || !theta_dst || !theta_dst_pair || n_theta < 0)
+    return fail(ASR_E_ARG, "asr_param_map_pair: C=64 and non-null maps required");
+  return theta_dst_pair_host(theta_dst, n_theta, C, theta_dst_pair);
 }
 
 long asr_wpack_elems(int C) {
@@ -445,6 +453,45 @@ __global__ void k_theta_dst_tile(const int32_t* __restrict__ in, long n, int C, 
   const long e = v >> 1, m = e / C, o = e % C;
   const long et = (((m / 16) * (C / 16) + o / 16) * 64 + 16 * ((m % 16) / 4) + o % 16) * 4 + m % 4;
   out[i] = (int32_t)((et << 1) | (v & 1));
+}
+
+// theta_dst (pairs of (e << 1 | neg) entries per theta, asr_param_map) of an
+// antisymmetric parametrisation -> the same pull-back from the pair-local
+// slabs (pair_encode of the first entry: the second is its mirror)
+__global__ void k_theta_dst_pair(const int32_t* __restrict__ in, long n_theta, int C, int32_t* __restrict__ out) {
+  const long j = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (j >= n_theta) return;
+  int32_t o[2] = {-1, -1};
+  const int32_t v = in[2 * j];
+  if (v >= 0) pair_encode(v >> 1, v & 1, C, o);
+  out[2 * j] = o[0];
+  out[2 * j + 1] = o[1];
+}
+
+int theta_dst_pair(const int32_t* in, long n_theta, int C, int32_t* out, hipStream_t s) {
+  if (C != 64) return fail(ASR_E_UNSUPPORTED, "pair-local slabs: C=64 only");
+  hipLaunchKernelGGL(k_theta_dst_pair, dim3((unsigned)((n_theta + 255) / 256)), dim3(256), 0, s, in, n_theta, C, out);
+  ASR_LAUNCH_CHECK("k_theta_dst_pair");
+  return ASR_OK;
+}
+
+// host: the same from a host theta_dst; ASR_E_ARG when some theta is not an
+// antisymmetric pair (e, mirror(e)) with opposite signs (the pair-local path
+// does not apply)
+int theta_dst_pair_host(const int32_t* in, long n_theta, int C, int32_t* out) {
+  for (long j = 0; j < n_theta; ++j) {
+    const int32_t v0 = in[2 * j], v1 = in[2 * j + 1];
+    if (v0 < 0 || v1 < 0) return fail(ASR_E_ARG, "theta %ld: not an antisymmetric pair", j);
+    const long e0 = v0 >> 1, e1 = v1 >> 1;
+    const int t = (int)(e0 / ((long)C * C)), i = (int)((e0 / C) % C), o = (int)(e0 % C);
+    const long mirror = ((long)(8 - t) * C + o) * C + i;
+    if (e1 != mirror || ((v0 ^ v1) & 1) == 0) return fail(ASR_E_ARG, "theta %ld: not an antisymmetric pair", j);
+    int32_t o2[2] = {-1, -1};
+    if (pair_encode(e0, v0 & 1, C, o2) == 0) return fail(ASR_E_ARG, "theta %ld: no pair-local slab entry", j);
+    out[2 * j] = o2[0];
+    out[2 * j + 1] = o2[1];
+  }
+  return ASR_OK;
 }
 
 int theta_dst_tile_major(const int32_t* in, long n, int C, int32_t* out, hipStream_t s) {

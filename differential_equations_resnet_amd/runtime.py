@@ -16,7 +16,7 @@ from ._lib import (ASR_BF16, ASR_F32, ASR_INTEGRATOR_EULER, ASR_INTEGRATOR_RK2, 
                    ASR_PARAM_3BY3, ASR_PARAM_GENERAL, ASR_PARAM_REGULAR, ASR_VARIANT_NO_FOLD, ASR_VARIANT_STEM_FWD_VALU,
                    ASR_VARIANT_STEM_WGRAD_VALU, ASR_VARIANT_PER_BLOCK_FWD,
                    ASR_VARIANT_PER_BLOCK_BWD, ASR_VARIANT_INFERENCE, ASR_VARIANT_TIMED, ASR_VARIANT_FULL_DXL,
-                   NetConfig)
+                   ASR_VARIANT_FULL_SLABS, NetConfig)
 
 __all__ = [
     "require_gpu", "dtype_code", "torch_dtype", "ParamMap", "param_map", "theta_count", "theta_to_w",

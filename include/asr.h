@@ -101,6 +101,16 @@ int asr_param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* t
  * backward's w. */
 int asr_param_is_antisymmetric(int kind, int antisymmetric);
 int asr_param_map_transpose(int C, const int32_t* w_src, int32_t* w_src_bwd);
+/* Host: the pull-back of an antisymmetric parametrisation (C = 64) from the
+ * pair-local slabs of the stacked backward (asr_block_stack_backward, the
+ * network's C=64 bf16 backward): every theta's entries (e, mirror(e)) of
+ * theta_dst (asr_param_map) become 1 or 2 entries (s << 1 | neg) into a slab
+ * of 74 16x16 tiles of D = dW - dW*^T (dW*[t][i][o] = dW[8-t][o][i]): tile
+ * 16p + 4a + b holds D(tap p < 4, input tile a, output tile b); 64 + k the
+ * tap-4 cross pair k; 70 + c tap 4's self tile c (raw, transposed for odd c);
+ * element (r, c) of tile T at T*256 + ((r/4)*16 + c)*4 + r%4.  ASR_E_ARG when
+ * some theta is not an antisymmetric pair. */
+int asr_param_map_pair(int C, const int32_t* theta_dst, long n_theta, int32_t* theta_dst_pair);
 
 /* Elements of the packed bf16 W consumed by the MFMA kernels. */
 long asr_wpack_elems(int C);
@@ -279,6 +289,11 @@ typedef struct asr_net_config {
                                      that the top block reads, instead of the
                                      per-image row it is constant over
                                      (cross-check of the synthesised dy)        */
+#define ASR_VARIANT_FULL_SLABS 256 /* C=64 bf16 stacked backward of an antisymmetric
+                                      operator: publish the full dW (144 tiles per
+                                      workgroup slab) instead of the pair-local
+                                      D = dW - dW*^T (74 tiles) the projection
+                                      needs (cross-check and A/B arm)           */
 
 long asr_net_param_count(const asr_net_config* cfg);
 size_t asr_net_workspace_bytes(const asr_net_config* cfg);

@@ -208,3 +208,59 @@ def test_forward_backward_rejects_inference_workspace_before_launching(lib):
         rc = lib.asr_net_forward_backward(ct.byref(cfg), fake, fake, fake, fake, fake, None, fake, wsb, None)
         assert rc == _lib.ASR_E_ARG, (kind, rc)
         assert "INFERENCE" in lib.asr_last_error().decode()
+
+
+def _pair_slab_from_dW(dW):
+    """The pair-local slab of the C=64 stacked backward (asr.h, asr_param_map_pair),
+    restated from its documented layout: 74 tiles of D = dW - dW*^T, then db."""
+    C = 64
+    W = dW.reshape(9, C, C)
+    slab = np.zeros(74 * 256)
+
+    def put(T, tile):  # element (r, c) of tile T at T*256 + ((r/4)*16 + c)*4 + r%4
+        r, c = np.meshgrid(np.arange(16), np.arange(16), indexing="ij")
+        slab[T * 256 + ((r // 4) * 16 + c) * 4 + r % 4] = tile
+
+    for p in range(4):
+        for a in range(4):
+            for b in range(4):
+                put(16 * p + 4 * a + b, W[p, 16 * a:16 * a + 16, 16 * b:16 * b + 16]
+                    - W[8 - p, 16 * b:16 * b + 16, 16 * a:16 * a + 16].T)
+    for k, (a, b) in enumerate([(1, 0), (2, 0), (3, 1), (3, 2), (1, 2), (0, 3)]):
+        put(64 + k, W[4, 16 * a:16 * a + 16, 16 * b:16 * b + 16] - W[4, 16 * b:16 * b + 16, 16 * a:16 * a + 16].T)
+    for c in range(4):
+        X = W[4, 16 * c:16 * c + 16, 16 * c:16 * c + 16]
+        put(70 + c, X.T if c & 1 else X)
+    return slab
+
+
+@pytest.mark.parametrize("kind,anti", [(0, 1), (1, 1)])
+def test_pair_map_projects_like_the_full_dW(lib, kind, anti):
+    """asr_param_map_pair (the stacked backward's pull-back from its pair-local
+    slabs) gives every theta the same dtheta as the full-dW projection (the
+    oracle's project_dW), exactly in float64 (the same two terms); a
+    non-antisymmetric parametrisation is refused."""
+    C = 64
+    n = lib.asr_theta_count(C, kind, anti)
+    w_src = np.empty(9 * C * C, np.int32)
+    dst = np.empty(2 * n, np.int32)
+    assert lib.asr_param_map(C, kind, anti, w_src.ctypes.data, dst.ctypes.data) == 0
+    pr = np.empty(2 * n, np.int32)
+    assert lib.asr_param_map_pair(C, dst.ctypes.data, n, pr.ctypes.data) == 0
+    dW = np.random.default_rng(3).standard_normal(9 * C * C)
+    slab = _pair_slab_from_dW(dW)
+    got = np.zeros(n)
+    for q in range(2):
+        v = pr[q::2]
+        ok = v >= 0
+        got[ok] += np.where(v[ok] & 1, -1.0, 1.0) * slab[v[ok] >> 1]
+    src, sign = O.param_map(C, "3by3" if kind == 0 else "general", 3, bool(anti))
+    assert np.array_equal(got, O.project_dW(dW, src, sign, n))
+    # the regular kind (no antisymmetry) has no pair-local pull-back
+    nr = lib.asr_theta_count(C, 2, 0)
+    w2 = np.empty(9 * C * C, np.int32)
+    d2 = np.empty(2 * nr, np.int32)
+    assert lib.asr_param_map(C, 2, 0, w2.ctypes.data, d2.ctypes.data) == 0
+    p2 = np.empty(2 * nr, np.int32)
+    from differential_equations_resnet_amd import _lib
+    assert lib.asr_param_map_pair(C, d2.ctypes.data, nr, p2.ctypes.data) == _lib.ASR_E_ARG

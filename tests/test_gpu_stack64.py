@@ -438,3 +438,36 @@ def test_stacked_step_run_to_run(rt, N, L, integ):
         loss, g = ex.forward_backward(params, imgs, tgt)
         assert torch.equal(loss, loss0) and torch.equal(g, g0)
     assert g0.abs().max().item() > 0
+
+
+@pytest.mark.parametrize("N,L,integrator,gamma", [(512, 4, "euler", 0.0), (8, 3, "euler", -0.1), (192, 5, "euler", 0.0),
+                                                  (64, 3, "rk2", 0.0)])
+def test_pair_local_slabs_equal_full_slabs(rt, N, L, integrator, gamma):
+    """The production stacked backward publishes pair-local slabs (74 tiles of
+    D = dW - dW*^T, formed in the wgrad waves' registers) and projects them
+    with asr_param_map_pair's map; ASR_VARIANT_FULL_SLABS publishes the full dW
+    (144 tiles) and projects with the two-term map.  dx is untouched: loss,
+    stem and head gradients bitwise; block gradients the same products summed
+    in another order: 1e-5 of max|g| per block; the pair arm is deterministic."""
+    C = 64
+    dev, params, imgs, tgt = _net_case(rt, N, C, L, seed=11)
+    ex = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / max(L, 4), gamma, subtract_mean=127.5, divide_by_stddev=127.5,
+                        dtype="bfloat16", input_u8=True, device=dev, integrator=integrator)
+    loss, g = ex.forward_backward(params, imgs, tgt)
+    loss, g = loss.clone(), g.clone()
+    _, g2 = ex.forward_backward(params, imgs, tgt)
+    assert torch.equal(g, g2), "pair-local stacked backward is not deterministic"
+    ex.variant = rt.ASR_VARIANT_FULL_SLABS
+    loss1, g1 = ex.forward_backward(params, imgs, tgt)
+    ex.variant = 0
+    ex.check_status()
+    assert torch.equal(loss, loss1)
+    a, b = g.cpu().numpy(), g1.cpu().numpy()
+    n_blk = (ex.n_params - (9 * 3 * C + C) - (C * 10 + 10)) // L
+    stem, head = 9 * 3 * C + C, C * 10 + 10
+    assert np.array_equal(a[:stem], b[:stem]) and np.array_equal(a[-head:], b[-head:])
+    for l in range(L):
+        o = stem + l * n_blk
+        ga, gb = a[o:o + n_blk], b[o:o + n_blk]
+        assert np.abs(gb).max() > 0
+        assert np.abs(ga - gb).max() <= 1e-5 * np.abs(gb).max(), (l, np.abs(ga - gb).max(), np.abs(gb).max())
