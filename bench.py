@@ -70,6 +70,27 @@ CONFIGS = {
               "train"),
     "c5": (64, 30, 512, "bfloat16", "antisym-ResNet-32 (C=64, 30 RK2 midpoint blocks) batch 512/GPU bf16", "rk2",
            "train"),
+    "c2_f32": (64, 30, 512, "float32", "antisym-ResNet-32 (C=64, 30 Euler blocks) batch 512/GPU fp32 (the reference's "
+               "precision, fp32 MFMA)", "euler", "train"),
+    # the notebooks' trained model: 64 blocks x 16 filters, h = 8/64, batch 32 (experiments_antisymmetric_resnet_v6.ipynb
+    # cells 1, 5, 9, :30-45, :107-135, :353-389) and its batch-1 predict (_v7.ipynb cells 19-25, :571-672)
+    "v6": (16, 64, 32, "bfloat16", "antisym 64 blocks x 16 filters (v6 notebook model), batch 32 bf16", "euler",
+           "train"),
+    "v6_f32": (16, 64, 32, "float32", "antisym 64 blocks x 16 filters (v6 notebook model), batch 32 fp32", "euler",
+               "train"),
+    "v7_predict": (16, 64, 1, "bfloat16", "antisym 64 blocks x 16 filters, Model.predict of ONE image (v7 notebook "
+                   "speed test), bf16", "euler", "eval"),
+}
+# the reference's own measurements of the same metric (TF 1.12, fp32, one NVIDIA GPU)
+REFERENCE = {
+    "v6": (46.7, "images/s", "training 1.46 it/s x 32, experiments_antisymmetric_resnet_v6.ipynb:362"),
+    "v6_f32": (46.7, "images/s", "training 1.46 it/s x 32, experiments_antisymmetric_resnet_v6.ipynb:362"),
+    "v7_predict": (5.02, "images/s", "batch-1 predict 0.1993 s/image, experiments_antisymmetric_resnet_v7.ipynb:650-651"),
+}
+METRICS = {
+    "v6": "CIFAR-10 images/sec (fwd+bwd) antisym 64x16 (v6 notebook model) @ batch 32; 1 GPU",
+    "v6_f32": "CIFAR-10 images/sec (fwd+bwd) antisym 64x16 (v6 notebook model) @ batch 32 fp32; 1 GPU",
+    "v7_predict": "batch-1 Model.predict images/sec (1 / latency) antisym 64x16; 1 GPU",
 }
 
 
@@ -595,8 +616,11 @@ def main():
         elif stacked:
             kname = ("all L Euler blocks in one launch each: blk::k_fwd3_stack (forward), blk::k_bwd3_stack "
                      "(backward, pass 1 of the slab reduction in-launch)")
+        elif dtype_name == "float32":
+            kname = ("the per-block fp32 MFMA kernels of every block (asr_conv_f32.hip: k_conv32 forward / dgrad, "
+                     "k_wgrad32; v_mfma_f32_16x16x4_f32)")
         else:
-            kname = "the per-block kernels of every block (fp32: asr_conv_f32.hip)"
+            kname = "the per-block kernels of every block"
         if not train:
             kname = ("all L Euler blocks in one launch: blk::k_fwd3_stack over two ping-pong activation slots, "
                      "no relu masks (forward only)" if stacked else kname + " (forward only)")
@@ -612,6 +636,12 @@ def main():
                 "mfma_tflops": round(tflops, 1), "mfma_frac": round(tflops / peak_tf, 4),
                 "kernels": {"fwd": {"avg_us": round(t_fwd * 1e6, 2), "algorithmic_bytes": b_fwd,
                                     "frac": round(b_fwd / t_fwd / 1e9 / HBM_PEAK_GBS, 4)}}}
+        if dtype_name == "float32":
+            # fp32 blocks sit far right of the fp32 ridge (157 TF / 8 TB/s = 20 FLOP/B; C=16: 43, C=64: 173):
+            # the bound is the fp32 MFMA pipe (v_mfma_f32_16x16x4_f32 = the fp32 vector rate)
+            roof.update({"bound": "mfma", "achieved": round(tflops, 2), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tflops / F32_PEAK_TFLOPS, 4), "hbm_gbs": round(achieved, 1),
+                         "hbm_frac": round(achieved / HBM_PEAK_GBS, 4)})
         if train:
             roof["kernels"]["bwd"] = {"avg_us": round(t_bwd * 1e6, 2), "algorithmic_bytes": b_bwd,
                                       "frac": round(b_bwd / t_bwd / 1e9 / HBM_PEAK_GBS, 4)}
@@ -640,11 +670,13 @@ def main():
                 cpu = cpu_baseline(threads)
             elif args.config == "c2_eval":
                 cpu = cpu_eval_baseline(threads)
+        ref = REFERENCE.get(args.config)
         out = {
-            "metric": METRIC if train else METRIC.replace("(fwd+bwd)", "(forward only, evaluation)"),
+            "metric": METRICS.get(args.config, METRIC if train else METRIC.replace("(fwd+bwd)",
+                                                                                 "(forward only, evaluation)")),
             "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None,
+            "scaling": "weak", "vs_baseline": round(value / ref[0], 1) if ref else None,
             "dtype": "bf16" if dtype_name == "bfloat16" else "f32",
             "data": f"synthetic ({N_BATCHES} HBM-resident batches of uniform uint8 32x32x3 images with random one-hot "
                     f"labels, cycled; reference init with block thetas x{THETA_SCALE} and fc kernel x{FC_SCALE})",
@@ -659,6 +691,9 @@ def main():
                        "degraded_handoffs": degraded},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if ref:
+            out["baseline"] = {"value": ref[0], "unit": ref[1], "source": ref[2],
+                               "hardware": "one NVIDIA GPU, TensorFlow 1.12, fp32 (BASELINE.md §1)"}
         print(json.dumps(out), flush=True)
     distributed.shutdown()
     if live is not None and live < 0.9:

@@ -293,3 +293,67 @@ def test_stem_fwd_mfma_matches_fp32_path(rt, N, u8, C):
     assert np.isfinite(a).all()
     assert np.abs(a - b).max() <= 1e-3, np.abs(a - b).max()
     assert (a.argmax(1) == b.argmax(1)).mean() >= 0.98
+
+
+def _bf16_emulated_probs(spec, params, img):
+    """The notebooks' network on ONE image in float64 with the bf16 path's
+    roundings (W_l, the stem output and every x_{l+1} rounded to bf16; fp32
+    parameters otherwise): oracle.net_forward's composition, step by step."""
+    conv1_k, conv1_b, blocks, fc_k, fc_b = O.split_params(spec, params)
+    x = bf16_round(np.maximum(O.conv2d_same(O.normalize_input(img[None], spec), conv1_k) + conv1_b, 0))
+    src, sign = O.param_map(spec.C)
+    for theta, b in blocks:
+        W = bf16_round(O.assemble_from_map(O.flatten(theta), spec.C, src, sign, spec.gamma)).astype(np.float64)
+        z = O.conv2d_same(x.astype(np.float64), W) + b
+        x = bf16_round(x + spec.h * np.maximum(z, 0)).astype(np.float64)
+    return O.softmax(x.mean(axis=(1, 2)) @ fc_k + fc_b)[0]
+
+
+def test_v6_small_batch_and_batch1_predict(rt):
+    """The notebooks' trained configuration (experiments_antisymmetric_resnet_v6.ipynb
+    cells 1, 5, 9: 64 blocks x 16 filters, h = 8/64, batch 32) on the bf16 path
+    (the fused C=16 stack: one workgroup per image, all 64 blocks in one launch
+    each way), and its batch-1 predict (_v7.ipynb cells 19-25):
+      * per-image spot checks: the probabilities of images 0 and 31 against the
+        float64 oracle with the same bf16 roundings (5e-3 absolute);
+      * batch-1 predict (the forward-only executor at N=1) equals the batch-32
+        training forward's probabilities of that image bitwise (images never
+        interact);
+      * batch additivity: the batch-32 gradient is the mean of the two halves'
+        (1e-4 of max|g|), and two calls are bitwise identical."""
+    from differential_equations_resnet_amd.netparams import init_net_params
+    C, L, N = 16, 64, 32
+    spec = O.NetSpec(C=C, L=L, h=8.0 / L)
+    dev = torch.device("cuda")
+    flat = (init_net_params(C, L, 3, 10, seed=6) * 0.5).astype(np.float32)
+    params = O.unflatten(flat.astype(np.float64), spec.param_shapes())
+    rng = np.random.default_rng(64)
+    raw = rng.integers(0, 256, (N, 32, 32, 3), dtype=np.uint8)
+    imgs = torch.from_numpy(raw).to(dev)
+    tgt = torch.from_numpy(np.eye(10, dtype=np.float32)[rng.integers(0, 10, N)]).to(dev)
+    p = torch.from_numpy(flat).to(dev)
+
+    def ex(n, inference=False):
+        return rt.NetExecutor(n, 32, 32, 3, C, L, 10, spec.h, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
+                              dtype="bfloat16", input_u8=True, device=dev, inference=inference)
+    full = ex(N)
+    loss, g = full.forward_backward(p, imgs, tgt, want_probs=True)
+    probs = full.probs.clone()
+    loss, g = loss.clone(), g.clone()
+    loss2, g2 = full.forward_backward(p, imgs, tgt)
+    assert torch.equal(g, g2) and torch.equal(loss, loss2), "not deterministic"
+    half = ex(N // 2)
+    la, ga = half.forward_backward(p, imgs[:N // 2].contiguous(), tgt[:N // 2].contiguous())
+    la, ga = la.clone(), ga.clone()
+    lb, gb = half.forward_backward(p, imgs[N // 2:].contiguous(), tgt[N // 2:].contiguous())
+    torch.cuda.synchronize()
+    assert abs(loss.item() - 0.5 * (la.item() + lb.item())) <= 1e-5 * abs(loss.item())
+    gf, gm = g.cpu().numpy(), (0.5 * (ga + gb)).cpu().numpy()
+    assert np.abs(gf - gm).max() <= 1e-4 * np.abs(gf).max()
+    one = ex(1, inference=True)
+    for n in (0, N - 1):
+        want = _bf16_emulated_probs(spec, params, raw[n])
+        got = probs[n].cpu().numpy().astype(np.float64)
+        assert np.abs(got - want).max() <= 5e-3, (n, np.abs(got - want).max())
+        p1 = one.forward(p, imgs[n:n + 1].contiguous())
+        assert torch.equal(p1[0], probs[n]), "batch-1 predict differs from the image's row of the batch"
