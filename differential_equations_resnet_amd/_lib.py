@@ -79,6 +79,13 @@ SIGNATURES = [
     ("asr_param_is_antisymmetric", _I, [_I, _I]),
     ("asr_param_map_transpose", _I, [_I, _P, _P]),
     ("asr_param_map_pair", _I, [_I, _P, ct.c_long, _P]),
+    ("asr_theta_count_k", _L, [_I, _I, _I, _I]),
+    ("asr_param_map_k", _I, [_I, _I, _I, _I, _P, _P]),
+    ("asr_param_map_transpose_k", _I, [_I, _I, _P, _P]),
+    ("asr_theta_to_w_k", _I, [_P, _L, _I, _I, _I, _P, _F, _P, _L, _P]),
+    ("asr_conv_forward_k", _I, [_I, _I, _P, _P, _P, _P, _P, _F, _I, _I, _I, _I, _P]),
+    ("asr_conv_backward_workspace_bytes_k", _S, [_I, _I, _I, _I, _I]),
+    ("asr_conv_backward_k", _I, [_I, _I, _P, _P, _P, _P, _P, _L, _F, _F, _I, _I, _I, _I, _P, _P, _P, _P, _P, _S, _P]),
     ("asr_wpack_elems", _L, [_I]),
     ("asr_theta_to_w", _I, [_P, _L, _I, _I, _P, _F, _P, _L, _I, _P]),
     ("asr_conv_forward", _I, [_I, _P, _P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P]),

@@ -81,7 +81,9 @@ int conv_f32(int fmode, const void* xin, void* out, uint8_t* mask, const float* 
 int make_dz(int fmode, const void* dy, const uint8_t* mask, const void* relu_src, float h, int N, int H, int W, int C,
             int src_bf16, float* dz, hipStream_t s);
 int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, int Ci, int Co, float* slabs,
-              int* nslabs, hipStream_t s);
+              int* nslabs, hipStream_t s, int K = 3);
+int conv_f32_k(int fmode, int K, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
+               float two_gamma, const float* dy, int N, int H, int W, int C, hipStream_t s, const float* extra);
 int wgrad_f32_chunks(int N, int H);
 // asr_stem_head.hip
 bool stem_supported(int Cin, int H, int W, int C);
@@ -114,9 +116,9 @@ struct BwdWs {
   size_t dz, slabs, red, g, total;
 };
 
-static BwdWs bwd_ws_layout(int N, int H, int W, int C, int dtype, int stages = 1) {
+static BwdWs bwd_ws_layout(int N, int H, int W, int C, int dtype, int stages = 1, int K = 3) {
   BwdWs b{};
-  const long E = 9L * C * C;
+  const long E = (long)K * K * C * C;
   const long P = (long)N * H * W * C;
   const int nsl = kMaxSlabsApi * stages;
   size_t off = 0;
@@ -795,6 +797,55 @@ int asr_rk2_stack_backward(const void* dyL, const void* xs, const void* xmids, l
     int32_t* tm = (int32_t*)(base + Lw.tdst);
     ASR_TRY(theta_dst_pair(theta_dst, n_theta, C, tm, s));
     ASR_TRY(project_layers(grp, gst, reduce_groups(Lw.grid), ES - C, C, tm, n_theta, L, dparams, n_theta + C, s));
+  }
+  return ASR_OK;
+}
+
+size_t asr_conv_backward_workspace_bytes_k(int N, int H, int W, int C, int kernel_size) {
+  if (check_shape(N, H, W, C) != ASR_OK || kernel_size < 1 || !(kernel_size & 1)) return 0;
+  return bwd_ws_layout(N, H, W, C, ASR_F32, 1, kernel_size).total;
+}
+
+// Conv2DAntisymmetric(kernel_size != 3) (…Conv2DAntisymmetric.py:60-68, 109-145, 163-170): the
+// same operator family on a K x K kernel, fp32 (the reference's precision) on the VALU kernels;
+// K = 3 is asr_conv_forward / asr_conv_backward.
+int asr_conv_forward_k(int mode, int kernel_size, const float* x, float* y, uint8_t* mask, const float* w,
+                       const float* bias, float h, int N, int H, int W, int C, asr_stream_t stream) {
+  ASR_TRY(check_shape(N, H, W, C));
+  if (!x || !y || !w) return fail(ASR_E_ARG, "asr_conv_forward_k: null pointer");
+  if (mode != ASR_MODE_EULER && mode != ASR_MODE_CONV) return fail(ASR_E_ARG, "asr_conv_forward_k: bad mode %d", mode);
+  if (kernel_size < 1 || kernel_size > 15 || !(kernel_size & 1))
+    return fail(ASR_E_ARG, "asr_conv_forward_k: kernel_size %d (odd, 1..15)", kernel_size);
+  return conv_f32_k(mode == ASR_MODE_EULER ? F_EULER : F_CONV, kernel_size, x, y, mask, w, bias, h, 0.f, nullptr, N, H, W,
+                    C, (hipStream_t)stream, nullptr);
+}
+
+int asr_conv_backward_k(int mode, int kernel_size, const float* dy, const float* x, const uint8_t* mask,
+                        const float* w, const int32_t* theta_dst, long n_theta, float h, float gamma, int N, int H,
+                        int W, int C, float* dx, float* dtheta, float* dbias, float* dw, void* ws, size_t ws_bytes,
+                        asr_stream_t stream) {
+  ASR_TRY(check_shape(N, H, W, C));
+  if (mode != ASR_MODE_EULER && mode != ASR_MODE_CONV) return fail(ASR_E_ARG, "asr_conv_backward_k: bad mode %d", mode);
+  if (kernel_size < 1 || kernel_size > 15 || !(kernel_size & 1))
+    return fail(ASR_E_ARG, "asr_conv_backward_k: kernel_size %d (odd, 1..15)", kernel_size);
+  if (!dy || !w || (mode == ASR_MODE_EULER && !mask)) return fail(ASR_E_ARG, "asr_conv_backward_k: null pointer");
+  if ((dtheta || dbias || dw) && !x) return fail(ASR_E_ARG, "asr_conv_backward_k: x needed for weight gradients");
+  if (dtheta && !theta_dst) return fail(ASR_E_ARG, "asr_conv_backward_k: theta_dst needed for dtheta");
+  const BwdWs Lw = bwd_ws_layout(N, H, W, C, ASR_F32, 1, kernel_size);
+  if (!ws || ws_bytes < Lw.total) return fail(ASR_E_WORKSPACE, "asr_conv_backward_k: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  unsigned char* base = (unsigned char*)ws;
+  float* dz = (float*)(base + Lw.dz);
+  float* slabs = (float*)(base + Lw.slabs);
+  const bool euler = mode == ASR_MODE_EULER;
+  ASR_TRY(make_dz(euler ? F_EULER : F_CONV, dy, mask, nullptr, h, N, H, W, C, 0, dz, s));
+  if (dx) ASR_TRY(conv_f32_k(euler ? B_EULER : B_CONV, kernel_size, dz, dx, nullptr, w, nullptr, h, 2.f * gamma, dy, N, H,
+                             W, C, s, nullptr));
+  if (dtheta || dbias || dw) {
+    int nsl = 0;
+    ASR_TRY(wgrad_f32(x, 0, dz, N, H, W, C, C, slabs, &nsl, s, kernel_size));
+    ASR_TRY(reduce_and_project(slabs, nsl, (long)kernel_size * kernel_size * C * C, C, dtheta ? theta_dst : nullptr,
+                               n_theta, dtheta, dbias, dw, (float*)(base + Lw.red), s));
   }
   return ASR_OK;
 }

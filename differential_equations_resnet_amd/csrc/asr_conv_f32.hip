@@ -17,13 +17,14 @@ enum { F_EULER = 0, F_CONV = 1, F_RELU = 2, B_EULER = 3, B_CONV = 4 };
 // One wave = (n, y, 16-pixel tile, 16-channel tile).  Lane (g = lane>>4,
 // lx = lane&15) computes pixel 16*pt+lx, channels 16*ot+4g .. +3 (the MFMA D
 // fragment map).  Relu mask: bit (pixel*C + o) (asr.h), set with atomicOr on
-// a zeroed buffer because C need not be a multiple of 8 here.
+// a zeroed buffer because C need not be a multiple of 8 here.  K x K kernel
+// (odd K, SAME: pad K/2), HWIO weights [K][K][Ci][Co].
 template <typename Tin, typename Tout, int MODE>
 __global__ __launch_bounds__(256) void k_conv_f32(const Tin* __restrict__ xin, Tout* __restrict__ out,
                                                   uint32_t* __restrict__ mask, const float* __restrict__ w,
                                                   const float* __restrict__ bias, float h, float two_gamma,
                                                   const float* __restrict__ dy, const float* __restrict__ extra,
-                                                  int N, int H, int W, int Ci, int Co) {
+                                                  int N, int H, int W, int Ci, int Co, int K) {
   const int PT = (W + 15) / 16, OT = (Co + 15) / 16;
   const long tasks = (long)N * H * PT * OT;
   const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -39,8 +40,8 @@ __global__ __launch_bounds__(256) void k_conv_f32(const Tin* __restrict__ xin, T
   const int o0 = 16 * ot + 4 * g;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   if (px < W) {
-    for (int tap = 0; tap < 9; ++tap) {
-      const int gy = y + tap / 3 - 1, gx = px + tap % 3 - 1;
+    for (int tap = 0; tap < K * K; ++tap) {
+      const int gy = y + tap / K - K / 2, gx = px + tap % K - K / 2;
       if (gy < 0 || gy >= H || gx < 0 || gx >= W) continue;
       const Tin* xp = xin + (((long)n * H + gy) * W + gx) * Ci;
       const float* wp = w + (long)tap * Ci * Co;
@@ -114,14 +115,14 @@ __global__ void k_make_dz(const T* __restrict__ dy, const uint8_t* __restrict__ 
 template <typename Tx>
 __global__ __launch_bounds__(256) void k_wgrad_f32(const Tx* __restrict__ x, const float* __restrict__ dz, int N,
                                                    int H, int W, int Ci, int Co, int rows_per_chunk,
-                                                   float* __restrict__ slabs) {
-  const long E = 9L * Ci * Co;
+                                                   float* __restrict__ slabs, int K) {
+  const long E = (long)K * K * Ci * Co;
   const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
   if (e >= E) return;
   const int o = (int)(e % Co);
   const int i = (int)((e / Co) % Ci);
   const int tap = (int)(e / ((long)Ci * Co));
-  const int sy = tap / 3 - 1, sx = tap % 3 - 1;
+  const int sy = tap / K - K / 2, sx = tap % K - K / 2;
   const long R = (long)N * H;
   const long r0 = (long)blockIdx.y * rows_per_chunk, r1 = min(R, r0 + rows_per_chunk);
   float acc = 0.f;
@@ -412,7 +413,7 @@ static int launch_wgrad32(const float* x, const float* dz, int N, int H, float* 
 template <typename Tin, typename Tout, int MODE>
 static int launch_conv_f32(const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
                            float two_gamma, const float* dy, const float* extra, int N, int H, int W, int Ci, int Co,
-                           hipStream_t s) {
+                           hipStream_t s, int K = 3) {
   const long tasks = (long)N * H * ((W + 15) / 16) * ((Co + 15) / 16);
   const long blocks = (tasks + 3) / 4;
   if (blocks > 0x7fffffffL) return fail(ASR_E_ARG, "conv f32: problem too large");
@@ -421,7 +422,7 @@ static int launch_conv_f32(const void* xin, void* out, uint8_t* mask, const floa
     ASR_TRY(hip_check(hipMemsetAsync(mask, 0, bytes, s), "hipMemsetAsync(mask)"));
   }
   hipLaunchKernelGGL((k_conv_f32<Tin, Tout, MODE>), dim3((unsigned)blocks), dim3(256), 0, s, (const Tin*)xin,
-                     (Tout*)out, (uint32_t*)mask, w, bias, h, two_gamma, dy, extra, N, H, W, Ci, Co);
+                     (Tout*)out, (uint32_t*)mask, w, bias, h, two_gamma, dy, extra, N, H, W, Ci, Co, K);
   ASR_LAUNCH_CHECK("k_conv_f32");
   return ASR_OK;
 }
@@ -454,6 +455,24 @@ int conv_f32(int fmode, const void* xin, void* out, uint8_t* mask, const float* 
   return fail(ASR_E_ARG, "conv f32: bad mode");
 }
 
+// K x K (odd K != 3: Conv2DAntisymmetric(kernel_size), …Conv2DAntisymmetric.py:60-68, 109-145) on the
+// fp32 VALU kernel, same modes as conv_f32
+int conv_f32_k(int fmode, int K, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
+               float two_gamma, const float* dy, int N, int H, int W, int C, hipStream_t s, const float* extra) {
+  if (K == 3) return conv_f32(fmode, xin, out, mask, w, bias, h, two_gamma, dy, N, H, W, C, C, 0, s, extra);
+  switch (fmode) {
+    case F_EULER:
+      return launch_conv_f32<float, float, F_EULER>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, W, C, C, s, K);
+    case F_CONV:
+      return launch_conv_f32<float, float, F_CONV>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, W, C, C, s, K);
+    case B_EULER:
+      return launch_conv_f32<float, float, B_EULER>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, W, C, C, s, K);
+    case B_CONV:
+      return launch_conv_f32<float, float, B_CONV>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, W, C, C, s, K);
+  }
+  return fail(ASR_E_ARG, "conv f32 (k=%d): bad mode", K);
+}
+
 int make_dz(int fmode, const void* dy, const uint8_t* mask, const void* relu_src, float h, int N, int H, int W, int C,
             int src_bf16, float* dz, hipStream_t s) {
   const long P = (long)N * H * W * C;
@@ -477,8 +496,8 @@ int wgrad_f32_chunks(int N, int H) {
 }
 
 int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, int Ci, int Co, float* slabs,
-              int* nslabs, hipStream_t s) {
-  if (!x_bf16 && conv32_supported(W, Ci, Co)) {  // the network's blocks: fp32 MFMA, db included
+              int* nslabs, hipStream_t s, int K) {
+  if (!x_bf16 && K == 3 && conv32_supported(W, Ci, Co)) {  // the network's blocks: fp32 MFMA, db included
     switch (Ci) {
       case 16: return launch_wgrad32<16>((const float*)x, dz, N, H, slabs, nslabs, s);
       case 32: return launch_wgrad32<32>((const float*)x, dz, N, H, slabs, nslabs, s);
@@ -489,12 +508,12 @@ int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, i
   const int chunks = wgrad_f32_chunks(N, H);
   const int rpc = (int)((R + chunks - 1) / chunks);
   const int nch = (int)((R + rpc - 1) / rpc);
-  const long E = 9L * Ci * Co;
+  const long E = (long)K * K * Ci * Co;
   dim3 grid((unsigned)((E + 255) / 256), nch);
   if (x_bf16)
-    hipLaunchKernelGGL(k_wgrad_f32<bf16>, grid, dim3(256), 0, s, (const bf16*)x, dz, N, H, W, Ci, Co, rpc, slabs);
+    hipLaunchKernelGGL(k_wgrad_f32<bf16>, grid, dim3(256), 0, s, (const bf16*)x, dz, N, H, W, Ci, Co, rpc, slabs, K);
   else
-    hipLaunchKernelGGL(k_wgrad_f32<float>, grid, dim3(256), 0, s, (const float*)x, dz, N, H, W, Ci, Co, rpc, slabs);
+    hipLaunchKernelGGL(k_wgrad_f32<float>, grid, dim3(256), 0, s, (const float*)x, dz, N, H, W, Ci, Co, rpc, slabs, K);
   ASR_LAUNCH_CHECK("k_wgrad_f32");
   if (Co > 1024) return fail(ASR_E_UNSUPPORTED, "db: C > 1024");
   hipLaunchKernelGGL(k_db_f32, dim3(nch), dim3(((Co + 63) / 64) * 64), 0, s, dz, R, W, Co, rpc, E, slabs);

@@ -56,9 +56,8 @@ int cu_count() {
 // ---------------------------------------------------------------------------
 
 // Free positions of the general layer's diagonal block in variable-creation
-// order (…Conv2DAntisymmetric.py:231-264), for kernel_size 3.
-static void general_free_positions(int antisymmetric, std::vector<std::pair<int, int>>& out) {
-  const int k = 3;
+// order (…Conv2DAntisymmetric.py:231-264), for an odd kernel_size k.
+static void general_free_positions(int k, int antisymmetric, std::vector<std::pair<int, int>>& out) {
   for (int i = 0; i < k; ++i)
     for (int j = i; j < k; ++j) {
       if (j > i || (j == i && i <= k / 2 - 1))
@@ -68,24 +67,35 @@ static void general_free_positions(int antisymmetric, std::vector<std::pair<int,
     }
 }
 
-long theta_count(int C, int kind, int antisymmetric) {
-  if (C < 1) return -1;
+static bool kernel_size_ok(int kind, int k) {
+  return kind == ASR_PARAM_3BY3 ? k == 3 : (k >= 1 && k <= 15 && (k & 1));
+}
+
+long theta_count_k(int C, int k, int kind, int antisymmetric) {
+  if (C < 1 || !kernel_size_ok(kind, k)) return -1;
+  const long kk = (long)k * k;
   if (kind == ASR_PARAM_3BY3) return 4L * C + 9L * C * (C - 1) / 2;
   if (kind == ASR_PARAM_GENERAL) {
     std::vector<std::pair<int, int>> fp;
-    general_free_positions(antisymmetric, fp);
-    return (long)fp.size() * C + 9L * C * (C - 1) / 2;
+    general_free_positions(k, antisymmetric, fp);
+    return (long)fp.size() * C + kk * C * (C - 1) / 2;
   }
-  if (kind == ASR_PARAM_REGULAR) return 9L * C * C;
+  if (kind == ASR_PARAM_REGULAR) return kk * C * C;
   return -1;
 }
+long theta_count(int C, int kind, int antisymmetric) { return theta_count_k(C, 3, kind, antisymmetric); }
 
-int param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta_dst) {
+// The element map of a k x k layer: w_src[e] (e = ((ky*k + kx)*C + i)*C + o,
+// HWIO) = (theta index << 1 | negated), -1 for the gamma centre; theta_dst its
+// transpose (<= 2 entries per theta).
+int param_map_k(int C, int k, int kind, int antisymmetric, int32_t* w_src, int32_t* theta_dst) {
   if (C < 1 || !w_src) return fail(ASR_E_ARG, "asr_param_map: bad arguments");
   if (kind == ASR_PARAM_3BY3 && !antisymmetric)
     return fail(ASR_E_ARG, "asr_param_map: the 3by3 layer is always antisymmetric");
-  const long E = 9L * C * C;
-  auto idx = [C](int ky, int kx, int i, int o) { return ((long)(ky * 3 + kx) * C + i) * C + o; };
+  if (!kernel_size_ok(kind, k))
+    return fail(ASR_E_ARG, "asr_param_map: kernel_size %d (3 for the 3by3 layer, odd 1..15 otherwise)", k);
+  const long E = (long)k * k * C * C;
+  auto idx = [C, k](int ky, int kx, int i, int o) { return ((long)(ky * k + kx) * C + i) * C + o; };
   for (long e = 0; e < E; ++e) w_src[e] = -1;  // gamma unless set below
   if (kind == ASR_PARAM_3BY3) {
     // diagonal: a (0,0) b (0,1) c (0,2) d (1,0); mirrors negated (…3By3.py:261-275)
@@ -111,14 +121,14 @@ int param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta
     }
   } else if (kind == ASR_PARAM_GENERAL) {
     std::vector<std::pair<int, int>> fp;
-    general_free_positions(antisymmetric, fp);
+    general_free_positions(k, antisymmetric, fp);
     long off = 0;
     for (int o = 0; o < C; ++o) {
       for (size_t n = 0; n < fp.size(); ++n) {
         const int i = fp[n].first, j = fp[n].second;
         const long t = off + (long)n;
         w_src[idx(i, j, o, o)] = (int32_t)(t << 1);
-        const int mi = 2 - i, mj = 2 - j;
+        const int mi = k - 1 - i, mj = k - 1 - j;
         if (mi != i || mj != j) w_src[idx(mi, mj, o, o)] = (int32_t)((t << 1) | (antisymmetric ? 1 : 0));
       }
       off += (long)fp.size();
@@ -126,14 +136,14 @@ int param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta
       if (nind > 0) {
         for (int i = o + 1; i < C; ++i) {
           const int m = i - o - 1;
-          for (int ky = 0; ky < 3; ++ky)
-            for (int kx = 0; kx < 3; ++kx) {
-              const long j = off + (long)(ky * 3 + kx) * nind + m;  // [k,k,nind,1]
+          for (int ky = 0; ky < k; ++ky)
+            for (int kx = 0; kx < k; ++kx) {
+              const long j = off + (long)(ky * k + kx) * nind + m;  // [k,k,nind,1]
               w_src[idx(ky, kx, i, o)] = (int32_t)(j << 1);
-              w_src[idx(2 - ky, 2 - kx, o, i)] = (int32_t)((j << 1) | 1);
+              w_src[idx(k - 1 - ky, k - 1 - kx, o, i)] = (int32_t)((j << 1) | 1);  // -J K J (:139)
             }
         }
-        off += 9L * nind;
+        off += (long)k * k * nind;
       }
     }
   } else if (kind == ASR_PARAM_REGULAR) {
@@ -142,7 +152,7 @@ int param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta
     return fail(ASR_E_ARG, "asr_param_map: unknown kind %d", kind);
   }
   if (theta_dst) {
-    const long nt = theta_count(C, kind, antisymmetric);
+    const long nt = theta_count_k(C, k, kind, antisymmetric);
     for (long j = 0; j < 2 * nt; ++j) theta_dst[j] = -1;
     for (long e = 0; e < E; ++e) {
       const int32_t v = w_src[e];
@@ -160,6 +170,10 @@ int param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta
   return ASR_OK;
 }
 
+int param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta_dst) {
+  return param_map_k(C, 3, kind, antisymmetric, w_src, theta_dst);
+}
+
 int param_is_antisymmetric(int kind, int antisymmetric) {
   if (kind == ASR_PARAM_3BY3) return 1;
   if (kind == ASR_PARAM_GENERAL) return antisymmetric ? 1 : 0;
@@ -167,21 +181,22 @@ int param_is_antisymmetric(int kind, int antisymmetric) {
   return fail(ASR_E_ARG, "asr_param_is_antisymmetric: unknown kind %d", kind);
 }
 
-// W_bwd[ky,kx,i,o] = -W[2-ky,2-kx,o,i]: conv(dz, W_bwd) = -A^T dz, so the
+// W_bwd[ky,kx,i,o] = -W[k-1-ky,k-1-kx,o,i]: conv(dz, W_bwd) = -A^T dz, so the
 // backward's dx = dy - conv(dz, W_bwd) (+ 2*0*dz) is dy + A^T dz for any W.
-int param_map_transpose(int C, const int32_t* w_src, int32_t* w_bwd) {
-  if (C < 1 || !w_src || !w_bwd) return fail(ASR_E_ARG, "asr_param_map_transpose: bad arguments");
-  auto idx = [C](int ky, int kx, int i, int o) { return ((long)(ky * 3 + kx) * C + i) * C + o; };
-  for (int ky = 0; ky < 3; ++ky)
-    for (int kx = 0; kx < 3; ++kx)
+int param_map_transpose_k(int C, int k, const int32_t* w_src, int32_t* w_bwd) {
+  if (C < 1 || k < 1 || !w_src || !w_bwd) return fail(ASR_E_ARG, "asr_param_map_transpose: bad arguments");
+  auto idx = [C, k](int ky, int kx, int i, int o) { return ((long)(ky * k + kx) * C + i) * C + o; };
+  for (int ky = 0; ky < k; ++ky)
+    for (int kx = 0; kx < k; ++kx)
       for (int i = 0; i < C; ++i)
         for (int o = 0; o < C; ++o) {
-          const int32_t v = w_src[idx(2 - ky, 2 - kx, o, i)];
+          const int32_t v = w_src[idx(k - 1 - ky, k - 1 - kx, o, i)];
           if (v < 0) return fail(ASR_E_ARG, "asr_param_map_transpose: map has constant (gamma) entries");
           w_bwd[idx(ky, kx, i, o)] = v ^ 1;
         }
   return ASR_OK;
 }
+int param_map_transpose(int C, const int32_t* w_src, int32_t* w_bwd) { return param_map_transpose_k(C, 3, w_src, w_bwd); }
 
 // ---------------------------------------------------------------------------
 // device: materialisation
@@ -194,11 +209,10 @@ __device__ __forceinline__ float w_value(const float* theta, const int32_t* w_sr
   return (v & 1) ? -t : t;
 }
 
-// plain HWIO float: one thread per element, blockIdx.y = layer
-__global__ void k_theta_to_w_hwio(const float* __restrict__ theta, long theta_stride, int C,
+// plain HWIO float (E = k*k*C*C elements): one thread per element, blockIdx.y = layer
+__global__ void k_theta_to_w_hwio(const float* __restrict__ theta, long theta_stride, long E,
                                   const int32_t* __restrict__ w_src, float gamma, float* __restrict__ w,
                                   long w_stride) {
-  const long E = 9L * C * C;
   const int l = blockIdx.y;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < E; e += (long)gridDim.x * blockDim.x)
     w[l * w_stride + e] = w_value(theta + l * theta_stride, w_src, e, gamma);
@@ -305,6 +319,15 @@ int asr_abi_version(void) { return 6; }
 int asr_device_cu_count(void) { return cu_count(); }
 
 long asr_theta_count(int C, int kind, int antisymmetric) { return theta_count(C, kind, antisymmetric); }
+long asr_theta_count_k(int C, int kernel_size, int kind, int antisymmetric) {
+  return theta_count_k(C, kernel_size, kind, antisymmetric);
+}
+int asr_param_map_k(int C, int kernel_size, int kind, int antisymmetric, int32_t* w_src, int32_t* theta_dst) {
+  return param_map_k(C, kernel_size, kind, antisymmetric, w_src, theta_dst);
+}
+int asr_param_map_transpose_k(int C, int kernel_size, const int32_t* w_src, int32_t* w_src_bwd) {
+  return param_map_transpose_k(C, kernel_size, w_src, w_src_bwd);
+}
 
 int asr_param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta_dst) {
   return param_map(C, kind, antisymmetric, w_src, theta_dst);
@@ -327,6 +350,19 @@ long asr_wpack_elems(int C) {
   return (long)(C / 16) * ((9 * C + 31) / 32) * 64 * 8;
 }
 
+int asr_theta_to_w_k(const float* theta, long theta_stride, int L, int C, int kernel_size, const int32_t* w_src,
+                     float gamma, float* w_out, long w_stride, asr_stream_t stream) {
+  if (!theta || !w_src || !w_out || L < 1 || C < 1 || L > 65535 || kernel_size < 1)
+    return fail(ASR_E_ARG, "asr_theta_to_w_k: bad arguments");
+  const long E = (long)kernel_size * kernel_size * C * C;
+  if (w_stride < E) return fail(ASR_E_ARG, "asr_theta_to_w_k: w_stride too small");
+  dim3 grid((unsigned)std::min<long>((E + 255) / 256, 1024), L);
+  hipLaunchKernelGGL(k_theta_to_w_hwio, grid, dim3(256), 0, (hipStream_t)stream, theta, theta_stride, E, w_src, gamma,
+                     w_out, w_stride);
+  ASR_LAUNCH_CHECK("k_theta_to_w_hwio");
+  return ASR_OK;
+}
+
 int asr_theta_to_w(const float* theta, long theta_stride, int L, int C, const int32_t* w_src, float gamma,
                    void* w_out, long w_stride, int dtype, asr_stream_t stream) {
   if (!theta || !w_src || !w_out || L < 1 || C < 1 || L > 65535)
@@ -336,7 +372,7 @@ int asr_theta_to_w(const float* theta, long theta_stride, int L, int C, const in
     const long E = 9L * C * C;
     if (w_stride < E) return fail(ASR_E_ARG, "asr_theta_to_w: w_stride too small");
     dim3 grid((unsigned)std::min<long>((E + 255) / 256, 1024), L);
-    hipLaunchKernelGGL(k_theta_to_w_hwio, grid, dim3(256), 0, s, theta, theta_stride, C, w_src, gamma,
+    hipLaunchKernelGGL(k_theta_to_w_hwio, grid, dim3(256), 0, s, theta, theta_stride, E, w_src, gamma,
                        (float*)w_out, w_stride);
     ASR_LAUNCH_CHECK("k_theta_to_w_hwio");
   } else if (dtype == ASR_BF16) {

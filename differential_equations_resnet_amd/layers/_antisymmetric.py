@@ -67,18 +67,20 @@ class AntisymmetricConvBase(Layer):
     def theta_flat(self) -> np.ndarray:
         return np.concatenate([v.value.ravel() for v in self.theta_vars]).astype(np.float32)
 
-    def _check_native(self):
-        if self.kernel_size != 3:
-            raise _lib.AsrUnsupported(f"{self.name}: only 3x3 antisymmetric kernels have native kernels "
-                                      f"(kernel_size={self.kernel_size})")
+    def _check_native(self, dtype=None):
+        k = self.kernel_size
+        if k < 1 or k % 2 == 0 or k > 15:
+            raise _lib.AsrUnsupported(f"{self.name}: kernel_size {k} (odd 1..15 have native kernels)")
+        if k != 3 and dtype is not None and str(dtype) != "torch.float32":
+            raise _lib.AsrUnsupported(f"{self.name}: kernel_size {k} runs the fp32 k x k kernels (input {dtype})")
 
     def param_map(self):
         from .. import runtime
         self._check_native()
-        return runtime.param_map(self.num_channels, self.param_kind, self.antisymmetric)
+        return runtime.param_map(self.num_channels, self.param_kind, self.antisymmetric, self.kernel_size)
 
     def get_kernel(self) -> np.ndarray:
-        """The assembled kernel [3,3,C,C] (HWIO).  Reads theta through the
+        """The assembled kernel [k,k,C,C] (HWIO).  Reads theta through the
         native element map (asr_param_map, the same map the device
         materialisation consumes), so W here is bit-identical to the W the
         kernels run with (…3By3.py:188-199)."""
@@ -86,7 +88,8 @@ class AntisymmetricConvBase(Layer):
         th = self.theta_flat()
         src = pm.w_src
         W = np.where(src >= 0, th[np.maximum(src, 0) >> 1] * np.where(src & 1, -1.0, 1.0), self.gamma)
-        return W.astype(np.float32).reshape(3, 3, self.num_channels, self.num_channels)
+        k = self.kernel_size
+        return W.astype(np.float32).reshape(k, k, self.num_channels, self.num_channels)
 
     def get_bias(self) -> np.ndarray:
         if self.bias is None:
@@ -140,7 +143,7 @@ class AntisymmetricConvBase(Layer):
             raise _lib.AsrUnsupported(f"{self.name}: strides {self.strides} (native kernels are stride 1)")
         if x.dim() != 4 or x.shape[-1] != self.num_channels:
             raise ValueError(f"{self.name}: expected NHWC input with {self.num_channels} channels, got {tuple(x.shape)}")
-        self._check_native()
+        self._check_native(x.dtype)
         th, b = self.device_variables(x.device)
         return _AntisymConv2D.apply(x, th, b, self)
 
@@ -161,7 +164,8 @@ def _make_fn():
             C = layer.num_channels
             x = x.contiguous()
             w = runtime.theta_to_w(theta.detach(), C, pm, layer.gamma, dt)
-            y = runtime.conv_forward(runtime.ASR_MODE_CONV, x, w, None if bias is None else bias.detach(), 1.0)
+            y = runtime.conv_forward(runtime.ASR_MODE_CONV, x, w, None if bias is None else bias.detach(), 1.0,
+                                     k=pm.k)
             ctx.layer = layer
             ctx.has_bias = bias is not None
             ctx.save_for_backward(x, theta)

@@ -9,8 +9,9 @@ input_kernels_for_output_kernel_{o} [k,k,C-o-1,1] (:123-128); bias [C] last
 (:150-156).  Dependent off-diagonal blocks are -J K J (:139).  get_config
 omits gamma like the reference (:181-192).
 
-Native kernels exist for kernel_size 3; other sizes build (weights, config)
-but raise AsrUnsupported when executed."""
+Every odd kernel_size (1..15) executes natively: 3 on the fp32 / bf16 kernels
+of the network path, other sizes on the fp32 k x k kernels
+(asr_conv_forward_k / asr_conv_backward_k, the reference's precision)."""
 from __future__ import annotations
 
 from .. import _lib

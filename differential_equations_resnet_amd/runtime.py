@@ -74,10 +74,10 @@ def torch_dtype(code: int):
     return torch.float32 if code == ASR_F32 else torch.bfloat16
 
 
-def theta_count(C: int, kind: int = ASR_PARAM_3BY3, antisymmetric: bool = True) -> int:
-    n = _lib.load().asr_theta_count(C, kind, int(antisymmetric))
+def theta_count(C: int, kind: int = ASR_PARAM_3BY3, antisymmetric: bool = True, k: int = 3) -> int:
+    n = _lib.load().asr_theta_count_k(C, k, kind, int(antisymmetric))
     if n < 0:
-        raise ValueError(f"bad theta_count arguments C={C} kind={kind}")
+        raise ValueError(f"bad theta_count arguments C={C} kind={kind} kernel_size={k}")
     return int(n)
 
 
@@ -86,9 +86,10 @@ class ParamMap:
     C: int
     kind: int
     antisymmetric: bool
-    w_src: np.ndarray      # int32 [9*C*C]
+    w_src: np.ndarray      # int32 [k*k*C*C]
     theta_dst: np.ndarray  # int32 [2*n_theta]
     _dev: dict
+    k: int = 3             # kernel_size
 
     @property
     def operator_antisymmetric(self) -> bool:
@@ -100,7 +101,7 @@ class ParamMap:
         key = ("bwd", str(device))
         if key not in self._dev:
             wb = np.empty_like(self.w_src)
-            _lib.call("asr_param_map_transpose", self.C, self.w_src.ctypes.data, wb.ctypes.data)
+            _lib.call("asr_param_map_transpose_k", self.C, self.k, self.w_src.ctypes.data, wb.ctypes.data)
             self._dev[key] = torch.from_numpy(wb).to(device)
         return self._dev[key]
 
@@ -118,15 +119,15 @@ class ParamMap:
 _MAPS: dict = {}
 
 
-def param_map(C: int, kind: int = ASR_PARAM_3BY3, antisymmetric: bool = True) -> ParamMap:
-    """Element map of W(theta) and its pull-back (asr_param_map, host)."""
-    key = (C, kind, bool(antisymmetric))
+def param_map(C: int, kind: int = ASR_PARAM_3BY3, antisymmetric: bool = True, k: int = 3) -> ParamMap:
+    """Element map of W(theta) and its pull-back (asr_param_map_k, host)."""
+    key = (C, kind, bool(antisymmetric), int(k))
     if key not in _MAPS:
-        nt = theta_count(C, kind, antisymmetric)
-        w_src = np.empty(9 * C * C, dtype=np.int32)
+        nt = theta_count(C, kind, antisymmetric, k)
+        w_src = np.empty(k * k * C * C, dtype=np.int32)
         dst = np.empty(2 * nt, dtype=np.int32)
-        _lib.call("asr_param_map", C, kind, int(antisymmetric), w_src.ctypes.data, dst.ctypes.data)
-        _MAPS[key] = ParamMap(C, kind, bool(antisymmetric), w_src, dst, {})
+        _lib.call("asr_param_map_k", C, k, kind, int(antisymmetric), w_src.ctypes.data, dst.ctypes.data)
+        _MAPS[key] = ParamMap(C, kind, bool(antisymmetric), w_src, dst, {}, int(k))
     return _MAPS[key]
 
 
@@ -140,10 +141,18 @@ def wpack_elems(C: int) -> int:
 def theta_to_w(theta: torch.Tensor, C: int, pmap: ParamMap, gamma: float, dtype: int, layers: int = 1,
                theta_stride: int | None = None) -> torch.Tensor:
     """Materialise W for `layers` layers whose thetas are theta_stride floats
-    apart.  bf16 -> MFMA-packed layout, f32 -> HWIO [layers, 3, 3, C, C]."""
+    apart.  bf16 -> MFMA-packed layout, f32 -> HWIO [layers, k, k, C, C]."""
     dev = theta.device
     w_src, _ = pmap.device(dev)
     stride = pmap.n_theta if theta_stride is None else theta_stride
+    if pmap.k != 3:  # Conv2DAntisymmetric(kernel_size != 3): fp32 HWIO only
+        if dtype != ASR_F32:
+            raise _lib.AsrUnsupported(f"kernel_size {pmap.k}: the k x k kernels are fp32")
+        per = pmap.k * pmap.k * C * C
+        out = torch.empty(layers * per, dtype=torch.float32, device=dev)
+        _lib.call("asr_theta_to_w_k", _p(theta), stride, layers, C, pmap.k, _p(w_src), float(gamma), _p(out), per,
+                  _stream())
+        return out.view(layers, pmap.k, pmap.k, C, C)
     if dtype == ASR_BF16:
         per = wpack_elems(C)
         out = torch.empty(layers * per, dtype=torch.bfloat16, device=dev)
@@ -161,6 +170,13 @@ def theta_to_w_transposed(theta: torch.Tensor, C: int, pmap: ParamMap, dtype: in
     (pass it to conv_backward with gamma 0)."""
     dev = theta.device
     wb = pmap.w_src_bwd(dev)
+    if pmap.k != 3:
+        if dtype != ASR_F32:
+            raise _lib.AsrUnsupported(f"kernel_size {pmap.k}: the k x k kernels are fp32")
+        per = pmap.k * pmap.k * C * C
+        out = torch.empty(per, dtype=torch.float32, device=dev)
+        _lib.call("asr_theta_to_w_k", _p(theta), pmap.n_theta, 1, C, pmap.k, _p(wb), 0.0, _p(out), per, _stream())
+        return out.view(1, pmap.k, pmap.k, C, C)
     if dtype == ASR_BF16:
         per = wpack_elems(C)
         out = torch.empty(per, dtype=torch.bfloat16, device=dev)
@@ -193,12 +209,18 @@ def batch_metrics(probs, targets, loss, accum):
 
 
 def conv_forward(mode: int, x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, h: float = 1.0,
-                 mask: torch.Tensor | None = None) -> torch.Tensor:
+                 mask: torch.Tensor | None = None, k: int = 3) -> torch.Tensor:
     N, H, W, C = x.shape
     dt = dtype_code(x.dtype)
     if not x.is_contiguous():
         raise ValueError("x must be contiguous NHWC")
     y = torch.empty_like(x)
+    if k != 3:
+        if dt != ASR_F32:
+            raise _lib.AsrUnsupported(f"kernel_size {k}: the k x k kernels are fp32")
+        _lib.call("asr_conv_forward_k", mode, k, _p(x), _p(y), _p(mask), _p(w), _p(bias), float(h), N, H, W, C,
+                  _stream())
+        return y
     _lib.call("asr_conv_forward", mode, _p(x), _p(y), _p(mask), _p(w), _p(bias), float(h), N, H, W, C, dt, _stream())
     return y
 
@@ -257,13 +279,23 @@ def conv_backward(mode: int, dy: torch.Tensor, x: torch.Tensor, mask: torch.Tens
     N, H, W, C = dy.shape
     dt = dtype_code(dy.dtype)
     dev = dy.device
-    ws_bytes = int(_lib.load().asr_conv_backward_workspace_bytes(N, H, W, C, dt))
+    k = pmap.k
+    if k != 3 and dt != ASR_F32:
+        raise _lib.AsrUnsupported(f"kernel_size {k}: the k x k kernels are fp32")
+    if k != 3:
+        ws_bytes = int(_lib.load().asr_conv_backward_workspace_bytes_k(N, H, W, C, k))
+    else:
+        ws_bytes = int(_lib.load().asr_conv_backward_workspace_bytes(N, H, W, C, dt))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     dx = torch.empty_like(dy) if want_dx else None
     dth = torch.empty(pmap.n_theta, dtype=torch.float32, device=dev) if want_dtheta else None
     db = torch.empty(C, dtype=torch.float32, device=dev) if want_dbias else None
-    dw = torch.empty(3, 3, C, C, dtype=torch.float32, device=dev) if want_dw else None
+    dw = torch.empty(k, k, C, C, dtype=torch.float32, device=dev) if want_dw else None
     _, theta_dst = pmap.device(dev)
+    if k != 3:
+        _lib.call("asr_conv_backward_k", mode, k, _p(dy), _p(x), _p(mask), _p(w), _p(theta_dst), pmap.n_theta,
+                  float(h), float(gamma), N, H, W, C, _p(dx), _p(dth), _p(db), _p(dw), _p(ws), ws_bytes, _stream())
+        return dx, dth, db, dw
     _lib.call("asr_conv_backward", mode, _p(dy), _p(x), _p(mask), _p(w), _p(theta_dst), pmap.n_theta, float(h),
               float(gamma), N, H, W, C, dt, _p(dx), _p(dth), _p(db), _p(dw), _p(ws), ws_bytes, _stream())
     return dx, dth, db, dw

@@ -189,6 +189,28 @@ int asr_conv_backward(int mode, const void* dy, const void* x, const uint8_t* ma
                       asr_stream_t stream);
 
 /* ------------------------------------------------------------------------
+ * Conv2DAntisymmetric(kernel_size = k) for odd k != 3
+ * (layers/tfkeras_layer_Conv2DAntisymmetric.py:60-68, 109-145, 163-170):
+ * the same operator family on a k x k kernel (k = 3 is the functions above).
+ * fp32 (the reference's precision); W HWIO [k,k,C,C]; maps of k*k*C*C
+ * entries.  The antisymmetric kinds keep A^T = -A + 2 gamma I, so
+ * asr_conv_backward_k takes the forward W (else W_bwd of
+ * asr_param_map_transpose_k with gamma 0), as asr_conv_backward.
+ * ---------------------------------------------------------------------- */
+long asr_theta_count_k(int C, int kernel_size, int kind, int antisymmetric);
+int asr_param_map_k(int C, int kernel_size, int kind, int antisymmetric, int32_t* w_src, int32_t* theta_dst);
+int asr_param_map_transpose_k(int C, int kernel_size, const int32_t* w_src, int32_t* w_src_bwd);
+int asr_theta_to_w_k(const float* theta, long theta_stride, int L, int C, int kernel_size, const int32_t* w_src,
+                     float gamma, float* w_out, long w_stride, asr_stream_t stream);
+int asr_conv_forward_k(int mode, int kernel_size, const float* x, float* y, uint8_t* mask, const float* w,
+                       const float* bias, float h, int N, int H, int W, int C, asr_stream_t stream);
+size_t asr_conv_backward_workspace_bytes_k(int N, int H, int W, int C, int kernel_size);
+int asr_conv_backward_k(int mode, int kernel_size, const float* dy, const float* x, const uint8_t* mask,
+                        const float* w, const int32_t* theta_dst, long n_theta, float h, float gamma, int N, int H,
+                        int W, int C, float* dx, float* dtheta, float* dbias, float* dw, void* ws, size_t ws_bytes,
+                        asr_stream_t stream);
+
+/* ------------------------------------------------------------------------
  * RK2 (explicit midpoint) block — an EXTENSION, not in the reference
  * (BASELINE.json config 5; the reference integrates with forward Euler,
  * tfkeras_resnets.py:69-92).  Same W and bias in both stages:

@@ -207,3 +207,41 @@ def test_backward_projection_in_epilogue(rt, C):
     a, bb = th_a.cpu().numpy(), th_b.cpu().numpy()
     assert np.abs(a - bb).max() <= 1e-5 * np.abs(bb).max()
     np.testing.assert_allclose(db_a.cpu().numpy(), db_b.cpu().numpy(), rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("k", [5, 7])
+@pytest.mark.parametrize("anti,gamma", [(True, 0.0), (True, -0.1), (False, 0.0)])
+def test_general_k_layer_matches_oracle(rt, k, anti, gamma):
+    """Conv2DAntisymmetric(kernel_size=k) on a device tensor (fp32 k x k kernels:
+    asr_theta_to_w_k, asr_conv_forward_k, asr_conv_backward_k through the
+    layer's autograd) against the literal restatement of the reference's
+    assembly (oracle.assemble_general_literal, …Conv2DAntisymmetric.py:109-145)
+    and fp64 conv / autodiff: y, dx, dtheta, dbias (fp32 tolerances)."""
+    from differential_equations_resnet_amd.layers import Conv2DAntisymmetric
+    C, N, H, W_ = 8, 2, 11, 13
+    layer = Conv2DAntisymmetric(k, gamma=gamma, antisymmetric=anti, name=f"ca{k}")
+    layer.build((None, H, W_, C))
+    rng = np.random.default_rng(k * 10 + int(anti))
+    for v in layer.theta_vars:
+        v.assign((rng.standard_normal(v.shape) * 0.2).astype(np.float32))
+    layer.bias.assign((rng.standard_normal(C) * 0.1).astype(np.float32))
+    theta_list = [v.value.astype(np.float64) for v in layer.theta_vars]
+    Wl = O.assemble_general_literal(theta_list, C, k, gamma, anti)
+    np.testing.assert_array_equal(layer.get_kernel(), Wl.astype(np.float32))
+    x_np = rng.standard_normal((N, H, W_, C)).astype(np.float32)
+    dy_np = rng.standard_normal((N, H, W_, C)).astype(np.float32)
+    x = torch.from_numpy(x_np).cuda().requires_grad_(True)
+    y = layer.call_device(x)
+    y.backward(torch.from_numpy(dy_np).cuda())
+    th, b = layer.device_variables(x.device)
+    b_np = layer.bias.value.astype(np.float64)
+    y_want = O.conv2d_same(x_np.astype(np.float64), Wl) + b_np
+    assert_close(y.detach().cpu().numpy(), y_want, rtol=1e-5, atol=2e-5 * np.abs(y_want).max(), what="y")
+    dx_want = O.conv2d_backprop_input(dy_np.astype(np.float64), Wl, x_np.shape)
+    assert_close(x.grad.cpu().numpy(), dx_want, rtol=1e-5, atol=2e-5 * np.abs(dx_want).max(), what="dx")
+    src, sign = O.param_map(C, "general", k, anti)
+    dth_want = O.project_dW(O.conv2d_backprop_filter(x_np.astype(np.float64), dy_np.astype(np.float64), k), src, sign,
+                            th.numel())
+    assert np.abs(th.grad.cpu().numpy() - dth_want).max() <= 1e-4 * np.abs(dth_want).max()
+    db_want = dy_np.astype(np.float64).sum(axis=(0, 1, 2))
+    assert np.abs(b.grad.cpu().numpy() - db_want).max() <= 1e-4 * np.abs(db_want).max()

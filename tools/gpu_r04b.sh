@@ -6,7 +6,7 @@ set -o pipefail
 TAG=$1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/test_gpu_stack64.py tests/test_gpu_headline.py tests/test_gpu_distributed.py "tests/test_gpu_fullsize.py::test_v6_small_batch_and_batch1_predict" -m gpu -v --timeout 240 --timeout-method thread -p no:cacheprovider > gpurun_out/test_$TAG.log 2>&1; rc=$?; tail -3 gpurun_out/test_$TAG.log; [ $rc -le 1 ] || exit $rc
+timeout -k 10 900 python -u -m pytest tests/test_gpu_stack64.py tests/test_gpu_headline.py tests/test_gpu_distributed.py "tests/test_gpu_fullsize.py::test_v6_small_batch_and_batch1_predict" tests/test_gpu_kernels.py tests/test_gpu_api.py -m gpu -v --timeout 240 --timeout-method thread -p no:cacheprovider > gpurun_out/test_$TAG.log 2>&1; rc=$?; tail -3 gpurun_out/test_$TAG.log; [ $rc -le 1 ] || exit $rc
 grep -E "FAILED|ERROR" gpurun_out/test_$TAG.log | head -20
 timeout -k 10 600 python3 tools/varab.py --config c2 --arms 0,256 --rounds 6 > gpurun_out/varab_$TAG.txt 2>&1 || { echo VARAB FAILED; tail -20 gpurun_out/varab_$TAG.txt; exit 1; }
 cat gpurun_out/varab_$TAG.txt
