@@ -50,6 +50,18 @@
 #ifndef ASR_FWD3_WGS
 #define ASR_FWD3_WGS 3  // k_fwd3 workgroups per CU (grid = min(bands, WGS x CUs))
 #endif
+#ifndef ASR_BWD_PF
+#define ASR_BWD_PF 1  // k_bwd3_stack pair-local wgrad: row r+1's first fragments read during row r's second phase
+#endif
+#ifndef ASR_BWD_PFD
+#define ASR_BWD_PFD 3  // ASR_BWD_PF: fragments read ahead of their first MFMA
+#endif
+#ifndef ASR_BWD_XDG
+#define ASR_BWD_XDG 0  // k_bwd3_stack: the next band's x rows DMA'd by the dgrad waves (1: after their epilogue, 2: before their conv; 0: by the wgrad waves)
+#endif
+#ifndef ASR_BWD_HALO_DG
+#define ASR_BWD_HALO_DG 1  // k_bwd3_stack: the halo rows of the next band copied by the dgrad waves (0: wgrad waves)
+#endif
 #ifndef ASR_BWD3_DMA0
 #define ASR_BWD3_DMA0 16  // k_bwd3 wgrad waves: DMA pieces issued right after the barrier, the rest one per row (A/B: spreading them lengthened the MFMA phase as much as it saved; the stacks: all at once 16 vs 9 +0.3-0.5 %, 4 -0.7 %)
 #endif
@@ -176,6 +188,21 @@ __device__ __forceinline__ void dma_row_instr(const bf16* __restrict__ src, unsi
                                   ? (const unsigned char*)src + ((long)n * H + gy) * (W * C * 2) + seg * (PPI * C * 2)
                                   : (const unsigned char*)g_zero_page;
   dma16(base + loff, tile + ((r * TW + 1 + seg * PPI) * NQ) * 16);
+}
+
+// dma_row_instr to a tile at an LDS byte address (no generic -> LDS pointer cast: its
+// null check trips a ROCm 7.2 codegen bug in the register-tight stacked backward)
+template <int C, int W>
+__device__ __forceinline__ void dma_row_instr_at(const bf16* __restrict__ src, unsigned tile, int n, int gy0, int j,
+                                                 int H, unsigned loff) {
+  using G = Geo<C>;
+  constexpr int TW = W + 2, NQ = G::NQ, PPI = G::PPI, IPR = W / PPI;
+  const int r = (unsigned)j / IPR, seg = (unsigned)j % IPR;  // wave-uniform
+  const int gy = gy0 + r;
+  const unsigned char* base = ((unsigned)gy < (unsigned)H)
+                                  ? (const unsigned char*)src + ((long)n * H + gy) * (W * C * 2) + seg * (PPI * C * 2)
+                                  : (const unsigned char*)g_zero_page;
+  dma16_at(base + loff, tile + (unsigned)((r * TW + 1 + seg * PPI) * NQ) * 16u);
 }
 
 template <int C, int W>
@@ -2262,7 +2289,10 @@ typedef __attribute__((address_space(1))) float gf32;
 // projection forms X - X^T there).  perm(0..3) orders the tiles a wave walks
 // (its b-set first) so that every accumulator and register index is
 // compile-time: acc[a][b] / acc[4+a][b] hold tiles (perm(a), perm(b)).
-using PairSlab = PairSlabLayout;  // (asr_common.h: the layout and the projection's pair_encode)
+using PairSlab = PairSlabLayout;
+constexpr int cmin(int a, int b) { return a < b ? a : b; }
+// the pipelined pair wgrad (k_bwd3_stack, ASR_BWD_PF): the last of a row's 12 fragments MFMA group g uses
+constexpr int pf_last(int g) { return g == 0 ? 2 : g == 1 ? 3 : g == 2 ? 5 : g + 3; }  // (asr_common.h: the layout and the projection's pair_encode)
 struct PairRole {
   // one wave-uniform word (the wgrad role sits at the SGPR limit): bits 0-7 perm(0..3),
   // 8-9 t, 10 self, 11 (s1 == 2), 12-14 k4
@@ -2333,6 +2363,9 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       tab[i] = (((m >> (2 * d)) & 1u) ? 0xffffu : 0u) | (((m >> (2 * d + 1)) & 1u) ? 0xffff0000u : 0u);
     }
   }
+  // the LDS byte address of the allocation, taken here (uniform code): casting in the dgrad
+  // role's code made hipcc (ROCm 7.2) emit the cast's null check as an illegal VALU compare
+  const unsigned lds0 = lds_u32(lds);
   unsigned* late = (unsigned*)(lds + LL::TOTAL);  // a slab wait of this workgroup ran out: stop waiting
   if (tid == 0) *late = 0u;
   const int n0 = (int)((long)blockIdx.x * N / gridDim.x), n1 = (int)((long)(blockIdx.x + 1) * N / gridDim.x);
@@ -2412,6 +2445,18 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
 #pragma unroll
         for (int r = 0; r < (RK2 ? BR : 1); ++r)
           exv[r] = *(const u32x4*)((const unsigned char*)(eb + (long)min(r, rows - 1) * W * C) + ldx);
+      }
+      if (ASR_BWD_XDG == 2 && !RK2 && it + 1 < total) {
+        // the next item's x rows by LDS-DMA from these waves before their conv (the wgrad
+        // waves then issue only their dy rows); older than this item's dx stores, so the
+        // next barrier_vm(nst) retires them
+        Cur nx = cur;
+        adv(nx);
+        const int xr0 = cur.b + 1 < nb ? 2 : 0;
+        const bf16* xsrc = x_of(nx.l);
+        const unsigned xtile = lds0 + (unsigned)(LL::X + (buf ^ 1) * LL::TILE + xr0 * LL::ROWB);
+        for (int j = __builtin_amdgcn_readfirstlane(wave); j < (BR + 2 - xr0) * IPR; j += 4)
+          dma_row_instr_at<C, W>(xsrc, xtile, nx.n, nx.b * BR - 1 + xr0, j, H, loff);
       }
       f32x4 acc[BR][2];
 #pragma unroll
@@ -2505,6 +2550,42 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         }
       }
       nst = nld;
+      if (ASR_BWD_HALO_DG && !RK2 && cur.b + 1 < nb) {  // (RK2: the wgrad waves; its dgrad role has no registers to spare)
+        // the next item continues this image: its tile rows 0, 1 are this band's rows BR, BR+1
+        // (dz, x; dy row 1 only), copied here, where the dgrad waves would otherwise wait at
+        // the band barrier for the wgrad waves.  Rows BR, BR+1 of this item's tiles were
+        // complete at its barrier, and no wave touches rows 0, 1 of the other buffer before
+        // the next one (its DMAs and the convert fill rows 2..).  Compiler-visible LDS
+        // accesses: the epilogue's asm reads were retired by its last lgkm_wait<0>, and these
+        // waves have no LDS-DMA in flight
+        const unsigned base = lds0;
+        const int nbf = buf ^ 1;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+          const int c = tid + 256 * k;  // 5 x 256 16-B chunks: dz rows, x rows, dy row
+          const unsigned o = (unsigned)((c & 255) + NQ) * 16u;
+          const unsigned sreg = k < 2 ? LL::DZ : k < 4 ? LL::X : LL::DY;
+          const int srow = k == 4 ? BR + 1 : BR + (k & 1);
+          const int drow = k == 4 ? 1 : (k & 1);
+          lds_st128(base + sreg + nbf * LL::TILE + drow * LL::ROWB + o,
+                    lds_ld128(base + sreg + buf * LL::TILE + srow * LL::ROWB + o));
+        }
+      }
+      if (ASR_BWD_XDG == 1 && !RK2 && it + 1 < total) {  // (RK2: the wgrad waves, as the halo copy)
+        // the next item's x rows (all 6, or rows 2.. when it continues this image) by LDS-DMA
+        // from these waves, idle until the band barrier, instead of the wgrad waves, whose
+        // MFMAs then start one DMA burst earlier.  Into the other buffer, which no wave reads
+        // in this band; the next barrier waits for every vector-memory op of these waves
+        // (nst = 0), so the rows have landed before any wave reads them
+        Cur nx = cur;
+        adv(nx);
+        const int xr0 = cur.b + 1 < nb ? 2 : 0;
+        const bf16* xsrc = x_of(nx.l);
+        const unsigned xtile = lds0 + (unsigned)(LL::X + (buf ^ 1) * LL::TILE + xr0 * LL::ROWB);
+        for (int j = __builtin_amdgcn_readfirstlane(wave); j < (BR + 2 - xr0) * IPR; j += 4)
+          dma_row_instr_at<C, W>(xsrc, xtile, nx.n, nx.b * BR - 1 + xr0, j, H, loff);
+        nst = 0;
+      }
       if (wave == 0) ASR_BTR(1, 0, it, 3);
       adv(cur);
     }
@@ -2584,7 +2665,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         return;
       }
       for (int j = 0; j < IPR; ++j)
-        dma_row_instr<C, W>(dy_of(c.l), lds + LL::DY + nbuf * LL::TILE + row * LL::ROWB, c.n, c.b * BR - 1 + row, j,
+        dma_row_instr_at<C, W>(dy_of(c.l), lds0 + (unsigned)(LL::DY + nbuf * LL::TILE + row * LL::ROWB), c.n, c.b * BR - 1 + row, j,
                             H, loff);
     };
     auto convert_own = [&](int row, int nbuf, unsigned mwv) {
@@ -2657,7 +2738,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       const int row0 = own_row(false);
       stage_own(c0, row0, 0, mw0);
       for (int j = w8; j < (BR + 2) * IPR; j += 8)
-        dma_row_instr<C, W>(x_of(c0.l), lds + LL::X, c0.n, c0.b * BR - 1, j, H, loff);
+        dma_row_instr_at<C, W>(x_of(c0.l), lds0 + (unsigned)LL::X, c0.n, c0.b * BR - 1, j, H, loff);
       vm_wait(0);
       convert_own(row0, 0, mw0);
     }
@@ -2706,17 +2787,17 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       const bool syn = orow >= 0 && synth(nxt);
       if (syn) synth_row(nxt, orow, buf ^ 1);
       const int ndy = orow >= 0 && !syn ? IPR : 0;
-      const int nx = (more && w8 >= 4) ? ((BR + 2 - xr0) * IPR - (w8 - 4) + 3) / 4 : 0;
+      const int nx = (!(ASR_BWD_XDG && !RK2) && more && w8 >= 4) ? ((BR + 2 - xr0) * IPR - (w8 - 4) + 3) / 4 : 0;
       const int npc = ndy + nx;
       int ipc = 0;
       const bf16* nxdy = dy_of(nxt.l);
       const bf16* nxx = x_of(nxt.l);
       auto piece = [&]() {
         if (ipc < ndy) {
-          dma_row_instr<C, W>(nxdy, lds + LL::DY + (buf ^ 1) * LL::TILE + orow * LL::ROWB, nxt.n,
+          dma_row_instr_at<C, W>(nxdy, lds0 + (unsigned)(LL::DY + (buf ^ 1) * LL::TILE + orow * LL::ROWB), nxt.n,
                               nxt.b * BR - 1 + orow, ipc, H, loff);
         } else {
-          dma_row_instr<C, W>(nxx, lds + LL::X + (buf ^ 1) * LL::TILE + xr0 * LL::ROWB, nxt.n, nxt.b * BR - 1 + xr0,
+          dma_row_instr_at<C, W>(nxx, lds0 + (unsigned)(LL::X + (buf ^ 1) * LL::TILE + xr0 * LL::ROWB), nxt.n, nxt.b * BR - 1 + xr0,
                               (w8 - 4) + 4 * (ipc - ndy), H, loff);
         }
         ++ipc;
@@ -2759,6 +2840,69 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       // tap-4 partner's, phase 2 the direct products of tap t (A = x(t, perm[a]),
       // B = dz(perm[b]): acc[a][b]) and the tap-4 tile; D = acc[a][b] - acc[4 + a][b]
       // leaves at the block's end
+      // Pipelined form (ASR_BWD_PF): the band's 4 x 12 operand fragments are one read
+      // stream, each read issued ASR_BWD_PFD fragments ahead of the MFMA group that
+      // first uses it, across the row boundaries (the transposed reads are compiler-
+      // visible builtins: hipcc places their waits); row r's fragments in use order:
+      //   0 dz(p0) 1 x(8-t, p0) 2 x(8-t, p1) 3 dz(p1) 4 dz(p2) 5 x(4, v1) 6 dz(p3)
+      //   7..10 x(t, p0..p3) 11 x(4, u0)
+      // The registers come from the transposed tiles' accumulators: their products enter
+      // acc[a][b] with the x(8-t) operand negated (bf16 sign flips, exact), so acc[a][b]
+      // holds D = X - Y^T itself (acc[4..7] unused).  No row guard: rows past `rows` (the
+      // image's last band when H % 4 != 0) are outside the image, where the dz tile is
+      // zero (zero-page DMA, zero mask words), so their products add zeros.
+      auto mfma_band_pair_pf = [&](auto bo) {
+        constexpr int BO = decltype(bo)::value, NF = 12, P = ASR_BWD_PFD;
+        bf16x8 F[BR * NF];  // compile-time indices only: registers, allocated by liveness
+        auto rd = [&](auto jc) {
+          constexpr int j = decltype(jc)::value, k = j % NF, R = BO + (j / NF) * LL::ROWB;
+          if constexpr (k == 0 || k == 3 || k == 4 || k == 6)
+            F[j] = tr_pair_px<R>(offB[0] ^ pr.sh(k == 0 ? 0 : k == 3 ? 1 : k == 4 ? 2 : 3));
+          else if constexpr (k == 1 || k == 2) F[j] = tr_pair_px<R>(offA[k]);
+          else if constexpr (k == 5) F[j] = tr_pair_px<R>(offA[4]);
+          else if constexpr (k < 11) F[j] = tr_pair_px<R>(offA[0] ^ pr.sh(k - 7));
+          else F[j] = tr_pair_px<R>(offA[3]);
+        };
+        // group g of a row first needs fragment pf_last(g); reads up to that + P are issued before it
+        static_for<0, BR>([&](auto rc) {
+          constexpr int r = decltype(rc)::value, b = r * NF;
+          bf16x8 nxa, nxb;
+          static_for<0, 9>([&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            constexpr int lo = g == 0 ? (r == 0 ? 0 : cmin(BR * NF, b - NF + pf_last(8) + 1 + P))
+                                      : cmin(BR * NF, b + pf_last(g - 1) + 1 + P);
+            constexpr int hi = cmin(BR * NF, b + pf_last(g) + 1 + P);
+            static_for<lo, hi>(rd);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (g == 0) {
+              nxa = neg_bf16x8(F[b + 1]);
+              nxb = neg_bf16x8(F[b + 2]);
+            }
+            if constexpr (g < 4) {  // transposed products of tap 8-t (+ the tap-4 partner's)
+              constexpr int dzk = g == 0 ? 0 : g == 1 ? 3 : g == 2 ? 4 : 6;
+              acc[g][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F[b + dzk], nxa, acc[g][0], 0, 0, 0);
+              acc[g][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F[b + dzk], nxb, acc[g][1], 0, 0, 0);
+              if constexpr (g == 2) {  // dz(perm[s1]) x x(4, v1)
+                const bf16x8 sel = pr.s1_is_2() ? F[b + 4] : F[b + 3];
+                acc[8][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, F[b + 5], acc[8][1], 0, 0, 0);
+              }
+            } else if constexpr (g < 8) {  // direct products of tap t
+              acc[g - 4][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F[b + 3 + g], F[b], acc[g - 4][0], 0, 0, 0);
+              acc[g - 4][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F[b + 3 + g], F[b + 3], acc[g - 4][1], 0, 0, 0);
+            } else {  // the tap-4 tile, db
+              acc[8][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F[b + 11], F[b], acc[8][0], 0, 0, 0);
+              if (dbw) {
+                accb[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, F[b], accb[0], 0, 0, 0);
+                accb[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, F[b + 3], accb[1], 0, 0, 0);
+              }
+            }
+            // DMA pieces left after the first ASR_BWD3_DMA0: two per row group 3 and 7
+            if constexpr ((g == 3 || g == 7) && r < BR - 1) {
+              if (ipc < npc) piece();
+            }
+          });
+        });
+      };
       auto mfma_band_pair = [&](auto bo) {
         constexpr int BO = decltype(bo)::value;
         static_for<0, BR>([&](auto rc) {
@@ -2800,7 +2944,8 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         });
       };
       auto mfma_band = [&](auto bo) {
-        if constexpr (PAIR) mfma_band_pair(bo);
+        if constexpr (PAIR && ASR_BWD_PF) mfma_band_pair_pf(bo);
+        else if constexpr (PAIR) mfma_band_pair(bo);
         else mfma_band_full(bo);
       };
       if (it > 0) {
@@ -2818,7 +2963,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         convert_own(orow, buf ^ 1, mwv);
       }
       if (wave == 4) ASR_BTR(1, 1, it, 4);
-      if (cont) {  // halo rows of the next band of this image
+      if (!(ASR_BWD_HALO_DG && !RK2) && cont) {  // halo rows of the next band of this image
         // compiler-visible LDS accesses: the item's DMAs were retired by the vm_wait(0)
         // before the convert (cont implies more), so hipcc's own waits cost nothing
         // here, and a copied or spilled read result stays correct
@@ -2864,7 +3009,8 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
 #pragma unroll
           for (int a = 0; a < 4; ++a)
 #pragma unroll
-            for (int b = 0; b < 2; ++b) put(pr.tile(a, b), (acc[a][b] - acc[4 + a][b]) * hsb);
+            for (int b = 0; b < 2; ++b)
+              put(pr.tile(a, b), (ASR_BWD_PF ? acc[a][b] : acc[a][b] - acc[4 + a][b]) * hsb);
           if (pr.self()) {
             put(PairSlab::kSelf + pr.perm(0), acc[8][0] * hsb);  // raw X(4, c, c), c even
             put(PairSlab::kSelf + pr.perm(1), acc[8][1] * hsb);  // X(4, c, c)^T, c odd

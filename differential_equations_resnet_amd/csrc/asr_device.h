@@ -233,6 +233,11 @@ __device__ __forceinline__ unsigned bit01(int v) {
   asm("v_med3_i32 %0, %1, 0, 1" : "=v"(r) : "v"(v));
   return r;
 }
+// -v for 8 bf16 (sign bits flipped: exact, 4 v_xor_b32)
+__device__ __forceinline__ bf16x8 neg_bf16x8(bf16x8 v) {
+  typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(bf16x8, __builtin_bit_cast(u32x4_, v) ^ 0x80008000u);
+}
 // f(integral_constant<int, k>) for k = K .. N-1: compile-time register-array
 // indices (a runtime index would put the array in scratch memory)
 template <int K, int N, typename F>

@@ -51,8 +51,8 @@ SPILL_ALLOW = {
     r"k_bwd3_stackILi64ELi32ELi4ELb0ELb1E": (0, 0, "the production C=64 stacked backward (Euler, pair-local slabs): no "
                                                    "spills (a 16-channel tile's operand address is tile 0's XOR bits "
                                                    "5-6: one register per operand row)"),
-    r"k_bwd3_stackILi64ELi32ELi4ELb1ELb1E": (2, 12, "its RK2 instantiation: one 64-bit value reloaded once per block "
-                                                    "(the fold's start), outside the band loop"),
+    r"k_bwd3_stackILi64ELi32ELi4ELb1ELb1E": (0, 0, "its RK2 instantiation: no spills (the row-pipelined pair wgrad "
+                                                   "accumulates D = X - Y^T in 40 registers instead of 72)"),
     r"k_bwd16_fusedILb0E": (8, 28, "12-wave fused C=16 backward at 168 registers (fp32 dx of 8 layers in the "
                                    "dgrad waves)"),
     r"k_bwd16_fusedILb1E": (12, 36, "its gamma != 0 instantiation (+ the dz tile term)"),
