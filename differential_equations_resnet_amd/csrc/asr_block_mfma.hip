@@ -56,6 +56,12 @@
 #ifndef ASR_BWD_PFD
 #define ASR_BWD_PFD 3  // ASR_BWD_PF: fragments read ahead of their first MFMA
 #endif
+#ifndef ASR_BWD_STAGGER
+#define ASR_BWD_STAGGER 0  // k_bwd3_stack: start delay of half the workgroups, ~1k-cycle units
+#endif
+#ifndef ASR_FWD_STAGGER
+#define ASR_FWD_STAGGER 0  // k_fwd3_stack: the same
+#endif
 #ifndef ASR_BWD_XDG
 #define ASR_BWD_XDG 0  // k_bwd3_stack: the next band's x rows DMA'd by the dgrad waves (1: after their epilogue, 2: before their conv; 0: by the wgrad waves)
 #endif
@@ -134,6 +140,14 @@ __device__ __forceinline__ void tr_store(unsigned long long* p, unsigned long lo
   do {                        \
   } while (0)
 #endif
+
+// Workgroups (blockIdx.x >> 3) odd (half of every XCD's) start `units` x ~1k cycles late:
+// the stacks' workgroups run the same band schedule, so without it every CU issues its
+// next-band DMA burst at the same moment and the bursts queue at the HBM
+__device__ __forceinline__ void stagger_start(int units) {
+  if (units > 0 && ((blockIdx.x >> 3) & 1))
+    for (int k = 0; k < units; ++k) __builtin_amdgcn_s_sleep(16);
+}
 
 template <int C>
 struct Geo {
@@ -1101,6 +1115,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
     }
   };
   adv(xl, xn, xb);
+  stagger_start(ASR_FWD_STAGGER);
   dma_rows<C, W>(x0, lds, cn, -1, min(BR, H) + 2, H, wave, NW, lane);
   int nst = 0;
   const int total = (RK2 ? 2 : 1) * L * per;
@@ -1164,9 +1179,14 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
     lgkm_wait<0>();
     const int y0 = cb * BR, rows = min(BR, H - y0);
     const long rowb = ((long)cn * H + y0) * W;
-    unsigned char* yb = (unsigned char*)(out_of(l) + rowb * C) + ly;
-    uint8_t* mb = mask_of(l);
-    if (mb) mb += rowb * (C / 8) + lm;
+    // the band's y rows and mask rows as buffer stores: a wave-uniform base (SGPRs), the
+    // lane's 32-bit offset and the row as the scalar offset, so no per-lane 64-bit
+    // address math per row, and whether there is a mask is a wave-uniform test
+    uint8_t* mk = mask_of(l);
+    const bool hasm = mk != nullptr;
+    const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)(out_of(l) + rowb * C), 0, RB * W * C * 2, 0x00020000);
+    const auto mrs = __builtin_amdgcn_make_buffer_rsrc((void*)(hasm ? mk + rowb * (C / 8) : mk), 0, RB * W * (C / 8),
+                                                       0x00020000);
     const float hst = (RK2 && !(l & 1)) ? 0.5f * h : h;
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
@@ -1182,11 +1202,11 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
         bits = d == 0 ? bit01(ra) : lshl_or<2 * d>(bit01(ra), bits);
         bits = lshl_or<2 * d + 1>(bit01(rb), bits);
       });
-      if (mb) {
-        mb[r * W * (C / 8)] = (uint8_t)bits;
+      if (hasm) {
+        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bits, mrs, (int)lm, r * W * (C / 8), 0);
         ++nst;
       }
-      *(u32x4*)(yb + r * W * C * 2) = yw;
+      __builtin_amdgcn_raw_buffer_store_b128(yw, yrs, (int)ly, r * W * C * 2, 0);
       ++nst;
     }
     if (wave == 0) ASR_BTR(0, 0, it, 4);
@@ -2409,6 +2429,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
   };
   __syncthreads();
   if (n0 >= n1) return;  // (uniform per workgroup: never with grid <= N)
+  stagger_start(ASR_BWD_STAGGER);
   ASR_BCLK(1, 0);
 
   constexpr int ES = PAIR ? PairSlab::ES : 9 * C * C + C, ECH = ES / 4;
@@ -2467,6 +2488,8 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       if (last_of_stage && blk_of(l) > 0 && (!RK2 || s1))
         load_A1_untracked<C>(wpack + (long)(blk_of(l) - 1) * w_stride, ot, lane, A);
       bf16* drow = dx_of(l) + ((long)n * H + y0) * W * C;
+      // dx rows as buffer stores (uniform base, the lane's 32-bit offset, the row as the scalar offset)
+      const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)(RK2 ? nullptr : drow), 0, BR * W * C * 2, 0x00020000);
       int nld = 0;
       auto epilogue = [&](auto g2c, auto roc, auto kc) {
         // KIND 0: Euler (+dy), 1: second RK2 stage (no +dy), 2: first RK2 stage (+dy +extra)
@@ -2520,7 +2543,10 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
                 ow[d] &= ((int)(short)(xd & 0xffffu) > 0 ? 0xffffu : 0u) | ((int)xd > 0xffff ? 0xffff0000u : 0u);
               }
             }
-            *(u32x4*)((unsigned char*)(drow + (long)r * W * C) + ldx) = ow;
+            if constexpr (RK2)  // (its dgrad role has no SGPRs to spare for the descriptor)
+              *(u32x4*)((unsigned char*)(drow + (long)r * W * C) + ldx) = ow;
+            else
+              __builtin_amdgcn_raw_buffer_store_b128(ow, drs, (int)ldx, r * W * C * 2, 0);
             ++nld;
           }
         });
