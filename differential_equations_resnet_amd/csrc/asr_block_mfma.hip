@@ -56,6 +56,9 @@
 #ifndef ASR_BWD_PFD
 #define ASR_BWD_PFD 3  // ASR_BWD_PF: fragments read ahead of their first MFMA
 #endif
+#ifndef ASR_FWD_RING
+#define ASR_FWD_RING 1  // k_fwd3_stack: ring of three tiles, halo rows read in place (0: two tiles + halo copy)
+#endif
 #ifndef ASR_BWD_STAGGER
 #define ASR_BWD_STAGGER 0  // k_bwd3_stack: start delay of half the workgroups, ~1k-cycle units
 #endif
@@ -380,13 +383,16 @@ struct Band {
   static_assert(NR * ROWB < 65536, "ds_read immediate offset range");
 };
 
+// input rows 0, 1 (the halo rows shared with the previous band) at baseh, rows 2.. at base
+// (the same tile when baseh == base)
 template <int C, int W, int RB, int S>
-__device__ __forceinline__ void band_issue(unsigned base, const unsigned (&lo)[3 * Band<C, W, RB>::NCB],
+__device__ __forceinline__ void band_issue(unsigned base, unsigned baseh, const unsigned (&lo)[3 * Band<C, W, RB>::NCB],
                                            bf16x8 (&B)[Band<C, W, RB>::PT]) {
   using BD = Band<C, W, RB>;
   constexpr int blk = S / BD::NR, ir = S % BD::NR;
-  B[0] = ds_read128<ir * BD::ROWB>(base + lo[blk]);
-  if constexpr (BD::PT >= 2) B[1] = ds_read128<ir * BD::ROWB + BD::PTB>(base + lo[blk]);
+  const unsigned b = (ir < 2 ? baseh : base) + lo[blk];
+  B[0] = ds_read128<ir * BD::ROWB>(b);
+  if constexpr (BD::PT >= 2) B[1] = ds_read128<ir * BD::ROWB + BD::PTB>(b);
   static_assert(BD::PT <= 2, "band conv handles up to two pixel tiles");
 }
 
@@ -412,7 +418,7 @@ struct NoHook {
 // evenly over the pipeline stages (the forward interleaves the previous
 // band's epilogue with this band's MFMAs that way)
 template <int C, int W, int RB, int NU, int S, typename Hook>
-__device__ __forceinline__ void band_step(unsigned base, const unsigned (&lo)[3 * Band<C, W, RB>::NCB],
+__device__ __forceinline__ void band_step(unsigned base, unsigned baseh, const unsigned (&lo)[3 * Band<C, W, RB>::NCB],
                                           const bf16x8 (&A)[Geo<C>::KS], f32x4 (&acc)[RB][W / 16],
                                           bf16x8 (&B)[3][W / 16], Hook& hook) {
   using BD = Band<C, W, RB>;
@@ -424,25 +430,30 @@ __device__ __forceinline__ void band_step(unsigned base, const unsigned (&lo)[3 
     band_mfma<C, W, RB, ir, kx, cb, 0>(A, acc, B[S % 3]);
     band_mfma<C, W, RB, ir, kx, cb, 1>(A, acc, B[S % 3]);
     band_mfma<C, W, RB, ir, kx, cb, 2>(A, acc, B[S % 3]);
-    if constexpr (S + 2 < BD::NS) band_issue<C, W, RB, S + 2>(base, lo, B[(S + 2) % 3]);
+    if constexpr (S + 2 < BD::NS) band_issue<C, W, RB, S + 2>(base, baseh, lo, B[(S + 2) % 3]);
     if constexpr (NU > 0) {
       constexpr int SP = BD::NS / NU;
       if constexpr (SP > 0 && S % SP == SP / 2 && S / SP < NU) hook(std::integral_constant<int, S / SP>{});
     }
-    band_step<C, W, RB, NU, S + 1>(base, lo, A, acc, B, hook);
+    band_step<C, W, RB, NU, S + 1>(base, baseh, lo, A, acc, B, hook);
   }
 }
 
 // acc[r][pt] += conv over the RB output rows whose first input row is the
 // tile row at LDS byte address `base`
 template <int C, int W, int RB, int NU = 0, typename Hook = NoHook>
-__device__ __forceinline__ void conv_band(unsigned base, const unsigned (&lo)[3 * Band<C, W, RB>::NCB],
-                                          const bf16x8 (&A)[Geo<C>::KS], f32x4 (&acc)[RB][W / 16], Hook hook = {}) {
+__device__ __forceinline__ void conv_band2(unsigned base, unsigned baseh, const unsigned (&lo)[3 * Band<C, W, RB>::NCB],
+                                           const bf16x8 (&A)[Geo<C>::KS], f32x4 (&acc)[RB][W / 16], Hook hook = {}) {
   bf16x8 B[3][W / 16];
   lgkm_wait<0>();
-  band_issue<C, W, RB, 0>(base, lo, B[0]);
-  band_issue<C, W, RB, 1>(base, lo, B[1]);
-  band_step<C, W, RB, NU, 0>(base, lo, A, acc, B, hook);
+  band_issue<C, W, RB, 0>(base, baseh, lo, B[0]);
+  band_issue<C, W, RB, 1>(base, baseh, lo, B[1]);
+  band_step<C, W, RB, NU, 0>(base, baseh, lo, A, acc, B, hook);
+}
+template <int C, int W, int RB, int NU = 0, typename Hook = NoHook>
+__device__ __forceinline__ void conv_band(unsigned base, const unsigned (&lo)[3 * Band<C, W, RB>::NCB],
+                                          const bf16x8 (&A)[Geo<C>::KS], f32x4 (&acc)[RB][W / 16], Hook hook = {}) {
+  conv_band2<C, W, RB, NU, Hook>(base, base, lo, A, acc, hook);
 }
 
 template <int C, int W, int RB>
@@ -1098,8 +1109,14 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
   const unsigned lxr = (unsigned)toff<C>(1, px + 1, cg, TW);
   const unsigned ly = (unsigned)(px * C + 8 * cg) * 2u, lm = (unsigned)(px * (C / 8) + cg);
 
-  zero_halo_cols<C, W>(lds, BR + 2, tid, 64 * NW);
-  zero_halo_cols<C, W>(lds + TILE, BR + 2, tid, 64 * NW);
+  // ASR_FWD_RING: a ring of three tiles; a band that continues the previous band's image
+  // reads its two halo rows where that band's tile holds them (rows BR, BR+1), so only its
+  // BR new rows are DMA'd and nothing is copied inside LDS.  The DMA of band it+1 goes to
+  // the tile band it-2 used, which band it-1 read last (as its halo rows): free after
+  // band it's barrier.  (2 tiles: the halo rows copied into the next tile.)
+  constexpr int NT = ASR_FWD_RING ? 3 : 2;
+#pragma unroll
+  for (int k = 0; k < NT; ++k) zero_halo_cols<C, W>(lds + k * TILE, BR + 2, tid, 64 * NW);
   constexpr int IPR = W / G::PPI;  // DMA pieces per row
   const unsigned loff = (unsigned)dma_lane_off<C, W>(lane) * 2u;
   // cursor over (block l, image n, band b)
@@ -1120,8 +1137,8 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
   int nst = 0;
   const int total = (RK2 ? 2 : 1) * L * per;
   ASR_BCLK(0, 0);
+  int buf = 0, nbuf = 1, pbuf = NT - 1;  // this band's tile, the next band's, the previous band's
   for (int it = 0; it < total; ++it) {
-    const int buf = it & 1;
     if (wave == 0) ASR_BTR(0, 0, it, 0);
     barrier_vm(nst);  // band it landed; every wave is done with band it-1's tile
     if (wave == 0) ASR_BTR(0, 0, it, 1);
@@ -1132,17 +1149,19 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
     const bf16* nxs = x0;
     int ngy0 = 0, nrows = 0;
     if (it + 1 < total) {
-      unsigned char* nt = lds + (buf ^ 1) * TILE;
+      unsigned char* nt = lds + nbuf * TILE;
       const int yy = xb * BR;
       nxs = src_of(xl);
       if (xl == cl && xn == cn && xb == cb + 1) {
         ntile = nt + 2 * BD::ROWB, ngy0 = yy + 1, nrows = min(BR, H - yy);
-        const uint4* src = (const uint4*)(lds + buf * TILE + BR * BD::ROWB);
-        uint4* dst = (uint4*)nt;
-        constexpr int NCH = 2 * W * NQ;
-        for (int i = tid; i < NCH; i += 64 * NW) {
-          const int o = ((i / (W * NQ)) * TW + 1) * NQ + i % (W * NQ);
-          dst[o] = src[o];
+        if constexpr (!ASR_FWD_RING) {
+          const uint4* src = (const uint4*)(lds + buf * TILE + BR * BD::ROWB);
+          uint4* dst = (uint4*)nt;
+          constexpr int NCH = 2 * W * NQ;
+          for (int i = tid; i < NCH; i += 64 * NW) {
+            const int o = ((i / (W * NQ)) * TW + 1) * NQ + i % (W * NQ);
+            dst[o] = src[o];
+          }
         }
       } else {
         ntile = nt, ngy0 = yy - 1, nrows = min(BR, H - yy) + 2;
@@ -1152,6 +1171,8 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
     }
     if (wave == 0) ASR_BTR(0, 0, it, 2);
     const unsigned tb = lds_u32(lds + buf * TILE);
+    // input rows 0, 1: the previous band's tile rows BR, BR+1 when this band continues its image
+    const unsigned th = (ASR_FWD_RING && cb > 0) ? lds_u32(lds + pbuf * TILE) + (unsigned)(BR * BD::ROWB) : tb;
     f32x4 acc[RB][2];
 #pragma unroll
     for (int r = 0; r < RB; ++r)
@@ -1165,11 +1186,11 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
 #pragma unroll
       for (int r = 0; r < RB; ++r) xr[r] = *(const u32x4*)(rb + (long)min(r, rows - 1) * W * C * 2);
     }
-    conv_band<C, W, RB>(tb, lo, A, acc);
+    conv_band2<C, W, RB>(tb, th, lo, A, acc);
     if (wave == 0) ASR_BTR(0, 0, it, 3);
-    if (!resg) {
+    if (!resg) {  // tile rows 1..RB (row 1 a halo row)
 #pragma unroll
-      for (int r = 0; r < RB; ++r) xr[r] = lds_rd128(tb + lxr + (unsigned)(r * BD::ROWB));
+      for (int r = 0; r < RB; ++r) xr[r] = lds_rd128((r == 0 ? th : tb) + lxr + (unsigned)(r * BD::ROWB));
     }
     const int l = cl;
     if (blk_of(xl) != blk_of(cl) && it + 1 < total) {  // the next item starts block l+1: its W and bias (L2 hits)
@@ -1212,6 +1233,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
     if (wave == 0) ASR_BTR(0, 0, it, 4);
     cl = xl, cn = xn, cb = xb;
     adv(xl, xn, xb);
+    pbuf = buf, buf = nbuf, nbuf = nbuf + 1 == NT ? 0 : nbuf + 1;
   }
   ASR_BCLK(0, 1);
 }
@@ -3515,7 +3537,7 @@ int block_stack_fwd_mfma(const void* x0, void* ys, long y_stride, uint8_t* masks
   int cus = cu_count();
   if (cus <= 0) cus = 256;
   const int grid = std::max(1, std::min(N, 2 * cus));
-  const size_t lds = 2 * (size_t)(kFwdBR + 2) * (W + 2) * C * 2;
+  const size_t lds = (ASR_FWD_RING ? 3 : 2) * (size_t)(kFwdBR + 2) * (W + 2) * C * 2;  // k_fwd3_stack's tiles
   hipLaunchKernelGGL((blk::k_fwd3_stack<64, 32, kFwdBR>), dim3(grid), dim3(256), lds, s, (const bf16*)x0,
                      (bf16*)ys, y_stride, masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, H, L,
                      slots);
@@ -3664,7 +3686,7 @@ int block_stack_fwd_rk2_mfma(const void* x0, void* ys, void* xm, long y_stride, 
   int cus = cu_count();
   if (cus <= 0) cus = 256;
   const int grid = std::max(1, std::min(N, 2 * cus));
-  const size_t lds = 2 * (size_t)(kFwdBR + 2) * (W + 2) * C * 2;
+  const size_t lds = (ASR_FWD_RING ? 3 : 2) * (size_t)(kFwdBR + 2) * (W + 2) * C * 2;  // k_fwd3_stack's tiles
   hipLaunchKernelGGL((blk::k_fwd3_stack<64, 32, kFwdBR, true>), dim3(grid), dim3(256), lds, s, (const bf16*)x0,
                      (bf16*)ys, y_stride, masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, H, L, 0,
                      (bf16*)xm, masks2);
