@@ -59,6 +59,12 @@
 #ifndef ASR_FWD_RING
 #define ASR_FWD_RING 1  // k_fwd3_stack: ring of three tiles, halo rows read in place (0: two tiles + halo copy)
 #endif
+#ifndef ASR_BWD_CVROW
+#define ASR_BWD_CVROW -1  // k_bwd3_stack pair wgrad: the next band's dz convert after this MFMA row (-1: after the band; 0, 1: flat, 2: -0.8 % in r04m)
+#endif
+#ifndef ASR_BWD_XLATE
+#define ASR_BWD_XLATE 0  // k_bwd3_stack pair wgrad: the next band's x DMA after the MFMA band (0: with the dy row, up front; 1 measured -8 %)
+#endif
 #ifndef ASR_BWD_STAGGER
 #define ASR_BWD_STAGGER 0  // k_bwd3_stack: start delay of half the workgroups, ~1k-cycle units
 #endif
@@ -2850,7 +2856,12 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         }
         ++ipc;
       };
-      while (ipc < npc && ipc < ASR_BWD3_DMA0) piece();
+      // ASR_BWD_XLATE: only the own dy row up front; the next band's x rows after the MFMA band
+      // (the waves that issue them, w8 >= 4, have no own row in a band that continues an image)
+      if (ASR_BWD_XLATE && PAIR && ASR_BWD_PF)
+        while (ipc < ndy) piece();
+      else
+        while (ipc < npc && ipc < ASR_BWD3_DMA0) piece();
       if (wave == 4) ASR_BTR(1, 1, it, 2);
       bf16x8 Bf[2], Ar[3];
       auto mfma_band_full = [&](auto bo) {
@@ -2899,7 +2910,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       // holds D = X - Y^T itself (acc[4..7] unused).  No row guard: rows past `rows` (the
       // image's last band when H % 4 != 0) are outside the image, where the dz tile is
       // zero (zero-page DMA, zero mask words), so their products add zeros.
-      auto mfma_band_pair_pf = [&](auto bo) {
+      auto mfma_band_pair_pf = [&](auto bo, auto&& mid) {
         constexpr int BO = decltype(bo)::value, NF = 12, P = ASR_BWD_PFD;
         bf16x8 F[BR * NF];  // compile-time indices only: registers, allocated by liveness
         auto rd = [&](auto jc) {
@@ -2945,9 +2956,10 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
               }
             }
             // DMA pieces left after the first ASR_BWD3_DMA0: two per row group 3 and 7
-            if constexpr ((g == 3 || g == 7) && r < BR - 1) {
+            if constexpr (!ASR_BWD_XLATE && (g == 3 || g == 7) && r < BR - 1) {
               if (ipc < npc) piece();
             }
+            if constexpr (g == 8 && r == ASR_BWD_CVROW) mid();
           });
         });
       };
@@ -2991,9 +3003,22 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
           }
         });
       };
+      // ASR_BWD_CVROW >= 0: the next band's dz convert of this wave's own row runs after
+      // row ASR_BWD_CVROW's MFMAs instead of after the band, so it overlaps the MFMAs of the
+      // SIMD's other wgrad wave (which has no own row in a band that continues an image)
+      auto convert_next = [&]() {
+        if (more) {
+          while (ipc < npc) piece();
+          vm_wait(0);  // own dy row and mask dwords of band it+1 (x DMA and fold loads too)
+          convert_own(orow, buf ^ 1, mwv);
+        }
+      };
+      constexpr bool CV_MID = PAIR && ASR_BWD_PF && ASR_BWD_CVROW >= 0;
       auto mfma_band = [&](auto bo) {
-        if constexpr (PAIR && ASR_BWD_PF) mfma_band_pair_pf(bo);
-        else if constexpr (PAIR) mfma_band_pair(bo);
+        if constexpr (PAIR && ASR_BWD_PF) {
+          if constexpr (CV_MID) mfma_band_pair_pf(bo, convert_next);
+          else mfma_band_pair_pf(bo, [] {});
+        } else if constexpr (PAIR) mfma_band_pair(bo);
         else mfma_band_full(bo);
       };
       if (it > 0) {
@@ -3006,10 +3031,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       mfma_band(std::integral_constant<int, 0>{});
       while (ipc < npc) piece();
       if (wave == 4) ASR_BTR(1, 1, it, 3);
-      if (more) {
-        vm_wait(0);
-        convert_own(orow, buf ^ 1, mwv);
-      }
+      if (!CV_MID) convert_next();
       if (wave == 4) ASR_BTR(1, 1, it, 4);
       if (!(ASR_BWD_HALO_DG && !RK2) && cont) {  // halo rows of the next band of this image
         // compiler-visible LDS accesses: the item's DMAs were retired by the vm_wait(0)
