@@ -265,6 +265,9 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
 // One barrier per layer.  LDS: 2 dz tiles (swizzled, zero halo) + zero row |
 // 2 x tiles (image rows, zero halo columns) | 2 x 2 KiB masks | db partials.
 // ---------------------------------------------------------------------------
+#ifndef ASR_DEEP_WDEPTH
+#define ASR_DEEP_WDEPTH 2  // wgrad waves: x / dz row fragments read this many rows ahead of their MFMAs (3: flat, r04p)
+#endif
 #ifndef ASR_DEEP_NDG
 #define ASR_DEEP_NDG 8
 #endif
@@ -477,7 +480,7 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
     // fragment of image row ir-1 feeds output rows ir - ky; reads run DEPTH rows
     // ahead of the MFMAs
     auto wgrad_layer = [&](f32x4 (&a)[3], int tt) {
-      constexpr int DEPTH = 2;
+      constexpr int DEPTH = ASR_DEEP_WDEPTH;
       const int par = tt & 1;
       const unsigned char* xt = lds + L_X + par * XT + kx * 32 - ROWB;  // + ir*ROWB: image row ir-1 < XS
       const unsigned char* xh = lds + xhi_base(tt) - XS * ROWB + kx * 32 - ROWB;  // image rows >= XS
