@@ -31,7 +31,8 @@ def rt():
     return runtime
 
 
-@pytest.mark.parametrize("N,L,with_bias", [(1, 3, True), (5, 4, False), (300, 3, True), (600, 2, True)])
+@pytest.mark.parametrize("N,L,with_bias", [(1, 3, True), (5, 4, False), (300, 3, True), (600, 2, True),
+                                            (512, 5, True), (1000, 3, False)])
 def test_stack64_equals_single_blocks(rt, N, L, with_bias):
     C, H, W, h = 64, 32, 32, 8.0 / 30
     rng = np.random.default_rng(N * 7 + L)
@@ -343,14 +344,14 @@ def test_stack_handoff_degrades_gracefully(rt):
     assert np.isfinite(loss2.item()) and g2.abs().max().item() > 0
 
 
-@pytest.mark.parametrize("C,L,dtype", [(64, 5, "bfloat16"), (64, 4, "bfloat16"), (16, 5, "bfloat16"),
-                                       (16, 3, "float32")])
-def test_inference_executor_matches_training_forward(rt, C, L, dtype):
+@pytest.mark.parametrize("C,L,dtype,N", [(64, 5, "bfloat16", 96), (64, 4, "bfloat16", 96), (16, 5, "bfloat16", 96),
+                                         (16, 3, "float32", 96), (64, 5, "bfloat16", 512), (64, 4, "bfloat16", 600)])
+def test_inference_executor_matches_training_forward(rt, C, L, dtype, N):
     """The forward-only workspace (ASR_VARIANT_INFERENCE: x_0 + two ping-pong
     slots; at C=64 bf16 one k_fwd3_stack launch with slots=2 and no masks)
     gives the training forward's probabilities bitwise (the same kernels'
-    arithmetic), for both parities of L, at a fraction of the memory."""
-    N = 96
+    arithmetic), for both parities of L, at a fraction of the memory; the
+    bench's batch (two images per workgroup) and a ragged one included."""
     dev, params, imgs, tgt = _net_case(rt, N, C, L, seed=11)
     kw = dict(subtract_mean=127.5, divide_by_stddev=127.5, dtype=dtype, input_u8=True, device=dev)
     tr = rt.NetExecutor(N, 32, 32, 3, C, L, 10, 8.0 / L, 0.0, **kw)
