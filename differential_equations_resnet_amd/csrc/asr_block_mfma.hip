@@ -65,6 +65,12 @@
 #ifndef ASR_BWD_XLATE
 #define ASR_BWD_XLATE 0  // k_bwd3_stack pair wgrad: the next band's x DMA after the MFMA band (0: with the dy row, up front; 1 measured -8 %)
 #endif
+#ifndef ASR_FWD_PKMASK
+#define ASR_FWD_PKMASK 1  // k_fwd3_stack: relu-mask bits two at a time (v_cvt_pk_u16_u32 + v_pk_min_u16: 13 VALU per row instead of 15; masks bitwise equal; speed flat, r04r)
+#endif
+#ifndef ASR_BWD_WPRIO
+#define ASR_BWD_WPRIO 0  // k_bwd3_stack: static s_setprio of the wgrad waves (1, 2: flat, r04r)
+#endif
 #ifndef ASR_BWD_STAGGER
 #define ASR_BWD_STAGGER 0  // k_bwd3_stack: start delay of half the workgroups, ~1k-cycle units
 #endif
@@ -1226,9 +1232,15 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
         constexpr int d = decltype(dc)::value;
         const int ra = max(__float_as_int(z[2 * d]), 0), rb = max(__float_as_int(z[2 * d + 1]), 0);
         yw[d] = pk_bf16(fmaf(hst, __int_as_float(ra), lo_f(xr[r][d])), fmaf(hst, __int_as_float(rb), hi_f(xr[r][d])));
-        bits = d == 0 ? bit01(ra) : lshl_or<2 * d>(bit01(ra), bits);
-        bits = lshl_or<2 * d + 1>(bit01(rb), bits);
+        if constexpr (ASR_FWD_PKMASK) {  // bits 2d (low half) and 2d+1 (high half) of a pair word
+          const unsigned pw = bits01_pair(ra, rb);
+          bits = d == 0 ? pw : lshl_or<2 * d>(pw, bits);
+        } else {
+          bits = d == 0 ? bit01(ra) : lshl_or<2 * d>(bit01(ra), bits);
+          bits = lshl_or<2 * d + 1>(bit01(rb), bits);
+        }
       });
+      if constexpr (ASR_FWD_PKMASK) bits = pair_bits_to_byte(bits);
       if (hasm) {
         __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bits, mrs, (int)lm, r * W * (C / 8), 0);
         ++nst;
@@ -2646,6 +2658,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
     barrier_vm(0);  // matches the wgrad waves' end-of-loop barrier
   } else {
     // ---------------- wgrad waves ----------------
+    if (ASR_BWD_WPRIO) __builtin_amdgcn_s_setprio(ASR_BWD_WPRIO);
     const int w8 = __builtin_amdgcn_readfirstlane(wave) - 4;
     const int tg = w8 >> 1, oq = 2 * (w8 & 1);
     const int tq = lx >> 2, tp = lx & 3;

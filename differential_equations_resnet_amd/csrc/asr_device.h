@@ -238,6 +238,19 @@ __device__ __forceinline__ bf16x8 neg_bf16x8(bf16x8 v) {
   typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
   return __builtin_bit_cast(bf16x8, __builtin_bit_cast(u32x4_, v) ^ 0x80008000u);
 }
+// relu-mask bits of a pair of relu'd values (ra, rb >= 0, bit patterns of floats):
+// [ra > 0] in bit 0 and [rb > 0] in bit 16 (saturating pack to 16 bits keeps a
+// nonzero value nonzero, then a packed min with 1; the inline constant 1 is the low
+// half of src1, op_sel_hi:[1,0] reads it for the high half too)
+__device__ __forceinline__ unsigned bits01_pair(int ra, int rb) {
+  unsigned p, r;
+  asm("v_cvt_pk_u16_u32 %0, %1, %2" : "=v"(p) : "v"(ra), "v"(rb));
+  asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(r) : "v"(p));
+  return r;
+}
+// the four pair words OR-ed at shifts 0, 2, 4, 6 (element 2d at bit 2d, 2d+1 at bit
+// 16+2d) -> the mask byte, element i at bit i (low 8 bits of the result)
+__device__ __forceinline__ unsigned pair_bits_to_byte(unsigned q) { return q | (q >> 15); }
 // f(integral_constant<int, k>) for k = K .. N-1: compile-time register-array
 // indices (a runtime index would put the array in scratch memory)
 template <int K, int N, typename F>
