@@ -71,6 +71,9 @@
 #ifndef ASR_BWD_WPRIO
 #define ASR_BWD_WPRIO 0  // k_bwd3_stack: static s_setprio of the wgrad waves (1, 2: flat, r04r)
 #endif
+#ifndef ASR_BWD_SLAB_EARLY
+#define ASR_BWD_SLAB_EARLY 0  // k_bwd3_stack (Euler): a block's slab stores right after its last MFMA band (-0.6 %, r04t)
+#endif
 #ifndef ASR_BWD_STAGGER
 #define ASR_BWD_STAGGER 0  // k_bwd3_stack: start delay of half the workgroups, ~1k-cycle units
 #endif
@@ -3041,8 +3044,59 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
 #pragma unroll
         for (int k = 0; k < NOB; ++k) offB[k] += dlt;
       }
+      // block l's dW tiles and db (write-through stores; the next band barrier drains them).
+      // ASR_BWD_SLAB_EARLY (Euler): issued right after the block's last MFMA band, before the
+      // convert's wait for the next band's DMA, so the burst drains in that wait's shadow
+      // instead of at the next barrier
+      constexpr bool SLAB_EARLY = ASR_BWD_SLAB_EARLY && !RK2;
+      auto publish = [&]() {
+          // publish block l's dW tiles and db (write-through; drained at the next band barrier)
+          float* slab = slabs + (long)l * slab_stride + (long)blockIdx.x * ES;
+          const auto rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, ES * 4, 0x00020000);
+          auto put = [&](int tile, f32x4 v) {
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, ((tile * 64 + lane) * 4) * 4, 0, 16);
+          };
+          if constexpr (PAIR) {  // D = X - Y^T per pair tile: 8 (+1 or 2 tap-4) tiles of the 74
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+              for (int b = 0; b < 2; ++b)
+                put(pr.tile(a, b), (ASR_BWD_PF ? acc[a][b] : acc[a][b] - acc[4 + a][b]) * hsb);
+            if (pr.self()) {
+              put(PairSlab::kSelf + pr.perm(0), acc[8][0] * hsb);  // raw X(4, c, c), c even
+              put(PairSlab::kSelf + pr.perm(1), acc[8][1] * hsb);  // X(4, c, c)^T, c odd
+            } else {
+              put(PairSlab::kTap4 + pr.k4(), (acc[8][0] - acc[8][1]) * hsb);
+            }
+#pragma unroll
+            for (int mi = 0; mi < MTW; ++mi) acc[mi][0] = acc[mi][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+          } else {
+#pragma unroll
+            for (int mi = 0; mi < MTW; ++mi)
+#pragma unroll
+              for (int oi = 0; oi < 2; ++oi) {
+                const int mt = tg * MTW + mi;
+                put(mt * 4 + oq + oi, acc[mi][oi] * hsb);
+                acc[mi][oi] = f32x4{0.f, 0.f, 0.f, 0.f};
+              }
+          }
+          if (dbw) {
+            if (g == 0) {
+#pragma unroll
+              for (int oi = 0; oi < 2; ++oi) {
+                const int ob = PAIR ? pr.perm(oi) : oq + oi;
+                __hip_atomic_store((gf32*)(slab + (ES - C) + 16 * ob + lx), hsb * accb[oi][0], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+              }
+            }
+            accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+      };
       mfma_band(std::integral_constant<int, 0>{});
       while (ipc < npc) piece();
+      if constexpr (SLAB_EARLY) {
+        if (cur.b == nb - 1 && cur.n == n1 - 1) publish();  // (Euler: the stage is the block)
+      }
       if (wave == 4) ASR_BTR(1, 1, it, 3);
       if (!CV_MID) convert_next();
       if (wave == 4) ASR_BTR(1, 1, it, 4);
@@ -3082,46 +3136,48 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       }
       if (last_of_block) {
         if (l + 2 < L && l + 2 >= lfold) fold_end(l + 2);
-        // publish block l's dW tiles and db (write-through; drained at the next band barrier)
-        float* slab = slabs + (long)l * slab_stride + (long)blockIdx.x * ES;
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, ES * 4, 0x00020000);
-        auto put = [&](int tile, f32x4 v) {
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, ((tile * 64 + lane) * 4) * 4, 0, 16);
-        };
-        if constexpr (PAIR) {  // D = X - Y^T per pair tile: 8 (+1 or 2 tap-4) tiles of the 74
+        if constexpr (!SLAB_EARLY) {
+          // publish block l's dW tiles and db (write-through; drained at the next band barrier)
+          float* slab = slabs + (long)l * slab_stride + (long)blockIdx.x * ES;
+          const auto rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, ES * 4, 0x00020000);
+          auto put = [&](int tile, f32x4 v) {
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, ((tile * 64 + lane) * 4) * 4, 0, 16);
+          };
+          if constexpr (PAIR) {  // D = X - Y^T per pair tile: 8 (+1 or 2 tap-4) tiles of the 74
 #pragma unroll
-          for (int a = 0; a < 4; ++a)
+            for (int a = 0; a < 4; ++a)
 #pragma unroll
-            for (int b = 0; b < 2; ++b)
-              put(pr.tile(a, b), (ASR_BWD_PF ? acc[a][b] : acc[a][b] - acc[4 + a][b]) * hsb);
-          if (pr.self()) {
-            put(PairSlab::kSelf + pr.perm(0), acc[8][0] * hsb);  // raw X(4, c, c), c even
-            put(PairSlab::kSelf + pr.perm(1), acc[8][1] * hsb);  // X(4, c, c)^T, c odd
+              for (int b = 0; b < 2; ++b)
+                put(pr.tile(a, b), (ASR_BWD_PF ? acc[a][b] : acc[a][b] - acc[4 + a][b]) * hsb);
+            if (pr.self()) {
+              put(PairSlab::kSelf + pr.perm(0), acc[8][0] * hsb);  // raw X(4, c, c), c even
+              put(PairSlab::kSelf + pr.perm(1), acc[8][1] * hsb);  // X(4, c, c)^T, c odd
+            } else {
+              put(PairSlab::kTap4 + pr.k4(), (acc[8][0] - acc[8][1]) * hsb);
+            }
+#pragma unroll
+            for (int mi = 0; mi < MTW; ++mi) acc[mi][0] = acc[mi][1] = f32x4{0.f, 0.f, 0.f, 0.f};
           } else {
-            put(PairSlab::kTap4 + pr.k4(), (acc[8][0] - acc[8][1]) * hsb);
+#pragma unroll
+            for (int mi = 0; mi < MTW; ++mi)
+#pragma unroll
+              for (int oi = 0; oi < 2; ++oi) {
+                const int mt = tg * MTW + mi;
+                put(mt * 4 + oq + oi, acc[mi][oi] * hsb);
+                acc[mi][oi] = f32x4{0.f, 0.f, 0.f, 0.f};
+              }
           }
+          if (dbw) {
+            if (g == 0) {
 #pragma unroll
-          for (int mi = 0; mi < MTW; ++mi) acc[mi][0] = acc[mi][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-        } else {
-#pragma unroll
-          for (int mi = 0; mi < MTW; ++mi)
-#pragma unroll
-            for (int oi = 0; oi < 2; ++oi) {
-              const int mt = tg * MTW + mi;
-              put(mt * 4 + oq + oi, acc[mi][oi] * hsb);
-              acc[mi][oi] = f32x4{0.f, 0.f, 0.f, 0.f};
+              for (int oi = 0; oi < 2; ++oi) {
+                const int ob = PAIR ? pr.perm(oi) : oq + oi;
+                __hip_atomic_store((gf32*)(slab + (ES - C) + 16 * ob + lx), hsb * accb[oi][0], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+              }
             }
-        }
-        if (dbw) {
-          if (g == 0) {
-#pragma unroll
-            for (int oi = 0; oi < 2; ++oi) {
-              const int ob = PAIR ? pr.perm(oi) : oq + oi;
-              __hip_atomic_store((gf32*)(slab + (ES - C) + 16 * ob + lx), hsb * accb[oi][0], __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-            }
+            accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
           }
-          accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
       if (wave == 4) ASR_BTR(1, 1, it, 5);
