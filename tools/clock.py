@@ -25,9 +25,14 @@ for f in glob.glob(os.path.join(root, "**", "*kernel_trace.csv"), recursive=True
 
 
 def short(name):
+    """k_fwd3_stack<C, W, BR, RK2> / k_bwd3_stack<C, W, BR, RK2, PAIR>: RK2 is the first bool
+    template argument (mangled ...Li4ELb<RK2>E..., demangled '<64, 32, 4, true' ...)."""
+    import re
     for k in ("k_fwd3_stack", "k_bwd3_stack", "k_fwd16_fused", "k_bwd16_fused"):
         if k in name:
-            return k + ("<RK2>" if ("Lb1E" in name or "true>" in name) and "stack" in k else "")
+            m = re.search(r"Li4ELb([01])E", name) or re.search(r"<64, 32, 4, (true|false)", name)
+            rk2 = m is not None and m.group(1) in ("1", "true")
+            return k + ("<RK2>" if rk2 and "stack" in k else "")
     return None
 
 
