@@ -50,42 +50,6 @@
 #ifndef ASR_FWD3_WGS
 #define ASR_FWD3_WGS 3  // k_fwd3 workgroups per CU (grid = min(bands, WGS x CUs))
 #endif
-#ifndef ASR_BWD_PF
-#define ASR_BWD_PF 1  // k_bwd3_stack pair-local wgrad: row r+1's first fragments read during row r's second phase
-#endif
-#ifndef ASR_BWD_PFD
-#define ASR_BWD_PFD 3  // ASR_BWD_PF: fragments read ahead of their first MFMA
-#endif
-#ifndef ASR_FWD_RING
-#define ASR_FWD_RING 1  // k_fwd3_stack: ring of three tiles, halo rows read in place (0: two tiles + halo copy)
-#endif
-#ifndef ASR_BWD_CVROW
-#define ASR_BWD_CVROW -1  // k_bwd3_stack pair wgrad: the next band's dz convert after this MFMA row (-1: after the band; 0, 1: flat, 2: -0.8 % in r04m)
-#endif
-#ifndef ASR_BWD_XLATE
-#define ASR_BWD_XLATE 0  // k_bwd3_stack pair wgrad: the next band's x DMA after the MFMA band (0: with the dy row, up front; 1 measured -8 %)
-#endif
-#ifndef ASR_FWD_PKMASK
-#define ASR_FWD_PKMASK 1  // k_fwd3_stack: relu-mask bits two at a time (v_cvt_pk_u16_u32 + v_pk_min_u16: 13 VALU per row instead of 15; masks bitwise equal; speed flat, r04r)
-#endif
-#ifndef ASR_BWD_WPRIO
-#define ASR_BWD_WPRIO 0  // k_bwd3_stack: static s_setprio of the wgrad waves (1, 2: flat, r04r)
-#endif
-#ifndef ASR_BWD_SLAB_EARLY
-#define ASR_BWD_SLAB_EARLY 0  // k_bwd3_stack (Euler): a block's slab stores right after its last MFMA band (-0.6 %, r04t)
-#endif
-#ifndef ASR_BWD_STAGGER
-#define ASR_BWD_STAGGER 0  // k_bwd3_stack: start delay of half the workgroups, ~1k-cycle units
-#endif
-#ifndef ASR_FWD_STAGGER
-#define ASR_FWD_STAGGER 0  // k_fwd3_stack: the same
-#endif
-#ifndef ASR_BWD_XDG
-#define ASR_BWD_XDG 0  // k_bwd3_stack: the next band's x rows DMA'd by the dgrad waves (1: after their epilogue, 2: before their conv; 0: by the wgrad waves)
-#endif
-#ifndef ASR_BWD_HALO_DG
-#define ASR_BWD_HALO_DG 1  // k_bwd3_stack: the halo rows of the next band copied by the dgrad waves (0: wgrad waves)
-#endif
 #ifndef ASR_BWD3_DMA0
 #define ASR_BWD3_DMA0 16  // k_bwd3 wgrad waves: DMA pieces issued right after the barrier, the rest one per row (A/B: spreading them lengthened the MFMA phase as much as it saved; the stacks: all at once 16 vs 9 +0.3-0.5 %, 4 -0.7 %)
 #endif
@@ -158,14 +122,6 @@ __device__ __forceinline__ void tr_store(unsigned long long* p, unsigned long lo
   do {                        \
   } while (0)
 #endif
-
-// Workgroups (blockIdx.x >> 3) odd (half of every XCD's) start `units` x ~1k cycles late:
-// the stacks' workgroups run the same band schedule, so without it every CU issues its
-// next-band DMA burst at the same moment and the bursts queue at the HBM
-__device__ __forceinline__ void stagger_start(int units) {
-  if (units > 0 && ((blockIdx.x >> 3) & 1))
-    for (int k = 0; k < units; ++k) __builtin_amdgcn_s_sleep(16);
-}
 
 template <int C>
 struct Geo {
@@ -1124,12 +1080,12 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
   const unsigned lxr = (unsigned)toff<C>(1, px + 1, cg, TW);
   const unsigned ly = (unsigned)(px * C + 8 * cg) * 2u, lm = (unsigned)(px * (C / 8) + cg);
 
-  // ASR_FWD_RING: a ring of three tiles; a band that continues the previous band's image
+  // A ring of three tiles: a band that continues the previous band's image
   // reads its two halo rows where that band's tile holds them (rows BR, BR+1), so only its
   // BR new rows are DMA'd and nothing is copied inside LDS.  The DMA of band it+1 goes to
   // the tile band it-2 used, which band it-1 read last (as its halo rows): free after
   // band it's barrier.  (2 tiles: the halo rows copied into the next tile.)
-  constexpr int NT = ASR_FWD_RING ? 3 : 2;
+  constexpr int NT = 3;
 #pragma unroll
   for (int k = 0; k < NT; ++k) zero_halo_cols<C, W>(lds + k * TILE, BR + 2, tid, 64 * NW);
   constexpr int IPR = W / G::PPI;  // DMA pieces per row
@@ -1147,7 +1103,6 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
     }
   };
   adv(xl, xn, xb);
-  stagger_start(ASR_FWD_STAGGER);
   dma_rows<C, W>(x0, lds, cn, -1, min(BR, H) + 2, H, wave, NW, lane);
   int nst = 0;
   const int total = (RK2 ? 2 : 1) * L * per;
@@ -1169,15 +1124,6 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
       nxs = src_of(xl);
       if (xl == cl && xn == cn && xb == cb + 1) {
         ntile = nt + 2 * BD::ROWB, ngy0 = yy + 1, nrows = min(BR, H - yy);
-        if constexpr (!ASR_FWD_RING) {
-          const uint4* src = (const uint4*)(lds + buf * TILE + BR * BD::ROWB);
-          uint4* dst = (uint4*)nt;
-          constexpr int NCH = 2 * W * NQ;
-          for (int i = tid; i < NCH; i += 64 * NW) {
-            const int o = ((i / (W * NQ)) * TW + 1) * NQ + i % (W * NQ);
-            dst[o] = src[o];
-          }
-        }
       } else {
         ntile = nt, ngy0 = yy - 1, nrows = min(BR, H - yy) + 2;
       }
@@ -1187,7 +1133,7 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
     if (wave == 0) ASR_BTR(0, 0, it, 2);
     const unsigned tb = lds_u32(lds + buf * TILE);
     // input rows 0, 1: the previous band's tile rows BR, BR+1 when this band continues its image
-    const unsigned th = (ASR_FWD_RING && cb > 0) ? lds_u32(lds + pbuf * TILE) + (unsigned)(BR * BD::ROWB) : tb;
+    const unsigned th = cb > 0 ? lds_u32(lds + pbuf * TILE) + (unsigned)(BR * BD::ROWB) : tb;
     f32x4 acc[RB][2];
 #pragma unroll
     for (int r = 0; r < RB; ++r)
@@ -1235,15 +1181,11 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
         constexpr int d = decltype(dc)::value;
         const int ra = max(__float_as_int(z[2 * d]), 0), rb = max(__float_as_int(z[2 * d + 1]), 0);
         yw[d] = pk_bf16(fmaf(hst, __int_as_float(ra), lo_f(xr[r][d])), fmaf(hst, __int_as_float(rb), hi_f(xr[r][d])));
-        if constexpr (ASR_FWD_PKMASK) {  // bits 2d (low half) and 2d+1 (high half) of a pair word
-          const unsigned pw = bits01_pair(ra, rb);
-          bits = d == 0 ? pw : lshl_or<2 * d>(pw, bits);
-        } else {
-          bits = d == 0 ? bit01(ra) : lshl_or<2 * d>(bit01(ra), bits);
-          bits = lshl_or<2 * d + 1>(bit01(rb), bits);
-        }
+        // relu-mask bits two at a time: [ra > 0] at bit 2d, [rb > 0] at bit 16 + 2d
+        const unsigned pw = bits01_pair(ra, rb);
+        bits = d == 0 ? pw : lshl_or<2 * d>(pw, bits);
       });
-      if constexpr (ASR_FWD_PKMASK) bits = pair_bits_to_byte(bits);
+      bits = pair_bits_to_byte(bits);
       if (hasm) {
         __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bits, mrs, (int)lm, r * W * (C / 8), 0);
         ++nst;
@@ -2354,7 +2296,7 @@ typedef __attribute__((address_space(1))) float gf32;
 // compile-time: acc[a][b] / acc[4+a][b] hold tiles (perm(a), perm(b)).
 using PairSlab = PairSlabLayout;
 constexpr int cmin(int a, int b) { return a < b ? a : b; }
-// the pipelined pair wgrad (k_bwd3_stack, ASR_BWD_PF): the last of a row's 12 fragments MFMA group g uses
+// the pipelined pair wgrad (k_bwd3_stack): the last of a row's 12 fragments MFMA group g uses
 constexpr int pf_last(int g) { return g == 0 ? 2 : g == 1 ? 3 : g == 2 ? 5 : g + 3; }  // (asr_common.h: the layout and the projection's pair_encode)
 struct PairRole {
   // one wave-uniform word (the wgrad role sits at the SGPR limit): bits 0-7 perm(0..3),
@@ -2472,7 +2414,6 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
   };
   __syncthreads();
   if (n0 >= n1) return;  // (uniform per workgroup: never with grid <= N)
-  stagger_start(ASR_BWD_STAGGER);
   ASR_BCLK(1, 0);
 
   constexpr int ES = PAIR ? PairSlab::ES : 9 * C * C + C, ECH = ES / 4;
@@ -2509,18 +2450,6 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
 #pragma unroll
         for (int r = 0; r < (RK2 ? BR : 1); ++r)
           exv[r] = *(const u32x4*)((const unsigned char*)(eb + (long)min(r, rows - 1) * W * C) + ldx);
-      }
-      if (ASR_BWD_XDG == 2 && !RK2 && it + 1 < total) {
-        // the next item's x rows by LDS-DMA from these waves before their conv (the wgrad
-        // waves then issue only their dy rows); older than this item's dx stores, so the
-        // next barrier_vm(nst) retires them
-        Cur nx = cur;
-        adv(nx);
-        const int xr0 = cur.b + 1 < nb ? 2 : 0;
-        const bf16* xsrc = x_of(nx.l);
-        const unsigned xtile = lds0 + (unsigned)(LL::X + (buf ^ 1) * LL::TILE + xr0 * LL::ROWB);
-        for (int j = __builtin_amdgcn_readfirstlane(wave); j < (BR + 2 - xr0) * IPR; j += 4)
-          dma_row_instr_at<C, W>(xsrc, xtile, nx.n, nx.b * BR - 1 + xr0, j, H, loff);
       }
       f32x4 acc[BR][2];
 #pragma unroll
@@ -2619,7 +2548,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         }
       }
       nst = nld;
-      if (ASR_BWD_HALO_DG && !RK2 && cur.b + 1 < nb) {  // (RK2: the wgrad waves; its dgrad role has no registers to spare)
+      if (!RK2 && cur.b + 1 < nb) {  // (RK2: the wgrad waves copy them; its dgrad role has no registers to spare)
         // the next item continues this image: its tile rows 0, 1 are this band's rows BR, BR+1
         // (dz, x; dy row 1 only), copied here, where the dgrad waves would otherwise wait at
         // the band barrier for the wgrad waves.  Rows BR, BR+1 of this item's tiles were
@@ -2640,28 +2569,12 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
                     lds_ld128(base + sreg + buf * LL::TILE + srow * LL::ROWB + o));
         }
       }
-      if (ASR_BWD_XDG == 1 && !RK2 && it + 1 < total) {  // (RK2: the wgrad waves, as the halo copy)
-        // the next item's x rows (all 6, or rows 2.. when it continues this image) by LDS-DMA
-        // from these waves, idle until the band barrier, instead of the wgrad waves, whose
-        // MFMAs then start one DMA burst earlier.  Into the other buffer, which no wave reads
-        // in this band; the next barrier waits for every vector-memory op of these waves
-        // (nst = 0), so the rows have landed before any wave reads them
-        Cur nx = cur;
-        adv(nx);
-        const int xr0 = cur.b + 1 < nb ? 2 : 0;
-        const bf16* xsrc = x_of(nx.l);
-        const unsigned xtile = lds0 + (unsigned)(LL::X + (buf ^ 1) * LL::TILE + xr0 * LL::ROWB);
-        for (int j = __builtin_amdgcn_readfirstlane(wave); j < (BR + 2 - xr0) * IPR; j += 4)
-          dma_row_instr_at<C, W>(xsrc, xtile, nx.n, nx.b * BR - 1 + xr0, j, H, loff);
-        nst = 0;
-      }
       if (wave == 0) ASR_BTR(1, 0, it, 3);
       adv(cur);
     }
     barrier_vm(0);  // matches the wgrad waves' end-of-loop barrier
   } else {
     // ---------------- wgrad waves ----------------
-    if (ASR_BWD_WPRIO) __builtin_amdgcn_s_setprio(ASR_BWD_WPRIO);
     const int w8 = __builtin_amdgcn_readfirstlane(wave) - 4;
     const int tg = w8 >> 1, oq = 2 * (w8 & 1);
     const int tq = lx >> 2, tp = lx & 3;
@@ -2857,7 +2770,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       const bool syn = orow >= 0 && synth(nxt);
       if (syn) synth_row(nxt, orow, buf ^ 1);
       const int ndy = orow >= 0 && !syn ? IPR : 0;
-      const int nx = (!(ASR_BWD_XDG && !RK2) && more && w8 >= 4) ? ((BR + 2 - xr0) * IPR - (w8 - 4) + 3) / 4 : 0;
+      const int nx = (more && w8 >= 4) ? ((BR + 2 - xr0) * IPR - (w8 - 4) + 3) / 4 : 0;
       const int npc = ndy + nx;
       int ipc = 0;
       const bf16* nxdy = dy_of(nxt.l);
@@ -2872,12 +2785,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         }
         ++ipc;
       };
-      // ASR_BWD_XLATE: only the own dy row up front; the next band's x rows after the MFMA band
-      // (the waves that issue them, w8 >= 4, have no own row in a band that continues an image)
-      if (ASR_BWD_XLATE && PAIR && ASR_BWD_PF)
-        while (ipc < ndy) piece();
-      else
-        while (ipc < npc && ipc < ASR_BWD3_DMA0) piece();
+      while (ipc < npc && ipc < ASR_BWD3_DMA0) piece();
       if (wave == 4) ASR_BTR(1, 1, it, 2);
       bf16x8 Bf[2], Ar[3];
       auto mfma_band_full = [&](auto bo) {
@@ -2911,23 +2819,23 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         });
       };
       // pair-local tiling (PairRole): per row, phase 1 the transposed products of tap 8-t
-      // (A = dz(perm[a]), B = x(8-t, perm[b]): acc[4 + a][b] = dW[8-t]^T tiles) and the
-      // tap-4 partner's, phase 2 the direct products of tap t (A = x(t, perm[a]),
-      // B = dz(perm[b]): acc[a][b]) and the tap-4 tile; D = acc[a][b] - acc[4 + a][b]
-      // leaves at the block's end
-      // Pipelined form (ASR_BWD_PF): the band's 4 x 12 operand fragments are one read
-      // stream, each read issued ASR_BWD_PFD fragments ahead of the MFMA group that
-      // first uses it, across the row boundaries (the transposed reads are compiler-
-      // visible builtins: hipcc places their waits); row r's fragments in use order:
+      // (A = dz(perm[a]), B = -x(8-t, perm[b]): -dW[8-t]^T tiles) and the tap-4 partner's,
+      // phase 2 the direct products of tap t (A = x(t, perm[a]), B = dz(perm[b])) and the
+      // tap-4 tile, both into acc[a][b], which holds D = X - Y^T at the block's end.
+      // The band's 4 x 12 operand fragments are one read stream, each read issued P = 3
+      // fragments ahead of the MFMA group that first uses it, across the row boundaries
+      // (the transposed reads are compiler-visible builtins: hipcc places their waits; a
+      // version reading each row's fragments at the row's start ran its MFMA phase 0.5-0.6 k
+      // cycles longer per band); row r's fragments in use order:
       //   0 dz(p0) 1 x(8-t, p0) 2 x(8-t, p1) 3 dz(p1) 4 dz(p2) 5 x(4, v1) 6 dz(p3)
       //   7..10 x(t, p0..p3) 11 x(4, u0)
-      // The registers come from the transposed tiles' accumulators: their products enter
-      // acc[a][b] with the x(8-t) operand negated (bf16 sign flips, exact), so acc[a][b]
-      // holds D = X - Y^T itself (acc[4..7] unused).  No row guard: rows past `rows` (the
+      // The registers of the stream come from accumulating the transposed products into
+      // acc[a][b] with the x(8-t) operand negated (bf16 sign flips, exact) instead of into
+      // separate Y^T tiles: 40 accumulator VGPRs instead of 72 (acc[4..7] unused).  No row guard: rows past `rows` (the
       // image's last band when H % 4 != 0) are outside the image, where the dz tile is
       // zero (zero-page DMA, zero mask words), so their products add zeros.
-      auto mfma_band_pair_pf = [&](auto bo, auto&& mid) {
-        constexpr int BO = decltype(bo)::value, NF = 12, P = ASR_BWD_PFD;
+      auto mfma_band_pair = [&](auto bo) {
+        constexpr int BO = decltype(bo)::value, NF = 12, P = 3;
         bf16x8 F[BR * NF];  // compile-time indices only: registers, allocated by liveness
         auto rd = [&](auto jc) {
           constexpr int j = decltype(jc)::value, k = j % NF, R = BO + (j / NF) * LL::ROWB;
@@ -2972,69 +2880,21 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
               }
             }
             // DMA pieces left after the first ASR_BWD3_DMA0: two per row group 3 and 7
-            if constexpr (!ASR_BWD_XLATE && (g == 3 || g == 7) && r < BR - 1) {
+            if constexpr ((g == 3 || g == 7) && r < BR - 1) {
               if (ipc < npc) piece();
             }
-            if constexpr (g == 8 && r == ASR_BWD_CVROW) mid();
           });
         });
       };
-      auto mfma_band_pair = [&](auto bo) {
-        constexpr int BO = decltype(bo)::value;
-        static_for<0, BR>([&](auto rc) {
-          constexpr int r = decltype(rc)::value, RO_ = BO + r * LL::ROWB;
-          __builtin_amdgcn_sched_barrier(0);
-          if (r < rows) {
-            const bf16x8 x8a = tr_pair_px<RO_>(offA[1]), x8b = tr_pair_px<RO_>(offA[2]);
-            bf16x8 dz[4];
-            dz[0] = tr_pair_px<RO_>(offB[0] ^ pr.sh(0));
-            dz[1] = tr_pair_px<RO_>(offB[0] ^ pr.sh(1));
-            const bf16x8 x4v = tr_pair_px<RO_>(offA[4]);
-            static_for<0, 4>([&](auto ac) {
-              constexpr int a = decltype(ac)::value;
-              if constexpr (a >= 2) dz[a] = tr_pair_px<RO_>(offB[0] ^ pr.sh(a));
-              acc[4 + a][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dz[a], x8a, acc[4 + a][0], 0, 0, 0);
-              acc[4 + a][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dz[a], x8b, acc[4 + a][1], 0, 0, 0);
-              if constexpr (a == 2) {  // tap-4 transposed product: dz(perm[s1]) x x(4, v1)
-                const bf16x8 sel = pr.s1_is_2() ? dz[2] : dz[1];
-                acc[8][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, x4v, acc[8][1], 0, 0, 0);
-              }
-            });
-            bf16x8 xa[2];
-            xa[0] = tr_pair_px<RO_>(offA[0] ^ pr.sh(0));
-            static_for<0, 4>([&](auto ac) {
-              constexpr int a = decltype(ac)::value;
-              if constexpr (a + 1 < 4) xa[(a + 1) & 1] = tr_pair_px<RO_>(offA[0] ^ pr.sh(a + 1));
-              else xa[0] = tr_pair_px<RO_>(offA[3]);  // x(4, u0)
-              acc[a][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[a & 1], dz[0], acc[a][0], 0, 0, 0);
-              acc[a][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[a & 1], dz[1], acc[a][1], 0, 0, 0);
-            });
-            acc[8][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[0], dz[0], acc[8][0], 0, 0, 0);
-            if (dbw) {
-#pragma unroll
-              for (int oi = 0; oi < 2; ++oi)
-                accb[oi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, dz[oi], accb[oi], 0, 0, 0);
-            }
-            if (r < BR - 1 && ipc < npc) piece();
-          }
-        });
-      };
-      // ASR_BWD_CVROW >= 0: the next band's dz convert of this wave's own row runs after
-      // row ASR_BWD_CVROW's MFMAs instead of after the band, so it overlaps the MFMAs of the
-      // SIMD's other wgrad wave (which has no own row in a band that continues an image)
-      auto convert_next = [&]() {
+      auto convert_next = [&]() {  // the next band's dz of this wave's own row
         if (more) {
           while (ipc < npc) piece();
           vm_wait(0);  // own dy row and mask dwords of band it+1 (x DMA and fold loads too)
           convert_own(orow, buf ^ 1, mwv);
         }
       };
-      constexpr bool CV_MID = PAIR && ASR_BWD_PF && ASR_BWD_CVROW >= 0;
       auto mfma_band = [&](auto bo) {
-        if constexpr (PAIR && ASR_BWD_PF) {
-          if constexpr (CV_MID) mfma_band_pair_pf(bo, convert_next);
-          else mfma_band_pair_pf(bo, [] {});
-        } else if constexpr (PAIR) mfma_band_pair(bo);
+        if constexpr (PAIR) mfma_band_pair(bo);
         else mfma_band_full(bo);
       };
       if (it > 0) {
@@ -3044,63 +2904,12 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
 #pragma unroll
         for (int k = 0; k < NOB; ++k) offB[k] += dlt;
       }
-      // block l's dW tiles and db (write-through stores; the next band barrier drains them).
-      // ASR_BWD_SLAB_EARLY (Euler): issued right after the block's last MFMA band, before the
-      // convert's wait for the next band's DMA, so the burst drains in that wait's shadow
-      // instead of at the next barrier
-      constexpr bool SLAB_EARLY = ASR_BWD_SLAB_EARLY && !RK2;
-      auto publish = [&]() {
-          // publish block l's dW tiles and db (write-through; drained at the next band barrier)
-          float* slab = slabs + (long)l * slab_stride + (long)blockIdx.x * ES;
-          const auto rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, ES * 4, 0x00020000);
-          auto put = [&](int tile, f32x4 v) {
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, ((tile * 64 + lane) * 4) * 4, 0, 16);
-          };
-          if constexpr (PAIR) {  // D = X - Y^T per pair tile: 8 (+1 or 2 tap-4) tiles of the 74
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-              for (int b = 0; b < 2; ++b)
-                put(pr.tile(a, b), (ASR_BWD_PF ? acc[a][b] : acc[a][b] - acc[4 + a][b]) * hsb);
-            if (pr.self()) {
-              put(PairSlab::kSelf + pr.perm(0), acc[8][0] * hsb);  // raw X(4, c, c), c even
-              put(PairSlab::kSelf + pr.perm(1), acc[8][1] * hsb);  // X(4, c, c)^T, c odd
-            } else {
-              put(PairSlab::kTap4 + pr.k4(), (acc[8][0] - acc[8][1]) * hsb);
-            }
-#pragma unroll
-            for (int mi = 0; mi < MTW; ++mi) acc[mi][0] = acc[mi][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-          } else {
-#pragma unroll
-            for (int mi = 0; mi < MTW; ++mi)
-#pragma unroll
-              for (int oi = 0; oi < 2; ++oi) {
-                const int mt = tg * MTW + mi;
-                put(mt * 4 + oq + oi, acc[mi][oi] * hsb);
-                acc[mi][oi] = f32x4{0.f, 0.f, 0.f, 0.f};
-              }
-          }
-          if (dbw) {
-            if (g == 0) {
-#pragma unroll
-              for (int oi = 0; oi < 2; ++oi) {
-                const int ob = PAIR ? pr.perm(oi) : oq + oi;
-                __hip_atomic_store((gf32*)(slab + (ES - C) + 16 * ob + lx), hsb * accb[oi][0], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-              }
-            }
-            accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-      };
       mfma_band(std::integral_constant<int, 0>{});
       while (ipc < npc) piece();
-      if constexpr (SLAB_EARLY) {
-        if (cur.b == nb - 1 && cur.n == n1 - 1) publish();  // (Euler: the stage is the block)
-      }
       if (wave == 4) ASR_BTR(1, 1, it, 3);
-      if (!CV_MID) convert_next();
+      convert_next();
       if (wave == 4) ASR_BTR(1, 1, it, 4);
-      if (!(ASR_BWD_HALO_DG && !RK2) && cont) {  // halo rows of the next band of this image
+      if (RK2 && cont) {  // halo rows of the next band of this image (Euler: the dgrad waves copy them)
         // compiler-visible LDS accesses: the item's DMAs were retired by the vm_wait(0)
         // before the convert (cont implies more), so hipcc's own waits cost nothing
         // here, and a copied or spilled read result stays correct
@@ -3136,48 +2945,46 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       }
       if (last_of_block) {
         if (l + 2 < L && l + 2 >= lfold) fold_end(l + 2);
-        if constexpr (!SLAB_EARLY) {
-          // publish block l's dW tiles and db (write-through; drained at the next band barrier)
-          float* slab = slabs + (long)l * slab_stride + (long)blockIdx.x * ES;
-          const auto rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, ES * 4, 0x00020000);
-          auto put = [&](int tile, f32x4 v) {
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, ((tile * 64 + lane) * 4) * 4, 0, 16);
-          };
-          if constexpr (PAIR) {  // D = X - Y^T per pair tile: 8 (+1 or 2 tap-4) tiles of the 74
+        // publish block l's dW tiles and db (write-through; drained at the next band barrier)
+        float* slab = slabs + (long)l * slab_stride + (long)blockIdx.x * ES;
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, ES * 4, 0x00020000);
+        auto put = [&](int tile, f32x4 v) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, ((tile * 64 + lane) * 4) * 4, 0, 16);
+        };
+        if constexpr (PAIR) {  // D = X - Y^T per pair tile: 8 (+1 or 2 tap-4) tiles of the 74
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
+          for (int a = 0; a < 4; ++a)
 #pragma unroll
-              for (int b = 0; b < 2; ++b)
-                put(pr.tile(a, b), (ASR_BWD_PF ? acc[a][b] : acc[a][b] - acc[4 + a][b]) * hsb);
-            if (pr.self()) {
-              put(PairSlab::kSelf + pr.perm(0), acc[8][0] * hsb);  // raw X(4, c, c), c even
-              put(PairSlab::kSelf + pr.perm(1), acc[8][1] * hsb);  // X(4, c, c)^T, c odd
-            } else {
-              put(PairSlab::kTap4 + pr.k4(), (acc[8][0] - acc[8][1]) * hsb);
-            }
-#pragma unroll
-            for (int mi = 0; mi < MTW; ++mi) acc[mi][0] = acc[mi][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int b = 0; b < 2; ++b)
+              put(pr.tile(a, b), acc[a][b] * hsb);
+          if (pr.self()) {
+            put(PairSlab::kSelf + pr.perm(0), acc[8][0] * hsb);  // raw X(4, c, c), c even
+            put(PairSlab::kSelf + pr.perm(1), acc[8][1] * hsb);  // X(4, c, c)^T, c odd
           } else {
-#pragma unroll
-            for (int mi = 0; mi < MTW; ++mi)
-#pragma unroll
-              for (int oi = 0; oi < 2; ++oi) {
-                const int mt = tg * MTW + mi;
-                put(mt * 4 + oq + oi, acc[mi][oi] * hsb);
-                acc[mi][oi] = f32x4{0.f, 0.f, 0.f, 0.f};
-              }
+            put(PairSlab::kTap4 + pr.k4(), (acc[8][0] - acc[8][1]) * hsb);
           }
-          if (dbw) {
-            if (g == 0) {
 #pragma unroll
-              for (int oi = 0; oi < 2; ++oi) {
-                const int ob = PAIR ? pr.perm(oi) : oq + oi;
-                __hip_atomic_store((gf32*)(slab + (ES - C) + 16 * ob + lx), hsb * accb[oi][0], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-              }
+          for (int mi = 0; mi < MTW; ++mi) acc[mi][0] = acc[mi][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        } else {
+#pragma unroll
+          for (int mi = 0; mi < MTW; ++mi)
+#pragma unroll
+            for (int oi = 0; oi < 2; ++oi) {
+              const int mt = tg * MTW + mi;
+              put(mt * 4 + oq + oi, acc[mi][oi] * hsb);
+              acc[mi][oi] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
-            accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        if (dbw) {
+          if (g == 0) {
+#pragma unroll
+            for (int oi = 0; oi < 2; ++oi) {
+              const int ob = PAIR ? pr.perm(oi) : oq + oi;
+              __hip_atomic_store((gf32*)(slab + (ES - C) + 16 * ob + lx), hsb * accb[oi][0], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+            }
           }
+          accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
       if (wave == 4) ASR_BTR(1, 1, it, 5);
@@ -3628,7 +3435,7 @@ int block_stack_fwd_mfma(const void* x0, void* ys, long y_stride, uint8_t* masks
   int cus = cu_count();
   if (cus <= 0) cus = 256;
   const int grid = std::max(1, std::min(N, 2 * cus));
-  const size_t lds = (ASR_FWD_RING ? 3 : 2) * (size_t)(kFwdBR + 2) * (W + 2) * C * 2;  // k_fwd3_stack's tiles
+  const size_t lds = 3 * (size_t)(kFwdBR + 2) * (W + 2) * C * 2;  // k_fwd3_stack's ring of three tiles
   hipLaunchKernelGGL((blk::k_fwd3_stack<64, 32, kFwdBR>), dim3(grid), dim3(256), lds, s, (const bf16*)x0,
                      (bf16*)ys, y_stride, masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, H, L,
                      slots);
@@ -3777,7 +3584,7 @@ int block_stack_fwd_rk2_mfma(const void* x0, void* ys, void* xm, long y_stride, 
   int cus = cu_count();
   if (cus <= 0) cus = 256;
   const int grid = std::max(1, std::min(N, 2 * cus));
-  const size_t lds = (ASR_FWD_RING ? 3 : 2) * (size_t)(kFwdBR + 2) * (W + 2) * C * 2;  // k_fwd3_stack's tiles
+  const size_t lds = 3 * (size_t)(kFwdBR + 2) * (W + 2) * C * 2;  // k_fwd3_stack's ring of three tiles
   hipLaunchKernelGGL((blk::k_fwd3_stack<64, 32, kFwdBR, true>), dim3(grid), dim3(256), lds, s, (const bf16*)x0,
                      (bf16*)ys, y_stride, masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, H, L, 0,
                      (bf16*)xm, masks2);
