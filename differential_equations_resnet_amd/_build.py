@@ -15,7 +15,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libasr.so")
-SOURCES = ["asr_theta.hip", "asr_block_mfma.hip", "asr_conv_f32.hip", "asr_stem_head.hip", "asr_api.hip", "asr_dist.hip", "asr_deep16.hip"]
+SOURCES = ["asr_theta.hip", "asr_block_mfma.hip", "asr_conv_f32.hip", "asr_stem_head.hip", "asr_api.hip", "asr_dist.hip", "asr_deep16.hip", "asr_stages.hip"]
 HEADERS = ["asr_common.h", "asr_device.h", os.path.join("..", "..", "include", "asr.h")]
 ARCH = "gfx950"
 

@@ -29,7 +29,7 @@ ASR_BF16 = 1
 ASR_PARAM_3BY3 = 0
 ASR_PARAM_GENERAL = 1
 ASR_PARAM_REGULAR = 2
-ABI_VERSION = 6
+ABI_VERSION = 7
 ASR_MODE_EULER = 0
 ASR_MODE_CONV = 1
 ASR_INTEGRATOR_EULER = 0
@@ -44,6 +44,7 @@ ASR_VARIANT_TIMED = 64
 ASR_VARIANT_FULL_DXL = 128
 ASR_VARIANT_FULL_SLABS = 256
 ASR_DIST_UNIQUE_ID_BYTES = 128
+ASR_STAGES_MAX = 8
 
 
 class AsrError(RuntimeError):
@@ -60,6 +61,16 @@ class NetConfig(ct.Structure):
         ("num_classes", ct.c_int), ("h", ct.c_float), ("gamma", ct.c_float), ("subtract_mean", ct.c_float),
         ("divide_by_stddev", ct.c_float), ("use_norm", ct.c_int), ("dtype", ct.c_int), ("input_u8", ct.c_int),
         ("param_kind", ct.c_int), ("antisymmetric", ct.c_int), ("integrator", ct.c_int), ("variant", ct.c_int),
+    ]
+
+
+class StagesConfig(ct.Structure):
+    """asr_stages_config (include/asr.h, ABI 7)."""
+    _fields_ = [
+        ("N", ct.c_int), ("H", ct.c_int), ("W", ct.c_int), ("Cin", ct.c_int), ("num_classes", ct.c_int),
+        ("n_stages", ct.c_int), ("C", ct.c_int * 8), ("L", ct.c_int * 8), ("stride", ct.c_int * 8),
+        ("h", ct.c_float), ("gamma", ct.c_float), ("subtract_mean", ct.c_float), ("divide_by_stddev", ct.c_float),
+        ("use_norm", ct.c_int), ("input_u8", ct.c_int), ("param_kind", ct.c_int), ("antisymmetric", ct.c_int),
     ]
 
 
@@ -113,6 +124,14 @@ SIGNATURES = [
     ("asr_rk2_stack_backward_workspace_bytes", _S, [_I, _I, _I, _I, _I, _I]),
     ("asr_rk2_stack_backward", _I, [_P, _P, _P, _L, _P, _P, _L, _P, _L, _P, _L, _F, _F, _I, _I, _I, _I, _I, _I, _P,
                                     _P, _P, _S, _P]),
+    ("asr_transition_forward", _I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    ("asr_transition_backward_workspace_bytes", _S, [_I, _I, _I, _I, _I, _I]),
+    ("asr_transition_backward", _I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _S, _P]),
+    ("asr_stages_param_count", _L, [ct.POINTER(StagesConfig)]),
+    ("asr_stages_workspace_bytes", _S, [ct.POINTER(StagesConfig)]),
+    ("asr_stages_prepare", _I, [ct.POINTER(StagesConfig), _P, _S]),
+    ("asr_stages_forward", _I, [ct.POINTER(StagesConfig), _P, _P, _P, _P, _S, _P]),
+    ("asr_stages_forward_backward", _I, [ct.POINTER(StagesConfig), _P, _P, _P, _P, _P, _P, _P, _S, _P]),
     ("asr_adam_update", _I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _L, _F, _P]),
     ("asr_segment_sq_norms", _I, [_P, _P, _I, _P, _P]),
     ("asr_batch_metrics", _I, [_P, _P, _P, _I, _I, _P, _P]),

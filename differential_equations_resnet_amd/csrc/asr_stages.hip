@@ -1,0 +1,585 @@
+// Multi-stage single-block ResNet (ABI 7, include/asr.h "Multi-stage"): the
+// stage transition single_layer_conv_block (models/tfkeras_resnets.py:204-269)
+// as fp32 kernels, and the executor of get_single_block_resnet_build_function
+// with num_stages > 2 (tfkeras_resnets.py:547-597, e.g. the He-style ResNet-32:
+// [10, 10, 10] blocks at 32^2 x 16, 16^2 x 32, 8^2 x 64).
+//
+// The identity blocks of every stage run the fp32 block kernels of the
+// single-stage executor (asr_conv_forward / asr_conv_backward: fp32 MFMA at
+// W = 32, C in {16, 32, 64}, the fp32 VALU kernel at the smaller stages); the
+// stem and head are the single-stage executor's kernels.
+//
+// Transition, for output pixel p = (n, yo, xo) and channel o (stride S, TF
+// 'same' padding for the 3x3: pad_top = ((Ho-1)S + 3 - H) / 2, the remainder
+// at the bottom / right; the 1x1 is 'valid', i.e. it reads input (S yo, S xo)):
+//     z  = b2[o] + sum_{ky,kx,i} x[S yo + ky - pt][S xo + kx - pl][i] K2[ky][kx][i][o]
+//     y  = relu(z) + b1[o] + sum_i x[S yo][S xo][i] K1[i][o]
+// Backward (dz = dy [z > 0]):
+//     dx[gy][gx][i] = sum_{ky,kx: gy + pt - ky = S yo, gx + pl - kx = S xo} sum_o dz[yo][xo][o] K2[ky][kx][i][o]
+//                   + [S | gy, S | gx] sum_o dy[gy/S][gx/S][o] K1[i][o]
+//     dK2[ky][kx][i][o] = sum_p x[S yo + ky - pt][S xo + kx - pl][i] dz[p][o],  db2 = sum_p dz
+//     dK1[i][o]         = sum_p x[S yo][S xo][i] dy[p][o],                     db1 = sum_p dy
+// These convolutions carry ~2 % of a ResNet-32 step's FLOPs (two transitions
+// against 28 identity blocks), so they stay on the VALU: one lane per (pixel,
+// 4 output channels) in the forward, per (input pixel, channel) in dgrad, per
+// weight element over a chunk of output rows in wgrad (partials reduced by one
+// more launch).
+#include <algorithm>
+#include <vector>
+
+#include "asr_common.h"
+
+namespace asr {
+// asr_theta.hip
+long theta_count(int C, int kind, int antisymmetric);
+int param_map(int C, int kind, int antisymmetric, int32_t* w_src, int32_t* theta_dst);
+int param_is_antisymmetric(int kind, int antisymmetric);
+int param_map_transpose(int C, const int32_t* w_src, int32_t* w_bwd);
+int reduce_and_project(const float* slabs, int P, long E, int Cb, const int32_t* theta_dst, long n_theta,
+                       float* dtheta, float* dbias, float* dw_out, float* ws, hipStream_t s);
+size_t reduce_ws_bytes(int P, long ES);
+// asr_stem_head.hip
+bool stem_supported(int Cin, int H, int W, int C);
+int stem_forward(const void* img, int input_u8, const float* w1, const float* b1, int N, int H, int W, int Cin, int C,
+                 float mean, float inv_std, int use_norm, void* out, int out_bf16, hipStream_t s);
+int stem_wgrad(const void* img, int input_u8, const void* dx1, const void* x1, int act_bf16, int N, int H, int W,
+               int Cin, int C, float mean, float inv_std, int use_norm, float* slabs, int* nslabs, hipStream_t s);
+int head(const void* xL, int act_bf16, const float* fck, const float* fcb, const float* targets, int N, int HW, int C,
+         int K, float* probs, float* loss_per, float* dlogits, float* gap, void* dxL, hipStream_t s,
+         void* growL = nullptr);
+int head_param_grads(const float* gap, const float* dlogits, int N, int C, int K, float* dfck, float* dfcb,
+                     const float* loss_per, float* loss_out, hipStream_t s);
+
+namespace {
+
+constexpr int kTK = 3;              // the transition's kxk (the builder's kernel_size; 3 in every reference config)
+constexpr int kMaxTransChunks = 256;  // wgrad row chunks
+constexpr int kMaxStemSlabs = 512;    // asr_stem_head.hip stem_grid bound
+
+struct TGeom {
+  int Ho, Wo, pt, pl;
+};
+TGeom tgeom(int H, int W, int S) {
+  TGeom g;
+  g.Ho = (H + S - 1) / S;
+  g.Wo = (W + S - 1) / S;
+  g.pt = std::max((g.Ho - 1) * S + kTK - H, 0) / 2;
+  g.pl = std::max((g.Wo - 1) * S + kTK - W, 0) / 2;
+  return g;
+}
+long trans_param_floats(int Ci, int Co) { return (long)kTK * kTK * Ci * Co + Co + (long)Ci * Co + Co; }
+
+// one wave = (n, yo, 16-pixel tile, 16-channel tile); lane (lx, g): pixel 16 pt + lx, channels o0 .. o0 + 3
+__global__ __launch_bounds__(256) void k_trans_fwd(const float* __restrict__ x, float* __restrict__ y,
+                                                   uint8_t* __restrict__ mask, const float* __restrict__ k2,
+                                                   const float* __restrict__ b2, const float* __restrict__ k1,
+                                                   const float* __restrict__ b1, int N, int H, int W, int Ci, int Co,
+                                                   int S, int Ho, int Wo, int pt, int pl) {
+  const int PT = (Wo + 15) / 16, OT = (Co + 15) / 16;
+  const long tasks = (long)N * Ho * PT * OT;
+  const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (task >= tasks) return;
+  const int lane = threadIdx.x & 63, g = lane >> 4, lx = lane & 15;
+  const int ot = (int)(task % OT);
+  long rest = task / OT;
+  const int ptile = (int)(rest % PT);
+  rest /= PT;
+  const int yo = (int)(rest % Ho);
+  const int n = (int)(rest / Ho);
+  const int xo = 16 * ptile + lx, o0 = 16 * ot + 4 * g;
+  if (xo >= Wo || o0 >= Co) return;
+  const int no = min(4, Co - o0);
+  float z[4] = {0.f, 0.f, 0.f, 0.f}, sc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int ky = 0; ky < kTK; ++ky) {
+    const int gy = S * yo + ky - pt;
+    if (gy < 0 || gy >= H) continue;
+    for (int kx = 0; kx < kTK; ++kx) {
+      const int gx = S * xo + kx - pl;
+      if (gx < 0 || gx >= W) continue;
+      const float* xp = x + (((long)n * H + gy) * W + gx) * Ci;
+      const float* wp = k2 + (long)(ky * kTK + kx) * Ci * Co + o0;
+      for (int i = 0; i < Ci; ++i) {
+        const float xv = xp[i];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (e < no) z[e] = fmaf(xv, wp[(long)i * Co + e], z[e]);
+      }
+    }
+  }
+  {
+    const float* xp = x + (((long)n * H + S * yo) * W + S * xo) * Ci;
+    for (int i = 0; i < Ci; ++i) {
+      const float xv = xp[i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (e < no) sc[e] = fmaf(xv, k1[(long)i * Co + o0 + e], sc[e]);
+    }
+  }
+  const long p = ((long)n * Ho + yo) * Wo + xo;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (e >= no) continue;
+    const int o = o0 + e;
+    const float zz = z[e] + b2[o];
+    y[p * Co + o] = fmaxf(zz, 0.f) + (sc[e] + b1[o]);
+    if (mask) mask[p * Co + o] = zz > 0.f ? 1 : 0;
+  }
+}
+
+// one thread per (n, gy, gx, i)
+__global__ __launch_bounds__(256) void k_trans_dgrad(const float* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                     const float* __restrict__ k2, const float* __restrict__ k1,
+                                                     float* __restrict__ dx, int N, int H, int W, int Ci, int Co,
+                                                     int S, int Ho, int Wo, int pt, int pl) {
+  const long total = (long)N * H * W * Ci;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int i = (int)(idx % Ci);
+    long rest = idx / Ci;
+    const int gx = (int)(rest % W);
+    rest /= W;
+    const int gy = (int)(rest % H);
+    const int n = (int)(rest / H);
+    float acc = 0.f;
+    for (int ky = 0; ky < kTK; ++ky) {
+      const int ty = gy + pt - ky;
+      if (ty < 0 || ty % S) continue;
+      const int yo = ty / S;
+      if (yo >= Ho) continue;
+      for (int kx = 0; kx < kTK; ++kx) {
+        const int tx = gx + pl - kx;
+        if (tx < 0 || tx % S) continue;
+        const int xo = tx / S;
+        if (xo >= Wo) continue;
+        const long p = ((long)n * Ho + yo) * Wo + xo;
+        const float* dp = dy + p * Co;
+        const uint8_t* mp = mask + p * Co;
+        const float* wp = k2 + ((long)(ky * kTK + kx) * Ci + i) * Co;
+        for (int o = 0; o < Co; ++o)
+          if (mp[o]) acc = fmaf(dp[o], wp[o], acc);
+      }
+    }
+    if (gy % S == 0 && gx % S == 0 && gy / S < Ho && gx / S < Wo) {
+      const float* dp = dy + (((long)n * Ho + gy / S) * Wo + gx / S) * Co;
+      const float* wp = k1 + (long)i * Co;
+      for (int o = 0; o < Co; ++o) acc = fmaf(dp[o], wp[o], acc);
+    }
+    dx[idx] = acc;
+  }
+}
+
+// partial [dK2 | db2 | dK1 | db1] of one chunk of output rows (n, yo) per blockIdx.y
+__global__ __launch_bounds__(256) void k_trans_wgrad(const float* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                     const float* __restrict__ x, float* __restrict__ part, int N,
+                                                     int H, int W, int Ci, int Co, int S, int Ho, int Wo, int pt,
+                                                     int pl, int rows_per_chunk) {
+  const long E2 = (long)kTK * kTK * Ci * Co, E1 = (long)Ci * Co, ET = E2 + Co + E1 + Co;
+  const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e >= ET) return;
+  // decode the element: which sum, which operands
+  int kind, ky = 0, kx = 0, i = 0, o;
+  if (e < E2) {
+    kind = 0;
+    o = (int)(e % Co);
+    i = (int)((e / Co) % Ci);
+    const int tap = (int)(e / ((long)Ci * Co));
+    ky = tap / kTK;
+    kx = tap % kTK;
+  } else if (e < E2 + Co) {
+    kind = 1;
+    o = (int)(e - E2);
+  } else if (e < E2 + Co + E1) {
+    kind = 2;
+    const long f = e - E2 - Co;
+    o = (int)(f % Co);
+    i = (int)(f / Co);
+  } else {
+    kind = 3;
+    o = (int)(e - E2 - Co - E1);
+  }
+  const long R = (long)N * Ho;
+  const long r0 = (long)blockIdx.y * rows_per_chunk, r1 = min(R, r0 + rows_per_chunk);
+  float acc = 0.f;
+  for (long rr = r0; rr < r1; ++rr) {
+    const int yo = (int)(rr % Ho);
+    const int n = (int)(rr / Ho);
+    const float* dr = dy + rr * Wo * Co;
+    const uint8_t* mr = mask + rr * Wo * Co;
+    if (kind == 0) {
+      const int gy = S * yo + ky - pt;
+      if (gy < 0 || gy >= H) continue;
+      const float* xr = x + ((long)n * H + gy) * W * Ci;
+      for (int xo = 0; xo < Wo; ++xo) {
+        const int gx = S * xo + kx - pl;
+        if (gx < 0 || gx >= W) continue;
+        if (mr[(long)xo * Co + o]) acc = fmaf(xr[(long)gx * Ci + i], dr[(long)xo * Co + o], acc);
+      }
+    } else if (kind == 1) {
+      for (int xo = 0; xo < Wo; ++xo)
+        if (mr[(long)xo * Co + o]) acc += dr[(long)xo * Co + o];
+    } else if (kind == 2) {
+      const float* xr = x + ((long)n * H + S * yo) * W * Ci;
+      for (int xo = 0; xo < Wo; ++xo) acc = fmaf(xr[(long)S * xo * Ci + i], dr[(long)xo * Co + o], acc);
+    } else {
+      for (int xo = 0; xo < Wo; ++xo) acc += dr[(long)xo * Co + o];
+    }
+  }
+  part[(long)blockIdx.y * ET + e] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_sum_chunks(const float* __restrict__ part, int chunks, long E,
+                                                    float* __restrict__ out) {
+  const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  float acc = 0.f;
+  for (int c = 0; c < chunks; ++c) acc += part[(long)c * E + e];
+  out[e] = acc;
+}
+
+int trans_chunks(int N, int Ho, int* rpc) {
+  const long R = (long)N * Ho;
+  const long chunks = std::max<long>(1, std::min<long>(R, kMaxTransChunks));
+  *rpc = (int)((R + chunks - 1) / chunks);
+  return (int)((R + *rpc - 1) / *rpc);
+}
+
+int check_trans(int N, int H, int W, int Ci, int Co, int S) {
+  if (N < 1 || H < 1 || W < 1 || Ci < 1 || Co < 1 || (S != 1 && S != 2))
+    return fail(ASR_E_ARG, "transition: bad shape N=%d H=%d W=%d Ci=%d Co=%d stride=%d", N, H, W, Ci, Co, S);
+  if ((long)N * H * W * std::max(Ci, Co) > (1L << 40)) return fail(ASR_E_ARG, "transition: shape too large");
+  return ASR_OK;
+}
+
+int trans_forward(const float* x, float* y, uint8_t* mask, const float* k2, const float* b2, const float* k1,
+                  const float* b1, int N, int H, int W, int Ci, int Co, int S, hipStream_t s) {
+  const TGeom g = tgeom(H, W, S);
+  const long tasks = (long)N * g.Ho * ((g.Wo + 15) / 16) * ((Co + 15) / 16);
+  const long blocks = (tasks + 3) / 4;
+  if (blocks > 0x7fffffffL) return fail(ASR_E_ARG, "transition: problem too large");
+  hipLaunchKernelGGL(k_trans_fwd, dim3((unsigned)blocks), dim3(256), 0, s, x, y, mask, k2, b2, k1, b1, N, H, W, Ci,
+                     Co, S, g.Ho, g.Wo, g.pt, g.pl);
+  ASR_LAUNCH_CHECK("k_trans_fwd");
+  return ASR_OK;
+}
+
+size_t trans_ws_bytes(int N, int H, int W, int Ci, int Co, int S) {
+  int rpc = 0;
+  const int nch = trans_chunks(N, tgeom(H, W, S).Ho, &rpc);
+  return align_up((size_t)nch * trans_param_floats(Ci, Co) * 4, 256);
+}
+
+int trans_backward(const float* dy, const float* x, const uint8_t* mask, const float* k2, const float* k1, int N,
+                   int H, int W, int Ci, int Co, int S, float* dx, float* dparams, float* part, hipStream_t s) {
+  const TGeom g = tgeom(H, W, S);
+  if (dx) {
+    const long total = (long)N * H * W * Ci;
+    const unsigned grid = (unsigned)std::max<long>(1, std::min<long>((total + 255) / 256, 65536));
+    hipLaunchKernelGGL(k_trans_dgrad, dim3(grid), dim3(256), 0, s, dy, mask, k2, k1, dx, N, H, W, Ci, Co, S, g.Ho,
+                       g.Wo, g.pt, g.pl);
+    ASR_LAUNCH_CHECK("k_trans_dgrad");
+  }
+  if (dparams) {
+    int rpc = 0;
+    const int nch = trans_chunks(N, g.Ho, &rpc);
+    const long ET = trans_param_floats(Ci, Co);
+    hipLaunchKernelGGL(k_trans_wgrad, dim3((unsigned)((ET + 255) / 256), nch), dim3(256), 0, s, dy, mask, x, part, N,
+                       H, W, Ci, Co, S, g.Ho, g.Wo, g.pt, g.pl, rpc);
+    ASR_LAUNCH_CHECK("k_trans_wgrad");
+    hipLaunchKernelGGL(k_sum_chunks, dim3((unsigned)((ET + 255) / 256)), dim3(256), 0, s, part, nch, ET, dparams);
+    ASR_LAUNCH_CHECK("k_sum_chunks");
+  }
+  return ASR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// the multi-stage executor
+// ---------------------------------------------------------------------------
+struct StageL {
+  int C, L, H, W, S, Cp, Hp, Wp;  // S = 0: no transition; Cp/Hp/Wp the stage input's shape
+  long P, ntheta, E, blk_stride, mask_bytes;
+  long off_t, off_blk;          // parameter offsets (floats)
+  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, act_t, mask_t, acts, masks;  // workspace offsets
+};
+struct SLayout {
+  int ns;
+  StageL st[ASR_STAGES_MAX];
+  bool sep_bwd;
+  long off_c1k, off_c1b, off_fck, off_fcb, n_params, Pmax;
+  size_t act0, probs, loss_per, dlogits, gap, dA, dB, cws, tws, sslabs, sred, total;
+  size_t cws_bytes, tws_bytes, sred_bytes;
+};
+
+int stages_check(const asr_stages_config* c) {
+  if (!c) return fail(ASR_E_ARG, "asr_stages: null config");
+  if (c->N < 1 || c->H < 1 || c->W < 1 || c->num_classes < 1 || c->n_stages < 1 || c->n_stages > ASR_STAGES_MAX)
+    return fail(ASR_E_ARG, "asr_stages: bad config (N=%d H=%d W=%d K=%d stages=%d)", c->N, c->H, c->W,
+                c->num_classes, c->n_stages);
+  if (c->param_kind < ASR_PARAM_3BY3 || c->param_kind > ASR_PARAM_REGULAR) return fail(ASR_E_ARG, "asr_stages: param_kind");
+  if (c->stride[0] != 0) return fail(ASR_E_ARG, "asr_stages: stage 0 has no transition (stride[0] must be 0)");
+  for (int s = 0; s < c->n_stages; ++s) {
+    if (c->C[s] < 1 || c->L[s] < 0) return fail(ASR_E_ARG, "asr_stages: stage %d: C=%d L=%d", s, c->C[s], c->L[s]);
+    if (s > 0 && c->stride[s] == 0 && c->C[s] != c->C[s - 1])
+      return fail(ASR_E_ARG, "asr_stages: stage %d changes filters without a transition", s);
+    if (s > 0 && c->stride[s] != 0 && c->stride[s] != 1 && c->stride[s] != 2)
+      return fail(ASR_E_UNSUPPORTED, "asr_stages: stage %d: transition stride %d (1 or 2)", s, c->stride[s]);
+  }
+  if (!stem_supported(c->Cin, c->H, c->W, c->C[0]))
+    return fail(ASR_E_UNSUPPORTED, "asr_stages: stem Cin=%d C=%d at %dx%d", c->Cin, c->C[0], c->H, c->W);
+  if (c->C[c->n_stages - 1] > 256 || c->num_classes > 256)
+    return fail(ASR_E_UNSUPPORTED, "asr_stages: head needs C and num_classes <= 256");
+  if (c->use_norm && c->divide_by_stddev == 0.f) return fail(ASR_E_ARG, "asr_stages: divide_by_stddev == 0");
+  return ASR_OK;
+}
+
+SLayout stages_layout(const asr_stages_config* c) {
+  SLayout L{};
+  L.ns = c->n_stages;
+  L.sep_bwd = param_is_antisymmetric(c->param_kind, c->antisymmetric) == 0;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off += align_up(bytes, 256);
+    return o;
+  };
+  long po = 0;
+  L.off_c1k = po;
+  po += 9L * c->Cin * c->C[0];
+  L.off_c1b = po;
+  po += c->C[0];
+  int H = c->H, W = c->W, Cp = c->C[0];
+  L.Pmax = (long)c->N * H * W * Cp;
+  for (int s = 0; s < L.ns; ++s) {
+    StageL& g = L.st[s];
+    g.C = c->C[s];
+    g.L = c->L[s];
+    g.S = s > 0 ? c->stride[s] : 0;
+    g.Cp = Cp;
+    g.Hp = H;
+    g.Wp = W;
+    if (g.S) {
+      const TGeom tg = tgeom(H, W, g.S);
+      H = tg.Ho;
+      W = tg.Wo;
+    }
+    g.H = H;
+    g.W = W;
+    g.P = (long)c->N * H * W * g.C;
+    L.Pmax = std::max(L.Pmax, g.P);
+    g.ntheta = theta_count(g.C, c->param_kind, c->antisymmetric);
+    g.E = 9L * g.C * g.C;
+    g.blk_stride = g.ntheta + g.C;
+    g.mask_bytes = (long)align_up((size_t)asr_mask_bytes(c->N, H, W, g.C), 256);
+    g.off_t = po;
+    if (g.S) po += trans_param_floats(Cp, g.C);
+    g.off_blk = po;
+    po += (long)g.L * g.blk_stride;
+    Cp = g.C;
+  }
+  L.off_fck = po;
+  po += (long)Cp * c->num_classes;
+  L.off_fcb = po;
+  po += c->num_classes;
+  L.n_params = po;
+  // workspace
+  L.act0 = take((size_t)c->N * c->H * c->W * c->C[0] * 4);
+  L.cws_bytes = 0;
+  L.tws_bytes = 0;
+  for (int s = 0; s < L.ns; ++s) {
+    StageL& g = L.st[s];
+    g.w_src = take((size_t)g.E * 4);
+    g.theta_dst = take((size_t)g.ntheta * 2 * 4);
+    g.w_src_bwd = L.sep_bwd ? take((size_t)g.E * 4) : 0;
+    g.wbuf = take((size_t)std::max(g.L, 1) * g.E * 4);
+    g.wbuf_bwd = L.sep_bwd ? take((size_t)std::max(g.L, 1) * g.E * 4) : 0;
+    g.act_t = g.S ? take((size_t)g.P * 4) : 0;
+    g.mask_t = g.S ? take((size_t)g.P) : 0;
+    g.acts = take((size_t)std::max(g.L, 1) * g.P * 4);
+    g.masks = take((size_t)std::max(g.L, 1) * g.mask_bytes);
+    if (g.L > 0) L.cws_bytes = std::max(L.cws_bytes, asr_conv_backward_workspace_bytes(c->N, g.H, g.W, g.C, ASR_F32));
+    if (g.S) L.tws_bytes = std::max(L.tws_bytes, trans_ws_bytes(c->N, g.Hp, g.Wp, g.Cp, g.C, g.S));
+  }
+  const int K = c->num_classes;
+  L.probs = take((size_t)c->N * K * 4);
+  L.loss_per = take((size_t)c->N * 4);
+  L.dlogits = take((size_t)c->N * K * 4);
+  L.gap = take((size_t)c->N * Cp * 4);
+  L.dA = take((size_t)L.Pmax * 4);
+  L.dB = take((size_t)L.Pmax * 4);
+  L.cws = take(std::max<size_t>(L.cws_bytes, 256));
+  L.tws = take(std::max<size_t>(L.tws_bytes, 256));
+  const long E1 = 9L * c->Cin * c->C[0];
+  L.sslabs = take((size_t)kMaxStemSlabs * (E1 + c->C[0]) * 4);
+  L.sred_bytes = reduce_ws_bytes(kMaxStemSlabs, E1 + c->C[0]);
+  L.sred = take(L.sred_bytes);
+  L.total = off;
+  return L;
+}
+
+// forward through the stem and all stages; *xL = the last activation (fp32)
+int stages_forward_impl(const asr_stages_config* c, const SLayout& L, const float* params, const void* images,
+                        bool training, unsigned char* b, hipStream_t s, const float** xL) {
+  const float inv_std = c->use_norm ? 1.f / c->divide_by_stddev : 1.f;
+  ASR_TRY(stem_forward(images, c->input_u8, params + L.off_c1k, params + L.off_c1b, c->N, c->H, c->W, c->Cin,
+                       c->C[0], c->subtract_mean, inv_std, c->use_norm, b + L.act0, 0, s));
+  const float* x = (const float*)(b + L.act0);
+  for (int si = 0; si < L.ns; ++si) {
+    const StageL& g = L.st[si];
+    if (g.S) {
+      const float* pt = params + g.off_t;
+      const long e2 = 9L * g.Cp * g.C;
+      ASR_TRY(trans_forward(x, (float*)(b + g.act_t), (uint8_t*)(b + g.mask_t), pt, pt + e2, pt + e2 + g.C,
+                            pt + e2 + g.C + (long)g.Cp * g.C, c->N, g.Hp, g.Wp, g.Cp, g.C, g.S, s));
+      x = (const float*)(b + g.act_t);
+    }
+    if (g.L == 0) continue;
+    ASR_TRY(asr_theta_to_w(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src), c->gamma,
+                           b + g.wbuf, g.E, ASR_F32, s));
+    if (training && L.sep_bwd)
+      ASR_TRY(asr_theta_to_w(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src_bwd), 0.f,
+                             b + g.wbuf_bwd, g.E, ASR_F32, s));
+    for (int l = 0; l < g.L; ++l) {
+      float* y = (float*)(b + g.acts) + (size_t)l * g.P;
+      ASR_TRY(asr_conv_forward(ASR_MODE_EULER, x, y, (uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes,
+                               (const float*)(b + g.wbuf) + (size_t)l * g.E,
+                               params + g.off_blk + (long)l * g.blk_stride + g.ntheta, c->h, c->N, g.H, g.W, g.C,
+                               ASR_F32, s));
+      x = y;
+    }
+  }
+  *xL = x;
+  return ASR_OK;
+}
+
+}  // namespace
+}  // namespace asr
+
+using namespace asr;
+
+extern "C" {
+
+int asr_transition_forward(const float* x, float* y, uint8_t* mask, const float* k2, const float* b2, const float* k1,
+                           const float* b1, int N, int H, int W, int Ci, int Co, int stride, asr_stream_t stream) {
+  ASR_TRY(check_trans(N, H, W, Ci, Co, stride));
+  if (!x || !y || !k2 || !b2 || !k1 || !b1) return fail(ASR_E_ARG, "asr_transition_forward: null pointer");
+  return trans_forward(x, y, mask, k2, b2, k1, b1, N, H, W, Ci, Co, stride, (hipStream_t)stream);
+}
+
+size_t asr_transition_backward_workspace_bytes(int N, int H, int W, int Ci, int Co, int stride) {
+  if (check_trans(N, H, W, Ci, Co, stride) != ASR_OK) return 0;
+  return trans_ws_bytes(N, H, W, Ci, Co, stride);
+}
+
+int asr_transition_backward(const float* dy, const float* x, const uint8_t* mask, const float* k2, const float* k1,
+                            int N, int H, int W, int Ci, int Co, int stride, float* dx, float* dparams, void* ws,
+                            size_t ws_bytes, asr_stream_t stream) {
+  ASR_TRY(check_trans(N, H, W, Ci, Co, stride));
+  if (!dy || !x || !mask || !k2 || !k1) return fail(ASR_E_ARG, "asr_transition_backward: null pointer");
+  if (dparams && (!ws || ws_bytes < trans_ws_bytes(N, H, W, Ci, Co, stride)))
+    return fail(ASR_E_WORKSPACE, "asr_transition_backward: workspace too small");
+  return trans_backward(dy, x, mask, k2, k1, N, H, W, Ci, Co, stride, dx, dparams, (float*)ws, (hipStream_t)stream);
+}
+
+long asr_stages_param_count(const asr_stages_config* cfg) {
+  if (stages_check(cfg) != ASR_OK) return -1;
+  return stages_layout(cfg).n_params;
+}
+
+size_t asr_stages_workspace_bytes(const asr_stages_config* cfg) {
+  if (stages_check(cfg) != ASR_OK) return 0;
+  return stages_layout(cfg).total;
+}
+
+int asr_stages_prepare(const asr_stages_config* cfg, void* ws, size_t ws_bytes) {
+  ASR_TRY(stages_check(cfg));
+  const SLayout L = stages_layout(cfg);
+  if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_stages_prepare: workspace too small");
+  unsigned char* b = (unsigned char*)ws;
+  for (int s = 0; s < L.ns; ++s) {
+    const StageL& g = L.st[s];
+    std::vector<int32_t> w_src((size_t)g.E), theta_dst((size_t)g.ntheta * 2);
+    ASR_TRY(param_map(g.C, cfg->param_kind, cfg->antisymmetric, w_src.data(), theta_dst.data()));
+    ASR_TRY(hip_check(hipMemcpy(b + g.w_src, w_src.data(), w_src.size() * 4, hipMemcpyHostToDevice), "hipMemcpy"));
+    ASR_TRY(hip_check(hipMemcpy(b + g.theta_dst, theta_dst.data(), theta_dst.size() * 4, hipMemcpyHostToDevice),
+                      "hipMemcpy"));
+    if (L.sep_bwd) {
+      std::vector<int32_t> w_bwd((size_t)g.E);
+      ASR_TRY(param_map_transpose(g.C, w_src.data(), w_bwd.data()));
+      ASR_TRY(hip_check(hipMemcpy(b + g.w_src_bwd, w_bwd.data(), w_bwd.size() * 4, hipMemcpyHostToDevice), "hipMemcpy"));
+    }
+  }
+  return ASR_OK;
+}
+
+int asr_stages_forward(const asr_stages_config* cfg, const float* params, const void* images, float* probs, void* ws,
+                       size_t ws_bytes, asr_stream_t stream) {
+  ASR_TRY(stages_check(cfg));
+  const SLayout L = stages_layout(cfg);
+  if (!params || !images || !probs) return fail(ASR_E_ARG, "asr_stages_forward: null pointer");
+  if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_stages_forward: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  unsigned char* b = (unsigned char*)ws;
+  const float* xL = nullptr;
+  ASR_TRY(stages_forward_impl(cfg, L, params, images, false, b, s, &xL));
+  const StageL& g = L.st[L.ns - 1];
+  return head(xL, 0, params + L.off_fck, params + L.off_fcb, nullptr, cfg->N, g.H * g.W, g.C, cfg->num_classes, probs,
+              nullptr, nullptr, nullptr, nullptr, s);
+}
+
+int asr_stages_forward_backward(const asr_stages_config* cfg, const float* params, const void* images,
+                                const float* targets, float* grads, float* loss, float* probs, void* ws,
+                                size_t ws_bytes, asr_stream_t stream) {
+  ASR_TRY(stages_check(cfg));
+  const SLayout L = stages_layout(cfg);
+  if (!params || !images || !targets || !grads || !loss) return fail(ASR_E_ARG, "asr_stages_forward_backward: null");
+  if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_stages_forward_backward: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  unsigned char* b = (unsigned char*)ws;
+  const int N = cfg->N, K = cfg->num_classes;
+  const float* xL = nullptr;
+  ASR_TRY(stages_forward_impl(cfg, L, params, images, true, b, s, &xL));
+  float* d = (float*)(b + L.dA);
+  float* e = (float*)(b + L.dB);
+  const StageL& top = L.st[L.ns - 1];
+  ASR_TRY(head(xL, 0, params + L.off_fck, params + L.off_fcb, targets, N, top.H * top.W, top.C, K,
+               probs ? probs : (float*)(b + L.probs), (float*)(b + L.loss_per), (float*)(b + L.dlogits),
+               (float*)(b + L.gap), d, s));
+  ASR_TRY(head_param_grads((const float*)(b + L.gap), (const float*)(b + L.dlogits), N, top.C, K, grads + L.off_fck,
+                           grads + L.off_fcb, (const float*)(b + L.loss_per), loss, s));
+  for (int si = L.ns - 1; si >= 0; --si) {
+    const StageL& g = L.st[si];
+    // the stage's chain input: its transition's output, else the previous stage's last activation
+    const float* prev_out = (const float*)(b + L.act0);
+    for (int sp = si - 1; sp >= 0; --sp) {
+      const StageL& q = L.st[sp];
+      if (q.L > 0) { prev_out = (const float*)(b + q.acts) + (size_t)(q.L - 1) * q.P; break; }
+      if (q.S) { prev_out = (const float*)(b + q.act_t); break; }
+    }
+    const float* chain_in = g.S ? (const float*)(b + g.act_t) : prev_out;
+    const float gam = L.sep_bwd ? 0.f : cfg->gamma;
+    for (int l = g.L - 1; l >= 0; --l) {
+      const float* x_in = l == 0 ? chain_in : (const float*)(b + g.acts) + (size_t)(l - 1) * g.P;
+      const unsigned char* wl = b + (L.sep_bwd ? g.wbuf_bwd : g.wbuf) + (size_t)l * g.E * 4;
+      float* gp = grads + g.off_blk + (long)l * g.blk_stride;
+      ASR_TRY(asr_conv_backward(ASR_MODE_EULER, d, x_in, (const uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes, wl,
+                                (const int32_t*)(b + g.theta_dst), g.ntheta, cfg->h, gam, N, g.H, g.W, g.C, ASR_F32, e,
+                                gp, gp + g.ntheta, nullptr, b + L.cws, L.cws_bytes, s));
+      std::swap(d, e);
+    }
+    if (g.S) {
+      const float* pt = params + g.off_t;
+      const long e2 = 9L * g.Cp * g.C;
+      ASR_TRY(trans_backward(d, prev_out, (const uint8_t*)(b + g.mask_t), pt, pt + e2 + g.C, N, g.Hp, g.Wp, g.Cp, g.C,
+                             g.S, e, grads + g.off_t, (float*)(b + L.tws), s));
+      std::swap(d, e);
+    }
+  }
+  // stem: dz1 = dx1 [x1 > 0] inside stem_wgrad; conv1 kernel / bias gradients
+  const float inv_std = cfg->use_norm ? 1.f / cfg->divide_by_stddev : 1.f;
+  int nsl = 0;
+  ASR_TRY(stem_wgrad(images, cfg->input_u8, d, b + L.act0, 0, N, cfg->H, cfg->W, cfg->Cin, cfg->C[0],
+                     cfg->subtract_mean, inv_std, cfg->use_norm, (float*)(b + L.sslabs), &nsl, s));
+  if (nsl > kMaxStemSlabs) return fail(ASR_E_UNSUPPORTED, "asr_stages: stem slabs %d > %d", nsl, kMaxStemSlabs);
+  return reduce_and_project((const float*)(b + L.sslabs), nsl, 9L * cfg->Cin * cfg->C[0], cfg->C[0], nullptr, 0,
+                            nullptr, grads + L.off_c1b, grads + L.off_c1k, (float*)(b + L.sred), s);
+}
+
+}  // extern "C"

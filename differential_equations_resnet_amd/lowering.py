@@ -18,9 +18,19 @@ the midpoint step built by single_layer_identity_block:
 
 with the SAME conv layer applied twice.
 
-Anything else (BN, pooling, stage transitions, strided or non-3x3 convs,
-per-block differing h/gamma/integrator) raises AsrUnsupported naming the
-layer: there is no fallback executor.
+With num_stages > 2 (e.g. the He-style ResNet-32, blocks [10, 10, 10] at
+32^2 x 16, 16^2 x 32, 8^2 x 64; tfkeras_resnets.py:575-593) a stage whose
+filters or stride change opens with single_layer_conv_block
+(tfkeras_resnets.py:204-269):
+
+          add(relu(Conv2D 3x3 'same' stride s (..._branch2)), Conv2D 1x1 'valid' stride s (..._branch1))
+
+and the model lowers onto the multi-stage executor (asr_stages_*, fp32,
+Euler blocks) as a StagesPlan.
+
+Anything else (BN, pooling, strided stem, non-3x3 convs, per-block differing
+h/gamma/integrator, RK2 blocks in a multi-stage net) raises AsrUnsupported
+naming the layer: there is no fallback executor.
 """
 from __future__ import annotations
 
@@ -33,7 +43,7 @@ from .graph import (Activation, Add, Conv2D, Dense, GlobalAveragePooling2D, Inpu
                     SymbolicTensor)
 from .layers._antisymmetric import AntisymmetricConvBase
 
-__all__ = ["NetPlan", "analyze", "NativeModel"]
+__all__ = ["NetPlan", "StagesPlan", "analyze", "NativeModel"]
 
 
 @dataclass
@@ -66,6 +76,76 @@ class NetPlan:
     def block_theta_sizes(self):
         """Per block: number of theta (kernel) floats, excluding the bias."""
         return [sum(v.value.size for v in conv.weights) - self.C for conv in self.blocks]
+
+
+@dataclass
+class StagesPlan:
+    """A multi-stage single-block ResNet (asr_stages_config): stage 0 holds
+    conv1's filters; every later stage may open with a transition."""
+    H: int
+    W: int
+    Cin: int
+    num_classes: int
+    h: float
+    gamma: float
+    subtract_mean: float | None
+    divide_by_stddev: float | None
+    param_kind: int
+    antisymmetric: bool
+    stages: list                 # [(C, L, stride)], stride 0 = no transition
+    transitions: list            # per stage: None or (conv_3x3 '..._branch2', conv_1x1 '..._branch1')
+    stage_blocks: list           # per stage: the identity blocks' convs
+    integrator: str = "euler"
+    conv1: Conv2D = None
+    fc: Dense = None
+
+    @property
+    def blocks(self):
+        return [b for bl in self.stage_blocks for b in bl]
+
+    @property
+    def L(self):
+        return len(self.blocks)
+
+    @property
+    def C(self):
+        return self.stages[-1][0]
+
+    def weight_vars(self):
+        """Variables in the executor's flat order (asr_stages_config)."""
+        out = [self.conv1.kernel, self.conv1.bias]
+        for tr, blocks in zip(self.transitions, self.stage_blocks):
+            if tr is not None:
+                c2, c1 = tr
+                out += [c2.kernel, c2.bias, c1.kernel, c1.bias]
+            for conv in blocks:
+                out += conv.weights
+        out += [self.fc.kernel, self.fc.bias]
+        return out
+
+
+def _transition(t: SymbolicTensor):
+    """Match t = add(relu(conv_3x3(x)), conv_1x1(x)) (single_layer_conv_block,
+    tfkeras_resnets.py:238-269); return (conv_3x3, conv_1x1, x) or None."""
+    if len(t.inbound) != 2:
+        return None
+    branch, short = t.inbound
+    if not (isinstance(short.layer, Conv2D) and short.layer.kernel_size == (1, 1) and _is_relu(branch)
+            and isinstance(branch.inbound[0].layer, Conv2D)):
+        return None
+    c2, c1 = branch.inbound[0].layer, short.layer
+    x = short.inbound[0]
+    if branch.inbound[0].inbound[0] is not x:
+        raise _unsupported(t.layer, "transition branches must read the same tensor")
+    if c2.kernel_size != (3, 3) or c2.padding != "same" or not c2.use_bias or c2.activation not in (None, "linear"):
+        raise _unsupported(c2, "transition conv must be a 3x3 'same' conv with bias, no activation")
+    if c1.padding != "valid" or not c1.use_bias or c1.activation not in (None, "linear"):
+        raise _unsupported(c1, "transition shortcut must be a 1x1 'valid' conv with bias")
+    if c2.strides != c1.strides or c2.strides[0] != c2.strides[1] or c2.strides[0] not in (1, 2):
+        raise _unsupported(c2, f"transition strides {c2.strides} / {c1.strides} (equal, 1 or 2)")
+    if c2.dilation_rate != (1, 1) or c1.dilation_rate != (1, 1) or c2.filters != c1.filters:
+        raise _unsupported(c2, "transition convs must be undilated with equal filters")
+    return c2, c1, x
 
 
 def _unsupported(layer, why):
@@ -135,9 +215,16 @@ def analyze(model: Model) -> NetPlan:
     if not isinstance(t.layer, GlobalAveragePooling2D):
         raise _unsupported(t.layer, "expected GlobalAveragePooling2D before fc")
     t = t.inbound[0]
-    # identity blocks, last to first
+    # identity blocks (and stage transitions), last to first
     blocks, hs, integ = [], [], []
+    segs = []  # completed stages, top first: (transition, blocks top first)
     while isinstance(t.layer, Add):
+        tr = _transition(t)
+        if tr is not None:
+            segs.append(((tr[0], tr[1]), blocks))
+            blocks = []
+            t = tr[2]
+            continue
         conv, h, inner = _euler_step(t)
         skip = t.inbound[1]
         if inner is skip:
@@ -155,7 +242,9 @@ def analyze(model: Model) -> NetPlan:
         blocks.append(conv)
         hs.append(h)
         t = skip
-    blocks.reverse()
+    segs.append((None, blocks))
+    segs.reverse()
+    blocks = [b for _, bl in segs for b in reversed(bl)]
     hs.reverse()
     if not blocks:
         raise _lib.AsrUnsupported("no identity blocks found")
@@ -192,6 +281,9 @@ def analyze(model: Model) -> NetPlan:
         kind, anti, gamma = first.param_kind, bool(first.antisymmetric), float(first.gamma)
     else:
         kind, anti, gamma = _lib.ASR_PARAM_REGULAR, False, 0.0
+    if len(segs) > 1:
+        return _stages_plan(segs, int(H), int(W), int(Cin), int(C), fc, float(hs[0]), gamma, mean, std, kind, anti,
+                            integ[0], conv1)
     plan = NetPlan(H=int(H), W=int(W), Cin=int(Cin), C=int(C), L=len(blocks), num_classes=fc.units, h=float(hs[0]),
                    gamma=gamma, subtract_mean=mean, divide_by_stddev=std, param_kind=kind, antisymmetric=anti,
                    integrator=integ[0], conv1=conv1, blocks=blocks, fc=fc)
@@ -199,6 +291,31 @@ def analyze(model: Model) -> NetPlan:
         if b.weights[-1].shape != (C,):
             raise _unsupported(b, f"block channels must equal conv1 filters ({C})")
     return plan
+
+
+def _stages_plan(segs, H, W, Cin, C0, fc, h, gamma, mean, std, kind, anti, integrator, conv1) -> StagesPlan:
+    if integrator != "euler":
+        raise _lib.AsrUnsupported("multi-stage nets run Euler identity blocks (integrator='rk2' is single-stage)")
+    if len(segs) > _lib.ASR_STAGES_MAX:
+        raise _lib.AsrUnsupported(f"{len(segs)} stages (at most {_lib.ASR_STAGES_MAX})")
+    stages, transitions, stage_blocks = [], [], []
+    Cp = C0
+    for s, (tr, bl) in enumerate(segs):
+        bl = list(reversed(bl))
+        if tr is None:
+            C, S = Cp, 0
+        else:
+            C, S = tr[0].filters, tr[0].strides[0]
+        for b in bl:
+            if b.weights[-1].shape != (C,):
+                raise _unsupported(b, f"block channels must equal the stage's filters ({C})")
+        stages.append((C, len(bl), S))
+        transitions.append(tr)
+        stage_blocks.append(bl)
+        Cp = C
+    return StagesPlan(H=H, W=W, Cin=Cin, num_classes=fc.units, h=h, gamma=gamma, subtract_mean=mean,
+                      divide_by_stddev=std, param_kind=kind, antisymmetric=anti, stages=stages,
+                      transitions=transitions, stage_blocks=stage_blocks, integrator=integrator, conv1=conv1, fc=fc)
 
 
 class NativeModel:
@@ -262,6 +379,16 @@ class NativeModel:
         forward-only one (bounded workspace: x_0 + two activation slots)."""
         key = (int(batch_size), dtype, bool(input_u8), bool(inference))
         ex = self._executors.get(key)
+        if ex is None and isinstance(self.plan, StagesPlan):
+            # fp32 whatever dtype is asked: the multi-stage executor has the reference's precision only
+            p = self.plan
+            ex = self._rt.StagesExecutor(int(batch_size), p.H, p.W, p.Cin, p.stages, p.num_classes, p.h, p.gamma,
+                                         subtract_mean=p.subtract_mean, divide_by_stddev=p.divide_by_stddev,
+                                         dtype="float32", input_u8=input_u8, device=self.device,
+                                         param_kind=p.param_kind, antisymmetric=p.antisymmetric, inference=inference)
+            if ex.n_params != self.n_params:
+                raise _lib.AsrError(f"executor expects {ex.n_params} parameters, model has {self.n_params}")
+            self._executors[key] = ex
         if ex is None:
             p = self.plan
             ex = self._rt.NetExecutor(int(batch_size), p.H, p.W, p.Cin, p.C, p.L, p.num_classes, p.h, p.gamma,

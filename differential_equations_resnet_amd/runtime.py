@@ -16,12 +16,13 @@ from ._lib import (ASR_BF16, ASR_F32, ASR_INTEGRATOR_EULER, ASR_INTEGRATOR_RK2, 
                    ASR_PARAM_3BY3, ASR_PARAM_GENERAL, ASR_PARAM_REGULAR, ASR_VARIANT_NO_FOLD, ASR_VARIANT_STEM_FWD_VALU,
                    ASR_VARIANT_STEM_WGRAD_VALU, ASR_VARIANT_PER_BLOCK_FWD,
                    ASR_VARIANT_PER_BLOCK_BWD, ASR_VARIANT_INFERENCE, ASR_VARIANT_TIMED, ASR_VARIANT_FULL_DXL,
-                   ASR_VARIANT_FULL_SLABS, NetConfig)
+                   ASR_VARIANT_FULL_SLABS, NetConfig, StagesConfig)
 
 __all__ = [
     "require_gpu", "dtype_code", "torch_dtype", "ParamMap", "param_map", "theta_count", "theta_to_w",
     "conv_forward", "block_stack_forward", "block_stack_backward", "conv_backward", "rk2_forward", "rk2_backward",
-    "integrator_code", "NetExecutor", "adam_update", "stack_status",
+    "integrator_code", "NetExecutor", "adam_update", "stack_status", "transition_forward", "transition_backward",
+    "StagesExecutor",
 ]
 
 
@@ -462,6 +463,107 @@ class NetExecutor:
         if tuple(targets.shape) != (self.cfg.N, self.cfg.num_classes) or targets.dtype != torch.float32:
             raise ValueError("targets must be float32 one-hot [N, num_classes]")
         _lib.call("asr_net_forward_backward", ct.byref(self.cfg), _p(params), _p(images), _p(targets),
+                  _p(self.grads), _p(self.loss), _p(self.probs) if want_probs else None, _p(self.ws),
+                  self.ws_bytes, _stream())
+        return self.loss, self.grads
+
+
+def transition_forward(x: torch.Tensor, k2, b2, k1, b1, stride: int):
+    """single_layer_conv_block (tfkeras_resnets.py:204-269) on fp32 NHWC x:
+    (y, mask) with y = relu(conv3x3_same(x, k2, stride) + b2) + conv1x1(x, k1,
+    stride) + b1 and mask = [conv3x3 + b2 > 0] (asr_transition_forward)."""
+    N, H, W, Ci = x.shape
+    Co = int(k2.shape[-1])
+    Ho, Wo = -(-H // stride), -(-W // stride)
+    y = torch.empty((N, Ho, Wo, Co), dtype=torch.float32, device=x.device)
+    mask = torch.empty((N, Ho, Wo, Co), dtype=torch.uint8, device=x.device)
+    _lib.call("asr_transition_forward", _p(x), _p(y), _p(mask), _p(k2), _p(b2), _p(k1), _p(b1), N, H, W, Ci, Co,
+              int(stride), _stream())
+    return y, mask
+
+
+def transition_backward(dy, x, mask, k2, k1, stride: int, want_dx=True, want_dparams=True):
+    """Backward of transition_forward: (dx, dparams) with dparams =
+    [dK2 | db2 | dK1 | db1] flat (asr_transition_backward)."""
+    N, H, W, Ci = x.shape
+    Co = int(k2.shape[-1])
+    dx = torch.empty_like(x) if want_dx else None
+    dparams = torch.empty(9 * Ci * Co + Co + Ci * Co + Co, dtype=torch.float32, device=x.device) if want_dparams else None
+    nb = int(_lib.load().asr_transition_backward_workspace_bytes(N, H, W, Ci, Co, int(stride)))
+    ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=x.device)
+    _lib.call("asr_transition_backward", _p(dy), _p(x), _p(mask), _p(k2), _p(k1), N, H, W, Ci, Co, int(stride),
+              _p(dx), _p(dparams), _p(ws), nb, _stream())
+    return dx, dparams
+
+
+class StagesExecutor:
+    """Native executor of the multi-stage single-block ResNet (asr_stages_*
+    in include/asr.h): stem, per stage an optional transition
+    (single_layer_conv_block) and its identity Euler blocks, head.  fp32 (the
+    reference's precision).  Parameters / gradients are flat float32 buffers
+    in the asr_stages_config order; same call surface as NetExecutor."""
+
+    def __init__(self, N, H, W, Cin, stages, num_classes, h, gamma=0.0, subtract_mean=None, divide_by_stddev=None,
+                 dtype="float32", input_u8=True, device=None, param_kind=ASR_PARAM_3BY3, antisymmetric=True,
+                 inference=False):
+        """stages: [(C, L, stride)] per stage, stride 0 for no transition."""
+        if dtype_code(dtype) != ASR_F32:
+            raise _lib.AsrUnsupported("the multi-stage executor computes in float32 (the reference's precision)")
+        if not 1 <= len(stages) <= _lib.ASR_STAGES_MAX:
+            raise _lib.AsrUnsupported(f"{len(stages)} stages (1..{_lib.ASR_STAGES_MAX})")
+        self.device = device or require_gpu()
+        use_norm = subtract_mean is not None or divide_by_stddev is not None
+        c = StagesConfig()
+        c.N, c.H, c.W, c.Cin, c.num_classes, c.n_stages = int(N), int(H), int(W), int(Cin), int(num_classes), len(stages)
+        for i, (C, L, S) in enumerate(stages):
+            c.C[i], c.L[i], c.stride[i] = int(C), int(L), int(S)
+        c.h, c.gamma = float(h), float(gamma)
+        c.subtract_mean = float(subtract_mean or 0.0)
+        c.divide_by_stddev = float(divide_by_stddev if divide_by_stddev is not None else 1.0)
+        c.use_norm, c.input_u8 = int(use_norm), int(bool(input_u8))
+        c.param_kind, c.antisymmetric = int(param_kind), int(bool(antisymmetric))
+        self.cfg = c
+        self.stages = [tuple(int(v) for v in st) for st in stages]
+        lib = _lib.load()
+        self.n_params = int(lib.asr_stages_param_count(ct.byref(c)))
+        if self.n_params < 0:
+            _lib.check(_lib.ASR_E_ARG, "asr_stages_param_count")
+        self.ws_bytes = int(lib.asr_stages_workspace_bytes(ct.byref(c)))
+        if self.ws_bytes == 0:
+            _lib.check(_lib.ASR_E_ARG, "asr_stages_workspace_bytes")
+        self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
+        _lib.call("asr_stages_prepare", ct.byref(c), _p(self.ws), self.ws_bytes)
+        self.inference = bool(inference)
+        self.grads = None if inference else torch.zeros(self.n_params, dtype=torch.float32, device=self.device)
+        self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.probs = torch.zeros(N, num_classes, dtype=torch.float32, device=self.device)
+
+    def _check_inputs(self, params, images):
+        c = self.cfg
+        if params.numel() != self.n_params or params.dtype != torch.float32 or not params.is_cuda:
+            raise ValueError(f"params must be a float32 device buffer of {self.n_params} elements")
+        want = torch.uint8 if c.input_u8 else torch.float32
+        if tuple(images.shape) != (c.N, c.H, c.W, c.Cin) or images.dtype != want or not images.is_contiguous():
+            raise ValueError(f"images must be contiguous {want} [{c.N},{c.H},{c.W},{c.Cin}] (NHWC)")
+
+    def forward(self, params, images) -> torch.Tensor:
+        self._check_inputs(params, images)
+        _lib.call("asr_stages_forward", ct.byref(self.cfg), _p(params), _p(images), _p(self.probs), _p(self.ws),
+                  self.ws_bytes, _stream())
+        return self.probs
+
+    def check_status(self):
+        """Blocking: synchronises the stream (a failed launch raises there; the
+        launches' own errors are raised by the calls that made them)."""
+        torch.cuda.current_stream().synchronize()
+
+    def forward_backward(self, params, images, targets, want_probs=False):
+        if self.inference:
+            raise ValueError("an inference executor has no backward")
+        self._check_inputs(params, images)
+        if tuple(targets.shape) != (self.cfg.N, self.cfg.num_classes) or targets.dtype != torch.float32:
+            raise ValueError("targets must be float32 one-hot [N, num_classes]")
+        _lib.call("asr_stages_forward_backward", ct.byref(self.cfg), _p(params), _p(images), _p(targets),
                   _p(self.grads), _p(self.loss), _p(self.probs) if want_probs else None, _p(self.ws),
                   self.ws_bytes, _stream())
         return self.loss, self.grads

@@ -361,6 +361,57 @@ int asr_stack_status(int reset);
  * setting it. */
 int asr_debug_stack_backward(int grid);
 
+/* ------------------------------------------------------------------------
+ * Multi-stage single-block ResNet (ABI 7): get_single_block_resnet_build_function
+ * with num_stages > 2 (models/tfkeras_resnets.py:547-597), e.g. the He-style
+ * ResNet-32: conv1 (3x3 'same', stride 1) + relu, then stages of identity Euler
+ * blocks at 32^2 x 16, 16^2 x 32, 8^2 x 64; a stage whose filters or stride
+ * change opens with single_layer_conv_block (tfkeras_resnets.py:204-269):
+ *     y = relu(conv_3x3(x, K2, stride) + b2) + conv_1x1(x, K1, stride) + b1
+ * (the 3x3 'same' with TF's asymmetric stride padding, the 1x1 'valid'), then
+ * GAP + Dense softmax.  fp32 (the reference's precision); no BN / pooling.
+ * ---------------------------------------------------------------------- */
+
+/* The transition alone.  x [N,H,W,Ci] -> y [N,Ho,Wo,Co], Ho = ceil(H/stride);
+ * k2 HWIO [3,3,Ci,Co], k1 [1,1,Ci,Co]; mask: N*Ho*Wo*Co bytes, 1 where
+ * conv_3x3 + b2 > 0 (may be NULL).  Replaces single_layer_conv_block's
+ * Conv2D '2' / '1' + relu + add (tfkeras_resnets.py:238-269). */
+int asr_transition_forward(const float* x, float* y, uint8_t* mask, const float* k2, const float* b2,
+                           const float* k1, const float* b1, int N, int H, int W, int Ci, int Co, int stride,
+                           asr_stream_t stream);
+/* Its backward: dx = dL/dx (may be NULL); dparams (may be NULL): the
+ * gradients [dK2 | db2 | dK1 | db1] contiguous (the parameter order of
+ * asr_stages_config). */
+size_t asr_transition_backward_workspace_bytes(int N, int H, int W, int Ci, int Co, int stride);
+int asr_transition_backward(const float* dy, const float* x, const uint8_t* mask, const float* k2, const float* k1,
+                            int N, int H, int W, int Ci, int Co, int stride, float* dx, float* dparams, void* ws,
+                            size_t ws_bytes, asr_stream_t stream);
+
+#define ASR_STAGES_MAX 8
+typedef struct asr_stages_config {
+  int N, H, W, Cin, num_classes;
+  int n_stages;               /* identity-block stages (the reference's num_stages - 1) */
+  int C[ASR_STAGES_MAX];      /* filters of stage s (C[0] = conv1's filters)           */
+  int L[ASR_STAGES_MAX];      /* identity blocks of stage s (>= 0)                     */
+  int stride[ASR_STAGES_MAX]; /* s > 0: the opening transition's stride (1 or 2), 0 =
+                                 no transition (then C[s] == C[s-1]); stride[0] = 0   */
+  float h, gamma;
+  float subtract_mean, divide_by_stddev; /* applied when use_norm != 0 */
+  int use_norm, input_u8, param_kind, antisymmetric;
+} asr_stages_config;
+/* params / grads (float32): conv1 kernel [3,3,Cin,C0], bias [C0]; per stage s:
+ * the transition (if any) K2 [3,3,C[s-1],C[s]], b2, K1 [1,1,C[s-1],C[s]], b1,
+ * then L[s] x (theta [asr_theta_count(C[s], param_kind, antisymmetric)], bias
+ * [C[s]]); fc kernel [C_last, K], bias [K]. */
+long asr_stages_param_count(const asr_stages_config* cfg);
+size_t asr_stages_workspace_bytes(const asr_stages_config* cfg);
+int asr_stages_prepare(const asr_stages_config* cfg, void* ws, size_t ws_bytes);
+int asr_stages_forward(const asr_stages_config* cfg, const float* params, const void* images, float* probs,
+                       void* ws, size_t ws_bytes, asr_stream_t stream);
+int asr_stages_forward_backward(const asr_stages_config* cfg, const float* params, const void* images,
+                                const float* targets, float* grads, float* loss, float* probs, void* ws,
+                                size_t ws_bytes, asr_stream_t stream);
+
 /* tf.train.AdamOptimizer.apply_gradients (training.py:300-301), TF1
  * epsilon-hat form; step is the 1-based update count; g is multiplied by
  * grad_scale first (1/world for data-parallel mean). */

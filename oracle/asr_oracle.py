@@ -629,3 +629,186 @@ def adam_tf1(params, grads, m, v, t, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-7):
         vv += (1.0 - beta2) * g * g
         p -= lr_t * mm / (np.sqrt(vv) + eps)
     return params, m, v
+
+
+# --------------------------------------------------------------------------
+# multi-stage network: get_single_block_resnet_build_function with
+# num_stages > 2 (tfkeras_resnets.py:547-597), stage transitions by
+# single_layer_conv_block (tfkeras_resnets.py:204-269)
+# --------------------------------------------------------------------------
+
+
+def _same_pads(H, W, k, stride):
+    Ho, Wo = -(-H // stride), -(-W // stride)
+    ph = max((Ho - 1) * stride + k - H, 0)
+    pw = max((Wo - 1) * stride + k - W, 0)
+    return Ho, Wo, ph, pw
+
+
+def conv2d_backprop_input_strided(dz, W, x_shape, stride):
+    """Conv2DBackpropInput of conv2d_same(x, W, stride) (TF 'SAME': pad_top =
+    pad_total // 2, the remainder at the bottom/right)."""
+    N, H, Wd, Ci = x_shape
+    kh, kw, _, Co = W.shape
+    Ho, Wo, ph, pw = _same_pads(H, Wd, kh, stride)
+    dxp = np.zeros((N, H + ph, Wd + pw, Ci), dtype=np.result_type(dz, W))
+    for ky in range(kh):
+        for kx in range(kw):
+            dxp[:, ky:ky + (Ho - 1) * stride + 1:stride, kx:kx + (Wo - 1) * stride + 1:stride, :] += dz @ W[ky, kx].T
+    return dxp[:, ph // 2:ph // 2 + H, pw // 2:pw // 2 + Wd, :]
+
+
+def conv2d_backprop_filter_strided(x, dz, k, stride):
+    """Conv2DBackpropFilter of conv2d_same(x, W[k,k], stride)."""
+    N, H, Wd, Ci = x.shape
+    Co = dz.shape[-1]
+    Ho, Wo, ph, pw = _same_pads(H, Wd, k, stride)
+    xp = np.zeros((N, H + ph, Wd + pw, Ci), dtype=np.result_type(x, dz))
+    xp[:, ph // 2:ph // 2 + H, pw // 2:pw // 2 + Wd, :] = x
+    dz2 = dz.reshape(-1, Co)
+    dW = np.zeros((k, k, Ci, Co), dtype=xp.dtype)
+    for ky in range(k):
+        for kx in range(k):
+            dW[ky, kx] = xp[:, ky:ky + (Ho - 1) * stride + 1:stride, kx:kx + (Wo - 1) * stride + 1:stride, :] \
+                .reshape(-1, Ci).T @ dz2
+    return dW
+
+
+def transition_fwd(x, K2, b2, K1, b1, stride):
+    """single_layer_conv_block without BN (tfkeras_resnets.py:238-269):
+    x2 = Conv2D(k, strides, 'same')(x) (:238-245); shortcut = Conv2D(1x1,
+    strides, default 'valid')(x) (:247-252); relu(x2) + shortcut (:261-262).
+    Returns (y, z) with z the 3x3 branch's pre-activation."""
+    z = conv2d_same(x, K2, stride) + b2
+    sc = x[:, ::stride, ::stride, :] @ np.asarray(K1)[0, 0] + b1
+    return np.maximum(z, 0) + sc, z
+
+
+def transition_bwd(dy, x, z, K2, K1, stride):
+    """Autodiff of transition_fwd: (dx, [dK2, db2, dK1, db1])."""
+    dz = dy * (z > 0)
+    dx = conv2d_backprop_input_strided(dz, K2, x.shape, stride)
+    K1m = np.asarray(K1)[0, 0]
+    dx[:, ::stride, ::stride, :] += dy @ K1m.T
+    Ci, Co = K1m.shape
+    dK2 = conv2d_backprop_filter_strided(x, dz, K2.shape[0], stride)
+    dK1 = (x[:, ::stride, ::stride, :].reshape(-1, Ci).T @ dy.reshape(-1, Co))[None, None]
+    return dx, [dK2, dz.sum(axis=(0, 1, 2)), dK1, dy.sum(axis=(0, 1, 2))]
+
+
+@dataclass
+class StagesSpec:
+    """A multi-stage net: stages [(C, L, stride)] (stride 0: no transition),
+    Euler identity blocks of one conv kind (NetSpec's kinds)."""
+    stages: list = field(default_factory=lambda: [(16, 2, 0), (32, 2, 2), (64, 2, 2)])
+    h: float = 1.0
+    gamma: float = 0.0
+    num_classes: int = 10
+    H: int = 32
+    W: int = 32
+    Cin: int = 3
+    subtract_mean: float | None = 127.5
+    divide_by_stddev: float | None = 127.5
+    kind: str = "3by3"
+    antisymmetric: bool = True
+
+    def block_spec(self, C):
+        return NetSpec(C=C, L=0, h=self.h, gamma=self.gamma, kind=self.kind, antisymmetric=self.antisymmetric)
+
+    def param_shapes(self):
+        """asr_stages_config order: conv1 kernel/bias; per stage the transition
+        (K2, b2, K1, b1) then per block [theta..., bias]; fc kernel/bias."""
+        C0 = self.stages[0][0]
+        s = [(3, 3, self.Cin, C0), (C0,)]
+        Cp = C0
+        for C, L, S in self.stages:
+            if S:
+                s += [(3, 3, Cp, C), (C,), (1, 1, Cp, C), (C,)]
+            for _ in range(L):
+                s += self.block_spec(C).theta_shapes() + [(C,)]
+            Cp = C
+        s += [(Cp, self.num_classes), (self.num_classes,)]
+        return s
+
+    def n_params(self):
+        return int(sum(np.prod(x) for x in self.param_shapes()))
+
+
+def stages_init_params(spec: StagesSpec, rng, dtype=np.float64, bias_std=0.0):
+    """he_normal kernels (truncated, 2 sigma), biases zero or N(0, bias_std)."""
+    out = []
+    for shp in spec.param_shapes():
+        if len(shp) == 1:
+            out.append(np.zeros(shp, dtype) if bias_std == 0 else (rng.standard_normal(shp) * bias_std).astype(dtype))
+        else:
+            fan_in = int(np.prod(shp[:-1]))
+            out.append(truncated_normal(rng, shp, math.sqrt(2.0 / fan_in), dtype))
+    return out
+
+
+def _block_W(spec: StagesSpec, C, theta):
+    if spec.kind == "regular":
+        return np.asarray(theta[0])
+    src, sign = _cached_map(C, spec.kind, spec.antisymmetric)
+    return assemble_from_map(flatten(theta), C, src, sign, spec.gamma)
+
+
+def stages_forward(spec: StagesSpec, params, images, dtype=np.float64):
+    ns = NetSpec(subtract_mean=spec.subtract_mean, divide_by_stddev=spec.divide_by_stddev)
+    x0 = normalize_input(images, ns, dtype)
+    z1 = conv2d_same(x0, params[0]) + params[1]
+    x = np.maximum(z1, 0)
+    i = 2
+    ops = []  # per op: ("t", x_in, z, K2, K1, S) or ("b", x_in, z, W, C)
+    for C, L, S in spec.stages:
+        if S:
+            K2, b2, K1, b1 = params[i:i + 4]
+            i += 4
+            y, z = transition_fwd(x, K2, b2, K1, b1, S)
+            ops.append(("t", x, z, K2, K1, S))
+            x = y
+        nt = len(spec.block_spec(C).theta_shapes())
+        for _ in range(L):
+            theta, b = params[i:i + nt], params[i + nt]
+            i += nt + 1
+            W = _block_W(spec, C, theta)
+            y, z = euler_fwd(x, W, b, spec.h)
+            ops.append(("b", x, z, W, C))
+            x = y
+    fc_k, fc_b = params[i], params[i + 1]
+    gap = x.mean(axis=(1, 2))
+    probs = softmax(gap @ fc_k + fc_b)
+    return probs, dict(x0=x0, z1=z1, ops=ops, xL=x, gap=gap, probs=probs, fc_k=fc_k)
+
+
+def stages_backward(spec: StagesSpec, params, cache, onehot):
+    """Gradients of the mean Keras CE loss, in StagesSpec.param_shapes order."""
+    Nb = onehot.shape[0]
+    dlogits = keras_cce_grad_logits(cache["probs"], onehot, 1.0 / Nb)
+    d_fck = cache["gap"].T @ dlogits
+    d_fcb = dlogits.sum(axis=0)
+    xL = cache["xL"]
+    dx = np.broadcast_to((dlogits @ cache["fc_k"].T)[:, None, None, :] / (xL.shape[1] * xL.shape[2]),
+                         xL.shape).copy()
+    back = []
+    for op in reversed(cache["ops"]):
+        if op[0] == "t":
+            _, x_in, z, K2, K1, S = op
+            dx, g = transition_bwd(dx, x_in, z, K2, K1, S)
+            back.append(g)
+        else:
+            _, x_in, z, W, C = op
+            bs = spec.block_spec(C)
+            if bs.operator_antisymmetric():
+                dx, dW, db = euler_bwd(dx, x_in, z, W, spec.h, spec.gamma)
+            else:
+                dx, dW, db = euler_bwd_generic(dx, x_in, z, W, spec.h)
+            shapes = bs.theta_shapes()
+            src, sign = _cached_map(C, spec.kind, spec.antisymmetric)
+            ntheta = int(sum(np.prod(x) for x in shapes))
+            back.append(unflatten(project_dW(dW, src, sign, ntheta), shapes) + [db])
+    dz1 = dx * (cache["z1"] > 0)
+    grads = [conv2d_backprop_filter(cache["x0"], dz1), dz1.sum(axis=(0, 1, 2))]
+    for g in reversed(back):
+        grads += list(g)
+    return grads + [d_fck, d_fcb]

@@ -158,11 +158,43 @@ def test_analyze_rejects_unsupported(kw):
         analyze(_single_block(L=2, **kw))
 
 
-def test_analyze_rejects_multistage_and_per_channel_mean():
+def test_analyze_multistage_plan():
+    """num_stages > 2 (tfkeras_resnets.py:575-593): the He-style ResNet-32 lowers
+    onto the multi-stage executor; its flat parameter order is the model's
+    weight order and the C ABI's count (host function, no launch)."""
+    import ctypes as ct
+    from differential_equations_resnet_amd.lowering import StagesPlan
+    from differential_equations_resnet_amd.runtime import StagesConfig
+    fn = R.get_single_block_resnet_build_function(num_stages=4, blocks_per_stage=[10, 10, 10], h=0.5,
+                                                  filters_per_block=[16, 32, 64], strides=[(1, 1), (2, 2), (2, 2)],
+                                                  num_classes=10, subtract_mean=127.5, divide_by_stddev=127.5)
+    m = fn(Input(shape=(32, 32, 3)))
+    p = analyze(m)
+    assert isinstance(p, StagesPlan) and p.stages == [(16, 10, 0), (32, 9, 2), (64, 9, 2)] and p.L == 28
+    assert [t is None for t in p.transitions] == [True, False, False]
+    assert p.transitions[1][0].name == "res3_0_branch2" and p.transitions[1][1].name == "res3_0_branch1"
+    assert [v.name for v in p.weight_vars()] == [w.name for w in m.weights]
+    spec = O.StagesSpec(stages=p.stages, h=0.5)
+    assert [tuple(v.shape) for v in p.weight_vars()] == [tuple(s) for s in spec.param_shapes()]
+    assert m.count_params() == spec.n_params()
+    c = StagesConfig()
+    c.N, c.H, c.W, c.Cin, c.num_classes, c.n_stages = 8, 32, 32, 3, 10, 3
+    for i, (C, L, S) in enumerate(p.stages):
+        c.C[i], c.L[i], c.stride[i] = C, L, S
+    c.h, c.divide_by_stddev = 0.5, 1.0
+    lib = _lib.load()
+    assert lib.asr_stages_param_count(ct.byref(c)) == spec.n_params()
+    assert lib.asr_stages_workspace_bytes(ct.byref(c)) > 0
+    c.stride[0] = 2
+    assert lib.asr_stages_param_count(ct.byref(c)) == -1
+    # RK2 identity blocks are single-stage only
     fn = R.get_single_block_resnet_build_function(num_stages=3, blocks_per_stage=[2, 2], filters_per_block=[8, 16],
-                                                  strides=[(1, 1), (2, 2)], num_classes=10)
-    with pytest.raises(_lib.AsrUnsupported):
+                                                  strides=[(1, 1), (2, 2)], num_classes=10, integrator="rk2")
+    with pytest.raises(_lib.AsrUnsupported, match="rk2"):
         analyze(fn(Input(shape=(32, 32, 3))))
+
+
+def test_analyze_rejects_per_channel_mean():
     fn = R.get_single_block_resnet_build_function(num_stages=2, blocks_per_stage=[2], filters_per_block=[8],
                                                   strides=[(1, 1)], num_classes=10, subtract_mean=[120, 115, 100])
     with pytest.raises(_lib.AsrUnsupported, match="per-channel"):

@@ -1,0 +1,142 @@
+"""GPU parity of the multi-stage single-block ResNet (asr_stages_*,
+asr_transition_*) against the oracle's restatement of
+get_single_block_resnet_build_function with num_stages > 2
+(tfkeras_resnets.py:547-597) and single_layer_conv_block
+(tfkeras_resnets.py:204-269).
+
+Tolerances (fp32, the reference's precision, vs the fp64 oracle on the
+same fp32-representable inputs): transition outputs / gradients within
+1e-5 of the tensor's max |oracle| value and the relu mask exact (the few
+pre-activations within 1e-5 of 0 excepted); network probabilities within
+1e-5 relative, loss within 1e-5 relative, every gradient within 1e-4 of
+its tensor's max |oracle| value (the single-stage fp32 bar,
+test_gpu_network.py).
+"""
+import numpy as np
+import pytest
+
+from helpers import assert_close
+from oracle import asr_oracle as O
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+KINDS = {"3by3": 0, "general": 1, "regular": 2}
+
+
+def _t(a, dtype=np.float32):
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=dtype))).cuda()
+
+
+@pytest.mark.parametrize("N,H,W,Ci,Co,S", [(3, 32, 32, 16, 32, 2), (2, 16, 16, 32, 64, 2), (2, 7, 9, 5, 6, 2),
+                                           (2, 8, 8, 6, 4, 1), (1, 1, 1, 3, 5, 2)])
+def test_transition_vs_oracle(N, H, W, Ci, Co, S):
+    from differential_equations_resnet_amd import runtime as rt
+    rng = np.random.default_rng(N * 100 + H + Ci)
+    x = rng.standard_normal((N, H, W, Ci)).astype(np.float32).astype(np.float64)
+    K2 = (rng.standard_normal((3, 3, Ci, Co)) * np.sqrt(2 / (9 * Ci))).astype(np.float32).astype(np.float64)
+    K1 = (rng.standard_normal((1, 1, Ci, Co)) * np.sqrt(2 / Ci)).astype(np.float32).astype(np.float64)
+    b2 = (rng.standard_normal(Co) * 0.1).astype(np.float32).astype(np.float64)
+    b1 = (rng.standard_normal(Co) * 0.1).astype(np.float32).astype(np.float64)
+    y_want, z = O.transition_fwd(x, K2, b2, K1, b1, S)
+    y, mask = rt.transition_forward(_t(x), _t(K2), _t(b2), _t(K1), _t(b1), S)
+    assert tuple(y.shape) == y_want.shape
+    assert_close(y.cpu().numpy(), y_want, rtol=0, atol=1e-5 * np.abs(y_want).max(), what="y")
+    m = mask.cpu().numpy().astype(bool)
+    near = np.abs(z) < 1e-5
+    assert np.array_equal(m[~near], (z > 0)[~near])
+    dy = rng.standard_normal(y_want.shape).astype(np.float32).astype(np.float64)
+    # the oracle backward on the kernel's own mask (ties at 0 decided as the GPU did)
+    zz = np.where(m, 1.0, -1.0)
+    dx_want, g_want = O.transition_bwd(dy, x, zz, K2, K1, S)
+    dx, dp = rt.transition_backward(_t(dy), _t(x), mask, _t(K2), _t(K1), S)
+    assert_close(dx.cpu().numpy(), dx_want, rtol=0, atol=1e-5 * np.abs(dx_want).max(), what="dx")
+    got = O.unflatten(dp.cpu().numpy().astype(np.float64), [g.shape for g in g_want])
+    for name, a, b in zip(("dK2", "db2", "dK1", "db1"), got, g_want):
+        assert_close(a, b, rtol=0, atol=1e-5 * max(np.abs(b).max(), 1e-12), what=name)
+
+
+def _stages_setup(stages, kind="3by3", anti=True, h=0.5, gamma=0.0, N=4, H=32, W=32, seed=0):
+    spec = O.StagesSpec(stages=stages, h=h, gamma=gamma, H=H, W=W, kind=kind, antisymmetric=anti)
+    rng = np.random.default_rng(seed)
+    params = O.stages_init_params(spec, rng, np.float64, bias_std=0.05)
+    # a smaller fc kernel keeps the logits O(1) (the deeper stages grow the activations; saturated
+    # softmaxes would turn fp32 rounding of the logits into probability errors above the bar)
+    params[-2] = params[-2] * 0.05
+    params = [p.astype(np.float32).astype(np.float64) for p in params]
+    imgs = rng.integers(0, 256, (N, H, W, 3)).astype(np.uint8)
+    onehot = np.eye(10)[rng.integers(0, 10, N)]
+    return spec, params, imgs, onehot
+
+
+def _check_net(ex, spec, params, imgs, onehot):
+    flat = _t(O.flatten(params))
+    assert flat.numel() == ex.n_params == spec.n_params()
+    probs_gpu = ex.forward(flat, torch.from_numpy(imgs).cuda()).cpu().numpy()
+    probs, cache = O.stages_forward(spec, params, imgs)
+    assert_close(probs_gpu, probs, rtol=1e-5, atol=1e-6, what="probs")
+    loss, grads = ex.forward_backward(flat, torch.from_numpy(imgs).cuda(), _t(onehot), want_probs=True)
+    want_loss = O.net_loss(probs, onehot)
+    assert abs(loss.item() - want_loss) <= 1e-5 * abs(want_loss)
+    assert_close(ex.probs.cpu().numpy(), probs, rtol=1e-5, atol=1e-6, what="probs (training call)")
+    g_want = O.stages_backward(spec, params, cache, onehot)
+    g_got = O.unflatten(grads.cpu().numpy().astype(np.float64), [p.shape for p in params])
+    for i, (a, b) in enumerate(zip(g_got, g_want)):
+        assert_close(a, b, rtol=0, atol=1e-4 * max(np.abs(b).max(), 1e-12), what=f"grad[{i}] {b.shape}")
+
+
+@pytest.mark.parametrize("stages,kind,anti,gamma", [
+    ([(16, 2, 0), (32, 2, 2), (64, 2, 2)], "3by3", True, 0.0),     # He-style ResNet-32 layout, 2 blocks per stage
+    ([(16, 2, 0), (32, 2, 2), (64, 2, 2)], "3by3", True, -0.05),
+    ([(16, 1, 0), (32, 1, 2), (32, 1, 0), (64, 0, 2)], "regular", False, 0.0),  # no-transition stage, empty stage
+    ([(8, 1, 0), (12, 2, 1)], "general", False, 0.0),               # stride-1 transition, generic shapes
+])
+def test_stages_network_vs_oracle(stages, kind, anti, gamma):
+    from differential_equations_resnet_amd.runtime import StagesExecutor
+    spec, params, imgs, onehot = _stages_setup(stages, kind, anti, gamma=gamma)
+    ex = StagesExecutor(imgs.shape[0], spec.H, spec.W, 3, stages, 10, spec.h, spec.gamma, subtract_mean=127.5,
+                        divide_by_stddev=127.5, input_u8=True, param_kind=KINDS[kind], antisymmetric=anti)
+    _check_net(ex, spec, params, imgs, onehot)
+
+
+def test_resnet32_he_model_lowers_and_matches_oracle():
+    """The He-style ResNet-32 as the reference builds it (num_stages=4, blocks
+    [10,10,10] at 32^2 x 16, 16^2 x 32, 8^2 x 64, tfkeras_resnets.py:575-593),
+    through the drop-in Model API: compile_native -> forward_backward, Adam."""
+    from differential_equations_resnet_amd import graph
+    from differential_equations_resnet_amd.graph import Input
+    from differential_equations_resnet_amd.lowering import StagesPlan
+    from differential_equations_resnet_amd.models import tfkeras_resnets as R
+    graph.set_seed(3)
+    fn = R.get_single_block_resnet_build_function(kernel_type="antisymmetric", h=0.5, num_stages=4,
+                                                  blocks_per_stage=[10, 10, 10], filters_per_block=[16, 32, 64],
+                                                  strides=[(1, 1), (2, 2), (2, 2)], subtract_mean=127.5,
+                                                  divide_by_stddev=127.5, num_classes=10)
+    m = fn(Input(shape=(32, 32, 3)))
+    nv = m.compile_native(6)
+    assert isinstance(nv.state.plan, StagesPlan) and nv.state.plan.stages == [(16, 10, 0), (32, 9, 2), (64, 9, 2)]
+    spec = O.StagesSpec(stages=nv.state.plan.stages, h=0.5)
+    params = [v.value.astype(np.float64) for v in nv.state.plan.weight_vars()]
+    rng = np.random.default_rng(5)
+    imgs = rng.integers(0, 256, (6, 32, 32, 3)).astype(np.uint8)
+    onehot = np.eye(10)[rng.integers(0, 10, 6)]
+    loss, grads, probs = nv.forward_backward(imgs, onehot.astype(np.float32), want_probs=True)
+    p_want, cache = O.stages_forward(spec, params, imgs)
+    assert_close(probs.cpu().numpy(), p_want, rtol=1e-5, atol=1e-6, what="probs")
+    assert abs(loss.item() - O.net_loss(p_want, onehot)) <= 1e-5 * O.net_loss(p_want, onehot)
+    g_want = O.stages_backward(spec, params, cache, onehot)
+    g_got = O.unflatten(grads.cpu().numpy().astype(np.float64), [p.shape for p in params])
+    for i, (a, b) in enumerate(zip(g_got, g_want)):
+        assert_close(a, b, rtol=0, atol=1e-4 * max(np.abs(b).max(), 1e-12), what=f"grad[{i}] {b.shape}")
+    # one TF1 Adam step through the native update, then predict() on the inference executor
+    m0 = [p.copy() for p in params]
+    nv.apply_adam(grads, 1e-3)
+    mm = [np.zeros_like(p) for p in params]
+    vv = [np.zeros_like(p) for p in params]
+    O.adam_tf1(m0, g_want, mm, vv, 1)
+    got = O.unflatten(nv.params.cpu().numpy().astype(np.float64), [p.shape for p in params])
+    for a, b in zip(got, m0):
+        assert_close(a, b, rtol=0, atol=1e-5 * max(np.abs(b).max(), 1e-12), what="adam")
+    pr = nv.predict(imgs)
+    p2, _ = O.stages_forward(spec, got, imgs)
+    assert_close(pr, p2, rtol=1e-5, atol=1e-6, what="predict after adam")

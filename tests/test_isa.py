@@ -40,7 +40,7 @@ import asm_vmem_audit  # noqa: E402
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 pytestmark = pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S", "-w"]
-KERNEL_SOURCES = ["asr_block_mfma.hip", "asr_deep16.hip", "asr_stem_head.hip", "asr_conv_f32.hip", "asr_theta.hip",
+KERNEL_SOURCES = ["asr_block_mfma.hip", "asr_deep16.hip", "asr_stem_head.hip", "asr_conv_f32.hip", "asr_theta.hip", "asr_stages.hip",
                   "asr_api.hip"]
 
 # (kernel-name regex) -> (max VGPR spills, max scratch bytes, why)

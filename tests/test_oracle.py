@@ -241,3 +241,62 @@ def test_torch_cpu_restatement_matches_numpy_oracle():
     g = O.net_backward(spec, params, cache, oh)
     for a, b in zip(net.params, g):
         assert np.abs(a.grad.numpy() - b).max() <= 1e-4 * max(np.abs(b).max(), 1e-6)
+
+
+@pytest.mark.parametrize("H,W,S", [(6, 7, 2), (7, 7, 2), (5, 6, 1)])
+def test_transition_oracle_finite_differences(H, W, S):
+    """single_layer_conv_block's restatement (TF 'same' stride padding, 1x1
+    'valid' shortcut) against central differences of its own forward."""
+    rng = np.random.default_rng(H * 10 + S)
+    x = rng.standard_normal((2, H, W, 3))
+    K2, b2 = rng.standard_normal((3, 3, 3, 4)), rng.standard_normal(4) * 0.1
+    K1, b1 = rng.standard_normal((1, 1, 3, 4)), rng.standard_normal(4)
+    y, z = O.transition_fwd(x, K2, b2, K1, b1, S)
+    assert y.shape == (2, -(-H // S), -(-W // S), 4)
+    dy = rng.standard_normal(y.shape)
+    dx, g = O.transition_bwd(dy, x, z, K2, K1, S)
+    args = [x, K2, b2, K1, b1]
+    grads = [dx] + g
+
+    def f(a):
+        return (O.transition_fwd(*a, S)[0] * dy).sum()
+    for k in range(5):
+        for _ in range(4):
+            j = tuple(rng.integers(0, s) for s in args[k].shape)
+            a = [v.copy() for v in args]
+            a[k][j] += 1e-6
+            fp = f(a)
+            a[k][j] -= 2e-6
+            fm = f(a)
+            assert abs((fp - fm) / 2e-6 - grads[k][j]) < 1e-6 * max(1.0, abs(grads[k][j]))
+
+
+def test_transition_oracle_same_padding_is_tf_asymmetric():
+    """TF 'SAME' at stride 2 on an even input pads only bottom/right: output
+    (0, 0) of a 3x3 reads input rows/cols 0..2, not -1..1."""
+    x = np.zeros((1, 4, 4, 1))
+    x[0, 0, 0, 0] = 1.0
+    K2 = np.zeros((3, 3, 1, 1))
+    K2[0, 0, 0, 0] = 1.0  # top-left tap
+    y, _ = O.transition_fwd(x, K2, np.zeros(1), np.zeros((1, 1, 1, 1)), np.zeros(1), 2)
+    assert y[0, 0, 0, 0] == 1.0
+
+
+def test_stages_oracle_finite_differences():
+    rng = np.random.default_rng(1)
+    sp = O.StagesSpec(stages=[(4, 1, 0), (8, 2, 2), (8, 1, 0)], H=6, W=7, num_classes=5, h=0.7, gamma=0.1)
+    P = O.stages_init_params(sp, rng, bias_std=0.1)
+    imgs = rng.integers(0, 256, (3, 6, 7, 3)).astype(np.float64)
+    oh = np.eye(5)[rng.integers(0, 5, 3)]
+    pr, c = O.stages_forward(sp, P, imgs)
+    g = O.stages_backward(sp, P, c, oh)
+    assert [x.shape for x in g] == [tuple(s) for s in sp.param_shapes()]
+    for k in range(len(P)):
+        for _ in range(2):
+            j = tuple(rng.integers(0, s) for s in P[k].shape)
+            a = [v.copy() for v in P]
+            a[k][j] += 1e-6
+            fp = O.net_loss(O.stages_forward(sp, a, imgs)[0], oh)
+            a[k][j] -= 2e-6
+            fm = O.net_loss(O.stages_forward(sp, a, imgs)[0], oh)
+            assert abs((fp - fm) / 2e-6 - g[k][j]) < 1e-7 + 1e-4 * abs(g[k][j])
