@@ -1,6 +1,7 @@
 // fp32 path of the 3x3 conv / Euler block: fp32 MFMA (v_mfma_f32_16x16x4_f32)
-// for the network's blocks (C in {16, 32, 64}, W = 32), exact fp32 FMA chains
-// on the VALU for every other shape.
+// for the network's blocks (C in {16, 32, 64}, W in {32, 16, 8}: the single-stage
+// nets and the stages of the multi-stage ones), exact fp32 FMA chains on the
+// VALU for every other shape.
 //
 // This is the reference-precision path (the reference computes everything in
 // fp32, layers/tfkeras_layer_Conv2DAntisymmetric3By3.py:157-171), used for the
@@ -153,15 +154,16 @@ __global__ void k_db_f32(const float* __restrict__ dz, long rows, int W, int C, 
 // ===========================================================================
 // fp32 on the matrix cores: v_mfma_f32_16x16x4_f32 (fp32 operands, fp32
 // accumulation: the reference's precision, …3By3.py:157-171) for the 3x3
-// SAME conv / Euler block with C_in = C_out = C in {16, 32, 64}, W = 32.
+// SAME conv / Euler block with C_in = C_out = C in {16, 32, 64}, W in {32, 16, 8}.
 //
 // Forward / dgrad (k_conv32): implicit GEMM D[o][px] = sum_kappa W^T[o][kappa]
 // X[kappa][px], kappa = (tap, i).  A workgroup (4 waves) owns a band of BR = 4
 // output rows of one image: the BR + 2 input rows (zero rows outside the
 // image, zero halo columns) are staged in LDS once, every wave keeps its
 // o-tile's A = W^T fragments in registers for the launch (9C/4 VGPRs) and
-// walks its rows (C=16: one row per wave; C=64: one o-tile per wave, all 4
-// rows).  K-step s of channel group q at a tap gives lane (lx, g) the
+// walks its share of the band's 16-pixel tiles (band pixel 16 tile + lx; at
+// W = 8 a tile spans two rows; C=16: the 4 waves deal the tiles round-robin;
+// C=64: one o-tile per wave, every tile).  K-step s of channel group q at a tap gives lane (lx, g) the
 // channel 16q + 4g + s, so one 16-B LDS read per lane (the pixel's channels
 // 16q+4g .. +3) feeds four MFMAs.  The accumulator lane (lx, g) holds
 // channels 4g .. 4g+3 of pixel lx: the residual / dy / dz operands and the
@@ -177,20 +179,22 @@ __global__ void k_db_f32(const float* __restrict__ dz, long rows, int W, int C, 
 // waves), reduced by the same two-pass k_reduce_slabs / projection as the
 // bf16 path.
 // ===========================================================================
-template <int C>
+template <int C, int W_>
 struct F32Band {
-  static constexpr int OT = C / 16, W = 32, TW = W + 2, BR = 4, ROWF = TW * C, TILEF = (BR + 2) * ROWF;
-  static constexpr int RSTEP = 4 / OT;  // rows between a wave's rows (forward / dgrad)
+  static constexpr int OT = C / 16, W = W_, TW = W + 2, BR = 4, ROWF = TW * C, TILEF = (BR + 2) * ROWF;
+  static constexpr int T = BR * W / 16;  // 16-pixel tiles per band (band pixel p = 16 tile + lx: row p / W, col p % W)
+  static constexpr int WPT = 4 / OT;    // forward / dgrad: waves sharing an o-tile, tiles dealt round-robin
   static constexpr int RS = 4 / OT;     // wgrad row split: 3 * OT * RS = 12 waves
   static constexpr int DZF = BR * W * C;
+  static_assert(W == 8 || W == 16 || W == 32, "fp32 MFMA band: W in {8, 16, 32}");
 };
 
 // stage rows y0-1 .. y0+BR of image n into tile (zeros outside the image and
 // in the two halo columns), float4 per thread
-template <int C>
+template <int C, int W>
 __device__ __forceinline__ void f32_stage_rows(const float* __restrict__ src, float* tile, int n, int y0, int H,
                                                int tid, int nthreads) {
-  using G = F32Band<C>;
+  using G = F32Band<C, W>;
   constexpr int C4 = C / 4, NCH = (G::BR + 2) * G::TW * C4;
   for (int i = tid; i < NCH; i += nthreads) {
     const int r = i / (G::TW * C4), rem = i % (G::TW * C4), col = rem / C4, c4 = rem % C4;
@@ -202,13 +206,13 @@ __device__ __forceinline__ void f32_stage_rows(const float* __restrict__ src, fl
   }
 }
 
-template <int C, int MODE>
+template <int C, int W, int MODE>
 __global__ __launch_bounds__(256) void k_conv32(const float* __restrict__ xin, float* __restrict__ out,
                                                 uint8_t* __restrict__ mask, const float* __restrict__ w,
                                                 const float* __restrict__ bias, float h, float two_gamma,
                                                 const float* __restrict__ dy, const float* __restrict__ extra, int N,
                                                 int H) {
-  using G = F32Band<C>;
+  using G = F32Band<C, W>;
   constexpr int OT = G::OT, TW = G::TW, BR = G::BR;
   __shared__ __attribute__((aligned(16))) float tile[G::TILEF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
@@ -226,63 +230,67 @@ __global__ __launch_bounds__(256) void k_conv32(const float* __restrict__ xin, f
       for (int s = 0; s < 4; ++s) A[t][q][s] = w[((long)t * C + 16 * q + 4 * g + s) * C + 16 * ot + lx];
   f32x4 bz = {0.f, 0.f, 0.f, 0.f};
   if (MODE <= F_RELU && bias) bz = *(const f32x4*)(bias + 16 * ot + 4 * g);
-  f32_stage_rows<C>(xin, tile, n, y0, H, tid, 256);
+  f32_stage_rows<C, W>(xin, tile, n, y0, H, tid, 256);
   __syncthreads();
+  // wave (ot, rw) takes the band's 16-pixel tiles rw, rw + WPT, ..; lane lx's pixel of tile tau is band
+  // pixel 16 tau + lx (W = 8: a tile spans two rows, so validity is per lane)
+  constexpr int NT = (G::T + G::WPT - 1) / G::WPT;
 #pragma unroll
-  for (int k = 0; k < OT; ++k) {
-    const int r = rw + k * G::RSTEP;
-    if (y0 + r >= H) break;  // (wave-uniform)
-    f32x4 acc[2] = {bz, bz};
+  for (int j = 0; j < NT; ++j) {
+    const int tau = rw + j * G::WPT;
+    if (tau >= G::T) break;  // (wave-uniform)
+    const int bp = 16 * tau + lx, r = bp / W, px = bp % W;
+    if (W >= 16 && y0 + r >= H) break;  // (wave-uniform for W >= 16; rows only grow with tau)
+    f32x4 acc = bz;
 #pragma unroll
-    for (int pt = 0; pt < 2; ++pt)
+    for (int t = 0; t < 9; ++t)
 #pragma unroll
-      for (int t = 0; t < 9; ++t)
+      for (int q = 0; q < OT; ++q) {
+        const f32x4 bv = *(const f32x4*)(tile + ((r + t / 3) * TW + px + t % 3) * C + 16 * q + 4 * g);
 #pragma unroll
-        for (int q = 0; q < OT; ++q) {
-          const f32x4 bv = *(const f32x4*)(tile + ((r + t / 3) * TW + 16 * pt + lx + t % 3) * C + 16 * q + 4 * g);
-#pragma unroll
-          for (int s = 0; s < 4; ++s) acc[pt] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[t][q][s], bv[s], acc[pt], 0, 0, 0);
-        }
-#pragma unroll
-    for (int pt = 0; pt < 2; ++pt) {
-      const int px = 16 * pt + lx;
-      const long pix = ((long)n * H + y0 + r) * G::W + px;
+        for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[t][q][s], bv[s], acc, 0, 0, 0);
+      }
+    {
+      const bool ok = y0 + r < H;
+      const long pix = ((long)n * H + y0 + r) * W + px;
       const long oi = pix * C + 16 * ot + 4 * g;  // this lane's 4 channels
       const f32x4 ctr = *(const f32x4*)(tile + ((r + 1) * TW + px + 1) * C + 16 * ot + 4 * g);  // x or dz at the pixel
       f32x4 v;
       if constexpr (MODE == F_EULER) {
-        const f32x4 res = extra ? *(const f32x4*)(extra + oi) : ctr;
+        const f32x4 res = (extra && ok) ? *(const f32x4*)(extra + oi) : ctr;
         unsigned nib = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float z = acc[pt][j];
-          nib |= (z > 0.f ? 1u : 0u) << j;
-          v[j] = res[j] + h * fmaxf(z, 0.f);
+        for (int e = 0; e < 4; ++e) {
+          const float z = acc[e];
+          nib |= (z > 0.f ? 1u : 0u) << e;
+          v[e] = res[e] + h * fmaxf(z, 0.f);
         }
         if (mask) {  // the pixel's 16 channels of this o-tile: 4 nibbles, one 16-bit store
           unsigned m = nib << (4 * g);
           m |= (unsigned)__shfl_xor((int)m, 16, 64);
           m |= (unsigned)__shfl_xor((int)m, 32, 64);
-          if (g == 0) *(uint16_t*)(mask + (pix * C + 16 * ot) / 8) = (uint16_t)m;
+          if (g == 0 && ok) *(uint16_t*)(mask + (pix * C + 16 * ot) / 8) = (uint16_t)m;
         }
       } else if constexpr (MODE == F_CONV) {
-        v = acc[pt];
+        v = acc;
       } else {  // B_EULER / B_CONV: the tile holds dz; dx = [dy] - A dz + 2 gamma dz [+ extra]
         f32x4 d0 = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (MODE == B_EULER) d0 = *(const f32x4*)(dy + oi);
-        if (extra) d0 += *(const f32x4*)(extra + oi);
+        if (ok) {
+          if constexpr (MODE == B_EULER) d0 = *(const f32x4*)(dy + oi);
+          if (extra) d0 += *(const f32x4*)(extra + oi);
+        }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = d0[j] - acc[pt][j] + two_gamma * ctr[j];
+        for (int e = 0; e < 4; ++e) v[e] = d0[e] - acc[e] + two_gamma * ctr[e];
       }
-      *(f32x4*)(out + oi) = v;
+      if (ok) *(f32x4*)(out + oi) = v;
     }
   }
 }
 
-template <int C>
+template <int C, int W>
 __global__ __launch_bounds__(768) void k_wgrad32(const float* __restrict__ x, const float* __restrict__ dz, int N,
                                                  int H, float* __restrict__ slabs) {
-  using G = F32Band<C>;
+  using G = F32Band<C, W>;
   constexpr int OT = G::OT, TW = G::TW, BR = G::BR, RS = G::RS, E = 9 * C * C;
   extern __shared__ __attribute__((aligned(16))) float lds32[];
   float* xt = lds32;               // [BR+2][TW][C]
@@ -301,7 +309,7 @@ __global__ __launch_bounds__(768) void k_wgrad32(const float* __restrict__ x, co
     const int n = (int)(item / nb), y0 = (int)(item % nb) * BR;
     const int rows = min(BR, H - y0);
     __syncthreads();  // the previous item's tiles consumed
-    f32_stage_rows<C>(x, xt, n, y0, H, tid, 768);
+    f32_stage_rows<C, W>(x, xt, n, y0, H, tid, 768);
     for (int i = tid; i < BR * G::W * C / 4; i += 768) {
       const int r = i / (G::W * C / 4);
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -364,47 +372,62 @@ __global__ __launch_bounds__(768) void k_wgrad32(const float* __restrict__ x, co
   }
 }
 
-template <int C>
+template <int C, int W>
 static size_t wgrad32_lds() {
-  using G = F32Band<C>;
+  using G = F32Band<C, W>;
   const size_t stage = (size_t)(G::TILEF + G::DZF) * 4;
   const size_t red = G::RS > 1 ? (size_t)12 * (3 * G::OT + 1) * 256 * 4 : 0;
   return std::max(stage, red);
 }
 
-static bool conv32_supported(int W, int Ci, int Co) { return W == 32 && Ci == Co && (Ci == 16 || Ci == 32 || Ci == 64); }
+// the multi-stage nets' 16x16 and 8x8 stages (asr_stages.hip) run the same kernels at W = 16 / 8
+static bool conv32_supported(int W, int Ci, int Co) {
+  return (W == 32 || W == 16 || W == 8) && Ci == Co && (Ci == 16 || Ci == 32 || Ci == 64);
+}
 
-template <int C, int MODE>
+template <int C, int W, int MODE>
 static int launch_conv32(const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
                          float two_gamma, const float* dy, const float* extra, int N, int H, hipStream_t s) {
   const long blocks = (long)N * ((H + 3) / 4);
   if (blocks > 0x7fffffffL) return fail(ASR_E_ARG, "conv f32: problem too large");
-  hipLaunchKernelGGL((k_conv32<C, MODE>), dim3((unsigned)blocks), dim3(256), 0, s, (const float*)xin, (float*)out,
-                     mask, w, bias, h, two_gamma, dy, extra, N, H);
+  hipLaunchKernelGGL((k_conv32<C, W, MODE>), dim3((unsigned)blocks), dim3(256), 0, s, (const float*)xin,
+                     (float*)out, mask, w, bias, h, two_gamma, dy, extra, N, H);
   ASR_LAUNCH_CHECK("k_conv32");
   return ASR_OK;
 }
 
+template <int C, int MODE>
+static int conv32_dispatch_w(int W, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias,
+                             float h, float two_gamma, const float* dy, const float* extra, int N, int H,
+                             hipStream_t s) {
+  switch (W) {
+    case 32: return launch_conv32<C, 32, MODE>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+    case 16: return launch_conv32<C, 16, MODE>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+    case 8: return launch_conv32<C, 8, MODE>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+  }
+  return fail(ASR_E_UNSUPPORTED, "conv f32 (MFMA): W=%d", W);
+}
+
 template <int MODE>
-static int conv32_dispatch(int C, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias,
+static int conv32_dispatch(int C, int W, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias,
                            float h, float two_gamma, const float* dy, const float* extra, int N, int H, hipStream_t s) {
   switch (C) {
-    case 16: return launch_conv32<16, MODE>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
-    case 32: return launch_conv32<32, MODE>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
-    case 64: return launch_conv32<64, MODE>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+    case 16: return conv32_dispatch_w<16, MODE>(W, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+    case 32: return conv32_dispatch_w<32, MODE>(W, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+    case 64: return conv32_dispatch_w<64, MODE>(W, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
   }
   return fail(ASR_E_UNSUPPORTED, "conv f32 (MFMA): C=%d", C);
 }
 
-template <int C>
+template <int C, int W>
 static int launch_wgrad32(const float* x, const float* dz, int N, int H, float* slabs, int* nslabs, hipStream_t s) {
   const long items = (long)N * ((H + 3) / 4);
   int cus = cu_count();
   if (cus <= 0) cus = 256;
-  const size_t lds = wgrad32_lds<C>();
+  const size_t lds = wgrad32_lds<C, W>();
   const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
   const int grid = (int)std::max<long>(1, std::min<long>({items, (long)per_cu * cus, 512L}));
-  hipLaunchKernelGGL((k_wgrad32<C>), dim3(grid), dim3(768), lds, s, x, dz, N, H, slabs);
+  hipLaunchKernelGGL((k_wgrad32<C, W>), dim3(grid), dim3(768), lds, s, x, dz, N, H, slabs);
   ASR_LAUNCH_CHECK("k_wgrad32");
   *nslabs = grid;
   return ASR_OK;
@@ -432,10 +455,10 @@ int conv_f32(int fmode, const void* xin, void* out, uint8_t* mask, const float* 
              const float* extra) {
   if (conv32_supported(W, Ci, Co) && fmode != F_RELU) {  // the network's blocks: fp32 MFMA
     switch (fmode) {
-      case F_EULER: return conv32_dispatch<F_EULER>(Ci, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
-      case F_CONV: return conv32_dispatch<F_CONV>(Ci, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
-      case B_EULER: return conv32_dispatch<B_EULER>(Ci, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
-      case B_CONV: return conv32_dispatch<B_CONV>(Ci, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+      case F_EULER: return conv32_dispatch<F_EULER>(Ci, W, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+      case F_CONV: return conv32_dispatch<F_CONV>(Ci, W, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+      case B_EULER: return conv32_dispatch<B_EULER>(Ci, W, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+      case B_CONV: return conv32_dispatch<B_CONV>(Ci, W, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
     }
   }
   switch (fmode) {
@@ -498,11 +521,19 @@ int wgrad_f32_chunks(int N, int H) {
 int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, int Ci, int Co, float* slabs,
               int* nslabs, hipStream_t s, int K) {
   if (!x_bf16 && K == 3 && conv32_supported(W, Ci, Co)) {  // the network's blocks: fp32 MFMA, db included
+#define ASR_WG32(CC)                                                                         \
+  switch (W) {                                                                               \
+    case 32: return launch_wgrad32<CC, 32>((const float*)x, dz, N, H, slabs, nslabs, s);     \
+    case 16: return launch_wgrad32<CC, 16>((const float*)x, dz, N, H, slabs, nslabs, s);     \
+    case 8: return launch_wgrad32<CC, 8>((const float*)x, dz, N, H, slabs, nslabs, s);       \
+  }                                                                                          \
+  break
     switch (Ci) {
-      case 16: return launch_wgrad32<16>((const float*)x, dz, N, H, slabs, nslabs, s);
-      case 32: return launch_wgrad32<32>((const float*)x, dz, N, H, slabs, nslabs, s);
-      case 64: return launch_wgrad32<64>((const float*)x, dz, N, H, slabs, nslabs, s);
+      case 16: ASR_WG32(16);
+      case 32: ASR_WG32(32);
+      case 64: ASR_WG32(64);
     }
+#undef ASR_WG32
   }
   const long R = (long)N * H;
   const int chunks = wgrad_f32_chunks(N, H);

@@ -78,7 +78,9 @@ def _oracle_W(th, C, gamma, bf):
 
 
 SHAPES_BF16 = [(2, 32, 32, 16), (2, 32, 32, 32), (2, 32, 32, 64), (1, 11, 32, 64), (3, 5, 32, 16)]
-SHAPES_F32 = [(2, 32, 32, 16), (1, 7, 13, 5), (2, 9, 32, 64), (1, 3, 3, 1), (2, 32, 32, 32), (3, 6, 32, 16)]
+SHAPES_F32 = [(2, 32, 32, 16), (1, 7, 13, 5), (2, 9, 32, 64), (1, 3, 3, 1), (2, 32, 32, 32), (3, 6, 32, 16),
+              # the multi-stage nets' 16x16 / 8x8 stages on the same fp32 MFMA kernels (odd H: partial bands)
+              (2, 16, 16, 32), (3, 7, 16, 16), (2, 8, 8, 64), (2, 5, 8, 16), (1, 9, 8, 32)]
 
 
 @pytest.mark.parametrize("dtype_name,shape", [("f32", s) for s in SHAPES_F32] + [("bf16", s) for s in SHAPES_BF16])
