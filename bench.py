@@ -81,6 +81,12 @@ CONFIGS = {
     "v7_predict": (16, 64, 1, "bfloat16", "antisym 64 blocks x 16 filters, Model.predict of ONE image (v7 notebook "
                    "speed test), bf16", "euler", "eval"),
 }
+# multi-stage nets (asr_stages_*, fp32): name -> (stages [(C, L, transition stride)], per-GPU batch, description)
+STAGE_CONFIGS = {
+    "he32": ([(16, 10, 0), (32, 9, 2), (64, 9, 2)], 128,
+             "He-style antisym-ResNet-32 (num_stages=4, blocks [10,10,10] at 32^2 x 16, 16^2 x 32, 8^2 x 64, stride-2 "
+             "single_layer_conv_block transitions, tfkeras_resnets.py:575-593) batch 128/GPU fp32"),
+}
 # the reference's own measurements of the same metric (TF 1.12, fp32, one NVIDIA GPU)
 REFERENCE = {
     "v6": (46.7, "images/s", "training 1.46 it/s x 32, experiments_antisymmetric_resnet_v6.ipynb:362"),
@@ -99,7 +105,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + sorted(STAGE_CONFIGS))
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--block-reps", type=int, default=50)
     ap.add_argument("--timed-steps", type=int, default=10,
@@ -492,10 +498,111 @@ def cpu_eval_baseline(threads):
                       f"op-by-op restatement of the reference TF graph, after 1 untimed pass; {dt:.1f} s"}
 
 
+def stages_params(stages, num_classes=10, seed=0):
+    """Flat parameters in the asr_stages_config order: he_normal (2-sigma
+    truncated) kernels, zero biases, block thetas x THETA_SCALE and the fc
+    kernel x FC_SCALE (as bench_params)."""
+    from differential_equations_resnet_amd import runtime as rt
+    rng = np.random.default_rng(seed)
+
+    def he(shape, fan_in, scale=1.0):
+        return (np.clip(rng.standard_normal(shape), -2, 2) * np.sqrt(2.0 / fan_in) * scale).astype(np.float32)
+    out = [he(3 * 3 * 3 * stages[0][0], 27), np.zeros(stages[0][0], np.float32)]
+    Cp = stages[0][0]
+    for C, L, S in stages:
+        if S:
+            out += [he(9 * Cp * C, 9 * Cp), np.zeros(C, np.float32), he(Cp * C, Cp), np.zeros(C, np.float32)]
+        for _ in range(L):
+            out += [he(rt.theta_count(C), 9 * C, THETA_SCALE), np.zeros(C, np.float32)]
+        Cp = C
+    out += [he(Cp * num_classes, Cp, FC_SCALE), np.zeros(num_classes, np.float32)]
+    return np.concatenate(out)
+
+
+def stages_main(args):
+    """--config he32: one training step (fwd + bwd + Adam) of a multi-stage
+    net on the asr_stages_* executor, same timing contract as main()."""
+    import torch
+    from differential_equations_resnet_amd import distributed, runtime as rt
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    dev = rt.require_gpu()
+    distributed.init_from_env(device=dev)
+    stages, N, desc = STAGE_CONFIGS[args.config]
+    L = sum(l for _, l, _ in stages)
+    h = 8.0 / L
+    ex = rt.StagesExecutor(N, 32, 32, 3, stages, 10, h, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
+                           input_u8=True, device=dev)
+    params = torch.from_numpy(stages_params(stages)).to(dev)
+    assert params.numel() == ex.n_params
+    distributed.broadcast_params(params, 0)
+    m, v = torch.zeros_like(params), torch.zeros_like(params)
+    rng = np.random.default_rng(1234 + rank)
+    batches = [(torch.from_numpy(rng.integers(0, 256, (N, 32, 32, 3), dtype=np.uint8)).to(dev),
+                torch.from_numpy(np.eye(10, dtype=np.float32)[rng.integers(0, 10, N)]).to(dev))
+               for _ in range(N_BATCHES)]
+    k = [0]
+
+    def step():
+        images, targets = batches[k[0] % N_BATCHES]
+        k[0] += 1
+        loss, grads = ex.forward_backward(params, images, targets)
+        distributed.allreduce_grads(grads)
+        rt.adam_update(params, grads, m, v, args.lr, 0.9, 0.999, 1e-7, k[0], 1.0 / world)
+        return loss
+    first = None
+    for i in range(args.warmup):
+        out = step()
+        if i == 0:
+            first = float(out.item())
+    distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = distributed.max_over_ranks(time.perf_counter() - t0)
+    value = N * world * args.steps / elapsed
+    if rank == 0:
+        # conv FLOPs per image, forward: stem, transitions (3x3 + 1x1), identity blocks; train = 3x forward
+        fl, Hc, Cp = 2 * 9 * 3 * stages[0][0] * 32 * 32, 32, stages[0][0]
+        for C, Lb, S in stages:
+            if S:
+                Hc = -(-Hc // S)
+                fl += 2 * 10 * Cp * C * Hc * Hc
+            fl += Lb * 2 * 9 * C * C * Hc * Hc
+            Cp = C
+        tflops = 3 * fl * N * world / (elapsed / args.steps) / 1e12 / world
+        out_line = {
+            "metric": f"CIFAR-10 images/sec (fwd+bwd) {desc}; {world} GPU", "value": round(value, 1),
+            "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": f"synthetic ({N_BATCHES} HBM-resident batches of uniform uint8 32x32x3 images, random one-hot "
+                    f"labels; he_normal init, thetas x{THETA_SCALE}, fc x{FC_SCALE})",
+            "config": {"workload": desc + "; train step = fwd + bwd + Adam (asr_stages_forward_backward)",
+                       "global_batch": N * world, "per_gpu_batch": N, "stages": stages, "h": round(h, 6),
+                       "parallelism": f"dp{world}", "initial_loss": round(first, 4) if first is not None else None,
+                       "final_loss": round(float(out.item()), 4)},
+            "roofline": {"bound": "mfma", "achieved": round(tflops, 2), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tflops / F32_PEAK_TFLOPS, 4), "traffic": None,
+                         "kernel": "whole step per GPU (conv FLOPs 3 x forward / step time; all kernels incl. "
+                                   "stem, head, reductions, Adam)"},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(out_line), flush=True)
+    distributed.shutdown()
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))
+    if args.config in STAGE_CONFIGS:
+        return stages_main(args)
 
     import torch
     from differential_equations_resnet_amd import _lib, distributed, runtime as rt

@@ -5,8 +5,8 @@
 // [10, 10, 10] blocks at 32^2 x 16, 16^2 x 32, 8^2 x 64).
 //
 // The identity blocks of every stage run the fp32 block kernels of the
-// single-stage executor (asr_conv_forward / asr_conv_backward: fp32 MFMA at
-// W = 32, C in {16, 32, 64}, the fp32 VALU kernel at the smaller stages); the
+// single-stage executor (asr_conv_forward / asr_conv_backward: fp32 MFMA for
+// C in {16, 32, 64} at W in {32, 16, 8}, the fp32 VALU kernel otherwise); the
 // stem and head are the single-stage executor's kernels.
 //
 // Transition, for output pixel p = (n, yo, xo) and channel o (stride S, TF
@@ -20,10 +20,12 @@
 //     dK2[ky][kx][i][o] = sum_p x[S yo + ky - pt][S xo + kx - pl][i] dz[p][o],  db2 = sum_p dz
 //     dK1[i][o]         = sum_p x[S yo][S xo][i] dy[p][o],                     db1 = sum_p dy
 // These convolutions carry ~2 % of a ResNet-32 step's FLOPs (two transitions
-// against 28 identity blocks), so they stay on the VALU: one lane per (pixel,
-// 4 output channels) in the forward, per (input pixel, channel) in dgrad, per
-// weight element over a chunk of output rows in wgrad (partials reduced by one
-// more launch).
+// against 28 identity blocks).  With Ci, Co multiples of 16 they run on the
+// fp32 matrix cores (k_trans_*_mfma, one wave per 16 x 16 output tile,
+// operands from global memory); other shapes on the VALU: one lane per
+// (pixel, 4 output channels) in the forward, per (input pixel, channel) in
+// dgrad, per weight element over a chunk of output rows in wgrad.  Weight
+// gradient partials per chunk are reduced by one more launch.
 #include <algorithm>
 #include <vector>
 
@@ -235,6 +237,192 @@ __global__ __launch_bounds__(256) void k_sum_chunks(const float* __restrict__ pa
   out[e] = acc;
 }
 
+// ---------------------------------------------------------------------------
+// the same three convolutions on the fp32 matrix cores (v_mfma_f32_16x16x4_f32,
+// fp32 products and accumulation) when Ci and Co are multiples of 16 (every
+// transition of the reference's ResNets).  One wave per 16 x 16 output tile;
+// operands straight from global memory (L1/L2-resident weights and rows).
+// Lane (lx, g) of an MFMA step s over a 16-channel group q supplies reduction
+// index 16q + 4g + s for both operands, so A / B are 16-B loads of 4
+// consecutive channels; the accumulator lane (lx, g) holds rows 4g .. 4g+3 of
+// column lx.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; }
+__device__ __forceinline__ f32x4 mask4(const uint8_t* m) {
+  const unsigned u = *(const unsigned*)m;
+  return f32x4{(float)(u & 0xff), (float)((u >> 8) & 0xff), (float)((u >> 16) & 0xff), (float)(u >> 24)};
+}
+
+// forward: D[o][xo] over (tap, i) + the 1x1 shortcut; wave = (n, yo, 16 xo, 16 o)
+__global__ __launch_bounds__(256) void k_trans_fwd_mfma(const float* __restrict__ x, float* __restrict__ y,
+                                                        uint8_t* __restrict__ mask, const float* __restrict__ k2,
+                                                        const float* __restrict__ b2, const float* __restrict__ k1,
+                                                        const float* __restrict__ b1, int N, int H, int W, int Ci,
+                                                        int Co, int S, int Ho, int Wo, int pt, int pl) {
+  const int PT = (Wo + 15) / 16, OT = Co / 16;
+  const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (task >= (long)N * Ho * PT * OT) return;
+  const int lane = threadIdx.x & 63, g = lane >> 4, lx = lane & 15;
+  const int ot = (int)(task % OT);
+  long rest = task / OT;
+  const int ptile = (int)(rest % PT);
+  rest /= PT;
+  const int yo = (int)(rest % Ho), n = (int)(rest / Ho);
+  const int xo = 16 * ptile + lx;  // the B column (pixel) of this lane
+  const int o = 16 * ot + lx;      // the A row (output channel) of this lane
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accs = {0.f, 0.f, 0.f, 0.f};
+  for (int ky = 0; ky < kTK; ++ky) {
+    const int gy = S * yo + ky - pt;
+    if (gy < 0 || gy >= H) continue;  // (wave-uniform)
+    for (int kx = 0; kx < kTK; ++kx) {
+      const int gx = S * xo + kx - pl;
+      const bool ok = xo < Wo && gx >= 0 && gx < W;
+      const float* xp = x + (((long)n * H + gy) * W + (ok ? gx : 0)) * Ci + 4 * g;
+      const float* wp = k2 + (long)(ky * kTK + kx) * Ci * Co + (long)(4 * g) * Co + o;
+      for (int q = 0; q < Ci / 16; ++q) {
+        const f32x4 bv = ok ? ld4(xp + 16 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wp[(long)(16 * q + s4) * Co], bv[s4], acc, 0, 0, 0);
+      }
+    }
+  }
+  {
+    const bool ok = xo < Wo;
+    const float* xp = x + (((long)n * H + S * yo) * W + (ok ? S * xo : 0)) * Ci + 4 * g;
+    const float* wp = k1 + (long)(4 * g) * Co + o;
+    for (int q = 0; q < Ci / 16; ++q) {
+      const f32x4 bv = ok ? ld4(xp + 16 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+        accs = __builtin_amdgcn_mfma_f32_16x16x4f32(wp[(long)(16 * q + s4) * Co], bv[s4], accs, 0, 0, 0);
+    }
+  }
+  if (xo >= Wo) return;
+  const long p = ((long)n * Ho + yo) * Wo + xo;
+  const int o0 = 16 * ot + 4 * g;  // this lane's 4 output channels (accumulator rows)
+  const f32x4 bb2 = ld4(b2 + o0), bb1 = ld4(b1 + o0);
+  f32x4 v;
+  unsigned mb = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float z = acc[j] + bb2[j];
+    v[j] = fmaxf(z, 0.f) + (accs[j] + bb1[j]);
+    mb |= (z > 0.f ? 1u : 0u) << (8 * j);
+  }
+  *(f32x4*)(y + p * Co + o0) = v;
+  if (mask) *(unsigned*)(mask + p * Co + o0) = mb;
+}
+
+// dgrad: D[i][gx] over (tap, o) of dz = dy [z > 0] + the shortcut's dy; wave = (n, gy, 16 gx, 16 i)
+__global__ __launch_bounds__(256) void k_trans_dgrad_mfma(const float* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                          const float* __restrict__ k2, const float* __restrict__ k1,
+                                                          float* __restrict__ dx, int N, int H, int W, int Ci, int Co,
+                                                          int S, int Ho, int Wo, int pt, int pl) {
+  const int PT = (W + 15) / 16, IT = Ci / 16;
+  const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (task >= (long)N * H * PT * IT) return;
+  const int lane = threadIdx.x & 63, g = lane >> 4, lx = lane & 15;
+  const int it = (int)(task % IT);
+  long rest = task / IT;
+  const int ptile = (int)(rest % PT);
+  rest /= PT;
+  const int gy = (int)(rest % H), n = (int)(rest / H);
+  const int gx = 16 * ptile + lx;  // B column (input pixel)
+  const int i = 16 * it + lx;      // A row (input channel)
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int ky = 0; ky < kTK; ++ky) {
+    const int ty = gy + pt - ky;
+    if (ty < 0 || ty % S) continue;  // (wave-uniform)
+    const int yo = ty / S;
+    if (yo >= Ho) continue;
+    for (int kx = 0; kx < kTK; ++kx) {
+      const int tx = gx + pl - kx;
+      const bool ok = gx < W && tx >= 0 && tx % S == 0 && tx / S < Wo;
+      const long p = ((long)n * Ho + yo) * Wo + (ok ? tx / S : 0);
+      const float* dp = dy + p * Co + 4 * g;
+      const uint8_t* mp = mask + p * Co + 4 * g;
+      const float* wp = k2 + ((long)(ky * kTK + kx) * Ci + i) * Co + 4 * g;
+      for (int q = 0; q < Co / 16; ++q) {
+        const f32x4 av = ld4(wp + 16 * q);
+        const f32x4 bv = ok ? ld4(dp + 16 * q) * mask4(mp + 16 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s4], bv[s4], acc, 0, 0, 0);
+      }
+    }
+  }
+  if (gy % S == 0 && gy / S < Ho) {  // (wave-uniform)
+    const bool ok = gx < W && gx % S == 0 && gx / S < Wo;
+    const float* dp = dy + (((long)n * Ho + gy / S) * Wo + (ok ? gx / S : 0)) * Co + 4 * g;
+    const float* wp = k1 + (long)i * Co + 4 * g;
+    for (int q = 0; q < Co / 16; ++q) {
+      const f32x4 av = ld4(wp + 16 * q);
+      const f32x4 bv = ok ? ld4(dp + 16 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s4], bv[s4], acc, 0, 0, 0);
+    }
+  }
+  if (gx < W) *(f32x4*)(dx + (((long)n * H + gy) * W + gx) * Ci + 16 * it + 4 * g) = acc;
+}
+
+// wgrad partials: wave = (chunk of output pixels, 16 i, 16 o); the 9 taps' D[i][o] = sum_p x_tap[p][i] dz[p][o],
+// the shortcut's x_1x1 (x) dy, and (it == 0) db2 / db1 as ones (x) dz / dy; 4 pixels per MFMA step
+__global__ __launch_bounds__(256) void k_trans_wgrad_mfma(const float* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                          const float* __restrict__ x, float* __restrict__ part, int N,
+                                                          int H, int W, int Ci, int Co, int S, int Ho, int Wo, int pt,
+                                                          int pl, int px_per_chunk, int chunks) {
+  const int IT = Ci / 16, OT = Co / 16;
+  const long task = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (task >= (long)chunks * IT * OT) return;
+  const int lane = threadIdx.x & 63, g = lane >> 4, lx = lane & 15;
+  const int ot = (int)(task % OT), it = (int)((task / OT) % IT), chunk = (int)(task / ((long)OT * IT));
+  const long P = (long)N * Ho * Wo;
+  const long p0 = (long)chunk * px_per_chunk, p1 = min(P, p0 + px_per_chunk);
+  f32x4 acc[kTK * kTK + 1], accb2 = {0.f, 0.f, 0.f, 0.f}, accb1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t <= kTK * kTK; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ci = 16 * it + lx, co = 16 * ot + lx;  // A row (input channel), B column (output channel)
+  for (long pb = p0; pb < p1; pb += 4) {
+    const long p = pb + g;  // this lane group's pixel of the step
+    const bool pin = p < p1;
+    const long pc = pin ? p : p0;
+    const int xo = (int)(pc % Wo), yo = (int)((pc / Wo) % Ho), n = (int)(pc / ((long)Wo * Ho));
+    const float dyv = pin ? dy[pc * Co + co] : 0.f;
+    const float dzv = (pin && mask[pc * Co + co]) ? dyv : 0.f;
+#pragma unroll
+    for (int ky = 0; ky < kTK; ++ky) {
+      const int gy = S * yo + ky - pt;
+#pragma unroll
+      for (int kx = 0; kx < kTK; ++kx) {
+        const int gx = S * xo + kx - pl;
+        const bool ok = pin && gy >= 0 && gy < H && gx >= 0 && gx < W;
+        const float xv = ok ? x[(((long)n * H + gy) * W + gx) * Ci + ci] : 0.f;
+        acc[ky * kTK + kx] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv, dzv, acc[ky * kTK + kx], 0, 0, 0);
+      }
+    }
+    const float xs = pin ? x[(((long)n * H + S * yo) * W + S * xo) * Ci + ci] : 0.f;
+    acc[kTK * kTK] = __builtin_amdgcn_mfma_f32_16x16x4f32(xs, dyv, acc[kTK * kTK], 0, 0, 0);
+    if (it == 0) {  // (wave-uniform)
+      accb2 = __builtin_amdgcn_mfma_f32_16x16x4f32(1.f, dzv, accb2, 0, 0, 0);
+      accb1 = __builtin_amdgcn_mfma_f32_16x16x4f32(1.f, dyv, accb1, 0, 0, 0);
+    }
+  }
+  const long E2 = (long)kTK * kTK * Ci * Co, E1 = (long)Ci * Co, ET = E2 + Co + E1 + Co;
+  float* out = part + (long)chunk * ET;
+#pragma unroll
+  for (int t = 0; t < kTK * kTK; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[((long)t * Ci + 16 * it + 4 * g + j) * Co + co] = acc[t][j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) out[E2 + Co + (long)(16 * it + 4 * g + j) * Co + co] = acc[kTK * kTK][j];
+  if (it == 0 && g == 0) {  // every accumulator row of ones (x) dz is the column sum
+    out[E2 + co] = accb2[0];
+    out[E2 + Co + E1 + co] = accb1[0];
+  }
+}
+
+bool trans_mfma(int Ci, int Co) { return Ci % 16 == 0 && Co % 16 == 0; }
+
 int trans_chunks(int N, int Ho, int* rpc) {
   const long R = (long)N * Ho;
   const long chunks = std::max<long>(1, std::min<long>(R, kMaxTransChunks));
@@ -255,6 +443,12 @@ int trans_forward(const float* x, float* y, uint8_t* mask, const float* k2, cons
   const long tasks = (long)N * g.Ho * ((g.Wo + 15) / 16) * ((Co + 15) / 16);
   const long blocks = (tasks + 3) / 4;
   if (blocks > 0x7fffffffL) return fail(ASR_E_ARG, "transition: problem too large");
+  if (trans_mfma(Ci, Co)) {
+    hipLaunchKernelGGL(k_trans_fwd_mfma, dim3((unsigned)blocks), dim3(256), 0, s, x, y, mask, k2, b2, k1, b1, N, H,
+                       W, Ci, Co, S, g.Ho, g.Wo, g.pt, g.pl);
+    ASR_LAUNCH_CHECK("k_trans_fwd_mfma");
+    return ASR_OK;
+  }
   hipLaunchKernelGGL(k_trans_fwd, dim3((unsigned)blocks), dim3(256), 0, s, x, y, mask, k2, b2, k1, b1, N, H, W, Ci,
                      Co, S, g.Ho, g.Wo, g.pt, g.pl);
   ASR_LAUNCH_CHECK("k_trans_fwd");
@@ -270,6 +464,30 @@ size_t trans_ws_bytes(int N, int H, int W, int Ci, int Co, int S) {
 int trans_backward(const float* dy, const float* x, const uint8_t* mask, const float* k2, const float* k1, int N,
                    int H, int W, int Ci, int Co, int S, float* dx, float* dparams, float* part, hipStream_t s) {
   const TGeom g = tgeom(H, W, S);
+  if (trans_mfma(Ci, Co)) {
+    if (dx) {
+      const long blocks = ((long)N * H * ((W + 15) / 16) * (Ci / 16) + 3) / 4;
+      if (blocks > 0x7fffffffL) return fail(ASR_E_ARG, "transition: problem too large");
+      hipLaunchKernelGGL(k_trans_dgrad_mfma, dim3((unsigned)blocks), dim3(256), 0, s, dy, mask, k2, k1, dx, N, H, W,
+                         Ci, Co, S, g.Ho, g.Wo, g.pt, g.pl);
+      ASR_LAUNCH_CHECK("k_trans_dgrad_mfma");
+    }
+    if (dparams) {
+      int rpc = 0;
+      const int nch = trans_chunks(N, g.Ho, &rpc);  // the same chunk count as the VALU path (workspace)
+      const long P = (long)N * g.Ho * g.Wo;
+      const int ppc = (int)(((P + nch - 1) / nch + 3) / 4 * 4);
+      const int chunks = (int)((P + ppc - 1) / ppc);
+      const long ET = trans_param_floats(Ci, Co);
+      const long blocks = ((long)chunks * (Ci / 16) * (Co / 16) + 3) / 4;
+      hipLaunchKernelGGL(k_trans_wgrad_mfma, dim3((unsigned)blocks), dim3(256), 0, s, dy, mask, x, part, N, H, W, Ci,
+                         Co, S, g.Ho, g.Wo, g.pt, g.pl, ppc, chunks);
+      ASR_LAUNCH_CHECK("k_trans_wgrad_mfma");
+      hipLaunchKernelGGL(k_sum_chunks, dim3((unsigned)((ET + 255) / 256)), dim3(256), 0, s, part, chunks, ET, dparams);
+      ASR_LAUNCH_CHECK("k_sum_chunks");
+    }
+    return ASR_OK;
+  }
   if (dx) {
     const long total = (long)N * H * W * Ci;
     const unsigned grid = (unsigned)std::max<long>(1, std::min<long>((total + 255) / 256, 65536));
