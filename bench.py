@@ -523,10 +523,12 @@ def stages_main(args):
     """--config he32: one training step (fwd + bwd + Adam) of a multi-stage
     net on the asr_stages_* executor, same timing contract as main()."""
     import torch
-    from differential_equations_resnet_amd import distributed, runtime as rt
+    from differential_equations_resnet_amd import _lib, distributed, runtime as rt
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    if args.lib:
+        _lib.load(path=os.path.abspath(args.lib))
     dev = rt.require_gpu()
     distributed.init_from_env(device=dev)
     stages, N, desc = STAGE_CONFIGS[args.config]

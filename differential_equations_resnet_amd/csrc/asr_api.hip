@@ -85,6 +85,10 @@ int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, i
 int conv_f32_k(int fmode, int K, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
                float two_gamma, const float* dy, int N, int H, int W, int C, hipStream_t s, const float* extra);
 int wgrad_f32_chunks(int N, int H);
+bool conv32_fused_bwd_supported(int W, int C);
+int conv32_bwd_fused(const float* dy, const uint8_t* mask, float h, const float* x, const float* w, float two_gamma,
+                     const float* extra, bool skip_dy, int N, int H, int W, int C, float* dx, bool need_w,
+                     float* slabs, int* nslabs, hipStream_t s);
 // asr_stem_head.hip
 bool stem_supported(int Cin, int H, int W, int C);
 int stem_forward(const void* img, int input_u8, const float* w1, const float* b1, int N, int H, int W, int Cin, int C,
@@ -155,6 +159,9 @@ static int block_backward(int mode, const void* dy, const void* x, const uint8_t
   }
   if (accum_slabs) return fail(ASR_E_UNSUPPORTED, "slab accumulation: bf16 path only");
   const bool euler = mode == ASR_MODE_EULER;
+  if (euler && conv32_fused_bwd_supported(W, C))  // fp32 MFMA: dz formed while staging, no dz pass
+    return conv32_bwd_fused((const float*)dy, mask, h, (const float*)x, (const float*)w, 2.f * gamma,
+                            (const float*)extra, skip_dy, N, H, W, C, (float*)dx, need_w, slabs, nsl, s);
   ASR_TRY(make_dz(euler ? F_EULER : F_CONV, dy, mask, nullptr, h, N, H, W, C, 0, dz_scratch, s));
   if (dx)
     ASR_TRY(conv_f32((euler && !skip_dy) ? B_EULER : B_CONV, dz_scratch, dx, nullptr, (const float*)w, nullptr, h,
@@ -184,6 +191,16 @@ static int conv_backward_impl(int mode, const void* dy, const void* x, const uin
     ASR_TRY(reduce_and_project(slabs, nsl, 9L * C * C, C, dtheta ? theta_dst : nullptr, n_theta, dtheta, dbias,
                                dw_hwio, red, s));
   return ASR_OK;
+}
+
+// One layer's backward whose weight-gradient pass 2 + projection the caller
+// batches over its layers (project_layers): pass 1 of the slab reduction
+// writes reduce_groups(*nsl_out) group rows at grp (the multi-stage executor).
+int conv_backward_to_groups(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
+                            float gamma, int N, int H, int W, int C, int dtype, void* dx, void* ws, float* grp,
+                            int* nsl_out, hipStream_t s) {
+  return conv_backward_impl(mode, dy, x, mask, w, nullptr, 0, h, gamma, N, H, W, C, dtype, dx, nullptr, nullptr,
+                            nullptr, ws, s, grp, nsl_out);
 }
 
 // RK2 (explicit midpoint) block, BASELINE config 5 (an extension: the

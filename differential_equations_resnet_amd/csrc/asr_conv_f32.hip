@@ -189,19 +189,32 @@ struct F32Band {
   static_assert(W == 8 || W == 16 || W == 32, "fp32 MFMA band: W in {8, 16, 32}");
 };
 
+// dz = h dy [relu bit] of 4 channels (bit index pixel*C + c, C a multiple of 16: a nibble)
+__device__ __forceinline__ f32x4 masked_dz4(f32x4 v, const uint8_t* __restrict__ dmask, long bit, float dh) {
+  const unsigned nib = (unsigned)(dmask[bit >> 3] >> (bit & 7));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = ((nib >> j) & 1u) ? dh * v[j] : 0.f;
+  return v;
+}
+
 // stage rows y0-1 .. y0+BR of image n into tile (zeros outside the image and
-// in the two halo columns), float4 per thread
+// in the two halo columns), float4 per thread; with dmask, src is dy and the
+// tile gets dz = dh * dy * [relu bit] (the Euler block's dz, no separate pass)
 template <int C, int W>
 __device__ __forceinline__ void f32_stage_rows(const float* __restrict__ src, float* tile, int n, int y0, int H,
-                                               int tid, int nthreads) {
+                                               int tid, int nthreads, const uint8_t* __restrict__ dmask = nullptr,
+                                               float dh = 1.f) {
   using G = F32Band<C, W>;
   constexpr int C4 = C / 4, NCH = (G::BR + 2) * G::TW * C4;
   for (int i = tid; i < NCH; i += nthreads) {
     const int r = i / (G::TW * C4), rem = i % (G::TW * C4), col = rem / C4, c4 = rem % C4;
     const int gy = y0 - 1 + r, gx = col - 1;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)G::W)
-      v = *(const f32x4*)(src + (((long)n * H + gy) * G::W + gx) * C + 4 * c4);
+    if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)G::W) {
+      const long e = (((long)n * H + gy) * G::W + gx) * C + 4 * c4;
+      v = *(const f32x4*)(src + e);
+      if (dmask) v = masked_dz4(v, dmask, e, dh);
+    }
     *(f32x4*)(tile + (r * G::TW + col) * C + 4 * c4) = v;
   }
 }
@@ -211,7 +224,7 @@ __global__ __launch_bounds__(256) void k_conv32(const float* __restrict__ xin, f
                                                 uint8_t* __restrict__ mask, const float* __restrict__ w,
                                                 const float* __restrict__ bias, float h, float two_gamma,
                                                 const float* __restrict__ dy, const float* __restrict__ extra, int N,
-                                                int H) {
+                                                int H, const uint8_t* __restrict__ dmask) {
   using G = F32Band<C, W>;
   constexpr int OT = G::OT, TW = G::TW, BR = G::BR;
   __shared__ __attribute__((aligned(16))) float tile[G::TILEF];
@@ -230,7 +243,8 @@ __global__ __launch_bounds__(256) void k_conv32(const float* __restrict__ xin, f
       for (int s = 0; s < 4; ++s) A[t][q][s] = w[((long)t * C + 16 * q + 4 * g + s) * C + 16 * ot + lx];
   f32x4 bz = {0.f, 0.f, 0.f, 0.f};
   if (MODE <= F_RELU && bias) bz = *(const f32x4*)(bias + 16 * ot + 4 * g);
-  f32_stage_rows<C, W>(xin, tile, n, y0, H, tid, 256);
+  // (backward with dmask: xin is dy, the tile gets dz = h dy [relu bit])
+  f32_stage_rows<C, W>(xin, tile, n, y0, H, tid, 256, MODE >= B_EULER ? dmask : nullptr, h);
   __syncthreads();
   // wave (ot, rw) takes the band's 16-pixel tiles rw, rw + WPT, ..; lane lx's pixel of tile tau is band
   // pixel 16 tau + lx (W = 8: a tile spans two rows, so validity is per lane)
@@ -289,7 +303,8 @@ __global__ __launch_bounds__(256) void k_conv32(const float* __restrict__ xin, f
 
 template <int C, int W>
 __global__ __launch_bounds__(768) void k_wgrad32(const float* __restrict__ x, const float* __restrict__ dz, int N,
-                                                 int H, float* __restrict__ slabs) {
+                                                 int H, float* __restrict__ slabs, const uint8_t* __restrict__ dmask,
+                                                 float dh) {
   using G = F32Band<C, W>;
   constexpr int OT = G::OT, TW = G::TW, BR = G::BR, RS = G::RS, E = 9 * C * C;
   extern __shared__ __attribute__((aligned(16))) float lds32[];
@@ -313,7 +328,11 @@ __global__ __launch_bounds__(768) void k_wgrad32(const float* __restrict__ x, co
     for (int i = tid; i < BR * G::W * C / 4; i += 768) {
       const int r = i / (G::W * C / 4);
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (r < rows) v = *(const f32x4*)(dz + ((long)n * H + y0) * G::W * C + 4 * i);
+      if (r < rows) {
+        const long e = ((long)n * H + y0) * G::W * C + 4 * i;
+        v = *(const f32x4*)(dz + e);
+        if (dmask) v = masked_dz4(v, dmask, e, dh);  // dz is dy here: dz = dh dy [relu bit]
+      }
       *(f32x4*)(dzt + 4 * i) = v;
     }
     __syncthreads();
@@ -387,11 +406,12 @@ static bool conv32_supported(int W, int Ci, int Co) {
 
 template <int C, int W, int MODE>
 static int launch_conv32(const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
-                         float two_gamma, const float* dy, const float* extra, int N, int H, hipStream_t s) {
+                         float two_gamma, const float* dy, const float* extra, int N, int H, hipStream_t s,
+                         const uint8_t* dmask = nullptr) {
   const long blocks = (long)N * ((H + 3) / 4);
   if (blocks > 0x7fffffffL) return fail(ASR_E_ARG, "conv f32: problem too large");
   hipLaunchKernelGGL((k_conv32<C, W, MODE>), dim3((unsigned)blocks), dim3(256), 0, s, (const float*)xin,
-                     (float*)out, mask, w, bias, h, two_gamma, dy, extra, N, H);
+                     (float*)out, mask, w, bias, h, two_gamma, dy, extra, N, H, dmask);
   ASR_LAUNCH_CHECK("k_conv32");
   return ASR_OK;
 }
@@ -399,35 +419,37 @@ static int launch_conv32(const void* xin, void* out, uint8_t* mask, const float*
 template <int C, int MODE>
 static int conv32_dispatch_w(int W, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias,
                              float h, float two_gamma, const float* dy, const float* extra, int N, int H,
-                             hipStream_t s) {
+                             hipStream_t s, const uint8_t* dmask) {
   switch (W) {
-    case 32: return launch_conv32<C, 32, MODE>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
-    case 16: return launch_conv32<C, 16, MODE>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
-    case 8: return launch_conv32<C, 8, MODE>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+    case 32: return launch_conv32<C, 32, MODE>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s, dmask);
+    case 16: return launch_conv32<C, 16, MODE>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s, dmask);
+    case 8: return launch_conv32<C, 8, MODE>(xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s, dmask);
   }
   return fail(ASR_E_UNSUPPORTED, "conv f32 (MFMA): W=%d", W);
 }
 
 template <int MODE>
 static int conv32_dispatch(int C, int W, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias,
-                           float h, float two_gamma, const float* dy, const float* extra, int N, int H, hipStream_t s) {
+                           float h, float two_gamma, const float* dy, const float* extra, int N, int H, hipStream_t s,
+                           const uint8_t* dmask = nullptr) {
   switch (C) {
-    case 16: return conv32_dispatch_w<16, MODE>(W, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
-    case 32: return conv32_dispatch_w<32, MODE>(W, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
-    case 64: return conv32_dispatch_w<64, MODE>(W, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s);
+    case 16: return conv32_dispatch_w<16, MODE>(W, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s, dmask);
+    case 32: return conv32_dispatch_w<32, MODE>(W, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s, dmask);
+    case 64: return conv32_dispatch_w<64, MODE>(W, xin, out, mask, w, bias, h, two_gamma, dy, extra, N, H, s, dmask);
   }
   return fail(ASR_E_UNSUPPORTED, "conv f32 (MFMA): C=%d", C);
 }
 
 template <int C, int W>
-static int launch_wgrad32(const float* x, const float* dz, int N, int H, float* slabs, int* nslabs, hipStream_t s) {
+static int launch_wgrad32(const float* x, const float* dz, int N, int H, float* slabs, int* nslabs, hipStream_t s,
+                          const uint8_t* dmask = nullptr, float dh = 1.f) {
   const long items = (long)N * ((H + 3) / 4);
   int cus = cu_count();
   if (cus <= 0) cus = 256;
   const size_t lds = wgrad32_lds<C, W>();
   const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
   const int grid = (int)std::max<long>(1, std::min<long>({items, (long)per_cu * cus, 512L}));
-  hipLaunchKernelGGL((k_wgrad32<C, W>), dim3(grid), dim3(768), lds, s, x, dz, N, H, slabs);
+  hipLaunchKernelGGL((k_wgrad32<C, W>), dim3(grid), dim3(768), lds, s, x, dz, N, H, slabs, dmask, dh);
   ASR_LAUNCH_CHECK("k_wgrad32");
   *nslabs = grid;
   return ASR_OK;
@@ -508,6 +530,41 @@ int make_dz(int fmode, const void* dy, const uint8_t* mask, const void* relu_src
                        (const float*)relu_src, fmode, h, N, H, W, C, dz);
   ASR_LAUNCH_CHECK("k_make_dz");
   return ASR_OK;
+}
+
+// The fp32 Euler block's backward on the matrix cores without the dz pass:
+// dgrad (B_EULER, or B_CONV when skip_dy: the second RK2 stage) and the weight
+// gradient stage dz = h dy [relu bit] straight from dy and the mask.  Only for
+// conv32_supported shapes (else ASR_E_UNSUPPORTED: the caller runs make_dz +
+// conv_f32 + wgrad_f32).
+bool conv32_fused_bwd_supported(int W, int C) { return conv32_supported(W, C, C); }
+
+int conv32_bwd_fused(const float* dy, const uint8_t* mask, float h, const float* x, const float* w, float two_gamma,
+                     const float* extra, bool skip_dy, int N, int H, int W, int C, float* dx, bool need_w,
+                     float* slabs, int* nslabs, hipStream_t s) {
+  if (!conv32_supported(W, C, C)) return fail(ASR_E_UNSUPPORTED, "conv f32 fused backward: C=%d W=%d", C, W);
+  *nslabs = 0;
+  if (dx) {
+    if (skip_dy)
+      ASR_TRY(conv32_dispatch<B_CONV>(C, W, dy, dx, nullptr, w, nullptr, h, two_gamma, nullptr, extra, N, H, s, mask));
+    else
+      ASR_TRY(conv32_dispatch<B_EULER>(C, W, dy, dx, nullptr, w, nullptr, h, two_gamma, dy, extra, N, H, s, mask));
+  }
+  if (!need_w) return ASR_OK;
+#define ASR_WG32F(CC)                                                                         \
+  switch (W) {                                                                                \
+    case 32: return launch_wgrad32<CC, 32>(x, dy, N, H, slabs, nslabs, s, mask, h);           \
+    case 16: return launch_wgrad32<CC, 16>(x, dy, N, H, slabs, nslabs, s, mask, h);           \
+    case 8: return launch_wgrad32<CC, 8>(x, dy, N, H, slabs, nslabs, s, mask, h);             \
+  }                                                                                           \
+  break
+  switch (C) {
+    case 16: ASR_WG32F(16);
+    case 32: ASR_WG32F(32);
+    case 64: ASR_WG32F(64);
+  }
+#undef ASR_WG32F
+  return fail(ASR_E_UNSUPPORTED, "conv f32 fused backward: C=%d W=%d", C, W);
 }
 
 // number of row chunks used by the fp32 wgrad (bounded by kMaxSlabs in the

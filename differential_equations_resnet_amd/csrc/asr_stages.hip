@@ -40,6 +40,13 @@ int param_map_transpose(int C, const int32_t* w_src, int32_t* w_bwd);
 int reduce_and_project(const float* slabs, int P, long E, int Cb, const int32_t* theta_dst, long n_theta,
                        float* dtheta, float* dbias, float* dw_out, float* ws, hipStream_t s);
 size_t reduce_ws_bytes(int P, long ES);
+int reduce_groups(int P);
+int project_layers(float* grp, long grp_stride, int G, long E, int Cb, const int32_t* theta_dst, long n_theta,
+                   int L, float* out, long out_stride, hipStream_t s);
+// asr_api.hip
+int conv_backward_to_groups(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
+                            float gamma, int N, int H, int W, int C, int dtype, void* dx, void* ws, float* grp,
+                            int* nsl_out, hipStream_t s);
 // asr_stem_head.hip
 bool stem_supported(int Cin, int H, int W, int C);
 int stem_forward(const void* img, int input_u8, const float* w1, const float* b1, int N, int H, int W, int Cin, int C,
@@ -57,6 +64,7 @@ namespace {
 constexpr int kTK = 3;              // the transition's kxk (the builder's kernel_size; 3 in every reference config)
 constexpr int kMaxTransChunks = 256;  // wgrad row chunks
 constexpr int kMaxStemSlabs = 512;    // asr_stem_head.hip stem_grid bound
+constexpr int kMaxBlockSlabs = 512;   // asr_api.hip kMaxSlabsApi: slab rows of one block's fp32 weight gradient
 
 struct TGeom {
   int Ho, Wo, pt, pl;
@@ -228,13 +236,27 @@ __global__ __launch_bounds__(256) void k_trans_wgrad(const float* __restrict__ d
   part[(long)blockIdx.y * ET + e] = acc;
 }
 
+// out[e] = sum_c part[c][e]: a workgroup = 64 elements x 4 chunk slices, 4 independent
+// partial sums per thread (loads in flight), the slices combined through LDS in a fixed order
 __global__ __launch_bounds__(256) void k_sum_chunks(const float* __restrict__ part, int chunks, long E,
                                                     float* __restrict__ out) {
-  const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  if (e >= E) return;
-  float acc = 0.f;
-  for (int c = 0; c < chunks; ++c) acc += part[(long)c * E + e];
-  out[e] = acc;
+  __shared__ float red[4][64];
+  const int lx = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const long e = blockIdx.x * 64L + lx;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (e < E) {
+    int c = sl;
+    for (; c + 12 < chunks; c += 16) {
+      a0 += part[(long)c * E + e];
+      a1 += part[(long)(c + 4) * E + e];
+      a2 += part[(long)(c + 8) * E + e];
+      a3 += part[(long)(c + 12) * E + e];
+    }
+    for (; c < chunks; c += 4) a0 += part[(long)c * E + e];
+  }
+  red[sl][lx] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (sl == 0 && e < E) out[e] = (red[0][lx] + red[1][lx]) + (red[2][lx] + red[3][lx]);
 }
 
 // ---------------------------------------------------------------------------
@@ -483,7 +505,7 @@ int trans_backward(const float* dy, const float* x, const uint8_t* mask, const f
       hipLaunchKernelGGL(k_trans_wgrad_mfma, dim3((unsigned)blocks), dim3(256), 0, s, dy, mask, x, part, N, H, W, Ci,
                          Co, S, g.Ho, g.Wo, g.pt, g.pl, ppc, chunks);
       ASR_LAUNCH_CHECK("k_trans_wgrad_mfma");
-      hipLaunchKernelGGL(k_sum_chunks, dim3((unsigned)((ET + 255) / 256)), dim3(256), 0, s, part, chunks, ET, dparams);
+      hipLaunchKernelGGL(k_sum_chunks, dim3((unsigned)((ET + 63) / 64)), dim3(256), 0, s, part, chunks, ET, dparams);
       ASR_LAUNCH_CHECK("k_sum_chunks");
     }
     return ASR_OK;
@@ -502,7 +524,7 @@ int trans_backward(const float* dy, const float* x, const uint8_t* mask, const f
     hipLaunchKernelGGL(k_trans_wgrad, dim3((unsigned)((ET + 255) / 256), nch), dim3(256), 0, s, dy, mask, x, part, N,
                        H, W, Ci, Co, S, g.Ho, g.Wo, g.pt, g.pl, rpc);
     ASR_LAUNCH_CHECK("k_trans_wgrad");
-    hipLaunchKernelGGL(k_sum_chunks, dim3((unsigned)((ET + 255) / 256)), dim3(256), 0, s, part, nch, ET, dparams);
+    hipLaunchKernelGGL(k_sum_chunks, dim3((unsigned)((ET + 63) / 64)), dim3(256), 0, s, part, nch, ET, dparams);
     ASR_LAUNCH_CHECK("k_sum_chunks");
   }
   return ASR_OK;
@@ -515,7 +537,8 @@ struct StageL {
   int C, L, H, W, S, Cp, Hp, Wp;  // S = 0: no transition; Cp/Hp/Wp the stage input's shape
   long P, ntheta, E, blk_stride, mask_bytes;
   long off_t, off_blk;          // parameter offsets (floats)
-  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, act_t, mask_t, acts, masks;  // workspace offsets
+  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, act_t, mask_t, acts, masks, grp;  // workspace offsets
+  long grp_stride;  // floats per block of pass-1 group rows
 };
 struct SLayout {
   int ns;
@@ -612,6 +635,8 @@ SLayout stages_layout(const asr_stages_config* c) {
     g.mask_t = g.S ? take((size_t)g.P) : 0;
     g.acts = take((size_t)std::max(g.L, 1) * g.P * 4);
     g.masks = take((size_t)std::max(g.L, 1) * g.mask_bytes);
+    g.grp_stride = (long)reduce_groups(kMaxBlockSlabs) * (g.E + g.C);
+    g.grp = take((size_t)std::max(g.L, 1) * g.grp_stride * 4);
     if (g.L > 0) L.cws_bytes = std::max(L.cws_bytes, asr_conv_backward_workspace_bytes(c->N, g.H, g.W, g.C, ASR_F32));
     if (g.S) L.tws_bytes = std::max(L.tws_bytes, trans_ws_bytes(c->N, g.Hp, g.Wp, g.Cp, g.C, g.S));
   }
@@ -773,15 +798,20 @@ int asr_stages_forward_backward(const asr_stages_config* cfg, const float* param
     }
     const float* chain_in = g.S ? (const float*)(b + g.act_t) : prev_out;
     const float gam = L.sep_bwd ? 0.f : cfg->gamma;
+    int nsl = 0;
     for (int l = g.L - 1; l >= 0; --l) {
       const float* x_in = l == 0 ? chain_in : (const float*)(b + g.acts) + (size_t)(l - 1) * g.P;
       const unsigned char* wl = b + (L.sep_bwd ? g.wbuf_bwd : g.wbuf) + (size_t)l * g.E * 4;
-      float* gp = grads + g.off_blk + (long)l * g.blk_stride;
-      ASR_TRY(asr_conv_backward(ASR_MODE_EULER, d, x_in, (const uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes, wl,
-                                (const int32_t*)(b + g.theta_dst), g.ntheta, cfg->h, gam, N, g.H, g.W, g.C, ASR_F32, e,
-                                gp, gp + g.ntheta, nullptr, b + L.cws, L.cws_bytes, s));
+      // pass 1 of the block's slab reduction into its group rows; pass 2 + projection once per stage
+      ASR_TRY(conv_backward_to_groups(ASR_MODE_EULER, d, x_in, (const uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes,
+                                      wl, cfg->h, gam, N, g.H, g.W, g.C, ASR_F32, e, b + L.cws,
+                                      (float*)(b + g.grp) + (size_t)l * g.grp_stride, &nsl, s));
+      if (nsl > kMaxBlockSlabs) return fail(ASR_E_UNSUPPORTED, "asr_stages: %d slab rows > %d", nsl, kMaxBlockSlabs);
       std::swap(d, e);
     }
+    if (g.L > 0)
+      ASR_TRY(project_layers((float*)(b + g.grp), g.grp_stride, reduce_groups(nsl), g.E, g.C,
+                             (const int32_t*)(b + g.theta_dst), g.ntheta, g.L, grads + g.off_blk, g.blk_stride, s));
     if (g.S) {
       const float* pt = params + g.off_t;
       const long e2 = 9L * g.Cp * g.C;
