@@ -16,7 +16,7 @@ cat gpurun_out/bench_$TAG.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 20 --warmup 5 > gpurun_out/prof_$TAG.log 2>&1 || { echo PROF FAILED; tail -20 gpurun_out/prof_$TAG.log; exit 1; }
 python3 tools/kstats.py gpurun_out/prof_$TAG/run_kernel_stats.csv 14
 python3 tools/step_breakdown.py gpurun_out/prof_$TAG/run_kernel_trace.csv > gpurun_out/prof_$TAG/step_breakdown.txt && cat gpurun_out/prof_$TAG/step_breakdown.txt
-for cfg in c2_eval c5 c3 c1 c2_f32 v6 v7_predict; do
+for cfg in c2_eval c5 c3 c1 c2_f32 v6 v7_predict he32; do
   timeout -k 10 600 python3 bench.py --config $cfg --no-cpu-baseline > gpurun_out/bench_${TAG}_$cfg.json 2> gpurun_out/bench_${TAG}_$cfg.err || { echo "BENCH $cfg FAILED"; tail -5 gpurun_out/bench_${TAG}_$cfg.err; exit 1; }
   python3 -c "import json; d=json.load(open('gpurun_out/bench_${TAG}_$cfg.json')); r=d['roofline']; print('$cfg', d['value'], d['ms_per_step'], r['frac'], {k: v.get('avg_us') for k, v in r.get('kernels', {}).items()})"
 done
