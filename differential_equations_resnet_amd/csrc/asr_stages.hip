@@ -404,6 +404,7 @@ __global__ __launch_bounds__(256) void k_trans_wgrad_mfma(const float* __restric
 #pragma unroll
   for (int t = 0; t <= kTK * kTK; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int ci = 16 * it + lx, co = 16 * ot + lx;  // A row (input channel), B column (output channel)
+#pragma unroll 2
   for (long pb = p0; pb < p1; pb += 4) {
     const long p = pb + g;  // this lane group's pixel of the step
     const bool pin = p < p1;
@@ -445,6 +446,15 @@ __global__ __launch_bounds__(256) void k_trans_wgrad_mfma(const float* __restric
 
 bool trans_mfma(int Ci, int Co) { return Ci % 16 == 0 && Co % 16 == 0; }
 
+// MFMA weight gradient: chunks of ppc output pixels (a multiple of 4) such that about 2048 waves
+// run, each over few pixel steps (the steps are gather-latency bound)
+int trans_mfma_chunks(int N, int Ho, int Wo, int Ci, int Co, int* ppc) {
+  const long P = (long)N * Ho * Wo;
+  const long target = std::max(1, 2048 / ((Ci / 16) * (Co / 16)));
+  *ppc = (int)std::max<long>(16, ((P + target - 1) / target + 3) / 4 * 4);
+  return (int)((P + *ppc - 1) / *ppc);
+}
+
 int trans_chunks(int N, int Ho, int* rpc) {
   const long R = (long)N * Ho;
   const long chunks = std::max<long>(1, std::min<long>(R, kMaxTransChunks));
@@ -478,8 +488,9 @@ int trans_forward(const float* x, float* y, uint8_t* mask, const float* k2, cons
 }
 
 size_t trans_ws_bytes(int N, int H, int W, int Ci, int Co, int S) {
+  const TGeom g = tgeom(H, W, S);
   int rpc = 0;
-  const int nch = trans_chunks(N, tgeom(H, W, S).Ho, &rpc);
+  const int nch = trans_mfma(Ci, Co) ? trans_mfma_chunks(N, g.Ho, g.Wo, Ci, Co, &rpc) : trans_chunks(N, g.Ho, &rpc);
   return align_up((size_t)nch * trans_param_floats(Ci, Co) * 4, 256);
 }
 
@@ -495,11 +506,8 @@ int trans_backward(const float* dy, const float* x, const uint8_t* mask, const f
       ASR_LAUNCH_CHECK("k_trans_dgrad_mfma");
     }
     if (dparams) {
-      int rpc = 0;
-      const int nch = trans_chunks(N, g.Ho, &rpc);  // the same chunk count as the VALU path (workspace)
-      const long P = (long)N * g.Ho * g.Wo;
-      const int ppc = (int)(((P + nch - 1) / nch + 3) / 4 * 4);
-      const int chunks = (int)((P + ppc - 1) / ppc);
+      int ppc = 0;
+      const int chunks = trans_mfma_chunks(N, g.Ho, g.Wo, Ci, Co, &ppc);
       const long ET = trans_param_floats(Ci, Co);
       const long blocks = ((long)chunks * (Ci / 16) * (Co / 16) + 3) / 4;
       hipLaunchKernelGGL(k_trans_wgrad_mfma, dim3((unsigned)blocks), dim3(256), 0, s, dy, mask, x, part, N, H, W, Ci,
