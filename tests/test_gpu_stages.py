@@ -140,3 +140,38 @@ def test_resnet32_he_model_lowers_and_matches_oracle():
     pr = nv.predict(imgs)
     p2, _ = O.stages_forward(spec, got, imgs)
     assert_close(pr, p2, rtol=1e-5, atol=1e-6, what="predict after adam")
+
+
+def test_training_multistage_overfits_one_batch(tmp_path):
+    """The reference's Training loop over a multi-stage net (default dtype:
+    the multi-stage executor computes in fp32): gradient mean-norm CSV rows
+    include the transition-free identity blocks of every stage, and the loss
+    of a learnable batch falls."""
+    import csv
+    from differential_equations_resnet_amd import graph
+    from differential_equations_resnet_amd.dataset_utils import ArrayDataset
+    from differential_equations_resnet_amd.models import tfkeras_resnets as R
+    from differential_equations_resnet_amd.training import AdamOptimizer, Training
+    rng = np.random.default_rng(2)
+    labels = rng.integers(0, 4, 32)  # learnable: the class sets the image brightness
+    feats = np.clip(labels[:, None, None, None] * 60 + 20 + rng.integers(-15, 16, (32, 32, 32, 3)), 0,
+                    255).astype(np.uint8)
+    ds = ArrayDataset(feats, labels, 32, shuffle=False, num_classes=10)
+    graph.set_seed(0)
+    build = R.get_single_block_resnet_build_function(h=0.25, num_stages=4, blocks_per_stage=[2, 2, 2],
+                                                     filters_per_block=[16, 32, 64],
+                                                     strides=[(1, 1), (2, 2), (2, 2)], subtract_mean=127.5,
+                                                     divide_by_stddev=127.5, num_classes=10)
+    tr = Training(build, "antisymmetric", AdamOptimizer(epsilon=1e-7), train_dataset=ds,
+                  summaries_dir=str(tmp_path), summaries_name="run", csv_logger_dir=str(tmp_path),
+                  csv_logger_name="gradient_history")
+    first = tr.evaluate("train", 1)["mean_loss"]
+    norms = tr.train_step(3e-3, with_norms=True)
+    assert len(norms) == 1 + 4  # conv1 + the 4 identity blocks (2 + 1 + 1)
+    for _ in range(60):
+        tr.train_step(3e-3)
+    last = tr.evaluate("train", 1)["mean_loss"]
+    assert last < 0.5 * first, (first, last)
+    tr.train(epochs=1, steps_per_epoch=2, learning_rate_schedule=lambda s: 1e-3, summaries_frequency=1)
+    rows = list(csv.reader(open(tmp_path / "run_gradient_history.csv"), delimiter=" "))
+    assert rows[0][3] == "conv1_kernel_gradient_mean_norm" and "res4_1_branch2_kernel_gradient_mean_norm" in rows[0]
