@@ -23,6 +23,8 @@ int reduce_and_project(const float* slabs, int P, long E, int Cb, const int32_t*
 size_t reduce_ws_bytes(int P, long ES);
 int reduce_groups(int P);
 int reduce_slabs_to_groups(const float* slabs, int P, long ES, float* grp, hipStream_t s);
+int reduce_slab_layers(const float* slabs, long slab_stride, int P, long ES, float* grp, long grp_stride, int L,
+                       hipStream_t s);
 int project_layers(float* grp, long grp_stride, int G, long E, int Cb, const int32_t* theta_dst, long n_theta,
                    int L, float* out, long out_stride, hipStream_t s);
 // asr_block_mfma.hip
@@ -193,14 +195,13 @@ static int conv_backward_impl(int mode, const void* dy, const void* x, const uin
   return ASR_OK;
 }
 
-// One layer's backward whose weight-gradient pass 2 + projection the caller
-// batches over its layers (project_layers): pass 1 of the slab reduction
-// writes reduce_groups(*nsl_out) group rows at grp (the multi-stage executor).
-int conv_backward_to_groups(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
-                            float gamma, int N, int H, int W, int C, int dtype, void* dx, void* ws, float* grp,
-                            int* nsl_out, hipStream_t s) {
-  return conv_backward_impl(mode, dy, x, mask, w, nullptr, 0, h, gamma, N, H, W, C, dtype, dx, nullptr, nullptr,
-                            nullptr, ws, s, grp, nsl_out);
+// One fp32 Euler block's backward that leaves its weight-gradient slabs (*nsl rows of 9C^2 + C
+// floats) at `slabs` for the caller to reduce together with other blocks' (reduce_slab_layers).
+int conv_backward_keep_slabs(const void* dy, const void* x, const uint8_t* mask, const void* w, float h, float gamma,
+                             int N, int H, int W, int C, void* dx, void* ws, float* slabs, int* nsl, hipStream_t s) {
+  const BwdWs L = bwd_ws_layout(N, H, W, C, ASR_F32);
+  return block_backward(ASR_MODE_EULER, dy, x, mask, w, h, gamma, N, H, W, C, ASR_F32, dx, true, nullptr, false, slabs,
+                        (float*)((unsigned char*)ws + L.dz), nsl, s);
 }
 
 // RK2 (explicit midpoint) block, BASELINE config 5 (an extension: the
@@ -344,6 +345,8 @@ struct NetLayout {
   int stages;    // conv applications per block (1 Euler, 2 RK2)
   long grp_stride;  // floats of slab group sums per layer
   size_t grp;  // per-layer slab group sums, projected after the whole backward
+  size_t slabs_all;  // fp32: every block's slabs, pass 1 of all blocks in one launch after the loop
+  long slab_stride;
   size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, x0, acts, xmids, masks, dxa, dxb, dxg, bwdws, slabs2, slabs, red, probs,
       loss_per, dlogits, gap, total;
   long mask_bytes;
@@ -436,6 +439,8 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.slabs2 = take(tr ? (size_t)L.stages * kMaxSlabsApi * (L.E + C) * 4 : 0);  // every other block's slabs
   L.grp_stride = (long)reduce_groups(L.stages * kMaxSlabsApi) * (L.E + C);
   L.grp = take(tr ? (size_t)c->L * L.grp_stride * 4 : 0);
+  L.slab_stride = (long)L.stages * kMaxSlabsApi * (L.E + C);
+  L.slabs_all = take(tr && c->dtype == ASR_F32 ? (size_t)c->L * L.slab_stride * 4 : 0);
   L.deep_slabs = take(L.deep && tr ? deep16_slab_bytes(c->N, c->L) : 0);
   L.theta_dst_tm = take(L.stack_bwd ? (size_t)L.ntheta * 2 * 4 : 0);
   L.theta_dst_pr = take(L.stack_pair ? (size_t)L.ntheta * 2 * 4 : 0);
@@ -1110,7 +1115,9 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
     // (deeper) block's reduction rides in this block's (second-stage) kernel
     // when it can (else it runs here), and this block's waits for the next
     // block (or the end of the loop)
-    float* slabs_l = (float*)(b + ((l & 1) ? L.slabs2 : L.bwdws + bw.slabs));
+    // (fp32: every block keeps its own slabs; one launch reduces them all after the loop)
+    float* slabs_l = !bf ? (float*)(b + L.slabs_all) + (size_t)l * L.slab_stride
+                         : (float*)(b + ((l & 1) ? L.slabs2 : L.bwdws + bw.slabs));
     int nsl = 0, folded = 0;
     if (L.rk2) {
       const unsigned char* xm = b + L.xmids + (size_t)l * L.P * L.act_bytes;
@@ -1123,14 +1130,18 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
                              l == 0 && L.fast_stem && bf && !stem_v1, l == 0 ? &dz1_fused : nullptr,
                              fold_on ? pend_slabs : nullptr, fold_on ? pend_P : 0, pend_grp, &folded));
     }
+    nsl_blk = nsl;
+    std::swap(dcur, dnext);
+    if (!bf) continue;
     if (pend_P > 0 && !folded) ASR_TRY(reduce_slabs_to_groups(pend_slabs, pend_P, L.E + C, pend_grp, s));
     pend_slabs = slabs_l;
     pend_P = nsl;
     pend_grp = grp_l;
-    nsl_blk = nsl;
-    std::swap(dcur, dnext);
   }
   if (pend_P > 0) ASR_TRY(reduce_slabs_to_groups(pend_slabs, pend_P, L.E + C, pend_grp, s));
+  if (!bf && !L.deep && !stacked && nsl_blk > 0)  // (every block of a network has the same slab count)
+    ASR_TRY(reduce_slab_layers((const float*)(b + L.slabs_all), L.slab_stride, nsl_blk, L.E + C,
+                               (float*)(b + L.grp), L.grp_stride, cfg->L, s));
   // pass 2 of every block's weight-gradient reduction + projection onto theta, one launch
   if (!L.deep && !stacked) {
     ASR_TRY(timed_event(cfg, 3, s));  // (per-block kernels: their slab passes ride inside)

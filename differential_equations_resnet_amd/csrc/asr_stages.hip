@@ -43,10 +43,11 @@ size_t reduce_ws_bytes(int P, long ES);
 int reduce_groups(int P);
 int project_layers(float* grp, long grp_stride, int G, long E, int Cb, const int32_t* theta_dst, long n_theta,
                    int L, float* out, long out_stride, hipStream_t s);
+int reduce_slab_layers(const float* slabs, long slab_stride, int P, long ES, float* grp, long grp_stride, int L,
+                       hipStream_t s);
 // asr_api.hip
-int conv_backward_to_groups(int mode, const void* dy, const void* x, const uint8_t* mask, const void* w, float h,
-                            float gamma, int N, int H, int W, int C, int dtype, void* dx, void* ws, float* grp,
-                            int* nsl_out, hipStream_t s);
+int conv_backward_keep_slabs(const void* dy, const void* x, const uint8_t* mask, const void* w, float h, float gamma,
+                             int N, int H, int W, int C, void* dx, void* ws, float* slabs, int* nsl, hipStream_t s);
 // asr_stem_head.hip
 bool stem_supported(int Cin, int H, int W, int C);
 int stem_forward(const void* img, int input_u8, const float* w1, const float* b1, int N, int H, int W, int Cin, int C,
@@ -545,8 +546,9 @@ struct StageL {
   int C, L, H, W, S, Cp, Hp, Wp;  // S = 0: no transition; Cp/Hp/Wp the stage input's shape
   long P, ntheta, E, blk_stride, mask_bytes;
   long off_t, off_blk;          // parameter offsets (floats)
-  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, act_t, mask_t, acts, masks, grp;  // workspace offsets
-  long grp_stride;  // floats per block of pass-1 group rows
+  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, act_t, mask_t, acts, masks, grp, slabs;  // workspace offsets
+  long grp_stride;   // floats per block of pass-1 group rows
+  long slab_stride;  // floats per block of weight-gradient slabs
 };
 struct SLayout {
   int ns;
@@ -645,6 +647,8 @@ SLayout stages_layout(const asr_stages_config* c) {
     g.masks = take((size_t)std::max(g.L, 1) * g.mask_bytes);
     g.grp_stride = (long)reduce_groups(kMaxBlockSlabs) * (g.E + g.C);
     g.grp = take((size_t)std::max(g.L, 1) * g.grp_stride * 4);
+    g.slab_stride = (long)kMaxBlockSlabs * (g.E + g.C);
+    g.slabs = take((size_t)g.L * g.slab_stride * 4);
     if (g.L > 0) L.cws_bytes = std::max(L.cws_bytes, asr_conv_backward_workspace_bytes(c->N, g.H, g.W, g.C, ASR_F32));
     if (g.S) L.tws_bytes = std::max(L.tws_bytes, trans_ws_bytes(c->N, g.Hp, g.Wp, g.Cp, g.C, g.S));
   }
@@ -810,13 +814,17 @@ int asr_stages_forward_backward(const asr_stages_config* cfg, const float* param
     for (int l = g.L - 1; l >= 0; --l) {
       const float* x_in = l == 0 ? chain_in : (const float*)(b + g.acts) + (size_t)(l - 1) * g.P;
       const unsigned char* wl = b + (L.sep_bwd ? g.wbuf_bwd : g.wbuf) + (size_t)l * g.E * 4;
-      // pass 1 of the block's slab reduction into its group rows; pass 2 + projection once per stage
-      ASR_TRY(conv_backward_to_groups(ASR_MODE_EULER, d, x_in, (const uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes,
-                                      wl, cfg->h, gam, N, g.H, g.W, g.C, ASR_F32, e, b + L.cws,
-                                      (float*)(b + g.grp) + (size_t)l * g.grp_stride, &nsl, s));
+      // the block's weight-gradient slabs stay in its own slot: the stage's blocks are reduced
+      // (pass 1, one launch) and projected (pass 2 + projection, one launch) after the loop
+      ASR_TRY(conv_backward_keep_slabs(d, x_in, (const uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes, wl, cfg->h, gam,
+                                       N, g.H, g.W, g.C, e, b + L.cws, (float*)(b + g.slabs) + (size_t)l * g.slab_stride,
+                                       &nsl, s));
       if (nsl > kMaxBlockSlabs) return fail(ASR_E_UNSUPPORTED, "asr_stages: %d slab rows > %d", nsl, kMaxBlockSlabs);
       std::swap(d, e);
     }
+    if (g.L > 0)
+      ASR_TRY(reduce_slab_layers((const float*)(b + g.slabs), g.slab_stride, nsl, g.E + g.C, (float*)(b + g.grp),
+                                 g.grp_stride, g.L, s));
     if (g.L > 0)
       ASR_TRY(project_layers((float*)(b + g.grp), g.grp_stride, reduce_groups(nsl), g.E, g.C,
                              (const int32_t*)(b + g.theta_dst), g.ntheta, g.L, grads + g.off_blk, g.blk_stride, s));

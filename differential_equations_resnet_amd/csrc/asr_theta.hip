@@ -419,6 +419,36 @@ size_t reduce_ws_bytes(int P, long ES) { return (size_t)((P + 31) / 32 + 1) * ES
 
 int reduce_groups(int P) { return (P + 31) / 32; }
 
+// Pass 1 for L layers in one launch: layer z's P slab rows at slabs + z*slab_stride -> its
+// reduce_groups(P) group rows at grp + z*grp_stride (the fp32 network's per-block slabs)
+__global__ void k_reduce_slabs_layers(const float* __restrict__ in, long slab_stride, long E, int P, int per,
+                                      float* __restrict__ out, long out_stride) {
+  const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int g = blockIdx.y;
+  if (e >= E) return;
+  const float* src = in + blockIdx.z * slab_stride;
+  const int p0 = g * per, p1 = min(P, p0 + per);
+  float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+  int p = p0;
+  for (; p + 3 < p1; p += 4) {
+    acc0 += src[(long)p * E + e];
+    acc1 += src[(long)(p + 1) * E + e];
+    acc2 += src[(long)(p + 2) * E + e];
+    acc3 += src[(long)(p + 3) * E + e];
+  }
+  for (; p < p1; ++p) acc0 += src[(long)p * E + e];
+  out[blockIdx.z * out_stride + (long)g * E + e] = (acc0 + acc1) + (acc2 + acc3);
+}
+
+int reduce_slab_layers(const float* slabs, long slab_stride, int P, long ES, float* grp, long grp_stride, int L,
+                       hipStream_t s) {
+  if (L < 1 || P < 1) return ASR_OK;
+  dim3 g1((unsigned)((ES + 255) / 256), reduce_groups(P), L);
+  hipLaunchKernelGGL(k_reduce_slabs_layers, g1, dim3(256), 0, s, slabs, slab_stride, ES, P, 32, grp, grp_stride);
+  ASR_LAUNCH_CHECK("k_reduce_slabs_layers");
+  return ASR_OK;
+}
+
 // Pass 1 only: P slab rows of ES floats -> reduce_groups(P) group rows at grp.
 int reduce_slabs_to_groups(const float* slabs, int P, long ES, float* grp, hipStream_t s) {
   const int G = reduce_groups(P);
