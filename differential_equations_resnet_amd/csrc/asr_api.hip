@@ -87,6 +87,7 @@ int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, i
 int conv_f32_k(int fmode, int K, const void* xin, void* out, uint8_t* mask, const float* w, const float* bias, float h,
                float two_gamma, const float* dy, int N, int H, int W, int C, hipStream_t s, const float* extra);
 int wgrad_f32_chunks(int N, int H);
+int f32_block_slab_rows(int N, int H, int W, int C);
 bool conv32_fused_bwd_supported(int W, int C);
 int conv32_bwd_fused(const float* dy, const uint8_t* mask, float h, const float* x, const float* w, float two_gamma,
                      const float* extra, bool skip_dy, int N, int H, int W, int C, float* dx, bool need_w,
@@ -122,11 +123,11 @@ struct BwdWs {
   size_t dz, slabs, red, g, total;
 };
 
-static BwdWs bwd_ws_layout(int N, int H, int W, int C, int dtype, int stages = 1, int K = 3) {
+static BwdWs bwd_ws_layout(int N, int H, int W, int C, int dtype, int stages = 1, int K = 3, int slab_rows = -1) {
   BwdWs b{};
   const long E = (long)K * K * C * C;
   const long P = (long)N * H * W * C;
-  const int nsl = kMaxSlabsApi * stages;
+  const int nsl = slab_rows >= 0 ? slab_rows : kMaxSlabsApi * stages;
   size_t off = 0;
   b.dz = off;
   if (dtype == ASR_F32) off += align_up((size_t)P * 4, 256);
@@ -360,6 +361,7 @@ struct NetLayout {
   int stack_grid;     // its workgroups
   size_t theta_dst_tm, stack_slabs, stack_done;  // tile-major projection map, [L][grid][E+C] slabs, counters
   size_t theta_dst_pr;  // the pull-back from the pair-local slabs (stack_pair)
+  int f32_rows;         // fp32: slab rows of one block application's weight gradient (f32_block_slab_rows)
   size_t grow;        // stacked Euler backward: dL/dx_L as one bf16 row per image (the GAP gradient) [N][C]
 };
 
@@ -428,19 +430,24 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.dxa = take(tr ? (size_t)L.P * L.act_bytes : 0);
   L.dxb = take(tr ? (size_t)L.P * L.act_bytes : 0);
   L.dxg = take(L.rk2 && tr ? (size_t)L.P * L.act_bytes : 0);
-  // per-block backward workspace (asr_conv_backward layout), reused by the stem
-  const BwdWs bw = bwd_ws_layout(c->N, c->H, c->W, C, c->dtype, L.stages);
+  // per-block backward workspace (asr_conv_backward layout), reused by the stem.
+  // fp32 keeps every block's slabs in slabs_all, sized by the grid its weight
+  // gradient runs (not the 512-row maximum): no slab rows here, no slabs2
+  const bool f32 = c->dtype == ASR_F32;
+  L.f32_rows = f32 ? f32_block_slab_rows(c->N, c->H, c->W, C) : 0;
+  const BwdWs bw = bwd_ws_layout(c->N, c->H, c->W, C, c->dtype, L.stages, 3, f32 ? 0 : -1);
   const long E1 = 9L * c->Cin * C;
   const size_t stem_ws = align_up((size_t)L.P * 4, 256) + align_up((size_t)kMaxSlabsApi * (E1 + C) * 4, 256) +
                          align_up(reduce_ws_bytes(kMaxSlabsApi, E1 + C), 256);
   L.bwdws = take(tr ? std::max(bw.total, stem_ws) : 0);
   // odd Euler blocks' slabs (even ones use the backward workspace's): a
   // block's slabs stay readable while the next block's kernel reduces them
-  L.slabs2 = take(tr ? (size_t)L.stages * kMaxSlabsApi * (L.E + C) * 4 : 0);  // every other block's slabs
-  L.grp_stride = (long)reduce_groups(L.stages * kMaxSlabsApi) * (L.E + C);
+  L.slabs2 = take(tr && !f32 ? (size_t)L.stages * kMaxSlabsApi * (L.E + C) * 4 : 0);  // every other block's slabs
+  const int rows = f32 ? L.stages * L.f32_rows : L.stages * kMaxSlabsApi;
+  L.grp_stride = (long)reduce_groups(rows) * (L.E + C);
   L.grp = take(tr ? (size_t)c->L * L.grp_stride * 4 : 0);
-  L.slab_stride = (long)L.stages * kMaxSlabsApi * (L.E + C);
-  L.slabs_all = take(tr && c->dtype == ASR_F32 ? (size_t)c->L * L.slab_stride * 4 : 0);
+  L.slab_stride = (long)rows * (L.E + C);
+  L.slabs_all = take(tr && f32 ? (size_t)c->L * L.slab_stride * 4 : 0);
   L.deep_slabs = take(L.deep && tr ? deep16_slab_bytes(c->N, c->L) : 0);
   L.theta_dst_tm = take(L.stack_bwd ? (size_t)L.ntheta * 2 * 4 : 0);
   L.theta_dst_pr = take(L.stack_pair ? (size_t)L.ntheta * 2 * 4 : 0);
@@ -1001,8 +1008,9 @@ int asr_net_check_status(const asr_net_config* cfg, const void* ws, size_t ws_by
   ASR_TRY(net_check(cfg));
   const NetLayout L = net_layout(cfg);
   if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_net_check_status: workspace too small");
-  ASR_TRY(hip_check(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize"));
-  return hip_check(hipGetLastError(), "asr_net_check_status");
+  // the stream's own completion status only (hipGetLastError would report, and clear,
+  // whatever error another HIP call on this thread left behind)
+  return hip_check(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
 }
 
 int asr_net_kernel_times(float* us) {
@@ -1056,7 +1064,7 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   // blocks, last to first
   const int32_t* theta_dst = (const int32_t*)(b + L.theta_dst);
   int nsl_blk = 0;
-  const BwdWs bw = bwd_ws_layout(N, H, W, C, cfg->dtype, L.stages);
+  const BwdWs bw = bwd_ws_layout(N, H, W, C, cfg->dtype, L.stages, 3, bf ? -1 : 0);  // (net_layout's)
   int dz1_fused = 0;  // dcur holds dz1 = dx1 * [x1 > 0] after the block loop
   const float* pend_slabs = nullptr;  // the slabs whose pass-1 reduction is still pending
   int pend_P = 0;
@@ -1132,7 +1140,12 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
     }
     nsl_blk = nsl;
     std::swap(dcur, dnext);
-    if (!bf) continue;
+    if (!bf) {
+      if (nsl > L.stages * L.f32_rows)  // (the device differs from the one the workspace was sized on)
+        return fail(ASR_E_WORKSPACE, "fp32 block %d wrote %d slab rows, the workspace holds %d (sized on another device?)",
+                    l, nsl, L.stages * L.f32_rows);
+      continue;
+    }
     if (pend_P > 0 && !folded) ASR_TRY(reduce_slabs_to_groups(pend_slabs, pend_P, L.E + C, pend_grp, s));
     pend_slabs = slabs_l;
     pend_P = nsl;

@@ -3626,18 +3626,29 @@ extern "C" int asr_debug_stack_backward(int grid) {
   return ASR_OK;
 }
 
+namespace asr {
+namespace blk {
+__device__ unsigned g_stack_degraded_taken = 0u;
+// asr_stack_status: read (and with reset, clear) the degraded-wait count in one
+// device atomic, so a stacked backward still running on another stream cannot
+// add a count between the read and the reset
+__global__ void k_stack_status_take(int reset) {
+  g_stack_degraded_taken =
+      reset ? __hip_atomic_exchange(&g_stack_degraded, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+            : __hip_atomic_load(&g_stack_degraded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+}  // namespace blk
+}  // namespace asr
+
 // host, blocking: waits of stacked-backward workgroups that ran out since the
 // last reset (each one a slower launch, never a wrong gradient); reset != 0
-// then clears the count
+// then clears the count (atomically with the read, on the device)
 extern "C" int asr_stack_status(int reset) {
+  hipLaunchKernelGGL(asr::blk::k_stack_status_take, dim3(1), dim3(1), 0, (hipStream_t)0, reset ? 1 : 0);
+  if (hipGetLastError() != hipSuccess) return asr::fail(ASR_E_HIP, "asr_stack_status: launch failed");
   unsigned n = 0;
-  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(asr::blk::g_stack_degraded), sizeof(n)) != hipSuccess)
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(asr::blk::g_stack_degraded_taken), sizeof(n)) != hipSuccess)
     return asr::fail(ASR_E_HIP, "asr_stack_status: hipMemcpyFromSymbol failed");
-  if (reset) {
-    const unsigned z = 0;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(asr::blk::g_stack_degraded), &z, sizeof(z)) != hipSuccess)
-      return asr::fail(ASR_E_HIP, "asr_stack_status: hipMemcpyToSymbol failed");
-  }
   return (int)std::min<unsigned>(n, 0x7fffffffu);
 }
 

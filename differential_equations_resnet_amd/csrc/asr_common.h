@@ -98,4 +98,18 @@ __device__ __forceinline__ bf16 from_f32<bf16>(float v) { return (bf16)v; }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// The wait states of a v_mfma_f32_16x16x4_f32 result (10 on gfx950), spent on
+// the straight line right after the MFMA chain, before the epilogue's first
+// branch.  hipcc (ROCm 7.2) pads a join block for its longer predecessor
+// only: where an epilogue branch skips a few instructions, the join read the
+// accumulator 2 states early (k_conv32 forward) or 5-7 early (a
+// persistent-band k_conv32).  sched_barrier keeps the nops
+// between the chain and the code after it; tests/test_isa.py
+// (tools/asm_mfma_audit.py) checks every path of the compiled kernels.
+__device__ __forceinline__ void mfma_f32_settle() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 9");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 }  // namespace asr

@@ -264,6 +264,7 @@ __global__ __launch_bounds__(256) void k_conv32(const float* __restrict__ xin, f
 #pragma unroll
         for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[t][q][s], bv[s], acc, 0, 0, 0);
       }
+    mfma_f32_settle();  // (the epilogue branches: every path must see the result's wait states)
     {
       const bool ok = y0 + r < H;
       const long pix = ((long)n * H + y0 + r) * W + px;
@@ -440,15 +441,21 @@ static int conv32_dispatch(int C, int W, const void* xin, void* out, uint8_t* ma
   return fail(ASR_E_UNSUPPORTED, "conv f32 (MFMA): C=%d", C);
 }
 
+// k_wgrad32's grid = its slab rows (one [dW | db] slab per workgroup)
 template <int C, int W>
-static int launch_wgrad32(const float* x, const float* dz, int N, int H, float* slabs, int* nslabs, hipStream_t s,
-                          const uint8_t* dmask = nullptr, float dh = 1.f) {
+static int wgrad32_grid(int N, int H) {
   const long items = (long)N * ((H + 3) / 4);
   int cus = cu_count();
   if (cus <= 0) cus = 256;
+  const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / wgrad32_lds<C, W>())));
+  return (int)std::max<long>(1, std::min<long>({items, (long)per_cu * cus, 512L}));
+}
+
+template <int C, int W>
+static int launch_wgrad32(const float* x, const float* dz, int N, int H, float* slabs, int* nslabs, hipStream_t s,
+                          const uint8_t* dmask = nullptr, float dh = 1.f) {
   const size_t lds = wgrad32_lds<C, W>();
-  const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
-  const int grid = (int)std::max<long>(1, std::min<long>({items, (long)per_cu * cus, 512L}));
+  const int grid = wgrad32_grid<C, W>(N, H);
   hipLaunchKernelGGL((k_wgrad32<C, W>), dim3(grid), dim3(768), lds, s, x, dz, N, H, slabs, dmask, dh);
   ASR_LAUNCH_CHECK("k_wgrad32");
   *nslabs = grid;
@@ -573,6 +580,29 @@ int wgrad_f32_chunks(int N, int H) {
   const long R = (long)N * H;
   long chunks = std::min<long>(R, 256);
   return (int)std::max<long>(chunks, 1);
+}
+
+// Slab rows one fp32 3x3 C -> C block application's weight gradient writes
+// (conv32_bwd_fused / wgrad_f32): the workspace of the fp32 networks keeps
+// every block's slabs, so it is sized by this, not by the 512-row maximum.
+// On the device the workspace was sized for (the MFMA grid follows its CU count).
+int f32_block_slab_rows(int N, int H, int W, int C) {
+  if (conv32_supported(W, C, C)) {
+#define ASR_WR(CC)                                      \
+  switch (W) {                                          \
+    case 32: return wgrad32_grid<CC, 32>(N, H);         \
+    case 16: return wgrad32_grid<CC, 16>(N, H);         \
+    case 8: return wgrad32_grid<CC, 8>(N, H);           \
+  }                                                     \
+  break
+    switch (C) {
+      case 16: ASR_WR(16);
+      case 32: ASR_WR(32);
+      case 64: ASR_WR(64);
+    }
+#undef ASR_WR
+  }
+  return wgrad_f32_chunks(N, H);
 }
 
 int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, int Ci, int Co, float* slabs,

@@ -41,6 +41,7 @@ int reduce_and_project(const float* slabs, int P, long E, int Cb, const int32_t*
                        float* dtheta, float* dbias, float* dw_out, float* ws, hipStream_t s);
 size_t reduce_ws_bytes(int P, long ES);
 int reduce_groups(int P);
+int f32_block_slab_rows(int N, int H, int W, int C);
 int project_layers(float* grp, long grp_stride, int G, long E, int Cb, const int32_t* theta_dst, long n_theta,
                    int L, float* out, long out_stride, hipStream_t s);
 int reduce_slab_layers(const float* slabs, long slab_stride, int P, long ES, float* grp, long grp_stride, int L,
@@ -65,7 +66,6 @@ namespace {
 constexpr int kTK = 3;              // the transition's kxk (the builder's kernel_size; 3 in every reference config)
 constexpr int kMaxTransChunks = 256;  // wgrad row chunks
 constexpr int kMaxStemSlabs = 512;    // asr_stem_head.hip stem_grid bound
-constexpr int kMaxBlockSlabs = 512;   // asr_api.hip kMaxSlabsApi: slab rows of one block's fp32 weight gradient
 
 struct TGeom {
   int Ho, Wo, pt, pl;
@@ -549,6 +549,7 @@ struct StageL {
   size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, act_t, mask_t, acts, masks, grp, slabs;  // workspace offsets
   long grp_stride;   // floats per block of pass-1 group rows
   long slab_stride;  // floats per block of weight-gradient slabs
+  int slab_rows;     // slab rows of one block's weight gradient (f32_block_slab_rows)
 };
 struct SLayout {
   int ns;
@@ -645,9 +646,12 @@ SLayout stages_layout(const asr_stages_config* c) {
     g.mask_t = g.S ? take((size_t)g.P) : 0;
     g.acts = take((size_t)std::max(g.L, 1) * g.P * 4);
     g.masks = take((size_t)std::max(g.L, 1) * g.mask_bytes);
-    g.grp_stride = (long)reduce_groups(kMaxBlockSlabs) * (g.E + g.C);
+    // every block keeps its slabs until the stage's one reduction launch: sized by the
+    // grid the fp32 weight gradient runs at this shape, not by the 512-row maximum
+    g.slab_rows = f32_block_slab_rows(c->N, g.H, g.W, g.C);
+    g.grp_stride = (long)reduce_groups(g.slab_rows) * (g.E + g.C);
     g.grp = take((size_t)std::max(g.L, 1) * g.grp_stride * 4);
-    g.slab_stride = (long)kMaxBlockSlabs * (g.E + g.C);
+    g.slab_stride = (long)g.slab_rows * (g.E + g.C);
     g.slabs = take((size_t)g.L * g.slab_stride * 4);
     if (g.L > 0) L.cws_bytes = std::max(L.cws_bytes, asr_conv_backward_workspace_bytes(c->N, g.H, g.W, g.C, ASR_F32));
     if (g.S) L.tws_bytes = std::max(L.tws_bytes, trans_ws_bytes(c->N, g.Hp, g.Wp, g.Cp, g.C, g.S));
@@ -819,7 +823,9 @@ int asr_stages_forward_backward(const asr_stages_config* cfg, const float* param
       ASR_TRY(conv_backward_keep_slabs(d, x_in, (const uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes, wl, cfg->h, gam,
                                        N, g.H, g.W, g.C, e, b + L.cws, (float*)(b + g.slabs) + (size_t)l * g.slab_stride,
                                        &nsl, s));
-      if (nsl > kMaxBlockSlabs) return fail(ASR_E_UNSUPPORTED, "asr_stages: %d slab rows > %d", nsl, kMaxBlockSlabs);
+      if (nsl > g.slab_rows)  // (the device differs from the one the workspace was sized on)
+        return fail(ASR_E_WORKSPACE, "asr_stages: %d slab rows > the workspace's %d (sized on another device?)", nsl,
+                    g.slab_rows);
       std::swap(d, e);
     }
     if (g.L > 0)

@@ -543,16 +543,17 @@ class Model:
         if self._native is not None:
             self._native.push_weights()
 
-    def compile_native(self, batch_size, dtype="bfloat16", device=None):
+    def compile_native(self, batch_size, dtype=None, device=None):
         """Lower this model onto the native executor (lowering.py).  The
         model owns one device parameter set; every (batch size, dtype) view
-        returned here shares it."""
+        returned here shares it.  dtype None: the executor's own precision
+        (bfloat16 for single-stage nets, float32 for multi-stage ones)."""
         from .lowering import NativeModel
         if self._native is None:
             self._native = NativeModel(self, device)
         return self._native.view(batch_size, dtype)
 
-    def predict(self, x, batch_size=None, dtype="bfloat16"):
+    def predict(self, x, batch_size=None, dtype=None):
         """Softmax outputs for images `x` (numpy or device, NHWC), in batches
         of `batch_size` (default: min(len(x), 256), so the executor's
         training-sized workspace stays bounded)."""

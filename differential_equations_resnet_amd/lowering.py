@@ -36,6 +36,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 
+import warnings
+
 import numpy as np
 
 from . import _lib
@@ -339,6 +341,7 @@ class NativeModel:
         self._torch = torch
         self._rt = runtime
         self._executors = {}
+        self._warned_stages_dtype = False
         self.vars = self.plan.weight_vars()
         self.n_params = int(sum(v.value.size for v in self.vars))
         self.params = torch.empty(self.n_params, dtype=torch.float32, device=self.device)
@@ -348,8 +351,28 @@ class NativeModel:
         self._host_stale = False
         self.push_weights()
 
-    def view(self, batch_size: int, dtype="bfloat16") -> "NativeView":
-        return NativeView(self, int(batch_size), dtype)
+    def resolve_dtype(self, dtype):
+        """The activation dtype an executor of this model runs in.  None: the
+        plan's own (bfloat16 single-stage, float32 multi-stage).  A multi-stage
+        net always runs in float32 (its block kernels at 16x16 / 8x8 are fp32
+        only): an explicit bfloat16 request is warned about once and mapped to
+        float32, so train and predict views share one executor per batch size."""
+        if isinstance(self.plan, StagesPlan):
+            if dtype not in (None, "float32") and not self._warned_stages_dtype:
+                warnings.warn(f"multi-stage nets run in float32 on the native executor (dtype={dtype!r} requested)",
+                              stacklevel=3)
+                self._warned_stages_dtype = True
+            return "float32"
+        return "bfloat16" if dtype is None else dtype
+
+    def view(self, batch_size: int, dtype=None) -> "NativeView":
+        return NativeView(self, int(batch_size), self.resolve_dtype(dtype))
+
+    def check_status(self):
+        """Blocking: synchronise and check every executor built for this model
+        (a failed launch raises AsrError)."""
+        for ex in self._executors.values():
+            ex.check_status()
 
     # -- weights ---------------------------------------------------------------
     def push_weights(self):
@@ -377,6 +400,7 @@ class NativeModel:
     def executor(self, batch_size: int, dtype, input_u8: bool, inference: bool = False):
         """The executor for (batch, dtype, input kind); inference=True gives the
         forward-only one (bounded workspace: x_0 + two activation slots)."""
+        dtype = self.resolve_dtype(dtype)
         key = (int(batch_size), dtype, bool(input_u8), bool(inference))
         ex = self._executors.get(key)
         if ex is None and isinstance(self.plan, StagesPlan):
@@ -440,7 +464,7 @@ class NativeView:
             object.__setattr__(self, name, value)
 
     def matches(self, batch_size, dtype):
-        return self.batch_size == int(batch_size) and self.dtype == dtype
+        return self.batch_size == int(batch_size) and self.dtype == self.state.resolve_dtype(dtype)
 
     def executor(self, input_u8: bool, inference: bool = False):
         return self.state.executor(self.batch_size, self.dtype, input_u8, inference)

@@ -70,7 +70,7 @@ class Training:
                  train_labels_placeholder=None, val_features_placeholder=None, val_labels_placeholder=None,
                  train_features=None, train_labels=None, val_features=None, val_labels=None, global_step=0,
                  num_layers=None, record_summaries=True, summaries=["mean_gradient_norms"], summaries_dir=None,
-                 summaries_name=None, csv_logger_dir=None, csv_logger_name=None, dtype="bfloat16"):
+                 summaries_name=None, csv_logger_dir=None, csv_logger_name=None, dtype=None):
         import torch
         if train_dataset is None or not hasattr(train_dataset, "__iter__"):
             raise ValueError("train_dataset must be an ArrayDataset (dataset_utils) or another iterable of "

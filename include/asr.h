@@ -331,7 +331,9 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
                              const float* targets, float* grads, float* loss, float* probs,
                              void* ws, size_t ws_bytes, asr_stream_t stream);
 /* Host, blocking (synchronises the stream): ASR_OK, or ASR_E_HIP with the
- * runtime's error when a launch of this thread failed.  (Since ABI 6 a missed
+ * runtime's error when work on the stream failed (the stream's status only:
+ * a pending error of another HIP call on this thread is neither reported nor
+ * cleared).  (Since ABI 6 a missed
  * in-launch hand-off of the C=64 stacked backward is not an error: it costs
  * speed, see asr_stack_status.) */
 int asr_net_check_status(const asr_net_config* cfg, const void* ws, size_t ws_bytes, asr_stream_t stream);
@@ -353,7 +355,8 @@ int asr_net_kernel_times(float* us);
  * launch, on the same stream, before the projection: the gradients are those
  * of the full hand-off, only slower (e.g. a grid that is not co-resident
  * because another kernel or process shares the device).  reset != 0 clears
- * the count after reading it. */
+ * the count in the same device atomic that reads it (a backward running on
+ * another stream meanwhile loses no count). */
 int asr_stack_status(int reset);
 /* Test knob: force the stacked backward's grid (0: one workgroup per CU;
  * larger than the resident capacity makes hand-offs run out and degrade, see

@@ -2,15 +2,21 @@
 configs[1]: the C=64 Euler bf16 network) against the fp64 oracle, and the
 reference-held conv KAT run through the C ABI itself.
 
-The bf16 network runs with the production kernel set (variant 0): the MFMA
-stem forward (k_stem_fwd_mfma), the band-conv block forward (k_fwd3, three
-workgroups per CU), the 12-wave fused backward with the stem's relu' folded
-into the first block (k_bwd3<..., RO>), the slab reduction folded into the
-next block's backward, and the MFMA stem weight gradient (k_stem_wgrad_mfma).
-The N=192 case gives every persistent workgroup several row bands (fwd: 1536
-bands over 768 workgroups, bwd: 6 bands per workgroup), so the band pipeline,
-the halo-row copies and the per-workgroup dW accumulation across bands are
-all compared with the oracle, not only the single-band path.  It is compared with
+The bf16 network runs with the production kernel set (variant 0, the
+composition the bench line times): at C=64 the MFMA stem forward
+(k_stem_fwd_mfma), ALL L blocks' forward in one k_fwd3_stack launch (two
+4-wave workgroups per CU, whole images per workgroup, a ring of three LDS
+tiles), ALL L blocks' backward in one k_bwd3_stack launch (one 12-wave
+workgroup per CU: dgrad waves 0-3, pair-local wgrad waves 4-11, the stem's
+relu' folded into block 0, pair-local weight-gradient slabs published
+write-through with pass 1 of block l's reduction folded into block l-2's bands
+behind the done[] counters, blocks 0-1 reduced after the launch), the
+projection onto theta, and the MFMA stem weight gradient (k_stem_wgrad_mfma);
+at C=16 the fused deep stack (k_fwd16_fused / k_bwd16_fused).  Every
+workgroup walks 8 row bands per image and block, so the band pipeline, the
+halo rows and the per-workgroup dW accumulation across bands are compared
+with the oracle; N=192 also exercises the one-image-per-workgroup grid of
+192 workgroups.  It is compared with
 the fp64 oracle (oracle.net_forward / net_backward, a restatement of
 tfkeras_resnets.py:547-597, training.py:295) on the same fp32 parameters and
 uint8 images.

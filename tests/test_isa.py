@@ -14,6 +14,12 @@ LDS reads and LDS-DMA, which the compiler cannot see:
     control-flow graph from each such load and flags any instruction that
     touches its registers before a retiring vmcnt wait or barrier_vm's
     barrier (self-test below);
+  * MFMA results: no instruction may read or write an MFMA's D registers
+    before the result's wait states have passed, on any control-flow path
+    from the MFMA (tools/asm_mfma_audit.py).  hipcc pads a join block for one
+    predecessor only: the shipped fp32 k_conv32 forward read its accumulator
+    2 states early on one epilogue path and a persistent-band k_conv32 (the
+    fixture under tests/fixtures/) 5-6 early, which failed GPU parity;
   * register spills: a compiler-inserted scratch access only ever adds
     vector-memory ops, which makes a counted `vmcnt(n)` wait MORE conservative
     (it retires the oldest ops first), never less; but a spill is also where
@@ -35,6 +41,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "differential_equations_resnet_amd", "csrc")
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import asm_lds_audit  # noqa: E402
+import asm_mfma_audit  # noqa: E402
 import asm_vmem_audit  # noqa: E402
 
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
@@ -187,3 +194,76 @@ def test_hot_kernels_spill_allow_list(asm_files):
                         f"({vmax} / {smax}: {why}); re-run the audit and the GPU parity tests before raising it")
     missing = [k for k, v in seen.items() if v == 0]
     assert not missing, f"allow-listed kernels not found in the build: {missing}"
+
+
+def _probe_required(op_builtin, a_ty, tmp_path):
+    """wait states hipcc puts between an MFMA and a dependent VALU read on a
+    straight line (the audit's requirement table must match the toolchain)."""
+    src = tmp_path / "probe.hip"
+    src.write_text(r"""
+#include <hip/hip_runtime.h>
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+extern "C" __global__ void k(float* out, const A_TY* a) {
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  acc = OP(a[threadIdx.x], a[threadIdx.x + 64], acc, 0, 0, 0);
+  out[threadIdx.x] = acc[3] * 2.f;
+}
+""".replace("A_TY", a_ty).replace("OP", op_builtin))
+    asm = open(_compile(str(src), str(src) + ".s")).read()
+    m = re.search(r"v_mfma\w+[^\n]*\n\s*s_nop (\d+)\n\s*v_\w+[^\n]*v\d", asm)
+    assert m, asm[:2000]
+    return int(m.group(1)) + 1
+
+
+def test_mfma_wait_state_table_matches_compiler(asm_files, tmp_path):
+    probes = {"v_mfma_f32_16x16x32_bf16": ("__builtin_amdgcn_mfma_f32_16x16x32_bf16", "bf16x8"),
+              "v_mfma_f32_16x16x4_f32": ("__builtin_amdgcn_mfma_f32_16x16x4f32", "float")}
+    used = set()
+    for f in asm_files:
+        used |= set(re.findall(r"\b(v_mfma_\w+)", open(f).read()))
+    assert used and used <= set(asm_mfma_audit.REQUIRED), f"MFMA opcodes without a requirement: {used - set(asm_mfma_audit.REQUIRED)}"
+    for op, (builtin, ty) in probes.items():
+        assert _probe_required(builtin, ty, tmp_path) == asm_mfma_audit.REQUIRED[op], op
+
+
+def test_asm_mfma_audit_clean(asm_files):
+    n_mfma = 0
+    for f in asm_files:
+        text = open(f).read()
+        n_mfma += len(re.findall(r"\bv_mfma_", text))
+        bad, findings = asm_mfma_audit.audit(text)
+        assert bad == 0, f"{os.path.basename(f)}: " + "\n".join(findings[:10])
+    assert n_mfma > 10000
+
+
+def test_asm_mfma_audit_flags_persistent_band_fixture():
+    """The reconstructed persistent-band k_conv32 (tools/pb_fixture.py): the
+    epilogue reads a3 after 4-5 of the 10 states, on the path that enters the
+    join by a branch from the last MFMA."""
+    text = open(os.path.join(ROOT, "tests", "fixtures", "isa_k_conv32p_persistent_band.s")).read()
+    bad, findings = asm_mfma_audit.audit(text)
+    assert bad >= 1 and all("k_conv32p" in f and "v_accvgpr_read_b32" in f for f in findings), findings
+
+
+def test_asm_mfma_audit_follows_branches():
+    """Short path through a branch to the join: flagged; with the states
+    spent before the branch: clean; an accumulate chain: clean."""
+    asm = """_Z1kv:                                   ; @_Z1kv
+\tv_mfma_f32_16x16x4_f32 a[0:3], v1, v2, a[0:3]
+\tPAD
+\ts_cbranch_vccnz .LBB0_2
+\tv_mov_b32_e32 v9, 0
+\tv_mov_b32_e32 v9, 1
+\tv_mov_b32_e32 v9, 2
+\tv_mov_b32_e32 v9, 3
+.LBB0_2:
+\ts_nop 4
+\tv_accvgpr_read_b32 v5, a3
+\ts_endpgm
+"""
+    assert asm_mfma_audit.audit(asm.replace("\tPAD\n", ""))[0] == 1
+    assert asm_mfma_audit.audit(asm.replace("PAD", "s_nop 9"))[0] == 0
+    chain = asm.replace("\tPAD\n", "\tv_mfma_f32_16x16x4_f32 a[4:7], v1, v2, a[0:3]\n\ts_nop 9\n").replace(
+        "v_accvgpr_read_b32 v5, a3", "v_accvgpr_read_b32 v5, a7")
+    assert asm_mfma_audit.audit(chain)[0] == 0
