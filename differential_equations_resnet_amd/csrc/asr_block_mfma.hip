@@ -193,6 +193,21 @@ __device__ __forceinline__ void dma_row_instr_at(const bf16* __restrict__ src, u
   dma16_at(base + loff, tile + (unsigned)((r * TW + 1 + seg * PPI) * NQ) * 16u);
 }
 
+// Image row gy (zeros outside [0, H)) into a tile row: its W / PPI = 4 pieces in
+// one dma16x4_at (the lane's swizzled source offset is the same for every
+// piece: the swizzle is segment-invariant).  tile_row = the tile row's LDS byte address.
+template <int C, int W>
+__device__ __forceinline__ void dma_row_whole_at(const bf16* __restrict__ src, unsigned tile_row, int n, int gy, int H,
+                                                 unsigned loff) {
+  using G = Geo<C>;
+  constexpr int NQ = G::NQ, PPI = G::PPI;
+  static_assert(W / PPI == 4 && PPI * C * 2 == 1024 && PPI * NQ * 16 == 1024, "whole-row DMA: four 1 KiB pieces");
+  const unsigned char* base = ((unsigned)gy < (unsigned)H)
+                                  ? (const unsigned char*)src + ((long)n * H + gy) * (W * C * 2)
+                                  : (const unsigned char*)g_zero_page;
+  dma16x4_at(base + loff, tile_row + (unsigned)(NQ * 16));
+}
+
 template <int C, int W>
 __device__ __forceinline__ void dma_rows(const bf16* __restrict__ src, unsigned char* tile, int n, int gy0,
                                          int nrows, int H, int wave, int nwaves, int lane) {
@@ -1127,8 +1142,10 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
       } else {
         ntile = nt, ngy0 = yy - 1, nrows = min(BR, H - yy) + 2;
       }
-      for (int j = __builtin_amdgcn_readfirstlane(wave); j < nrows * IPR; j += NW)
-        dma_row_instr<C, W>(nxs, ntile, xn, ngy0, j, H, loff);
+      // whole rows, one dma16x4 each (wave w: rows w, w + 4)
+      const unsigned nt0 = lds_u32(ntile);
+      for (int r = __builtin_amdgcn_readfirstlane(wave); r < nrows; r += NW)
+        dma_row_whole_at<C, W>(nxs, nt0 + (unsigned)(r * BD::ROWB), xn, ngy0 + r, H, loff);
     }
     if (wave == 0) ASR_BTR(0, 0, it, 2);
     const unsigned tb = lds_u32(lds + buf * TILE);
@@ -2130,7 +2147,6 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
               for (int oi = 0; oi < 2; ++oi)
                 accb[oi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, Bf[oi], accb[oi], 0, 0, 0);
             }
-            if (r < BR - 1 && ipc < npc) piece();
           }
         });
       };
@@ -2769,23 +2785,19 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       const int xr0 = cont ? 2 : 0;
       const bool syn = orow >= 0 && synth(nxt);
       if (syn) synth_row(nxt, orow, buf ^ 1);
-      const int ndy = orow >= 0 && !syn ? IPR : 0;
-      const int nx = (more && w8 >= 4) ? ((BR + 2 - xr0) * IPR - (w8 - 4) + 3) / 4 : 0;
-      const int npc = ndy + nx;
-      int ipc = 0;
-      const bf16* nxdy = dy_of(nxt.l);
-      const bf16* nxx = x_of(nxt.l);
-      auto piece = [&]() {
-        if (ipc < ndy) {
-          dma_row_instr_at<C, W>(nxdy, lds0 + (unsigned)(LL::DY + (buf ^ 1) * LL::TILE + orow * LL::ROWB), nxt.n,
-                              nxt.b * BR - 1 + orow, ipc, H, loff);
-        } else {
-          dma_row_instr_at<C, W>(nxx, lds0 + (unsigned)(LL::X + (buf ^ 1) * LL::TILE + xr0 * LL::ROWB), nxt.n, nxt.b * BR - 1 + xr0,
-                              (w8 - 4) + 4 * (ipc - ndy), H, loff);
-        }
-        ++ipc;
-      };
-      while (ipc < npc && ipc < ASR_BWD3_DMA0) piece();
+      // the next band's rows, each by one whole-row DMA (4 pieces on one address): the own dy
+      // row, and x rows 2..5 on waves 4..7 when the next band continues this image (rows 0, 1
+      // are the halo copy), else rows 0..5 with row r on wave (r + 6) & 7.  (Measured and not
+      // kept: the x rows DMA'd by the dgrad waves before their conv, -1.8 %, r05c)
+      if (orow >= 0 && !syn)
+        dma_row_whole_at<C, W>(dy_of(nxt.l), lds0 + (unsigned)(LL::DY + (buf ^ 1) * LL::TILE + orow * LL::ROWB), nxt.n,
+                               nxt.b * BR - 1 + orow, H, loff);
+      if (more) {
+        const int xrow = cont ? (w8 >= 4 ? w8 - 2 : -1) : (((w8 + 2) & 7) < BR + 2 ? ((w8 + 2) & 7) : -1);
+        if (xrow >= 0)
+          dma_row_whole_at<C, W>(x_of(nxt.l), lds0 + (unsigned)(LL::X + (buf ^ 1) * LL::TILE + xrow * LL::ROWB), nxt.n,
+                                 nxt.b * BR - 1 + xrow, H, loff);
+      }
       if (wave == 4) ASR_BTR(1, 1, it, 2);
       bf16x8 Bf[2], Ar[3];
       auto mfma_band_full = [&](auto bo) {
@@ -2814,7 +2826,6 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
               for (int oi = 0; oi < 2; ++oi)
                 accb[oi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, Bf[oi], accb[oi], 0, 0, 0);
             }
-            if (r < BR - 1 && ipc < npc) piece();
           }
         });
       };
@@ -2879,16 +2890,11 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
                 accb[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, F[b + 3], accb[1], 0, 0, 0);
               }
             }
-            // DMA pieces left after the first ASR_BWD3_DMA0: two per row group 3 and 7
-            if constexpr ((g == 3 || g == 7) && r < BR - 1) {
-              if (ipc < npc) piece();
-            }
           });
         });
       };
       auto convert_next = [&]() {  // the next band's dz of this wave's own row
         if (more) {
-          while (ipc < npc) piece();
           vm_wait(0);  // own dy row and mask dwords of band it+1 (x DMA and fold loads too)
           convert_own(orow, buf ^ 1, mwv);
         }
@@ -2905,7 +2911,6 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         for (int k = 0; k < NOB; ++k) offB[k] += dlt;
       }
       mfma_band(std::integral_constant<int, 0>{});
-      while (ipc < npc) piece();
       if (wave == 4) ASR_BTR(1, 1, it, 3);
       convert_next();
       if (wave == 4) ASR_BTR(1, 1, it, 4);

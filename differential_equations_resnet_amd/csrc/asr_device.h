@@ -10,7 +10,7 @@
 namespace asr {
 namespace blk {
 
-static __device__ __attribute__((aligned(16))) uint4 g_zero_page[64];  // 1 KiB of zeros (DMA source for padding)
+static __device__ __attribute__((aligned(16))) uint4 g_zero_page[256];  // 4 KiB of zeros (DMA source for padding: one whole C=64 row)
 
 typedef const __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
@@ -55,6 +55,26 @@ __device__ __forceinline__ void dma16_at(const void* src, unsigned lds_addr) {
       "s_mov_b32 m0, %1\n\t"
       "s_nop 0\n\t"
       "global_load_lds_dwordx4 %0, off"
+      :
+      : "v"(src), "s"(l)
+      : "memory", "m0");
+}
+
+// Four consecutive 1 KiB LDS-DMA pieces on ONE address: the instruction offset
+// advances the global source and the LDS destination alike (probed on gfx950,
+// tools/probe/lds_dma_offset.hip), so a whole 4 KiB tile row costs one M0 write
+// and no per-piece scalar address math.  (The per-piece form cost the
+// stacked backward's wgrad waves ~1.8k cycles per band in scalar issue: 8
+// waves' address arithmetic through one SALU slot per SIMD.)
+__device__ __forceinline__ void dma16x4_at(const void* src, unsigned lds_addr) {
+  const unsigned l = __builtin_amdgcn_readfirstlane(lds_addr);
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off\n\t"
+      "global_load_lds_dwordx4 %0, off offset:1024\n\t"
+      "global_load_lds_dwordx4 %0, off offset:2048\n\t"
+      "global_load_lds_dwordx4 %0, off offset:3072"
       :
       : "v"(src), "s"(l)
       : "memory", "m0");
