@@ -469,7 +469,9 @@ template <int C, int KS0 = 0>
 __device__ __forceinline__ void load_A1_untracked_at(const unsigned char* base, unsigned voff, bf16x8 (&A)[Geo<C>::KS]) {
   if constexpr (KS0 < Geo<C>::KS) {
     u32x4 v = __builtin_bit_cast(u32x4, A[KS0]);
-    gload128_untracked<(KS0 % 4) * 1024>(v, base + (KS0 / 4) * 4096, voff);
+    // the base advances by 4 KiB every 4 loads (an SALU add): only a load right after
+    // such an add (or the readfirstlane of the first) needs the 5 wait states
+    gload128_untracked<(KS0 % 4) * 1024, KS0 % 4 == 0>(v, base + (KS0 / 4) * 4096, voff);
     A[KS0] = __builtin_bit_cast(bf16x8, v);
     load_A1_untracked_at<C, KS0 + 1>(base, voff, A);
   }
@@ -941,7 +943,7 @@ __global__ __launch_bounds__(256, WPE) void k_fwd3(const bf16* __restrict__ x, c
   for (int it = i0; it < i1; ++it, cur.next(nb), nxt.next(nb)) {
     const int buf = (it - i0) & 1;
     if (wave == 0) ASR_BTR(0, 0, it - i0, 0);
-    barrier_vm(nst);  // band it landed; every wave is done with band it-1's tile
+    barrier_vm_usual<2 * BR>(nst);  // band it landed; every wave is done with band it-1's tile
     if (wave == 0) ASR_BTR(0, 0, it - i0, 1);
     nst = 0;
     if (it + 1 < i1) {
@@ -1105,47 +1107,78 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
   for (int k = 0; k < NT; ++k) zero_halo_cols<C, W>(lds + k * TILE, BR + 2, tid, 64 * NW);
   constexpr int IPR = W / G::PPI;  // DMA pieces per row
   const unsigned loff = (unsigned)dma_lane_off<C, W>(lane) * 2u;
-  // cursor over (block l, image n, band b)
-  int cl = 0, cn = n0, cb = 0;
-  int xl = 0, xn = n0, xb = 0;  // next item
-  auto adv = [&](int& l, int& n, int& b) {
+  // cursor over (stage l, image n, band b) and the band's first row R within this
+  // workgroup's images ((n - n0) H + b BR, 32-bit): every address of a band is a per-stage
+  // 64-bit base (computed once per stage) plus R times a power of two, so a band costs a
+  // few scalar adds instead of 64-bit multiplies (the r05f instruction mix: ~180 scalar
+  // instructions per band and wave before, a wave issues one instruction per ~4 cycles)
+  int cl = 0, cn = n0, cb = 0, cR = 0;
+  int xl = 0, xn = n0, xb = 0, xR = 0;  // next item
+  auto adv = [&](int& l, int& n, int& b, int& R) {
     if (++b == nb) {
       b = 0;
       if (++n == n1) {
         n = n0;
         ++l;
+        R = 0;
+      } else {
+        R = (n - n0) * H;
       }
+    } else {
+      R += BR;
     }
   };
-  adv(xl, xn, xb);
+  constexpr unsigned ROWBYTES = W * C * 2, MROWBYTES = W * C / 8;
+  static_assert(ROWBYTES == 4096 && MROWBYTES == 256, "row byte shifts");
+  const long img0 = (long)n0 * H;  // this workgroup's first image row
+  const unsigned region = (unsigned)((n1 - n0) * H);  // its image rows
+  // per stage: the output / mask buffer descriptors (base = this workgroup's first row) and
+  // the next stage's DMA source base
+  auto out_rs = [&](int st) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(out_of(st) + img0 * W * C), 0, region * ROWBYTES, 0x00020000);
+  };
+  auto mask_rs = [&](int st) {
+    uint8_t* m = mask_of(st);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(m ? m + img0 * MROWBYTES : m), 0, m ? region * MROWBYTES : 0u,
+                                             0x00020000);
+  };
+  auto src_base = [&](int st) { return (const unsigned char*)(src_of(st) + img0 * W * C); };
+  adv(xl, xn, xb, xR);
   dma_rows<C, W>(x0, lds, cn, -1, min(BR, H) + 2, H, wave, NW, lane);
   int nst = 0;
   const int total = (RK2 ? 2 : 1) * L * per;
   ASR_BCLK(0, 0);
   int buf = 0, nbuf = 1, pbuf = NT - 1;  // this band's tile, the next band's, the previous band's
+  auto yrs = out_rs(0);
+  auto mrs = mask_rs(0);
+  bool hasm = mask_of(0) != nullptr;
+  const unsigned char* nsrc = src_base(0);  // the next item's stage's source rows
+  int nsrc_st = 0;
   for (int it = 0; it < total; ++it) {
     if (wave == 0) ASR_BTR(0, 0, it, 0);
-    barrier_vm(nst);  // band it landed; every wave is done with band it-1's tile
+    barrier_vm_usual<2 * BR>(nst);  // band it landed; every wave is done with band it-1's tile
     if (wave == 0) ASR_BTR(0, 0, it, 1);
     nst = 0;
-    // the next band into the other buffer: rows 0, 1 are this band's rows BR, BR+1
-    // when it continues the image (copied inside LDS), the rest by DMA
-    unsigned char* ntile = lds;
-    const bf16* nxs = x0;
-    int ngy0 = 0, nrows = 0;
+    // the next band into the ring: rows 0, 1 are this band's rows BR, BR+1 when it
+    // continues the image (read in place), the rest by DMA
     if (it + 1 < total) {
-      unsigned char* nt = lds + nbuf * TILE;
-      const int yy = xb * BR;
-      nxs = src_of(xl);
-      if (xl == cl && xn == cn && xb == cb + 1) {
-        ntile = nt + 2 * BD::ROWB, ngy0 = yy + 1, nrows = min(BR, H - yy);
-      } else {
-        ntile = nt, ngy0 = yy - 1, nrows = min(BR, H - yy) + 2;
+      if (xl != nsrc_st) {  // (once per stage)
+        nsrc = src_base(xl);
+        nsrc_st = xl;
       }
+      const int yy = xb * BR;
+      const bool ncont = xl == cl && xn == cn && xb == cb + 1;
+      const int r0 = ncont ? 1 : -1;  // image row offset of the first DMA'd tile row
+      const int nrows = min(BR, H - yy) + (ncont ? 0 : 2);
+      const unsigned nt0 = lds_u32(lds + nbuf * TILE) + (ncont ? 2u * BD::ROWB : 0u);
       // whole rows, one dma16x4 each (wave w: rows w, w + 4)
-      const unsigned nt0 = lds_u32(ntile);
-      for (int r = __builtin_amdgcn_readfirstlane(wave); r < nrows; r += NW)
-        dma_row_whole_at<C, W>(nxs, nt0 + (unsigned)(r * BD::ROWB), xn, ngy0 + r, H, loff);
+      for (int r = __builtin_amdgcn_readfirstlane(wave); r < nrows; r += NW) {
+        const int gy = yy + r0 + r;
+        const unsigned char* rowp = (unsigned)gy < (unsigned)H
+                                        ? nsrc + (size_t)((unsigned)(xR + r0 + r) * ROWBYTES)
+                                        : (const unsigned char*)g_zero_page;
+        dma16x4_at(rowp + loff, nt0 + (unsigned)(r * BD::ROWB) + (unsigned)(NQ * 16));
+      }
     }
     if (wave == 0) ASR_BTR(0, 0, it, 2);
     const unsigned tb = lds_u32(lds + buf * TILE);
@@ -1176,16 +1209,9 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
       load_bias4_untracked(bias ? bias + (long)blk_of(xl) * bias_stride + 16 * ot : nullptr, g, bz);
     }
     lgkm_wait<0>();
-    const int y0 = cb * BR, rows = min(BR, H - y0);
-    const long rowb = ((long)cn * H + y0) * W;
-    // the band's y rows and mask rows as buffer stores: a wave-uniform base (SGPRs), the
-    // lane's 32-bit offset and the row as the scalar offset, so no per-lane 64-bit
-    // address math per row, and whether there is a mask is a wave-uniform test
-    uint8_t* mk = mask_of(l);
-    const bool hasm = mk != nullptr;
-    const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)(out_of(l) + rowb * C), 0, RB * W * C * 2, 0x00020000);
-    const auto mrs = __builtin_amdgcn_make_buffer_rsrc((void*)(hasm ? mk + rowb * (C / 8) : mk), 0, RB * W * (C / 8),
-                                                       0x00020000);
+    const int rows = min(BR, H - cb * BR);
+    // the band's y rows and mask rows as buffer stores: the stage's descriptor, the lane's
+    // 32-bit offset and the row (R + r) as the scalar offset
     const float hst = (RK2 && !(l & 1)) ? 0.5f * h : h;
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
@@ -1204,15 +1230,20 @@ __global__ __launch_bounds__(256, 2) void k_fwd3_stack(const bf16* __restrict__ 
       });
       bits = pair_bits_to_byte(bits);
       if (hasm) {
-        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bits, mrs, (int)lm, r * W * (C / 8), 0);
+        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bits, mrs, (int)lm, (int)((unsigned)(cR + r) * MROWBYTES), 0);
         ++nst;
       }
-      __builtin_amdgcn_raw_buffer_store_b128(yw, yrs, (int)ly, r * W * C * 2, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(yw, yrs, (int)ly, (int)((unsigned)(cR + r) * ROWBYTES), 0);
       ++nst;
     }
     if (wave == 0) ASR_BTR(0, 0, it, 4);
-    cl = xl, cn = xn, cb = xb;
-    adv(xl, xn, xb);
+    if (xl != cl && it + 1 < total) {  // the next item starts a new stage: its store descriptors
+      yrs = out_rs(xl);
+      mrs = mask_rs(xl);
+      hasm = mask_of(xl) != nullptr;
+    }
+    cl = xl, cn = xn, cb = xb, cR = xR;
+    adv(xl, xn, xb, xR);
     pbuf = buf, buf = nbuf, nbuf = nbuf + 1 == NT ? 0 : nbuf + 1;
   }
   ASR_BCLK(0, 1);
@@ -1877,7 +1908,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
       const int n = cur.n, y0 = cur.b * BR;
       const int rows = min(BR, H - y0);
       if (wave == 0) ASR_BTR(1, 0, it - i0, 0);
-      barrier_vm(nst);  // band it staged everywhere; band it-1 fully consumed
+      barrier_vm_usual<BR>(nst);  // band it staged everywhere; band it-1 fully consumed
       if (wave == 0) ASR_BTR(1, 0, it - i0, 1);
       // XT: the extra dx term of the band's rows (in flight during the conv)
       u32x4 exv[XT ? BR : 1];
@@ -2453,7 +2484,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       const int n = cur.n, y0 = cur.b * BR, l = cur.l;
       const int rows = min(BR, H - y0);
       if (wave == 0) ASR_BTR(1, 0, it, 0);
-      barrier_vm(nst);  // item it staged everywhere; item it-1 fully consumed
+      barrier_vm_usual<BR>(nst);  // item it staged everywhere; item it-1 fully consumed
       if (wave == 0) ASR_BTR(1, 0, it, 1);
       const unsigned dzt = lds_u32(lds + LL::DZ + buf * LL::TILE), dyt = lds_u32(lds + LL::DY + buf * LL::TILE);
       const unsigned xt = lds_u32(lds + LL::X + buf * LL::TILE);

@@ -93,10 +93,13 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // base usually comes from v_readfirstlane (a VALU write of an SGPR), which a
 // VMEM instruction may read only 5 wait states later; hipcc does not insert
 // them in front of inline asm, so the asm does (s_nop 4).
-template <int IMM>
+template <int IMM, bool NOP = true>
 __device__ __forceinline__ void gload128_untracked(u32x4& v, const void* sbase, unsigned voff) {
   static_assert(IMM >= 0 && IMM < 4096, "global immediate offset range");
-  asm volatile("s_nop 4\n\tglobal_load_dwordx4 %0, %1, %2 offset:%3" : "+v"(v) : "v"(voff), "s"(sbase), "i"(IMM) : "memory");
+  if constexpr (NOP)
+    asm volatile("s_nop 4\n\tglobal_load_dwordx4 %0, %1, %2 offset:%3" : "+v"(v) : "v"(voff), "s"(sbase), "i"(IMM) : "memory");
+  else  // (a later load of a run on the same base: the base's SGPR write is >= 5 states old)
+    asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3" : "+v"(v) : "v"(voff), "s"(sbase), "i"(IMM) : "memory");
 }
 template <int IMM>
 __device__ __forceinline__ void gload32_untracked(float& v, const void* sbase, unsigned voff) {
@@ -180,6 +183,18 @@ __device__ __forceinline__ void vm_wait(int n) {
 // also wait for the global stores issued after that DMA.
 __device__ __forceinline__ void barrier_vm(int n) {
   vm_wait(n);  // the counted wait, then one barrier every path reaches
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+// barrier_vm for a count that is usually K: the general vm_wait is a switch
+// over 25 immediates, which hipcc lowers to a chain of predicate tests (~40
+// scalar instructions and ~14 branches per call, r05f instruction mix): the
+// usual count takes one compare and one wait instead
+template <int K>
+__device__ __forceinline__ void barrier_vm_usual(int n) {
+  if (__builtin_amdgcn_readfirstlane(n) == K)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(K) : "memory");
+  else
+    vm_wait(n);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 // instructions one wave issues in a `for (j = wave; j < total; j += nw)` loop
