@@ -81,11 +81,14 @@ CONFIGS = {
     "v7_predict": (16, 64, 1, "bfloat16", "antisym 64 blocks x 16 filters, Model.predict of ONE image (v7 notebook "
                    "speed test), bf16", "euler", "eval"),
 }
-# multi-stage nets (asr_stages_*, fp32): name -> (stages [(C, L, transition stride)], per-GPU batch, description)
+# multi-stage nets (asr_stages_*): name -> (stages [(C, L, transition stride)], per-GPU batch, dtype, description)
+HE32 = ("He-style antisym-ResNet-32 (num_stages=4, blocks [10,10,10] at 32^2 x 16, 16^2 x 32, 8^2 x 64, stride-2 "
+        "single_layer_conv_block transitions, tfkeras_resnets.py:575-593)")
 STAGE_CONFIGS = {
-    "he32": ([(16, 10, 0), (32, 9, 2), (64, 9, 2)], 128,
-             "He-style antisym-ResNet-32 (num_stages=4, blocks [10,10,10] at 32^2 x 16, 16^2 x 32, 8^2 x 64, stride-2 "
-             "single_layer_conv_block transitions, tfkeras_resnets.py:575-593) batch 128/GPU fp32"),
+    "he32": ([(16, 10, 0), (32, 9, 2), (64, 9, 2)], 128, "float32", HE32 + " batch 128/GPU fp32"),
+    "he32_bf16": ([(16, 10, 0), (32, 9, 2), (64, 9, 2)], 512, "bfloat16",
+                  HE32 + " batch 512/GPU bf16 (identity blocks bf16, fp32 accumulation; stem, transitions, head and "
+                         "weight gradients fp32)"),
 }
 # the reference's own measurements of the same metric (TF 1.12, fp32, one NVIDIA GPU)
 REFERENCE = {
@@ -520,7 +523,7 @@ def stages_params(stages, num_classes=10, seed=0):
 
 
 def stages_main(args):
-    """--config he32: one training step (fwd + bwd + Adam) of a multi-stage
+    """--config he32 / he32_bf16: one training step (fwd + bwd + Adam) of a multi-stage
     net on the asr_stages_* executor, same timing contract as main()."""
     import torch
     from differential_equations_resnet_amd import _lib, distributed, runtime as rt
@@ -531,11 +534,11 @@ def stages_main(args):
         _lib.load(path=os.path.abspath(args.lib))
     dev = rt.require_gpu()
     distributed.init_from_env(device=dev)
-    stages, N, desc = STAGE_CONFIGS[args.config]
+    stages, N, dtype, desc = STAGE_CONFIGS[args.config]
     L = sum(l for _, l, _ in stages)
     h = 8.0 / L
     ex = rt.StagesExecutor(N, 32, 32, 3, stages, 10, h, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
-                           input_u8=True, device=dev)
+                           input_u8=True, device=dev, dtype=dtype)
     params = torch.from_numpy(stages_params(stages)).to(dev)
     assert params.numel() == ex.n_params
     distributed.broadcast_params(params, 0)
@@ -578,19 +581,20 @@ def stages_main(args):
             fl += Lb * 2 * 9 * C * C * Hc * Hc
             Cp = C
         tflops = 3 * fl * N * world / (elapsed / args.steps) / 1e12 / world
+        peak = BF16_PEAK_TFLOPS if dtype == "bfloat16" else F32_PEAK_TFLOPS
         out_line = {
             "metric": f"CIFAR-10 images/sec (fwd+bwd) {desc}; {world} GPU", "value": round(value, 1),
             "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32",
+            "vs_baseline": None, "dtype": "bf16" if dtype == "bfloat16" else "f32",
             "data": f"synthetic ({N_BATCHES} HBM-resident batches of uniform uint8 32x32x3 images, random one-hot "
                     f"labels; he_normal init, thetas x{THETA_SCALE}, fc x{FC_SCALE})",
             "config": {"workload": desc + "; train step = fwd + bwd + Adam (asr_stages_forward_backward)",
                        "global_batch": N * world, "per_gpu_batch": N, "stages": stages, "h": round(h, 6),
                        "parallelism": f"dp{world}", "initial_loss": round(first, 4) if first is not None else None,
                        "final_loss": round(float(out.item()), 4)},
-            "roofline": {"bound": "mfma", "achieved": round(tflops, 2), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(tflops / F32_PEAK_TFLOPS, 4), "traffic": None,
+            "roofline": {"bound": "mfma", "achieved": round(tflops, 2), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(tflops / peak, 4), "traffic": None,
                          "kernel": "whole step per GPU (conv FLOPs 3 x forward / step time; all kernels incl. "
                                    "stem, head, reductions, Adam)"},
             "cpu_baseline": None,

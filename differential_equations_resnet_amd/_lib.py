@@ -29,7 +29,7 @@ ASR_BF16 = 1
 ASR_PARAM_3BY3 = 0
 ASR_PARAM_GENERAL = 1
 ASR_PARAM_REGULAR = 2
-ABI_VERSION = 7
+ABI_VERSION = 8
 ASR_MODE_EULER = 0
 ASR_MODE_CONV = 1
 ASR_INTEGRATOR_EULER = 0
@@ -71,6 +71,7 @@ class StagesConfig(ct.Structure):
         ("n_stages", ct.c_int), ("C", ct.c_int * 8), ("L", ct.c_int * 8), ("stride", ct.c_int * 8),
         ("h", ct.c_float), ("gamma", ct.c_float), ("subtract_mean", ct.c_float), ("divide_by_stddev", ct.c_float),
         ("use_norm", ct.c_int), ("input_u8", ct.c_int), ("param_kind", ct.c_int), ("antisymmetric", ct.c_int),
+        ("dtype", ct.c_int),
     ]
 
 
@@ -127,6 +128,7 @@ SIGNATURES = [
     ("asr_transition_forward", _I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     ("asr_transition_backward_workspace_bytes", _S, [_I, _I, _I, _I, _I, _I]),
     ("asr_transition_backward", _I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _S, _P]),
+    ("asr_stages_check", ct.c_int, [ct.POINTER(StagesConfig)]),
     ("asr_stages_param_count", _L, [ct.POINTER(StagesConfig)]),
     ("asr_stages_workspace_bytes", _S, [ct.POINTER(StagesConfig)]),
     ("asr_stages_prepare", _I, [ct.POINTER(StagesConfig), _P, _S]),

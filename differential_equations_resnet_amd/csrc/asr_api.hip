@@ -46,6 +46,12 @@ int stem_fwd_mfma(const void* img, int input_u8, const float* w1, const float* b
                   float mean, float inv_std, int use_norm, void* out, hipStream_t s);
 bool stem_fwd_mfma_supported(int Cin, int H, int W, int C);
 static bool mfma_supported(int C, int W) { return (C == 16 || C == 32 || C == 64) && W == 32; }
+// asr_conv_f32.hip: bf16 Euler blocks at any stage width (W in {32, 16, 8}), the multi-stage nets' path
+bool convb_supported(int W, int C);
+int convb_forward(const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h, int N, int H, int W,
+                  int C, hipStream_t s);
+int convb_backward(const void* dy, const uint8_t* mask, const void* x, const void* w, float h, float two_gamma, int N,
+                   int H, int W, int C, void* dx, bool need_w, float* slabs, int* nslabs, hipStream_t s);
 // asr_deep16.hip
 bool deep16_supported(int H, int W, int C);
 bool block_stack_fwd_supported(int N, int H, int W, int C);
@@ -156,6 +162,11 @@ static int block_backward(int mode, const void* dy, const void* x, const uint8_t
   if (fold_done) *fold_done = 0;
   if (dtype == ASR_BF16) {
     if (!dx && !need_w) return ASR_OK;
+    if (!mfma_supported(C, W)) {  // W = 16 / 8: the any-width bf16 kernels (plain Euler blocks only)
+      if (mode != ASR_MODE_EULER || extra || skip_dy || relu_dx || fold_slabs || accum_slabs || !convb_supported(W, C))
+        return fail(ASR_E_UNSUPPORTED, "bf16 backward at C=%d W=%d: Euler blocks only", C, W);
+      return convb_backward(dy, mask, x, w, h, 2.f * gamma, N, H, W, C, dx, need_w, slabs, nsl, s);
+    }
     const int cm = (mode == ASR_MODE_EULER) ? 2 : 3;  // BWD_EULER / BWD_CONV
     return block_bwd_mfma(cm, dy, x, mask, w, h, 2.f * gamma, N, H, W, C, dx, slabs, nsl, extra, skip_dy ? 1 : 0, s,
                           relu_dx ? 1 : 0, relu_done, fold_slabs, fold_P, fold_grp, fold_done, accum_slabs ? 1 : 0);
@@ -615,8 +626,11 @@ int asr_conv_forward(int mode, const void* x, void* y, uint8_t* mask, const void
   if (mode != ASR_MODE_EULER && mode != ASR_MODE_CONV) return fail(ASR_E_ARG, "asr_conv_forward: bad mode %d", mode);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == ASR_BF16) {
-    if (!mfma_supported(C, W))
-      return fail(ASR_E_UNSUPPORTED, "bf16 conv needs C in {16,32,64} and W == 32 (C=%d W=%d)", C, W);
+    if (!mfma_supported(C, W)) {  // the Euler block at W = 16 / 8 (multi-stage nets)
+      if (mode == ASR_MODE_EULER && convb_supported(W, C)) return convb_forward(x, y, mask, w, bias, h, N, H, W, C, s);
+      return fail(ASR_E_UNSUPPORTED, "bf16 conv needs C in {16,32,64} and W == 32 (W in {16, 8}: Euler mode) (C=%d W=%d)",
+                  C, W);
+    }
     if (mode == ASR_MODE_EULER && deep16_supported(H, W, C))
       return deep16_forward(x, y, 0, mask, 0, w, bias, 0, h, N, 1, true, s);
     return block_fwd_mfma(mode == ASR_MODE_EULER ? 0 : 1, x, nullptr, y, mask, w, bias, h, N, H, W, C, s);
@@ -894,8 +908,9 @@ int asr_conv_backward(int mode, const void* dy, const void* x, const uint8_t* ma
   if ((dtheta || dbias || dw_hwio) && !x) return fail(ASR_E_ARG, "asr_conv_backward: x needed for weight gradients");
   if (dtheta && !theta_dst) return fail(ASR_E_ARG, "asr_conv_backward: theta_dst needed for dtheta");
   if (dtype != ASR_F32 && dtype != ASR_BF16) return fail(ASR_E_ARG, "asr_conv_backward: bad dtype");
-  if (dtype == ASR_BF16 && !mfma_supported(C, W))
-    return fail(ASR_E_UNSUPPORTED, "bf16 conv needs C in {16,32,64} and W == 32 (C=%d W=%d)", C, W);
+  if (dtype == ASR_BF16 && !mfma_supported(C, W) && !(mode == ASR_MODE_EULER && convb_supported(W, C)))
+    return fail(ASR_E_UNSUPPORTED, "bf16 conv needs C in {16,32,64} and W == 32 (W in {16, 8}: Euler mode) (C=%d W=%d)",
+                C, W);
   if (!ws || ws_bytes < bwd_ws_layout(N, H, W, C, dtype).total)
     return fail(ASR_E_WORKSPACE, "asr_conv_backward: workspace too small");
   return conv_backward_impl(mode, dy, x, mask, w, theta_dst, n_theta, h, gamma, N, H, W, C, dtype, dx, dtheta, dbias,

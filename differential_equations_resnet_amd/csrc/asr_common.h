@@ -98,6 +98,13 @@ __device__ __forceinline__ bf16 from_f32<bf16>(float v) { return (bf16)v; }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// two fp32 -> packed bf16 pair, round to nearest even (one v_cvt_pk_bf16_f32)
+__device__ __forceinline__ unsigned pk_bf16_rn(float a, float b) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const bf16x2_t v = {(bf16)a, (bf16)b};
+  return __builtin_bit_cast(unsigned, v);
+}
+
 // The wait states of a v_mfma_f32_16x16x4_f32 result (10 on gfx950), spent on
 // the straight line right after the MFMA chain, before the epilogue's first
 // branch.  hipcc (ROCm 7.2) pads a join block for its longer predecessor

@@ -189,6 +189,14 @@ struct F32Band {
   static_assert(W == 8 || W == 16 || W == 32, "fp32 MFMA band: W in {8, 16, 32}");
 };
 
+// 4 consecutive elements as fp32 (a 16-B load, or 8 B of bf16 converted)
+__device__ __forceinline__ f32x4 load4f(const float* p) { return *(const f32x4*)p; }
+__device__ __forceinline__ f32x4 load4f(const bf16* p) {
+  const uint2 u = *(const uint2*)p;
+  return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+               __uint_as_float(u.y & 0xffff0000u)};
+}
+
 // dz = h dy [relu bit] of 4 channels (bit index pixel*C + c, C a multiple of 16: a nibble)
 __device__ __forceinline__ f32x4 masked_dz4(f32x4 v, const uint8_t* __restrict__ dmask, long bit, float dh) {
   const unsigned nib = (unsigned)(dmask[bit >> 3] >> (bit & 7));
@@ -200,8 +208,8 @@ __device__ __forceinline__ f32x4 masked_dz4(f32x4 v, const uint8_t* __restrict__
 // stage rows y0-1 .. y0+BR of image n into tile (zeros outside the image and
 // in the two halo columns), float4 per thread; with dmask, src is dy and the
 // tile gets dz = dh * dy * [relu bit] (the Euler block's dz, no separate pass)
-template <int C, int W>
-__device__ __forceinline__ void f32_stage_rows(const float* __restrict__ src, float* tile, int n, int y0, int H,
+template <int C, int W, typename Ts = float>
+__device__ __forceinline__ void f32_stage_rows(const Ts* __restrict__ src, float* tile, int n, int y0, int H,
                                                int tid, int nthreads, const uint8_t* __restrict__ dmask = nullptr,
                                                float dh = 1.f) {
   using G = F32Band<C, W>;
@@ -212,7 +220,7 @@ __device__ __forceinline__ void f32_stage_rows(const float* __restrict__ src, fl
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)G::W) {
       const long e = (((long)n * H + gy) * G::W + gx) * C + 4 * c4;
-      v = *(const f32x4*)(src + e);
+      v = load4f(src + e);
       if (dmask) v = masked_dz4(v, dmask, e, dh);
     }
     *(f32x4*)(tile + (r * G::TW + col) * C + 4 * c4) = v;
@@ -302,8 +310,8 @@ __global__ __launch_bounds__(256) void k_conv32(const float* __restrict__ xin, f
   }
 }
 
-template <int C, int W>
-__global__ __launch_bounds__(768) void k_wgrad32(const float* __restrict__ x, const float* __restrict__ dz, int N,
+template <int C, int W, typename Tx = float>
+__global__ __launch_bounds__(768) void k_wgrad32(const Tx* __restrict__ x, const Tx* __restrict__ dz, int N,
                                                  int H, float* __restrict__ slabs, const uint8_t* __restrict__ dmask,
                                                  float dh) {
   using G = F32Band<C, W>;
@@ -325,13 +333,13 @@ __global__ __launch_bounds__(768) void k_wgrad32(const float* __restrict__ x, co
     const int n = (int)(item / nb), y0 = (int)(item % nb) * BR;
     const int rows = min(BR, H - y0);
     __syncthreads();  // the previous item's tiles consumed
-    f32_stage_rows<C, W>(x, xt, n, y0, H, tid, 768);
+    f32_stage_rows<C, W, Tx>(x, xt, n, y0, H, tid, 768);
     for (int i = tid; i < BR * G::W * C / 4; i += 768) {
       const int r = i / (G::W * C / 4);
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (r < rows) {
         const long e = ((long)n * H + y0) * G::W * C + 4 * i;
-        v = *(const f32x4*)(dz + e);
+        v = load4f(dz + e);
         if (dmask) v = masked_dz4(v, dmask, e, dh);  // dz is dy here: dz = dh dy [relu bit]
       }
       *(f32x4*)(dzt + 4 * i) = v;
@@ -451,12 +459,12 @@ static int wgrad32_grid(int N, int H) {
   return (int)std::max<long>(1, std::min<long>({items, (long)per_cu * cus, 512L}));
 }
 
-template <int C, int W>
-static int launch_wgrad32(const float* x, const float* dz, int N, int H, float* slabs, int* nslabs, hipStream_t s,
+template <int C, int W, typename Tx = float>
+static int launch_wgrad32(const Tx* x, const Tx* dz, int N, int H, float* slabs, int* nslabs, hipStream_t s,
                           const uint8_t* dmask = nullptr, float dh = 1.f) {
   const size_t lds = wgrad32_lds<C, W>();
   const int grid = wgrad32_grid<C, W>(N, H);
-  hipLaunchKernelGGL((k_wgrad32<C, W>), dim3(grid), dim3(768), lds, s, x, dz, N, H, slabs, dmask, dh);
+  hipLaunchKernelGGL((k_wgrad32<C, W, Tx>), dim3(grid), dim3(768), lds, s, x, dz, N, H, slabs, dmask, dh);
   ASR_LAUNCH_CHECK("k_wgrad32");
   *nslabs = grid;
   return ASR_OK;
@@ -637,6 +645,215 @@ int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, i
   hipLaunchKernelGGL(k_db_f32, dim3(nch), dim3(((Co + 63) / 64) * 64), 0, s, dz, R, W, Co, rpc, E, slabs);
   ASR_LAUNCH_CHECK("k_db_f32");
   *nslabs = nch;
+  return ASR_OK;
+}
+
+// ===========================================================================
+// bf16 block kernels at any stage width (W in {32, 16, 8}, C in {16, 32, 64}):
+// the multi-stage nets' identity blocks in bf16 (the He-style ResNet-32 at the
+// metric's precision, tfkeras_resnets.py:575-593).  k_conv32's geometry on
+// v_mfma_f32_16x16x32_bf16: a workgroup (4 waves) owns a band of BR = 4 output
+// rows of one image, the BR + 2 input rows staged in LDS as bf16 (pixel-major,
+// C channels contiguous; zero rows outside the image and zero halo columns),
+// every wave keeps its o-tile's A = W^T fragments (asr_theta_to_w's bf16 pack:
+// lane (lx, g) holds W^T[16 ot + lx][32 ks + 8 g .. + 7]) in registers and walks
+// its share of the band's 16-pixel tiles.  B fragment of k-step ks, lane (lx, g):
+// kappa = 32 ks + 8 g .. + 7 = tap t, channels i0 .. i0 + 7 of the pixel shifted
+// by t: one 16-B LDS read.  The accumulator lane (lx, g) holds channels 4g..4g+3
+// of pixel lx, as in the fp32 kernel (the same epilogue and mask nibbles).
+//   F_EULER: y = x + h relu(conv(x) + b), relu-mask bits;
+//   B_EULER: the tile holds dz = dy & mask (exact), dx = dy - h conv(dz) + 2 gamma h dz.
+// The weight gradient runs k_wgrad32 on the bf16 operands (staged to fp32 in
+// LDS, fp32 MFMA: the reduction is in fp32 either way, as the bf16 stacks').
+// ===========================================================================
+template <int C, int W_>
+struct BfBand {
+  static constexpr int OT = C / 16, W = W_, TW = W + 2, BR = 4, TILEE = (BR + 2) * TW * C;
+  static constexpr int T = BR * W / 16;  // 16-pixel tiles per band
+  static constexpr int WPT = 4 / OT;     // waves sharing an o-tile
+  static constexpr int KS = (9 * C + 31) / 32;
+  static_assert(W == 8 || W == 16 || W == 32, "bf16 band: W in {8, 16, 32}");
+};
+
+// 8 bf16 masked by 8 relu bits (bit j -> halfword j)
+__device__ __forceinline__ uint4 mask8_bf16(uint4 v, unsigned bits) {
+  auto h2 = [&](unsigned b) { return ((b & 1u) ? 0xffffu : 0u) | ((b & 2u) ? 0xffff0000u : 0u); };
+  v.x &= h2(bits);
+  v.y &= h2(bits >> 2);
+  v.z &= h2(bits >> 4);
+  v.w &= h2(bits >> 6);
+  return v;
+}
+
+// rows y0-1 .. y0+BR of image n into the bf16 tile (zeros outside the image and in the halo
+// columns), 16 B (8 channels) per thread and step; with dmask, src is dy and the tile gets dz = dy & mask
+template <int C, int W>
+__device__ __forceinline__ void bf_stage_rows(const bf16* __restrict__ src, bf16* tile, int n, int y0, int H, int tid,
+                                              const uint8_t* __restrict__ dmask) {
+  using G = BfBand<C, W>;
+  constexpr int C8 = C / 8, NCH = (G::BR + 2) * G::TW * C8;
+  for (int i = tid; i < NCH; i += 256) {
+    const int r = i / (G::TW * C8), rem = i % (G::TW * C8), col = rem / C8, c8 = rem % C8;
+    const int gy = y0 - 1 + r, gx = col - 1;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W) {
+      const long e = (((long)n * H + gy) * W + gx) * C + 8 * c8;
+      v = *(const uint4*)(src + e);
+      if (dmask) v = mask8_bf16(v, dmask[e >> 3]);  // (bit index pixel*C + channel: a byte per 8 channels)
+    }
+    *(uint4*)(tile + (r * G::TW + col) * C + 8 * c8) = v;
+  }
+}
+
+template <int C, int W, int MODE>
+__global__ __launch_bounds__(256) void k_convb(const bf16* __restrict__ xin, bf16* __restrict__ out,
+                                               uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
+                                               const float* __restrict__ bias, float h, float two_gamma,
+                                               const bf16* __restrict__ dy, int N, int H,
+                                               const uint8_t* __restrict__ dmask) {
+  using G = BfBand<C, W>;
+  constexpr int OT = G::OT, TW = G::TW, BR = G::BR, KS = G::KS;
+  __shared__ __attribute__((aligned(16))) bf16 tile[G::TILEE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
+  const int ot = wave % OT, rw = wave / OT;
+  const int nb = (H + BR - 1) / BR;
+  const int n = blockIdx.x / nb, y0 = (blockIdx.x % nb) * BR;
+  if (n >= N) return;
+  bf16x8 A[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) A[ks] = *(const bf16x8*)(wpack + (((long)ot * KS + ks) * 64 + lane) * 8);
+  f32x4 bz = {0.f, 0.f, 0.f, 0.f};
+  if (MODE == F_EULER && bias) bz = *(const f32x4*)(bias + 16 * ot + 4 * g);
+  bf_stage_rows<C, W>(xin, tile, n, y0, H, tid, MODE == B_EULER ? dmask : nullptr);
+  __syncthreads();
+  constexpr int NT = (G::T + G::WPT - 1) / G::WPT;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int tau = rw + j * G::WPT;
+    if (tau >= G::T) break;  // (wave-uniform)
+    const int bp = 16 * tau + lx, r = bp / W, px = bp % W;
+    if (W >= 16 && y0 + r >= H) break;  // (wave-uniform for W >= 16; rows only grow with tau)
+    f32x4 acc = bz;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int kap = 32 * ks + 8 * g;
+      const int t = min(kap / C, 8), i0 = kap - (kap / C) * C;  // (C = 16, last k-step: tap 9 pads A with zeros)
+      const uint4 bv = *(const uint4*)(tile + ((r + t / 3) * TW + px + t % 3) * C + i0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], __builtin_bit_cast(bf16x8, bv), acc, 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // (the epilogue below reads acc: hipcc pads the wait states)
+    const bool ok = y0 + r < H;
+    const long pix = ((long)n * H + y0 + r) * W + px;
+    const long oi = pix * C + 16 * ot + 4 * g;  // this lane's 4 channels
+    const uint2 cw = *(const uint2*)(tile + ((r + 1) * TW + px + 1) * C + 16 * ot + 4 * g);  // x or dz at the pixel
+    const float ctr[4] = {__uint_as_float(cw.x << 16), __uint_as_float(cw.x & 0xffff0000u), __uint_as_float(cw.y << 16),
+                          __uint_as_float(cw.y & 0xffff0000u)};
+    float v[4];
+    if constexpr (MODE == F_EULER) {
+      unsigned nib = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float z = acc[e];
+        nib |= (z > 0.f ? 1u : 0u) << e;
+        v[e] = fmaf(h, fmaxf(z, 0.f), ctr[e]);
+      }
+      if (mask) {  // the pixel's 16 channels of this o-tile: 4 nibbles, one 16-bit store
+        unsigned m = nib << (4 * g);
+        m |= (unsigned)__shfl_xor((int)m, 16, 64);
+        m |= (unsigned)__shfl_xor((int)m, 32, 64);
+        if (g == 0 && ok) *(uint16_t*)(mask + (pix * C + 16 * ot) / 8) = (uint16_t)m;
+      }
+    } else {  // B_EULER: the tile holds dz = dy & mask
+      uint2 dw = make_uint2(0u, 0u);
+      if (ok) dw = *(const uint2*)(dy + oi);
+      const float d0[4] = {__uint_as_float(dw.x << 16), __uint_as_float(dw.x & 0xffff0000u),
+                           __uint_as_float(dw.y << 16), __uint_as_float(dw.y & 0xffff0000u)};
+      const float hg = h * two_gamma;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaf(hg, ctr[e], fmaf(-h, acc[e], d0[e]));
+    }
+    if (ok) *(uint2*)(out + oi) = make_uint2(pk_bf16_rn(v[0], v[1]), pk_bf16_rn(v[2], v[3]));
+  }
+}
+
+bool convb_supported(int W, int C) { return (W == 32 || W == 16 || W == 8) && (C == 16 || C == 32 || C == 64); }
+
+template <int C, int W, int MODE>
+static int launch_convb(const bf16* xin, bf16* out, uint8_t* mask, const bf16* w, const float* bias, float h,
+                        float two_gamma, const bf16* dy, int N, int H, const uint8_t* dmask, hipStream_t s) {
+  const long blocks = (long)N * ((H + 3) / 4);
+  if (blocks > 0x7fffffffL) return fail(ASR_E_ARG, "conv bf16: problem too large");
+  hipLaunchKernelGGL((k_convb<C, W, MODE>), dim3((unsigned)blocks), dim3(256), 0, s, xin, out, mask, w, bias, h,
+                     two_gamma, dy, N, H, dmask);
+  ASR_LAUNCH_CHECK("k_convb");
+  return ASR_OK;
+}
+
+// y = x + h relu(conv(x, W) + b) in bf16 (w: asr_theta_to_w's ASR_BF16 pack of one layer)
+int convb_forward(const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h, int N, int H, int W,
+                  int C, hipStream_t s) {
+#define ASR_CB(CC, WW)                                                                                             \
+  if (C == CC && W == WW)                                                                                          \
+    return launch_convb<CC, WW, F_EULER>((const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, 0.f, nullptr, N, H, \
+                                         nullptr, s);
+  ASR_CB(16, 32) ASR_CB(16, 16) ASR_CB(16, 8) ASR_CB(32, 32) ASR_CB(32, 16) ASR_CB(32, 8) ASR_CB(64, 32)
+  ASR_CB(64, 16) ASR_CB(64, 8)
+#undef ASR_CB
+  return fail(ASR_E_UNSUPPORTED, "conv bf16 (any width): C=%d W=%d", C, W);
+}
+
+// The Euler block's backward in bf16: dx = dy - h conv(dy & mask, W) + 2 gamma h (dy & mask)
+// (W: the forward pack for antisymmetric operators, whose transpose is -A + 2 gamma I; the
+// transposed operator's pack with gamma = 0 otherwise) and the weight-gradient slabs
+// (k_wgrad32 on the bf16 x and dy: dz = h dy [relu bit] staged in fp32)
+int convb_backward(const void* dy, const uint8_t* mask, const void* x, const void* w, float h, float two_gamma, int N,
+                   int H, int W, int C, void* dx, bool need_w, float* slabs, int* nslabs, hipStream_t s) {
+  *nslabs = 0;
+  if (!convb_supported(W, C)) return fail(ASR_E_UNSUPPORTED, "conv bf16 backward (any width): C=%d W=%d", C, W);
+  if (dx) {
+#define ASR_CB(CC, WW)                                                                                                  \
+  if (C == CC && W == WW)                                                                                               \
+    ASR_TRY((launch_convb<CC, WW, B_EULER>((const bf16*)dy, (bf16*)dx, nullptr, (const bf16*)w, nullptr, h, two_gamma, \
+                                           (const bf16*)dy, N, H, mask, s)));
+    ASR_CB(16, 32) ASR_CB(16, 16) ASR_CB(16, 8) ASR_CB(32, 32) ASR_CB(32, 16) ASR_CB(32, 8) ASR_CB(64, 32)
+    ASR_CB(64, 16) ASR_CB(64, 8)
+#undef ASR_CB
+  }
+  if (!need_w) return ASR_OK;
+#define ASR_WB(CC, WW)                                                                                     \
+  if (C == CC && W == WW)                                                                                  \
+    return launch_wgrad32<CC, WW, bf16>((const bf16*)x, (const bf16*)dy, N, H, slabs, nslabs, s, mask, h);
+  ASR_WB(16, 32) ASR_WB(16, 16) ASR_WB(16, 8) ASR_WB(32, 32) ASR_WB(32, 16) ASR_WB(32, 8) ASR_WB(64, 32)
+  ASR_WB(64, 16) ASR_WB(64, 8)
+#undef ASR_WB
+  return fail(ASR_E_UNSUPPORTED, "conv bf16 backward (any width): C=%d W=%d", C, W);
+}
+
+// elementwise bf16 <-> fp32 (the multi-stage bf16 net's transitions run in fp32)
+__global__ void k_bf16_to_f32(const bf16* __restrict__ a, float* __restrict__ b, long n8) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const uint4 u = ((const uint4*)a)[i];
+    const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      ((float2*)b)[4 * i + k] = make_float2(__uint_as_float(w[k] << 16), __uint_as_float(w[k] & 0xffff0000u));
+  }
+}
+__global__ void k_f32_to_bf16(const float* __restrict__ a, bf16* __restrict__ b, long n8) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const float4 p = ((const float4*)a)[2 * i], q = ((const float4*)a)[2 * i + 1];
+    ((uint4*)b)[i] = make_uint4(pk_bf16_rn(p.x, p.y), pk_bf16_rn(p.z, p.w), pk_bf16_rn(q.x, q.y), pk_bf16_rn(q.z, q.w));
+  }
+}
+int convert_bf16_f32(const void* src, void* dst, long n, int to_f32, hipStream_t s) {
+  if (n % 8) return fail(ASR_E_ARG, "bf16 <-> fp32: element count %ld not a multiple of 8", n);
+  const long n8 = n / 8;
+  const unsigned grid = (unsigned)std::max<long>(1, std::min<long>((n8 + 255) / 256, 8192));
+  if (to_f32)
+    hipLaunchKernelGGL(k_bf16_to_f32, dim3(grid), dim3(256), 0, s, (const bf16*)src, (float*)dst, n8);
+  else
+    hipLaunchKernelGGL(k_f32_to_bf16, dim3(grid), dim3(256), 0, s, (const float*)src, (bf16*)dst, n8);
+  ASR_LAUNCH_CHECK("k_bf16_f32");
   return ASR_OK;
 }
 

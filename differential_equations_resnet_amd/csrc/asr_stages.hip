@@ -46,6 +46,13 @@ int project_layers(float* grp, long grp_stride, int G, long E, int Cb, const int
                    int L, float* out, long out_stride, hipStream_t s);
 int reduce_slab_layers(const float* slabs, long slab_stride, int P, long ES, float* grp, long grp_stride, int L,
                        hipStream_t s);
+// asr_conv_f32.hip: the bf16 blocks at any stage width, bf16 <-> fp32
+bool convb_supported(int W, int C);
+int convb_forward(const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h, int N, int H, int W,
+                  int C, hipStream_t s);
+int convb_backward(const void* dy, const uint8_t* mask, const void* x, const void* w, float h, float two_gamma, int N,
+                   int H, int W, int C, void* dx, bool need_w, float* slabs, int* nslabs, hipStream_t s);
+int convert_bf16_f32(const void* src, void* dst, long n, int to_f32, hipStream_t s);
 // asr_api.hip
 int conv_backward_keep_slabs(const void* dy, const void* x, const uint8_t* mask, const void* w, float h, float gamma,
                              int N, int H, int W, int C, void* dx, void* ws, float* slabs, int* nsl, hipStream_t s);
@@ -547,6 +554,8 @@ struct StageL {
   long P, ntheta, E, blk_stride, mask_bytes;
   long off_t, off_blk;          // parameter offsets (floats)
   size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, act_t, mask_t, acts, masks, grp, slabs;  // workspace offsets
+  size_t act_tb, xin32;  // bf16 nets: the transition's output in bf16, its input in fp32 (kept for the backward)
+  long wstride;          // elements of one layer's W in wbuf (E fp32, or the bf16 MFMA pack)
   long grp_stride;   // floats per block of pass-1 group rows
   long slab_stride;  // floats per block of weight-gradient slabs
   int slab_rows;     // slab rows of one block's weight gradient (f32_block_slab_rows)
@@ -555,6 +564,9 @@ struct SLayout {
   int ns;
   StageL st[ASR_STAGES_MAX];
   bool sep_bwd;
+  bool bf;              // bf16 activations / block convs (asr_stages_config.dtype)
+  int act_bytes;
+  size_t t32a, t32b;    // bf16 nets: fp32 scratch of the transition backward (dy, dx)
   long off_c1k, off_c1b, off_fck, off_fcb, n_params, Pmax;
   size_t act0, probs, loss_per, dlogits, gap, dA, dB, cws, tws, sslabs, sred, total;
   size_t cws_bytes, tws_bytes, sred_bytes;
@@ -579,6 +591,17 @@ int stages_check(const asr_stages_config* c) {
   if (c->C[c->n_stages - 1] > 256 || c->num_classes > 256)
     return fail(ASR_E_UNSUPPORTED, "asr_stages: head needs C and num_classes <= 256");
   if (c->use_norm && c->divide_by_stddev == 0.f) return fail(ASR_E_ARG, "asr_stages: divide_by_stddev == 0");
+  if (c->dtype != ASR_F32 && c->dtype != ASR_BF16) return fail(ASR_E_ARG, "asr_stages: dtype %d", c->dtype);
+  if (c->dtype == ASR_BF16) {
+    int H = c->H, W = c->W;
+    for (int s = 0; s < c->n_stages; ++s) {
+      if (s > 0 && c->stride[s]) H = (H + c->stride[s] - 1) / c->stride[s], W = (W + c->stride[s] - 1) / c->stride[s];
+      if (c->L[s] > 0 && !convb_supported(W, c->C[s]))
+        return fail(ASR_E_UNSUPPORTED, "asr_stages: bf16 stage %d needs C in {16, 32, 64} and W in {32, 16, 8} (C=%d W=%d)",
+                    s, c->C[s], W);
+      if (c->C[s] % 8) return fail(ASR_E_UNSUPPORTED, "asr_stages: bf16 stage %d: C=%d not a multiple of 8", s, c->C[s]);
+    }
+  }
   return ASR_OK;
 }
 
@@ -586,6 +609,8 @@ SLayout stages_layout(const asr_stages_config* c) {
   SLayout L{};
   L.ns = c->n_stages;
   L.sep_bwd = param_is_antisymmetric(c->param_kind, c->antisymmetric) == 0;
+  L.bf = c->dtype == ASR_BF16;
+  L.act_bytes = L.bf ? 2 : 4;
   size_t off = 0;
   auto take = [&](size_t bytes) {
     const size_t o = off;
@@ -632,7 +657,7 @@ SLayout stages_layout(const asr_stages_config* c) {
   po += c->num_classes;
   L.n_params = po;
   // workspace
-  L.act0 = take((size_t)c->N * c->H * c->W * c->C[0] * 4);
+  L.act0 = take((size_t)c->N * c->H * c->W * c->C[0] * L.act_bytes);
   L.cws_bytes = 0;
   L.tws_bytes = 0;
   for (int s = 0; s < L.ns; ++s) {
@@ -640,11 +665,14 @@ SLayout stages_layout(const asr_stages_config* c) {
     g.w_src = take((size_t)g.E * 4);
     g.theta_dst = take((size_t)g.ntheta * 2 * 4);
     g.w_src_bwd = L.sep_bwd ? take((size_t)g.E * 4) : 0;
-    g.wbuf = take((size_t)std::max(g.L, 1) * g.E * 4);
-    g.wbuf_bwd = L.sep_bwd ? take((size_t)std::max(g.L, 1) * g.E * 4) : 0;
+    g.wstride = L.bf ? asr_wpack_elems(g.C) : g.E;
+    g.wbuf = take((size_t)std::max(g.L, 1) * g.wstride * L.act_bytes);
+    g.wbuf_bwd = L.sep_bwd ? take((size_t)std::max(g.L, 1) * g.wstride * L.act_bytes) : 0;
     g.act_t = g.S ? take((size_t)g.P * 4) : 0;
+    g.act_tb = g.S && L.bf ? take((size_t)g.P * 2) : 0;
+    g.xin32 = g.S && L.bf ? take((size_t)c->N * g.Hp * g.Wp * g.Cp * 4) : 0;
     g.mask_t = g.S ? take((size_t)g.P) : 0;
-    g.acts = take((size_t)std::max(g.L, 1) * g.P * 4);
+    g.acts = take((size_t)std::max(g.L, 1) * g.P * L.act_bytes);
     g.masks = take((size_t)std::max(g.L, 1) * g.mask_bytes);
     // every block keeps its slabs until the stage's one reduction launch: sized by the
     // grid the fp32 weight gradient runs at this shape, not by the 512-row maximum
@@ -665,6 +693,8 @@ SLayout stages_layout(const asr_stages_config* c) {
   L.dB = take((size_t)L.Pmax * 4);
   L.cws = take(std::max<size_t>(L.cws_bytes, 256));
   L.tws = take(std::max<size_t>(L.tws_bytes, 256));
+  L.t32a = L.bf ? take((size_t)L.Pmax * 4) : 0;
+  L.t32b = L.bf ? take((size_t)L.Pmax * 4) : 0;
   const long E1 = 9L * c->Cin * c->C[0];
   L.sslabs = take((size_t)kMaxStemSlabs * (E1 + c->C[0]) * 4);
   L.sred_bytes = reduce_ws_bytes(kMaxStemSlabs, E1 + c->C[0]);
@@ -673,34 +703,47 @@ SLayout stages_layout(const asr_stages_config* c) {
   return L;
 }
 
-// forward through the stem and all stages; *xL = the last activation (fp32)
+// forward through the stem and all stages; *xL = the last activation (fp32, or bf16 for a bf16 net)
 int stages_forward_impl(const asr_stages_config* c, const SLayout& L, const float* params, const void* images,
-                        bool training, unsigned char* b, hipStream_t s, const float** xL) {
+                        bool training, unsigned char* b, hipStream_t s, const void** xL) {
   const float inv_std = c->use_norm ? 1.f / c->divide_by_stddev : 1.f;
+  const int wdt = L.bf ? ASR_BF16 : ASR_F32;
   ASR_TRY(stem_forward(images, c->input_u8, params + L.off_c1k, params + L.off_c1b, c->N, c->H, c->W, c->Cin,
-                       c->C[0], c->subtract_mean, inv_std, c->use_norm, b + L.act0, 0, s));
-  const float* x = (const float*)(b + L.act0);
+                       c->C[0], c->subtract_mean, inv_std, c->use_norm, b + L.act0, L.bf ? 1 : 0, s));
+  const void* x = b + L.act0;
   for (int si = 0; si < L.ns; ++si) {
     const StageL& g = L.st[si];
     if (g.S) {
       const float* pt = params + g.off_t;
       const long e2 = 9L * g.Cp * g.C;
-      ASR_TRY(trans_forward(x, (float*)(b + g.act_t), (uint8_t*)(b + g.mask_t), pt, pt + e2, pt + e2 + g.C,
+      const float* xt = (const float*)x;
+      if (L.bf) {  // the transition in fp32: its input converted (and kept for the backward), its output back to bf16
+        ASR_TRY(convert_bf16_f32(x, b + g.xin32, (long)c->N * g.Hp * g.Wp * g.Cp, 1, s));
+        xt = (const float*)(b + g.xin32);
+      }
+      ASR_TRY(trans_forward(xt, (float*)(b + g.act_t), (uint8_t*)(b + g.mask_t), pt, pt + e2, pt + e2 + g.C,
                             pt + e2 + g.C + (long)g.Cp * g.C, c->N, g.Hp, g.Wp, g.Cp, g.C, g.S, s));
-      x = (const float*)(b + g.act_t);
+      x = b + g.act_t;
+      if (L.bf) {
+        ASR_TRY(convert_bf16_f32(b + g.act_t, b + g.act_tb, g.P, 0, s));
+        x = b + g.act_tb;
+      }
     }
     if (g.L == 0) continue;
     ASR_TRY(asr_theta_to_w(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src), c->gamma,
-                           b + g.wbuf, g.E, ASR_F32, s));
+                           b + g.wbuf, g.wstride, wdt, s));
     if (training && L.sep_bwd)
       ASR_TRY(asr_theta_to_w(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src_bwd), 0.f,
-                             b + g.wbuf_bwd, g.E, ASR_F32, s));
+                             b + g.wbuf_bwd, g.wstride, wdt, s));
     for (int l = 0; l < g.L; ++l) {
-      float* y = (float*)(b + g.acts) + (size_t)l * g.P;
-      ASR_TRY(asr_conv_forward(ASR_MODE_EULER, x, y, (uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes,
-                               (const float*)(b + g.wbuf) + (size_t)l * g.E,
-                               params + g.off_blk + (long)l * g.blk_stride + g.ntheta, c->h, c->N, g.H, g.W, g.C,
-                               ASR_F32, s));
+      unsigned char* y = b + g.acts + (size_t)l * g.P * L.act_bytes;
+      uint8_t* mk = (uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes;
+      const unsigned char* wl = b + g.wbuf + (size_t)l * g.wstride * L.act_bytes;
+      const float* bl = params + g.off_blk + (long)l * g.blk_stride + g.ntheta;
+      if (L.bf)  // (every width on the any-width bf16 kernels: one slab-row count per stage)
+        ASR_TRY(convb_forward(x, y, mk, wl, bl, c->h, c->N, g.H, g.W, g.C, s));
+      else
+        ASR_TRY(asr_conv_forward(ASR_MODE_EULER, x, y, mk, wl, bl, c->h, c->N, g.H, g.W, g.C, ASR_F32, s));
       x = y;
     }
   }
@@ -736,6 +779,8 @@ int asr_transition_backward(const float* dy, const float* x, const uint8_t* mask
     return fail(ASR_E_WORKSPACE, "asr_transition_backward: workspace too small");
   return trans_backward(dy, x, mask, k2, k1, N, H, W, Ci, Co, stride, dx, dparams, (float*)ws, (hipStream_t)stream);
 }
+
+int asr_stages_check(const asr_stages_config* cfg) { return stages_check(cfg); }
 
 long asr_stages_param_count(const asr_stages_config* cfg) {
   if (stages_check(cfg) != ASR_OK) return -1;
@@ -776,11 +821,11 @@ int asr_stages_forward(const asr_stages_config* cfg, const float* params, const 
   if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_stages_forward: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   unsigned char* b = (unsigned char*)ws;
-  const float* xL = nullptr;
+  const void* xL = nullptr;
   ASR_TRY(stages_forward_impl(cfg, L, params, images, false, b, s, &xL));
   const StageL& g = L.st[L.ns - 1];
-  return head(xL, 0, params + L.off_fck, params + L.off_fcb, nullptr, cfg->N, g.H * g.W, g.C, cfg->num_classes, probs,
-              nullptr, nullptr, nullptr, nullptr, s);
+  return head(xL, L.bf ? 1 : 0, params + L.off_fck, params + L.off_fcb, nullptr, cfg->N, g.H * g.W, g.C,
+              cfg->num_classes, probs, nullptr, nullptr, nullptr, nullptr, s);
 }
 
 int asr_stages_forward_backward(const asr_stages_config* cfg, const float* params, const void* images,
@@ -793,12 +838,14 @@ int asr_stages_forward_backward(const asr_stages_config* cfg, const float* param
   hipStream_t s = (hipStream_t)stream;
   unsigned char* b = (unsigned char*)ws;
   const int N = cfg->N, K = cfg->num_classes;
-  const float* xL = nullptr;
+  const size_t ab = L.act_bytes;
+  const void* xL = nullptr;
   ASR_TRY(stages_forward_impl(cfg, L, params, images, true, b, s, &xL));
-  float* d = (float*)(b + L.dA);
-  float* e = (float*)(b + L.dB);
+  // the chain gradient ping-pongs between dA and dB (bf16 nets: bf16 through the blocks)
+  unsigned char* d = b + L.dA;
+  unsigned char* e = b + L.dB;
   const StageL& top = L.st[L.ns - 1];
-  ASR_TRY(head(xL, 0, params + L.off_fck, params + L.off_fcb, targets, N, top.H * top.W, top.C, K,
+  ASR_TRY(head(xL, L.bf ? 1 : 0, params + L.off_fck, params + L.off_fcb, targets, N, top.H * top.W, top.C, K,
                probs ? probs : (float*)(b + L.probs), (float*)(b + L.loss_per), (float*)(b + L.dlogits),
                (float*)(b + L.gap), d, s));
   ASR_TRY(head_param_grads((const float*)(b + L.gap), (const float*)(b + L.dlogits), N, top.C, K, grads + L.off_fck,
@@ -806,23 +853,27 @@ int asr_stages_forward_backward(const asr_stages_config* cfg, const float* param
   for (int si = L.ns - 1; si >= 0; --si) {
     const StageL& g = L.st[si];
     // the stage's chain input: its transition's output, else the previous stage's last activation
-    const float* prev_out = (const float*)(b + L.act0);
+    // (in the net's activation type; a bf16 net's transition input is also kept in fp32, xin32)
+    const unsigned char* prev_out = b + L.act0;
     for (int sp = si - 1; sp >= 0; --sp) {
       const StageL& q = L.st[sp];
-      if (q.L > 0) { prev_out = (const float*)(b + q.acts) + (size_t)(q.L - 1) * q.P; break; }
-      if (q.S) { prev_out = (const float*)(b + q.act_t); break; }
+      if (q.L > 0) { prev_out = b + q.acts + (size_t)(q.L - 1) * q.P * ab; break; }
+      if (q.S) { prev_out = b + (L.bf ? q.act_tb : q.act_t); break; }
     }
-    const float* chain_in = g.S ? (const float*)(b + g.act_t) : prev_out;
+    const unsigned char* chain_in = g.S ? b + (L.bf ? g.act_tb : g.act_t) : prev_out;
     const float gam = L.sep_bwd ? 0.f : cfg->gamma;
     int nsl = 0;
     for (int l = g.L - 1; l >= 0; --l) {
-      const float* x_in = l == 0 ? chain_in : (const float*)(b + g.acts) + (size_t)(l - 1) * g.P;
-      const unsigned char* wl = b + (L.sep_bwd ? g.wbuf_bwd : g.wbuf) + (size_t)l * g.E * 4;
+      const unsigned char* x_in = l == 0 ? chain_in : b + g.acts + (size_t)(l - 1) * g.P * ab;
+      const unsigned char* wl = b + (L.sep_bwd ? g.wbuf_bwd : g.wbuf) + (size_t)l * g.wstride * ab;
+      const uint8_t* mk = (const uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes;
+      float* sl = (float*)(b + g.slabs) + (size_t)l * g.slab_stride;
       // the block's weight-gradient slabs stay in its own slot: the stage's blocks are reduced
       // (pass 1, one launch) and projected (pass 2 + projection, one launch) after the loop
-      ASR_TRY(conv_backward_keep_slabs(d, x_in, (const uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes, wl, cfg->h, gam,
-                                       N, g.H, g.W, g.C, e, b + L.cws, (float*)(b + g.slabs) + (size_t)l * g.slab_stride,
-                                       &nsl, s));
+      if (L.bf)
+        ASR_TRY(convb_backward(d, mk, x_in, wl, cfg->h, 2.f * gam, N, g.H, g.W, g.C, e, true, sl, &nsl, s));
+      else
+        ASR_TRY(conv_backward_keep_slabs(d, x_in, mk, wl, cfg->h, gam, N, g.H, g.W, g.C, e, b + L.cws, sl, &nsl, s));
       if (nsl > g.slab_rows)  // (the device differs from the one the workspace was sized on)
         return fail(ASR_E_WORKSPACE, "asr_stages: %d slab rows > the workspace's %d (sized on another device?)", nsl,
                     g.slab_rows);
@@ -837,15 +888,26 @@ int asr_stages_forward_backward(const asr_stages_config* cfg, const float* param
     if (g.S) {
       const float* pt = params + g.off_t;
       const long e2 = 9L * g.Cp * g.C;
-      ASR_TRY(trans_backward(d, prev_out, (const uint8_t*)(b + g.mask_t), pt, pt + e2 + g.C, N, g.Hp, g.Wp, g.Cp, g.C,
-                             g.S, e, grads + g.off_t, (float*)(b + L.tws), s));
+      const long Pin = (long)N * g.Hp * g.Wp * g.Cp;
+      if (L.bf) {  // in fp32: dy converted up, the transition's kept fp32 input, dx converted back down
+        float* dy32 = (float*)(b + L.t32a);
+        float* dx32 = (float*)(b + L.t32b);
+        ASR_TRY(convert_bf16_f32(d, dy32, g.P, 1, s));
+        ASR_TRY(trans_backward(dy32, (const float*)(b + g.xin32), (const uint8_t*)(b + g.mask_t), pt, pt + e2 + g.C,
+                               N, g.Hp, g.Wp, g.Cp, g.C, g.S, dx32, grads + g.off_t, (float*)(b + L.tws), s));
+        ASR_TRY(convert_bf16_f32(dx32, e, Pin, 0, s));
+      } else {
+        ASR_TRY(trans_backward((const float*)d, (const float*)prev_out, (const uint8_t*)(b + g.mask_t), pt,
+                               pt + e2 + g.C, N, g.Hp, g.Wp, g.Cp, g.C, g.S, (float*)e, grads + g.off_t,
+                               (float*)(b + L.tws), s));
+      }
       std::swap(d, e);
     }
   }
   // stem: dz1 = dx1 [x1 > 0] inside stem_wgrad; conv1 kernel / bias gradients
   const float inv_std = cfg->use_norm ? 1.f / cfg->divide_by_stddev : 1.f;
   int nsl = 0;
-  ASR_TRY(stem_wgrad(images, cfg->input_u8, d, b + L.act0, 0, N, cfg->H, cfg->W, cfg->Cin, cfg->C[0],
+  ASR_TRY(stem_wgrad(images, cfg->input_u8, d, b + L.act0, L.bf ? 1 : 0, N, cfg->H, cfg->W, cfg->Cin, cfg->C[0],
                      cfg->subtract_mean, inv_std, cfg->use_norm, (float*)(b + L.sslabs), &nsl, s));
   if (nsl > kMaxStemSlabs) return fail(ASR_E_UNSUPPORTED, "asr_stages: stem slabs %d > %d", nsl, kMaxStemSlabs);
   return reduce_and_project((const float*)(b + L.sslabs), nsl, 9L * cfg->Cin * cfg->C[0], cfg->C[0], nullptr, 0,

@@ -314,7 +314,7 @@ using namespace asr;
 extern "C" {
 
 const char* asr_last_error(void) { return g_err; }
-int asr_abi_version(void) { return 7; }
+int asr_abi_version(void) { return 8; }
 
 int asr_device_cu_count(void) { return cu_count(); }
 

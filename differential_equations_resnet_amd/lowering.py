@@ -113,6 +113,19 @@ class StagesPlan:
     def C(self):
         return self.stages[-1][0]
 
+    def stages_bf16_ok(self):
+        """Whether the bf16 block kernels take every stage with blocks (C in
+        {16, 32, 64}, W in {32, 16, 8}; asr_stages_config.dtype)."""
+        W = self.W
+        for C, L, S in self.stages:
+            if S:
+                W = (W + S - 1) // S
+            if L > 0 and (C not in (16, 32, 64) or W not in (32, 16, 8)):
+                return False
+            if C % 8:
+                return False
+        return True
+
     def weight_vars(self):
         """Variables in the executor's flat order (asr_stages_config)."""
         out = [self.conv1.kernel, self.conv1.bias]
@@ -353,14 +366,20 @@ class NativeModel:
 
     def resolve_dtype(self, dtype):
         """The activation dtype an executor of this model runs in.  None: the
-        plan's own (bfloat16 single-stage, float32 multi-stage).  A multi-stage
-        net always runs in float32 (its block kernels at 16x16 / 8x8 are fp32
-        only): an explicit bfloat16 request is warned about once and mapped to
-        float32, so train and predict views share one executor per batch size."""
+        plan's own (bfloat16 single-stage, float32 multi-stage: the reference's
+        precision).  A multi-stage net runs in bfloat16 when asked and every
+        stage with blocks is on the bf16 kernels' shapes (stages_bf16_ok);
+        otherwise the request is warned about once and mapped to float32, so
+        train and predict views share one executor per batch size."""
         if isinstance(self.plan, StagesPlan):
-            if dtype not in (None, "float32") and not self._warned_stages_dtype:
-                warnings.warn(f"multi-stage nets run in float32 on the native executor (dtype={dtype!r} requested)",
-                              stacklevel=3)
+            if dtype in (None, "float32"):
+                return "float32"
+            if dtype == "bfloat16" and self.plan.stages_bf16_ok():
+                return "bfloat16"
+            if not self._warned_stages_dtype:
+                warnings.warn(f"this multi-stage net runs in float32 on the native executor (dtype={dtype!r} "
+                              "requested: bf16 needs C in {16, 32, 64} and W in {32, 16, 8} at every stage with "
+                              "blocks)", stacklevel=3)
                 self._warned_stages_dtype = True
             return "float32"
         return "bfloat16" if dtype is None else dtype
@@ -404,11 +423,10 @@ class NativeModel:
         key = (int(batch_size), dtype, bool(input_u8), bool(inference))
         ex = self._executors.get(key)
         if ex is None and isinstance(self.plan, StagesPlan):
-            # fp32 whatever dtype is asked: the multi-stage executor has the reference's precision only
             p = self.plan
             ex = self._rt.StagesExecutor(int(batch_size), p.H, p.W, p.Cin, p.stages, p.num_classes, p.h, p.gamma,
                                          subtract_mean=p.subtract_mean, divide_by_stddev=p.divide_by_stddev,
-                                         dtype="float32", input_u8=input_u8, device=self.device,
+                                         dtype=dtype, input_u8=input_u8, device=self.device,
                                          param_kind=p.param_kind, antisymmetric=p.antisymmetric, inference=inference)
             if ex.n_params != self.n_params:
                 raise _lib.AsrError(f"executor expects {ex.n_params} parameters, model has {self.n_params}")

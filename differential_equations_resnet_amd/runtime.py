@@ -499,16 +499,17 @@ def transition_backward(dy, x, mask, k2, k1, stride: int, want_dx=True, want_dpa
 class StagesExecutor:
     """Native executor of the multi-stage single-block ResNet (asr_stages_*
     in include/asr.h): stem, per stage an optional transition
-    (single_layer_conv_block) and its identity Euler blocks, head.  fp32 (the
-    reference's precision).  Parameters / gradients are flat float32 buffers
-    in the asr_stages_config order; same call surface as NetExecutor."""
+    (single_layer_conv_block) and its identity Euler blocks, head.  float32
+    (the reference's precision) or bfloat16 (the identity blocks' activations
+    and convs in bf16 with fp32 accumulation; stem, transitions, head and every
+    weight gradient in fp32; stages with blocks need C in {16, 32, 64} and
+    W in {32, 16, 8}).  Parameters / gradients are flat float32 buffers in the
+    asr_stages_config order; same call surface as NetExecutor."""
 
     def __init__(self, N, H, W, Cin, stages, num_classes, h, gamma=0.0, subtract_mean=None, divide_by_stddev=None,
                  dtype="float32", input_u8=True, device=None, param_kind=ASR_PARAM_3BY3, antisymmetric=True,
                  inference=False):
         """stages: [(C, L, stride)] per stage, stride 0 for no transition."""
-        if dtype_code(dtype) != ASR_F32:
-            raise _lib.AsrUnsupported("the multi-stage executor computes in float32 (the reference's precision)")
         if not 1 <= len(stages) <= _lib.ASR_STAGES_MAX:
             raise _lib.AsrUnsupported(f"{len(stages)} stages (1..{_lib.ASR_STAGES_MAX})")
         self.device = device or require_gpu()
@@ -522,9 +523,12 @@ class StagesExecutor:
         c.divide_by_stddev = float(divide_by_stddev if divide_by_stddev is not None else 1.0)
         c.use_norm, c.input_u8 = int(use_norm), int(bool(input_u8))
         c.param_kind, c.antisymmetric = int(param_kind), int(bool(antisymmetric))
+        c.dtype = dtype_code(dtype)
         self.cfg = c
+        self.dtype = dtype
         self.stages = [tuple(int(v) for v in st) for st in stages]
         lib = _lib.load()
+        _lib.call("asr_stages_check", ct.byref(c))
         self.n_params = int(lib.asr_stages_param_count(ct.byref(c)))
         if self.n_params < 0:
             _lib.check(_lib.ASR_E_ARG, "asr_stages_param_count")

@@ -401,11 +401,19 @@ typedef struct asr_stages_config {
   float h, gamma;
   float subtract_mean, divide_by_stddev; /* applied when use_norm != 0 */
   int use_norm, input_u8, param_kind, antisymmetric;
+  int dtype;                  /* ABI 8: ASR_F32 (0) or ASR_BF16: the identity blocks'
+                                 activations and convs (bf16 MFMA, fp32 accumulation
+                                 and weight gradients); the transitions compute in fp32 */
 } asr_stages_config;
 /* params / grads (float32): conv1 kernel [3,3,Cin,C0], bias [C0]; per stage s:
  * the transition (if any) K2 [3,3,C[s-1],C[s]], b2, K1 [1,1,C[s-1],C[s]], b1,
  * then L[s] x (theta [asr_theta_count(C[s], param_kind, antisymmetric)], bias
  * [C[s]]); fc kernel [C_last, K], bias [K]. */
+/* ASR_OK, or the code (and asr_last_error) the calls below fail with for this
+ * config: ASR_E_ARG for a malformed one, ASR_E_UNSUPPORTED for a shape the
+ * kernels do not take (e.g. a bf16 stage outside C {16,32,64} x W {32,16,8}).
+ * ABI 8.  Host only. */
+int asr_stages_check(const asr_stages_config* cfg);
 long asr_stages_param_count(const asr_stages_config* cfg);
 size_t asr_stages_workspace_bytes(const asr_stages_config* cfg);
 int asr_stages_prepare(const asr_stages_config* cfg, void* ws, size_t ws_bytes);

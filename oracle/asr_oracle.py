@@ -753,11 +753,16 @@ def _block_W(spec: StagesSpec, C, theta):
     return assemble_from_map(flatten(theta), C, src, sign, spec.gamma)
 
 
-def stages_forward(spec: StagesSpec, params, images, dtype=np.float64):
+def stages_forward(spec: StagesSpec, params, images, dtype=np.float64, rnd=None):
+    """rnd (optional): a rounding applied where a bf16 net (asr_stages_config
+    dtype ASR_BF16) stores in bf16 -- the stem's output, every transition's and
+    block's output, the blocks' assembled W -- so the restatement follows the
+    bf16 executor's storage; everything else stays in `dtype`."""
+    r = rnd if rnd is not None else (lambda a: a)
     ns = NetSpec(subtract_mean=spec.subtract_mean, divide_by_stddev=spec.divide_by_stddev)
     x0 = normalize_input(images, ns, dtype)
     z1 = conv2d_same(x0, params[0]) + params[1]
-    x = np.maximum(z1, 0)
+    x = r(np.maximum(z1, 0))
     i = 2
     ops = []  # per op: ("t", x_in, z, K2, K1, S) or ("b", x_in, z, W, C)
     for C, L, S in spec.stages:
@@ -766,35 +771,39 @@ def stages_forward(spec: StagesSpec, params, images, dtype=np.float64):
             i += 4
             y, z = transition_fwd(x, K2, b2, K1, b1, S)
             ops.append(("t", x, z, K2, K1, S))
-            x = y
+            x = r(y)
         nt = len(spec.block_spec(C).theta_shapes())
         for _ in range(L):
             theta, b = params[i:i + nt], params[i + nt]
             i += nt + 1
-            W = _block_W(spec, C, theta)
+            W = r(_block_W(spec, C, theta))
             y, z = euler_fwd(x, W, b, spec.h)
             ops.append(("b", x, z, W, C))
-            x = y
+            x = r(y)
     fc_k, fc_b = params[i], params[i + 1]
     gap = x.mean(axis=(1, 2))
     probs = softmax(gap @ fc_k + fc_b)
-    return probs, dict(x0=x0, z1=z1, ops=ops, xL=x, gap=gap, probs=probs, fc_k=fc_k)
+    return probs, dict(x0=x0, z1=z1, ops=ops, xL=x, gap=gap, probs=probs, fc_k=fc_k, rnd=rnd)
 
 
 def stages_backward(spec: StagesSpec, params, cache, onehot):
-    """Gradients of the mean Keras CE loss, in StagesSpec.param_shapes order."""
+    """Gradients of the mean Keras CE loss, in StagesSpec.param_shapes order
+    (with the forward's rnd applied to the chain gradient where the bf16
+    executor stores it: after the head, every block and every transition)."""
+    r = cache.get("rnd") or (lambda a: a)
     Nb = onehot.shape[0]
     dlogits = keras_cce_grad_logits(cache["probs"], onehot, 1.0 / Nb)
     d_fck = cache["gap"].T @ dlogits
     d_fcb = dlogits.sum(axis=0)
     xL = cache["xL"]
-    dx = np.broadcast_to((dlogits @ cache["fc_k"].T)[:, None, None, :] / (xL.shape[1] * xL.shape[2]),
-                         xL.shape).copy()
+    dx = r(np.broadcast_to((dlogits @ cache["fc_k"].T)[:, None, None, :] / (xL.shape[1] * xL.shape[2]),
+                           xL.shape).copy())
     back = []
     for op in reversed(cache["ops"]):
         if op[0] == "t":
             _, x_in, z, K2, K1, S = op
             dx, g = transition_bwd(dx, x_in, z, K2, K1, S)
+            dx = r(dx)
             back.append(g)
         else:
             _, x_in, z, W, C = op
@@ -803,6 +812,7 @@ def stages_backward(spec: StagesSpec, params, cache, onehot):
                 dx, dW, db = euler_bwd(dx, x_in, z, W, spec.h, spec.gamma)
             else:
                 dx, dW, db = euler_bwd_generic(dx, x_in, z, W, spec.h)
+            dx = r(dx)
             shapes = bs.theta_shapes()
             src, sign = _cached_map(C, spec.kind, spec.antisymmetric)
             ntheta = int(sum(np.prod(x) for x in shapes))

@@ -185,7 +185,20 @@ def test_analyze_multistage_plan():
     lib = _lib.load()
     assert lib.asr_stages_param_count(ct.byref(c)) == spec.n_params()
     assert lib.asr_stages_workspace_bytes(ct.byref(c)) > 0
+    assert lib.asr_stages_check(ct.byref(c)) == _lib.ASR_OK
+    c.dtype = _lib.ASR_BF16  # bf16: every stage with blocks on C {16,32,64} x W {32,16,8}
+    assert lib.asr_stages_check(ct.byref(c)) == _lib.ASR_OK
+    assert lib.asr_stages_param_count(ct.byref(c)) == spec.n_params()
+    bf_ws = lib.asr_stages_workspace_bytes(ct.byref(c))
+    c.dtype = _lib.ASR_F32
+    assert 0 < bf_ws < lib.asr_stages_workspace_bytes(ct.byref(c))  # bf16 activations: a smaller workspace
+    c.dtype = 7
+    assert lib.asr_stages_check(ct.byref(c)) == _lib.ASR_E_ARG
+    c.dtype, c.W = _lib.ASR_BF16, 16  # the last stage at W = 4
+    assert lib.asr_stages_check(ct.byref(c)) == _lib.ASR_E_UNSUPPORTED and b"W=4" in lib.asr_last_error()
+    c.dtype, c.W = _lib.ASR_F32, 32
     c.stride[0] = 2
+    assert lib.asr_stages_check(ct.byref(c)) == _lib.ASR_E_ARG
     assert lib.asr_stages_param_count(ct.byref(c)) == -1
     # RK2 identity blocks are single-stage only
     fn = R.get_single_block_resnet_build_function(num_stages=3, blocks_per_stage=[2, 2], filters_per_block=[8, 16],

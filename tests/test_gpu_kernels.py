@@ -78,17 +78,26 @@ def _oracle_W(th, C, gamma, bf):
 
 
 SHAPES_BF16 = [(2, 32, 32, 16), (2, 32, 32, 32), (2, 32, 32, 64), (1, 11, 32, 64), (3, 5, 32, 16)]
+# bf16 Euler blocks at the multi-stage nets' widths (k_convb + k_wgrad32<bf16>, round 5; Euler mode only)
+SHAPES_BF16_W = [(2, 16, 16, 32), (3, 7, 16, 16), (2, 8, 8, 64), (2, 5, 8, 16), (1, 9, 8, 32), (2, 16, 16, 64),
+                 (2, 32, 32, 64)]
 SHAPES_F32 = [(2, 32, 32, 16), (1, 7, 13, 5), (2, 9, 32, 64), (1, 3, 3, 1), (2, 32, 32, 32), (3, 6, 32, 16),
               # the multi-stage nets' 16x16 / 8x8 stages on the same fp32 MFMA kernels (odd H: partial bands)
               (2, 16, 16, 32), (3, 7, 16, 16), (2, 8, 8, 64), (2, 5, 8, 16), (1, 9, 8, 32)]
 
 
-@pytest.mark.parametrize("dtype_name,shape", [("f32", s) for s in SHAPES_F32] + [("bf16", s) for s in SHAPES_BF16])
+@pytest.mark.parametrize("dtype_name,shape", [("f32", s) for s in SHAPES_F32] + [("bf16", s) for s in SHAPES_BF16]
+                         + [("bf16w", s) for s in SHAPES_BF16_W])
 @pytest.mark.parametrize("mode_name", ["euler", "conv"])
 @pytest.mark.parametrize("gamma,h", [(0.0, 0.25), (-0.1, 1.0)])
 def test_forward_parity(rt, dtype_name, shape, mode_name, gamma, h):
     N, H, W_, C = shape
-    bf = dtype_name == "bf16"
+    if dtype_name == "bf16w":
+        if mode_name != "euler":
+            pytest.skip("the any-width bf16 kernels run Euler blocks only")
+        if W_ == 32:
+            pytest.skip("W = 32 runs the C=16/32/64 band kernels (SHAPES_BF16); k_convb at W = 32 via the stages")
+    bf = dtype_name.startswith("bf16")
     dtype = rt.ASR_BF16 if bf else rt.ASR_F32
     mode = rt.ASR_MODE_EULER if mode_name == "euler" else rt.ASR_MODE_CONV
     rng = np.random.default_rng(hash((shape, mode_name, gamma)) % 2**32)
@@ -115,12 +124,18 @@ def test_forward_parity(rt, dtype_name, shape, mode_name, gamma, h):
         assert np.array_equal(m[sure], (z > 0)[sure]), "relu mask mismatch"
 
 
-@pytest.mark.parametrize("dtype_name,shape", [("f32", s) for s in SHAPES_F32] + [("bf16", s) for s in SHAPES_BF16])
+@pytest.mark.parametrize("dtype_name,shape", [("f32", s) for s in SHAPES_F32] + [("bf16", s) for s in SHAPES_BF16]
+                         + [("bf16w", s) for s in SHAPES_BF16_W])
 @pytest.mark.parametrize("mode_name", ["euler", "conv"])
 @pytest.mark.parametrize("gamma,h", [(0.0, 0.25), (-0.1, 1.0)])
 def test_backward_parity(rt, dtype_name, shape, mode_name, gamma, h):
     N, H, W_, C = shape
-    bf = dtype_name == "bf16"
+    if dtype_name == "bf16w":
+        if mode_name != "euler":
+            pytest.skip("the any-width bf16 kernels run Euler blocks only")
+        if W_ == 32:
+            pytest.skip("W = 32 runs the C=16/32/64 band kernels (SHAPES_BF16); k_convb at W = 32 via the stages")
+    bf = dtype_name.startswith("bf16")
     dtype = rt.ASR_BF16 if bf else rt.ASR_F32
     mode = rt.ASR_MODE_EULER if mode_name == "euler" else rt.ASR_MODE_CONV
     rng = np.random.default_rng(hash((shape, mode_name, gamma, 1)) % 2**32)

@@ -11,11 +11,16 @@ pre-activations within 1e-5 of 0 excepted); network probabilities within
 1e-5 relative, loss within 1e-5 relative, every gradient within 1e-4 of
 its tensor's max |oracle| value (the single-stage fp32 bar,
 test_gpu_network.py).
+
+bf16 nets (asr_stages_config.dtype = ASR_BF16: the identity blocks in bf16,
+fp32 accumulation; stem, transitions, head and weight gradients in fp32):
+see _assert_bf16_net -- a tight bar against the oracle with the executor's
+bf16 storage rounding, and the bf16 network bar against the plain oracle.
 """
 import numpy as np
 import pytest
 
-from helpers import assert_close
+from helpers import assert_close, bf16_round, rel_l2
 from oracle import asr_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -99,6 +104,16 @@ def test_stages_network_vs_oracle(stages, kind, anti, gamma):
     _check_net(ex, spec, params, imgs, onehot)
 
 
+def _unsaturate(nv):
+    """The he_normal-initialised 28-block net's logits reach the hundreds: the
+    softmax saturates, Keras' probability clip zeroes every gradient and the
+    comparison would be vacuous.  A smaller fc kernel (as _stages_setup)
+    keeps the logits O(1)."""
+    fc = nv.state.plan.fc.kernel
+    fc.assign(fc.value * 1e-3)
+    nv.state.push_weights()
+
+
 def test_resnet32_he_model_lowers_and_matches_oracle():
     """The He-style ResNet-32 as the reference builds it (num_stages=4, blocks
     [10,10,10] at 32^2 x 16, 16^2 x 32, 8^2 x 64, tfkeras_resnets.py:575-593),
@@ -115,6 +130,7 @@ def test_resnet32_he_model_lowers_and_matches_oracle():
     m = fn(Input(shape=(32, 32, 3)))
     nv = m.compile_native(6)
     assert isinstance(nv.state.plan, StagesPlan) and nv.state.plan.stages == [(16, 10, 0), (32, 9, 2), (64, 9, 2)]
+    _unsaturate(nv)
     spec = O.StagesSpec(stages=nv.state.plan.stages, h=0.5)
     params = [v.value.astype(np.float64) for v in nv.state.plan.weight_vars()]
     rng = np.random.default_rng(5)
@@ -125,6 +141,7 @@ def test_resnet32_he_model_lowers_and_matches_oracle():
     assert_close(probs.cpu().numpy(), p_want, rtol=1e-5, atol=1e-6, what="probs")
     assert abs(loss.item() - O.net_loss(p_want, onehot)) <= 1e-5 * O.net_loss(p_want, onehot)
     g_want = O.stages_backward(spec, params, cache, onehot)
+    assert all(np.abs(g).max() > 0 for g in g_want[:2])  # the stem's gradient reaches through all 28 blocks
     g_got = O.unflatten(grads.cpu().numpy().astype(np.float64), [p.shape for p in params])
     for i, (a, b) in enumerate(zip(g_got, g_want)):
         assert_close(a, b, rtol=0, atol=1e-4 * max(np.abs(b).max(), 1e-12), what=f"grad[{i}] {b.shape}")
@@ -175,3 +192,114 @@ def test_training_multistage_overfits_one_batch(tmp_path):
     tr.train(epochs=1, steps_per_epoch=2, learning_rate_schedule=lambda s: 1e-3, summaries_frequency=1)
     rows = list(csv.reader(open(tmp_path / "run_gradient_history.csv"), delimiter=" "))
     assert rows[0][3] == "conv1_kernel_gradient_mean_norm" and "res4_1_branch2_kernel_gradient_mean_norm" in rows[0]
+
+
+def _stage_groups(spec, g):
+    """(name, flat array) per layer: conv1 kernel + bias, each transition's
+    four tensors, each block's theta variables + bias, fc kernel + bias --
+    the per-layer groups of the reference's gradient norms
+    (training.py:385-409)."""
+    out = [("conv1", np.concatenate([np.ravel(g[0]), np.ravel(g[1])]))]
+    i = 2
+    for si, (C, L, S) in enumerate(spec.stages):
+        if S:
+            out.append((f"stage{si}/transition", np.concatenate([np.ravel(a) for a in g[i:i + 4]])))
+            i += 4
+        nt = len(spec.block_spec(C).theta_shapes())
+        for b in range(L):
+            out.append((f"stage{si}/block{b}", np.concatenate([np.ravel(a) for a in g[i:i + nt + 1]])))
+            i += nt + 1
+    out.append(("fc", np.concatenate([np.ravel(g[i]), np.ravel(g[i + 1])])))
+    return out
+
+
+def _bf16_net_errors(ex, spec, params, imgs, onehot, rnd=None):
+    """(max |probs - oracle|, |loss - oracle| / oracle, {layer: grad rel-L2})
+    of the bf16 executor vs the fp64 oracle (rnd: the oracle's bf16 storage
+    rounding, O.stages_forward)."""
+    flat = _t(O.flatten(params))
+    assert flat.numel() == ex.n_params == spec.n_params()
+    probs_gpu = ex.forward(flat, torch.from_numpy(imgs).cuda()).cpu().numpy()
+    probs, cache = O.stages_forward(spec, params, imgs, rnd=rnd)
+    loss, grads = ex.forward_backward(flat, torch.from_numpy(imgs).cuda(), _t(onehot), want_probs=True)
+    assert np.array_equal(ex.probs.cpu().numpy(), probs_gpu)  # the training call's forward is the same kernels
+    want_loss = O.net_loss(probs, onehot)
+    g_want = O.stages_backward(spec, params, cache, onehot)
+    assert np.abs(g_want[0]).max() > 0  # not saturated: the stem's gradient is live
+    g_got = O.unflatten(grads.cpu().numpy().astype(np.float64), [p.shape for p in params])
+    errs = {name: rel_l2(a, b) for (name, a), (_, b) in zip(_stage_groups(spec, g_got), _stage_groups(spec, g_want))}
+    return float(np.abs(probs_gpu - probs).max()), abs(loss.item() - want_loss) / abs(want_loss), errs
+
+
+def _assert_bf16_net(ex, spec, params, imgs, onehot):
+    """Two bars.  (1) Against the oracle with the executor's bf16 storage
+    rounding (helpers.bf16_round at every stored activation, chain gradient
+    and block W): what remains is fp32 accumulation order and the bf16
+    roundings it flips -- probabilities within 2e-3, loss within 1e-3
+    relative, every layer's gradient within 1e-2 relative L2.  (2) Against
+    the plain fp64 oracle (the reference's math) at the single-stage bf16
+    network bar: probabilities within 2e-2, loss within 1e-2 relative, every
+    layer's gradient within 5e-2 relative L2."""
+    dp, dl, errs = _bf16_net_errors(ex, spec, params, imgs, onehot, rnd=bf16_round)
+    print(f"\nbf16-storage oracle: probs {dp:.2e} loss {dl:.2e} worst grad {max(errs.values()):.2e} "
+          f"({max(errs, key=errs.get)})")
+    assert dp < 2e-3 and dl < 1e-3, (dp, dl)
+    bad = {k: v for k, v in errs.items() if not v <= 1e-2}
+    assert not bad, bad
+    dp, dl, errs = _bf16_net_errors(ex, spec, params, imgs, onehot)
+    print(f"fp64 oracle: probs {dp:.2e} loss {dl:.2e} worst grad {max(errs.values()):.2e} ({max(errs, key=errs.get)})")
+    assert dp < 2e-2 and dl < 1e-2, (dp, dl)
+    bad = {k: v for k, v in errs.items() if not v <= 5e-2}
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("stages,kind,anti,gamma", [
+    ([(16, 2, 0), (32, 2, 2), (64, 2, 2)], "3by3", True, 0.0),     # He-style ResNet-32 layout, 2 blocks per stage
+    ([(16, 2, 0), (32, 2, 2), (64, 2, 2)], "3by3", True, -0.05),
+    ([(16, 1, 0), (32, 1, 2), (32, 1, 0), (64, 0, 2)], "regular", False, 0.0),  # no-transition stage, empty stage
+    ([(32, 1, 0), (64, 2, 2), (64, 1, 2)], "general", False, 0.0),  # W = 32 / 16 / 8 at C = 64
+])
+def test_stages_network_bf16_vs_oracle(stages, kind, anti, gamma):
+    from differential_equations_resnet_amd.runtime import StagesExecutor
+    spec, params, imgs, onehot = _stages_setup(stages, kind, anti, h=0.25, gamma=gamma, N=8)
+    ex = StagesExecutor(imgs.shape[0], spec.H, spec.W, 3, stages, 10, spec.h, spec.gamma, subtract_mean=127.5,
+                        divide_by_stddev=127.5, input_u8=True, param_kind=KINDS[kind], antisymmetric=anti,
+                        dtype="bfloat16")
+    _assert_bf16_net(ex, spec, params, imgs, onehot)
+
+
+def test_stages_bf16_unsupported_width_raises():
+    from differential_equations_resnet_amd import _lib
+    from differential_equations_resnet_amd.runtime import StagesExecutor
+    with pytest.raises(_lib.AsrUnsupported, match="W=4"):  # W = 4 after two stride-2 transitions of a 16x16 input
+        StagesExecutor(2, 16, 16, 3, [(16, 1, 0), (32, 1, 2), (64, 1, 2)], 10, 0.5, dtype="bfloat16")
+
+
+def test_resnet32_he_model_bf16_matches_oracle():
+    """The He-style ResNet-32 (tfkeras_resnets.py:575-593, blocks [10,10,10])
+    through the drop-in Model API in bf16 (compile_native(dtype="bfloat16")),
+    at the bf16 network bar."""
+    from differential_equations_resnet_amd import graph
+    from differential_equations_resnet_amd.graph import Input
+    from differential_equations_resnet_amd.models import tfkeras_resnets as R
+    graph.set_seed(3)
+    fn = R.get_single_block_resnet_build_function(kernel_type="antisymmetric", h=0.5, num_stages=4,
+                                                  blocks_per_stage=[10, 10, 10], filters_per_block=[16, 32, 64],
+                                                  strides=[(1, 1), (2, 2), (2, 2)], subtract_mean=127.5,
+                                                  divide_by_stddev=127.5, num_classes=10)
+    m = fn(Input(shape=(32, 32, 3)))
+    nv = m.compile_native(8, dtype="bfloat16")
+    assert nv.dtype == "bfloat16"
+    _unsaturate(nv)
+    spec = O.StagesSpec(stages=nv.state.plan.stages, h=0.5)
+    params = [v.value.astype(np.float64) for v in nv.state.plan.weight_vars()]
+    rng = np.random.default_rng(5)
+    imgs = rng.integers(0, 256, (8, 32, 32, 3)).astype(np.uint8)
+    onehot = np.eye(10)[rng.integers(0, 10, 8)]
+    ex = nv.state.executor(8, "bfloat16", True)
+    assert ex.dtype == "bfloat16"
+    _assert_bf16_net(ex, spec, params, imgs, onehot)
+    # the Model API's own call runs the same executor
+    loss, grads, probs = nv.forward_backward(imgs, onehot.astype(np.float32), want_probs=True)
+    p_want, _ = O.stages_forward(spec, params, imgs)
+    assert np.abs(probs.cpu().numpy() - p_want).max() < 2e-2

@@ -24,10 +24,10 @@ def main():
     a = ap.parse_args()
     dev = rt.require_gpu()
     if a.config in bench.STAGE_CONFIGS:
-        stages, N, _ = bench.STAGE_CONFIGS[a.config]
+        stages, N, dt, _ = bench.STAGE_CONFIGS[a.config]
         L = sum(l for _, l, _ in stages)
         ex = rt.StagesExecutor(N, 32, 32, 3, stages, 10, 8.0 / L, 0.0, subtract_mean=127.5, divide_by_stddev=127.5,
-                               input_u8=True, device=dev)
+                               input_u8=True, device=dev, dtype=dt)
         params = torch.from_numpy(bench.stages_params(stages)).to(dev)
     else:
         C, L, N, dtype, _, integ, _ = bench.CONFIGS[a.config]
