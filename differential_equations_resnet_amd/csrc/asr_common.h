@@ -119,4 +119,11 @@ __device__ __forceinline__ void mfma_f32_settle() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// the same for a v_mfma_f32_16x16x32_bf16 result (8 wait states)
+__device__ __forceinline__ void mfma_bf16_settle() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 }  // namespace asr

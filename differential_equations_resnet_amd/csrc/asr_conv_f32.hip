@@ -712,67 +712,106 @@ __global__ __launch_bounds__(256) void k_convb(const bf16* __restrict__ xin, bf1
                                                const bf16* __restrict__ dy, int N, int H,
                                                const uint8_t* __restrict__ dmask) {
   using G = BfBand<C, W>;
-  constexpr int OT = G::OT, TW = G::TW, BR = G::BR, KS = G::KS;
+  constexpr int OT = G::OT, TW = G::TW, BR = G::BR, KS = G::KS, C8 = C / 8;
+  constexpr int NCH = (BR + 2) * TW * C8, NPT = (NCH + 255) / 256;
   __shared__ __attribute__((aligned(16))) bf16 tile[G::TILEE];
+  // backward: the band's own rows of dy unmasked (the epilogue's dy term), beside the dz tile
+  __shared__ __attribute__((aligned(16))) bf16 dyc[MODE == B_EULER ? BR * W * C : 8];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
   const int ot = wave % OT, rw = wave / OT;
   const int nb = (H + BR - 1) / BR;
-  const int n = blockIdx.x / nb, y0 = (blockIdx.x % nb) * BR;
-  if (n >= N) return;
+  const long items = (long)N * nb;
+  // persistent: a run of bands per workgroup, the W fragments loaded once, the next band's rows
+  // in registers while this band's MFMAs run
+  const long i0 = (long)blockIdx.x * items / gridDim.x, i1 = (long)(blockIdx.x + 1) * items / gridDim.x;
   bf16x8 A[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) A[ks] = *(const bf16x8*)(wpack + (((long)ot * KS + ks) * 64 + lane) * 8);
   f32x4 bz = {0.f, 0.f, 0.f, 0.f};
   if (MODE == F_EULER && bias) bz = *(const f32x4*)(bias + 16 * ot + 4 * g);
-  bf_stage_rows<C, W>(xin, tile, n, y0, H, tid, MODE == B_EULER ? dmask : nullptr);
-  __syncthreads();
-  constexpr int NT = (G::T + G::WPT - 1) / G::WPT;
+  uint4 pf[NPT];
+  unsigned pm[NPT];
+  auto fetch = [&](long item) {
+    const int n = (int)(item / nb), y0 = (int)(item % nb) * BR;
 #pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const int tau = rw + j * G::WPT;
-    if (tau >= G::T) break;  // (wave-uniform)
-    const int bp = 16 * tau + lx, r = bp / W, px = bp % W;
-    if (W >= 16 && y0 + r >= H) break;  // (wave-uniform for W >= 16; rows only grow with tau)
-    f32x4 acc = bz;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int kap = 32 * ks + 8 * g;
-      const int t = min(kap / C, 8), i0 = kap - (kap / C) * C;  // (C = 16, last k-step: tap 9 pads A with zeros)
-      const uint4 bv = *(const uint4*)(tile + ((r + t / 3) * TW + px + t % 3) * C + i0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], __builtin_bit_cast(bf16x8, bv), acc, 0, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);  // (the epilogue below reads acc: hipcc pads the wait states)
-    const bool ok = y0 + r < H;
-    const long pix = ((long)n * H + y0 + r) * W + px;
-    const long oi = pix * C + 16 * ot + 4 * g;  // this lane's 4 channels
-    const uint2 cw = *(const uint2*)(tile + ((r + 1) * TW + px + 1) * C + 16 * ot + 4 * g);  // x or dz at the pixel
-    const float ctr[4] = {__uint_as_float(cw.x << 16), __uint_as_float(cw.x & 0xffff0000u), __uint_as_float(cw.y << 16),
-                          __uint_as_float(cw.y & 0xffff0000u)};
-    float v[4];
-    if constexpr (MODE == F_EULER) {
-      unsigned nib = 0;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float z = acc[e];
-        nib |= (z > 0.f ? 1u : 0u) << e;
-        v[e] = fmaf(h, fmaxf(z, 0.f), ctr[e]);
+    for (int k = 0; k < NPT; ++k) {
+      const int i = tid + 256 * k;
+      const int r = i / (TW * C8), rem = i % (TW * C8), col = rem / C8, c8 = rem % C8;
+      const int gy = y0 - 1 + r, gx = col - 1;
+      pf[k] = make_uint4(0u, 0u, 0u, 0u);
+      pm[k] = 0u;
+      if (i < NCH && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W) {
+        const long e = (((long)n * H + gy) * W + gx) * C + 8 * c8;
+        pf[k] = *(const uint4*)(xin + e);
+        if (MODE == B_EULER) pm[k] = dmask[e >> 3];
       }
-      if (mask) {  // the pixel's 16 channels of this o-tile: 4 nibbles, one 16-bit store
-        unsigned m = nib << (4 * g);
-        m |= (unsigned)__shfl_xor((int)m, 16, 64);
-        m |= (unsigned)__shfl_xor((int)m, 32, 64);
-        if (g == 0 && ok) *(uint16_t*)(mask + (pix * C + 16 * ot) / 8) = (uint16_t)m;
-      }
-    } else {  // B_EULER: the tile holds dz = dy & mask
-      uint2 dw = make_uint2(0u, 0u);
-      if (ok) dw = *(const uint2*)(dy + oi);
-      const float d0[4] = {__uint_as_float(dw.x << 16), __uint_as_float(dw.x & 0xffff0000u),
-                           __uint_as_float(dw.y << 16), __uint_as_float(dw.y & 0xffff0000u)};
-      const float hg = h * two_gamma;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fmaf(hg, ctr[e], fmaf(-h, acc[e], d0[e]));
     }
-    if (ok) *(uint2*)(out + oi) = make_uint2(pk_bf16_rn(v[0], v[1]), pk_bf16_rn(v[2], v[3]));
+  };
+  if (i0 < i1) fetch(i0);
+  for (long item = i0; item < i1; ++item) {
+    const int n = (int)(item / nb), y0 = (int)(item % nb) * BR;
+    __syncthreads();  // the previous band's tile consumed
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int i = tid + 256 * k;
+      if (i >= NCH) break;
+      if constexpr (MODE == B_EULER) {  // the tile gets dz = dy & mask; the band's rows keep dy
+        *(uint4*)(tile + 8 * i) = mask8_bf16(pf[k], pm[k]);
+        const int r = i / (TW * C8), rem = i % (TW * C8), col = rem / C8;
+        if (r >= 1 && r <= BR && col >= 1 && col <= W) *(uint4*)(dyc + (((r - 1) * W + col - 1) * C8 + rem % C8) * 8) = pf[k];
+      } else {
+        *(uint4*)(tile + 8 * i) = pf[k];
+      }
+    }
+    __syncthreads();
+    if (item + 1 < i1) fetch(item + 1);
+    constexpr int NT = (G::T + G::WPT - 1) / G::WPT;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int tau = rw + j * G::WPT;
+      if (tau >= G::T) break;  // (wave-uniform)
+      const int bp = 16 * tau + lx, r = bp / W, px = bp % W;
+      if (W >= 16 && y0 + r >= H) break;  // (wave-uniform for W >= 16; rows only grow with tau)
+      f32x4 acc = bz;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int kap = 32 * ks + 8 * g;
+        const int t = min(kap / C, 8), i0c = kap - (kap / C) * C;  // (C = 16, last k-step: tap 9 pads A with zeros)
+        const uint4 bv = *(const uint4*)(tile + ((r + t / 3) * TW + px + t % 3) * C + i0c);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], __builtin_bit_cast(bf16x8, bv), acc, 0, 0, 0);
+      }
+      mfma_bf16_settle();  // (the epilogue branches: every path must see the result's wait states)
+      const bool ok = y0 + r < H;
+      const long pix = ((long)n * H + y0 + r) * W + px;
+      const long oi = pix * C + 16 * ot + 4 * g;  // this lane's 4 channels
+      const uint2 cw = *(const uint2*)(tile + ((r + 1) * TW + px + 1) * C + 16 * ot + 4 * g);  // x or dz at the pixel
+      const float ctr[4] = {__uint_as_float(cw.x << 16), __uint_as_float(cw.x & 0xffff0000u),
+                            __uint_as_float(cw.y << 16), __uint_as_float(cw.y & 0xffff0000u)};
+      float v[4];
+      if constexpr (MODE == F_EULER) {
+        unsigned nib = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float z = acc[e];
+          nib |= (z > 0.f ? 1u : 0u) << e;
+          v[e] = fmaf(h, fmaxf(z, 0.f), ctr[e]);
+        }
+        if (mask) {  // the pixel's 16 channels of this o-tile: 4 nibbles, one 16-bit store
+          unsigned m = nib << (4 * g);
+          m |= (unsigned)__shfl_xor((int)m, 16, 64);
+          m |= (unsigned)__shfl_xor((int)m, 32, 64);
+          if (g == 0 && ok) *(uint16_t*)(mask + (pix * C + 16 * ot) / 8) = (uint16_t)m;
+        }
+      } else {  // B_EULER: the tile holds dz = dy & mask
+        const uint2 dw = *(const uint2*)(dyc + (r * W + px) * C + 16 * ot + 4 * g);
+        const float d0[4] = {__uint_as_float(dw.x << 16), __uint_as_float(dw.x & 0xffff0000u),
+                             __uint_as_float(dw.y << 16), __uint_as_float(dw.y & 0xffff0000u)};
+        const float hg = h * two_gamma;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaf(hg, ctr[e], fmaf(-h, acc[e], d0[e]));
+      }
+      if (ok) *(uint2*)(out + oi) = make_uint2(pk_bf16_rn(v[0], v[1]), pk_bf16_rn(v[2], v[3]));
+    }
   }
 }
 
@@ -781,11 +820,222 @@ bool convb_supported(int W, int C) { return (W == 32 || W == 16 || W == 8) && (C
 template <int C, int W, int MODE>
 static int launch_convb(const bf16* xin, bf16* out, uint8_t* mask, const bf16* w, const float* bias, float h,
                         float two_gamma, const bf16* dy, int N, int H, const uint8_t* dmask, hipStream_t s) {
-  const long blocks = (long)N * ((H + 3) / 4);
-  if (blocks > 0x7fffffffL) return fail(ASR_E_ARG, "conv bf16: problem too large");
-  hipLaunchKernelGGL((k_convb<C, W, MODE>), dim3((unsigned)blocks), dim3(256), 0, s, xin, out, mask, w, bias, h,
+  const long items = (long)N * ((H + 3) / 4);
+  int cus = cu_count();
+  if (cus <= 0) cus = 256;
+#ifndef ASR_CONVB_WPC
+#define ASR_CONVB_WPC 4
+#endif
+  const long grid = std::max<long>(1, std::min<long>(items, (long)ASR_CONVB_WPC * cus));  // workgroups per CU
+  hipLaunchKernelGGL((k_convb<C, W, MODE>), dim3((unsigned)grid), dim3(256), 0, s, xin, out, mask, w, bias, h,
                      two_gamma, dy, N, H, dmask);
   ASR_LAUNCH_CHECK("k_convb");
+  return ASR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// The bf16 weight gradient at any stage width on v_mfma_f32_16x16x32_bf16
+// (k_wgradb): D[t][i][o] = h sum_px x[px + tap t][i] dz[px][o], dz = dy & mask
+// (exact in bf16; h applied to the fp32 sums), db[o] = h sum_px dz[px][o].
+// K = pixels: a workgroup stages a band of BR = 128 / W rows of one image (x
+// with its halo rows / columns, dz) in LDS, pixel-major with C channels
+// contiguous, and reads both operands with ds_read_b64_tr_b16 (T10): a 16-lane
+// group's lane (q, p) addresses pixel q of 4, channels 4p .. 4p+3, and lane lx
+// receives channel lx of the 4 pixels -- the MFMA fragment's k run.  A 32-pixel
+// chunk's k order is permuted the same way in both operands: lane group g takes
+// pixels 4g .. 4g+3 (first read) and 16 + 4g .. (second), so a 32-lane half
+// reads 8 consecutive pixels.  The 16-B chunk c of pixel P sits at chunk
+// c ^ f(P) (f = 2 ((P >> 1) & 3) at C = 64, 2 ((P >> 2) & 1) at C = 32, 0 at
+// C = 16): the half's 8 pixels x 32 B then cover all 64 banks.
+// Waves: TS pair splits (i-tile it, NO o-tiles: the 9 taps' A fragments feed
+// NO MFMAs each) x PS chunk splits, partials summed through LDS at the end;
+// db on MFMA (ones x dz) in the it = 0 waves.  Persistent over bands, the next
+// band's global loads in flight during this band's MFMAs; one [dW | db] slab
+// per workgroup, the rows the fp32 wgrad grid sizes (f32_block_slab_rows).
+// ---------------------------------------------------------------------------
+template <int C, int W_>
+struct WgB {
+  static constexpr int OT = C / 16, W = W_, TW = W + 2, BR = 128 / W;
+  static constexpr int NO = C == 16 ? 1 : 2, TS = OT * (OT / NO), PS = C == 64 ? 1 : 4, NW = TS * PS, NTH = 64 * NW;
+  static constexpr int C8 = C / 8, XCH = (BR + 2) * TW * C8, DCH = BR * W * C8;
+  static constexpr int XPT = (XCH + NTH - 1) / NTH, DPT = (DCH + NTH - 1) / NTH;
+  static constexpr int XE = (BR + 2) * TW * C, DE = BR * W * C;
+  static constexpr int ACC = (9 + 1) * NO;  // accumulator tiles per wave (9 taps + db per o-tile)
+  static constexpr size_t LDS = (size_t)(XE + DE) * 2 + (PS > 1 ? (size_t)TS * ACC * 256 * 4 : 0);
+  static_assert(W == 8 || W == 16 || W == 32, "bf16 wgrad: W in {8, 16, 32}");
+  __host__ __device__ static constexpr int swz(int P) {
+    return C == 64 ? 2 * ((P >> 1) & 3) : C == 32 ? 2 * ((P >> 2) & 1) : 0;
+  }
+};
+
+// one transposed-read k run: 4 pixels' 4 channels -> the lane's 4 bf16 of one channel
+__device__ __forceinline__ s16x4 tr4(const bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((ASR_LDS s16x4*)p);
+}
+
+template <int C, int W>
+__global__ __launch_bounds__((WgB<C, W>::NTH)) void k_wgradb(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                           const uint8_t* __restrict__ dmask, int N, int H, float h,
+                                                           float* __restrict__ slabs) {
+  using G = WgB<C, W>;
+  constexpr int TW = G::TW, BR = G::BR, NO = G::NO, OT = G::OT, E = 9 * C * C;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_wb[];
+  bf16* xt = (bf16*)lds_wb;               // [BR+2][TW][C] (chunk-swizzled per pixel)
+  bf16* dzt = xt + G::XE;                 // [BR][W][C]
+  float* red = (float*)(dzt + G::DE);     // [TS][ACC][64][4] (PS > 1)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
+  const int q = lx >> 2, pq = lx & 3;
+  const int ts = wave % G::TS, ps = wave / G::TS;
+  const int it = ts / (OT / NO), ob = (ts % (OT / NO)) * NO;
+  const int nb = (H + BR - 1) / BR;
+  const long items = (long)N * nb;
+  const long i0 = (long)blockIdx.x * items / gridDim.x, i1 = (long)(blockIdx.x + 1) * items / gridDim.x;
+  f32x4 acc[9][NO], accb[NO];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int o = 0; o < NO; ++o) acc[t][o] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int o = 0; o < NO; ++o) accb[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint4 px[G::XPT], pd[G::DPT];
+  auto fetch = [&](long item) {
+    const int n = (int)(item / nb), y0 = (int)(item % nb) * BR;
+#pragma unroll
+    for (int k = 0; k < G::XPT; ++k) {
+      const int i = tid + k * G::NTH;
+      px[k] = make_uint4(0u, 0u, 0u, 0u);
+      const int r = i / (TW * G::C8), rem = i % (TW * G::C8), col = rem / G::C8, c8 = rem % G::C8;
+      const int gy = y0 - 1 + r, gx = col - 1;
+      if (i < G::XCH && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
+        px[k] = *(const uint4*)(x + (((long)n * H + gy) * W + gx) * C + 8 * c8);
+    }
+#pragma unroll
+    for (int k = 0; k < G::DPT; ++k) {
+      const int i = tid + k * G::NTH;
+      pd[k] = make_uint4(0u, 0u, 0u, 0u);
+      const int r = i / (W * G::C8);
+      if (i < G::DCH && y0 + r < H) {
+        const long e = ((long)n * H + y0) * W * C + 8L * i;
+        pd[k] = mask8_bf16(*(const uint4*)(dy + e), dmask[e >> 3]);
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int k = 0; k < G::XPT; ++k) {
+      const int i = tid + k * G::NTH;
+      const int P = i / G::C8, c8 = i % G::C8;
+      if (i < G::XCH) *(uint4*)(xt + P * C + 8 * (c8 ^ G::swz(P))) = px[k];
+    }
+#pragma unroll
+    for (int k = 0; k < G::DPT; ++k) {
+      const int i = tid + k * G::NTH;
+      const int P = i / G::C8, c8 = i % G::C8;
+      if (i < G::DCH) *(uint4*)(dzt + P * C + 8 * (c8 ^ G::swz(P))) = pd[k];
+    }
+  };
+  // the lane's 8-B piece of channels 16 ch + 4 pq .. +3 at pixel P of a tile
+  auto piece = [&](const bf16* tile, int P, int ch) {
+    const int c16 = 2 * ch + (pq >> 1);
+    return tile + P * C + 8 * (c16 ^ G::swz(P)) + 4 * (pq & 1);
+  };
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  auto frag = [&](const bf16* tile, int P1, int P2, int ch) {
+    const s16x4 a = tr4(piece(tile, P1, ch)), b = tr4(piece(tile, P2, ch));
+    const s16x8 c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    return __builtin_bit_cast(bf16x8, c);
+  };
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.f;
+  if (i0 < i1) fetch(i0);
+  for (long item = i0; item < i1; ++item) {
+    const int y0 = (int)(item % nb) * BR;
+    const int rows = min(BR, H - y0), nch = (rows * W + 31) / 32;
+    __syncthreads();  // the previous band's operands consumed
+    store();
+    __syncthreads();
+    if (item + 1 < i1) fetch(item + 1);  // in flight during this band's MFMAs
+    for (int ch = ps; ch < nch; ch += G::PS) {  // (wave-uniform: EXEC stays full for the transposed reads)
+      const int k1 = 32 * ch + 4 * g + q, k2 = k1 + 16;
+      const int r1 = k1 / W, c1 = k1 % W, r2 = k2 / W, c2 = k2 % W;
+      bf16x8 B[NO];
+#pragma unroll
+      for (int o = 0; o < NO; ++o) B[o] = frag(dzt, r1 * W + c1, r2 * W + c2, ob + o);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int d = (t / 3) * TW + t % 3;
+        const bf16x8 A = frag(xt, r1 * TW + c1 + d, r2 * TW + c2 + d, it);
+#pragma unroll
+        for (int o = 0; o < NO; ++o) acc[t][o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[o], acc[t][o], 0, 0, 0);
+      }
+      if (it == 0) {
+#pragma unroll
+        for (int o = 0; o < NO; ++o) accb[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, B[o], accb[o], 0, 0, 0);
+      }
+    }
+  }
+  // the PS chunk-split partials, summed in a fixed order through LDS (one split at a time)
+  if constexpr (G::PS > 1) {
+    float* mine = red + (long)ts * G::ACC * 256;
+#pragma unroll 1
+    for (int src = 1; src < G::PS; ++src) {
+      __syncthreads();
+      if (ps == src) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int o = 0; o < NO; ++o) *(f32x4*)(mine + ((t * NO + o) * 64 + lane) * 4) = acc[t][o];
+#pragma unroll
+        for (int o = 0; o < NO; ++o) *(f32x4*)(mine + ((9 * NO + o) * 64 + lane) * 4) = accb[o];
+      }
+      __syncthreads();
+      if (ps == 0) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int o = 0; o < NO; ++o) acc[t][o] += *(const f32x4*)(mine + ((t * NO + o) * 64 + lane) * 4);
+#pragma unroll
+        for (int o = 0; o < NO; ++o) accb[o] += *(const f32x4*)(mine + ((9 * NO + o) * 64 + lane) * 4);
+      }
+    }
+  }
+  if (ps == 0) {
+    float* slab = slabs + (long)blockIdx.x * (E + C);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int o = 0; o < NO; ++o)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          slab[((long)t * C + 16 * it + 4 * g + e) * C + 16 * (ob + o) + lx] = h * acc[t][o][e];
+    if (it == 0 && g == 0) {
+#pragma unroll
+      for (int o = 0; o < NO; ++o) slab[E + 16 * (ob + o) + lx] = h * accb[o][0];
+    }
+  }
+}
+
+template <int C, int W>
+static int launch_wgradb(const bf16* x, const bf16* dy, const uint8_t* mask, int N, int H, float h, float* slabs,
+                         int* nslabs, hipStream_t s) {
+  using G = WgB<C, W>;
+  const long items = (long)N * ((H + G::BR - 1) / G::BR);
+  // at most the fp32 wgrad's grid: the rows the workspaces size per block (f32_block_slab_rows)
+#ifndef ASR_WGB_B16
+#define ASR_WGB_B16 1
+#endif
+#ifndef ASR_WGB_B32
+#define ASR_WGB_B32 2
+#endif
+#ifndef ASR_WGB_B64
+#define ASR_WGB_B64 4
+#endif
+  constexpr int minb = C == 16 ? ASR_WGB_B16 : C == 32 ? ASR_WGB_B32 : ASR_WGB_B64;
+  const int grid = (int)std::max<long>(1, std::min<long>((items + minb - 1) / minb, wgrad32_grid<C, W>(N, H)));
+  hipLaunchKernelGGL((k_wgradb<C, W>), dim3(grid), dim3(G::NTH), G::LDS, s, x, dy, mask, N, H, h, slabs);
+  ASR_LAUNCH_CHECK("k_wgradb");
+  *nslabs = grid;
   return ASR_OK;
 }
 
@@ -820,9 +1070,8 @@ int convb_backward(const void* dy, const uint8_t* mask, const void* x, const voi
 #undef ASR_CB
   }
   if (!need_w) return ASR_OK;
-#define ASR_WB(CC, WW)                                                                                     \
-  if (C == CC && W == WW)                                                                                  \
-    return launch_wgrad32<CC, WW, bf16>((const bf16*)x, (const bf16*)dy, N, H, slabs, nslabs, s, mask, h);
+#define ASR_WB(CC, WW) \
+  if (C == CC && W == WW) return launch_wgradb<CC, WW>((const bf16*)x, (const bf16*)dy, mask, N, H, h, slabs, nslabs, s);
   ASR_WB(16, 32) ASR_WB(16, 16) ASR_WB(16, 8) ASR_WB(32, 32) ASR_WB(32, 16) ASR_WB(32, 8) ASR_WB(64, 32)
   ASR_WB(64, 16) ASR_WB(64, 8)
 #undef ASR_WB

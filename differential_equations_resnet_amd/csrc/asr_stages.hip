@@ -452,6 +452,294 @@ __global__ __launch_bounds__(256) void k_trans_wgrad_mfma(const float* __restric
   }
 }
 
+// ---------------------------------------------------------------------------
+// The stride-2 transition's weight gradient with LDS-staged operands
+// (k_trans_wgrad_lds; even H and W, so TF's 'same' padding puts no row / column
+// before the image: output (yo, xo) reads input rows 2yo .. 2yo+2, columns
+// 2xo .. 2xo+2, and the 1x1 shortcut reads (2yo, 2xo) = tap 0's position).
+// A workgroup (8 waves) stages a band of BRO = 4 output rows: the 2 BRO + 1
+// input rows (W + 1 columns, zeros past the image) and the band's dy and
+// dz = dy [z > 0], pixel strides padded (x: CI + 8 floats, so the lane groups'
+// even pixels of a half fall on disjoint banks; dy / dz: CO + 16 when CO is a
+// multiple of 32).  Waves = (i-tile, o-tile) pair x RS k-step splits; K = 4
+// output pixels per v_mfma_f32_16x16x4_f32; a wave holds the 9 taps + the 1x1
+// (sharing tap 0's A operand) and, at it = 0, db2 / db1 (ones x dz / dy).
+// Persistent over bands; the RS partials summed through LDS, one partial slab
+// [dK2 | db2 | dK1 | db1] per workgroup, summed by k_sum_chunks.
+// ---------------------------------------------------------------------------
+template <int CI, int CO, int WO>
+struct TWg {
+  static constexpr int IT = CI / 16, OT = CO / 16, P = IT * OT, NW = 8, RS = NW / P, BRO = 4, XR = 2 * BRO + 1;
+  static constexpr int TW = 2 * WO + 1, XS = CI + 8, DS = CO % 32 == 0 ? CO + 16 : CO, NPX = BRO * WO;
+  static constexpr int XF = XR * TW * XS, DF = NPX * DS, ACC = 12;
+  static constexpr size_t LDS = std::max((size_t)(XF + 2 * DF) * 4, RS > 1 ? (size_t)P * ACC * 256 * 4 : (size_t)0);
+  static_assert(P * RS == NW, "transition wgrad: IT x OT must divide 8");
+};
+
+template <int CI, int CO, int WO>
+__global__ __launch_bounds__(512) void k_trans_wgrad_lds(const float* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                         const float* __restrict__ x, float* __restrict__ part, int N,
+                                                         int H) {
+  using G = TWg<CI, CO, WO>;
+  constexpr int W = 2 * WO, TW = G::TW, XS = G::XS, DS = G::DS, BRO = G::BRO;
+  extern __shared__ __attribute__((aligned(16))) float lds_tw[];
+  float* xt = lds_tw;              // [XR][TW][XS]
+  float* dzt = lds_tw + G::XF;     // [NPX][DS]
+  float* dyt = dzt + G::DF;        // [NPX][DS]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
+  const int pr = wave % G::P, rs = wave / G::P, it = pr / G::OT, ot = pr % G::OT;
+  const int Ho = H / 2, nb = (Ho + BRO - 1) / BRO;
+  const long items = (long)N * nb;
+  const long i0 = (long)blockIdx.x * items / gridDim.x, i1 = (long)(blockIdx.x + 1) * items / gridDim.x;
+  f32x4 acc[10], accb2 = {0.f, 0.f, 0.f, 0.f}, accb1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 10; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (long item = i0; item < i1; ++item) {
+    const int n = (int)(item / nb), yo0 = (int)(item % nb) * BRO;
+    const int rows = min(BRO, Ho - yo0);
+    __syncthreads();  // the previous band's operands consumed
+    for (int i = tid; i < G::XR * TW * (CI / 4); i += 512) {
+      const int j = i / (TW * (CI / 4)), rem = i % (TW * (CI / 4)), col = rem / (CI / 4), c4 = rem % (CI / 4);
+      const int gy = 2 * yo0 + j;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (gy < H && col < W) v = *(const f32x4*)(x + (((long)n * H + gy) * W + col) * CI + 4 * c4);
+      *(f32x4*)(xt + (j * TW + col) * XS + 4 * c4) = v;
+    }
+    for (int i = tid; i < G::NPX * (CO / 4); i += 512) {
+      const int k = i / (CO / 4), c4 = i % (CO / 4);
+      f32x4 v = {0.f, 0.f, 0.f, 0.f}, z = {0.f, 0.f, 0.f, 0.f};
+      if (k / WO < rows) {
+        const long e = (((long)n * Ho + yo0) * WO + k) * CO + 4 * c4;
+        v = *(const f32x4*)(dy + e);
+        z = v * mask4(mask + e);
+      }
+      *(f32x4*)(dyt + k * DS + 4 * c4) = v;
+      *(f32x4*)(dzt + k * DS + 4 * c4) = z;
+    }
+    __syncthreads();
+    const int steps = rows * WO / 4;
+    for (int st = rs; st < steps; st += G::RS) {
+      const int k = 4 * st + g, r = k / WO, xo = k % WO;
+      const float bz = dzt[k * DS + 16 * ot + lx], by = dyt[k * DS + 16 * ot + lx];
+      const float* xa = xt + ((2 * r) * TW + 2 * xo) * XS + 16 * it + lx;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const float a = xa[((t / 3) * TW + t % 3) * XS];
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bz, acc[t], 0, 0, 0);
+        if (t == 0) acc[9] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, by, acc[9], 0, 0, 0);
+      }
+      if (it == 0) {  // (wave-uniform)
+        accb2 = __builtin_amdgcn_mfma_f32_16x16x4f32(1.f, bz, accb2, 0, 0, 0);
+        accb1 = __builtin_amdgcn_mfma_f32_16x16x4f32(1.f, by, accb1, 0, 0, 0);
+      }
+    }
+  }
+  mfma_f32_settle();  // (the result is read below: every path sees the wait states)
+  if constexpr (G::RS > 1) {  // the k-step splits' partials, one split at a time, fixed order
+    float* mine = lds_tw + (long)pr * G::ACC * 256;
+#pragma unroll 1
+    for (int src = 1; src < G::RS; ++src) {
+      __syncthreads();
+      if (rs == src) {
+#pragma unroll
+        for (int t = 0; t < 10; ++t) *(f32x4*)(mine + (t * 64 + lane) * 4) = acc[t];
+        *(f32x4*)(mine + (10 * 64 + lane) * 4) = accb2;
+        *(f32x4*)(mine + (11 * 64 + lane) * 4) = accb1;
+      }
+      __syncthreads();
+      if (rs == 0) {
+#pragma unroll
+        for (int t = 0; t < 10; ++t) acc[t] += *(const f32x4*)(mine + (t * 64 + lane) * 4);
+        accb2 += *(const f32x4*)(mine + (10 * 64 + lane) * 4);
+        accb1 += *(const f32x4*)(mine + (11 * 64 + lane) * 4);
+      }
+    }
+  }
+  if (rs != 0) return;
+  constexpr long E2 = 9L * CI * CO, E1 = (long)CI * CO, ET = E2 + CO + E1 + CO;
+  float* out = part + (long)blockIdx.x * ET;
+  const int co = 16 * ot + lx;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[((long)t * CI + 16 * it + 4 * g + j) * CO + co] = acc[t][j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) out[E2 + CO + (long)(16 * it + 4 * g + j) * CO + co] = acc[9][j];
+  if (it == 0 && g == 0) {
+    out[E2 + co] = accb2[0];
+    out[E2 + CO + E1 + co] = accb1[0];
+  }
+}
+
+// The stride-2 transition's input gradient with LDS-staged operands
+// (k_trans_dgrad_lds; even H and W).  dx[gy][gx] = sum over the taps with
+// gy - ky, gx - kx even of K2[ky][kx] dz[(gy-ky)/2][(gx-kx)/2] (+ K1 dy[gy/2][gx/2]
+// at even gy, gx): by the parities of (gy, gx) the output splits into four
+// classes with 4 (+ the 1x1), 2, 2 and 1 taps, and a 16-pixel MFMA tile holds
+// pixels of one class (one row's 16 even or odd columns at W = 32; two rows
+// gy, gy + 2 of 8 such columns at W = 16), so no MFMA multiplies a structural
+// zero.  A workgroup (8 waves) stages a band of BR = 8 output rows' operands:
+// dz = dy [z > 0] and dy on the BR / 2 + 1 source rows x WO + 1 columns
+// (source row / column -1 as zeros), pixel stride CO + 4 floats (the 16
+// lanes' 16-B reads on disjoint banks).  A wave keeps its i-tile's K2 / K1
+// fragments in registers and takes the band's (row group, column parity)
+// tiles round-robin; v_mfma_f32_16x16x4_f32, D = dx tile [i][pixel].
+template <int CI, int CO, int WO>
+struct TDg {
+  static constexpr int W = 2 * WO, IT = CI / 16, OQ = CO / 16, BR = 8, SR = BR / 2 + 1, SC = WO + 1;
+  static constexpr int PS = CO + 4, SF = SR * SC * PS;       // floats per staged tile
+  static constexpr int RPT = W == 32 ? 1 : 2;                // rows per MFMA tile (W/2 columns each)
+  static constexpr int TPB = (BR / RPT) * 2;                 // (row group, column parity) tiles per band per i-tile
+  static constexpr int NW = 8, WPI = NW / IT;                // waves per i-tile
+  static constexpr size_t LDS = (size_t)2 * SF * 4;
+  static_assert(W == 32 || W == 16, "transition dgrad (LDS): W in {32, 16}");
+  static_assert(NW % IT == 0, "transition dgrad (LDS): CI / 16 must divide 8");
+};
+
+template <int CI, int CO, int WO>
+__global__ __launch_bounds__(512) void k_trans_dgrad_lds(const float* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                         const float* __restrict__ k2, const float* __restrict__ k1,
+                                                         float* __restrict__ dx, int N, int H) {
+  using G = TDg<CI, CO, WO>;
+  constexpr int W = G::W, BR = G::BR, SC = G::SC, PS = G::PS, OQ = G::OQ;
+  extern __shared__ __attribute__((aligned(16))) float lds_td[];
+  float* dzt = lds_td;          // [SR][SC][PS]
+  float* dyt = lds_td + G::SF;  // [SR][SC][PS]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
+  const int it = wave / G::WPI, wi = wave % G::WPI;
+  const int Ho = H / 2, nb = H / BR;
+  const long items = (long)N * nb;
+  const long i0 = (long)blockIdx.x * items / gridDim.x, i1 = (long)(blockIdx.x + 1) * items / gridDim.x;
+  // A = K2[tap][i][o]^T fragments of i-tile it: lane (lx, g), k-step s of o-group q: o = 16q + 4g + s
+  float A2[9][OQ][4], A1[OQ][4];
+  const int i = 16 * it + lx;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int q = 0; q < OQ; ++q) {
+      const f32x4 v = ld4(k2 + ((long)t * CI + i) * CO + 16 * q + 4 * g);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) A2[t][q][s4] = v[s4];
+    }
+#pragma unroll
+  for (int q = 0; q < OQ; ++q) {
+    const f32x4 v = ld4(k1 + (long)i * CO + 16 * q + 4 * g);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) A1[q][s4] = v[s4];
+  }
+  for (long item = i0; item < i1; ++item) {
+    const int n = (int)(item / nb), gy0 = (int)(item % nb) * BR, yb = gy0 / 2 - 1;  // staged source row 0 = yo yb
+    __syncthreads();  // the previous band's operands consumed
+    for (int e = tid; e < G::SR * SC * (CO / 4); e += 512) {
+      const int j = e / (SC * (CO / 4)), rem = e % (SC * (CO / 4)), c = rem / (CO / 4), c4 = rem % (CO / 4);
+      const int yo = yb + j, xo = c - 1;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f}, z = {0.f, 0.f, 0.f, 0.f};
+      if (yo >= 0 && yo < Ho && xo >= 0) {
+        const long off = (((long)n * Ho + yo) * WO + xo) * CO + 4 * c4;
+        v = ld4(dy + off);
+        z = v * mask4(mask + off);
+      }
+      *(f32x4*)(dyt + (j * SC + c) * PS + 4 * c4) = v;
+      *(f32x4*)(dzt + (j * SC + c) * PS + 4 * c4) = z;
+    }
+    __syncthreads();
+    for (int tk = wi; tk < G::TPB; tk += G::WPI) {  // (wave-uniform)
+      const int pxp = tk & 1, rg = tk >> 1;          // column parity, row group
+      // row group rg: W = 32 one row gy0 + rg; W = 16 rows {a, a + 2}, a = gy0 + (rg & 1) + 4 (rg >> 1)
+      const int gyA = G::RPT == 1 ? gy0 + rg : gy0 + (rg & 1) + 4 * (rg >> 1);
+      const int gy = gyA + (G::RPT == 2 ? 2 * (lx / (W / 2)) : 0), gx = 2 * (lx % (W / 2)) + pxp;
+      const int py = gyA & 1;  // (the same for both rows of a W = 16 tile)
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        if ((ky & 1) != py) continue;  // (wave-uniform)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          if ((kx & 1) != pxp) continue;  // (wave-uniform)
+          const int j = (gy - ky) / 2 - yb, c = (gx - kx) / 2 + 1;  // ((gy - ky) even: exact halves, -1 allowed)
+          const float* bp = dzt + (j * SC + c) * PS + 4 * g;
+#pragma unroll
+          for (int q = 0; q < OQ; ++q) {
+            const f32x4 bv = *(const f32x4*)(bp + 16 * q);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4)
+              acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A2[3 * ky + kx][q][s4], bv[s4], acc, 0, 0, 0);
+          }
+        }
+      }
+      if (py == 0 && pxp == 0) {  // the 1x1 shortcut at even (gy, gx)
+        const float* bp = dyt + ((gy / 2 - yb) * SC + gx / 2 + 1) * PS + 4 * g;
+#pragma unroll
+        for (int q = 0; q < OQ; ++q) {
+          const f32x4 bv = *(const f32x4*)(bp + 16 * q);
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A1[q][s4], bv[s4], acc, 0, 0, 0);
+        }
+      }
+      mfma_f32_settle();
+      *(f32x4*)(dx + (((long)n * H + gy) * W + gx) * CI + 16 * it + 4 * g) = acc;
+    }
+  }
+}
+
+bool trans_dgrad_lds_supported(int H, int W, int Ci, int Co, int S) {
+  if (S != 2 || H % 8 || (W != 32 && W != 16)) return false;
+  return (Ci == 16 && (Co == 16 || Co == 32)) || (Ci == 32 && (Co == 32 || Co == 64));
+}
+
+template <int CI, int CO, int WO>
+int launch_trans_dgrad_lds(const float* dy, const uint8_t* mask, const float* k2, const float* k1, float* dx, int N,
+                           int H, hipStream_t s) {
+  using G = TDg<CI, CO, WO>;
+  const long items = (long)N * (H / G::BR);
+  int cus = cu_count();
+  if (cus <= 0) cus = 256;
+  const int grid = (int)std::max<long>(1, std::min<long>(items, 2L * cus));
+  hipLaunchKernelGGL((k_trans_dgrad_lds<CI, CO, WO>), dim3(grid), dim3(512), G::LDS, s, dy, mask, k2, k1, dx, N, H);
+  ASR_LAUNCH_CHECK("k_trans_dgrad_lds");
+  return ASR_OK;
+}
+
+int trans_dgrad_lds(const float* dy, const uint8_t* mask, const float* k2, const float* k1, float* dx, int N, int H,
+                    int W, int Ci, int Co, hipStream_t s) {
+#define ASR_TDL(CI_, CO_, WO_) \
+  if (Ci == CI_ && Co == CO_ && W == 2 * WO_) return launch_trans_dgrad_lds<CI_, CO_, WO_>(dy, mask, k2, k1, dx, N, H, s);
+  ASR_TDL(16, 16, 16) ASR_TDL(16, 32, 16) ASR_TDL(32, 32, 16) ASR_TDL(32, 64, 16)
+  ASR_TDL(16, 16, 8) ASR_TDL(16, 32, 8) ASR_TDL(32, 32, 8) ASR_TDL(32, 64, 8)
+#undef ASR_TDL
+  return fail(ASR_E_UNSUPPORTED, "transition dgrad (LDS): Ci=%d Co=%d W=%d", Ci, Co, W);
+}
+
+// the LDS-staged weight gradient's shapes: stride 2, even H / W, W/2 in {16, 8}, (Ci, Co) pairs with IT x OT <= 8
+bool trans_wgrad_lds_supported(int H, int W, int Ci, int Co, int S) {
+  if (S != 2 || (H & 1) || (W & 1) || (W != 32 && W != 16)) return false;
+  return (Ci == 16 && (Co == 16 || Co == 32)) || (Ci == 32 && (Co == 32 || Co == 64));
+}
+
+template <int CI, int CO, int WO>
+int launch_trans_wgrad_lds(const float* dy, const uint8_t* mask, const float* x, float* part, int N, int H,
+                           int max_rows, int* rows_out, hipStream_t s) {
+  using G = TWg<CI, CO, WO>;
+  const long items = (long)N * ((H / 2 + G::BRO - 1) / G::BRO);
+  int cus = cu_count();
+  if (cus <= 0) cus = 256;
+  const int grid = (int)std::max<long>(1, std::min<long>({items, 2L * cus, (long)max_rows}));
+  hipLaunchKernelGGL((k_trans_wgrad_lds<CI, CO, WO>), dim3(grid), dim3(512), G::LDS, s, dy, mask, x, part, N, H);
+  ASR_LAUNCH_CHECK("k_trans_wgrad_lds");
+  *rows_out = grid;
+  return ASR_OK;
+}
+
+int trans_wgrad_lds(const float* dy, const uint8_t* mask, const float* x, float* part, int N, int H, int W, int Ci,
+                    int Co, int max_rows, int* rows, hipStream_t s) {
+#define ASR_TWL(CI_, CO_, WO_) \
+  if (Ci == CI_ && Co == CO_ && W == 2 * WO_) return launch_trans_wgrad_lds<CI_, CO_, WO_>(dy, mask, x, part, N, H, max_rows, rows, s);
+  ASR_TWL(16, 16, 16) ASR_TWL(16, 32, 16) ASR_TWL(32, 32, 16) ASR_TWL(32, 64, 16)
+  ASR_TWL(16, 16, 8) ASR_TWL(16, 32, 8) ASR_TWL(32, 32, 8) ASR_TWL(32, 64, 8)
+#undef ASR_TWL
+  return fail(ASR_E_UNSUPPORTED, "transition wgrad (LDS): Ci=%d Co=%d W=%d", Ci, Co, W);
+}
+
 bool trans_mfma(int Ci, int Co) { return Ci % 16 == 0 && Co % 16 == 0; }
 
 // MFMA weight gradient: chunks of ppc output pixels (a multiple of 4) such that about 2048 waves
@@ -506,7 +794,9 @@ int trans_backward(const float* dy, const float* x, const uint8_t* mask, const f
                    int H, int W, int Ci, int Co, int S, float* dx, float* dparams, float* part, hipStream_t s) {
   const TGeom g = tgeom(H, W, S);
   if (trans_mfma(Ci, Co)) {
-    if (dx) {
+    if (dx && trans_dgrad_lds_supported(H, W, Ci, Co, S)) {
+      ASR_TRY(trans_dgrad_lds(dy, mask, k2, k1, dx, N, H, W, Ci, Co, s));
+    } else if (dx) {
       const long blocks = ((long)N * H * ((W + 15) / 16) * (Ci / 16) + 3) / 4;
       if (blocks > 0x7fffffffL) return fail(ASR_E_ARG, "transition: problem too large");
       hipLaunchKernelGGL(k_trans_dgrad_mfma, dim3((unsigned)blocks), dim3(256), 0, s, dy, mask, k2, k1, dx, N, H, W,
@@ -515,12 +805,16 @@ int trans_backward(const float* dy, const float* x, const uint8_t* mask, const f
     }
     if (dparams) {
       int ppc = 0;
-      const int chunks = trans_mfma_chunks(N, g.Ho, g.Wo, Ci, Co, &ppc);
+      int chunks = trans_mfma_chunks(N, g.Ho, g.Wo, Ci, Co, &ppc);  // (the workspace's partial rows)
       const long ET = trans_param_floats(Ci, Co);
-      const long blocks = ((long)chunks * (Ci / 16) * (Co / 16) + 3) / 4;
-      hipLaunchKernelGGL(k_trans_wgrad_mfma, dim3((unsigned)blocks), dim3(256), 0, s, dy, mask, x, part, N, H, W, Ci,
-                         Co, S, g.Ho, g.Wo, g.pt, g.pl, ppc, chunks);
-      ASR_LAUNCH_CHECK("k_trans_wgrad_mfma");
+      if (trans_wgrad_lds_supported(H, W, Ci, Co, S)) {
+        ASR_TRY(trans_wgrad_lds(dy, mask, x, part, N, H, W, Ci, Co, chunks, &chunks, s));
+      } else {
+        const long blocks = ((long)chunks * (Ci / 16) * (Co / 16) + 3) / 4;
+        hipLaunchKernelGGL(k_trans_wgrad_mfma, dim3((unsigned)blocks), dim3(256), 0, s, dy, mask, x, part, N, H, W,
+                           Ci, Co, S, g.Ho, g.Wo, g.pt, g.pl, ppc, chunks);
+        ASR_LAUNCH_CHECK("k_trans_wgrad_mfma");
+      }
       hipLaunchKernelGGL(k_sum_chunks, dim3((unsigned)((ET + 63) / 64)), dim3(256), 0, s, part, chunks, ET, dparams);
       ASR_LAUNCH_CHECK("k_sum_chunks");
     }
