@@ -278,6 +278,16 @@ __global__ __launch_bounds__(256) void k_sum_chunks(const float* __restrict__ pa
 // column lx.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; }
+// 4 consecutive bf16 as fp32 (the bf16 nets' activations, exact)
+__device__ __forceinline__ f32x4 ld4(const bf16* p) {
+  const uint2 u = *(const uint2*)p;
+  return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+               __uint_as_float(u.y & 0xffff0000u)};
+}
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *(f32x4*)p = v; }
+__device__ __forceinline__ void st4(bf16* p, f32x4 v) {
+  *(uint2*)p = make_uint2(pk_bf16_rn(v[0], v[1]), pk_bf16_rn(v[2], v[3]));
+}
 __device__ __forceinline__ f32x4 mask4(const uint8_t* m) {
   const unsigned u = *(const unsigned*)m;
   return f32x4{(float)(u & 0xff), (float)((u >> 8) & 0xff), (float)((u >> 16) & 0xff), (float)(u >> 24)};
@@ -476,9 +486,9 @@ struct TWg {
   static_assert(P * RS == NW, "transition wgrad: IT x OT must divide 8");
 };
 
-template <int CI, int CO, int WO>
-__global__ __launch_bounds__(512) void k_trans_wgrad_lds(const float* __restrict__ dy, const uint8_t* __restrict__ mask,
-                                                         const float* __restrict__ x, float* __restrict__ part, int N,
+template <int CI, int CO, int WO, typename T>
+__global__ __launch_bounds__(512) void k_trans_wgrad_lds(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                         const T* __restrict__ x, float* __restrict__ part, int N,
                                                          int H) {
   using G = TWg<CI, CO, WO>;
   constexpr int W = 2 * WO, TW = G::TW, XS = G::XS, DS = G::DS, BRO = G::BRO;
@@ -502,7 +512,7 @@ __global__ __launch_bounds__(512) void k_trans_wgrad_lds(const float* __restrict
       const int j = i / (TW * (CI / 4)), rem = i % (TW * (CI / 4)), col = rem / (CI / 4), c4 = rem % (CI / 4);
       const int gy = 2 * yo0 + j;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (gy < H && col < W) v = *(const f32x4*)(x + (((long)n * H + gy) * W + col) * CI + 4 * c4);
+      if (gy < H && col < W) v = ld4(x + (((long)n * H + gy) * W + col) * CI + 4 * c4);
       *(f32x4*)(xt + (j * TW + col) * XS + 4 * c4) = v;
     }
     for (int i = tid; i < G::NPX * (CO / 4); i += 512) {
@@ -510,7 +520,7 @@ __global__ __launch_bounds__(512) void k_trans_wgrad_lds(const float* __restrict
       f32x4 v = {0.f, 0.f, 0.f, 0.f}, z = {0.f, 0.f, 0.f, 0.f};
       if (k / WO < rows) {
         const long e = (((long)n * Ho + yo0) * WO + k) * CO + 4 * c4;
-        v = *(const f32x4*)(dy + e);
+        v = ld4(dy + e);
         z = v * mask4(mask + e);
       }
       *(f32x4*)(dyt + k * DS + 4 * c4) = v;
@@ -571,6 +581,119 @@ __global__ __launch_bounds__(512) void k_trans_wgrad_lds(const float* __restrict
   }
 }
 
+// The stride-2 transition's forward with LDS-staged input rows (k_trans_fwd_lds;
+// H a multiple of 8, W in {32, 16}): a workgroup stages the 2 BRO + 1 input
+// rows of a band of BRO = 4 output rows (W + 1 columns, the last zero; pixel
+// stride CI + 4 floats), a wave = (o-tile, 16-pixel tile of the band) keeps its
+// K2 / K1 fragments in registers: D[o][pixel] over (tap, i), the 1x1 shortcut
+// from tap 0's operand, y = relu(z) + shortcut and the relu mask bytes in the
+// epilogue.  T = bf16 for the bf16 nets (the activations in and out in bf16,
+// staged and computed in fp32), float otherwise.
+template <int CI, int CO, int WO>
+struct TFw {
+  static constexpr int W = 2 * WO, OT = CO / 16, IQ = CI / 16, BRO = 4, XR = 2 * BRO + 1, TW = W + 1, PX = CI + 4;
+  static constexpr int PT = BRO * WO / 16, NW = OT * PT, XF = XR * TW * PX;
+  static constexpr size_t LDS = (size_t)XF * 4;
+};
+
+template <int CI, int CO, int WO, typename T>
+__global__ __launch_bounds__((64 * TFw<CI, CO, WO>::NW)) void k_trans_fwd_lds(
+    const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ mask, const float* __restrict__ k2,
+    const float* __restrict__ b2, const float* __restrict__ k1, const float* __restrict__ b1, int N, int H) {
+  using G = TFw<CI, CO, WO>;
+  constexpr int W = G::W, TW = G::TW, PX = G::PX, BRO = G::BRO, IQ = G::IQ;
+  extern __shared__ __attribute__((aligned(16))) float lds_tf[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
+  const int ot = wave % G::OT, pt = wave / G::OT;
+  const int Ho = H / 2, nb = Ho / BRO;
+  const long items = (long)N * nb;
+  const long i0 = (long)blockIdx.x * items / gridDim.x, i1 = (long)(blockIdx.x + 1) * items / gridDim.x;
+  // A = K^T fragments of o-tile ot: lane (lx, g), k-step s of i-group q: i = 16q + 4g + s, o = 16 ot + lx
+  float A2[9][IQ][4], A1[IQ][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int q = 0; q < IQ; ++q)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) A2[t][q][s4] = k2[((long)t * CI + 16 * q + 4 * g + s4) * CO + 16 * ot + lx];
+#pragma unroll
+  for (int q = 0; q < IQ; ++q)
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) A1[q][s4] = k1[(long)(16 * q + 4 * g + s4) * CO + 16 * ot + lx];
+  const int o0 = 16 * ot + 4 * g;  // the lane's 4 output channels (accumulator rows)
+  const f32x4 bb2 = ld4(b2 + o0), bb1 = ld4(b1 + o0);
+  const int p = 16 * pt + lx, r = p / WO, xo = p % WO;  // the lane's output pixel in the band
+  for (long item = i0; item < i1; ++item) {
+    const int n = (int)(item / nb), yo0 = (int)(item % nb) * BRO;
+    __syncthreads();  // the previous band's rows consumed
+    for (int e = tid; e < G::XR * TW * (CI / 4); e += 64 * G::NW) {
+      const int j = e / (TW * (CI / 4)), rem = e % (TW * (CI / 4)), col = rem / (CI / 4), c4 = rem % (CI / 4);
+      const int gy = 2 * yo0 + j;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (gy < H && col < W) v = ld4(x + (((long)n * H + gy) * W + col) * CI + 4 * c4);
+      *(f32x4*)(lds_tf + (j * TW + col) * PX + 4 * c4) = v;
+    }
+    __syncthreads();
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accs = {0.f, 0.f, 0.f, 0.f};
+    const float* xb = lds_tf + ((2 * r) * TW + 2 * xo) * PX + 4 * g;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int q = 0; q < IQ; ++q) {
+        const f32x4 bv = *(const f32x4*)(xb + ((t / 3) * TW + t % 3) * PX + 16 * q);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A2[t][q][s4], bv[s4], acc, 0, 0, 0);
+          if (t == 0) accs = __builtin_amdgcn_mfma_f32_16x16x4f32(A1[q][s4], bv[s4], accs, 0, 0, 0);
+        }
+      }
+    mfma_f32_settle();
+    const long pg = ((long)n * Ho + yo0 + r) * WO + xo;
+    f32x4 v;
+    unsigned mb = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float z = acc[j] + bb2[j];
+      v[j] = fmaxf(z, 0.f) + (accs[j] + bb1[j]);
+      mb |= (z > 0.f ? 1u : 0u) << (8 * j);
+    }
+    st4(y + pg * CO + o0, v);
+    if (mask) *(unsigned*)(mask + pg * CO + o0) = mb;
+  }
+}
+
+// the LDS-staged transition kernels' shapes (forward, input and weight gradients)
+bool trans_lds_supported(int H, int W, int Ci, int Co, int S) {
+  if (S != 2 || H % 8 || (W != 32 && W != 16)) return false;
+  return (Ci == 16 && (Co == 16 || Co == 32)) || (Ci == 32 && (Co == 32 || Co == 64));
+}
+
+template <int CI, int CO, int WO, typename T>
+int launch_trans_fwd_lds(const T* x, T* y, uint8_t* mask, const float* k2, const float* b2, const float* k1,
+                         const float* b1, int N, int H, hipStream_t s) {
+  using G = TFw<CI, CO, WO>;
+  const long items = (long)N * (H / 2 / G::BRO);
+  int cus = cu_count();
+  if (cus <= 0) cus = 256;
+  const int grid = (int)std::max<long>(1, std::min<long>(items, 4L * cus));
+  hipLaunchKernelGGL((k_trans_fwd_lds<CI, CO, WO, T>), dim3(grid), dim3(64 * G::NW), G::LDS, s, x, y, mask, k2, b2, k1,
+                     b1, N, H);
+  ASR_LAUNCH_CHECK("k_trans_fwd_lds");
+  return ASR_OK;
+}
+
+int trans_fwd_lds(const void* x, void* y, uint8_t* mask, const float* k2, const float* b2, const float* k1,
+                  const float* b1, int act_bf16, int N, int H, int W, int Ci, int Co, hipStream_t s) {
+#define ASR_TFL(CI_, CO_, WO_)                                                                                       \
+  if (Ci == CI_ && Co == CO_ && W == 2 * WO_)                                                                        \
+    return act_bf16 ? launch_trans_fwd_lds<CI_, CO_, WO_>((const bf16*)x, (bf16*)y, mask, k2, b2, k1, b1, N, H, s)   \
+                    : launch_trans_fwd_lds<CI_, CO_, WO_>((const float*)x, (float*)y, mask, k2, b2, k1, b1, N, H, s);
+  ASR_TFL(16, 16, 16) ASR_TFL(16, 32, 16) ASR_TFL(32, 32, 16) ASR_TFL(32, 64, 16)
+  ASR_TFL(16, 16, 8) ASR_TFL(16, 32, 8) ASR_TFL(32, 32, 8) ASR_TFL(32, 64, 8)
+#undef ASR_TFL
+  return fail(ASR_E_UNSUPPORTED, "transition forward (LDS): Ci=%d Co=%d W=%d", Ci, Co, W);
+}
+
 // The stride-2 transition's input gradient with LDS-staged operands
 // (k_trans_dgrad_lds; even H and W).  dx[gy][gx] = sum over the taps with
 // gy - ky, gx - kx even of K2[ky][kx] dz[(gy-ky)/2][(gx-kx)/2] (+ K1 dy[gy/2][gx/2]
@@ -596,10 +719,10 @@ struct TDg {
   static_assert(NW % IT == 0, "transition dgrad (LDS): CI / 16 must divide 8");
 };
 
-template <int CI, int CO, int WO>
-__global__ __launch_bounds__(512) void k_trans_dgrad_lds(const float* __restrict__ dy, const uint8_t* __restrict__ mask,
+template <int CI, int CO, int WO, typename T>
+__global__ __launch_bounds__(512) void k_trans_dgrad_lds(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
                                                          const float* __restrict__ k2, const float* __restrict__ k1,
-                                                         float* __restrict__ dx, int N, int H) {
+                                                         T* __restrict__ dx, int N, int H) {
   using G = TDg<CI, CO, WO>;
   constexpr int W = G::W, BR = G::BR, SC = G::SC, PS = G::PS, OQ = G::OQ;
   extern __shared__ __attribute__((aligned(16))) float lds_td[];
@@ -677,33 +800,31 @@ __global__ __launch_bounds__(512) void k_trans_dgrad_lds(const float* __restrict
         }
       }
       mfma_f32_settle();
-      *(f32x4*)(dx + (((long)n * H + gy) * W + gx) * CI + 16 * it + 4 * g) = acc;
+      st4(dx + (((long)n * H + gy) * W + gx) * CI + 16 * it + 4 * g, acc);
     }
   }
 }
 
-bool trans_dgrad_lds_supported(int H, int W, int Ci, int Co, int S) {
-  if (S != 2 || H % 8 || (W != 32 && W != 16)) return false;
-  return (Ci == 16 && (Co == 16 || Co == 32)) || (Ci == 32 && (Co == 32 || Co == 64));
-}
 
-template <int CI, int CO, int WO>
-int launch_trans_dgrad_lds(const float* dy, const uint8_t* mask, const float* k2, const float* k1, float* dx, int N,
+template <int CI, int CO, int WO, typename T>
+int launch_trans_dgrad_lds(const T* dy, const uint8_t* mask, const float* k2, const float* k1, T* dx, int N,
                            int H, hipStream_t s) {
   using G = TDg<CI, CO, WO>;
   const long items = (long)N * (H / G::BR);
   int cus = cu_count();
   if (cus <= 0) cus = 256;
   const int grid = (int)std::max<long>(1, std::min<long>(items, 2L * cus));
-  hipLaunchKernelGGL((k_trans_dgrad_lds<CI, CO, WO>), dim3(grid), dim3(512), G::LDS, s, dy, mask, k2, k1, dx, N, H);
+  hipLaunchKernelGGL((k_trans_dgrad_lds<CI, CO, WO, T>), dim3(grid), dim3(512), G::LDS, s, dy, mask, k2, k1, dx, N, H);
   ASR_LAUNCH_CHECK("k_trans_dgrad_lds");
   return ASR_OK;
 }
 
-int trans_dgrad_lds(const float* dy, const uint8_t* mask, const float* k2, const float* k1, float* dx, int N, int H,
-                    int W, int Ci, int Co, hipStream_t s) {
-#define ASR_TDL(CI_, CO_, WO_) \
-  if (Ci == CI_ && Co == CO_ && W == 2 * WO_) return launch_trans_dgrad_lds<CI_, CO_, WO_>(dy, mask, k2, k1, dx, N, H, s);
+int trans_dgrad_lds(const void* dy, const uint8_t* mask, const float* k2, const float* k1, void* dx, int act_bf16, int N,
+                    int H, int W, int Ci, int Co, hipStream_t s) {
+#define ASR_TDL(CI_, CO_, WO_)                                                                                       \
+  if (Ci == CI_ && Co == CO_ && W == 2 * WO_)                                                                        \
+    return act_bf16 ? launch_trans_dgrad_lds<CI_, CO_, WO_>((const bf16*)dy, mask, k2, k1, (bf16*)dx, N, H, s)       \
+                    : launch_trans_dgrad_lds<CI_, CO_, WO_>((const float*)dy, mask, k2, k1, (float*)dx, N, H, s);
   ASR_TDL(16, 16, 16) ASR_TDL(16, 32, 16) ASR_TDL(32, 32, 16) ASR_TDL(32, 64, 16)
   ASR_TDL(16, 16, 8) ASR_TDL(16, 32, 8) ASR_TDL(32, 32, 8) ASR_TDL(32, 64, 8)
 #undef ASR_TDL
@@ -716,24 +837,29 @@ bool trans_wgrad_lds_supported(int H, int W, int Ci, int Co, int S) {
   return (Ci == 16 && (Co == 16 || Co == 32)) || (Ci == 32 && (Co == 32 || Co == 64));
 }
 
-template <int CI, int CO, int WO>
-int launch_trans_wgrad_lds(const float* dy, const uint8_t* mask, const float* x, float* part, int N, int H,
+template <int CI, int CO, int WO, typename T>
+int launch_trans_wgrad_lds(const T* dy, const uint8_t* mask, const T* x, float* part, int N, int H,
                            int max_rows, int* rows_out, hipStream_t s) {
   using G = TWg<CI, CO, WO>;
   const long items = (long)N * ((H / 2 + G::BRO - 1) / G::BRO);
   int cus = cu_count();
   if (cus <= 0) cus = 256;
   const int grid = (int)std::max<long>(1, std::min<long>({items, 2L * cus, (long)max_rows}));
-  hipLaunchKernelGGL((k_trans_wgrad_lds<CI, CO, WO>), dim3(grid), dim3(512), G::LDS, s, dy, mask, x, part, N, H);
+  hipLaunchKernelGGL((k_trans_wgrad_lds<CI, CO, WO, T>), dim3(grid), dim3(512), G::LDS, s, dy, mask, x, part, N, H);
   ASR_LAUNCH_CHECK("k_trans_wgrad_lds");
   *rows_out = grid;
   return ASR_OK;
 }
 
-int trans_wgrad_lds(const float* dy, const uint8_t* mask, const float* x, float* part, int N, int H, int W, int Ci,
-                    int Co, int max_rows, int* rows, hipStream_t s) {
-#define ASR_TWL(CI_, CO_, WO_) \
-  if (Ci == CI_ && Co == CO_ && W == 2 * WO_) return launch_trans_wgrad_lds<CI_, CO_, WO_>(dy, mask, x, part, N, H, max_rows, rows, s);
+// act_bf16: dy and x are the bf16 net's activations (bf16), else fp32
+int trans_wgrad_lds(const void* dy, const uint8_t* mask, const void* x, int act_bf16, float* part, int N, int H, int W,
+                    int Ci, int Co, int max_rows, int* rows, hipStream_t s) {
+#define ASR_TWL(CI_, CO_, WO_)                                                                                        \
+  if (Ci == CI_ && Co == CO_ && W == 2 * WO_)                                                                         \
+    return act_bf16 ? launch_trans_wgrad_lds<CI_, CO_, WO_>((const bf16*)dy, mask, (const bf16*)x, part, N, H,        \
+                                                            max_rows, rows, s)                                        \
+                    : launch_trans_wgrad_lds<CI_, CO_, WO_>((const float*)dy, mask, (const float*)x, part, N, H,      \
+                                                            max_rows, rows, s);
   ASR_TWL(16, 16, 16) ASR_TWL(16, 32, 16) ASR_TWL(32, 32, 16) ASR_TWL(32, 64, 16)
   ASR_TWL(16, 16, 8) ASR_TWL(16, 32, 8) ASR_TWL(32, 32, 8) ASR_TWL(32, 64, 8)
 #undef ASR_TWL
@@ -771,6 +897,7 @@ int trans_forward(const float* x, float* y, uint8_t* mask, const float* k2, cons
   const long tasks = (long)N * g.Ho * ((g.Wo + 15) / 16) * ((Co + 15) / 16);
   const long blocks = (tasks + 3) / 4;
   if (blocks > 0x7fffffffL) return fail(ASR_E_ARG, "transition: problem too large");
+  if (trans_lds_supported(H, W, Ci, Co, S)) return trans_fwd_lds(x, y, mask, k2, b2, k1, b1, 0, N, H, W, Ci, Co, s);
   if (trans_mfma(Ci, Co)) {
     hipLaunchKernelGGL(k_trans_fwd_mfma, dim3((unsigned)blocks), dim3(256), 0, s, x, y, mask, k2, b2, k1, b1, N, H,
                        W, Ci, Co, S, g.Ho, g.Wo, g.pt, g.pl);
@@ -790,12 +917,27 @@ size_t trans_ws_bytes(int N, int H, int W, int Ci, int Co, int S) {
   return align_up((size_t)nch * trans_param_floats(Ci, Co) * 4, 256);
 }
 
+// the bf16 nets' transition backward on the LDS kernels (trans_lds_supported shapes): dy, x and dx in bf16
+int trans_backward_bf16(const bf16* dy, const bf16* x, const uint8_t* mask, const float* k2, const float* k1, int N,
+                        int H, int W, int Ci, int Co, int S, bf16* dx, float* dparams, float* part, hipStream_t s) {
+  if (!trans_lds_supported(H, W, Ci, Co, S)) return fail(ASR_E_UNSUPPORTED, "transition (bf16): shape");
+  const TGeom g = tgeom(H, W, S);
+  ASR_TRY(trans_dgrad_lds(dy, mask, k2, k1, dx, 1, N, H, W, Ci, Co, s));
+  int ppc = 0;
+  int rows = trans_mfma_chunks(N, g.Ho, g.Wo, Ci, Co, &ppc);  // (the workspace's partial rows, trans_ws_bytes)
+  ASR_TRY(trans_wgrad_lds(dy, mask, x, 1, part, N, H, W, Ci, Co, rows, &rows, s));
+  const long ET = trans_param_floats(Ci, Co);
+  hipLaunchKernelGGL(k_sum_chunks, dim3((unsigned)((ET + 63) / 64)), dim3(256), 0, s, part, rows, ET, dparams);
+  ASR_LAUNCH_CHECK("k_sum_chunks");
+  return ASR_OK;
+}
+
 int trans_backward(const float* dy, const float* x, const uint8_t* mask, const float* k2, const float* k1, int N,
                    int H, int W, int Ci, int Co, int S, float* dx, float* dparams, float* part, hipStream_t s) {
   const TGeom g = tgeom(H, W, S);
   if (trans_mfma(Ci, Co)) {
-    if (dx && trans_dgrad_lds_supported(H, W, Ci, Co, S)) {
-      ASR_TRY(trans_dgrad_lds(dy, mask, k2, k1, dx, N, H, W, Ci, Co, s));
+    if (dx && trans_lds_supported(H, W, Ci, Co, S)) {
+      ASR_TRY(trans_dgrad_lds(dy, mask, k2, k1, dx, 0, N, H, W, Ci, Co, s));
     } else if (dx) {
       const long blocks = ((long)N * H * ((W + 15) / 16) * (Ci / 16) + 3) / 4;
       if (blocks > 0x7fffffffL) return fail(ASR_E_ARG, "transition: problem too large");
@@ -808,7 +950,7 @@ int trans_backward(const float* dy, const float* x, const uint8_t* mask, const f
       int chunks = trans_mfma_chunks(N, g.Ho, g.Wo, Ci, Co, &ppc);  // (the workspace's partial rows)
       const long ET = trans_param_floats(Ci, Co);
       if (trans_wgrad_lds_supported(H, W, Ci, Co, S)) {
-        ASR_TRY(trans_wgrad_lds(dy, mask, x, part, N, H, W, Ci, Co, chunks, &chunks, s));
+        ASR_TRY(trans_wgrad_lds(dy, mask, x, 0, part, N, H, W, Ci, Co, chunks, &chunks, s));
       } else {
         const long blocks = ((long)chunks * (Ci / 16) * (Co / 16) + 3) / 4;
         hipLaunchKernelGGL(k_trans_wgrad_mfma, dim3((unsigned)blocks), dim3(256), 0, s, dy, mask, x, part, N, H, W,
@@ -849,6 +991,7 @@ struct StageL {
   long off_t, off_blk;          // parameter offsets (floats)
   size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, act_t, mask_t, acts, masks, grp, slabs;  // workspace offsets
   size_t act_tb, xin32;  // bf16 nets: the transition's output in bf16, its input in fp32 (kept for the backward)
+  bool tdirect;          // bf16 nets: the transition on the LDS kernels in bf16 (no fp32 copies)
   long wstride;          // elements of one layer's W in wbuf (E fp32, or the bf16 MFMA pack)
   long grp_stride;   // floats per block of pass-1 group rows
   long slab_stride;  // floats per block of weight-gradient slabs
@@ -859,6 +1002,7 @@ struct SLayout {
   StageL st[ASR_STAGES_MAX];
   bool sep_bwd;
   bool bf;              // bf16 activations / block convs (asr_stages_config.dtype)
+  bool any_tconv;       // bf16 nets: a transition off the LDS kernels (fp32 copies and converts)
   int act_bytes;
   size_t t32a, t32b;    // bf16 nets: fp32 scratch of the transition backward (dy, dx)
   long off_c1k, off_c1b, off_fck, off_fcb, n_params, Pmax;
@@ -962,9 +1106,11 @@ SLayout stages_layout(const asr_stages_config* c) {
     g.wstride = L.bf ? asr_wpack_elems(g.C) : g.E;
     g.wbuf = take((size_t)std::max(g.L, 1) * g.wstride * L.act_bytes);
     g.wbuf_bwd = L.sep_bwd ? take((size_t)std::max(g.L, 1) * g.wstride * L.act_bytes) : 0;
-    g.act_t = g.S ? take((size_t)g.P * 4) : 0;
+    g.tdirect = L.bf && g.S && trans_lds_supported(g.Hp, g.Wp, g.Cp, g.C, g.S);
+    L.any_tconv = L.any_tconv || (L.bf && g.S && !g.tdirect);
+    g.act_t = g.S && !g.tdirect ? take((size_t)g.P * 4) : 0;
     g.act_tb = g.S && L.bf ? take((size_t)g.P * 2) : 0;
-    g.xin32 = g.S && L.bf ? take((size_t)c->N * g.Hp * g.Wp * g.Cp * 4) : 0;
+    g.xin32 = g.S && L.bf && !g.tdirect ? take((size_t)c->N * g.Hp * g.Wp * g.Cp * 4) : 0;
     g.mask_t = g.S ? take((size_t)g.P) : 0;
     g.acts = take((size_t)std::max(g.L, 1) * g.P * L.act_bytes);
     g.masks = take((size_t)std::max(g.L, 1) * g.mask_bytes);
@@ -987,8 +1133,8 @@ SLayout stages_layout(const asr_stages_config* c) {
   L.dB = take((size_t)L.Pmax * 4);
   L.cws = take(std::max<size_t>(L.cws_bytes, 256));
   L.tws = take(std::max<size_t>(L.tws_bytes, 256));
-  L.t32a = L.bf ? take((size_t)L.Pmax * 4) : 0;
-  L.t32b = L.bf ? take((size_t)L.Pmax * 4) : 0;
+  L.t32a = L.any_tconv ? take((size_t)L.Pmax * 4) : 0;
+  L.t32b = L.any_tconv ? take((size_t)L.Pmax * 4) : 0;
   const long E1 = 9L * c->Cin * c->C[0];
   L.sslabs = take((size_t)kMaxStemSlabs * (E1 + c->C[0]) * 4);
   L.sred_bytes = reduce_ws_bytes(kMaxStemSlabs, E1 + c->C[0]);
@@ -1007,7 +1153,13 @@ int stages_forward_impl(const asr_stages_config* c, const SLayout& L, const floa
   const void* x = b + L.act0;
   for (int si = 0; si < L.ns; ++si) {
     const StageL& g = L.st[si];
-    if (g.S) {
+    if (g.tdirect) {  // bf16 in, bf16 out
+      const float* pt = params + g.off_t;
+      const long e2 = 9L * g.Cp * g.C;
+      ASR_TRY(trans_fwd_lds(x, b + g.act_tb, (uint8_t*)(b + g.mask_t), pt, pt + e2, pt + e2 + g.C,
+                            pt + e2 + g.C + (long)g.Cp * g.C, 1, c->N, g.Hp, g.Wp, g.Cp, g.C, s));
+      x = b + g.act_tb;
+    } else if (g.S) {
       const float* pt = params + g.off_t;
       const long e2 = 9L * g.Cp * g.C;
       const float* xt = (const float*)x;
@@ -1183,7 +1335,11 @@ int asr_stages_forward_backward(const asr_stages_config* cfg, const float* param
       const float* pt = params + g.off_t;
       const long e2 = 9L * g.Cp * g.C;
       const long Pin = (long)N * g.Hp * g.Wp * g.Cp;
-      if (L.bf) {  // in fp32: dy converted up, the transition's kept fp32 input, dx converted back down
+      if (g.tdirect) {
+        ASR_TRY(trans_backward_bf16((const bf16*)d, (const bf16*)prev_out, (const uint8_t*)(b + g.mask_t), pt,
+                                    pt + e2 + g.C, N, g.Hp, g.Wp, g.Cp, g.C, g.S, (bf16*)e, grads + g.off_t,
+                                    (float*)(b + L.tws), s));
+      } else if (L.bf) {  // in fp32: dy converted up, the transition's kept fp32 input, dx converted back down
         float* dy32 = (float*)(b + L.t32a);
         float* dx32 = (float*)(b + L.t32b);
         ASR_TRY(convert_bf16_f32(d, dy32, g.P, 1, s));
