@@ -53,6 +53,16 @@ int convb_forward(const void* x, void* y, uint8_t* mask, const void* w, const fl
 int convb_backward(const void* dy, const uint8_t* mask, const void* x, const void* w, float h, float two_gamma, int N,
                    int H, int W, int C, void* dx, bool need_w, float* slabs, int* nslabs, hipStream_t s);
 int convert_bf16_f32(const void* src, void* dst, long n, int to_f32, hipStream_t s);
+// asr_deep16.hip: the C = 16, 32 x 32 bf16 stage as one fused forward / backward launch
+bool deep16_supported(int H, int W, int C);
+int deep16_forward(const void* x0, void* y0, long y_stride, uint8_t* mask0, long mask_stride, const void* wpack,
+                   const float* bias, long bias_stride, float h, int N, int L, bool store_all, hipStream_t s);
+size_t deep16_slab_bytes(int N, int L);
+int deep16_backward(void* dbufA, void* dbufB, const void* xs, long x_stride, const uint8_t* masks, long mask_stride,
+                    const void* wpack, float h, float two_gamma, int N, int L, float* slabs, int* slab_rows,
+                    int* dx0_in_b, hipStream_t s);
+// asr_theta.hip
+int reduce_slabs_to_groups(const float* slabs, int P, long ES, float* grp, hipStream_t s);
 // asr_api.hip
 int conv_backward_keep_slabs(const void* dy, const void* x, const uint8_t* mask, const void* w, float h, float gamma,
                              int N, int H, int W, int C, void* dx, void* ws, float* slabs, int* nsl, hipStream_t s);
@@ -992,6 +1002,8 @@ struct StageL {
   size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, act_t, mask_t, acts, masks, grp, slabs;  // workspace offsets
   size_t act_tb, xin32;  // bf16 nets: the transition's output in bf16, its input in fp32 (kept for the backward)
   bool tdirect;          // bf16 nets: the transition on the LDS kernels in bf16 (no fp32 copies)
+  bool deep;             // bf16 nets: a C = 16, 32 x 32 stage on the fused deep16 kernels (x0: its input slot,
+  size_t x0;             //   followed by the L outputs at stride P, as deep16 reads them)
   long wstride;          // elements of one layer's W in wbuf (E fp32, or the bf16 MFMA pack)
   long grp_stride;   // floats per block of pass-1 group rows
   long slab_stride;  // floats per block of weight-gradient slabs
@@ -1080,6 +1092,7 @@ SLayout stages_layout(const asr_stages_config* c) {
     g.P = (long)c->N * H * W * g.C;
     L.Pmax = std::max(L.Pmax, g.P);
     g.ntheta = theta_count(g.C, c->param_kind, c->antisymmetric);
+    g.deep = c->dtype == ASR_BF16 && g.L > 0 && deep16_supported(H, W, g.C);
     g.E = 9L * g.C * g.C;
     g.blk_stride = g.ntheta + g.C;
     g.mask_bytes = (long)align_up((size_t)asr_mask_bytes(c->N, H, W, g.C), 256);
@@ -1095,7 +1108,7 @@ SLayout stages_layout(const asr_stages_config* c) {
   po += c->num_classes;
   L.n_params = po;
   // workspace
-  L.act0 = take((size_t)c->N * c->H * c->W * c->C[0] * L.act_bytes);
+  if (!L.st[0].deep) L.act0 = take((size_t)c->N * c->H * c->W * c->C[0] * L.act_bytes);
   L.cws_bytes = 0;
   L.tws_bytes = 0;
   for (int s = 0; s < L.ns; ++s) {
@@ -1109,18 +1122,25 @@ SLayout stages_layout(const asr_stages_config* c) {
     g.tdirect = L.bf && g.S && trans_lds_supported(g.Hp, g.Wp, g.Cp, g.C, g.S);
     L.any_tconv = L.any_tconv || (L.bf && g.S && !g.tdirect);
     g.act_t = g.S && !g.tdirect ? take((size_t)g.P * 4) : 0;
-    g.act_tb = g.S && L.bf ? take((size_t)g.P * 2) : 0;
+    if (g.deep) {  // [x0 | x1 .. xL] contiguous; the stem or the transition writes x0 in place
+      g.x0 = take((size_t)(g.L + 1) * g.P * 2);
+      g.acts = g.x0 + (size_t)g.P * 2;
+      if (s == 0) L.act0 = g.x0;
+    }
+    g.act_tb = g.S && L.bf ? (g.deep && g.tdirect ? g.x0 : take((size_t)g.P * 2)) : 0;
     g.xin32 = g.S && L.bf && !g.tdirect ? take((size_t)c->N * g.Hp * g.Wp * g.Cp * 4) : 0;
     g.mask_t = g.S ? take((size_t)g.P) : 0;
-    g.acts = take((size_t)std::max(g.L, 1) * g.P * L.act_bytes);
+    if (!g.deep) g.acts = take((size_t)std::max(g.L, 1) * g.P * L.act_bytes);
     g.masks = take((size_t)std::max(g.L, 1) * g.mask_bytes);
     // every block keeps its slabs until the stage's one reduction launch: sized by the
     // grid the fp32 weight gradient runs at this shape, not by the 512-row maximum
-    g.slab_rows = f32_block_slab_rows(c->N, g.H, g.W, g.C);
+    // (deep16: its own slab rows per layer)
+    g.slab_rows = g.deep ? (int)(deep16_slab_bytes(c->N, 1) / ((size_t)(g.E + g.C) * 4))
+                         : f32_block_slab_rows(c->N, g.H, g.W, g.C);
     g.grp_stride = (long)reduce_groups(g.slab_rows) * (g.E + g.C);
     g.grp = take((size_t)std::max(g.L, 1) * g.grp_stride * 4);
     g.slab_stride = (long)g.slab_rows * (g.E + g.C);
-    g.slabs = take((size_t)g.L * g.slab_stride * 4);
+    g.slabs = take(g.deep ? deep16_slab_bytes(c->N, g.L) : (size_t)g.L * g.slab_stride * 4);
     if (g.L > 0) L.cws_bytes = std::max(L.cws_bytes, asr_conv_backward_workspace_bytes(c->N, g.H, g.W, g.C, ASR_F32));
     if (g.S) L.tws_bytes = std::max(L.tws_bytes, trans_ws_bytes(c->N, g.Hp, g.Wp, g.Cp, g.C, g.S));
   }
@@ -1181,6 +1201,14 @@ int stages_forward_impl(const asr_stages_config* c, const SLayout& L, const floa
     if (training && L.sep_bwd)
       ASR_TRY(asr_theta_to_w(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src_bwd), 0.f,
                              b + g.wbuf_bwd, g.wstride, wdt, s));
+    if (g.deep) {  // all L blocks in one launch, images resident in LDS
+      if (x != b + g.x0)
+        ASR_TRY(hip_check(hipMemcpyAsync(b + g.x0, x, (size_t)g.P * 2, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync"));
+      ASR_TRY(deep16_forward(b + g.x0, b + g.acts, g.P, (uint8_t*)(b + g.masks), g.mask_bytes, b + g.wbuf,
+                             params + g.off_blk + g.ntheta, g.blk_stride, c->h, c->N, g.L, true, s));
+      x = b + g.acts + (size_t)(g.L - 1) * g.P * 2;
+      continue;
+    }
     for (int l = 0; l < g.L; ++l) {
       unsigned char* y = b + g.acts + (size_t)l * g.P * L.act_bytes;
       uint8_t* mk = (uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes;
@@ -1309,7 +1337,18 @@ int asr_stages_forward_backward(const asr_stages_config* cfg, const float* param
     const unsigned char* chain_in = g.S ? b + (L.bf ? g.act_tb : g.act_t) : prev_out;
     const float gam = L.sep_bwd ? 0.f : cfg->gamma;
     int nsl = 0;
-    for (int l = g.L - 1; l >= 0; --l) {
+    if (g.deep) {  // all L blocks in one launch (dx resident in LDS), one slab set per layer
+      int rows = 0, in_b = 0;
+      ASR_TRY(deep16_backward(d, e, b + g.x0, g.P, (const uint8_t*)(b + g.masks), g.mask_bytes,
+                              b + (L.sep_bwd ? g.wbuf_bwd : g.wbuf), cfg->h, 2.f * gam, N, g.L,
+                              (float*)(b + g.slabs), &rows, &in_b, s));
+      if (rows != g.slab_rows) return fail(ASR_E_WORKSPACE, "asr_stages: deep16 slab rows %d != %d", rows, g.slab_rows);
+      if (in_b) std::swap(d, e);
+      ASR_TRY(reduce_slabs_to_groups((const float*)(b + g.slabs), g.L * rows, g.E + g.C, (float*)(b + g.grp), s));
+      ASR_TRY(project_layers((float*)(b + g.grp), g.grp_stride, reduce_groups(rows), g.E, g.C,
+                             (const int32_t*)(b + g.theta_dst), g.ntheta, g.L, grads + g.off_blk, g.blk_stride, s));
+    }
+    for (int l = g.deep ? -1 : g.L - 1; l >= 0; --l) {
       const unsigned char* x_in = l == 0 ? chain_in : b + g.acts + (size_t)(l - 1) * g.P * ab;
       const unsigned char* wl = b + (L.sep_bwd ? g.wbuf_bwd : g.wbuf) + (size_t)l * g.wstride * ab;
       const uint8_t* mk = (const uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes;
@@ -1325,10 +1364,10 @@ int asr_stages_forward_backward(const asr_stages_config* cfg, const float* param
                     g.slab_rows);
       std::swap(d, e);
     }
-    if (g.L > 0)
+    if (g.L > 0 && !g.deep)
       ASR_TRY(reduce_slab_layers((const float*)(b + g.slabs), g.slab_stride, nsl, g.E + g.C, (float*)(b + g.grp),
                                  g.grp_stride, g.L, s));
-    if (g.L > 0)
+    if (g.L > 0 && !g.deep)
       ASR_TRY(project_layers((float*)(b + g.grp), g.grp_stride, reduce_groups(nsl), g.E, g.C,
                              (const int32_t*)(b + g.theta_dst), g.ntheta, g.L, grads + g.off_blk, g.blk_stride, s));
     if (g.S) {
