@@ -668,7 +668,12 @@ int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, i
 // ===========================================================================
 template <int C, int W_>
 struct BfBand {
-  static constexpr int OT = C / 16, W = W_, TW = W + 2, BR = 4, TILEE = (BR + 2) * TW * C;
+#ifndef ASR_PIXPAD
+#define ASR_PIXPAD 8
+#endif
+  // PS: a pixel's elements in the LDS tiles, padded so the 16 lanes of a 16-B read (16 consecutive
+  // pixels) fall on distinct banks (unpadded, C = 64 put them on 2 bank groups: 8-way conflicts)
+  static constexpr int OT = C / 16, W = W_, TW = W + 2, BR = 4, PS = C + ASR_PIXPAD, TILEE = (BR + 2) * TW * PS;
   static constexpr int T = BR * W / 16;  // 16-pixel tiles per band
   static constexpr int WPT = 4 / OT;     // waves sharing an o-tile
   static constexpr int KS = (9 * C + 31) / 32;
@@ -716,7 +721,7 @@ __global__ __launch_bounds__(256) void k_convb(const bf16* __restrict__ xin, bf1
   constexpr int NCH = (BR + 2) * TW * C8, NPT = (NCH + 255) / 256;
   __shared__ __attribute__((aligned(16))) bf16 tile[G::TILEE];
   // backward: the band's own rows of dy unmasked (the epilogue's dy term), beside the dz tile
-  __shared__ __attribute__((aligned(16))) bf16 dyc[MODE == B_EULER ? BR * W * C : 8];
+  __shared__ __attribute__((aligned(16))) bf16 dyc[MODE == B_EULER ? BR * W * G::PS : 8];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
   const int ot = wave % OT, rw = wave / OT;
   const int nb = (H + BR - 1) / BR;
@@ -755,12 +760,13 @@ __global__ __launch_bounds__(256) void k_convb(const bf16* __restrict__ xin, bf1
     for (int k = 0; k < NPT; ++k) {
       const int i = tid + 256 * k;
       if (i >= NCH) break;
+      const int r = i / (TW * C8), rem = i % (TW * C8), col = rem / C8, c8 = rem % C8;
+      bf16* dst = tile + (r * TW + col) * G::PS + 8 * c8;
       if constexpr (MODE == B_EULER) {  // the tile gets dz = dy & mask; the band's rows keep dy
-        *(uint4*)(tile + 8 * i) = mask8_bf16(pf[k], pm[k]);
-        const int r = i / (TW * C8), rem = i % (TW * C8), col = rem / C8;
-        if (r >= 1 && r <= BR && col >= 1 && col <= W) *(uint4*)(dyc + (((r - 1) * W + col - 1) * C8 + rem % C8) * 8) = pf[k];
+        *(uint4*)dst = mask8_bf16(pf[k], pm[k]);
+        if (r >= 1 && r <= BR && col >= 1 && col <= W) *(uint4*)(dyc + ((r - 1) * W + col - 1) * G::PS + 8 * c8) = pf[k];
       } else {
-        *(uint4*)(tile + 8 * i) = pf[k];
+        *(uint4*)dst = pf[k];
       }
     }
     __syncthreads();
@@ -777,14 +783,14 @@ __global__ __launch_bounds__(256) void k_convb(const bf16* __restrict__ xin, bf1
       for (int ks = 0; ks < KS; ++ks) {
         const int kap = 32 * ks + 8 * g;
         const int t = min(kap / C, 8), i0c = kap - (kap / C) * C;  // (C = 16, last k-step: tap 9 pads A with zeros)
-        const uint4 bv = *(const uint4*)(tile + ((r + t / 3) * TW + px + t % 3) * C + i0c);
+        const uint4 bv = *(const uint4*)(tile + ((r + t / 3) * TW + px + t % 3) * G::PS + i0c);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], __builtin_bit_cast(bf16x8, bv), acc, 0, 0, 0);
       }
       mfma_bf16_settle();  // (the epilogue branches: every path must see the result's wait states)
       const bool ok = y0 + r < H;
       const long pix = ((long)n * H + y0 + r) * W + px;
       const long oi = pix * C + 16 * ot + 4 * g;  // this lane's 4 channels
-      const uint2 cw = *(const uint2*)(tile + ((r + 1) * TW + px + 1) * C + 16 * ot + 4 * g);  // x or dz at the pixel
+      const uint2 cw = *(const uint2*)(tile + ((r + 1) * TW + px + 1) * G::PS + 16 * ot + 4 * g);  // x or dz at the pixel
       const float ctr[4] = {__uint_as_float(cw.x << 16), __uint_as_float(cw.x & 0xffff0000u),
                             __uint_as_float(cw.y << 16), __uint_as_float(cw.y & 0xffff0000u)};
       float v[4];
@@ -803,7 +809,7 @@ __global__ __launch_bounds__(256) void k_convb(const bf16* __restrict__ xin, bf1
           if (g == 0 && ok) *(uint16_t*)(mask + (pix * C + 16 * ot) / 8) = (uint16_t)m;
         }
       } else {  // B_EULER: the tile holds dz = dy & mask
-        const uint2 dw = *(const uint2*)(dyc + (r * W + px) * C + 16 * ot + 4 * g);
+        const uint2 dw = *(const uint2*)(dyc + (r * W + px) * G::PS + 16 * ot + 4 * g);
         const float d0[4] = {__uint_as_float(dw.x << 16), __uint_as_float(dw.x & 0xffff0000u),
                              __uint_as_float(dw.y << 16), __uint_as_float(dw.y & 0xffff0000u)};
         const float hg = h * two_gamma;
@@ -1076,6 +1082,239 @@ int convb_backward(const void* dy, const uint8_t* mask, const void* x, const voi
   ASR_WB(64, 16) ASR_WB(64, 8)
 #undef ASR_WB
   return fail(ASR_E_UNSUPPORTED, "conv bf16 backward (any width): C=%d W=%d", C, W);
+}
+
+// ===========================================================================
+// Image-resident bf16 stages (k_stagef / k_stageb): all L Euler blocks of a
+// 16 x 16 x 32 or 8 x 8 x 64 stage in one launch, a workgroup per image with
+// the image in LDS (20.3 / 12.5 KiB with its zero halo), as the deep16 kernels
+// do for 32 x 32 x 16.  The conv is k_convb's (v_mfma_f32_16x16x32_bf16, the
+// layer's A fragments in registers, B one 16-B LDS read per k-step); between
+// layers only LDS traffic and a barrier.
+//   forward: ping-pong image buffers; each layer's y and relu mask to HBM (the
+//     backward reads them), y into the other buffer;
+//   backward (input gradient only): dy in LDS, dz = dy & mask_l into the halo
+//     tile, dx = dy - h conv(dz) + 2 gamma h dz written over dy in place (a lane
+//     reads and writes only its own pixel's channels); the gradient entering
+//     each layer below the top goes to HBM for the weight gradient (k_wgradb
+//     per layer, unchanged), dx_0 at the end.
+// ===========================================================================
+template <int C, int W_>
+struct StImg {
+  static constexpr int W = W_, H = W_, TW = W + 2, OT = C / 16, WPT = 4 / OT, KS = (9 * C + 31) / 32, C8 = C / 8;
+  static constexpr int T = H * W / 16;              // 16-pixel tiles per image
+  static constexpr int PS = C + ASR_PIXPAD;          // a pixel's elements in LDS (padded, as BfBand)
+  static constexpr int IMGE = (H + 2) * TW * PS;    // elements of a haloed image tile
+  static constexpr int NCH = H * W * C8;            // 16-B chunks of an image
+  static_assert((W == 16 && C == 32) || (W == 8 && C == 64) || (W == 8 && C == 32),
+                "image-resident stage: 16 x 16 x 32, 8 x 8 x 32 or 8 x 8 x 64");
+};
+
+template <int C, int W>
+__device__ __forceinline__ int st_off(int r, int c) {  // element offset of interior pixel (r, c) in a haloed tile
+  return ((r + 1) * StImg<C, W>::TW + c + 1) * StImg<C, W>::PS;
+}
+
+// an LDS-only workgroup barrier: the layers' global stores (y, masks, dy) stay in flight across it
+// (__syncthreads waits for them too: a full store round trip per layer)
+__device__ __forceinline__ void st_barrier() {
+#ifdef ASR_ST_SYNC
+  __syncthreads();
+#else
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
+}
+
+template <int C, int W>
+__global__ __launch_bounds__(256) void k_stagef(const bf16* __restrict__ x0, bf16* __restrict__ ys, long y_stride,
+                                                uint8_t* __restrict__ masks, long mask_stride,
+                                                const bf16* __restrict__ wpack, long w_stride,
+                                                const float* __restrict__ bias, long bias_stride, float h, int N,
+                                                int L) {
+  using G = StImg<C, W>;
+  constexpr int TW = G::TW, KS = G::KS, OT = G::OT;
+  __shared__ __attribute__((aligned(16))) bf16 img[2][G::IMGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
+  const int ot = wave % OT, rw = wave / OT;
+  for (int i = tid; i < 2 * G::IMGE / 8; i += 256) ((uint4*)&img[0][0])[i] = make_uint4(0u, 0u, 0u, 0u);
+  st_barrier();
+  for (int n = blockIdx.x; n < N; n += gridDim.x) {
+    const long ib = (long)n * G::H * W * C;
+    for (int i = tid; i < G::NCH; i += 256) {
+      const int px = i / G::C8, c8 = i % G::C8;
+      *(uint4*)(&img[0][0] + st_off<C, W>(px / W, px % W) + 8 * c8) = *(const uint4*)(x0 + ib + 8L * i);
+    }
+    st_barrier();
+    for (int l = 0; l < L; ++l) {
+      const bf16* cur = &img[l & 1][0];
+      bf16* nxt = &img[(l & 1) ^ 1][0];
+      bf16x8 A[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        A[ks] = *(const bf16x8*)(wpack + (long)l * w_stride + (((long)ot * KS + ks) * 64 + lane) * 8);
+      const f32x4 bz = *(const f32x4*)(bias + (long)l * bias_stride + 16 * ot + 4 * g);
+      bf16* yl = ys + (long)l * y_stride + ib;
+      uint8_t* ml = masks + (long)l * mask_stride;
+      // two tiles per pass: two independent MFMA accumulate chains per wave
+      auto epi = [&](int p, const f32x4& acc) {
+        const int r = p / W, px = p % W;
+        const int co = st_off<C, W>(r, px) + 16 * ot + 4 * g;
+        const uint2 cw = *(const uint2*)(cur + co);
+        const float ctr[4] = {__uint_as_float(cw.x << 16), __uint_as_float(cw.x & 0xffff0000u),
+                              __uint_as_float(cw.y << 16), __uint_as_float(cw.y & 0xffff0000u)};
+        float v[4];
+        unsigned nib = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          nib |= (acc[e] > 0.f ? 1u : 0u) << e;
+          v[e] = fmaf(h, fmaxf(acc[e], 0.f), ctr[e]);
+        }
+        const uint2 yw = make_uint2(pk_bf16_rn(v[0], v[1]), pk_bf16_rn(v[2], v[3]));
+        *(uint2*)(nxt + co) = yw;
+        const long pix = (long)n * G::H * W + p;
+        *(uint2*)(yl + (long)p * C + 16 * ot + 4 * g) = yw;
+        unsigned m = nib << (4 * g);
+        m |= (unsigned)__shfl_xor((int)m, 16, 64);
+        m |= (unsigned)__shfl_xor((int)m, 32, 64);
+        if (g == 0) *(uint16_t*)(ml + (pix * C + 16 * ot) / 8) = (uint16_t)m;
+      };
+#pragma unroll 1
+      for (int j = 0; j < G::T / G::WPT; j += 2) {
+        const int p0 = 16 * (rw + j * G::WPT) + lx, p1 = 16 * (rw + (j + 1) * G::WPT) + lx;
+        const int r0 = p0 / W, x0p = p0 % W, r1 = p1 / W, x1p = p1 % W;
+        f32x4 acc0 = bz, acc1 = bz;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int kap = 32 * ks + 8 * g;
+          const int t = min(kap / C, 8), i0c = kap - (kap / C) * C;
+          const uint4 b0 = *(const uint4*)(cur + ((r0 + t / 3) * TW + x0p + t % 3) * G::PS + i0c);
+          const uint4 b1 = *(const uint4*)(cur + ((r1 + t / 3) * TW + x1p + t % 3) * G::PS + i0c);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], __builtin_bit_cast(bf16x8, b0), acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], __builtin_bit_cast(bf16x8, b1), acc1, 0, 0, 0);
+        }
+        mfma_bf16_settle();
+        epi(p0, acc0);
+        epi(p1, acc1);
+      }
+      st_barrier();  // layer l's outputs complete in nxt; cur free
+    }
+  }
+}
+
+template <int C, int W>
+__global__ __launch_bounds__(256) void k_stageb(const bf16* __restrict__ dyL, bf16* __restrict__ dys, long d_stride,
+                                                bf16* __restrict__ dx0, const uint8_t* __restrict__ masks,
+                                                long mask_stride, const bf16* __restrict__ wpack, long w_stride,
+                                                float h, float two_gamma, int N, int L) {
+  using G = StImg<C, W>;
+  constexpr int TW = G::TW, KS = G::KS, OT = G::OT;
+  __shared__ __attribute__((aligned(16))) bf16 dzt[G::IMGE];          // dz with a zero halo
+  __shared__ __attribute__((aligned(16))) bf16 dyt[G::H * W * G::PS];  // dy (becomes dx) of the image
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
+  const int ot = wave % OT, rw = wave / OT;
+  const float hg = h * two_gamma;
+  for (int i = tid; i < G::IMGE / 8; i += 256) ((uint4*)dzt)[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (int n = blockIdx.x; n < N; n += gridDim.x) {
+    const long ib = (long)n * G::H * W * C;
+    for (int i = tid; i < G::NCH; i += 256)
+      *(uint4*)(dyt + (i / G::C8) * G::PS + 8 * (i % G::C8)) = *(const uint4*)(dyL + ib + 8L * i);
+    for (int l = L - 1; l >= 0; --l) {
+      bf16x8 A[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        A[ks] = *(const bf16x8*)(wpack + (long)l * w_stride + (((long)ot * KS + ks) * 64 + lane) * 8);
+      st_barrier();  // dy of layer l complete (loaded, or the previous layer's dx); dz free
+      const uint8_t* ml = masks + (long)l * mask_stride;
+      for (int i = tid; i < G::NCH; i += 256) {
+        const int px = i / G::C8, c8 = i % G::C8;
+        const uint4 v = *(const uint4*)(dyt + px * G::PS + 8 * c8);
+        if (l < L - 1) *(uint4*)(dys + (long)l * d_stride + ib + 8L * i) = v;  // the gradient entering layer l
+        *(uint4*)(dzt + st_off<C, W>(px / W, px % W) + 8 * c8) = mask8_bf16(v, ml[(ib + 8L * i) >> 3]);
+      }
+      st_barrier();  // dz complete
+      auto epi = [&](int p, const f32x4& acc) {
+        const int r = p / W, px = p % W;
+        const int cz = st_off<C, W>(r, px) + 16 * ot + 4 * g, cy = p * G::PS + 16 * ot + 4 * g;
+        const uint2 zw = *(const uint2*)(dzt + cz), dw = *(const uint2*)(dyt + cy);
+        const float z4[4] = {__uint_as_float(zw.x << 16), __uint_as_float(zw.x & 0xffff0000u),
+                             __uint_as_float(zw.y << 16), __uint_as_float(zw.y & 0xffff0000u)};
+        const float d4[4] = {__uint_as_float(dw.x << 16), __uint_as_float(dw.x & 0xffff0000u),
+                             __uint_as_float(dw.y << 16), __uint_as_float(dw.y & 0xffff0000u)};
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaf(hg, z4[e], fmaf(-h, acc[e], d4[e]));
+        *(uint2*)(dyt + cy) = make_uint2(pk_bf16_rn(v[0], v[1]), pk_bf16_rn(v[2], v[3]));  // (own pixel, own channels)
+      };
+#pragma unroll 1
+      for (int j = 0; j < G::T / G::WPT; j += 2) {
+        const int p0 = 16 * (rw + j * G::WPT) + lx, p1 = 16 * (rw + (j + 1) * G::WPT) + lx;
+        const int r0 = p0 / W, x0p = p0 % W, r1 = p1 / W, x1p = p1 % W;
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int kap = 32 * ks + 8 * g;
+          const int t = min(kap / C, 8), i0c = kap - (kap / C) * C;
+          const uint4 b0 = *(const uint4*)(dzt + ((r0 + t / 3) * TW + x0p + t % 3) * G::PS + i0c);
+          const uint4 b1 = *(const uint4*)(dzt + ((r1 + t / 3) * TW + x1p + t % 3) * G::PS + i0c);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], __builtin_bit_cast(bf16x8, b0), acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], __builtin_bit_cast(bf16x8, b1), acc1, 0, 0, 0);
+        }
+        mfma_bf16_settle();
+        epi(p0, acc0);
+        epi(p1, acc1);
+      }
+    }
+    st_barrier();  // dx_0 complete
+    for (int i = tid; i < G::NCH; i += 256)
+      *(uint4*)(dx0 + ib + 8L * i) = *(const uint4*)(dyt + (i / G::C8) * G::PS + 8 * (i % G::C8));
+    st_barrier();  // (dyt reused by the next image)
+  }
+}
+
+bool stage_img_supported(int H, int W, int C) {
+  return H == W && ((W == 16 && C == 32) || (W == 8 && C == 64) || (W == 8 && C == 32));
+}
+
+// the image-resident stage forward: x0 [N][H][W][C] -> ys (L layers at y_stride), masks (L at mask_stride)
+int stage_img_forward(const void* x0, void* ys, long y_stride, uint8_t* masks, long mask_stride, const void* w,
+                      long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C, int L,
+                      hipStream_t s) {
+  if (!stage_img_supported(H, W, C)) return fail(ASR_E_UNSUPPORTED, "image-resident stage: H=%d W=%d C=%d", H, W, C);
+  const unsigned grid = (unsigned)std::max(1, N);
+#define ASR_SF(CC, WW)                                                                                        \
+  if (C == CC && W == WW) {                                                                                   \
+    hipLaunchKernelGGL((k_stagef<CC, WW>), dim3(grid), dim3(256), 0, s, (const bf16*)x0, (bf16*)ys, y_stride, \
+                       masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, L);             \
+    ASR_LAUNCH_CHECK("k_stagef");                                                                             \
+    return ASR_OK;                                                                                            \
+  }
+  ASR_SF(32, 16) ASR_SF(64, 8) ASR_SF(32, 8)
+#undef ASR_SF
+  return fail(ASR_E_UNSUPPORTED, "image-resident stage: C=%d W=%d", C, W);
+}
+
+// its backward (input gradient): dyL -> dx0; dys: the gradient entering layers 0 .. L-2 (d_stride apart)
+int stage_img_backward(const void* dyL, void* dys, long d_stride, void* dx0, const uint8_t* masks, long mask_stride,
+                       const void* w, long w_stride, float h, float two_gamma, int N, int H, int W, int C, int L,
+                       hipStream_t s) {
+  if (!stage_img_supported(H, W, C)) return fail(ASR_E_UNSUPPORTED, "image-resident stage: H=%d W=%d C=%d", H, W, C);
+  const unsigned grid = (unsigned)std::max(1, N);
+#define ASR_SB(CC, WW)                                                                                           \
+  if (C == CC && W == WW) {                                                                                      \
+    hipLaunchKernelGGL((k_stageb<CC, WW>), dim3(grid), dim3(256), 0, s, (const bf16*)dyL, (bf16*)dys, d_stride,  \
+                       (bf16*)dx0, masks, mask_stride, (const bf16*)w, w_stride, h, two_gamma, N, L);             \
+    ASR_LAUNCH_CHECK("k_stageb");                                                                                \
+    return ASR_OK;                                                                                               \
+  }
+  ASR_SB(32, 16) ASR_SB(64, 8) ASR_SB(32, 8)
+#undef ASR_SB
+  return fail(ASR_E_UNSUPPORTED, "image-resident stage: C=%d W=%d", C, W);
+}
+
+// the weight-gradient slabs of one layer at any width (k_wgradb), for the image-resident stage's layers
+int wgradb_layer(const void* x, const void* dy, const uint8_t* mask, float h, int N, int H, int W, int C, float* slabs,
+                 int* nslabs, hipStream_t s) {
+  return convb_backward(dy, mask, x, nullptr, h, 0.f, N, H, W, C, nullptr, true, slabs, nslabs, s);
 }
 
 // elementwise bf16 <-> fp32 (the multi-stage bf16 net's transitions run in fp32)

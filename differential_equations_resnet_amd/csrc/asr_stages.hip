@@ -53,6 +53,15 @@ int convb_forward(const void* x, void* y, uint8_t* mask, const void* w, const fl
 int convb_backward(const void* dy, const uint8_t* mask, const void* x, const void* w, float h, float two_gamma, int N,
                    int H, int W, int C, void* dx, bool need_w, float* slabs, int* nslabs, hipStream_t s);
 int convert_bf16_f32(const void* src, void* dst, long n, int to_f32, hipStream_t s);
+bool stage_img_supported(int H, int W, int C);
+int stage_img_forward(const void* x0, void* ys, long y_stride, uint8_t* masks, long mask_stride, const void* w,
+                      long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C, int L,
+                      hipStream_t s);
+int stage_img_backward(const void* dyL, void* dys, long d_stride, void* dx0, const uint8_t* masks, long mask_stride,
+                       const void* w, long w_stride, float h, float two_gamma, int N, int H, int W, int C, int L,
+                       hipStream_t s);
+int wgradb_layer(const void* x, const void* dy, const uint8_t* mask, float h, int N, int H, int W, int C, float* slabs,
+                 int* nslabs, hipStream_t s);
 // asr_deep16.hip: the C = 16, 32 x 32 bf16 stage as one fused forward / backward launch
 bool deep16_supported(int H, int W, int C);
 int deep16_forward(const void* x0, void* y0, long y_stride, uint8_t* mask0, long mask_stride, const void* wpack,
@@ -1004,6 +1013,8 @@ struct StageL {
   bool tdirect;          // bf16 nets: the transition on the LDS kernels in bf16 (no fp32 copies)
   bool deep;             // bf16 nets: a C = 16, 32 x 32 stage on the fused deep16 kernels (x0: its input slot,
   size_t x0;             //   followed by the L outputs at stride P, as deep16 reads them)
+  bool img;              // bf16 nets: a 16 x 16 x 32 / 8 x 8 x 64 stage on the image-resident kernels
+  size_t dys;            //   its backward's per-layer input gradients (layers 0 .. L-2)
   long wstride;          // elements of one layer's W in wbuf (E fp32, or the bf16 MFMA pack)
   long grp_stride;   // floats per block of pass-1 group rows
   long slab_stride;  // floats per block of weight-gradient slabs
@@ -1093,6 +1104,11 @@ SLayout stages_layout(const asr_stages_config* c) {
     L.Pmax = std::max(L.Pmax, g.P);
     g.ntheta = theta_count(g.C, c->param_kind, c->antisymmetric);
     g.deep = c->dtype == ASR_BF16 && g.L > 0 && deep16_supported(H, W, g.C);
+#ifndef ASR_NO_STAGE_IMG
+    g.img = c->dtype == ASR_BF16 && g.L > 0 && !g.deep && stage_img_supported(H, W, g.C);
+#else
+    g.img = false;
+#endif
     g.E = 9L * g.C * g.C;
     g.blk_stride = g.ntheta + g.C;
     g.mask_bytes = (long)align_up((size_t)asr_mask_bytes(c->N, H, W, g.C), 256);
@@ -1132,6 +1148,7 @@ SLayout stages_layout(const asr_stages_config* c) {
     g.mask_t = g.S ? take((size_t)g.P) : 0;
     if (!g.deep) g.acts = take((size_t)std::max(g.L, 1) * g.P * L.act_bytes);
     g.masks = take((size_t)std::max(g.L, 1) * g.mask_bytes);
+    g.dys = g.img && g.L > 1 ? take((size_t)(g.L - 1) * g.P * 2) : 0;
     // every block keeps its slabs until the stage's one reduction launch: sized by the
     // grid the fp32 weight gradient runs at this shape, not by the 512-row maximum
     // (deep16: its own slab rows per layer)
@@ -1201,6 +1218,12 @@ int stages_forward_impl(const asr_stages_config* c, const SLayout& L, const floa
     if (training && L.sep_bwd)
       ASR_TRY(asr_theta_to_w(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src_bwd), 0.f,
                              b + g.wbuf_bwd, g.wstride, wdt, s));
+    if (g.img) {  // all L blocks in one launch, a workgroup per image
+      ASR_TRY(stage_img_forward(x, b + g.acts, g.P, (uint8_t*)(b + g.masks), g.mask_bytes, b + g.wbuf, g.wstride,
+                                params + g.off_blk + g.ntheta, g.blk_stride, c->h, c->N, g.H, g.W, g.C, g.L, s));
+      x = b + g.acts + (size_t)(g.L - 1) * g.P * 2;
+      continue;
+    }
     if (g.deep) {  // all L blocks in one launch, images resident in LDS
       if (x != b + g.x0)
         ASR_TRY(hip_check(hipMemcpyAsync(b + g.x0, x, (size_t)g.P * 2, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync"));
@@ -1348,7 +1371,21 @@ int asr_stages_forward_backward(const asr_stages_config* cfg, const float* param
       ASR_TRY(project_layers((float*)(b + g.grp), g.grp_stride, reduce_groups(rows), g.E, g.C,
                              (const int32_t*)(b + g.theta_dst), g.ntheta, g.L, grads + g.off_blk, g.blk_stride, s));
     }
-    for (int l = g.deep ? -1 : g.L - 1; l >= 0; --l) {
+    if (g.img) {  // input gradients in one launch; then each layer's weight gradient from its stored input gradient
+      ASR_TRY(stage_img_backward(d, b + g.dys, g.P, e, (const uint8_t*)(b + g.masks), g.mask_bytes,
+                                 b + (L.sep_bwd ? g.wbuf_bwd : g.wbuf), g.wstride, cfg->h, 2.f * gam, N, g.H, g.W, g.C,
+                                 g.L, s));
+      for (int l = 0; l < g.L; ++l) {
+        const unsigned char* x_in = l == 0 ? chain_in : b + g.acts + (size_t)(l - 1) * g.P * ab;
+        const unsigned char* dyl = l == g.L - 1 ? d : b + g.dys + (size_t)l * g.P * 2;
+        ASR_TRY(wgradb_layer(x_in, dyl, (const uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes, cfg->h, N, g.H, g.W,
+                             g.C, (float*)(b + g.slabs) + (size_t)l * g.slab_stride, &nsl, s));
+        if (nsl > g.slab_rows)
+          return fail(ASR_E_WORKSPACE, "asr_stages: %d slab rows > the workspace's %d", nsl, g.slab_rows);
+      }
+      std::swap(d, e);
+    }
+    for (int l = (g.deep || g.img) ? -1 : g.L - 1; l >= 0; --l) {
       const unsigned char* x_in = l == 0 ? chain_in : b + g.acts + (size_t)(l - 1) * g.P * ab;
       const unsigned char* wl = b + (L.sep_bwd ? g.wbuf_bwd : g.wbuf) + (size_t)l * g.wstride * ab;
       const uint8_t* mk = (const uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes;
