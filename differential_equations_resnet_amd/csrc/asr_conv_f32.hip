@@ -882,8 +882,14 @@ __device__ __forceinline__ s16x4 tr4(const bf16* p) {
 template <int C, int W>
 __global__ __launch_bounds__((WgB<C, W>::NTH)) void k_wgradb(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                            const uint8_t* __restrict__ dmask, int N, int H, float h,
-                                                           float* __restrict__ slabs) {
+                                                           float* __restrict__ slabs, long x_stride, long dy_stride,
+                                                           long m_stride, long s_stride) {
   using G = WgB<C, W>;
+  // several layers in one launch: blockIdx.y is the layer (strides in elements / bytes / floats)
+  x += blockIdx.y * x_stride;
+  dy += blockIdx.y * dy_stride;
+  dmask += blockIdx.y * m_stride;
+  slabs += blockIdx.y * s_stride;
   constexpr int TW = G::TW, BR = G::BR, NO = G::NO, OT = G::OT, E = 9 * C * C;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_wb[];
   bf16* xt = (bf16*)lds_wb;               // [BR+2][TW][C] (chunk-swizzled per pixel)
@@ -1024,7 +1030,8 @@ __global__ __launch_bounds__((WgB<C, W>::NTH)) void k_wgradb(const bf16* __restr
 
 template <int C, int W>
 static int launch_wgradb(const bf16* x, const bf16* dy, const uint8_t* mask, int N, int H, float h, float* slabs,
-                         int* nslabs, hipStream_t s) {
+                         int* nslabs, hipStream_t s, int layers = 1, long x_stride = 0, long dy_stride = 0,
+                         long m_stride = 0, long s_stride = 0) {
   using G = WgB<C, W>;
   const long items = (long)N * ((H + G::BR - 1) / G::BR);
   // at most the fp32 wgrad's grid: the rows the workspaces size per block (f32_block_slab_rows)
@@ -1039,7 +1046,8 @@ static int launch_wgradb(const bf16* x, const bf16* dy, const uint8_t* mask, int
 #endif
   constexpr int minb = C == 16 ? ASR_WGB_B16 : C == 32 ? ASR_WGB_B32 : ASR_WGB_B64;
   const int grid = (int)std::max<long>(1, std::min<long>((items + minb - 1) / minb, wgrad32_grid<C, W>(N, H)));
-  hipLaunchKernelGGL((k_wgradb<C, W>), dim3(grid), dim3(G::NTH), G::LDS, s, x, dy, mask, N, H, h, slabs);
+  hipLaunchKernelGGL((k_wgradb<C, W>), dim3(grid, layers), dim3(G::NTH), G::LDS, s, x, dy, mask, N, H, h, slabs,
+                     x_stride, dy_stride, m_stride, s_stride);
   ASR_LAUNCH_CHECK("k_wgradb");
   *nslabs = grid;
   return ASR_OK;
@@ -1228,7 +1236,7 @@ __global__ __launch_bounds__(256) void k_stageb(const bf16* __restrict__ dyL, bf
       for (int i = tid; i < G::NCH; i += 256) {
         const int px = i / G::C8, c8 = i % G::C8;
         const uint4 v = *(const uint4*)(dyt + px * G::PS + 8 * c8);
-        if (l < L - 1) *(uint4*)(dys + (long)l * d_stride + ib + 8L * i) = v;  // the gradient entering layer l
+        *(uint4*)(dys + (long)l * d_stride + ib + 8L * i) = v;  // the gradient entering layer l (its wgrad's dy)
         *(uint4*)(dzt + st_off<C, W>(px / W, px % W) + 8 * c8) = mask8_bf16(v, ml[(ib + 8L * i) >> 3]);
       }
       st_barrier();  // dz complete
@@ -1293,7 +1301,7 @@ int stage_img_forward(const void* x0, void* ys, long y_stride, uint8_t* masks, l
   return fail(ASR_E_UNSUPPORTED, "image-resident stage: C=%d W=%d", C, W);
 }
 
-// its backward (input gradient): dyL -> dx0; dys: the gradient entering layers 0 .. L-2 (d_stride apart)
+// its backward (input gradient): dyL -> dx0; dys: the gradient entering each layer 0 .. L-1 (d_stride apart)
 int stage_img_backward(const void* dyL, void* dys, long d_stride, void* dx0, const uint8_t* masks, long mask_stride,
                        const void* w, long w_stride, float h, float two_gamma, int N, int H, int W, int C, int L,
                        hipStream_t s) {
@@ -1311,10 +1319,19 @@ int stage_img_backward(const void* dyL, void* dys, long d_stride, void* dx0, con
   return fail(ASR_E_UNSUPPORTED, "image-resident stage: C=%d W=%d", C, W);
 }
 
-// the weight-gradient slabs of one layer at any width (k_wgradb), for the image-resident stage's layers
-int wgradb_layer(const void* x, const void* dy, const uint8_t* mask, float h, int N, int H, int W, int C, float* slabs,
-                 int* nslabs, hipStream_t s) {
-  return convb_backward(dy, mask, x, nullptr, h, 0.f, N, H, W, C, nullptr, true, slabs, nslabs, s);
+// the weight-gradient slabs of L layers in one launch (k_wgradb, blockIdx.y = layer): layer l reads
+// x0 + l x_stride, dys + l d_stride, masks + l mask_stride and writes slabs + l slab_stride
+int wgradb_layers(const void* x0, long x_stride, const void* dys, long d_stride, const uint8_t* masks,
+                  long mask_stride, float h, int N, int H, int W, int C, int L, float* slabs, long slab_stride,
+                  int* nslabs, hipStream_t s) {
+#define ASR_WL(CC, WW)                                                                                              \
+  if (C == CC && W == WW)                                                                                           \
+    return launch_wgradb<CC, WW>((const bf16*)x0, (const bf16*)dys, masks, N, H, h, slabs, nslabs, s, L, x_stride, \
+                                 d_stride, mask_stride, slab_stride);
+  ASR_WL(16, 32) ASR_WL(16, 16) ASR_WL(16, 8) ASR_WL(32, 32) ASR_WL(32, 16) ASR_WL(32, 8) ASR_WL(64, 32)
+  ASR_WL(64, 16) ASR_WL(64, 8)
+#undef ASR_WL
+  return fail(ASR_E_UNSUPPORTED, "bf16 weight gradient: C=%d W=%d", C, W);
 }
 
 // elementwise bf16 <-> fp32 (the multi-stage bf16 net's transitions run in fp32)

@@ -60,8 +60,9 @@ int stage_img_forward(const void* x0, void* ys, long y_stride, uint8_t* masks, l
 int stage_img_backward(const void* dyL, void* dys, long d_stride, void* dx0, const uint8_t* masks, long mask_stride,
                        const void* w, long w_stride, float h, float two_gamma, int N, int H, int W, int C, int L,
                        hipStream_t s);
-int wgradb_layer(const void* x, const void* dy, const uint8_t* mask, float h, int N, int H, int W, int C, float* slabs,
-                 int* nslabs, hipStream_t s);
+int wgradb_layers(const void* x0, long x_stride, const void* dys, long d_stride, const uint8_t* masks,
+                  long mask_stride, float h, int N, int H, int W, int C, int L, float* slabs, long slab_stride,
+                  int* nslabs, hipStream_t s);
 // asr_deep16.hip: the C = 16, 32 x 32 bf16 stage as one fused forward / backward launch
 bool deep16_supported(int H, int W, int C);
 int deep16_forward(const void* x0, void* y0, long y_stride, uint8_t* mask0, long mask_stride, const void* wpack,
@@ -1124,7 +1125,7 @@ SLayout stages_layout(const asr_stages_config* c) {
   po += c->num_classes;
   L.n_params = po;
   // workspace
-  if (!L.st[0].deep) L.act0 = take((size_t)c->N * c->H * c->W * c->C[0] * L.act_bytes);
+  if (!L.st[0].deep && !L.st[0].img) L.act0 = take((size_t)c->N * c->H * c->W * c->C[0] * L.act_bytes);
   L.cws_bytes = 0;
   L.tws_bytes = 0;
   for (int s = 0; s < L.ns; ++s) {
@@ -1138,17 +1139,17 @@ SLayout stages_layout(const asr_stages_config* c) {
     g.tdirect = L.bf && g.S && trans_lds_supported(g.Hp, g.Wp, g.Cp, g.C, g.S);
     L.any_tconv = L.any_tconv || (L.bf && g.S && !g.tdirect);
     g.act_t = g.S && !g.tdirect ? take((size_t)g.P * 4) : 0;
-    if (g.deep) {  // [x0 | x1 .. xL] contiguous; the stem or the transition writes x0 in place
+    if (g.deep || g.img) {  // [x0 | x1 .. xL] contiguous; the stem or the transition writes x0 in place
       g.x0 = take((size_t)(g.L + 1) * g.P * 2);
       g.acts = g.x0 + (size_t)g.P * 2;
       if (s == 0) L.act0 = g.x0;
     }
-    g.act_tb = g.S && L.bf ? (g.deep && g.tdirect ? g.x0 : take((size_t)g.P * 2)) : 0;
+    g.act_tb = g.S && L.bf ? ((g.deep || g.img) && g.tdirect ? g.x0 : take((size_t)g.P * 2)) : 0;
     g.xin32 = g.S && L.bf && !g.tdirect ? take((size_t)c->N * g.Hp * g.Wp * g.Cp * 4) : 0;
     g.mask_t = g.S ? take((size_t)g.P) : 0;
-    if (!g.deep) g.acts = take((size_t)std::max(g.L, 1) * g.P * L.act_bytes);
+    if (!g.deep && !g.img) g.acts = take((size_t)std::max(g.L, 1) * g.P * L.act_bytes);
     g.masks = take((size_t)std::max(g.L, 1) * g.mask_bytes);
-    g.dys = g.img && g.L > 1 ? take((size_t)(g.L - 1) * g.P * 2) : 0;
+    g.dys = g.img ? take((size_t)g.L * g.P * 2) : 0;
     // every block keeps its slabs until the stage's one reduction launch: sized by the
     // grid the fp32 weight gradient runs at this shape, not by the 512-row maximum
     // (deep16: its own slab rows per layer)
@@ -1219,7 +1220,9 @@ int stages_forward_impl(const asr_stages_config* c, const SLayout& L, const floa
       ASR_TRY(asr_theta_to_w(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src_bwd), 0.f,
                              b + g.wbuf_bwd, g.wstride, wdt, s));
     if (g.img) {  // all L blocks in one launch, a workgroup per image
-      ASR_TRY(stage_img_forward(x, b + g.acts, g.P, (uint8_t*)(b + g.masks), g.mask_bytes, b + g.wbuf, g.wstride,
+      if (x != b + g.x0)
+        ASR_TRY(hip_check(hipMemcpyAsync(b + g.x0, x, (size_t)g.P * 2, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync"));
+      ASR_TRY(stage_img_forward(b + g.x0, b + g.acts, g.P, (uint8_t*)(b + g.masks), g.mask_bytes, b + g.wbuf, g.wstride,
                                 params + g.off_blk + g.ntheta, g.blk_stride, c->h, c->N, g.H, g.W, g.C, g.L, s));
       x = b + g.acts + (size_t)(g.L - 1) * g.P * 2;
       continue;
@@ -1375,14 +1378,10 @@ int asr_stages_forward_backward(const asr_stages_config* cfg, const float* param
       ASR_TRY(stage_img_backward(d, b + g.dys, g.P, e, (const uint8_t*)(b + g.masks), g.mask_bytes,
                                  b + (L.sep_bwd ? g.wbuf_bwd : g.wbuf), g.wstride, cfg->h, 2.f * gam, N, g.H, g.W, g.C,
                                  g.L, s));
-      for (int l = 0; l < g.L; ++l) {
-        const unsigned char* x_in = l == 0 ? chain_in : b + g.acts + (size_t)(l - 1) * g.P * ab;
-        const unsigned char* dyl = l == g.L - 1 ? d : b + g.dys + (size_t)l * g.P * 2;
-        ASR_TRY(wgradb_layer(x_in, dyl, (const uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes, cfg->h, N, g.H, g.W,
-                             g.C, (float*)(b + g.slabs) + (size_t)l * g.slab_stride, &nsl, s));
-        if (nsl > g.slab_rows)
-          return fail(ASR_E_WORKSPACE, "asr_stages: %d slab rows > the workspace's %d", nsl, g.slab_rows);
-      }
+      // every layer's weight gradient in one launch: x_l = x0 + l P, its input gradient dys + l P
+      ASR_TRY(wgradb_layers(b + g.x0, g.P, b + g.dys, g.P, (const uint8_t*)(b + g.masks), g.mask_bytes, cfg->h, N, g.H,
+                            g.W, g.C, g.L, (float*)(b + g.slabs), g.slab_stride, &nsl, s));
+      if (nsl > g.slab_rows) return fail(ASR_E_WORKSPACE, "asr_stages: %d slab rows > the workspace's %d", nsl, g.slab_rows);
       std::swap(d, e);
     }
     for (int l = (g.deep || g.img) ? -1 : g.L - 1; l >= 0; --l) {
