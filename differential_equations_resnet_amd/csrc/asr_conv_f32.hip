@@ -1039,10 +1039,10 @@ static int launch_wgradb(const bf16* x, const bf16* dy, const uint8_t* mask, int
 #define ASR_WGB_B16 1
 #endif
 #ifndef ASR_WGB_B32
-#define ASR_WGB_B32 2
+#define ASR_WGB_B32 8
 #endif
 #ifndef ASR_WGB_B64
-#define ASR_WGB_B64 4
+#define ASR_WGB_B64 32
 #endif
   constexpr int minb = C == 16 ? ASR_WGB_B16 : C == 32 ? ASR_WGB_B32 : ASR_WGB_B64;
   const int grid = (int)std::max<long>(1, std::min<long>((items + minb - 1) / minb, wgrad32_grid<C, W>(N, H)));
