@@ -181,11 +181,20 @@ __global__ void k_db_f32(const float* __restrict__ dz, long rows, int W, int C, 
 // ===========================================================================
 template <int C, int W_>
 struct F32Band {
-  static constexpr int OT = C / 16, W = W_, TW = W + 2, BR = 4, ROWF = TW * C, TILEF = (BR + 2) * ROWF;
+#ifndef ASR_F32PAD
+#define ASR_F32PAD 1
+#endif
+  // pixel strides in LDS (floats), padded against bank conflicts: PSC for the conv's 16-B reads
+  // (16 lanes = 16 consecutive pixels on distinct banks), PSW for the wgrad's 4-B reads (the two
+  // lane groups of a 32-lane half, one pixel apart, on disjoint banks); unpadded, a C = 64 tile
+  // put the 16 lanes of a conv read on one bank group
+  static constexpr int PSC = ASR_F32PAD ? C + 4 : C, PSW = ASR_F32PAD && C >= 32 ? C + 16 : C;
+  static constexpr int OT = C / 16, W = W_, TW = W + 2, BR = 4, TILEF = (BR + 2) * TW * PSC;
+  static constexpr int TILEW = (BR + 2) * TW * PSW;  // the wgrad's x tile
   static constexpr int T = BR * W / 16;  // 16-pixel tiles per band (band pixel p = 16 tile + lx: row p / W, col p % W)
   static constexpr int WPT = 4 / OT;    // forward / dgrad: waves sharing an o-tile, tiles dealt round-robin
   static constexpr int RS = 4 / OT;     // wgrad row split: 3 * OT * RS = 12 waves
-  static constexpr int DZF = BR * W * C;
+  static constexpr int DZF = BR * W * PSW;
   static_assert(W == 8 || W == 16 || W == 32, "fp32 MFMA band: W in {8, 16, 32}");
 };
 
@@ -208,7 +217,7 @@ __device__ __forceinline__ f32x4 masked_dz4(f32x4 v, const uint8_t* __restrict__
 // stage rows y0-1 .. y0+BR of image n into tile (zeros outside the image and
 // in the two halo columns), float4 per thread; with dmask, src is dy and the
 // tile gets dz = dh * dy * [relu bit] (the Euler block's dz, no separate pass)
-template <int C, int W, typename Ts = float>
+template <int C, int W, typename Ts = float, int PS = C>
 __device__ __forceinline__ void f32_stage_rows(const Ts* __restrict__ src, float* tile, int n, int y0, int H,
                                                int tid, int nthreads, const uint8_t* __restrict__ dmask = nullptr,
                                                float dh = 1.f) {
@@ -223,7 +232,7 @@ __device__ __forceinline__ void f32_stage_rows(const Ts* __restrict__ src, float
       v = load4f(src + e);
       if (dmask) v = masked_dz4(v, dmask, e, dh);
     }
-    *(f32x4*)(tile + (r * G::TW + col) * C + 4 * c4) = v;
+    *(f32x4*)(tile + (r * G::TW + col) * PS + 4 * c4) = v;
   }
 }
 
@@ -252,7 +261,7 @@ __global__ __launch_bounds__(256) void k_conv32(const float* __restrict__ xin, f
   f32x4 bz = {0.f, 0.f, 0.f, 0.f};
   if (MODE <= F_RELU && bias) bz = *(const f32x4*)(bias + 16 * ot + 4 * g);
   // (backward with dmask: xin is dy, the tile gets dz = h dy [relu bit])
-  f32_stage_rows<C, W>(xin, tile, n, y0, H, tid, 256, MODE >= B_EULER ? dmask : nullptr, h);
+  f32_stage_rows<C, W, float, G::PSC>(xin, tile, n, y0, H, tid, 256, MODE >= B_EULER ? dmask : nullptr, h);
   __syncthreads();
   // wave (ot, rw) takes the band's 16-pixel tiles rw, rw + WPT, ..; lane lx's pixel of tile tau is band
   // pixel 16 tau + lx (W = 8: a tile spans two rows, so validity is per lane)
@@ -268,7 +277,7 @@ __global__ __launch_bounds__(256) void k_conv32(const float* __restrict__ xin, f
     for (int t = 0; t < 9; ++t)
 #pragma unroll
       for (int q = 0; q < OT; ++q) {
-        const f32x4 bv = *(const f32x4*)(tile + ((r + t / 3) * TW + px + t % 3) * C + 16 * q + 4 * g);
+        const f32x4 bv = *(const f32x4*)(tile + ((r + t / 3) * TW + px + t % 3) * G::PSC + 16 * q + 4 * g);
 #pragma unroll
         for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[t][q][s], bv[s], acc, 0, 0, 0);
       }
@@ -277,7 +286,7 @@ __global__ __launch_bounds__(256) void k_conv32(const float* __restrict__ xin, f
       const bool ok = y0 + r < H;
       const long pix = ((long)n * H + y0 + r) * W + px;
       const long oi = pix * C + 16 * ot + 4 * g;  // this lane's 4 channels
-      const f32x4 ctr = *(const f32x4*)(tile + ((r + 1) * TW + px + 1) * C + 16 * ot + 4 * g);  // x or dz at the pixel
+      const f32x4 ctr = *(const f32x4*)(tile + ((r + 1) * TW + px + 1) * G::PSC + 16 * ot + 4 * g);  // x or dz at the pixel
       f32x4 v;
       if constexpr (MODE == F_EULER) {
         const f32x4 res = (extra && ok) ? *(const f32x4*)(extra + oi) : ctr;
@@ -318,7 +327,7 @@ __global__ __launch_bounds__(768) void k_wgrad32(const Tx* __restrict__ x, const
   constexpr int OT = G::OT, TW = G::TW, BR = G::BR, RS = G::RS, E = 9 * C * C;
   extern __shared__ __attribute__((aligned(16))) float lds32[];
   float* xt = lds32;               // [BR+2][TW][C]
-  float* dzt = lds32 + G::TILEF;   // [BR][W][C]
+  float* dzt = lds32 + G::TILEW;   // [BR][W][PSW]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
   const int ky = wave / (OT * RS), ot = (wave / RS) % OT, rs = wave % RS;
   const int nb = (H + BR - 1) / BR;
@@ -333,7 +342,7 @@ __global__ __launch_bounds__(768) void k_wgrad32(const Tx* __restrict__ x, const
     const int n = (int)(item / nb), y0 = (int)(item % nb) * BR;
     const int rows = min(BR, H - y0);
     __syncthreads();  // the previous item's tiles consumed
-    f32_stage_rows<C, W, Tx>(x, xt, n, y0, H, tid, 768);
+    f32_stage_rows<C, W, Tx, G::PSW>(x, xt, n, y0, H, tid, 768);
     for (int i = tid; i < BR * G::W * C / 4; i += 768) {
       const int r = i / (G::W * C / 4);
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -342,19 +351,19 @@ __global__ __launch_bounds__(768) void k_wgrad32(const Tx* __restrict__ x, const
         v = load4f(dz + e);
         if (dmask) v = masked_dz4(v, dmask, e, dh);  // dz is dy here: dz = dh dy [relu bit]
       }
-      *(f32x4*)(dzt + 4 * i) = v;
+      *(f32x4*)(dzt + (i / (C / 4)) * G::PSW + 4 * (i % (C / 4))) = v;
     }
     __syncthreads();
     for (int r = rs; r < rows; r += RS) {
 #pragma unroll
       for (int s = 0; s < G::W / 4; ++s) {
         const int p = 4 * s + g;  // this lane's pixel (k index) of the step
-        const float bv = dzt[(r * G::W + p) * C + 16 * ot + lx];
+        const float bv = dzt[(r * G::W + p) * G::PSW + 16 * ot + lx];
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
           for (int it = 0; it < OT; ++it) {
-            const float av = xt[((r + ky) * TW + p + kx) * C + 16 * it + lx];
+            const float av = xt[((r + ky) * TW + p + kx) * G::PSW + 16 * it + lx];
             acc[kx][it] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[kx][it], 0, 0, 0);
           }
         if (ky == 1) accb = __builtin_amdgcn_mfma_f32_16x16x4f32(1.f, bv, accb, 0, 0, 0);
@@ -403,7 +412,7 @@ __global__ __launch_bounds__(768) void k_wgrad32(const Tx* __restrict__ x, const
 template <int C, int W>
 static size_t wgrad32_lds() {
   using G = F32Band<C, W>;
-  const size_t stage = (size_t)(G::TILEF + G::DZF) * 4;
+  const size_t stage = (size_t)(G::TILEW + G::DZF) * 4;
   const size_t red = G::RS > 1 ? (size_t)12 * (3 * G::OT + 1) * 256 * 4 : 0;
   return std::max(stage, red);
 }
