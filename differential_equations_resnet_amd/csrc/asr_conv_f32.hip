@@ -322,8 +322,14 @@ __global__ __launch_bounds__(256) void k_conv32(const float* __restrict__ xin, f
 template <int C, int W, typename Tx = float>
 __global__ __launch_bounds__(768) void k_wgrad32(const Tx* __restrict__ x, const Tx* __restrict__ dz, int N,
                                                  int H, float* __restrict__ slabs, const uint8_t* __restrict__ dmask,
-                                                 float dh) {
+                                                 float dh, long x_stride = 0, long dz_stride = 0, long m_stride = 0,
+                                                 long s_stride = 0) {
   using G = F32Band<C, W>;
+  // several layers in one launch: blockIdx.y is the layer
+  x += blockIdx.y * x_stride;
+  dz += blockIdx.y * dz_stride;
+  if (dmask) dmask += blockIdx.y * m_stride;
+  slabs += blockIdx.y * s_stride;
   constexpr int OT = G::OT, TW = G::TW, BR = G::BR, RS = G::RS, E = 9 * C * C;
   extern __shared__ __attribute__((aligned(16))) float lds32[];
   float* xt = lds32;               // [BR+2][TW][C]
@@ -459,21 +465,31 @@ static int conv32_dispatch(int C, int W, const void* xin, void* out, uint8_t* ma
 }
 
 // k_wgrad32's grid = its slab rows (one [dW | db] slab per workgroup)
+#ifndef ASR_WG32_B32
+#define ASR_WG32_B32 1
+#endif
+#ifndef ASR_WG32_B64
+#define ASR_WG32_B64 1
+#endif
 template <int C, int W>
 static int wgrad32_grid(int N, int H) {
   const long items = (long)N * ((H + 3) / 4);
   int cus = cu_count();
   if (cus <= 0) cus = 256;
   const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / wgrad32_lds<C, W>())));
-  return (int)std::max<long>(1, std::min<long>({items, (long)per_cu * cus, 512L}));
+  // at least minb bands per workgroup at C = 32 / 64: a slab row is 37 / 148 KB, written and read back
+  constexpr int minb = C == 64 ? ASR_WG32_B64 : C == 32 ? ASR_WG32_B32 : 1;
+  return (int)std::max<long>(1, std::min<long>({(items + minb - 1) / minb, (long)per_cu * cus, 512L}));
 }
 
 template <int C, int W, typename Tx = float>
 static int launch_wgrad32(const Tx* x, const Tx* dz, int N, int H, float* slabs, int* nslabs, hipStream_t s,
-                          const uint8_t* dmask = nullptr, float dh = 1.f) {
+                          const uint8_t* dmask = nullptr, float dh = 1.f, int layers = 1, long x_stride = 0,
+                          long dz_stride = 0, long m_stride = 0, long s_stride = 0) {
   const size_t lds = wgrad32_lds<C, W>();
   const int grid = wgrad32_grid<C, W>(N, H);
-  hipLaunchKernelGGL((k_wgrad32<C, W, Tx>), dim3(grid), dim3(768), lds, s, x, dz, N, H, slabs, dmask, dh);
+  hipLaunchKernelGGL((k_wgrad32<C, W, Tx>), dim3(grid, layers), dim3(768), lds, s, x, dz, N, H, slabs, dmask, dh,
+                     x_stride, dz_stride, m_stride, s_stride);
   ASR_LAUNCH_CHECK("k_wgrad32");
   *nslabs = grid;
   return ASR_OK;
@@ -1286,6 +1302,239 @@ __global__ __launch_bounds__(256) void k_stageb(const bf16* __restrict__ dyL, bf
       *(uint4*)(dx0 + ib + 8L * i) = *(const uint4*)(dyt + (i / G::C8) * G::PS + 8 * (i % G::C8));
     st_barrier();  // (dyt reused by the next image)
   }
+}
+
+// ---------------------------------------------------------------------------
+// The fp32 image-resident stages (k_stagef32 / k_stageb32: the reference's
+// precision, v_mfma_f32_16x16x4_f32): the same structure as k_stagef /
+// k_stageb with fp32 image tiles (pixel stride C + 4 floats, dynamic LDS) and
+// the fp32 block's conventions: W in HWIO fp32, A = W^T fragments of the
+// wave's o-tile in registers (k_conv32's), dz = h dy [relu bit] staged in
+// fp32, dx = dy - conv(dz) + 2 gamma dz.
+// ---------------------------------------------------------------------------
+template <int C, int W_>
+struct StImg32 {
+#ifndef ASR_ST32_NW
+#define ASR_ST32_NW 4
+#endif
+  // NW waves per image: the fp32 MFMA is 4x the bf16's cycles per FLOP, and at the reference's batch
+  // sizes (128) one 4-wave workgroup per image would leave half the SIMDs idle
+  static constexpr int NW = ASR_ST32_NW, NTH = 64 * NW;
+  static constexpr int W = W_, H = W_, TW = W + 2, OT = C / 16, OQ = C / 16, WPT = NW / OT, PS = C + 4;
+  static constexpr int T = H * W / 16, IMGF = (H + 2) * TW * PS, NCH = H * W * C / 4;
+  static_assert((W == 16 && C == 32) || (W == 8 && C == 64), "fp32 image-resident stage: 16 x 16 x 32 or 8 x 8 x 64");
+};
+
+template <int C, int W>
+__device__ __forceinline__ int st32_off(int r, int c) {
+  return ((r + 1) * StImg32<C, W>::TW + c + 1) * StImg32<C, W>::PS;
+}
+
+template <int C, int W>
+__global__ __launch_bounds__((StImg32<C, W>::NTH)) void k_stagef32(const float* __restrict__ x0, float* __restrict__ ys, long y_stride,
+                                                  uint8_t* __restrict__ masks, long mask_stride,
+                                                  const float* __restrict__ w, long w_stride,
+                                                  const float* __restrict__ bias, long bias_stride, float h, int N,
+                                                  int L) {
+  using G = StImg32<C, W>;
+  constexpr int TW = G::TW, OQ = G::OQ, OT = G::OT, PS = G::PS;
+  extern __shared__ __attribute__((aligned(16))) float lds_sf[];
+  float* img0 = lds_sf;
+  float* img1 = lds_sf + G::IMGF;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
+  const int ot = wave % OT, rw = wave / OT;
+  for (int i = tid; i < 2 * G::IMGF / 4; i += G::NTH) ((f32x4*)lds_sf)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  for (int n = blockIdx.x; n < N; n += gridDim.x) {
+    const long ib = (long)n * G::H * W * C;
+    for (int i = tid; i < G::NCH; i += G::NTH) {
+      const int px = i / (C / 4), c4 = i % (C / 4);
+      *(f32x4*)(img0 + st32_off<C, W>(px / W, px % W) + 4 * c4) = *(const f32x4*)(x0 + ib + 4L * i);
+    }
+    __syncthreads();
+    for (int l = 0; l < L; ++l) {
+      const float* cur = (l & 1) ? img1 : img0;
+      float* nxt = (l & 1) ? img0 : img1;
+      const float* wl = w + (long)l * w_stride;
+      float A[9][OQ][4];
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int q = 0; q < OQ; ++q)
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) A[t][q][s4] = wl[((long)t * C + 16 * q + 4 * g + s4) * C + 16 * ot + lx];
+      const f32x4 bz = *(const f32x4*)(bias + (long)l * bias_stride + 16 * ot + 4 * g);
+      float* yl = ys + (long)l * y_stride + ib;
+      uint8_t* ml = masks + (long)l * mask_stride;
+      auto epi = [&](int p, const f32x4& acc) {
+        const int r = p / W, px = p % W;
+        const int co = st32_off<C, W>(r, px) + 16 * ot + 4 * g;
+        const f32x4 ctr = *(const f32x4*)(cur + co);
+        f32x4 v;
+        unsigned nib = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          nib |= (acc[e] > 0.f ? 1u : 0u) << e;
+          v[e] = ctr[e] + h * fmaxf(acc[e], 0.f);
+        }
+        *(f32x4*)(nxt + co) = v;
+        *(f32x4*)(yl + (long)p * C + 16 * ot + 4 * g) = v;
+        const long pix = (long)n * G::H * W + p;
+        unsigned m = nib << (4 * g);
+        m |= (unsigned)__shfl_xor((int)m, 16, 64);
+        m |= (unsigned)__shfl_xor((int)m, 32, 64);
+        if (g == 0) *(uint16_t*)(ml + (pix * C + 16 * ot) / 8) = (uint16_t)m;
+      };
+#pragma unroll 1
+      for (int j = 0; j < G::T / G::WPT; j += 2) {
+        const int p0 = 16 * (rw + j * G::WPT) + lx, p1 = 16 * (rw + (j + 1) * G::WPT) + lx;
+        const int r0 = p0 / W, x0p = p0 % W, r1 = p1 / W, x1p = p1 % W;
+        f32x4 acc0 = bz, acc1 = bz;
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int q = 0; q < OQ; ++q) {
+            const f32x4 b0 = *(const f32x4*)(cur + ((r0 + t / 3) * TW + x0p + t % 3) * PS + 16 * q + 4 * g);
+            const f32x4 b1 = *(const f32x4*)(cur + ((r1 + t / 3) * TW + x1p + t % 3) * PS + 16 * q + 4 * g);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+              acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(A[t][q][s4], b0[s4], acc0, 0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(A[t][q][s4], b1[s4], acc1, 0, 0, 0);
+            }
+          }
+        mfma_f32_settle();
+        epi(p0, acc0);
+        epi(p1, acc1);
+      }
+      st_barrier();  // layer l's outputs complete in nxt; cur free
+    }
+  }
+}
+
+template <int C, int W>
+__global__ __launch_bounds__((StImg32<C, W>::NTH)) void k_stageb32(const float* __restrict__ dyL, float* __restrict__ dys, long d_stride,
+                                                  float* __restrict__ dx0, const uint8_t* __restrict__ masks,
+                                                  long mask_stride, const float* __restrict__ w, long w_stride,
+                                                  float h, float two_gamma, int N, int L) {
+  using G = StImg32<C, W>;
+  constexpr int TW = G::TW, OQ = G::OQ, OT = G::OT, PS = G::PS;
+  extern __shared__ __attribute__((aligned(16))) float lds_sb[];
+  float* dzt = lds_sb;              // dz = h dy [relu bit], zero halo
+  float* dyt = lds_sb + G::IMGF;    // dy (becomes dx), pixel stride PS
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
+  const int ot = wave % OT, rw = wave / OT;
+  for (int i = tid; i < G::IMGF / 4; i += G::NTH) ((f32x4*)dzt)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int n = blockIdx.x; n < N; n += gridDim.x) {
+    const long ib = (long)n * G::H * W * C;
+    for (int i = tid; i < G::NCH; i += G::NTH)
+      *(f32x4*)(dyt + (i / (C / 4)) * PS + 4 * (i % (C / 4))) = *(const f32x4*)(dyL + ib + 4L * i);
+    for (int l = L - 1; l >= 0; --l) {
+      st_barrier();  // dy of layer l complete; dz free
+      const uint8_t* ml = masks + (long)l * mask_stride;
+      for (int i = tid; i < G::NCH; i += G::NTH) {
+        const int px = i / (C / 4), c4 = i % (C / 4);
+        const f32x4 v = *(const f32x4*)(dyt + px * PS + 4 * c4);
+        *(f32x4*)(dys + (long)l * d_stride + ib + 4L * i) = v;  // the gradient entering layer l (its wgrad's dy)
+        *(f32x4*)(dzt + st32_off<C, W>(px / W, px % W) + 4 * c4) = masked_dz4(v, ml, ib + 4L * i, h);
+      }
+      const float* wl = w + (long)l * w_stride;
+      float A[9][OQ][4];
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int q = 0; q < OQ; ++q)
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) A[t][q][s4] = wl[((long)t * C + 16 * q + 4 * g + s4) * C + 16 * ot + lx];
+      st_barrier();  // dz complete
+      auto epi = [&](int p, const f32x4& acc) {
+        const int r = p / W, px = p % W;
+        const int cz = st32_off<C, W>(r, px) + 16 * ot + 4 * g, cy = p * PS + 16 * ot + 4 * g;
+        const f32x4 z4 = *(const f32x4*)(dzt + cz), d4 = *(const f32x4*)(dyt + cy);
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = d4[e] - acc[e] + two_gamma * z4[e];
+        *(f32x4*)(dyt + cy) = v;  // (own pixel, own channels)
+      };
+#pragma unroll 1
+      for (int j = 0; j < G::T / G::WPT; j += 2) {
+        const int p0 = 16 * (rw + j * G::WPT) + lx, p1 = 16 * (rw + (j + 1) * G::WPT) + lx;
+        const int r0 = p0 / W, x0p = p0 % W, r1 = p1 / W, x1p = p1 % W;
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int q = 0; q < OQ; ++q) {
+            const f32x4 b0 = *(const f32x4*)(dzt + ((r0 + t / 3) * TW + x0p + t % 3) * PS + 16 * q + 4 * g);
+            const f32x4 b1 = *(const f32x4*)(dzt + ((r1 + t / 3) * TW + x1p + t % 3) * PS + 16 * q + 4 * g);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+              acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(A[t][q][s4], b0[s4], acc0, 0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(A[t][q][s4], b1[s4], acc1, 0, 0, 0);
+            }
+          }
+        mfma_f32_settle();
+        epi(p0, acc0);
+        epi(p1, acc1);
+      }
+    }
+    st_barrier();  // dx_0 complete
+    for (int i = tid; i < G::NCH; i += G::NTH)
+      *(f32x4*)(dx0 + ib + 4L * i) = *(const f32x4*)(dyt + (i / (C / 4)) * PS + 4 * (i % (C / 4)));
+    st_barrier();  // (dyt reused by the next image)
+  }
+}
+
+bool stage_img32_supported(int H, int W, int C) { return H == W && ((W == 16 && C == 32) || (W == 8 && C == 64)); }
+
+int stage_img32_forward(const float* x0, float* ys, long y_stride, uint8_t* masks, long mask_stride, const float* w,
+                        long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C, int L,
+                        hipStream_t s) {
+  if (!stage_img32_supported(H, W, C)) return fail(ASR_E_UNSUPPORTED, "fp32 image-resident stage: H=%d W=%d C=%d", H, W, C);
+  const unsigned grid = (unsigned)std::max(1, N);
+#define ASR_SF32(CC, WW)                                                                                             \
+  if (C == CC && W == WW) {                                                                                          \
+    using GG = StImg32<CC, WW>;                                                                                      \
+    const size_t lds = (size_t)2 * GG::IMGF * 4;                                                                     \
+    hipLaunchKernelGGL((k_stagef32<CC, WW>), dim3(grid), dim3(GG::NTH), lds, s, x0, ys, y_stride, masks, mask_stride, w, \
+                       w_stride, bias, bias_stride, h, N, L);                                                        \
+    ASR_LAUNCH_CHECK("k_stagef32");                                                                                  \
+    return ASR_OK;                                                                                                   \
+  }
+  ASR_SF32(32, 16) ASR_SF32(64, 8)
+#undef ASR_SF32
+  return fail(ASR_E_UNSUPPORTED, "fp32 image-resident stage: C=%d W=%d", C, W);
+}
+
+int stage_img32_backward(const float* dyL, float* dys, long d_stride, float* dx0, const uint8_t* masks,
+                         long mask_stride, const float* w, long w_stride, float h, float two_gamma, int N, int H, int W,
+                         int C, int L, hipStream_t s) {
+  if (!stage_img32_supported(H, W, C)) return fail(ASR_E_UNSUPPORTED, "fp32 image-resident stage: H=%d W=%d C=%d", H, W, C);
+  const unsigned grid = (unsigned)std::max(1, N);
+#define ASR_SB32(CC, WW)                                                                                            \
+  if (C == CC && W == WW) {                                                                                         \
+    using GG = StImg32<CC, WW>;                                                                                     \
+    const size_t lds = (size_t)(GG::IMGF + GG::H * WW * GG::PS) * 4;                                                \
+    hipLaunchKernelGGL((k_stageb32<CC, WW>), dim3(grid), dim3(GG::NTH), lds, s, dyL, dys, d_stride, dx0, masks,     \
+                       mask_stride, w, w_stride, h, two_gamma, N, L);                                               \
+    ASR_LAUNCH_CHECK("k_stageb32");                                                                                 \
+    return ASR_OK;                                                                                                  \
+  }
+  ASR_SB32(32, 16) ASR_SB32(64, 8)
+#undef ASR_SB32
+  return fail(ASR_E_UNSUPPORTED, "fp32 image-resident stage: C=%d W=%d", C, W);
+}
+
+// every layer's fp32 weight-gradient slabs in one launch (k_wgrad32, blockIdx.y = layer)
+int wgrad32_layers(const float* x0, long x_stride, const float* dys, long d_stride, const uint8_t* masks,
+                   long mask_stride, float h, int N, int H, int W, int C, int L, float* slabs, long slab_stride,
+                   int* nslabs, hipStream_t s) {
+#define ASR_W32L(CC, WW)                                                                                     \
+  if (C == CC && W == WW)                                                                                    \
+    return launch_wgrad32<CC, WW>(x0, dys, N, H, slabs, nslabs, s, masks, h, L, x_stride, d_stride, mask_stride, \
+                                  slab_stride);
+  ASR_W32L(32, 16) ASR_W32L(64, 8) ASR_W32L(16, 32) ASR_W32L(32, 32) ASR_W32L(64, 16)
+#undef ASR_W32L
+  return fail(ASR_E_UNSUPPORTED, "fp32 weight gradient (layers): C=%d W=%d", C, W);
 }
 
 bool stage_img_supported(int H, int W, int C) {

@@ -60,6 +60,16 @@ int stage_img_forward(const void* x0, void* ys, long y_stride, uint8_t* masks, l
 int stage_img_backward(const void* dyL, void* dys, long d_stride, void* dx0, const uint8_t* masks, long mask_stride,
                        const void* w, long w_stride, float h, float two_gamma, int N, int H, int W, int C, int L,
                        hipStream_t s);
+bool stage_img32_supported(int H, int W, int C);
+int stage_img32_forward(const float* x0, float* ys, long y_stride, uint8_t* masks, long mask_stride, const float* w,
+                        long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C, int L,
+                        hipStream_t s);
+int stage_img32_backward(const float* dyL, float* dys, long d_stride, float* dx0, const uint8_t* masks,
+                         long mask_stride, const float* w, long w_stride, float h, float two_gamma, int N, int H, int W,
+                         int C, int L, hipStream_t s);
+int wgrad32_layers(const float* x0, long x_stride, const float* dys, long d_stride, const uint8_t* masks,
+                   long mask_stride, float h, int N, int H, int W, int C, int L, float* slabs, long slab_stride,
+                   int* nslabs, hipStream_t s);
 int wgradb_layers(const void* x0, long x_stride, const void* dys, long d_stride, const uint8_t* masks,
                   long mask_stride, float h, int N, int H, int W, int C, int L, float* slabs, long slab_stride,
                   int* nslabs, hipStream_t s);
@@ -1015,6 +1025,7 @@ struct StageL {
   bool deep;             // bf16 nets: a C = 16, 32 x 32 stage on the fused deep16 kernels (x0: its input slot,
   size_t x0;             //   followed by the L outputs at stride P, as deep16 reads them)
   bool img;              // bf16 nets: a 16 x 16 x 32 / 8 x 8 x 64 stage on the image-resident kernels
+  bool img32;            // fp32 nets: the same on the fp32 image-resident kernels
   size_t dys;            //   its backward's per-layer input gradients (layers 0 .. L-2)
   long wstride;          // elements of one layer's W in wbuf (E fp32, or the bf16 MFMA pack)
   long grp_stride;   // floats per block of pass-1 group rows
@@ -1107,8 +1118,9 @@ SLayout stages_layout(const asr_stages_config* c) {
     g.deep = c->dtype == ASR_BF16 && g.L > 0 && deep16_supported(H, W, g.C);
 #ifndef ASR_NO_STAGE_IMG
     g.img = c->dtype == ASR_BF16 && g.L > 0 && !g.deep && stage_img_supported(H, W, g.C);
+    g.img32 = c->dtype != ASR_BF16 && g.L > 0 && stage_img32_supported(H, W, g.C);
 #else
-    g.img = false;
+    g.img = g.img32 = false;
 #endif
     g.E = 9L * g.C * g.C;
     g.blk_stride = g.ntheta + g.C;
@@ -1125,7 +1137,8 @@ SLayout stages_layout(const asr_stages_config* c) {
   po += c->num_classes;
   L.n_params = po;
   // workspace
-  if (!L.st[0].deep && !L.st[0].img) L.act0 = take((size_t)c->N * c->H * c->W * c->C[0] * L.act_bytes);
+  if (!L.st[0].deep && !L.st[0].img && !L.st[0].img32)
+    L.act0 = take((size_t)c->N * c->H * c->W * c->C[0] * L.act_bytes);
   L.cws_bytes = 0;
   L.tws_bytes = 0;
   for (int s = 0; s < L.ns; ++s) {
@@ -1138,18 +1151,18 @@ SLayout stages_layout(const asr_stages_config* c) {
     g.wbuf_bwd = L.sep_bwd ? take((size_t)std::max(g.L, 1) * g.wstride * L.act_bytes) : 0;
     g.tdirect = L.bf && g.S && trans_lds_supported(g.Hp, g.Wp, g.Cp, g.C, g.S);
     L.any_tconv = L.any_tconv || (L.bf && g.S && !g.tdirect);
-    g.act_t = g.S && !g.tdirect ? take((size_t)g.P * 4) : 0;
-    if (g.deep || g.img) {  // [x0 | x1 .. xL] contiguous; the stem or the transition writes x0 in place
-      g.x0 = take((size_t)(g.L + 1) * g.P * 2);
-      g.acts = g.x0 + (size_t)g.P * 2;
+    if (g.deep || g.img || g.img32) {  // [x0 | x1 .. xL] contiguous; the stem or the transition writes x0 in place
+      g.x0 = take((size_t)(g.L + 1) * g.P * L.act_bytes);
+      g.acts = g.x0 + (size_t)g.P * L.act_bytes;
       if (s == 0) L.act0 = g.x0;
     }
+    g.act_t = g.S && !g.tdirect ? (g.img32 ? g.x0 : take((size_t)g.P * 4)) : 0;  // (after x0: it may be x0)
     g.act_tb = g.S && L.bf ? ((g.deep || g.img) && g.tdirect ? g.x0 : take((size_t)g.P * 2)) : 0;
     g.xin32 = g.S && L.bf && !g.tdirect ? take((size_t)c->N * g.Hp * g.Wp * g.Cp * 4) : 0;
     g.mask_t = g.S ? take((size_t)g.P) : 0;
-    if (!g.deep && !g.img) g.acts = take((size_t)std::max(g.L, 1) * g.P * L.act_bytes);
+    if (!g.deep && !g.img && !g.img32) g.acts = take((size_t)std::max(g.L, 1) * g.P * L.act_bytes);
     g.masks = take((size_t)std::max(g.L, 1) * g.mask_bytes);
-    g.dys = g.img ? take((size_t)g.L * g.P * 2) : 0;
+    g.dys = g.img || g.img32 ? take((size_t)g.L * g.P * L.act_bytes) : 0;
     // every block keeps its slabs until the stage's one reduction launch: sized by the
     // grid the fp32 weight gradient runs at this shape, not by the 512-row maximum
     // (deep16: its own slab rows per layer)
@@ -1219,6 +1232,15 @@ int stages_forward_impl(const asr_stages_config* c, const SLayout& L, const floa
     if (training && L.sep_bwd)
       ASR_TRY(asr_theta_to_w(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src_bwd), 0.f,
                              b + g.wbuf_bwd, g.wstride, wdt, s));
+    if (g.img32) {  // fp32: all L blocks in one launch, a workgroup per image
+      if (x != b + g.x0)
+        ASR_TRY(hip_check(hipMemcpyAsync(b + g.x0, x, (size_t)g.P * 4, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync"));
+      ASR_TRY(stage_img32_forward((const float*)(b + g.x0), (float*)(b + g.acts), g.P, (uint8_t*)(b + g.masks),
+                                  g.mask_bytes, (const float*)(b + g.wbuf), g.wstride, params + g.off_blk + g.ntheta,
+                                  g.blk_stride, c->h, c->N, g.H, g.W, g.C, g.L, s));
+      x = b + g.acts + (size_t)(g.L - 1) * g.P * 4;
+      continue;
+    }
     if (g.img) {  // all L blocks in one launch, a workgroup per image
       if (x != b + g.x0)
         ASR_TRY(hip_check(hipMemcpyAsync(b + g.x0, x, (size_t)g.P * 2, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync"));
@@ -1384,7 +1406,16 @@ int asr_stages_forward_backward(const asr_stages_config* cfg, const float* param
       if (nsl > g.slab_rows) return fail(ASR_E_WORKSPACE, "asr_stages: %d slab rows > the workspace's %d", nsl, g.slab_rows);
       std::swap(d, e);
     }
-    for (int l = (g.deep || g.img) ? -1 : g.L - 1; l >= 0; --l) {
+    if (g.img32) {  // fp32: input gradients in one launch, every layer's weight gradient in one launch
+      ASR_TRY(stage_img32_backward((const float*)d, (float*)(b + g.dys), g.P, (float*)e, (const uint8_t*)(b + g.masks),
+                                   g.mask_bytes, (const float*)(b + (L.sep_bwd ? g.wbuf_bwd : g.wbuf)), g.wstride,
+                                   cfg->h, 2.f * gam, N, g.H, g.W, g.C, g.L, s));
+      ASR_TRY(wgrad32_layers((const float*)(b + g.x0), g.P, (const float*)(b + g.dys), g.P, (const uint8_t*)(b + g.masks),
+                             g.mask_bytes, cfg->h, N, g.H, g.W, g.C, g.L, (float*)(b + g.slabs), g.slab_stride, &nsl, s));
+      if (nsl > g.slab_rows) return fail(ASR_E_WORKSPACE, "asr_stages: %d slab rows > the workspace's %d", nsl, g.slab_rows);
+      std::swap(d, e);
+    }
+    for (int l = (g.deep || g.img || g.img32) ? -1 : g.L - 1; l >= 0; --l) {
       const unsigned char* x_in = l == 0 ? chain_in : b + g.acts + (size_t)(l - 1) * g.P * ab;
       const unsigned char* wl = b + (L.sep_bwd ? g.wbuf_bwd : g.wbuf) + (size_t)l * g.wstride * ab;
       const uint8_t* mk = (const uint8_t*)(b + g.masks) + (size_t)l * g.mask_bytes;
