@@ -466,10 +466,10 @@ static int conv32_dispatch(int C, int W, const void* xin, void* out, uint8_t* ma
 
 // k_wgrad32's grid = its slab rows (one [dW | db] slab per workgroup)
 #ifndef ASR_WG32_B32
-#define ASR_WG32_B32 1
+#define ASR_WG32_B32 8
 #endif
 #ifndef ASR_WG32_B64
-#define ASR_WG32_B64 1
+#define ASR_WG32_B64 16
 #endif
 template <int C, int W>
 static int wgrad32_grid(int N, int H) {
