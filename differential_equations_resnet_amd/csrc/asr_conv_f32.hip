@@ -1158,6 +1158,11 @@ __device__ __forceinline__ void st_barrier() {
 #endif
 }
 
+#ifndef ASR_ST_IPW
+#define ASR_ST_IPW 1
+#endif
+// IPW images per workgroup: 1 (a wave's two MFMA chains are two tiles of the image); 2 (the chains are
+// one tile of each image, the layer's A fragments shared) measured -7 % (r05ar: half the workgroups)
 template <int C, int W>
 __global__ __launch_bounds__(256) void k_stagef(const bf16* __restrict__ x0, bf16* __restrict__ ys, long y_stride,
                                                 uint8_t* __restrict__ masks, long mask_stride,
@@ -1165,31 +1170,34 @@ __global__ __launch_bounds__(256) void k_stagef(const bf16* __restrict__ x0, bf1
                                                 const float* __restrict__ bias, long bias_stride, float h, int N,
                                                 int L) {
   using G = StImg<C, W>;
-  constexpr int TW = G::TW, KS = G::KS, OT = G::OT;
-  __shared__ __attribute__((aligned(16))) bf16 img[2][G::IMGE];
+  constexpr int TW = G::TW, KS = G::KS, OT = G::OT, IPW = ASR_ST_IPW, TP = 2 / IPW;
+  extern __shared__ __attribute__((aligned(16))) bf16 lds_stf[];  // [IPW][2][IMGE]
+  auto imgb = [&](int im, int pp) { return lds_stf + (im * 2 + pp) * G::IMGE; };
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
   const int ot = wave % OT, rw = wave / OT;
-  for (int i = tid; i < 2 * G::IMGE / 8; i += 256) ((uint4*)&img[0][0])[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = tid; i < IPW * 2 * G::IMGE / 8; i += 256) ((uint4*)lds_stf)[i] = make_uint4(0u, 0u, 0u, 0u);
   st_barrier();
-  for (int n = blockIdx.x; n < N; n += gridDim.x) {
-    const long ib = (long)n * G::H * W * C;
-    for (int i = tid; i < G::NCH; i += 256) {
-      const int px = i / G::C8, c8 = i % G::C8;
-      *(uint4*)(&img[0][0] + st_off<C, W>(px / W, px % W) + 8 * c8) = *(const uint4*)(x0 + ib + 8L * i);
+  for (int n0 = IPW * blockIdx.x; n0 < N; n0 += IPW * gridDim.x) {
+    const int nimg = min(IPW, N - n0);  // (uniform)
+    for (int im = 0; im < nimg; ++im) {
+      const long ib = (long)(n0 + im) * G::H * W * C;
+      for (int i = tid; i < G::NCH; i += 256) {
+        const int px = i / G::C8, c8 = i % G::C8;
+        *(uint4*)(imgb(im, 0) + st_off<C, W>(px / W, px % W) + 8 * c8) = *(const uint4*)(x0 + ib + 8L * i);
+      }
     }
     st_barrier();
     for (int l = 0; l < L; ++l) {
-      const bf16* cur = &img[l & 1][0];
-      bf16* nxt = &img[(l & 1) ^ 1][0];
       bf16x8 A[KS];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
         A[ks] = *(const bf16x8*)(wpack + (long)l * w_stride + (((long)ot * KS + ks) * 64 + lane) * 8);
       const f32x4 bz = *(const f32x4*)(bias + (long)l * bias_stride + 16 * ot + 4 * g);
-      bf16* yl = ys + (long)l * y_stride + ib;
       uint8_t* ml = masks + (long)l * mask_stride;
-      // two tiles per pass: two independent MFMA accumulate chains per wave
-      auto epi = [&](int p, const f32x4& acc) {
+      auto epi = [&](int im, int p, const f32x4& acc) {
+        const bf16* cur = imgb(im, l & 1);
+        bf16* nxt = imgb(im, (l & 1) ^ 1);
+        const long n = n0 + im;
         const int r = p / W, px = p % W;
         const int co = st_off<C, W>(r, px) + 16 * ot + 4 * g;
         const uint2 cw = *(const uint2*)(cur + co);
@@ -1204,32 +1212,43 @@ __global__ __launch_bounds__(256) void k_stagef(const bf16* __restrict__ x0, bf1
         }
         const uint2 yw = make_uint2(pk_bf16_rn(v[0], v[1]), pk_bf16_rn(v[2], v[3]));
         *(uint2*)(nxt + co) = yw;
-        const long pix = (long)n * G::H * W + p;
-        *(uint2*)(yl + (long)p * C + 16 * ot + 4 * g) = yw;
+        const long pix = n * G::H * W + p;
+        *(uint2*)(ys + (long)l * y_stride + pix * C + 16 * ot + 4 * g) = yw;
         unsigned m = nib << (4 * g);
         m |= (unsigned)__shfl_xor((int)m, 16, 64);
         m |= (unsigned)__shfl_xor((int)m, 32, 64);
         if (g == 0) *(uint16_t*)(ml + (pix * C + 16 * ot) / 8) = (uint16_t)m;
       };
 #pragma unroll 1
-      for (int j = 0; j < G::T / G::WPT; j += 2) {
-        const int p0 = 16 * (rw + j * G::WPT) + lx, p1 = 16 * (rw + (j + 1) * G::WPT) + lx;
-        const int r0 = p0 / W, x0p = p0 % W, r1 = p1 / W, x1p = p1 % W;
-        f32x4 acc0 = bz, acc1 = bz;
+      for (int j = 0; j < G::T / G::WPT; j += TP) {
+        int pc[2], rc[2], xc[2];
+        const bf16* bc[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {  // chain c: image c / TP, tile j + c % TP
+          pc[c] = 16 * (rw + (j + c % TP) * G::WPT) + lx;
+          rc[c] = pc[c] / W;
+          xc[c] = pc[c] % W;
+          bc[c] = imgb(c / TP, l & 1);
+        }
+        f32x4 acc[2] = {bz, bz};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const int kap = 32 * ks + 8 * g;
           const int t = min(kap / C, 8), i0c = kap - (kap / C) * C;
-          const uint4 b0 = *(const uint4*)(cur + ((r0 + t / 3) * TW + x0p + t % 3) * G::PS + i0c);
-          const uint4 b1 = *(const uint4*)(cur + ((r1 + t / 3) * TW + x1p + t % 3) * G::PS + i0c);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], __builtin_bit_cast(bf16x8, b0), acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], __builtin_bit_cast(bf16x8, b1), acc1, 0, 0, 0);
+          uint4 b[2];
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            b[c] = *(const uint4*)(bc[c] + ((rc[c] + t / 3) * TW + xc[c] + t % 3) * G::PS + i0c);
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], __builtin_bit_cast(bf16x8, b[c]), acc[c], 0, 0, 0);
         }
         mfma_bf16_settle();
-        epi(p0, acc0);
-        epi(p1, acc1);
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          if (c / TP < nimg) epi(c / TP, pc[c], acc[c]);
       }
-      st_barrier();  // layer l's outputs complete in nxt; cur free
+      st_barrier();  // layer l's outputs complete; the inputs free
     }
   }
 }
@@ -1240,17 +1259,23 @@ __global__ __launch_bounds__(256) void k_stageb(const bf16* __restrict__ dyL, bf
                                                 long mask_stride, const bf16* __restrict__ wpack, long w_stride,
                                                 float h, float two_gamma, int N, int L) {
   using G = StImg<C, W>;
-  constexpr int TW = G::TW, KS = G::KS, OT = G::OT;
-  __shared__ __attribute__((aligned(16))) bf16 dzt[G::IMGE];          // dz with a zero halo
-  __shared__ __attribute__((aligned(16))) bf16 dyt[G::H * W * G::PS];  // dy (becomes dx) of the image
+  constexpr int TW = G::TW, KS = G::KS, OT = G::OT, IPW = ASR_ST_IPW, TP = 2 / IPW;
+  constexpr int DYE = G::H * W * G::PS;
+  extern __shared__ __attribute__((aligned(16))) bf16 lds_stb[];  // [IPW][dz (haloed) | dy]
+  auto dzb = [&](int im) { return lds_stb + im * (G::IMGE + DYE); };
+  auto dyb = [&](int im) { return lds_stb + im * (G::IMGE + DYE) + G::IMGE; };
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
   const int ot = wave % OT, rw = wave / OT;
   const float hg = h * two_gamma;
-  for (int i = tid; i < G::IMGE / 8; i += 256) ((uint4*)dzt)[i] = make_uint4(0u, 0u, 0u, 0u);
-  for (int n = blockIdx.x; n < N; n += gridDim.x) {
-    const long ib = (long)n * G::H * W * C;
-    for (int i = tid; i < G::NCH; i += 256)
-      *(uint4*)(dyt + (i / G::C8) * G::PS + 8 * (i % G::C8)) = *(const uint4*)(dyL + ib + 8L * i);
+  for (int i = tid; i < IPW * (G::IMGE + DYE) / 8; i += 256) ((uint4*)lds_stb)[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (int n0 = IPW * blockIdx.x; n0 < N; n0 += IPW * gridDim.x) {
+    const int nimg = min(IPW, N - n0);  // (uniform)
+    st_barrier();  // (the previous images' dx read out)
+    for (int im = 0; im < nimg; ++im) {
+      const long ib = (long)(n0 + im) * G::H * W * C;
+      for (int i = tid; i < G::NCH; i += 256)
+        *(uint4*)(dyb(im) + (i / G::C8) * G::PS + 8 * (i % G::C8)) = *(const uint4*)(dyL + ib + 8L * i);
+    }
     for (int l = L - 1; l >= 0; --l) {
       bf16x8 A[KS];
 #pragma unroll
@@ -1258,17 +1283,20 @@ __global__ __launch_bounds__(256) void k_stageb(const bf16* __restrict__ dyL, bf
         A[ks] = *(const bf16x8*)(wpack + (long)l * w_stride + (((long)ot * KS + ks) * 64 + lane) * 8);
       st_barrier();  // dy of layer l complete (loaded, or the previous layer's dx); dz free
       const uint8_t* ml = masks + (long)l * mask_stride;
-      for (int i = tid; i < G::NCH; i += 256) {
-        const int px = i / G::C8, c8 = i % G::C8;
-        const uint4 v = *(const uint4*)(dyt + px * G::PS + 8 * c8);
-        *(uint4*)(dys + (long)l * d_stride + ib + 8L * i) = v;  // the gradient entering layer l (its wgrad's dy)
-        *(uint4*)(dzt + st_off<C, W>(px / W, px % W) + 8 * c8) = mask8_bf16(v, ml[(ib + 8L * i) >> 3]);
+      for (int im = 0; im < nimg; ++im) {
+        const long ib = (long)(n0 + im) * G::H * W * C;
+        for (int i = tid; i < G::NCH; i += 256) {
+          const int px = i / G::C8, c8 = i % G::C8;
+          const uint4 v = *(const uint4*)(dyb(im) + px * G::PS + 8 * c8);
+          *(uint4*)(dys + (long)l * d_stride + ib + 8L * i) = v;  // the gradient entering layer l (its wgrad's dy)
+          *(uint4*)(dzb(im) + st_off<C, W>(px / W, px % W) + 8 * c8) = mask8_bf16(v, ml[(ib + 8L * i) >> 3]);
+        }
       }
       st_barrier();  // dz complete
-      auto epi = [&](int p, const f32x4& acc) {
+      auto epi = [&](int im, int p, const f32x4& acc) {
         const int r = p / W, px = p % W;
         const int cz = st_off<C, W>(r, px) + 16 * ot + 4 * g, cy = p * G::PS + 16 * ot + 4 * g;
-        const uint2 zw = *(const uint2*)(dzt + cz), dw = *(const uint2*)(dyt + cy);
+        const uint2 zw = *(const uint2*)(dzb(im) + cz), dw = *(const uint2*)(dyb(im) + cy);
         const float z4[4] = {__uint_as_float(zw.x << 16), __uint_as_float(zw.x & 0xffff0000u),
                              __uint_as_float(zw.y << 16), __uint_as_float(zw.y & 0xffff0000u)};
         const float d4[4] = {__uint_as_float(dw.x << 16), __uint_as_float(dw.x & 0xffff0000u),
@@ -1276,31 +1304,44 @@ __global__ __launch_bounds__(256) void k_stageb(const bf16* __restrict__ dyL, bf
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = fmaf(hg, z4[e], fmaf(-h, acc[e], d4[e]));
-        *(uint2*)(dyt + cy) = make_uint2(pk_bf16_rn(v[0], v[1]), pk_bf16_rn(v[2], v[3]));  // (own pixel, own channels)
+        *(uint2*)(dyb(im) + cy) = make_uint2(pk_bf16_rn(v[0], v[1]), pk_bf16_rn(v[2], v[3]));  // (own pixel, own channels)
       };
 #pragma unroll 1
-      for (int j = 0; j < G::T / G::WPT; j += 2) {
-        const int p0 = 16 * (rw + j * G::WPT) + lx, p1 = 16 * (rw + (j + 1) * G::WPT) + lx;
-        const int r0 = p0 / W, x0p = p0 % W, r1 = p1 / W, x1p = p1 % W;
-        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < G::T / G::WPT; j += TP) {
+        int pc[2], rc[2], xc[2];
+        const bf16* bc[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          pc[c] = 16 * (rw + (j + c % TP) * G::WPT) + lx;
+          rc[c] = pc[c] / W;
+          xc[c] = pc[c] % W;
+          bc[c] = dzb(c / TP);
+        }
+        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const int kap = 32 * ks + 8 * g;
           const int t = min(kap / C, 8), i0c = kap - (kap / C) * C;
-          const uint4 b0 = *(const uint4*)(dzt + ((r0 + t / 3) * TW + x0p + t % 3) * G::PS + i0c);
-          const uint4 b1 = *(const uint4*)(dzt + ((r1 + t / 3) * TW + x1p + t % 3) * G::PS + i0c);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], __builtin_bit_cast(bf16x8, b0), acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], __builtin_bit_cast(bf16x8, b1), acc1, 0, 0, 0);
+          uint4 b[2];
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            b[c] = *(const uint4*)(bc[c] + ((rc[c] + t / 3) * TW + xc[c] + t % 3) * G::PS + i0c);
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ks], __builtin_bit_cast(bf16x8, b[c]), acc[c], 0, 0, 0);
         }
         mfma_bf16_settle();
-        epi(p0, acc0);
-        epi(p1, acc1);
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          if (c / TP < nimg) epi(c / TP, pc[c], acc[c]);
       }
     }
     st_barrier();  // dx_0 complete
-    for (int i = tid; i < G::NCH; i += 256)
-      *(uint4*)(dx0 + ib + 8L * i) = *(const uint4*)(dyt + (i / G::C8) * G::PS + 8 * (i % G::C8));
-    st_barrier();  // (dyt reused by the next image)
+    for (int im = 0; im < nimg; ++im) {
+      const long ib = (long)(n0 + im) * G::H * W * C;
+      for (int i = tid; i < G::NCH; i += 256)
+        *(uint4*)(dx0 + ib + 8L * i) = *(const uint4*)(dyb(im) + (i / G::C8) * G::PS + 8 * (i % G::C8));
+    }
   }
 }
 
@@ -1546,10 +1587,11 @@ int stage_img_forward(const void* x0, void* ys, long y_stride, uint8_t* masks, l
                       long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C, int L,
                       hipStream_t s) {
   if (!stage_img_supported(H, W, C)) return fail(ASR_E_UNSUPPORTED, "image-resident stage: H=%d W=%d C=%d", H, W, C);
-  const unsigned grid = (unsigned)std::max(1, N);
+  const unsigned grid = (unsigned)std::max(1, (N + ASR_ST_IPW - 1) / ASR_ST_IPW);
 #define ASR_SF(CC, WW)                                                                                        \
   if (C == CC && W == WW) {                                                                                   \
-    hipLaunchKernelGGL((k_stagef<CC, WW>), dim3(grid), dim3(256), 0, s, (const bf16*)x0, (bf16*)ys, y_stride, \
+    const size_t lds = (size_t)ASR_ST_IPW * 2 * StImg<CC, WW>::IMGE * 2;                                      \
+    hipLaunchKernelGGL((k_stagef<CC, WW>), dim3(grid), dim3(256), lds, s, (const bf16*)x0, (bf16*)ys, y_stride, \
                        masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, L);             \
     ASR_LAUNCH_CHECK("k_stagef");                                                                             \
     return ASR_OK;                                                                                            \
@@ -1564,10 +1606,12 @@ int stage_img_backward(const void* dyL, void* dys, long d_stride, void* dx0, con
                        const void* w, long w_stride, float h, float two_gamma, int N, int H, int W, int C, int L,
                        hipStream_t s) {
   if (!stage_img_supported(H, W, C)) return fail(ASR_E_UNSUPPORTED, "image-resident stage: H=%d W=%d C=%d", H, W, C);
-  const unsigned grid = (unsigned)std::max(1, N);
+  const unsigned grid = (unsigned)std::max(1, (N + ASR_ST_IPW - 1) / ASR_ST_IPW);
 #define ASR_SB(CC, WW)                                                                                           \
   if (C == CC && W == WW) {                                                                                      \
-    hipLaunchKernelGGL((k_stageb<CC, WW>), dim3(grid), dim3(256), 0, s, (const bf16*)dyL, (bf16*)dys, d_stride,  \
+    using GG = StImg<CC, WW>;                                                                                    \
+    const size_t lds = (size_t)ASR_ST_IPW * (GG::IMGE + GG::H * WW * GG::PS) * 2;                                \
+    hipLaunchKernelGGL((k_stageb<CC, WW>), dim3(grid), dim3(256), lds, s, (const bf16*)dyL, (bf16*)dys, d_stride, \
                        (bf16*)dx0, masks, mask_stride, (const bf16*)w, w_stride, h, two_gamma, N, L);             \
     ASR_LAUNCH_CHECK("k_stageb");                                                                                \
     return ASR_OK;                                                                                               \

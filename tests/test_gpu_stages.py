@@ -273,6 +273,17 @@ def test_stages_network_bf16_vs_oracle(stages, kind, anti, gamma):
     _assert_bf16_net(ex, spec, params, imgs, onehot)
 
 
+def test_stages_network_bf16_odd_batch():
+    """An odd batch: the image-resident stage kernels' last workgroup holds one image of two."""
+    from differential_equations_resnet_amd.runtime import StagesExecutor
+    stages, kind, anti, gamma = [(16, 1, 0), (32, 2, 2), (64, 2, 2)], "3by3", True, 0.0
+    spec, params, imgs, onehot = _stages_setup(stages, kind, anti, h=0.25, gamma=gamma, N=5, seed=4)
+    ex = StagesExecutor(imgs.shape[0], spec.H, spec.W, 3, stages, 10, spec.h, spec.gamma, subtract_mean=127.5,
+                        divide_by_stddev=127.5, input_u8=True, param_kind=KINDS[kind], antisymmetric=anti,
+                        dtype="bfloat16")
+    _assert_bf16_net(ex, spec, params, imgs, onehot)
+
+
 def test_stages_bf16_unsupported_width_raises():
     from differential_equations_resnet_amd import _lib
     from differential_equations_resnet_amd.runtime import StagesExecutor
