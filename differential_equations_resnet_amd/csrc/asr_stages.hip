@@ -1084,7 +1084,9 @@ SLayout stages_layout(const asr_stages_config* c) {
   L.sep_bwd = param_is_antisymmetric(c->param_kind, c->antisymmetric) == 0;
   L.bf = c->dtype == ASR_BF16;
   L.act_bytes = L.bf ? 2 : 4;
-  size_t off = 0;
+  // offset 0 is a reserved null page: a buffer offset left unassigned (0) can never alias a live
+  // buffer, and stages_layout_valid rejects it
+  size_t off = 256;
   auto take = [&](size_t bytes) {
     const size_t o = off;
     off += align_up(bytes, 256);
@@ -1192,6 +1194,21 @@ SLayout stages_layout(const asr_stages_config* c) {
   L.sred = take(L.sred_bytes);
   L.total = off;
   return L;
+}
+
+// every buffer the executor will touch has an assigned (non-null) offset
+bool stages_layout_valid(const SLayout& L) {
+  if (!L.act0 || !L.probs || !L.dA || !L.dB || !L.sslabs) return false;
+  for (int s = 0; s < L.ns; ++s) {
+    const StageL& g = L.st[s];
+    if (g.S && !g.mask_t) return false;
+    if (g.S && !(L.bf ? g.act_tb : g.act_t)) return false;
+    if (g.S && L.bf && !g.tdirect && (!g.act_t || !g.xin32)) return false;
+    if (g.L > 0 && (!g.acts || !g.masks || !g.wbuf || !g.slabs || !g.grp)) return false;
+    if ((g.deep || g.img || g.img32) && !g.x0) return false;
+    if ((g.img || g.img32) && !g.dys) return false;
+  }
+  return true;
 }
 
 // forward through the stem and all stages; *xL = the last activation (fp32, or bf16 for a bf16 net)
@@ -1317,6 +1334,7 @@ size_t asr_stages_workspace_bytes(const asr_stages_config* cfg) {
 int asr_stages_prepare(const asr_stages_config* cfg, void* ws, size_t ws_bytes) {
   ASR_TRY(stages_check(cfg));
   const SLayout L = stages_layout(cfg);
+  if (!stages_layout_valid(L)) return fail(ASR_E_ARG, "asr_stages: internal workspace layout error");
   if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_stages_prepare: workspace too small");
   unsigned char* b = (unsigned char*)ws;
   for (int s = 0; s < L.ns; ++s) {
@@ -1339,6 +1357,7 @@ int asr_stages_forward(const asr_stages_config* cfg, const float* params, const 
                        size_t ws_bytes, asr_stream_t stream) {
   ASR_TRY(stages_check(cfg));
   const SLayout L = stages_layout(cfg);
+  if (!stages_layout_valid(L)) return fail(ASR_E_ARG, "asr_stages: internal workspace layout error");
   if (!params || !images || !probs) return fail(ASR_E_ARG, "asr_stages_forward: null pointer");
   if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_stages_forward: workspace too small");
   hipStream_t s = (hipStream_t)stream;
@@ -1355,6 +1374,7 @@ int asr_stages_forward_backward(const asr_stages_config* cfg, const float* param
                                 size_t ws_bytes, asr_stream_t stream) {
   ASR_TRY(stages_check(cfg));
   const SLayout L = stages_layout(cfg);
+  if (!stages_layout_valid(L)) return fail(ASR_E_ARG, "asr_stages: internal workspace layout error");
   if (!params || !images || !targets || !grads || !loss) return fail(ASR_E_ARG, "asr_stages_forward_backward: null");
   if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_stages_forward_backward: workspace too small");
   hipStream_t s = (hipStream_t)stream;
