@@ -843,7 +843,10 @@ int launch_trans_dgrad_lds(const T* dy, const uint8_t* mask, const float* k2, co
   const long items = (long)N * (H / G::BR);
   int cus = cu_count();
   if (cus <= 0) cus = 256;
-  const int grid = (int)std::max<long>(1, std::min<long>(items, 2L * cus));
+#ifndef ASR_TDL_WPC
+#define ASR_TDL_WPC 1
+#endif
+  const int grid = (int)std::max<long>(1, std::min<long>(items, (long)ASR_TDL_WPC * cus));
   hipLaunchKernelGGL((k_trans_dgrad_lds<CI, CO, WO, T>), dim3(grid), dim3(512), G::LDS, s, dy, mask, k2, k1, dx, N, H);
   ASR_LAUNCH_CHECK("k_trans_dgrad_lds");
   return ASR_OK;
