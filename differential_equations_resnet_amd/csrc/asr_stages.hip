@@ -705,7 +705,10 @@ int launch_trans_fwd_lds(const T* x, T* y, uint8_t* mask, const float* k2, const
   const long items = (long)N * (H / 2 / G::BRO);
   int cus = cu_count();
   if (cus <= 0) cus = 256;
-  const int grid = (int)std::max<long>(1, std::min<long>(items, 4L * cus));
+#ifndef ASR_TFL_WPC
+#define ASR_TFL_WPC 2
+#endif
+  const int grid = (int)std::max<long>(1, std::min<long>(items, (long)ASR_TFL_WPC * cus));
   hipLaunchKernelGGL((k_trans_fwd_lds<CI, CO, WO, T>), dim3(grid), dim3(64 * G::NW), G::LDS, s, x, y, mask, k2, b2, k1,
                      b1, N, H);
   ASR_LAUNCH_CHECK("k_trans_fwd_lds");
@@ -877,7 +880,10 @@ int launch_trans_wgrad_lds(const T* dy, const uint8_t* mask, const T* x, float* 
   const long items = (long)N * ((H / 2 + G::BRO - 1) / G::BRO);
   int cus = cu_count();
   if (cus <= 0) cus = 256;
-  const int grid = (int)std::max<long>(1, std::min<long>({items, 2L * cus, (long)max_rows}));
+#ifndef ASR_TWL_WPC
+#define ASR_TWL_WPC 2
+#endif
+  const int grid = (int)std::max<long>(1, std::min<long>({items, (long)ASR_TWL_WPC * cus, (long)max_rows}));
   hipLaunchKernelGGL((k_trans_wgrad_lds<CI, CO, WO, T>), dim3(grid), dim3(512), G::LDS, s, dy, mask, x, part, N, H);
   ASR_LAUNCH_CHECK("k_trans_wgrad_lds");
   *rows_out = grid;
