@@ -1134,8 +1134,13 @@ int convb_backward(const void* dy, const uint8_t* mask, const void* x, const voi
 // ===========================================================================
 template <int C, int W_>
 struct StImg {
-  static constexpr int W = W_, H = W_, TW = W + 2, OT = C / 16, WPT = 4 / OT, KS = (9 * C + 31) / 32, C8 = C / 8;
+#ifndef ASR_ST_NW
+#define ASR_ST_NW 4
+#endif
+  static constexpr int NW = ASR_ST_NW, NTH = 64 * NW;  // waves per image
+  static constexpr int W = W_, H = W_, TW = W + 2, OT = C / 16, WPT = NW / OT, KS = (9 * C + 31) / 32, C8 = C / 8;
   static constexpr int T = H * W / 16;              // 16-pixel tiles per image
+  static_assert((T / WPT) % 2 == 0, "image-resident stage: a wave's tiles come in pairs (two MFMA chains)");
   static constexpr int PS = C + ASR_PIXPAD;          // a pixel's elements in LDS (padded, as BfBand)
   static constexpr int IMGE = (H + 2) * TW * PS;    // elements of a haloed image tile
   static constexpr int NCH = H * W * C8;            // 16-B chunks of an image
@@ -1164,7 +1169,7 @@ __device__ __forceinline__ void st_barrier() {
 // IPW images per workgroup: 1 (a wave's two MFMA chains are two tiles of the image); 2 (the chains are
 // one tile of each image, the layer's A fragments shared) measured -7 % (r05ar: half the workgroups)
 template <int C, int W>
-__global__ __launch_bounds__(256) void k_stagef(const bf16* __restrict__ x0, bf16* __restrict__ ys, long y_stride,
+__global__ __launch_bounds__((StImg<C, W>::NTH)) void k_stagef(const bf16* __restrict__ x0, bf16* __restrict__ ys, long y_stride,
                                                 uint8_t* __restrict__ masks, long mask_stride,
                                                 const bf16* __restrict__ wpack, long w_stride,
                                                 const float* __restrict__ bias, long bias_stride, float h, int N,
@@ -1175,13 +1180,13 @@ __global__ __launch_bounds__(256) void k_stagef(const bf16* __restrict__ x0, bf1
   auto imgb = [&](int im, int pp) { return lds_stf + (im * 2 + pp) * G::IMGE; };
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
   const int ot = wave % OT, rw = wave / OT;
-  for (int i = tid; i < IPW * 2 * G::IMGE / 8; i += 256) ((uint4*)lds_stf)[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = tid; i < IPW * 2 * G::IMGE / 8; i += G::NTH) ((uint4*)lds_stf)[i] = make_uint4(0u, 0u, 0u, 0u);
   st_barrier();
   for (int n0 = IPW * blockIdx.x; n0 < N; n0 += IPW * gridDim.x) {
     const int nimg = min(IPW, N - n0);  // (uniform)
     for (int im = 0; im < nimg; ++im) {
       const long ib = (long)(n0 + im) * G::H * W * C;
-      for (int i = tid; i < G::NCH; i += 256) {
+      for (int i = tid; i < G::NCH; i += G::NTH) {
         const int px = i / G::C8, c8 = i % G::C8;
         *(uint4*)(imgb(im, 0) + st_off<C, W>(px / W, px % W) + 8 * c8) = *(const uint4*)(x0 + ib + 8L * i);
       }
@@ -1254,7 +1259,7 @@ __global__ __launch_bounds__(256) void k_stagef(const bf16* __restrict__ x0, bf1
 }
 
 template <int C, int W>
-__global__ __launch_bounds__(256) void k_stageb(const bf16* __restrict__ dyL, bf16* __restrict__ dys, long d_stride,
+__global__ __launch_bounds__((StImg<C, W>::NTH)) void k_stageb(const bf16* __restrict__ dyL, bf16* __restrict__ dys, long d_stride,
                                                 bf16* __restrict__ dx0, const uint8_t* __restrict__ masks,
                                                 long mask_stride, const bf16* __restrict__ wpack, long w_stride,
                                                 float h, float two_gamma, int N, int L) {
@@ -1267,13 +1272,13 @@ __global__ __launch_bounds__(256) void k_stageb(const bf16* __restrict__ dyL, bf
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
   const int ot = wave % OT, rw = wave / OT;
   const float hg = h * two_gamma;
-  for (int i = tid; i < IPW * (G::IMGE + DYE) / 8; i += 256) ((uint4*)lds_stb)[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = tid; i < IPW * (G::IMGE + DYE) / 8; i += G::NTH) ((uint4*)lds_stb)[i] = make_uint4(0u, 0u, 0u, 0u);
   for (int n0 = IPW * blockIdx.x; n0 < N; n0 += IPW * gridDim.x) {
     const int nimg = min(IPW, N - n0);  // (uniform)
     st_barrier();  // (the previous images' dx read out)
     for (int im = 0; im < nimg; ++im) {
       const long ib = (long)(n0 + im) * G::H * W * C;
-      for (int i = tid; i < G::NCH; i += 256)
+      for (int i = tid; i < G::NCH; i += G::NTH)
         *(uint4*)(dyb(im) + (i / G::C8) * G::PS + 8 * (i % G::C8)) = *(const uint4*)(dyL + ib + 8L * i);
     }
     for (int l = L - 1; l >= 0; --l) {
@@ -1285,7 +1290,7 @@ __global__ __launch_bounds__(256) void k_stageb(const bf16* __restrict__ dyL, bf
       const uint8_t* ml = masks + (long)l * mask_stride;
       for (int im = 0; im < nimg; ++im) {
         const long ib = (long)(n0 + im) * G::H * W * C;
-        for (int i = tid; i < G::NCH; i += 256) {
+        for (int i = tid; i < G::NCH; i += G::NTH) {
           const int px = i / G::C8, c8 = i % G::C8;
           const uint4 v = *(const uint4*)(dyb(im) + px * G::PS + 8 * c8);
           *(uint4*)(dys + (long)l * d_stride + ib + 8L * i) = v;  // the gradient entering layer l (its wgrad's dy)
@@ -1339,7 +1344,7 @@ __global__ __launch_bounds__(256) void k_stageb(const bf16* __restrict__ dyL, bf
     st_barrier();  // dx_0 complete
     for (int im = 0; im < nimg; ++im) {
       const long ib = (long)(n0 + im) * G::H * W * C;
-      for (int i = tid; i < G::NCH; i += 256)
+      for (int i = tid; i < G::NCH; i += G::NTH)
         *(uint4*)(dx0 + ib + 8L * i) = *(const uint4*)(dyb(im) + (i / G::C8) * G::PS + 8 * (i % G::C8));
     }
   }
@@ -1579,7 +1584,7 @@ int wgrad32_layers(const float* x0, long x_stride, const float* dys, long d_stri
 }
 
 bool stage_img_supported(int H, int W, int C) {
-  return H == W && ((W == 16 && C == 32) || (W == 8 && C == 64) || (W == 8 && C == 32));
+  return H == W && ((W == 16 && C == 32) || (W == 8 && C == 64) || (ASR_ST_NW == 4 && W == 8 && C == 32));
 }
 
 // the image-resident stage forward: x0 [N][H][W][C] -> ys (L layers at y_stride), masks (L at mask_stride)
@@ -1591,12 +1596,16 @@ int stage_img_forward(const void* x0, void* ys, long y_stride, uint8_t* masks, l
 #define ASR_SF(CC, WW)                                                                                        \
   if (C == CC && W == WW) {                                                                                   \
     const size_t lds = (size_t)ASR_ST_IPW * 2 * StImg<CC, WW>::IMGE * 2;                                      \
-    hipLaunchKernelGGL((k_stagef<CC, WW>), dim3(grid), dim3(256), lds, s, (const bf16*)x0, (bf16*)ys, y_stride, \
+    hipLaunchKernelGGL((k_stagef<CC, WW>), dim3(grid), dim3(StImg<CC, WW>::NTH), lds, s, (const bf16*)x0, (bf16*)ys, \
+                       y_stride,                                                                              \
                        masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, L);             \
     ASR_LAUNCH_CHECK("k_stagef");                                                                             \
     return ASR_OK;                                                                                            \
   }
-  ASR_SF(32, 16) ASR_SF(64, 8) ASR_SF(32, 8)
+  ASR_SF(32, 16) ASR_SF(64, 8)
+#if ASR_ST_NW == 4
+  ASR_SF(32, 8)
+#endif
 #undef ASR_SF
   return fail(ASR_E_UNSUPPORTED, "image-resident stage: C=%d W=%d", C, W);
 }
@@ -1611,12 +1620,15 @@ int stage_img_backward(const void* dyL, void* dys, long d_stride, void* dx0, con
   if (C == CC && W == WW) {                                                                                      \
     using GG = StImg<CC, WW>;                                                                                    \
     const size_t lds = (size_t)ASR_ST_IPW * (GG::IMGE + GG::H * WW * GG::PS) * 2;                                \
-    hipLaunchKernelGGL((k_stageb<CC, WW>), dim3(grid), dim3(256), lds, s, (const bf16*)dyL, (bf16*)dys, d_stride, \
+    hipLaunchKernelGGL((k_stageb<CC, WW>), dim3(grid), dim3(GG::NTH), lds, s, (const bf16*)dyL, (bf16*)dys, d_stride, \
                        (bf16*)dx0, masks, mask_stride, (const bf16*)w, w_stride, h, two_gamma, N, L);             \
     ASR_LAUNCH_CHECK("k_stageb");                                                                                \
     return ASR_OK;                                                                                               \
   }
-  ASR_SB(32, 16) ASR_SB(64, 8) ASR_SB(32, 8)
+  ASR_SB(32, 16) ASR_SB(64, 8)
+#if ASR_ST_NW == 4
+  ASR_SB(32, 8)
+#endif
 #undef ASR_SB
   return fail(ASR_E_UNSUPPORTED, "image-resident stage: C=%d W=%d", C, W);
 }
