@@ -43,6 +43,7 @@ ASR_VARIANT_INFERENCE = 32
 ASR_VARIANT_TIMED = 64
 ASR_VARIANT_FULL_DXL = 128
 ASR_VARIANT_FULL_SLABS = 256
+ASR_VARIANT_W_BF16 = 512
 ASR_DIST_UNIQUE_ID_BYTES = 128
 ASR_STAGES_MAX = 8
 

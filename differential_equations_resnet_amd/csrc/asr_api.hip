@@ -77,7 +77,10 @@ int block_stack_fwd_mfma(const void* x0, void* ys, long y_stride, uint8_t* masks
                          long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C, int L,
                          hipStream_t s, int slots = 0);
 int deep16_forward(const void* x0, void* y0, long y_stride, uint8_t* mask0, long mask_stride, const void* wpack,
-                   const float* bias, long bias_stride, float h, int N, int L, bool store_all, hipStream_t s);
+                   const float* bias, long bias_stride, float h, int N, int L, bool store_all, hipStream_t s,
+                   const void* wlo = nullptr);
+int theta_to_w_pack_hilo(const float* theta, long theta_stride, int L, int C, const int32_t* w_src, float gamma,
+                         void* w_hi, void* w_lo, long w_stride, hipStream_t s);
 size_t deep16_slab_bytes(int N, int L);
 int deep16_backward(void* dbufA, void* dbufB, const void* xs, long x_stride, const uint8_t* masks, long mask_stride,
                     const void* wpack, float h, float two_gamma, int N, int L, float* slabs, int* slab_rows,
@@ -359,12 +362,13 @@ struct NetLayout {
   size_t grp;  // per-layer slab group sums, projected after the whole backward
   size_t slabs_all;  // fp32: every block's slabs, pass 1 of all blocks in one launch after the loop
   long slab_stride;
-  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, x0, acts, xmids, masks, dxa, dxb, dxg, bwdws, slabs2, slabs, red, probs,
+  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_lo, wbuf_bwd, x0, acts, xmids, masks, dxa, dxb, dxg, bwdws, slabs2, slabs, red, probs,
       loss_per, dlogits, gap, total;
   long mask_bytes;
   int act_bytes;
   bool fast_stem;
   bool deep;          // C=16 stack path: one fused launch forward, one backward (asr_deep16.hip)
+  bool hilo;          // ... its forward with W as bf16 hi + lo (not ASR_VARIANT_W_BF16)
   size_t deep_slabs;  // its weight-gradient slabs [L][rows][E+C]
   bool inference;     // ASR_VARIANT_INFERENCE: forward-only workspace (3 activation slots, no backward buffers)
   bool stack_bwd;     // C=64 Euler bf16: all blocks' backward in one k_bwd3_stack launch
@@ -389,7 +393,7 @@ static int net_check(const asr_net_config* c) {
     return fail(ASR_E_ARG, "bad integrator %d", c->integrator);
   if (c->variant & ~(ASR_VARIANT_NO_FOLD | ASR_VARIANT_STEM_FWD_VALU | ASR_VARIANT_STEM_WGRAD_VALU | ASR_VARIANT_PER_BLOCK_FWD |
                     ASR_VARIANT_PER_BLOCK_BWD | ASR_VARIANT_INFERENCE | ASR_VARIANT_TIMED | ASR_VARIANT_FULL_DXL |
-                    ASR_VARIANT_FULL_SLABS))
+                    ASR_VARIANT_FULL_SLABS | ASR_VARIANT_W_BF16))
     return fail(ASR_E_ARG, "bad variant bits 0x%x", c->variant);
   if (c->dtype == ASR_BF16 && !mfma_supported(c->C, c->W))
     return fail(ASR_E_UNSUPPORTED, "bf16 network needs C in {16,32,64} and W == 32 (C=%d W=%d)", c->C, c->W);
@@ -432,6 +436,9 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.w_src_bwd = take(L.sep_bwd && tr ? (size_t)L.E * 4 : 0);
   L.theta_dst = take((size_t)L.ntheta * 2 * 4);
   L.wbuf = take((size_t)c->L * L.wstride * L.act_bytes);
+  L.hilo = L.deep && !(c->variant & ASR_VARIANT_W_BF16);
+  // the fused C=16 forward's lo weights (also under ASR_VARIANT_W_BF16: a variant bit never moves the layout)
+  L.wbuf_lo = take(L.deep ? (size_t)c->L * L.wstride * L.act_bytes : 0);
   L.wbuf_bwd = take(L.sep_bwd && tr ? (size_t)c->L * L.wstride * L.act_bytes : 0);
   L.x0 = take(L.fast_stem ? 0 : (size_t)c->N * c->H * c->W * c->Cin * 4);
   // training keeps x_0 .. x_L for the backward; inference ping-pongs (x_0 + 2 slots)
@@ -526,8 +533,12 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
   const float inv_std = c->use_norm ? 1.f / c->divide_by_stddev : 1.f;
   if (training && L.inference) return fail(ASR_E_ARG, "an ASR_VARIANT_INFERENCE workspace has no training buffers");
   // 1. materialise W for all L blocks (one launch)
-  ASR_TRY(asr_theta_to_w(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src), c->gamma,
-                         ws + L.wbuf, L.wstride, c->dtype, s));
+  if (L.hilo)
+    ASR_TRY(theta_to_w_pack_hilo(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src), c->gamma,
+                                 ws + L.wbuf, ws + L.wbuf_lo, L.wstride, s));
+  else
+    ASR_TRY(asr_theta_to_w(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src), c->gamma,
+                           ws + L.wbuf, L.wstride, c->dtype, s));
   if (training && L.sep_bwd)
     ASR_TRY(asr_theta_to_w(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src_bwd), 0.f,
                            ws + L.wbuf_bwd, L.wstride, c->dtype, s));
@@ -563,7 +574,7 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
   if (L.deep) {  // C=16: all L steps in one launch, images resident in LDS
     ASR_TRY(deep16_forward(act(0), act(training ? 1 : c->L), L.P, training ? (uint8_t*)(ws + L.masks) : nullptr,
                            L.mask_bytes, ws + L.wbuf, params + L.off_blk + L.ntheta, L.blk_stride, c->h, N, c->L,
-                           training, s));
+                           training, s, L.hilo ? ws + L.wbuf_lo : nullptr));
     return timed_event(c, 1, s);
   }
   if (bf && training && L.rk2 && block_stack_fwd_supported(N, H, W, C) && !(c->variant & ASR_VARIANT_PER_BLOCK_FWD)) {
@@ -974,6 +985,7 @@ int asr_net_prepare(const asr_net_config* cfg, void* ws, size_t ws_bytes) {
   ASR_TRY(net_check(cfg));
   const NetLayout L = net_layout(cfg);
   if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_net_prepare: workspace too small");
+  ASR_TRY(check_ws_device(ws, "asr_net_prepare"));
   std::vector<int32_t> w_src((size_t)L.E), theta_dst((size_t)L.ntheta * 2);
   ASR_TRY(param_map(cfg->C, cfg->param_kind, cfg->antisymmetric, w_src.data(), theta_dst.data()));
   unsigned char* b = (unsigned char*)ws;
@@ -1010,6 +1022,7 @@ int asr_net_forward(const asr_net_config* cfg, const float* params, const void* 
   const NetLayout L = net_layout(cfg);
   if (!params || !images || !probs) return fail(ASR_E_ARG, "asr_net_forward: null pointer");
   if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_net_forward: workspace too small");
+  ASR_TRY(check_ws_device(ws, "asr_net_forward"));
   hipStream_t s = (hipStream_t)stream;
   unsigned char* b = (unsigned char*)ws;
   unsigned char* xL = nullptr;
@@ -1023,6 +1036,7 @@ int asr_net_check_status(const asr_net_config* cfg, const void* ws, size_t ws_by
   ASR_TRY(net_check(cfg));
   const NetLayout L = net_layout(cfg);
   if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_net_check_status: workspace too small");
+  ASR_TRY(check_ws_device(ws, "asr_net_check_status"));
   // the stream's own completion status only (hipGetLastError would report, and clear,
   // whatever error another HIP call on this thread left behind)
   return hip_check(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
@@ -1057,6 +1071,7 @@ int asr_net_forward_backward(const asr_net_config* cfg, const float* params, con
   // transposed operator and the training activations are absent)
   if (L.inference)
     return fail(ASR_E_ARG, "asr_net_forward_backward: an ASR_VARIANT_INFERENCE workspace has no training buffers");
+  ASR_TRY(check_ws_device(ws, "asr_net_forward_backward"));
   hipStream_t s = (hipStream_t)stream;
   unsigned char* b = (unsigned char*)ws;
   const int C = cfg->C, N = cfg->N, H = cfg->H, W = cfg->W, K = cfg->num_classes;

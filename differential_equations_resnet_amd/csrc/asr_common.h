@@ -35,6 +35,13 @@ inline int hip_check(hipError_t e, const char* what) {
 
 int cu_count();
 
+// A network / stage workspace must live on the current device: its layout (the
+// weight-gradient slab rows, hence every offset after them) follows the CU
+// count of the device current when it was sized, and the kernels size their
+// grids by the device current at launch.  ASR_E_WORKSPACE, before any launch,
+// when ws is not device memory of the current device.
+int check_ws_device(const void* ws, const char* who);
+
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 // Slab layout of the pair-local C=64 stacked backward (k_bwd3_stack<..., PAIR>,

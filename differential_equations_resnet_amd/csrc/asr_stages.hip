@@ -76,7 +76,10 @@ int wgradb_layers(const void* x0, long x_stride, const void* dys, long d_stride,
 // asr_deep16.hip: the C = 16, 32 x 32 bf16 stage as one fused forward / backward launch
 bool deep16_supported(int H, int W, int C);
 int deep16_forward(const void* x0, void* y0, long y_stride, uint8_t* mask0, long mask_stride, const void* wpack,
-                   const float* bias, long bias_stride, float h, int N, int L, bool store_all, hipStream_t s);
+                   const float* bias, long bias_stride, float h, int N, int L, bool store_all, hipStream_t s,
+                   const void* wlo = nullptr);
+int theta_to_w_pack_hilo(const float* theta, long theta_stride, int L, int C, const int32_t* w_src, float gamma,
+                         void* w_hi, void* w_lo, long w_stride, hipStream_t s);
 size_t deep16_slab_bytes(int N, int L);
 int deep16_backward(void* dbufA, void* dbufB, const void* xs, long x_stride, const uint8_t* masks, long mask_stride,
                     const void* wpack, float h, float two_gamma, int N, int L, float* slabs, int* slab_rows,
@@ -1028,7 +1031,7 @@ struct StageL {
   int C, L, H, W, S, Cp, Hp, Wp;  // S = 0: no transition; Cp/Hp/Wp the stage input's shape
   long P, ntheta, E, blk_stride, mask_bytes;
   long off_t, off_blk;          // parameter offsets (floats)
-  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, act_t, mask_t, acts, masks, grp, slabs;  // workspace offsets
+  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_lo, wbuf_bwd, act_t, mask_t, acts, masks, grp, slabs;  // workspace offsets
   size_t act_tb, xin32;  // bf16 nets: the transition's output in bf16, its input in fp32 (kept for the backward)
   bool tdirect;          // bf16 nets: the transition on the LDS kernels in bf16 (no fp32 copies)
   bool deep;             // bf16 nets: a C = 16, 32 x 32 stage on the fused deep16 kernels (x0: its input slot,
@@ -1160,6 +1163,7 @@ SLayout stages_layout(const asr_stages_config* c) {
     g.wstride = L.bf ? asr_wpack_elems(g.C) : g.E;
     g.wbuf = take((size_t)std::max(g.L, 1) * g.wstride * L.act_bytes);
     g.wbuf_bwd = L.sep_bwd ? take((size_t)std::max(g.L, 1) * g.wstride * L.act_bytes) : 0;
+    g.wbuf_lo = g.deep ? take((size_t)g.L * g.wstride * L.act_bytes) : 0;  // deep16's hi/lo forward weights
     g.tdirect = L.bf && g.S && trans_lds_supported(g.Hp, g.Wp, g.Cp, g.C, g.S);
     L.any_tconv = L.any_tconv || (L.bf && g.S && !g.tdirect);
     if (g.deep || g.img || g.img32) {  // [x0 | x1 .. xL] contiguous; the stem or the transition writes x0 in place
@@ -1253,8 +1257,12 @@ int stages_forward_impl(const asr_stages_config* c, const SLayout& L, const floa
       }
     }
     if (g.L == 0) continue;
-    ASR_TRY(asr_theta_to_w(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src), c->gamma,
-                           b + g.wbuf, g.wstride, wdt, s));
+    if (g.deep)
+      ASR_TRY(theta_to_w_pack_hilo(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src),
+                                   c->gamma, b + g.wbuf, b + g.wbuf_lo, g.wstride, s));
+    else
+      ASR_TRY(asr_theta_to_w(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src), c->gamma,
+                             b + g.wbuf, g.wstride, wdt, s));
     if (training && L.sep_bwd)
       ASR_TRY(asr_theta_to_w(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src_bwd), 0.f,
                              b + g.wbuf_bwd, g.wstride, wdt, s));
@@ -1279,7 +1287,7 @@ int stages_forward_impl(const asr_stages_config* c, const SLayout& L, const floa
       if (x != b + g.x0)
         ASR_TRY(hip_check(hipMemcpyAsync(b + g.x0, x, (size_t)g.P * 2, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync"));
       ASR_TRY(deep16_forward(b + g.x0, b + g.acts, g.P, (uint8_t*)(b + g.masks), g.mask_bytes, b + g.wbuf,
-                             params + g.off_blk + g.ntheta, g.blk_stride, c->h, c->N, g.L, true, s));
+                             params + g.off_blk + g.ntheta, g.blk_stride, c->h, c->N, g.L, true, s, b + g.wbuf_lo));
       x = b + g.acts + (size_t)(g.L - 1) * g.P * 2;
       continue;
     }
@@ -1345,6 +1353,7 @@ int asr_stages_prepare(const asr_stages_config* cfg, void* ws, size_t ws_bytes) 
   const SLayout L = stages_layout(cfg);
   if (!stages_layout_valid(L)) return fail(ASR_E_ARG, "asr_stages: internal workspace layout error");
   if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_stages_prepare: workspace too small");
+  ASR_TRY(check_ws_device(ws, "asr_stages_prepare"));
   unsigned char* b = (unsigned char*)ws;
   for (int s = 0; s < L.ns; ++s) {
     const StageL& g = L.st[s];
@@ -1369,6 +1378,7 @@ int asr_stages_forward(const asr_stages_config* cfg, const float* params, const 
   if (!stages_layout_valid(L)) return fail(ASR_E_ARG, "asr_stages: internal workspace layout error");
   if (!params || !images || !probs) return fail(ASR_E_ARG, "asr_stages_forward: null pointer");
   if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_stages_forward: workspace too small");
+  ASR_TRY(check_ws_device(ws, "asr_stages_forward"));
   hipStream_t s = (hipStream_t)stream;
   unsigned char* b = (unsigned char*)ws;
   const void* xL = nullptr;
@@ -1386,6 +1396,7 @@ int asr_stages_forward_backward(const asr_stages_config* cfg, const float* param
   if (!stages_layout_valid(L)) return fail(ASR_E_ARG, "asr_stages: internal workspace layout error");
   if (!params || !images || !targets || !grads || !loss) return fail(ASR_E_ARG, "asr_stages_forward_backward: null");
   if (!ws || ws_bytes < L.total) return fail(ASR_E_WORKSPACE, "asr_stages_forward_backward: workspace too small");
+  ASR_TRY(check_ws_device(ws, "asr_stages_forward_backward"));
   hipStream_t s = (hipStream_t)stream;
   unsigned char* b = (unsigned char*)ws;
   const int N = cfg->N, K = cfg->num_classes;

@@ -38,6 +38,22 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
+int check_ws_device(const void* ws, const char* who) {
+  int dev = 0;
+  ASR_TRY(hip_check(hipGetDevice(&dev), "hipGetDevice"));
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, ws) != hipSuccess) {
+    (void)hipGetLastError();  // (clear the failed query's error)
+    return fail(ASR_E_WORKSPACE, "%s: the workspace is not HIP device memory", who);
+  }
+  if (a.type != hipMemoryTypeDevice || a.device != dev)
+    return fail(ASR_E_WORKSPACE,
+                "%s: the workspace is not device memory of the current device %d (type %d, device %d): its layout "
+                "follows the CU count of the device it was sized on",
+                who, dev, (int)a.type, a.device);
+  return ASR_OK;
+}
+
 int cu_count() {
   static thread_local int dev_cached = -1, cus = 0;
   int dev = 0;
@@ -223,9 +239,11 @@ __global__ void k_theta_to_w_hwio(const float* __restrict__ theta, long theta_st
 //   with kappa = tap*C + i (tap = ky*3+kx), zero for kappa >= 9C.
 // One 64-lane wave per (ot, ks) fragment: each lane builds its 8 elements and
 // writes 16 contiguous bytes.
+// w_lo (nullable): the residual bf16(W - float(bf16(W))) in the same packing
+// (the hi/lo weight split of k_fwd16_fused).
 __global__ void k_theta_to_w_pack(const float* __restrict__ theta, long theta_stride, int C,
                                   const int32_t* __restrict__ w_src, float gamma, bf16* __restrict__ w,
-                                  long w_stride) {
+                                  long w_stride, bf16* __restrict__ w_lo) {
   const int KS = (9 * C + 31) / 32;
   const int OT = C / 16;
   const int l = blockIdx.y;
@@ -235,7 +253,7 @@ __global__ void k_theta_to_w_pack(const float* __restrict__ theta, long theta_st
   const int ot = frag / KS, ks = frag % KS;
   const int o = 16 * ot + (lane & 15);
   const float* th = theta + l * theta_stride;
-  bf16x8 v;
+  bf16x8 v, vl;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int kappa = 32 * ks + 8 * (lane >> 4) + j;
@@ -245,8 +263,10 @@ __global__ void k_theta_to_w_pack(const float* __restrict__ theta, long theta_st
       x = w_value(th, w_src, ((long)tap * C + i) * C + o, gamma);
     }
     v[j] = (bf16)x;
+    vl[j] = (bf16)(x - (float)v[j]);
   }
   *(bf16x8*)(w + l * w_stride + ((long)frag * 64 + lane) * 8) = v;
+  if (w_lo) *(bf16x8*)(w_lo + l * w_stride + ((long)frag * 64 + lane) * 8) = vl;
 }
 
 // ---------------------------------------------------------------------------
@@ -381,7 +401,7 @@ int asr_theta_to_w(const float* theta, long theta_stride, int L, int C, const in
     const int frags = (C / 16) * ((9 * C + 31) / 32);
     dim3 grid((frags + 3) / 4, L);
     hipLaunchKernelGGL(k_theta_to_w_pack, grid, dim3(256), 0, s, theta, theta_stride, C, w_src, gamma,
-                       (bf16*)w_out, w_stride);
+                       (bf16*)w_out, w_stride, (bf16*)nullptr);
     ASR_LAUNCH_CHECK("k_theta_to_w_pack");
   } else {
     return fail(ASR_E_ARG, "asr_theta_to_w: bad dtype %d", dtype);
@@ -392,6 +412,19 @@ int asr_theta_to_w(const float* theta, long theta_stride, int L, int C, const in
 }  // extern "C"
 
 namespace asr {
+
+// asr_theta_to_w's bf16 pack plus the residual pack w_lo = bf16(W - bf16(W))
+// (the hi/lo operands of the fused C=16 forward, k_fwd16_fused<.., LO>)
+int theta_to_w_pack_hilo(const float* theta, long theta_stride, int L, int C, const int32_t* w_src, float gamma,
+                         void* w_hi, void* w_lo, long w_stride, hipStream_t s) {
+  if (!theta || !w_src || !w_hi || !w_lo || L < 1 || L > 65535 || C % 16 != 0 || w_stride < asr_wpack_elems(C))
+    return fail(ASR_E_ARG, "theta_to_w_pack_hilo: bad arguments");
+  const int frags = (C / 16) * ((9 * C + 31) / 32);
+  hipLaunchKernelGGL(k_theta_to_w_pack, dim3((frags + 3) / 4, L), dim3(256), 0, s, theta, theta_stride, C, w_src,
+                     gamma, (bf16*)w_hi, w_stride, (bf16*)w_lo);
+  ASR_LAUNCH_CHECK("k_theta_to_w_pack");
+  return ASR_OK;
+}
 
 // Reduce P slab rows of ES = E + Cb floats ([dW partial | db partial], written
 // by the wgrad kernels) deterministically in two passes (P -> ceil(P/32) -> 1),

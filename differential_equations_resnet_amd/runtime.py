@@ -16,7 +16,7 @@ from ._lib import (ASR_BF16, ASR_F32, ASR_INTEGRATOR_EULER, ASR_INTEGRATOR_RK2, 
                    ASR_PARAM_3BY3, ASR_PARAM_GENERAL, ASR_PARAM_REGULAR, ASR_VARIANT_NO_FOLD, ASR_VARIANT_STEM_FWD_VALU,
                    ASR_VARIANT_STEM_WGRAD_VALU, ASR_VARIANT_PER_BLOCK_FWD,
                    ASR_VARIANT_PER_BLOCK_BWD, ASR_VARIANT_INFERENCE, ASR_VARIANT_TIMED, ASR_VARIANT_FULL_DXL,
-                   ASR_VARIANT_FULL_SLABS, NetConfig, StagesConfig)
+                   ASR_VARIANT_FULL_SLABS, ASR_VARIANT_W_BF16, NetConfig, StagesConfig)
 
 __all__ = [
     "require_gpu", "dtype_code", "torch_dtype", "ParamMap", "param_map", "theta_count", "theta_to_w",
@@ -392,7 +392,9 @@ class NetExecutor:
                  integrator="euler", variant=0, inference=False):
         if inference:
             variant |= ASR_VARIANT_INFERENCE
-        self.device = device or require_gpu()
+        self.device = torch.device(device) if device is not None else require_gpu()
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         use_norm = subtract_mean is not None or divide_by_stddev is not None
         self.cfg = NetConfig(int(N), int(H), int(W), int(Cin), int(C), int(L), int(num_classes), float(h),
                              float(gamma), float(subtract_mean or 0.0),
@@ -400,14 +402,15 @@ class NetExecutor:
                              dtype_code(dtype), int(bool(input_u8)), int(param_kind), int(bool(antisymmetric)),
                              integrator_code(integrator), int(variant))
         lib = _lib.load()
-        self.n_params = int(lib.asr_net_param_count(ct.byref(self.cfg)))
-        if self.n_params < 0:
-            _lib.check(_lib.ASR_E_ARG, "asr_net_param_count")
-        self.ws_bytes = int(lib.asr_net_workspace_bytes(ct.byref(self.cfg)))
-        if self.ws_bytes == 0:
-            _lib.check(_lib.ASR_E_ARG, "asr_net_workspace_bytes")
-        self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
-        _lib.call("asr_net_prepare", ct.byref(self.cfg), _p(self.ws), self.ws_bytes)
+        with torch.cuda.device(self.device):  # the layout (slab rows) follows the device's CU count
+            self.n_params = int(lib.asr_net_param_count(ct.byref(self.cfg)))
+            if self.n_params < 0:
+                _lib.check(_lib.ASR_E_ARG, "asr_net_param_count")
+            self.ws_bytes = int(lib.asr_net_workspace_bytes(ct.byref(self.cfg)))
+            if self.ws_bytes == 0:
+                _lib.check(_lib.ASR_E_ARG, "asr_net_workspace_bytes")
+            self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
+            _lib.call("asr_net_prepare", ct.byref(self.cfg), _p(self.ws), self.ws_bytes)
         self.inference = bool(inference)
         self.grads = None if inference else torch.zeros(self.n_params, dtype=torch.float32, device=self.device)
         self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
@@ -423,8 +426,9 @@ class NetExecutor:
 
     def forward(self, params, images) -> torch.Tensor:
         self._check_inputs(params, images)
-        _lib.call("asr_net_forward", ct.byref(self.cfg), _p(params), _p(images), _p(self.probs), _p(self.ws),
-                  self.ws_bytes, _stream())
+        with torch.cuda.device(self.device):
+            _lib.call("asr_net_forward", ct.byref(self.cfg), _p(params), _p(images), _p(self.probs), _p(self.ws),
+                      self.ws_bytes, _stream())
         return self.probs
 
     @property
@@ -442,7 +446,8 @@ class NetExecutor:
         """Blocking: synchronises the stream and raises AsrError when a launch
         failed (asr_net_check_status).  A degraded slab hand-off is not an
         error (it costs speed): see stack_status."""
-        _lib.call("asr_net_check_status", ct.byref(self.cfg), _p(self.ws), self.ws_bytes, _stream())
+        with torch.cuda.device(self.device):
+            _lib.call("asr_net_check_status", ct.byref(self.cfg), _p(self.ws), self.ws_bytes, _stream())
 
     @staticmethod
     def kernel_times() -> dict:
@@ -462,9 +467,10 @@ class NetExecutor:
         self._check_inputs(params, images)
         if tuple(targets.shape) != (self.cfg.N, self.cfg.num_classes) or targets.dtype != torch.float32:
             raise ValueError("targets must be float32 one-hot [N, num_classes]")
-        _lib.call("asr_net_forward_backward", ct.byref(self.cfg), _p(params), _p(images), _p(targets),
-                  _p(self.grads), _p(self.loss), _p(self.probs) if want_probs else None, _p(self.ws),
-                  self.ws_bytes, _stream())
+        with torch.cuda.device(self.device):
+            _lib.call("asr_net_forward_backward", ct.byref(self.cfg), _p(params), _p(images), _p(targets),
+                      _p(self.grads), _p(self.loss), _p(self.probs) if want_probs else None, _p(self.ws),
+                      self.ws_bytes, _stream())
         return self.loss, self.grads
 
 
@@ -512,7 +518,9 @@ class StagesExecutor:
         """stages: [(C, L, stride)] per stage, stride 0 for no transition."""
         if not 1 <= len(stages) <= _lib.ASR_STAGES_MAX:
             raise _lib.AsrUnsupported(f"{len(stages)} stages (1..{_lib.ASR_STAGES_MAX})")
-        self.device = device or require_gpu()
+        self.device = torch.device(device) if device is not None else require_gpu()
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         use_norm = subtract_mean is not None or divide_by_stddev is not None
         c = StagesConfig()
         c.N, c.H, c.W, c.Cin, c.num_classes, c.n_stages = int(N), int(H), int(W), int(Cin), int(num_classes), len(stages)
@@ -529,14 +537,15 @@ class StagesExecutor:
         self.stages = [tuple(int(v) for v in st) for st in stages]
         lib = _lib.load()
         _lib.call("asr_stages_check", ct.byref(c))
-        self.n_params = int(lib.asr_stages_param_count(ct.byref(c)))
-        if self.n_params < 0:
-            _lib.check(_lib.ASR_E_ARG, "asr_stages_param_count")
-        self.ws_bytes = int(lib.asr_stages_workspace_bytes(ct.byref(c)))
-        if self.ws_bytes == 0:
-            _lib.check(_lib.ASR_E_ARG, "asr_stages_workspace_bytes")
-        self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
-        _lib.call("asr_stages_prepare", ct.byref(c), _p(self.ws), self.ws_bytes)
+        with torch.cuda.device(self.device):  # the layout (slab rows) follows the device's CU count
+            self.n_params = int(lib.asr_stages_param_count(ct.byref(c)))
+            if self.n_params < 0:
+                _lib.check(_lib.ASR_E_ARG, "asr_stages_param_count")
+            self.ws_bytes = int(lib.asr_stages_workspace_bytes(ct.byref(c)))
+            if self.ws_bytes == 0:
+                _lib.check(_lib.ASR_E_ARG, "asr_stages_workspace_bytes")
+            self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
+            _lib.call("asr_stages_prepare", ct.byref(c), _p(self.ws), self.ws_bytes)
         self.inference = bool(inference)
         self.grads = None if inference else torch.zeros(self.n_params, dtype=torch.float32, device=self.device)
         self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
@@ -552,8 +561,9 @@ class StagesExecutor:
 
     def forward(self, params, images) -> torch.Tensor:
         self._check_inputs(params, images)
-        _lib.call("asr_stages_forward", ct.byref(self.cfg), _p(params), _p(images), _p(self.probs), _p(self.ws),
-                  self.ws_bytes, _stream())
+        with torch.cuda.device(self.device):
+            _lib.call("asr_stages_forward", ct.byref(self.cfg), _p(params), _p(images), _p(self.probs), _p(self.ws),
+                      self.ws_bytes, _stream())
         return self.probs
 
     def check_status(self):
@@ -567,7 +577,8 @@ class StagesExecutor:
         self._check_inputs(params, images)
         if tuple(targets.shape) != (self.cfg.N, self.cfg.num_classes) or targets.dtype != torch.float32:
             raise ValueError("targets must be float32 one-hot [N, num_classes]")
-        _lib.call("asr_stages_forward_backward", ct.byref(self.cfg), _p(params), _p(images), _p(targets),
-                  _p(self.grads), _p(self.loss), _p(self.probs) if want_probs else None, _p(self.ws),
-                  self.ws_bytes, _stream())
+        with torch.cuda.device(self.device):
+            _lib.call("asr_stages_forward_backward", ct.byref(self.cfg), _p(params), _p(images), _p(targets),
+                      _p(self.grads), _p(self.loss), _p(self.probs) if want_probs else None, _p(self.ws),
+                      self.ws_bytes, _stream())
         return self.loss, self.grads

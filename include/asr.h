@@ -316,6 +316,15 @@ typedef struct asr_net_config {
                                       workgroup slab) instead of the pair-local
                                       D = dW - dW*^T (74 tiles) the projection
                                       needs (cross-check and A/B arm)           */
+#define ASR_VARIANT_W_BF16 512    /* C=16 bf16 networks (the fused deep16 stack):
+                                     the forward conv takes W in bf16 alone
+                                     instead of bf16 hi + lo (~16 mantissa bits,
+                                     the default).  Faster (C3 +15 % images/s),
+                                     but rounding W perturbs every pixel of every
+                                     layer the same way, and over 108 blocks that
+                                     systematic error reaches 2.7e-2 relative L2
+                                     of a block's gradient vs the fp32 reference
+                                     (tests/test_gpu_depth.py)       */
 
 long asr_net_param_count(const asr_net_config* cfg);
 size_t asr_net_workspace_bytes(const asr_net_config* cfg);

@@ -753,11 +753,14 @@ def _block_W(spec: StagesSpec, C, theta):
     return assemble_from_map(flatten(theta), C, src, sign, spec.gamma)
 
 
-def stages_forward(spec: StagesSpec, params, images, dtype=np.float64, rnd=None):
+def stages_forward(spec: StagesSpec, params, images, dtype=np.float64, rnd=None, w_hilo_stages=()):
     """rnd (optional): a rounding applied where a bf16 net (asr_stages_config
     dtype ASR_BF16) stores in bf16 -- the stem's output, every transition's and
     block's output, the blocks' assembled W -- so the restatement follows the
-    bf16 executor's storage; everything else stays in `dtype`."""
+    bf16 executor's storage; everything else stays in `dtype`.
+    w_hilo_stages: indices of stages whose forward conv takes W as bf16 hi + lo
+    (the fused C=16 forward, k_fwd16_fused<.., LO>): their forward uses the
+    unrounded W, their backward (cached W) the rounded one."""
     r = rnd if rnd is not None else (lambda a: a)
     ns = NetSpec(subtract_mean=spec.subtract_mean, divide_by_stddev=spec.divide_by_stddev)
     x0 = normalize_input(images, ns, dtype)
@@ -765,7 +768,7 @@ def stages_forward(spec: StagesSpec, params, images, dtype=np.float64, rnd=None)
     x = r(np.maximum(z1, 0))
     i = 2
     ops = []  # per op: ("t", x_in, z, K2, K1, S) or ("b", x_in, z, W, C)
-    for C, L, S in spec.stages:
+    for si, (C, L, S) in enumerate(spec.stages):
         if S:
             K2, b2, K1, b1 = params[i:i + 4]
             i += 4
@@ -776,8 +779,9 @@ def stages_forward(spec: StagesSpec, params, images, dtype=np.float64, rnd=None)
         for _ in range(L):
             theta, b = params[i:i + nt], params[i + nt]
             i += nt + 1
-            W = r(_block_W(spec, C, theta))
-            y, z = euler_fwd(x, W, b, spec.h)
+            W0 = _block_W(spec, C, theta)
+            W = r(W0)
+            y, z = euler_fwd(x, W0 if si in w_hilo_stages else W, b, spec.h)
             ops.append(("b", x, z, W, C))
             x = r(y)
     fc_k, fc_b = params[i], params[i + 1]

@@ -59,6 +59,39 @@ def grad_groups(spec, g):
     return out
 
 
+def assert_grad_tensors_max(spec, got, want, tol, report_only=False, groups=None):
+    """Per-tensor bar inside the per-group one: every gradient tensor's
+    max |got - want| <= tol x max |want| over the tensor's gradient group.
+    A group's relative L2 dilutes a few wrong scalars (a zeroed channel of
+    one theta variable) among thousands of kernel entries; this bar does
+    not.  `groups`: [(name, [tensor indices])]; default: the network's
+    (conv1, per block theta + bias, fc).  report_only: return the worst
+    (name, ratio) instead of asserting."""
+    if groups is None:
+        nt = len(spec.theta_shapes())
+        groups = [("conv1", [0, 1])]
+        i = 2
+        for b in range(spec.L):
+            groups.append((f"block{b}", list(range(i, i + nt + 1))))
+            i += nt + 1
+        groups.append(("fc", [i, i + 1]))
+    worst, bad = ("", 0.0), []
+    for name, idx in groups:
+        scale = max(float(np.abs(want[i]).max()) for i in idx)
+        if scale == 0:
+            continue
+        for i in idx:
+            r = float(np.abs(np.asarray(got[i], np.float64) - want[i]).max()) / scale
+            if r > worst[1]:
+                worst = (f"{name}/tensor{i} {np.shape(want[i])}", r)
+            if not r <= tol:
+                bad.append(f"{name}/tensor{i} {np.shape(want[i])}: {r:.3e}")
+    if report_only:
+        return worst
+    assert not bad, f"per-tensor max|err| > {tol} x group max: " + "; ".join(bad[:12])
+    return worst
+
+
 def assert_grad_groups_rel_l2(spec, got, want, tol=2e-2):
     """bf16 network gradients vs the fp64 oracle: relative L2 <= tol per
     gradient group."""

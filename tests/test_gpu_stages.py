@@ -20,7 +20,7 @@ bf16 storage rounding, and the bf16 network bar against the plain oracle.
 import numpy as np
 import pytest
 
-from helpers import assert_close, bf16_round, rel_l2
+from helpers import assert_close, assert_grad_tensors_max, bf16_round, rel_l2
 from oracle import asr_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -197,22 +197,39 @@ def test_training_multistage_overfits_one_batch(tmp_path):
     assert rows[0][3] == "conv1_kernel_gradient_mean_norm" and "res4_1_branch2_kernel_gradient_mean_norm" in rows[0]
 
 
-def _stage_groups(spec, g):
-    """(name, flat array) per layer: conv1 kernel + bias, each transition's
-    four tensors, each block's theta variables + bias, fc kernel + bias --
-    the per-layer groups of the reference's gradient norms
+def _stage_group_indices(spec):
+    """(name, [parameter indices]) per layer: conv1 kernel + bias, each
+    transition's four tensors, each block's theta variables + bias, fc
+    kernel + bias -- the per-layer groups of the reference's gradient norms
     (training.py:385-409)."""
-    out = [("conv1", np.concatenate([np.ravel(g[0]), np.ravel(g[1])]))]
+    out = [("conv1", [0, 1])]
     i = 2
     for si, (C, L, S) in enumerate(spec.stages):
         if S:
-            out.append((f"stage{si}/transition", np.concatenate([np.ravel(a) for a in g[i:i + 4]])))
+            out.append((f"stage{si}/transition", list(range(i, i + 4))))
             i += 4
         nt = len(spec.block_spec(C).theta_shapes())
         for b in range(L):
-            out.append((f"stage{si}/block{b}", np.concatenate([np.ravel(a) for a in g[i:i + nt + 1]])))
+            out.append((f"stage{si}/block{b}", list(range(i, i + nt + 1))))
             i += nt + 1
-    out.append(("fc", np.concatenate([np.ravel(g[i]), np.ravel(g[i + 1])])))
+    out.append(("fc", [i, i + 1]))
+    return out
+
+
+def _stage_groups(spec, g):
+    """(name, flat array) per layer group (_stage_group_indices)."""
+    return [(name, np.concatenate([np.ravel(g[j]) for j in idx])) for name, idx in _stage_group_indices(spec)]
+
+
+def _hilo_stages(spec):
+    """Stages the executor runs on the fused C=16 kernels (asr_stages.hip: a bf16 stage at C=16,
+    32 x 32 with blocks), whose forward takes W as bf16 hi + lo (k_fwd16_fused<.., LO>)."""
+    out, H = set(), spec.H
+    for si, (C, L, S) in enumerate(spec.stages):
+        if S:
+            H = -(-H // S)
+        if C == 16 and H == 32 and spec.W == 32 and L > 0:
+            out.add(si)
     return out
 
 
@@ -223,7 +240,7 @@ def _bf16_net_errors(ex, spec, params, imgs, onehot, rnd=None):
     flat = _t(O.flatten(params))
     assert flat.numel() == ex.n_params == spec.n_params()
     probs_gpu = ex.forward(flat, torch.from_numpy(imgs).cuda()).cpu().numpy()
-    probs, cache = O.stages_forward(spec, params, imgs, rnd=rnd)
+    probs, cache = O.stages_forward(spec, params, imgs, rnd=rnd, w_hilo_stages=_hilo_stages(spec) if rnd else ())
     loss, grads = ex.forward_backward(flat, torch.from_numpy(imgs).cuda(), _t(onehot), want_probs=True)
     assert np.array_equal(ex.probs.cpu().numpy(), probs_gpu)  # the training call's forward is the same kernels
     want_loss = O.net_loss(probs, onehot)
@@ -231,31 +248,43 @@ def _bf16_net_errors(ex, spec, params, imgs, onehot, rnd=None):
     assert np.abs(g_want[0]).max() > 0  # not saturated: the stem's gradient is live
     g_got = O.unflatten(grads.cpu().numpy().astype(np.float64), [p.shape for p in params])
     errs = {name: rel_l2(a, b) for (name, a), (_, b) in zip(_stage_groups(spec, g_got), _stage_groups(spec, g_want))}
-    return float(np.abs(probs_gpu - probs).max()), abs(loss.item() - want_loss) / abs(want_loss), errs
+    return float(np.abs(probs_gpu - probs).max()), abs(loss.item() - want_loss) / abs(want_loss), errs, g_got, g_want
 
 
 def _assert_bf16_net(ex, spec, params, imgs, onehot):
     """Two bars.  (1) Against the oracle with the executor's bf16 storage
     rounding (helpers.bf16_round at every stored activation, chain gradient
-    and block W): what remains is fp32 accumulation order and the bf16
+    and block W; the C=16 32x32 stage's forward with the unrounded W, as its
+    hi/lo kernel): what remains is fp32 accumulation order and the bf16
     roundings it flips -- probabilities within 2e-3, loss within 1e-3
-    relative, every layer's gradient within 2e-2 relative L2 (the
-    single-stage bf16 network bar; measured up to 1.0e-2, at
-    conv1, whose gradient sums every flip propagated through the net).  (2) Against
-    the plain fp64 oracle (the reference's math) at the single-stage bf16
-    network bar: probabilities within 2e-2, loss within 1e-2 relative, every
-    layer's gradient within 5e-2 relative L2."""
-    dp, dl, errs = _bf16_net_errors(ex, spec, params, imgs, onehot, rnd=bf16_round)
+    relative, every layer's gradient within 2e-2 relative L2.
+    (2) Against the plain fp64 oracle (the reference's math): probabilities
+    within 2e-2, loss within 1e-2 relative, and every layer's gradient within
+    max(2e-2, 1.5 x the same layer's deviation of the bf16-storage oracle from
+    the plain one) relative L2 -- the SURVEY §8c bar, widened only for a layer
+    whose gradient bf16 storage itself moves further (measured: conv1 of the
+    two-blocks-per-stage nets, 3.7e-2 in the CPU emulation, a sum over every
+    flipped relu of the net: tools/bf16_depth_emulate.py); the He
+    ResNet-32 itself meets 2e-2 everywhere (1.2e-2).  Plus per tensor max |err|
+    <= 5e-2 x its layer's max |ref| (helpers.assert_grad_tensors_max: a wrong
+    tensor that matters to its layer fails even where the layer's relative L2
+    dilutes it)."""
+    dp, dl, errs, _, g_store = _bf16_net_errors(ex, spec, params, imgs, onehot, rnd=bf16_round)
     print(f"\nbf16-storage oracle: probs {dp:.2e} loss {dl:.2e} worst grad {max(errs.values()):.2e} "
           f"({max(errs, key=errs.get)})")
     assert dp < 2e-3 and dl < 1e-3, (dp, dl)
     bad = {k: v for k, v in errs.items() if not v <= 2e-2}
     assert not bad, bad
-    dp, dl, errs = _bf16_net_errors(ex, spec, params, imgs, onehot)
-    print(f"fp64 oracle: probs {dp:.2e} loss {dl:.2e} worst grad {max(errs.values()):.2e} ({max(errs, key=errs.get)})")
+    dp, dl, errs, g_got, g_want = _bf16_net_errors(ex, spec, params, imgs, onehot)
+    floor = {name: rel_l2(a, b) for (name, a), (_, b) in zip(_stage_groups(spec, g_store), _stage_groups(spec, g_want))}
+    worst_t = assert_grad_tensors_max(None, g_got, g_want, 5e-2, report_only=True, groups=_stage_group_indices(spec))
+    print(f"fp64 oracle: probs {dp:.2e} loss {dl:.2e} worst grad {max(errs.values()):.2e} ({max(errs, key=errs.get)}; "
+          f"bf16-storage floor there {floor[max(errs, key=errs.get)]:.2e}), worst tensor {worst_t[1]:.2e} ({worst_t[0]})")
     assert dp < 2e-2 and dl < 1e-2, (dp, dl)
-    bad = {k: v for k, v in errs.items() if not v <= 5e-2}
+    bad = {k: (v, floor[k]) for k, v in errs.items() if not v <= max(2e-2, 1.5 * floor[k])}
     assert not bad, bad
+    assert_grad_tensors_max(None, g_got, g_want, 5e-2, groups=_stage_group_indices(spec))
+    return errs
 
 
 @pytest.mark.parametrize("stages,kind,anti,gamma", [
@@ -314,8 +343,33 @@ def test_resnet32_he_model_bf16_matches_oracle():
     onehot = np.eye(10)[rng.integers(0, 10, 8)]
     ex = nv.state.executor(8, "bfloat16", True)
     assert ex.dtype == "bfloat16"
-    _assert_bf16_net(ex, spec, params, imgs, onehot)
+    errs = _assert_bf16_net(ex, spec, params, imgs, onehot)
+    assert max(errs.values()) <= 2e-2, errs  # the He ResNet-32 at the plain SURVEY §8c bar, no floor
     # the Model API's own call runs the same executor
     loss, grads, probs = nv.forward_backward(imgs, onehot.astype(np.float32), want_probs=True)
     p_want, _ = O.stages_forward(spec, params, imgs)
     assert np.abs(probs.cpu().numpy() - p_want).max() < 2e-2
+
+
+def test_workspace_on_another_device_fails_before_launch():
+    """The executors' workspace layout follows the CU count of the device it was
+    sized on (the weight-gradient slab rows), so a call whose workspace is not
+    device memory of the current device fails with ASR_E_WORKSPACE before any
+    launch (check_ws_device).  A pinned host buffer stands in for
+    another device's memory on the one-GPU box."""
+    import ctypes as ct
+
+    from differential_equations_resnet_amd import _lib
+    from differential_equations_resnet_amd.runtime import NetExecutor, StagesExecutor, _p, _stream
+    for ex, fn in [(StagesExecutor(2, 32, 32, 3, [(16, 1, 0), (32, 1, 2)], 10, 0.5, dtype="bfloat16"),
+                    "asr_stages_forward"),
+                   (NetExecutor(2, 32, 32, 3, 16, 2, 10, 0.5, dtype="bfloat16"), "asr_net_forward")]:
+        host = torch.empty(ex.ws_bytes, dtype=torch.uint8, pin_memory=True)
+        params = torch.zeros(ex.n_params, dtype=torch.float32, device="cuda")
+        imgs = torch.zeros(2, 32, 32, 3, dtype=torch.uint8, device="cuda")
+        rc = getattr(_lib.load(), fn)(ct.byref(ex.cfg), _p(params), _p(imgs), _p(ex.probs), host.data_ptr(),
+                                      ex.ws_bytes, _stream())
+        assert rc == _lib.ASR_E_WORKSPACE, (fn, rc)
+        assert "current device" in _lib.last_error()
+        ex.forward(params, imgs)  # its own workspace still works
+        torch.cuda.synchronize()
