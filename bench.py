@@ -87,8 +87,9 @@ HE32 = ("He-style antisym-ResNet-32 (num_stages=4, blocks [10,10,10] at 32^2 x 1
 STAGE_CONFIGS = {
     "he32": ([(16, 10, 0), (32, 9, 2), (64, 9, 2)], 128, "float32", HE32 + " batch 128/GPU fp32"),
     "he32_bf16": ([(16, 10, 0), (32, 9, 2), (64, 9, 2)], 512, "bfloat16",
-                  HE32 + " batch 512/GPU bf16 (identity blocks bf16, fp32 accumulation; stem, transitions, head and "
-                         "weight gradients fp32)"),
+                  HE32 + " batch 512/GPU bf16 (bf16 activations; identity blocks and their weight gradients on bf16 "
+                         "MFMA with fp32 accumulation, the 32^2 x 16 stage's forward with bf16 hi + lo weights; fp32 "
+                         "parameters, gradients and Adam; stem, transition and head weights fp32)"),
 }
 # the reference's own measurements of the same metric (TF 1.12, fp32, one NVIDIA GPU)
 REFERENCE = {
@@ -364,7 +365,7 @@ def stack_roofline(rt, N, L, reps, h, C=16, rk2=False):
                 bytes_bwd=bytes_bwd)
 
 
-def cpu_baseline(threads):
+def cpu_baseline(threads, c1_only=False):
     """The oracle's PyTorch-CPU restatements of the reference TF graph
     (oracle/torch_cpu_ref.py), timed on this box's host cores: the metric's
     workload (C2: C=64, 30 blocks, batch 512) with the reference's op-by-op
@@ -400,6 +401,12 @@ def cpu_baseline(threads):
               file=sys.stderr, flush=True)
         return round(batch * steps / dt, 3), dt
 
+    if c1_only:  # --config c1: BASELINE C1 itself
+        c1, t1 = run(16, 18, 128, 4, "reference")
+        return {"value": c1, "unit": "images/s", "cores": threads, "kind": "port",
+                "sample": f"4 training steps (fwd+bwd+Adam) of BASELINE C1 (C=16, 18 blocks, batch 128, fp32) in the "
+                          f"torch-CPU op-by-op restatement of the reference TF graph, after 1 untimed step; "
+                          f"{t1:.1f} s on {threads} threads of {cpu}"}
     c2, t2 = run(64, 30, 512, 1, "reference")
     c2v, t2v = run(64, 30, 512, 1, "vectorised")
     c1, t1 = run(16, 18, 128, 2, "reference")
@@ -501,6 +508,39 @@ def cpu_eval_baseline(threads):
                       f"op-by-op restatement of the reference TF graph, after 1 untimed pass; {dt:.1f} s"}
 
 
+def cpu_stages_baseline(threads, stages, flat, h, images=256):
+    """CPU baseline of a multi-stage net (--config he32 / he32_bf16): the
+    oracle's numpy restatement of the reference graph (oracle.asr_oracle
+    stages_forward / stages_backward: tfkeras_resnets.py:547-597 with the
+    single_layer_conv_block transitions, :204-269) in float32 on a bounded
+    sample of `images` images, forward + backward (no Adam: elementwise,
+    <1 % of a step), after one untimed pass."""
+    import threadpoolctl
+    from oracle import asr_oracle as O
+    spec = O.StagesSpec(stages=[tuple(s) for s in stages], h=h)
+    shapes = spec.param_shapes()
+    params, o = [], 0
+    for shp in shapes:
+        k = int(np.prod(shp))
+        params.append(flat[o:o + k].reshape(shp).astype(np.float32))
+        o += k
+    rng = np.random.default_rng(0)
+    imgs = rng.integers(0, 256, (images, 32, 32, 3)).astype(np.uint8)
+    onehot = np.eye(10, dtype=np.float32)[rng.integers(0, 10, images)]
+    with threadpoolctl.threadpool_limits(threads):
+        def one():
+            probs, cache = O.stages_forward(spec, params, imgs, dtype=np.float32)
+            O.stages_backward(spec, params, cache, onehot)
+        one()
+        t0 = time.perf_counter()
+        one()
+        dt = time.perf_counter() - t0
+    return {"value": round(images / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"1 forward + backward of {images} images in the oracle's numpy float32 restatement of the "
+                      f"reference graph (stages_forward / stages_backward), after 1 untimed pass; {dt:.1f} s on "
+                      f"{threads} threads (BLAS)"}
+
+
 def stages_params(stages, num_classes=10, seed=0):
     """Flat parameters in the asr_stages_config order: he_normal (2-sigma
     truncated) kernels, zero biases, block thetas x THETA_SCALE and the fc
@@ -599,6 +639,9 @@ def stages_main(args):
                                    "stem, head, reductions, Adam)"},
             "cpu_baseline": None,
         }
+        if world == 1 and not args.no_cpu_baseline:
+            out_line["cpu_baseline"] = cpu_stages_baseline(args.cpu_threads or host_threads(), stages,
+                                                           params.cpu().numpy(), h)
         print(json.dumps(out_line), flush=True)
     distributed.shutdown()
 
@@ -772,7 +815,8 @@ def main():
                     "avg_us": round(rb["t"] * 1e6, 2), "algorithmic_bytes": rb["bytes"],
                     "frac": round(rb["bytes"] / rb["t"] / 1e9 / HBM_PEAK_GBS, 4),
                     "fwd_us": round(rb["t_fwd"] * 1e6, 2), "bwd_with_reduction_us": round(rb["t_bwd"] * 1e6, 2),
-                    "operands": "random (x, dy ~ N(0,1) in bf16, theta ~ N(0, 0.05^2)) through the stack / layer ABI"}
+                    "operands": f"random (x, dy ~ N(0,1) in {'bf16' if dtype_name == 'bfloat16' else 'fp32'}, "
+                                f"theta ~ N(0, 0.05^2)) through the stack / layer ABI"}
         co = co_bound(args.config, flops, bytes_blk, t_blk, train, dtype_name)
         if co:
             roof.update(co)
@@ -781,12 +825,16 @@ def main():
             threads = args.cpu_threads or host_threads()
             if args.config == "c2":
                 cpu = cpu_baseline(threads)
+            elif args.config == "c1":
+                cpu = cpu_baseline(threads, c1_only=True)
             elif args.config == "c2_eval":
                 cpu = cpu_eval_baseline(threads)
         ref = REFERENCE.get(args.config)
         out = {
-            "metric": METRICS.get(args.config, METRIC if train else METRIC.replace("(fwd+bwd)",
-                                                                                 "(forward only, evaluation)")),
+            "metric": METRICS.get(args.config, (METRIC if train else METRIC.replace("(fwd+bwd)", "(forward only, "
+                                                                                 "evaluation)"))
+                                  if args.config in ("c2", "c2_eval") else
+                                  f"CIFAR-10 images/sec ({'fwd+bwd' if train else 'forward only'}) {desc}; {world} GPU"),
             "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": round(value / ref[0], 1) if ref else None,

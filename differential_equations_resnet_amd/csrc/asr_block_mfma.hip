@@ -94,7 +94,7 @@ enum { FWD_EULER = 0, FWD_CONV = 1, BWD_EULER = 2, BWD_CONV = 3 };
 #define ASR_BLK_TRACE 0
 #endif
 #if ASR_BLK_TRACE
-constexpr int kTrBands = 40, kTrSlots = 6;
+constexpr int kTrBands = 40, kTrSlots = 8;
 __device__ unsigned long long g_btrace[2][2][kTrBands][kTrSlots];
 __device__ unsigned long long g_bclock[2][1024][4];
 __device__ __forceinline__ void tr_store(unsigned long long* p, unsigned long long t) {
@@ -2595,6 +2595,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         }
       }
       nst = nld;
+      if (wave == 0) ASR_BTR(1, 0, it, 3);
       if (!RK2 && cur.b + 1 < nb) {  // (RK2: the wgrad waves copy them; its dgrad role has no registers to spare)
         // the next item continues this image: its tile rows 0, 1 are this band's rows BR, BR+1
         // (dz, x; dy row 1 only), copied here, where the dgrad waves would otherwise wait at
@@ -2616,7 +2617,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
                     lds_ld128(base + sreg + buf * LL::TILE + srow * LL::ROWB + o));
         }
       }
-      if (wave == 0) ASR_BTR(1, 0, it, 3);
+      if (wave == 0) ASR_BTR(1, 0, it, 4);
       adv(cur);
     }
     barrier_vm(0);  // matches the wgrad waves' end-of-loop barrier
@@ -2927,6 +2928,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       auto convert_next = [&]() {  // the next band's dz of this wave's own row
         if (more) {
           vm_wait(0);  // own dy row and mask dwords of band it+1 (x DMA and fold loads too)
+          if (wave == 4) ASR_BTR(1, 1, it, 4);
           convert_own(orow, buf ^ 1, mwv);
         }
       };
@@ -2944,7 +2946,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       mfma_band(std::integral_constant<int, 0>{});
       if (wave == 4) ASR_BTR(1, 1, it, 3);
       convert_next();
-      if (wave == 4) ASR_BTR(1, 1, it, 4);
+      if (wave == 4) ASR_BTR(1, 1, it, 5);
       if (RK2 && cont) {  // halo rows of the next band of this image (Euler: the dgrad waves copy them)
         // compiler-visible LDS accesses: the item's DMAs were retired by the vm_wait(0)
         // before the convert (cont implies more), so hipcc's own waits cost nothing
@@ -3023,7 +3025,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
           accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
-      if (wave == 4) ASR_BTR(1, 1, it, 5);
+      if (wave == 4) ASR_BTR(1, 1, it, 6);
       cur = nxt;
       adv(nxt);
     }
@@ -3664,27 +3666,31 @@ extern "C" int asr_debug_stack_backward(int grid) {
 
 namespace asr {
 namespace blk {
-__device__ unsigned g_stack_degraded_taken = 0u;
 // asr_stack_status: read (and with reset, clear) the degraded-wait count in one
-// device atomic, so a stacked backward still running on another stream cannot
-// add a count between the read and the reset
-__global__ void k_stack_status_take(int reset) {
-  g_stack_degraded_taken =
-      reset ? __hip_atomic_exchange(&g_stack_degraded, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-            : __hip_atomic_load(&g_stack_degraded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// device atomic, into the calling host thread's own result word
+__global__ void k_stack_status_take(int reset, unsigned* out) {
+  *out = reset ? __hip_atomic_exchange(&g_stack_degraded, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+               : __hip_atomic_load(&g_stack_degraded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 }  // namespace blk
 }  // namespace asr
 
 // host, blocking: waits of stacked-backward workgroups that ran out since the
 // last reset (each one a slower launch, never a wrong gradient); reset != 0
-// then clears the count (atomically with the read, on the device)
+// then clears the count (atomically with the read, on the device).  Each call
+// has its own result word (concurrent callers never read each other's), and
+// the launch status comes from hipLaunchKernel itself: no hipGetLastError,
+// which would also report and clear an unrelated pending error.
 extern "C" int asr_stack_status(int reset) {
-  hipLaunchKernelGGL(asr::blk::k_stack_status_take, dim3(1), dim3(1), 0, (hipStream_t)0, reset ? 1 : 0);
-  if (hipGetLastError() != hipSuccess) return asr::fail(ASR_E_HIP, "asr_stack_status: launch failed");
+  unsigned* d = nullptr;
+  if (hipMalloc(&d, sizeof(unsigned)) != hipSuccess) return asr::fail(ASR_E_HIP, "asr_stack_status: hipMalloc failed");
+  int rs = reset ? 1 : 0;
+  void* args[] = {&rs, &d};
+  hipError_t e = hipLaunchKernel((const void*)asr::blk::k_stack_status_take, dim3(1), dim3(1), args, 0, (hipStream_t)0);
   unsigned n = 0;
-  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(asr::blk::g_stack_degraded_taken), sizeof(n)) != hipSuccess)
-    return asr::fail(ASR_E_HIP, "asr_stack_status: hipMemcpyFromSymbol failed");
+  if (e == hipSuccess) e = hipMemcpy(&n, d, sizeof(n), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return asr::fail(ASR_E_HIP, "asr_stack_status: %s", hipGetErrorString(e));
   return (int)std::min<unsigned>(n, 0x7fffffffu);
 }
 

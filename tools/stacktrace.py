@@ -36,10 +36,10 @@ for _ in range(a.reps):
     rt.block_stack_backward(dy, x, ys, masks, w, pm, 0.25, 0.0)
 torch.cuda.synchronize()
 cl = ctypes.CDLL(path)
-tb = (ctypes.c_uint64 * (2 * 2 * 40 * 6))()
+tb = (ctypes.c_uint64 * (2 * 2 * 40 * 8))()
 cb = (ctypes.c_uint64 * (2 * 1024 * 4))()
 assert cl.asr_debug_blk_trace(tb, ctypes.sizeof(tb), cb, ctypes.sizeof(cb)) == 0
-tr = np.frombuffer(tb, np.uint64).reshape(2, 2, 40, 6).astype(np.int64)
+tr = np.frombuffer(tb, np.uint64).reshape(2, 2, 40, 8).astype(np.int64)
 ck = np.frombuffer(cb, np.uint64).reshape(2, 1024, 4).astype(np.int64)
 for k, name in ((0, "k_fwd3_stack"), (1, "k_bwd3_stack")):
     c = ck[k]
@@ -63,6 +63,6 @@ def rows(t, names, nslot):
 print("k_fwd3_stack wave 0 (cycles):")
 rows(tr[0, 0], ["barrier", "dma+copy", "conv", "epilogue"], 5)
 print("k_bwd3_stack dgrad wave 0:")
-rows(tr[1, 0], ["barrier", "conv", "epilogue"], 4)
+rows(tr[1, 0], ["barrier", "conv", "epilogue", "halo"], 5)
 print("k_bwd3_stack wgrad wave 4:")
-rows(tr[1, 1], ["poll+bar", "issue", "mfma", "convert", "halo+slab"], 6)
+rows(tr[1, 1], ["poll+bar", "issue", "mfma", "vmwait", "convert", "fold+slab"], 7)
