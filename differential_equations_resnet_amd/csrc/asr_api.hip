@@ -49,9 +49,10 @@ static bool mfma_supported(int C, int W) { return (C == 16 || C == 32 || C == 64
 // asr_conv_f32.hip: bf16 Euler blocks at any stage width (W in {32, 16, 8}), the multi-stage nets' path
 bool convb_supported(int W, int C);
 int convb_forward(const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h, int N, int H, int W,
-                  int C, hipStream_t s);
+                  int C, hipStream_t s, bool conv_only = false);
 int convb_backward(const void* dy, const uint8_t* mask, const void* x, const void* w, float h, float two_gamma, int N,
-                   int H, int W, int C, void* dx, bool need_w, float* slabs, int* nslabs, hipStream_t s);
+                   int H, int W, int C, void* dx, bool need_w, float* slabs, int* nslabs, hipStream_t s,
+                   bool conv_only = false);
 // asr_deep16.hip
 bool deep16_supported(int H, int W, int C);
 bool block_stack_fwd_supported(int N, int H, int W, int C);
@@ -165,10 +166,11 @@ static int block_backward(int mode, const void* dy, const void* x, const uint8_t
   if (fold_done) *fold_done = 0;
   if (dtype == ASR_BF16) {
     if (!dx && !need_w) return ASR_OK;
-    if (!mfma_supported(C, W)) {  // W = 16 / 8: the any-width bf16 kernels (plain Euler blocks only)
-      if (mode != ASR_MODE_EULER || extra || skip_dy || relu_dx || fold_slabs || accum_slabs || !convb_supported(W, C))
-        return fail(ASR_E_UNSUPPORTED, "bf16 backward at C=%d W=%d: Euler blocks only", C, W);
-      return convb_backward(dy, mask, x, w, h, 2.f * gamma, N, H, W, C, dx, need_w, slabs, nsl, s);
+    if (!mfma_supported(C, W)) {  // W = 16 / 8: the any-width bf16 kernels (plain Euler blocks and bare convs)
+      if (extra || skip_dy || relu_dx || fold_slabs || accum_slabs || !convb_supported(W, C))
+        return fail(ASR_E_UNSUPPORTED, "bf16 backward at C=%d W=%d: plain Euler blocks and convs only", C, W);
+      return convb_backward(dy, mask, x, w, h, 2.f * gamma, N, H, W, C, dx, need_w, slabs, nsl, s,
+                            mode == ASR_MODE_CONV);
     }
     const int cm = (mode == ASR_MODE_EULER) ? 2 : 3;  // BWD_EULER / BWD_CONV
     return block_bwd_mfma(cm, dy, x, mask, w, h, 2.f * gamma, N, H, W, C, dx, slabs, nsl, extra, skip_dy ? 1 : 0, s,
@@ -637,10 +639,10 @@ int asr_conv_forward(int mode, const void* x, void* y, uint8_t* mask, const void
   if (mode != ASR_MODE_EULER && mode != ASR_MODE_CONV) return fail(ASR_E_ARG, "asr_conv_forward: bad mode %d", mode);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == ASR_BF16) {
-    if (!mfma_supported(C, W)) {  // the Euler block at W = 16 / 8 (multi-stage nets)
-      if (mode == ASR_MODE_EULER && convb_supported(W, C)) return convb_forward(x, y, mask, w, bias, h, N, H, W, C, s);
-      return fail(ASR_E_UNSUPPORTED, "bf16 conv needs C in {16,32,64} and W == 32 (W in {16, 8}: Euler mode) (C=%d W=%d)",
-                  C, W);
+    if (!mfma_supported(C, W)) {  // W = 16 / 8 (multi-stage nets): the any-width bf16 kernels, Euler block or bare conv
+      if (convb_supported(W, C))
+        return convb_forward(x, y, mask, w, bias, h, N, H, W, C, s, mode == ASR_MODE_CONV);
+      return fail(ASR_E_UNSUPPORTED, "bf16 conv needs C in {16,32,64} and W in {32, 16, 8} (C=%d W=%d)", C, W);
     }
     if (mode == ASR_MODE_EULER && deep16_supported(H, W, C))
       return deep16_forward(x, y, 0, mask, 0, w, bias, 0, h, N, 1, true, s);

@@ -97,6 +97,12 @@ enum { FWD_EULER = 0, FWD_CONV = 1, BWD_EULER = 2, BWD_CONV = 3 };
 constexpr int kTrBands = 40, kTrSlots = 8;
 __device__ unsigned long long g_btrace[2][2][kTrBands][kTrSlots];
 __device__ unsigned long long g_bclock[2][1024][4];
+// every workgroup at every block switch of k_bwd3_stack (the first band of block l), [wg][l][slot]:
+// 0 wgrad wave 4 before the done[] poll, 1 after the poll and fence, 2 after its band barrier,
+// 3 dgrad wave 0 before its band barrier, 4 after it (s_memtime: durations inside a workgroup);
+// 5 / 6 s_memrealtime at slots 0 / 2 (100 MHz, one time base for every workgroup)
+constexpr int kSwBlocks = 128, kSwSlots = 7;
+__device__ unsigned long long g_bswitch[256][kSwBlocks][kSwSlots];
 __device__ __forceinline__ void tr_store(unsigned long long* p, unsigned long long t) {
   unsigned lo = (unsigned)t, hi = (unsigned)(t >> 32);
   asm volatile("v_mov_b32 %0, %0\n\tv_mov_b32 %1, %1" : "+v"(lo), "+v"(hi));  // vector store
@@ -107,6 +113,12 @@ __device__ __forceinline__ void tr_store(unsigned long long* p, unsigned long lo
     if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (band) < kTrBands)                        \
       tr_store(&g_btrace[kern][role][band][slot], __builtin_amdgcn_s_memtime());                \
   } while (0)
+#define ASR_BSW(l, slot, rt)                                                                   \
+  do {                                                                                         \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 256 && (l) < kSwBlocks)                       \
+      tr_store(&g_bswitch[blockIdx.x][l][slot],                                                \
+               (rt) ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime());       \
+  } while (0)
 #define ASR_BCLK(kern, which)                                                                    \
   do {                                                                                           \
     if (threadIdx.x == 0 && blockIdx.x < 1024) {                                                 \
@@ -115,6 +127,9 @@ __device__ __forceinline__ void tr_store(unsigned long long* p, unsigned long lo
     }                                                                                            \
   } while (0)
 #else
+#define ASR_BSW(l, slot, rt) \
+  do {                       \
+  } while (0)
 #define ASR_BTR(kern, role, band, slot) \
   do {                                  \
   } while (0)
@@ -2484,8 +2499,11 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       const int n = cur.n, y0 = cur.b * BR, l = cur.l;
       const int rows = min(BR, H - y0);
       if (wave == 0) ASR_BTR(1, 0, it, 0);
+      const bool sw_ = !RK2 && cur.b == 0 && n == n0;  // (trace build: the first band of block l)
+      if (wave == 0 && sw_) ASR_BSW(l, 3, false);
       barrier_vm_usual<BR>(nst);  // item it staged everywhere; item it-1 fully consumed
       if (wave == 0) ASR_BTR(1, 0, it, 1);
+      if (wave == 0 && sw_) ASR_BSW(l, 4, false);
       const unsigned dzt = lds_u32(lds + LL::DZ + buf * LL::TILE), dyt = lds_u32(lds + LL::DY + buf * LL::TILE);
       const unsigned xt = lds_u32(lds + LL::X + buf * LL::TILE);
       const bool s1 = s1_of(l);
@@ -2781,6 +2799,10 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
       const int rows = min(BR, H - y0);
       const bool first_of_block = cur.b == 0 && cur.n == n0 && (!RK2 || (cur.l & 1));
       if (wave == 4) ASR_BTR(1, 1, it, 0);
+      if (wave == 4 && first_of_block && !RK2) {
+        ASR_BSW(l, 0, false);
+        ASR_BSW(l, 5, true);
+      }
       if (first_of_block && l + 2 < L && l + 2 >= lfold && w8 == 0 && lane == 0) {
         // block l+2's slabs: every workgroup published them (bounded poll); once a
         // wait of this workgroup ran out, every later block it folds is flagged
@@ -2801,8 +2823,13 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         if (ran_out) __hip_atomic_store((gu32*)(skipf + l + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
+      if (wave == 4 && first_of_block && !RK2) ASR_BSW(l, 1, false);
       barrier_vm(0);  // this wave's x rows of item it landed (and its slab stores drained)
       if (wave == 4) ASR_BTR(1, 1, it, 1);
+      if (wave == 4 && first_of_block && !RK2) {
+        ASR_BSW(l, 2, false);
+        ASR_BSW(l, 6, true);
+      }
       if (first_of_block && l + 1 < L && l + 1 >= lfold && w8 == 0 && lane == 0)
         __hip_atomic_fetch_add((gu32*)(done + l + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // published
       if (first_of_block && l + 2 < L && l + 2 >= lfold) fold_begin(l + 2);
@@ -3255,6 +3282,10 @@ constexpr int kMaxBlockSlabs = 512;
 extern "C" int asr_debug_blk_trace(void* trace, size_t tbytes, void* clock, size_t cbytes) {
   if (hipMemcpyFromSymbol(trace, HIP_SYMBOL(asr::blk::g_btrace), tbytes) != hipSuccess) return -1;
   return hipMemcpyFromSymbol(clock, HIP_SYMBOL(asr::blk::g_bclock), cbytes) == hipSuccess ? 0 : -1;
+}
+extern "C" int asr_debug_blk_switch(void* dst, size_t bytes) {  // g_bswitch (k_bwd3_stack block switches)
+  if (bytes > sizeof(asr::blk::g_bswitch)) bytes = sizeof(asr::blk::g_bswitch);
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(asr::blk::g_bswitch), bytes) == hipSuccess ? 0 : -1;
 }
 namespace asr {
 #endif

@@ -758,7 +758,7 @@ __global__ __launch_bounds__(256) void k_convb(const bf16* __restrict__ xin, bf1
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) A[ks] = *(const bf16x8*)(wpack + (((long)ot * KS + ks) * 64 + lane) * 8);
   f32x4 bz = {0.f, 0.f, 0.f, 0.f};
-  if (MODE == F_EULER && bias) bz = *(const f32x4*)(bias + 16 * ot + 4 * g);
+  if ((MODE == F_EULER || MODE == F_CONV) && bias) bz = *(const f32x4*)(bias + 16 * ot + 4 * g);
   uint4 pf[NPT];
   unsigned pm[NPT];
   auto fetch = [&](long item) {
@@ -833,6 +833,12 @@ __global__ __launch_bounds__(256) void k_convb(const bf16* __restrict__ xin, bf1
           m |= (unsigned)__shfl_xor((int)m, 32, 64);
           if (g == 0 && ok) *(uint16_t*)(mask + (pix * C + 16 * ot) / 8) = (uint16_t)m;
         }
+      } else if constexpr (MODE == F_CONV) {  // the bare layer call: z = conv(x, W) + b
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[e];
+      } else if constexpr (MODE == B_CONV) {  // its backward: dz = dy (the tile), dx = A^T dz = -A dz + 2 gamma dz
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaf(two_gamma, ctr[e], -acc[e]);
       } else {  // B_EULER: the tile holds dz = dy & mask
         const uint2 dw = *(const uint2*)(dyc + (r * W + px) * G::PS + 16 * ot + 4 * g);
         const float d0[4] = {__uint_as_float(dw.x << 16), __uint_as_float(dw.x & 0xffff0000u),
@@ -904,7 +910,8 @@ __device__ __forceinline__ s16x4 tr4(const bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((ASR_LDS s16x4*)p);
 }
 
-template <int C, int W>
+// MASKED false: dz = dy (the bare conv's weight gradient, B_CONV; dmask unused)
+template <int C, int W, bool MASKED = true>
 __global__ __launch_bounds__((WgB<C, W>::NTH)) void k_wgradb(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                            const uint8_t* __restrict__ dmask, int N, int H, float h,
                                                            float* __restrict__ slabs, long x_stride, long dy_stride,
@@ -953,7 +960,8 @@ __global__ __launch_bounds__((WgB<C, W>::NTH)) void k_wgradb(const bf16* __restr
       const int r = i / (W * G::C8);
       if (i < G::DCH && y0 + r < H) {
         const long e = ((long)n * H + y0) * W * C + 8L * i;
-        pd[k] = mask8_bf16(*(const uint4*)(dy + e), dmask[e >> 3]);
+        pd[k] = *(const uint4*)(dy + e);
+        if constexpr (MASKED) pd[k] = mask8_bf16(pd[k], dmask[e >> 3]);
       }
     }
   };
@@ -1053,7 +1061,7 @@ __global__ __launch_bounds__((WgB<C, W>::NTH)) void k_wgradb(const bf16* __restr
   }
 }
 
-template <int C, int W>
+template <int C, int W, bool MASKED = true>
 static int launch_wgradb(const bf16* x, const bf16* dy, const uint8_t* mask, int N, int H, float h, float* slabs,
                          int* nslabs, hipStream_t s, int layers = 1, long x_stride = 0, long dy_stride = 0,
                          long m_stride = 0, long s_stride = 0) {
@@ -1071,20 +1079,25 @@ static int launch_wgradb(const bf16* x, const bf16* dy, const uint8_t* mask, int
 #endif
   constexpr int minb = C == 16 ? ASR_WGB_B16 : C == 32 ? ASR_WGB_B32 : ASR_WGB_B64;
   const int grid = (int)std::max<long>(1, std::min<long>((items + minb - 1) / minb, wgrad32_grid<C, W>(N, H)));
-  hipLaunchKernelGGL((k_wgradb<C, W>), dim3(grid, layers), dim3(G::NTH), G::LDS, s, x, dy, mask, N, H, h, slabs,
+  hipLaunchKernelGGL((k_wgradb<C, W, MASKED>), dim3(grid, layers), dim3(G::NTH), G::LDS, s, x, dy, mask, N, H, h, slabs,
                      x_stride, dy_stride, m_stride, s_stride);
   ASR_LAUNCH_CHECK("k_wgradb");
   *nslabs = grid;
   return ASR_OK;
 }
 
-// y = x + h relu(conv(x, W) + b) in bf16 (w: asr_theta_to_w's ASR_BF16 pack of one layer)
+// y = x + h relu(conv(x, W) + b) in bf16 (w: asr_theta_to_w's ASR_BF16 pack of one layer); with
+// conv_only the bare layer call y = conv(x, W) + b (…3By3.py:157-171; no mask, h unused)
 int convb_forward(const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h, int N, int H, int W,
-                  int C, hipStream_t s) {
-#define ASR_CB(CC, WW)                                                                                             \
-  if (C == CC && W == WW)                                                                                          \
+                  int C, hipStream_t s, bool conv_only) {
+#define ASR_CB(CC, WW)                                                                                              \
+  if (C == CC && W == WW) {                                                                                         \
+    if (conv_only)                                                                                                  \
+      return launch_convb<CC, WW, F_CONV>((const bf16*)x, (bf16*)y, nullptr, (const bf16*)w, bias, 1.f, 0.f,        \
+                                          nullptr, N, H, nullptr, s);                                               \
     return launch_convb<CC, WW, F_EULER>((const bf16*)x, (bf16*)y, mask, (const bf16*)w, bias, h, 0.f, nullptr, N, H, \
-                                         nullptr, s);
+                                         nullptr, s);                                                               \
+  }
   ASR_CB(16, 32) ASR_CB(16, 16) ASR_CB(16, 8) ASR_CB(32, 32) ASR_CB(32, 16) ASR_CB(32, 8) ASR_CB(64, 32)
   ASR_CB(64, 16) ASR_CB(64, 8)
 #undef ASR_CB
@@ -1094,23 +1107,34 @@ int convb_forward(const void* x, void* y, uint8_t* mask, const void* w, const fl
 // The Euler block's backward in bf16: dx = dy - h conv(dy & mask, W) + 2 gamma h (dy & mask)
 // (W: the forward pack for antisymmetric operators, whose transpose is -A + 2 gamma I; the
 // transposed operator's pack with gamma = 0 otherwise) and the weight-gradient slabs
-// (k_wgrad32 on the bf16 x and dy: dz = h dy [relu bit] staged in fp32)
+// (k_wgradb on the bf16 x and dz = dy & mask, h on the fp32 sums).  conv_only: the bare layer
+// call's backward, dz = dy: dx = -conv(dy, W) + 2 gamma dy, slabs of x (x) dy (h unused)
 int convb_backward(const void* dy, const uint8_t* mask, const void* x, const void* w, float h, float two_gamma, int N,
-                   int H, int W, int C, void* dx, bool need_w, float* slabs, int* nslabs, hipStream_t s) {
+                   int H, int W, int C, void* dx, bool need_w, float* slabs, int* nslabs, hipStream_t s,
+                   bool conv_only) {
   *nslabs = 0;
   if (!convb_supported(W, C)) return fail(ASR_E_UNSUPPORTED, "conv bf16 backward (any width): C=%d W=%d", C, W);
   if (dx) {
 #define ASR_CB(CC, WW)                                                                                                  \
-  if (C == CC && W == WW)                                                                                               \
-    ASR_TRY((launch_convb<CC, WW, B_EULER>((const bf16*)dy, (bf16*)dx, nullptr, (const bf16*)w, nullptr, h, two_gamma, \
-                                           (const bf16*)dy, N, H, mask, s)));
+  if (C == CC && W == WW) {                                                                                             \
+    if (conv_only)                                                                                                      \
+      ASR_TRY((launch_convb<CC, WW, B_CONV>((const bf16*)dy, (bf16*)dx, nullptr, (const bf16*)w, nullptr, 1.f,        \
+                                            two_gamma, nullptr, N, H, nullptr, s)));                                   \
+    else                                                                                                                \
+      ASR_TRY((launch_convb<CC, WW, B_EULER>((const bf16*)dy, (bf16*)dx, nullptr, (const bf16*)w, nullptr, h,         \
+                                             two_gamma, (const bf16*)dy, N, H, mask, s)));                             \
+  }
     ASR_CB(16, 32) ASR_CB(16, 16) ASR_CB(16, 8) ASR_CB(32, 32) ASR_CB(32, 16) ASR_CB(32, 8) ASR_CB(64, 32)
     ASR_CB(64, 16) ASR_CB(64, 8)
 #undef ASR_CB
   }
   if (!need_w) return ASR_OK;
-#define ASR_WB(CC, WW) \
-  if (C == CC && W == WW) return launch_wgradb<CC, WW>((const bf16*)x, (const bf16*)dy, mask, N, H, h, slabs, nslabs, s);
+#define ASR_WB(CC, WW)                                                                                             \
+  if (C == CC && W == WW) {                                                                                        \
+    if (conv_only)                                                                                                 \
+      return launch_wgradb<CC, WW, false>((const bf16*)x, (const bf16*)dy, nullptr, N, H, 1.f, slabs, nslabs, s); \
+    return launch_wgradb<CC, WW>((const bf16*)x, (const bf16*)dy, mask, N, H, h, slabs, nslabs, s);              \
+  }
   ASR_WB(16, 32) ASR_WB(16, 16) ASR_WB(16, 8) ASR_WB(32, 32) ASR_WB(32, 16) ASR_WB(32, 8) ASR_WB(64, 32)
   ASR_WB(64, 16) ASR_WB(64, 8)
 #undef ASR_WB

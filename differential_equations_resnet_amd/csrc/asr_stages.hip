@@ -49,9 +49,10 @@ int reduce_slab_layers(const float* slabs, long slab_stride, int P, long ES, flo
 // asr_conv_f32.hip: the bf16 blocks at any stage width, bf16 <-> fp32
 bool convb_supported(int W, int C);
 int convb_forward(const void* x, void* y, uint8_t* mask, const void* w, const float* bias, float h, int N, int H, int W,
-                  int C, hipStream_t s);
+                  int C, hipStream_t s, bool conv_only = false);
 int convb_backward(const void* dy, const uint8_t* mask, const void* x, const void* w, float h, float two_gamma, int N,
-                   int H, int W, int C, void* dx, bool need_w, float* slabs, int* nslabs, hipStream_t s);
+                   int H, int W, int C, void* dx, bool need_w, float* slabs, int* nslabs, hipStream_t s,
+                   bool conv_only = false);
 int convert_bf16_f32(const void* src, void* dst, long n, int to_f32, hipStream_t s);
 bool stage_img_supported(int H, int W, int C);
 int stage_img_forward(const void* x0, void* ys, long y_stride, uint8_t* masks, long mask_stride, const void* w,

@@ -60,6 +60,10 @@ def _layer_case(layer, shape, dtype, seed):
     (lambda: Conv2DAntisymmetric3By3(), (2, 32, 32, 16), torch.bfloat16),
     (lambda: Conv2DAntisymmetric(3, antisymmetric=False), (2, 32, 32, 32), torch.bfloat16),
     (lambda: Conv2DAntisymmetric3By3(use_bias=False), (1, 8, 8, 6), torch.float32),
+    # bf16 at the multi-stage nets' widths (k_convb's bare-conv modes, round 6)
+    (lambda: Conv2DAntisymmetric3By3(gamma=-0.1), (2, 16, 16, 32), torch.bfloat16),
+    (lambda: Conv2DAntisymmetric3By3(), (3, 7, 8, 64), torch.bfloat16),
+    (lambda: Conv2DAntisymmetric(3, antisymmetric=False), (2, 16, 16, 16), torch.bfloat16),
 ])
 def test_layer_eager_forward_backward(make, shape, dtype):
     y, dx, dth, db, want_y, want_dx, want_dth, want_db, bf = _layer_case(make(), shape, dtype, 5)
@@ -85,7 +89,7 @@ def test_layer_eager_is_native():
     layer = Conv2DAntisymmetric3By3()
     layer(Input(shape=(8, 8, 12)))
     with pytest.raises(AsrUnsupported):
-        layer(torch.zeros(1, 8, 8, 12, device="cuda", dtype=torch.bfloat16))  # bf16 needs C%16, W==32
+        layer(torch.zeros(1, 8, 8, 12, device="cuda", dtype=torch.bfloat16))  # bf16 needs C in {16,32,64}
     strided = Conv2DAntisymmetric3By3(strides=(2, 2))
     strided(Input(shape=(8, 8, 4)))
     with pytest.raises(AsrUnsupported):

@@ -78,7 +78,8 @@ def _oracle_W(th, C, gamma, bf):
 
 
 SHAPES_BF16 = [(2, 32, 32, 16), (2, 32, 32, 32), (2, 32, 32, 64), (1, 11, 32, 64), (3, 5, 32, 16)]
-# bf16 Euler blocks at the multi-stage nets' widths (k_convb + k_wgrad32<bf16>, round 5; Euler mode only)
+# bf16 Euler blocks and bare convs (Conv2DAntisymmetric3By3.call, …3By3.py:157-171) at the multi-stage nets' widths
+# (k_convb + k_wgradb: Euler mode since round 5, the bare conv since round 6)
 SHAPES_BF16_W = [(2, 16, 16, 32), (3, 7, 16, 16), (2, 8, 8, 64), (2, 5, 8, 16), (1, 9, 8, 32), (2, 16, 16, 64),
                  (2, 32, 32, 64)]
 SHAPES_F32 = [(2, 32, 32, 16), (1, 7, 13, 5), (2, 9, 32, 64), (1, 3, 3, 1), (2, 32, 32, 32), (3, 6, 32, 16),
@@ -93,8 +94,6 @@ SHAPES_F32 = [(2, 32, 32, 16), (1, 7, 13, 5), (2, 9, 32, 64), (1, 3, 3, 1), (2, 
 def test_forward_parity(rt, dtype_name, shape, mode_name, gamma, h):
     N, H, W_, C = shape
     if dtype_name == "bf16w":
-        if mode_name != "euler":
-            pytest.skip("the any-width bf16 kernels run Euler blocks only")
         if W_ == 32:
             pytest.skip("W = 32 runs the C=16/32/64 band kernels (SHAPES_BF16); k_convb at W = 32 via the stages")
     bf = dtype_name.startswith("bf16")
@@ -131,8 +130,6 @@ def test_forward_parity(rt, dtype_name, shape, mode_name, gamma, h):
 def test_backward_parity(rt, dtype_name, shape, mode_name, gamma, h):
     N, H, W_, C = shape
     if dtype_name == "bf16w":
-        if mode_name != "euler":
-            pytest.skip("the any-width bf16 kernels run Euler blocks only")
         if W_ == 32:
             pytest.skip("W = 32 runs the C=16/32/64 band kernels (SHAPES_BF16); k_convb at W = 32 via the stages")
     bf = dtype_name.startswith("bf16")
