@@ -32,27 +32,16 @@
 #include "asr_common.h"
 #include "asr_device.h"
 
-#ifndef ASR_BWD_DGRAD_DMA_PCT
-#define ASR_BWD_DGRAD_DMA_PCT 75  // share of the backward's prefetch DMAs issued by the dgrad waves
-#endif
-#ifndef ASR_BWD_DMA_HOOK
-#define ASR_BWD_DMA_HOOK 1  // issue the backward's prefetch inside the dgrad k-steps (0: before the convert)
-#endif
-#ifndef ASR_V2_MASKTAB
-#define ASR_V2_MASKTAB 1  // v2 backward convert: relu-mask expansion from a 4 KiB LDS table (0: bit ops)
-#endif
-#ifndef ASR_FWD_ST16
-#define ASR_FWD_ST16 1  // forward pipe: y as 16-B stores (row swap between the two pixel tiles)
-#endif
-#ifndef ASR_FWD_REUSE
-#define ASR_FWD_REUSE 1  // forward pipe: halo rows of a band continuing the previous band's image copied in LDS
-#endif
-#ifndef ASR_FWD3_WGS
-#define ASR_FWD3_WGS 3  // k_fwd3 workgroups per CU (grid = min(bands, WGS x CUs))
-#endif
-#ifndef ASR_BWD3_DMA0
-#define ASR_BWD3_DMA0 16  // k_bwd3 wgrad waves: DMA pieces issued right after the barrier, the rest one per row (A/B: spreading them lengthened the MFMA phase as much as it saved; the stacks: all at once 16 vs 9 +0.3-0.5 %, 4 -0.7 %)
-#endif
+// Measured settings (each an A/B of whole steps in the commit log; the other arms were removed in
+// round 6 and stay in git history).  The v1 backward (C = 16 / 32, RK2 stages): 75 % of its prefetch
+// DMAs issued by the dgrad waves, inside their k-steps.  The v2/v3 backward's convert: relu-mask
+// expansion from a 4 KiB LDS table.  The forward pipe: y as 16-B stores; halo rows of a band that
+// continues the previous band's image copied in LDS.
+constexpr int kBwdDgradDmaPct = 75;
+constexpr int kFwd3Wgs = 3;  // k_fwd3 workgroups per CU (grid = min(bands, 3 x CUs))
+// k_bwd3 wgrad waves: DMA pieces issued right after the barrier, the rest one per row (A/B: spreading them
+// lengthened the MFMA phase as much as it saved; the stacks: all at once 16 vs 9 +0.3-0.5 %, 4 -0.7 %)
+constexpr int kBwd3Dma0 = 16;
 
 namespace asr {
 
@@ -673,8 +662,8 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
   static_assert(BR % RS == 0, "row groups must split the band");
   using BD = Band<C, W, RB>;
   // epilogue units: (row, pixel tile), or rows with both pixel tiles stored
-  // as 16-B chunks (ASR_FWD_ST16)
-  constexpr bool ST16 = ASR_FWD_ST16 && PT == 2;
+  // as 16-B chunks
+  constexpr bool ST16 = PT == 2;
   constexpr int NU = ST16 ? RB : RB * PT;
   constexpr bool EULER = MODE == FWD_EULER;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -711,16 +700,15 @@ __global__ __launch_bounds__(64 * NW, 2) void k_fwd_pipe(const bf16* __restrict_
   };
   // band c continues band p's image (p's tile in the other buffer, complete):
   // its halo rows 0, 1 are p's rows BR, BR+1 -> copy them (interior columns),
-  // DMA only rows 2.. (ASR_FWD_REUSE)
+  // DMA only rows 2..
   auto dma_next2 = [&](const ItemCursor& c, const ItemCursor& p, int buf) {
-    if (!ASR_FWD_REUSE || c.n != p.n || c.b != p.b + 1) {
+    if (c.n != p.n || c.b != p.b + 1) {
       dma(c, buf);
       return;
     }
     const int yy = c.b * BR;
     constexpr int ROWB = TW * NQ * 16;
-    if (ASR_FWD_REUSE == 2) dma(c, buf);  // debug: full DMA, then the copy over rows 0, 1
-    else dma_rows<C, W>(x, lds + buf * TILE + 2 * ROWB, c.n, yy + 1, min(BR, H - yy), H, wave, NW, lane);
+    dma_rows<C, W>(x, lds + buf * TILE + 2 * ROWB, c.n, yy + 1, min(BR, H - yy), H, wave, NW, lane);
     // plain LDS accesses (the DMA is inline asm, invisible to the compiler,
     // so it waits only lgkmcnt for these; asm reads with a deferred wait are
     // unsafe where hipcc copies their results before the wait)
@@ -1526,7 +1514,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
       const bool reuse = it + 1 < i1 && nxt.n == cur.n;
       BwdPrefetch<C, W, BR, EULER> pf;
       pf.init(nxt, it + 1 < i1, reuse, lds, buf ^ 1, H);
-      const int dsplit = (pf.end * ASR_BWD_DGRAD_DMA_PCT) / 100;  // dgrad waves: [0, dsplit)
+      const int dsplit = (pf.end * kBwdDgradDmaPct) / 100;  // dgrad waves: [0, dsplit)
       int du = wv4;                                               // wave-uniform stream cursor
       const int dend = dsplit;
       auto dma_one = [&]() {
@@ -1537,8 +1525,6 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
           ++nd;
         }
       };
-      if (!ASR_BWD_DMA_HOOK)
-        while (du < dend) dma_one();
       bool ex_wait = has_extra;
       if (reuse) bwd_halo_copy<C, W, BR, EULER>(lds, buf, tid, 512);
       bwd_convert<C, W, BR, EULER>(lds, buf, rows + 2, tid, 512);
@@ -1556,7 +1542,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
         for (int t = 0; t < OTW; ++t)
 #pragma unroll
           for (int pt = 0; pt < PT; ++pt) acc[t][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (ASR_BWD_DMA_HOOK && k == 0) {
+        if (k == 0) {
           conv_row<C, W>(dzt, r, A, boff, acc, dma_one);
           while (du < dend) dma_one();
           ASR_STAMP(it - i0, 4);
@@ -1684,7 +1670,7 @@ __global__ __launch_bounds__(512) void k_bwd(const bf16* __restrict__ dy, const 
       const bool reuse = it + 1 < i1 && nxt.n == cur.n;
       BwdPrefetch<C, W, BR, EULER> pf;
       pf.init(nxt, it + 1 < i1, reuse, lds, buf ^ 1, H);
-      int du = (pf.end * ASR_BWD_DGRAD_DMA_PCT) / 100 + wv8 - 4;  // wgrad waves: [dsplit, end)
+      int du = (pf.end * kBwdDgradDmaPct) / 100 + wv8 - 4;  // wgrad waves: [dsplit, end)
       const int dend = pf.end;
       auto dma_one = [&]() {
         if (du < dend) {
@@ -1813,7 +1799,7 @@ struct Bwd2Lds {
   static constexpr int TILE = (BR + 2) * ROWB;
   static constexpr int DY = 0, X = 2 * TILE, DZ = 4 * TILE;
   // 256 x 16 B: the 16-bit-lane AND masks of one 16-B chunk per mask byte
-  static constexpr int MTAB = 6 * TILE, TOTAL = MTAB + (ASR_V2_MASKTAB ? 4096 : 0);
+  static constexpr int MTAB = 6 * TILE, TOTAL = MTAB + 4096;
 };
 
 // tile rows of band `nx` owned by dgrad wave wv (0..3): reuse -> row 2+wv;
@@ -1876,7 +1862,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
     zero_halo_cols<C, W>(lds + L::X + b * L::TILE, BR + 2, tid, 768);
     zero_halo_cols<C, W>(lds + L::DZ + b * L::TILE, BR + 2, tid, 768);
   }
-  if (ASR_V2_MASKTAB && EULER) {  // dword d of byte m's entry: 0xffff per set bit of (m >> 2d) & 3
+  if (EULER) {  // dword d of byte m's entry: 0xffff per set bit of (m >> 2d) & 3
     unsigned* tab = (unsigned*)(lds + L::MTAB);
     for (int i = tid; i < 1024; i += 768) {
       const unsigned m = (unsigned)i >> 2, d = (unsigned)i & 3;
@@ -2091,12 +2077,12 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
         for (int j = 0; j < 2; ++j) {
           off[j] = (unsigned)toff<C>(row, cpx + 1, 4 * hh + jj + j, TW) + (unsigned)(nbuf * L::TILE);
           v[j] = lds_ld128(base + L::DY + off[j]);
-          if (EULER && ASR_V2_MASKTAB) mt[j] = lds_ld128(base + L::MTAB + __builtin_amdgcn_ubfe(mwv, 8 * (jj + j), 8) * 16);
+          if (EULER) mt[j] = lds_ld128(base + L::MTAB + __builtin_amdgcn_ubfe(mwv, 8 * (jj + j), 8) * 16);
         }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           u32x4 z = v[j];
-          if constexpr (EULER && ASR_V2_MASKTAB) {
+          if constexpr (EULER) {
             z &= mt[j];
           } else if constexpr (EULER) {
 #pragma unroll
@@ -2143,7 +2129,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
       unsigned mwv = 0u;
       // the next band's DMA pieces of this wave: own dy row (waves 0-3, or 0-5 when
       // the next band starts an image), x rows (waves 4-7; rows 2.. when it
-      // continues this band's image); issued ASR_BWD3_DMA0 at once, the rest one
+      // continues this band's image); issued kBwd3Dma0 at once, the rest one
       // after each of the first rows' MFMAs (a piece among MFMAs issues cheaper)
       if constexpr (EULER) {
         if (orow >= 0) mwv = bwd2_mask_word<C, W>(mask, nxt.n, nxt.b * BR, orow, H, lane);
@@ -2163,7 +2149,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
         }
         ++ipc;
       };
-      while (ipc < npc && ipc < ASR_BWD3_DMA0) piece();
+      while (ipc < npc && ipc < kBwd3Dma0) piece();
       bf16x8 Bf[2], Ar[3];
       if (wave == 4) ASR_BTR(1, 1, it - i0, 2);
       // A fragments two m-tiles ahead (ring of 3), as in the round-1 v2 backward
@@ -2423,7 +2409,7 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
     zero_halo_cols<C, W>(lds + LL::X + b * LL::TILE, BR + 2, tid, 768);
     zero_halo_cols<C, W>(lds + LL::DZ + b * LL::TILE, BR + 2, tid, 768);
   }
-  if (ASR_V2_MASKTAB) {
+  {
     unsigned* tab = (unsigned*)(lds + LL::MTAB);
     for (int i = tid; i < 1024; i += 768) {
       const unsigned m = (unsigned)i >> 2, d = (unsigned)i & 3;
@@ -2729,21 +2715,12 @@ __global__ __launch_bounds__(768, 1) void k_bwd3_stack(bf16* __restrict__ dbuf0,
         for (int j = 0; j < 2; ++j) {
           off[j] = (unsigned)toff<C>(row, cpx + 1, 4 * hh + jj + j, TW) + (unsigned)(nbuf * LL::TILE);
           v[j] = lds_ld128(base + LL::DY + off[j]);
-          if (ASR_V2_MASKTAB) mt[j] = lds_ld128(base + LL::MTAB + __builtin_amdgcn_ubfe(mwv, 8 * (jj + j), 8) * 16);
+          mt[j] = lds_ld128(base + LL::MTAB + __builtin_amdgcn_ubfe(mwv, 8 * (jj + j), 8) * 16);
         }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           u32x4 z = v[j];
-          if constexpr (ASR_V2_MASKTAB) {
-            z &= mt[j];
-          } else {
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-              const unsigned lo = (unsigned)__builtin_amdgcn_sbfe((int)mwv, 8 * (jj + j) + 2 * d, 1);
-              const unsigned hi = (unsigned)__builtin_amdgcn_sbfe((int)mwv, 8 * (jj + j) + 2 * d + 1, 1);
-              z[d] &= __builtin_amdgcn_perm(hi, lo, 0x07060100u);
-            }
-          }
+          z &= mt[j];
           lds_st128(base + LL::DZ + off[j], z);
         }
       }
@@ -3308,7 +3285,7 @@ static int launch_fwd_v(int mode, const void* x, const void* resid, void* y, uin
   const size_t lds = 2 * (size_t)(BR + 2) * (W + 2) * C * 2;
   if constexpr (C == 64 && W == 32 && BR == 4 && NW == 4) {
     if (!resid || mode == blk::FWD_EULER) {
-      const int grid3 = (int)std::max<long>(1, std::min<long>(items, (long)cus * ASR_FWD3_WGS));
+      const int grid3 = (int)std::max<long>(1, std::min<long>(items, (long)cus * kFwd3Wgs));
       if (mode == blk::FWD_EULER && resid)
         hipLaunchKernelGGL((blk::k_fwd3<C, W, BR, blk::FWD_EULER, 3, true>), dim3(grid3), dim3(256), lds, s,
                            (const bf16*)x, (const bf16*)resid, (bf16*)y, mask, (const bf16*)w, bias, h, N, H);

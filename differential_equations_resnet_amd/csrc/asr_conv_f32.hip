@@ -181,14 +181,11 @@ __global__ void k_db_f32(const float* __restrict__ dz, long rows, int W, int C, 
 // ===========================================================================
 template <int C, int W_>
 struct F32Band {
-#ifndef ASR_F32PAD
-#define ASR_F32PAD 1
-#endif
   // pixel strides in LDS (floats), padded against bank conflicts: PSC for the conv's 16-B reads
   // (16 lanes = 16 consecutive pixels on distinct banks), PSW for the wgrad's 4-B reads (the two
   // lane groups of a 32-lane half, one pixel apart, on disjoint banks); unpadded, a C = 64 tile
   // put the 16 lanes of a conv read on one bank group
-  static constexpr int PSC = ASR_F32PAD ? C + 4 : C, PSW = ASR_F32PAD && C >= 32 ? C + 16 : C;
+  static constexpr int PSC = C + 4, PSW = C >= 32 ? C + 16 : C;
   static constexpr int OT = C / 16, W = W_, TW = W + 2, BR = 4, TILEF = (BR + 2) * TW * PSC;
   static constexpr int TILEW = (BR + 2) * TW * PSW;  // the wgrad's x tile
   static constexpr int T = BR * W / 16;  // 16-pixel tiles per band (band pixel p = 16 tile + lx: row p / W, col p % W)
@@ -465,12 +462,6 @@ static int conv32_dispatch(int C, int W, const void* xin, void* out, uint8_t* ma
 }
 
 // k_wgrad32's grid = its slab rows (one [dW | db] slab per workgroup)
-#ifndef ASR_WG32_B32
-#define ASR_WG32_B32 8
-#endif
-#ifndef ASR_WG32_B64
-#define ASR_WG32_B64 16
-#endif
 template <int C, int W>
 static int wgrad32_grid(int N, int H) {
   const long items = (long)N * ((H + 3) / 4);
@@ -478,7 +469,7 @@ static int wgrad32_grid(int N, int H) {
   if (cus <= 0) cus = 256;
   const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / wgrad32_lds<C, W>())));
   // at least minb bands per workgroup at C = 32 / 64: a slab row is 37 / 148 KB, written and read back
-  constexpr int minb = C == 64 ? ASR_WG32_B64 : C == 32 ? ASR_WG32_B32 : 1;
+  constexpr int minb = C == 64 ? 16 : C == 32 ? 8 : 1;  // (profiles/r05al_f32_wgrad_rows_ab.txt)
   return (int)std::max<long>(1, std::min<long>({(items + minb - 1) / minb, (long)per_cu * cus, 512L}));
 }
 
@@ -693,12 +684,9 @@ int wgrad_f32(const void* x, int x_bf16, const float* dz, int N, int H, int W, i
 // ===========================================================================
 template <int C, int W_>
 struct BfBand {
-#ifndef ASR_PIXPAD
-#define ASR_PIXPAD 8
-#endif
   // PS: a pixel's elements in the LDS tiles, padded so the 16 lanes of a 16-B read (16 consecutive
   // pixels) fall on distinct banks (unpadded, C = 64 put them on 2 bank groups: 8-way conflicts)
-  static constexpr int OT = C / 16, W = W_, TW = W + 2, BR = 4, PS = C + ASR_PIXPAD, TILEE = (BR + 2) * TW * PS;
+  static constexpr int OT = C / 16, W = W_, TW = W + 2, BR = 4, PS = C + 8, TILEE = (BR + 2) * TW * PS;
   static constexpr int T = BR * W / 16;  // 16-pixel tiles per band
   static constexpr int WPT = 4 / OT;     // waves sharing an o-tile
   static constexpr int KS = (9 * C + 31) / 32;
@@ -860,10 +848,7 @@ static int launch_convb(const bf16* xin, bf16* out, uint8_t* mask, const bf16* w
   const long items = (long)N * ((H + 3) / 4);
   int cus = cu_count();
   if (cus <= 0) cus = 256;
-#ifndef ASR_CONVB_WPC
-#define ASR_CONVB_WPC 4
-#endif
-  const long grid = std::max<long>(1, std::min<long>(items, (long)ASR_CONVB_WPC * cus));  // workgroups per CU
+  const long grid = std::max<long>(1, std::min<long>(items, 4L * cus));  // 4 persistent workgroups per CU (r05r)
   hipLaunchKernelGGL((k_convb<C, W, MODE>), dim3((unsigned)grid), dim3(256), 0, s, xin, out, mask, w, bias, h,
                      two_gamma, dy, N, H, dmask);
   ASR_LAUNCH_CHECK("k_convb");
@@ -1068,16 +1053,7 @@ static int launch_wgradb(const bf16* x, const bf16* dy, const uint8_t* mask, int
   using G = WgB<C, W>;
   const long items = (long)N * ((H + G::BR - 1) / G::BR);
   // at most the fp32 wgrad's grid: the rows the workspaces size per block (f32_block_slab_rows)
-#ifndef ASR_WGB_B16
-#define ASR_WGB_B16 1
-#endif
-#ifndef ASR_WGB_B32
-#define ASR_WGB_B32 8
-#endif
-#ifndef ASR_WGB_B64
-#define ASR_WGB_B64 32
-#endif
-  constexpr int minb = C == 16 ? ASR_WGB_B16 : C == 32 ? ASR_WGB_B32 : ASR_WGB_B64;
+  constexpr int minb = C == 16 ? 1 : C == 32 ? 8 : 32;  // bands per workgroup (profiles/r05_he32_bf16_ab.txt)
   const int grid = (int)std::max<long>(1, std::min<long>((items + minb - 1) / minb, wgrad32_grid<C, W>(N, H)));
   hipLaunchKernelGGL((k_wgradb<C, W, MASKED>), dim3(grid, layers), dim3(G::NTH), G::LDS, s, x, dy, mask, N, H, h, slabs,
                      x_stride, dy_stride, m_stride, s_stride);
@@ -1158,14 +1134,11 @@ int convb_backward(const void* dy, const uint8_t* mask, const void* x, const voi
 // ===========================================================================
 template <int C, int W_>
 struct StImg {
-#ifndef ASR_ST_NW
-#define ASR_ST_NW 4
-#endif
-  static constexpr int NW = ASR_ST_NW, NTH = 64 * NW;  // waves per image
+  static constexpr int NW = 4, NTH = 64 * NW;  // waves per image
   static constexpr int W = W_, H = W_, TW = W + 2, OT = C / 16, WPT = NW / OT, KS = (9 * C + 31) / 32, C8 = C / 8;
   static constexpr int T = H * W / 16;              // 16-pixel tiles per image
   static_assert((T / WPT) % 2 == 0, "image-resident stage: a wave's tiles come in pairs (two MFMA chains)");
-  static constexpr int PS = C + ASR_PIXPAD;          // a pixel's elements in LDS (padded, as BfBand)
+  static constexpr int PS = C + 8;          // a pixel's elements in LDS (padded, as BfBand)
   static constexpr int IMGE = (H + 2) * TW * PS;    // elements of a haloed image tile
   static constexpr int NCH = H * W * C8;            // 16-B chunks of an image
   static_assert((W == 16 && C == 32) || (W == 8 && C == 64) || (W == 8 && C == 32),
@@ -1180,16 +1153,10 @@ __device__ __forceinline__ int st_off(int r, int c) {  // element offset of inte
 // an LDS-only workgroup barrier: the layers' global stores (y, masks, dy) stay in flight across it
 // (__syncthreads waits for them too: a full store round trip per layer)
 __device__ __forceinline__ void st_barrier() {
-#ifdef ASR_ST_SYNC
-  __syncthreads();
-#else
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
 }
 
-#ifndef ASR_ST_IPW
-#define ASR_ST_IPW 1
-#endif
+constexpr int kStIpw = 1;
 // IPW images per workgroup: 1 (a wave's two MFMA chains are two tiles of the image); 2 (the chains are
 // one tile of each image, the layer's A fragments shared) measured -7 % (r05ar: half the workgroups)
 template <int C, int W>
@@ -1199,7 +1166,7 @@ __global__ __launch_bounds__((StImg<C, W>::NTH)) void k_stagef(const bf16* __res
                                                 const float* __restrict__ bias, long bias_stride, float h, int N,
                                                 int L) {
   using G = StImg<C, W>;
-  constexpr int TW = G::TW, KS = G::KS, OT = G::OT, IPW = ASR_ST_IPW, TP = 2 / IPW;
+  constexpr int TW = G::TW, KS = G::KS, OT = G::OT, IPW = kStIpw, TP = 2 / IPW;
   extern __shared__ __attribute__((aligned(16))) bf16 lds_stf[];  // [IPW][2][IMGE]
   auto imgb = [&](int im, int pp) { return lds_stf + (im * 2 + pp) * G::IMGE; };
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, lx = lane & 15;
@@ -1288,7 +1255,7 @@ __global__ __launch_bounds__((StImg<C, W>::NTH)) void k_stageb(const bf16* __res
                                                 long mask_stride, const bf16* __restrict__ wpack, long w_stride,
                                                 float h, float two_gamma, int N, int L) {
   using G = StImg<C, W>;
-  constexpr int TW = G::TW, KS = G::KS, OT = G::OT, IPW = ASR_ST_IPW, TP = 2 / IPW;
+  constexpr int TW = G::TW, KS = G::KS, OT = G::OT, IPW = kStIpw, TP = 2 / IPW;
   constexpr int DYE = G::H * W * G::PS;
   extern __shared__ __attribute__((aligned(16))) bf16 lds_stb[];  // [IPW][dz (haloed) | dy]
   auto dzb = [&](int im) { return lds_stb + im * (G::IMGE + DYE); };
@@ -1384,12 +1351,9 @@ __global__ __launch_bounds__((StImg<C, W>::NTH)) void k_stageb(const bf16* __res
 // ---------------------------------------------------------------------------
 template <int C, int W_>
 struct StImg32 {
-#ifndef ASR_ST32_NW
-#define ASR_ST32_NW 4
-#endif
   // NW waves per image: the fp32 MFMA is 4x the bf16's cycles per FLOP, and at the reference's batch
   // sizes (128) one 4-wave workgroup per image would leave half the SIMDs idle
-  static constexpr int NW = ASR_ST32_NW, NTH = 64 * NW;
+  static constexpr int NW = 4, NTH = 64 * NW;
   static constexpr int W = W_, H = W_, TW = W + 2, OT = C / 16, OQ = C / 16, WPT = NW / OT, PS = C + 4;
   static constexpr int T = H * W / 16, IMGF = (H + 2) * TW * PS, NCH = H * W * C / 4;
   static_assert((W == 16 && C == 32) || (W == 8 && C == 64), "fp32 image-resident stage: 16 x 16 x 32 or 8 x 8 x 64");
@@ -1608,7 +1572,7 @@ int wgrad32_layers(const float* x0, long x_stride, const float* dys, long d_stri
 }
 
 bool stage_img_supported(int H, int W, int C) {
-  return H == W && ((W == 16 && C == 32) || (W == 8 && C == 64) || (ASR_ST_NW == 4 && W == 8 && C == 32));
+  return H == W && ((W == 16 && C == 32) || (W == 8 && C == 64) || (W == 8 && C == 32));
 }
 
 // the image-resident stage forward: x0 [N][H][W][C] -> ys (L layers at y_stride), masks (L at mask_stride)
@@ -1616,10 +1580,10 @@ int stage_img_forward(const void* x0, void* ys, long y_stride, uint8_t* masks, l
                       long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C, int L,
                       hipStream_t s) {
   if (!stage_img_supported(H, W, C)) return fail(ASR_E_UNSUPPORTED, "image-resident stage: H=%d W=%d C=%d", H, W, C);
-  const unsigned grid = (unsigned)std::max(1, (N + ASR_ST_IPW - 1) / ASR_ST_IPW);
+  const unsigned grid = (unsigned)std::max(1, (N + kStIpw - 1) / kStIpw);
 #define ASR_SF(CC, WW)                                                                                        \
   if (C == CC && W == WW) {                                                                                   \
-    const size_t lds = (size_t)ASR_ST_IPW * 2 * StImg<CC, WW>::IMGE * 2;                                      \
+    const size_t lds = (size_t)kStIpw * 2 * StImg<CC, WW>::IMGE * 2;                                      \
     hipLaunchKernelGGL((k_stagef<CC, WW>), dim3(grid), dim3(StImg<CC, WW>::NTH), lds, s, (const bf16*)x0, (bf16*)ys, \
                        y_stride,                                                                              \
                        masks, mask_stride, (const bf16*)w, w_stride, bias, bias_stride, h, N, L);             \
@@ -1627,9 +1591,7 @@ int stage_img_forward(const void* x0, void* ys, long y_stride, uint8_t* masks, l
     return ASR_OK;                                                                                            \
   }
   ASR_SF(32, 16) ASR_SF(64, 8)
-#if ASR_ST_NW == 4
   ASR_SF(32, 8)
-#endif
 #undef ASR_SF
   return fail(ASR_E_UNSUPPORTED, "image-resident stage: C=%d W=%d", C, W);
 }
@@ -1639,20 +1601,18 @@ int stage_img_backward(const void* dyL, void* dys, long d_stride, void* dx0, con
                        const void* w, long w_stride, float h, float two_gamma, int N, int H, int W, int C, int L,
                        hipStream_t s) {
   if (!stage_img_supported(H, W, C)) return fail(ASR_E_UNSUPPORTED, "image-resident stage: H=%d W=%d C=%d", H, W, C);
-  const unsigned grid = (unsigned)std::max(1, (N + ASR_ST_IPW - 1) / ASR_ST_IPW);
+  const unsigned grid = (unsigned)std::max(1, (N + kStIpw - 1) / kStIpw);
 #define ASR_SB(CC, WW)                                                                                           \
   if (C == CC && W == WW) {                                                                                      \
     using GG = StImg<CC, WW>;                                                                                    \
-    const size_t lds = (size_t)ASR_ST_IPW * (GG::IMGE + GG::H * WW * GG::PS) * 2;                                \
+    const size_t lds = (size_t)kStIpw * (GG::IMGE + GG::H * WW * GG::PS) * 2;                                \
     hipLaunchKernelGGL((k_stageb<CC, WW>), dim3(grid), dim3(GG::NTH), lds, s, (const bf16*)dyL, (bf16*)dys, d_stride, \
                        (bf16*)dx0, masks, mask_stride, (const bf16*)w, w_stride, h, two_gamma, N, L);             \
     ASR_LAUNCH_CHECK("k_stageb");                                                                                \
     return ASR_OK;                                                                                               \
   }
   ASR_SB(32, 16) ASR_SB(64, 8)
-#if ASR_ST_NW == 4
   ASR_SB(32, 8)
-#endif
 #undef ASR_SB
   return fail(ASR_E_UNSUPPORTED, "image-resident stage: C=%d W=%d", C, W);
 }

@@ -43,9 +43,6 @@ namespace deep {
 
 using namespace blk;
 
-#ifndef ASR_DEEP_NT
-#define ASR_DEEP_NT 1  // streaming (nt) stores of the forward: +6 % forward, -1 % backward (A/B r02k)
-#endif
 #ifndef ASR_DEEP_TRACE
 #define ASR_DEEP_TRACE 0  // diagnostic build only: per-step s_memtime stamps of workgroup 0 (tools/tracebench.py)
 #endif
@@ -228,14 +225,10 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
         });
         const bf16x8 y = __builtin_bit_cast(bf16x8, yw);
         *(bf16x8*)(dst + oT + j * ROWB) = y;
-#if ASR_DEEP_NT
-        // streaming stores: x_{l+1} and its mask are read back only by the backward
+        // streaming (nt) stores: x_{l+1} and its mask are read back only by the backward
+        // (+6 % forward, -1 % backward against default-policy stores, A/B r02k)
         if (store) __builtin_nontemporal_store(yw, (u32x4v*)(yl + oG + j * ROW_G));
         if (MASK) __builtin_nontemporal_store((uint8_t)bits, ml + oM + j * 64);
-#else
-        if (store) *(bf16x8*)(yl + oG + j * ROW_G) = y;
-        if (MASK) ml[oM + j * 64] = (uint8_t)bits;
-#endif
         xr[j] = y;
       }
 #pragma unroll
@@ -282,15 +275,10 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
 // One barrier per layer.  LDS: 2 dz tiles (swizzled, zero halo) + zero row |
 // 2 x tiles (image rows, zero halo columns) | 2 x 2 KiB masks | db partials.
 // ---------------------------------------------------------------------------
-#ifndef ASR_DEEP_WDEPTH
-#define ASR_DEEP_WDEPTH 2  // wgrad waves: x / dz row fragments read this many rows ahead of their MFMAs (3: flat, r04p)
-#endif
-#ifndef ASR_DEEP_NDG
-#define ASR_DEEP_NDG 8
-#endif
-constexpr int NDG = ASR_DEEP_NDG;        // dgrad waves (image rows split among them)
-constexpr int RPB = H / NDG;             // image rows per dgrad wave
-constexpr int KSEG = NDG == 4 ? 12 : 8;  // layers per segment (dW accumulators in registers)
+constexpr int WDEPTH = 2;   // wgrad waves: x / dz row fragments read this many rows ahead of their MFMAs (3: flat, r04p)
+constexpr int NDG = 8;      // dgrad waves (image rows split among them; 4 waves: slower, r02i)
+constexpr int RPB = H / NDG;  // image rows per dgrad wave
+constexpr int KSEG = 8;     // layers per segment (dW accumulators in registers)
 constexpr int NWB = NDG + 4;             // waves per backward workgroup: dgrad, 3 wgrad, staging
 constexpr int ES = 9 * C * C + C;        // slab floats per layer
 constexpr int XT = H * ROWB;             // x tile: 32 image rows x 34 columns
@@ -497,7 +485,7 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
     // fragment of image row ir-1 feeds output rows ir - ky; reads run DEPTH rows
     // ahead of the MFMAs
     auto wgrad_layer = [&](f32x4 (&a)[3], int tt) {
-      constexpr int DEPTH = ASR_DEEP_WDEPTH;
+      constexpr int DEPTH = WDEPTH;
       const int par = tt & 1;
       const unsigned char* xt = lds + L_X + par * XT + kx * 32 - ROWB;  // + ir*ROWB: image row ir-1 < XS
       const unsigned char* xh = lds + xhi_base(tt) - XS * ROWB + kx * 32 - ROWB;  // image rows >= XS

@@ -709,10 +709,7 @@ int launch_trans_fwd_lds(const T* x, T* y, uint8_t* mask, const float* k2, const
   const long items = (long)N * (H / 2 / G::BRO);
   int cus = cu_count();
   if (cus <= 0) cus = 256;
-#ifndef ASR_TFL_WPC
-#define ASR_TFL_WPC 2
-#endif
-  const int grid = (int)std::max<long>(1, std::min<long>(items, (long)ASR_TFL_WPC * cus));
+  const int grid = (int)std::max<long>(1, std::min<long>(items, 2L * cus));  // 2 workgroups per CU
   hipLaunchKernelGGL((k_trans_fwd_lds<CI, CO, WO, T>), dim3(grid), dim3(64 * G::NW), G::LDS, s, x, y, mask, k2, b2, k1,
                      b1, N, H);
   ASR_LAUNCH_CHECK("k_trans_fwd_lds");
@@ -850,10 +847,7 @@ int launch_trans_dgrad_lds(const T* dy, const uint8_t* mask, const float* k2, co
   const long items = (long)N * (H / G::BR);
   int cus = cu_count();
   if (cus <= 0) cus = 256;
-#ifndef ASR_TDL_WPC
-#define ASR_TDL_WPC 1
-#endif
-  const int grid = (int)std::max<long>(1, std::min<long>(items, (long)ASR_TDL_WPC * cus));
+  const int grid = (int)std::max<long>(1, std::min<long>(items, (long)cus));  // 1 workgroup per CU
   hipLaunchKernelGGL((k_trans_dgrad_lds<CI, CO, WO, T>), dim3(grid), dim3(512), G::LDS, s, dy, mask, k2, k1, dx, N, H);
   ASR_LAUNCH_CHECK("k_trans_dgrad_lds");
   return ASR_OK;
@@ -884,10 +878,7 @@ int launch_trans_wgrad_lds(const T* dy, const uint8_t* mask, const T* x, float* 
   const long items = (long)N * ((H / 2 + G::BRO - 1) / G::BRO);
   int cus = cu_count();
   if (cus <= 0) cus = 256;
-#ifndef ASR_TWL_WPC
-#define ASR_TWL_WPC 2
-#endif
-  const int grid = (int)std::max<long>(1, std::min<long>({items, (long)ASR_TWL_WPC * cus, (long)max_rows}));
+  const int grid = (int)std::max<long>(1, std::min<long>({items, 2L * cus, (long)max_rows}));  // 2 per CU
   hipLaunchKernelGGL((k_trans_wgrad_lds<CI, CO, WO, T>), dim3(grid), dim3(512), G::LDS, s, dy, mask, x, part, N, H);
   ASR_LAUNCH_CHECK("k_trans_wgrad_lds");
   *rows_out = grid;
@@ -1131,12 +1122,8 @@ SLayout stages_layout(const asr_stages_config* c) {
     L.Pmax = std::max(L.Pmax, g.P);
     g.ntheta = theta_count(g.C, c->param_kind, c->antisymmetric);
     g.deep = c->dtype == ASR_BF16 && g.L > 0 && deep16_supported(H, W, g.C);
-#ifndef ASR_NO_STAGE_IMG
     g.img = c->dtype == ASR_BF16 && g.L > 0 && !g.deep && stage_img_supported(H, W, g.C);
     g.img32 = c->dtype != ASR_BF16 && g.L > 0 && stage_img32_supported(H, W, g.C);
-#else
-    g.img = g.img32 = false;
-#endif
     g.E = 9L * g.C * g.C;
     g.blk_stride = g.ntheta + g.C;
     g.mask_bytes = (long)align_up((size_t)asr_mask_bytes(c->N, H, W, g.C), 256);
