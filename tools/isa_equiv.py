@@ -20,7 +20,8 @@ def kernels(asm):
         if not name.startswith('_Z') or 's_endpgm' not in f:
             continue  # (data symbols and the metadata that follows them)
         body = [re.sub(r'\.LBB\d+_\d+', 'L', l.strip()) for l in f.split('\n')[1:]]
-        out[name] = [l for l in body if l and not l.startswith((';', '.'))]
+        # (the trailing __hip_cuid_<hash of the source file> symbol is not code)
+        out[name] = [l for l in body if l and not l.startswith((';', '.', '__hip_cuid_'))]
     return out
 
 
