@@ -288,6 +288,16 @@ __global__ __launch_bounds__(256) void k_relu_grad_bf16(bf16* __restrict__ d, co
   }
 }
 
+// host: k_relu_grad_bf16 over n elements (n % 8 == 0), in place on d
+int relu_grad_bf16(void* d, const void* x, long n, hipStream_t s) {
+  if (n % 8) return fail(ASR_E_ARG, "relu_grad_bf16: n %% 8 != 0");
+  const long n8 = n / 8;
+  hipLaunchKernelGGL(k_relu_grad_bf16, dim3((unsigned)std::max<long>(1, std::min<long>((n8 + 255) / 256, 4096))),
+                     dim3(256), 0, s, (bf16*)d, (const bf16*)x, n8);
+  ASR_LAUNCH_CHECK("k_relu_grad_bf16");
+  return ASR_OK;
+}
+
 // ---------------------------------------------------------------------------
 // metrics
 // ---------------------------------------------------------------------------
@@ -921,8 +931,8 @@ int asr_conv_backward(int mode, const void* dy, const void* x, const uint8_t* ma
   if ((dtheta || dbias || dw_hwio) && !x) return fail(ASR_E_ARG, "asr_conv_backward: x needed for weight gradients");
   if (dtheta && !theta_dst) return fail(ASR_E_ARG, "asr_conv_backward: theta_dst needed for dtheta");
   if (dtype != ASR_F32 && dtype != ASR_BF16) return fail(ASR_E_ARG, "asr_conv_backward: bad dtype");
-  if (dtype == ASR_BF16 && !mfma_supported(C, W) && !(mode == ASR_MODE_EULER && convb_supported(W, C)))
-    return fail(ASR_E_UNSUPPORTED, "bf16 conv needs C in {16,32,64} and W == 32 (W in {16, 8}: Euler mode) (C=%d W=%d)",
+  if (dtype == ASR_BF16 && !mfma_supported(C, W) && !convb_supported(W, C))
+    return fail(ASR_E_UNSUPPORTED, "bf16 conv needs C in {16,32,64} and W in {32, 16, 8} (C=%d W=%d)",
                 C, W);
   if (!ws || ws_bytes < bwd_ws_layout(N, H, W, C, dtype).total)
     return fail(ASR_E_WORKSPACE, "asr_conv_backward: workspace too small");

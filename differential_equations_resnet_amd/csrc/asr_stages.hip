@@ -94,6 +94,10 @@ int conv_backward_keep_slabs(const void* dy, const void* x, const uint8_t* mask,
 bool stem_supported(int Cin, int H, int W, int C);
 int stem_forward(const void* img, int input_u8, const float* w1, const float* b1, int N, int H, int W, int Cin, int C,
                  float mean, float inv_std, int use_norm, void* out, int out_bf16, hipStream_t s);
+int stem_wgrad_mfma(const void* img, int input_u8, const void* dz1, int N, int H, int W, int Cin, int C, float mean,
+                    float inv_std, int use_norm, float* slabs, int* nslabs, hipStream_t s);
+bool stem_wgrad_mfma_supported(int Cin, int H, int W, int C);
+int relu_grad_bf16(void* d, const void* x, long n, hipStream_t s);
 int stem_wgrad(const void* img, int input_u8, const void* dx1, const void* x1, int act_bf16, int N, int H, int W,
                int Cin, int C, float mean, float inv_std, int use_norm, float* slabs, int* nslabs, hipStream_t s);
 int head(const void* xL, int act_bf16, const float* fck, const float* fcb, const float* targets, int N, int HW, int C,
@@ -1488,11 +1492,21 @@ int asr_stages_forward_backward(const asr_stages_config* cfg, const float* param
       std::swap(d, e);
     }
   }
-  // stem: dz1 = dx1 [x1 > 0] inside stem_wgrad; conv1 kernel / bias gradients
+  // stem: conv1 kernel / bias gradients from dz1 = dx1 [x1 > 0].  bf16 nets at C = 16 / 64: dz1 in place
+  // (k_relu_grad_bf16), then the weight gradient on MFMA (k_stem_wgrad_mfma: bf16 (v - mean) and dz1,
+  // exact products for u8 images with a half-integer mean, fp32 sums; 51 -> ~18 us at he32_bf16's batch);
+  // else the fp32 VALU kernel, which applies the relu' itself
   const float inv_std = cfg->use_norm ? 1.f / cfg->divide_by_stddev : 1.f;
   int nsl = 0;
-  ASR_TRY(stem_wgrad(images, cfg->input_u8, d, b + L.act0, L.bf ? 1 : 0, N, cfg->H, cfg->W, cfg->Cin, cfg->C[0],
-                     cfg->subtract_mean, inv_std, cfg->use_norm, (float*)(b + L.sslabs), &nsl, s));
+  const long P0 = (long)N * cfg->H * cfg->W * cfg->C[0];
+  if (L.bf && P0 % 8 == 0 && stem_wgrad_mfma_supported(cfg->Cin, cfg->H, cfg->W, cfg->C[0])) {
+    ASR_TRY(relu_grad_bf16(d, b + L.act0, P0, s));
+    ASR_TRY(stem_wgrad_mfma(images, cfg->input_u8, d, N, cfg->H, cfg->W, cfg->Cin, cfg->C[0], cfg->subtract_mean,
+                            inv_std, cfg->use_norm, (float*)(b + L.sslabs), &nsl, s));
+  } else {
+    ASR_TRY(stem_wgrad(images, cfg->input_u8, d, b + L.act0, L.bf ? 1 : 0, N, cfg->H, cfg->W, cfg->Cin, cfg->C[0],
+                       cfg->subtract_mean, inv_std, cfg->use_norm, (float*)(b + L.sslabs), &nsl, s));
+  }
   if (nsl > kMaxStemSlabs) return fail(ASR_E_UNSUPPORTED, "asr_stages: stem slabs %d > %d", nsl, kMaxStemSlabs);
   return reduce_and_project((const float*)(b + L.sslabs), nsl, 9L * cfg->Cin * cfg->C[0], cfg->C[0], nullptr, 0,
                             nullptr, grads + L.off_c1b, grads + L.off_c1k, (float*)(b + L.sred), s);

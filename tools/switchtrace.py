@@ -65,9 +65,34 @@ for l in range(L - 1, -1, -1):
     if l < L - 1 and tot > wv:
         worst, wv = l, tot
 print(f"worst switch: block {worst} (max poll + wgrad barrier {wv} cycles)")
+sl = sw[:, :L - 1]  # the switches with a poll (blocks L-2 .. 0)
+ov_w = (sl[:, :, 2] - sl[:, :, 0]).ravel()
+ov_d = (sl[:, :, 4] - sl[:, :, 3]).ravel()
+print(f"mean switch overhead over {sl.shape[1]} switches x {grid} workgroups: wgrad wave poll + barrier "
+      f"{ov_w.mean():.0f} cycles (p50 {np.median(ov_w):.0f}, p99 {np.percentile(ov_w, 99):.0f}), dgrad wave barrier "
+      f"{ov_d.mean():.0f} cycles (p50 {np.median(ov_d):.0f}, p99 {np.percentile(ov_d, 99):.0f})")
 if a.raw and worst is not None:
     s = sw[:, worst]
     print("  wg   poll  wgrad_bar  dgrad_bar  arrival_us")
     for w in np.argsort(-(s[:, 1] - s[:, 0]))[:32]:
         print(f"  {w:3d} {s[w, 1] - s[w, 0]:6d} {s[w, 2] - s[w, 1]:10d} {s[w, 4] - s[w, 3]:10d} "
               f"{(s[w, 5] - t0) / 100.0:10.2f}")
+
+# per-XCD pace (workgroup w on XCD w % 8 under the dispatcher's round-robin): the in-kernel clock
+# (s_memtime / s_memrealtime over the workgroup's run) and its end time, both stack kernels
+tb = (ctypes.c_uint64 * (2 * 2 * 40 * 8))()
+cb = (ctypes.c_uint64 * (2 * 1024 * 4))()
+assert cl.asr_debug_blk_trace(tb, ctypes.sizeof(tb), cb, ctypes.sizeof(cb)) == 0
+ck = np.frombuffer(cb, np.uint64).reshape(2, 1024, 4).astype(np.int64)
+for k, name in ((0, "k_fwd3_stack"), (1, "k_bwd3_stack")):
+    c = ck[k]
+    ok = (c[:, 0] > 0) & (c[:, 2] > c[:, 0])
+    idx = np.nonzero(ok)[0]
+    c = c[ok]
+    ghz = (c[:, 2] - c[:, 0]) / (c[:, 3] - c[:, 1]) * 0.1
+    end = (c[:, 3] - c[:, 1].min()) / 100.0
+    dur = (c[:, 3] - c[:, 1]) / 100.0
+    print(f"{name}: {len(c)} workgroups, end us p0/p50/p100 {end.min():.1f}/{np.median(end):.1f}/{end.max():.1f}; "
+          f"per XCD (wg % 8): clock GHz / run us median / end us max")
+    print("   " + "  ".join(f"x{x}: {np.median(ghz[idx % 8 == x]):.3f} / {np.median(dur[idx % 8 == x]):.1f} / "
+                            f"{end[idx % 8 == x].max():.1f}" for x in range(8) if (idx % 8 == x).any()))
