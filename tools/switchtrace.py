@@ -96,3 +96,11 @@ for k, name in ((0, "k_fwd3_stack"), (1, "k_bwd3_stack")):
           f"per XCD (wg % 8): clock GHz / run us median / end us max")
     print("   " + "  ".join(f"x{x}: {np.median(ghz[idx % 8 == x]):.3f} / {np.median(dur[idx % 8 == x]):.1f} / "
                             f"{end[idx % 8 == x].max():.1f}" for x in range(8) if (idx % 8 == x).any()))
+# the forward's two workgroups per CU: the first-dispatched half (blockIdx < grid/2) vs the second
+c = ck[0]
+ok = (c[:, 0] > 0) & (c[:, 2] > c[:, 0])
+idx = np.nonzero(ok)[0]
+dur = (c[ok][:, 3] - c[ok][:, 1]) / 100.0
+half = len(idx) // 2
+print(f"k_fwd3_stack run us, blockIdx < {half}: p50 {np.median(dur[idx < half]):.1f} max {dur[idx < half].max():.1f}; "
+      f">= {half}: p50 {np.median(dur[idx >= half]):.1f} max {dur[idx >= half].max():.1f}")
