@@ -1,22 +1,24 @@
 """Per-training-step kernel time from a rocprofv3 kernel trace of bench.py:
-steps are delimited by k_theta_to_w_pack (first launch of every step); the
-standalone block-roofline launches after the last step are excluded.
+a step is every launch up to and including its k_adam (round 6: the
+multi-stage net opens each stage with a k_theta_to_w_pack, and the round-5
+segmentation from the last of them to k_adam missed the step's first part);
+the standalone block-roofline launches after the last step are excluded.
 usage: step_breakdown.py run_kernel_trace.csv"""
 import csv
 import sys
 from collections import defaultdict
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-steps = []
-i = 0
-while i < len(rows):  # a step: k_theta_to_w_pack ... k_adam (the network's first and last launch)
-    if "theta_to_w_pack" in rows[i]["Kernel_Name"]:
-        j = next((j for j in range(i + 1, len(rows)) if "k_adam" in rows[j]["Kernel_Name"]
-                  or "theta_to_w_pack" in rows[j]["Kernel_Name"]), None)
-        if j is not None and "k_adam" in rows[j]["Kernel_Name"]:
-            steps.append(rows[i:j + 1])
-            i = j
-    i += 1
+# a step: every launch after the previous step's k_adam up to and including its own (the single-stage
+# net opens a step with k_theta_to_w_pack; the multi-stage net launches one per stage, so the
+# first-to-adam segmentation counts every launch of the step); the launches after the last step
+# (block-roofline legs) are excluded
+steps, cur = [], []
+for r in rows:
+    cur.append(r)
+    if "k_adam" in r["Kernel_Name"]:
+        steps.append(cur)
+        cur = []
 steps = steps[-10:]  # timed-region steps
 per = defaultdict(float)
 wall = busy = 0.0
@@ -35,6 +37,7 @@ for st in steps:
                 break
         per[name[:60]] += d
 n = len(steps)
-print(f"{n} steps: wall {wall / n:.1f} us/step (first launch to last end), kernels busy {busy / n:.1f} us/step")
+print(f"{n} steps: wall {wall / n:.1f} us/step (first launch to last end), kernels busy {busy / n:.1f} us/step, "
+      f"{sum(len(st) for st in steps) / n:.0f} launches/step")
 for k, v in sorted(per.items(), key=lambda x: -x[1]):
     print(f"  {k:<40s} {v / n:9.1f} us/step")
