@@ -78,10 +78,10 @@ int block_stack_fwd_mfma(const void* x0, void* ys, long y_stride, uint8_t* masks
                          long w_stride, const float* bias, long bias_stride, float h, int N, int H, int W, int C, int L,
                          hipStream_t s, int slots = 0);
 int deep16_forward(const void* x0, void* y0, long y_stride, uint8_t* mask0, long mask_stride, const void* wpack,
-                   const float* bias, long bias_stride, float h, int N, int L, bool store_all, hipStream_t s,
-                   const void* wlo = nullptr);
-int theta_to_w_pack_hilo(const float* theta, long theta_stride, int L, int C, const int32_t* w_src, float gamma,
-                         void* w_hi, void* w_lo, long w_stride, hipStream_t s);
+                   const float* bias, long bias_stride, float h, int N, int L, bool store_all, hipStream_t s);
+int theta_to_w_bf16(const float* theta, long theta_stride, int L, int C, const int32_t* w_src, float gamma, void* w,
+                    long w_stride, bool balance, hipStream_t s, const int32_t* theta_dst = nullptr,
+                    long n_theta = 0);
 size_t deep16_slab_bytes(int N, int L);
 int deep16_backward(void* dbufA, void* dbufB, const void* xs, long x_stride, const uint8_t* masks, long mask_stride,
                     const void* wpack, float h, float two_gamma, int N, int L, float* slabs, int* slab_rows,
@@ -374,13 +374,12 @@ struct NetLayout {
   size_t grp;  // per-layer slab group sums, projected after the whole backward
   size_t slabs_all;  // fp32: every block's slabs, pass 1 of all blocks in one launch after the loop
   long slab_stride;
-  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_lo, wbuf_bwd, x0, acts, xmids, masks, dxa, dxb, dxg, bwdws, slabs2, slabs, red, probs,
+  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, x0, acts, xmids, masks, dxa, dxb, dxg, bwdws, slabs2, slabs, red, probs,
       loss_per, dlogits, gap, total;
   long mask_bytes;
   int act_bytes;
   bool fast_stem;
   bool deep;          // C=16 stack path: one fused launch forward, one backward (asr_deep16.hip)
-  bool hilo;          // ... its forward with W as bf16 hi + lo (not ASR_VARIANT_W_BF16)
   size_t deep_slabs;  // its weight-gradient slabs [L][rows][E+C]
   bool inference;     // ASR_VARIANT_INFERENCE: forward-only workspace (3 activation slots, no backward buffers)
   bool stack_bwd;     // C=64 Euler bf16: all blocks' backward in one k_bwd3_stack launch
@@ -448,9 +447,6 @@ static NetLayout net_layout(const asr_net_config* c) {
   L.w_src_bwd = take(L.sep_bwd && tr ? (size_t)L.E * 4 : 0);
   L.theta_dst = take((size_t)L.ntheta * 2 * 4);
   L.wbuf = take((size_t)c->L * L.wstride * L.act_bytes);
-  L.hilo = L.deep && !(c->variant & ASR_VARIANT_W_BF16);
-  // the fused C=16 forward's lo weights (also under ASR_VARIANT_W_BF16: a variant bit never moves the layout)
-  L.wbuf_lo = take(L.deep ? (size_t)c->L * L.wstride * L.act_bytes : 0);
   L.wbuf_bwd = take(L.sep_bwd && tr ? (size_t)c->L * L.wstride * L.act_bytes : 0);
   L.x0 = take(L.fast_stem ? 0 : (size_t)c->N * c->H * c->W * c->Cin * 4);
   // training keeps x_0 .. x_L for the backward; inference ping-pongs (x_0 + 2 slots)
@@ -545,15 +541,24 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
   const float inv_std = c->use_norm ? 1.f / c->divide_by_stddev : 1.f;
   if (training && L.inference) return fail(ASR_E_ARG, "an ASR_VARIANT_INFERENCE workspace has no training buffers");
   // 1. materialise W for all L blocks (one launch)
-  if (L.hilo)
-    ASR_TRY(theta_to_w_pack_hilo(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src), c->gamma,
-                                 ws + L.wbuf, ws + L.wbuf_lo, L.wstride, s));
+  //    (bf16: balanced rounding of the antisymmetric pairs, k_theta_to_w_pack_bal; ASR_VARIANT_W_BF16: to nearest)
+  const bool bal = !(c->variant & ASR_VARIANT_W_BF16);
+  if (bf)
+    ASR_TRY(theta_to_w_bf16(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src), c->gamma,
+                            ws + L.wbuf, L.wstride, bal, s,
+                            c->param_kind != ASR_PARAM_REGULAR ? (const int32_t*)(ws + L.theta_dst) : nullptr,
+                            L.ntheta));
   else
     ASR_TRY(asr_theta_to_w(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src), c->gamma,
                            ws + L.wbuf, L.wstride, c->dtype, s));
-  if (training && L.sep_bwd)
-    ASR_TRY(asr_theta_to_w(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src_bwd), 0.f,
-                           ws + L.wbuf_bwd, L.wstride, c->dtype, s));
+  if (training && L.sep_bwd) {  // (the transposed map pairs the same entries: W_bwd = -W^T after the rounding too)
+    if (bf)
+      ASR_TRY(theta_to_w_bf16(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src_bwd), 0.f,
+                              ws + L.wbuf_bwd, L.wstride, bal, s));
+    else
+      ASR_TRY(asr_theta_to_w(params + L.off_blk, L.blk_stride, c->L, C, (const int32_t*)(ws + L.w_src_bwd), 0.f,
+                             ws + L.wbuf_bwd, L.wstride, c->dtype, s));
+  }
   unsigned char* acts = ws + L.acts;
   auto act = [&](int i) -> unsigned char* {
     const int slot = training ? i : (i & 1);
@@ -586,7 +591,7 @@ static int net_forward_impl(const asr_net_config* c, const NetLayout& L, const f
   if (L.deep) {  // C=16: all L steps in one launch, images resident in LDS
     ASR_TRY(deep16_forward(act(0), act(training ? 1 : c->L), L.P, training ? (uint8_t*)(ws + L.masks) : nullptr,
                            L.mask_bytes, ws + L.wbuf, params + L.off_blk + L.ntheta, L.blk_stride, c->h, N, c->L,
-                           training, s, L.hilo ? ws + L.wbuf_lo : nullptr));
+                           training, s));
     return timed_event(c, 1, s);
   }
   if (bf && training && L.rk2 && block_stack_fwd_supported(N, H, W, C) && !(c->variant & ASR_VARIANT_PER_BLOCK_FWD)) {

@@ -44,6 +44,25 @@ int check_ws_device(const void* ws, const char* who);
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// One launch of the balanced bf16 weight pack for several layer sets (the
+// multi-stage net's stages, asr_stages.hip): one workgroup per layer, so the
+// stages' packs run side by side (asr_theta.hip, k_theta_to_w_pack_bal).
+struct PackJob {
+  const float* theta;
+  long theta_stride;
+  int L, C;
+  const int32_t* w_src;
+  float gamma;
+  void* w;
+  long w_stride;
+  // asr_param_map's theta_dst of a map known to pair its entries (3by3, general): theta read
+  // coalesced and no pairing check; nullptr: the entries gathered through w_src and checked
+  const int32_t* theta_dst;
+  long n_theta;
+};
+constexpr int kMaxPackJobs = 16;
+int theta_to_w_bf16_jobs(const PackJob* jobs, int njobs, hipStream_t s);
+
 // Slab layout of the pair-local C=64 stacked backward (k_bwd3_stack<..., PAIR>,
 // asr_block_mfma.hip): for an antisymmetric operator every theta pulls back
 // D(t,i,o) = dW[t][i][o] - dW[8-t][o][i] (tap t = 3ky+kx), and the slab holds

@@ -214,22 +214,38 @@ __device__ __forceinline__ f32x4 masked_dz4(f32x4 v, const uint8_t* __restrict__
 // stage rows y0-1 .. y0+BR of image n into tile (zeros outside the image and
 // in the two halo columns), float4 per thread; with dmask, src is dy and the
 // tile gets dz = dh * dy * [relu bit] (the Euler block's dz, no separate pass)
-template <int C, int W, typename Ts = float, int PS = C>
+template <int C, int W, typename Ts = float, int PS = C, int NT = 256>
 __device__ __forceinline__ void f32_stage_rows(const Ts* __restrict__ src, float* tile, int n, int y0, int H,
-                                               int tid, int nthreads, const uint8_t* __restrict__ dmask = nullptr,
+                                               int tid, const uint8_t* __restrict__ dmask = nullptr,
                                                float dh = 1.f) {
   using G = F32Band<C, W>;
-  constexpr int C4 = C / 4, NCH = (G::BR + 2) * G::TW * C4;
-  for (int i = tid; i < NCH; i += nthreads) {
-    const int r = i / (G::TW * C4), rem = i % (G::TW * C4), col = rem / C4, c4 = rem % C4;
-    const int gy = y0 - 1 + r, gx = col - 1;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)G::W) {
-      const long e = (((long)n * H + gy) * G::W + gx) * C + 4 * c4;
-      v = load4f(src + e);
-      if (dmask) v = masked_dz4(v, dmask, e, dh);
+  constexpr int C4 = C / 4, NCH = (G::BR + 2) * G::TW * C4, NIT = (NCH + NT - 1) / NT, B = 4;
+  // B loads in flight before their stores (a rolled loop waited for each load in turn)
+#pragma unroll
+  for (int k0 = 0; k0 < NIT; k0 += B) {
+    f32x4 v[B];
+    long ev[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+      const int i = tid + (k0 + k) * NT;
+      const int r = i / (G::TW * C4), rem = i % (G::TW * C4), col = rem / C4, c4 = rem % C4;
+      const int gy = y0 - 1 + r, gx = col - 1;
+      v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ev[k] = -1;
+      if (k0 + k < NIT && i < NCH && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)G::W) {
+        ev[k] = (((long)n * H + gy) * G::W + gx) * C + 4 * c4;
+        v[k] = load4f(src + ev[k]);
+      }
     }
-    *(f32x4*)(tile + (r * G::TW + col) * PS + 4 * c4) = v;
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+      const int i = tid + (k0 + k) * NT;
+      if (k0 + k < NIT && i < NCH) {
+        const int r = i / (G::TW * C4), rem = i % (G::TW * C4), col = rem / C4, c4 = rem % C4;
+        if (dmask && ev[k] >= 0) v[k] = masked_dz4(v[k], dmask, ev[k], dh);
+        *(f32x4*)(tile + (r * G::TW + col) * PS + 4 * c4) = v[k];
+      }
+    }
   }
 }
 
@@ -258,7 +274,7 @@ __global__ __launch_bounds__(256) void k_conv32(const float* __restrict__ xin, f
   f32x4 bz = {0.f, 0.f, 0.f, 0.f};
   if (MODE <= F_RELU && bias) bz = *(const f32x4*)(bias + 16 * ot + 4 * g);
   // (backward with dmask: xin is dy, the tile gets dz = h dy [relu bit])
-  f32_stage_rows<C, W, float, G::PSC>(xin, tile, n, y0, H, tid, 256, MODE >= B_EULER ? dmask : nullptr, h);
+  f32_stage_rows<C, W, float, G::PSC, 256>(xin, tile, n, y0, H, tid, MODE >= B_EULER ? dmask : nullptr, h);
   __syncthreads();
   // wave (ot, rw) takes the band's 16-pixel tiles rw, rw + WPT, ..; lane lx's pixel of tile tau is band
   // pixel 16 tau + lx (W = 8: a tile spans two rows, so validity is per lane)
@@ -345,7 +361,7 @@ __global__ __launch_bounds__(768) void k_wgrad32(const Tx* __restrict__ x, const
     const int n = (int)(item / nb), y0 = (int)(item % nb) * BR;
     const int rows = min(BR, H - y0);
     __syncthreads();  // the previous item's tiles consumed
-    f32_stage_rows<C, W, Tx, G::PSW>(x, xt, n, y0, H, tid, 768);
+    f32_stage_rows<C, W, Tx, G::PSW, 768>(x, xt, n, y0, H, tid);
     for (int i = tid; i < BR * G::W * C / 4; i += 768) {
       const int r = i / (G::W * C / 4);
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -872,7 +888,8 @@ static int launch_convb(const bf16* xin, bf16* out, uint8_t* mask, const bf16* w
 // Waves: TS pair splits (i-tile it, NO o-tiles: the 9 taps' A fragments feed
 // NO MFMAs each) x PS chunk splits, partials summed through LDS at the end;
 // db on MFMA (ones x dz) in the it = 0 waves.  Persistent over bands, the next
-// band's global loads in flight during this band's MFMAs; one [dW | db] slab
+// band's global loads in flight during this band's MFMAs (dz = dy & mask formed
+// at the LDS store, so nothing waits for them before); one [dW | db] slab
 // per workgroup, the rows the fp32 wgrad grid sizes (f32_block_slab_rows).
 // ---------------------------------------------------------------------------
 template <int C, int W_>
@@ -927,6 +944,7 @@ __global__ __launch_bounds__((WgB<C, W>::NTH)) void k_wgradb(const bf16* __restr
 #pragma unroll
   for (int o = 0; o < NO; ++o) accb[o] = f32x4{0.f, 0.f, 0.f, 0.f};
   uint4 px[G::XPT], pd[G::DPT];
+  unsigned pm[G::DPT];  // the relu bits, applied at the LDS store: masking here would wait for the loads
   auto fetch = [&](long item) {
     const int n = (int)(item / nb), y0 = (int)(item % nb) * BR;
 #pragma unroll
@@ -942,11 +960,12 @@ __global__ __launch_bounds__((WgB<C, W>::NTH)) void k_wgradb(const bf16* __restr
     for (int k = 0; k < G::DPT; ++k) {
       const int i = tid + k * G::NTH;
       pd[k] = make_uint4(0u, 0u, 0u, 0u);
+      pm[k] = 0u;
       const int r = i / (W * G::C8);
       if (i < G::DCH && y0 + r < H) {
         const long e = ((long)n * H + y0) * W * C + 8L * i;
         pd[k] = *(const uint4*)(dy + e);
-        if constexpr (MASKED) pd[k] = mask8_bf16(pd[k], dmask[e >> 3]);
+        if constexpr (MASKED) pm[k] = dmask[e >> 3];
       }
     }
   };
@@ -961,7 +980,7 @@ __global__ __launch_bounds__((WgB<C, W>::NTH)) void k_wgradb(const bf16* __restr
     for (int k = 0; k < G::DPT; ++k) {
       const int i = tid + k * G::NTH;
       const int P = i / G::C8, c8 = i % G::C8;
-      if (i < G::DCH) *(uint4*)(dzt + P * C + 8 * (c8 ^ G::swz(P))) = pd[k];
+      if (i < G::DCH) *(uint4*)(dzt + P * C + 8 * (c8 ^ G::swz(P))) = MASKED ? mask8_bf16(pd[k], pm[k]) : pd[k];
     }
   };
   // the lane's 8-B piece of channels 16 ch + 4 pq .. +3 at pixel P of a tile

@@ -132,19 +132,10 @@ using Frag = FragT<4>;
 //   mask0: relu masks (MASK), layer l at mask0 + l*mask_stride bytes; per
 //          pixel 16 bits, bit c = channel c
 //   wpack: packed W^T, layer l at wpack + l*WSTRIDE; bias: layer l at bias + l*bias_stride
-//   wlo (LO): the bf16 residual W - bf16(W) in the same packing; the conv then
-//          runs both operands (hi, then lo) on the same B fragments, so the
-//          weights enter with ~16 mantissa bits instead of 8.  Rounding W to
-//          bf16 perturbs every pixel of every layer the same way, and over a
-//          deep stack that systematic error dominates the bf16 path's
-//          deviation from the fp32 reference (tools/bf16_depth_emulate.py:
-//          C3 at L=108); the activation roundings are per element
-//          and average out.
-template <bool STORE_ALL, bool MASK, bool LO>
+template <bool STORE_ALL, bool MASK>
 __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __restrict__ x0, bf16* __restrict__ y0,
                                                             long y_stride, uint8_t* __restrict__ mask0,
                                                             long mask_stride, const bf16* __restrict__ wpack,
-                                                            const bf16* __restrict__ wlo,
                                                             const float* __restrict__ bias, long bias_stride,
                                                             float h, int N, int L) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -175,9 +166,8 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
     for (int j = 0; j < RPW; ++j) xr[j] = *(const bf16x8*)(xin + oG + j * ROW_G);
 #pragma unroll
     for (int j = 0; j < RPW; ++j) *(bf16x8*)(lds + oT + j * ROWB) = xr[j];
-    bf16x8 A[KS], An[KS], Al[LO ? KS : 1], Anl[LO ? KS : 1];
+    bf16x8 A[KS], An[KS];
     load_wt(wpack, wo, A);
-    if constexpr (LO) load_wt(wlo, wo, Al);
     float bz[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) bz[e] = bsrc[4 * g + e];
@@ -192,7 +182,6 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
       // (copied to A / bz at the layer end: alternating two register sets
       // instead makes this kernel spill)
       load_wt(wpack + (long)ln * WSTRIDE, wo, An);
-      if constexpr (LO) load_wt(wlo + (long)ln * WSTRIDE, wo, Anl);
 #pragma unroll
       for (int e = 0; e < 4; ++e) bn[e] = bsrc[ln * bstr + 4 * g + e];
       const bool store = STORE_ALL || l == L - 1;
@@ -206,8 +195,6 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
         if (j + 3 <= RPW + 1) fr.load(src, bF, bG, j + 3);
         f32x4 acc[2] = {{bz[0], bz[1], bz[2], bz[3]}, {bz[0], bz[1], bz[2], bz[3]}};
         row_mfma(A, fr.F[j & 3], fr.F[(j + 1) & 3], fr.F[(j + 2) & 3], fr.G[j & 3], fr.G[(j + 2) & 3], acc);
-        if constexpr (LO)
-          row_mfma(Al, fr.F[j & 3], fr.F[(j + 1) & 3], fr.F[(j + 2) & 3], fr.G[j & 3], fr.G[(j + 2) & 3], acc);
         // epilogue on the regrouped chunk: y = x + h * relu(z) (fp32, one rounding),
         // relu bits as TF's ReluGrad (z > 0)
         float z[8];
@@ -233,10 +220,6 @@ __global__ __launch_bounds__(64 * NWAVE, 2) void k_fwd16_fused(const bf16* __res
       }
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) A[ks] = An[ks];
-      if constexpr (LO) {
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) Al[ks] = Anl[ks];
-      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) bz[e] = bn[e];
       barrier_lds();  // layer l+1's tile complete; layer l's tile free
@@ -664,30 +647,23 @@ __global__ __launch_bounds__(64 * NWB, 1) void k_bwd16_fused(bf16* __restrict__ 
 bool deep16_supported(int H, int W, int C) { return C == deep::C && H == deep::H && W == deep::W; }
 
 // L Euler blocks in one launch (see k_fwd16_fused).  bias: layer l's at
-// bias + l*bias_stride; wpack: asr_theta_to_w's bf16 output for the L layers;
-// wlo (nullable): theta_to_w_pack_hilo's residual pack (hi + lo weights).
+// bias + l*bias_stride; wpack: asr_theta_to_w's bf16 output for the L layers.
 int deep16_forward(const void* x0, void* y0, long y_stride, uint8_t* mask0, long mask_stride, const void* wpack,
-                   const float* bias, long bias_stride, float h, int N, int L, bool store_all, hipStream_t s,
-                   const void* wlo) {
+                   const float* bias, long bias_stride, float h, int N, int L, bool store_all, hipStream_t s) {
   if (L < 1 || N < 1) return fail(ASR_E_ARG, "deep16_forward: bad N=%d L=%d", N, L);
   int cus = cu_count();
   if (cus <= 0) cus = 256;
   const int grid = std::max(1, std::min(N, 2 * cus));
   const size_t lds = 2 * (size_t)deep::TILE + deep::ROWB;
-#define ASR_FWD16(SA, MK, LO)                                                                                    \
-  hipLaunchKernelGGL((deep::k_fwd16_fused<SA, MK, LO>), dim3(grid), dim3(64 * deep::NWAVE), lds, s,            \
-                     (const bf16*)x0, (bf16*)y0, y_stride, mask0, mask_stride, (const bf16*)wpack,              \
-                     (const bf16*)wlo, bias, bias_stride, h, N, L)
-  if (wlo) {  // the networks' training and inference forwards
-    if (store_all && mask0) ASR_FWD16(true, true, true);
-    else if (!store_all && !mask0) ASR_FWD16(false, false, true);
-    else return fail(ASR_E_ARG, "deep16_forward: hi/lo weights need store_all == (mask0 != null)");
-  } else if (store_all) {
-    if (mask0) ASR_FWD16(true, true, false);
-    else ASR_FWD16(true, false, false);
+#define ASR_FWD16(SA, MK)                                                                                        \
+  hipLaunchKernelGGL((deep::k_fwd16_fused<SA, MK>), dim3(grid), dim3(64 * deep::NWAVE), lds, s, (const bf16*)x0, \
+                     (bf16*)y0, y_stride, mask0, mask_stride, (const bf16*)wpack, bias, bias_stride, h, N, L)
+  if (store_all) {
+    if (mask0) ASR_FWD16(true, true);
+    else ASR_FWD16(true, false);
   } else {
-    if (mask0) ASR_FWD16(false, true, false);
-    else ASR_FWD16(false, false, false);
+    if (mask0) ASR_FWD16(false, true);
+    else ASR_FWD16(false, false);
   }
 #undef ASR_FWD16
   ASR_LAUNCH_CHECK("k_fwd16_fused");

@@ -77,10 +77,7 @@ int wgradb_layers(const void* x0, long x_stride, const void* dys, long d_stride,
 // asr_deep16.hip: the C = 16, 32 x 32 bf16 stage as one fused forward / backward launch
 bool deep16_supported(int H, int W, int C);
 int deep16_forward(const void* x0, void* y0, long y_stride, uint8_t* mask0, long mask_stride, const void* wpack,
-                   const float* bias, long bias_stride, float h, int N, int L, bool store_all, hipStream_t s,
-                   const void* wlo = nullptr);
-int theta_to_w_pack_hilo(const float* theta, long theta_stride, int L, int C, const int32_t* w_src, float gamma,
-                         void* w_hi, void* w_lo, long w_stride, hipStream_t s);
+                   const float* bias, long bias_stride, float h, int N, int L, bool store_all, hipStream_t s);
 size_t deep16_slab_bytes(int N, int L);
 int deep16_backward(void* dbufA, void* dbufB, const void* xs, long x_stride, const uint8_t* masks, long mask_stride,
                     const void* wpack, float h, float two_gamma, int N, int L, float* slabs, int* slab_rows,
@@ -1027,7 +1024,7 @@ struct StageL {
   int C, L, H, W, S, Cp, Hp, Wp;  // S = 0: no transition; Cp/Hp/Wp the stage input's shape
   long P, ntheta, E, blk_stride, mask_bytes;
   long off_t, off_blk;          // parameter offsets (floats)
-  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_lo, wbuf_bwd, act_t, mask_t, acts, masks, grp, slabs;  // workspace offsets
+  size_t w_src, w_src_bwd, theta_dst, wbuf, wbuf_bwd, act_t, mask_t, acts, masks, grp, slabs;  // workspace offsets
   size_t act_tb, xin32;  // bf16 nets: the transition's output in bf16, its input in fp32 (kept for the backward)
   bool tdirect;          // bf16 nets: the transition on the LDS kernels in bf16 (no fp32 copies)
   bool deep;             // bf16 nets: a C = 16, 32 x 32 stage on the fused deep16 kernels (x0: its input slot,
@@ -1155,7 +1152,6 @@ SLayout stages_layout(const asr_stages_config* c) {
     g.wstride = L.bf ? asr_wpack_elems(g.C) : g.E;
     g.wbuf = take((size_t)std::max(g.L, 1) * g.wstride * L.act_bytes);
     g.wbuf_bwd = L.sep_bwd ? take((size_t)std::max(g.L, 1) * g.wstride * L.act_bytes) : 0;
-    g.wbuf_lo = g.deep ? take((size_t)g.L * g.wstride * L.act_bytes) : 0;  // deep16's hi/lo forward weights
     g.tdirect = L.bf && g.S && trans_lds_supported(g.Hp, g.Wp, g.Cp, g.C, g.S);
     L.any_tconv = L.any_tconv || (L.bf && g.S && !g.tdirect);
     if (g.deep || g.img || g.img32) {  // [x0 | x1 .. xL] contiguous; the stem or the transition writes x0 in place
@@ -1221,6 +1217,31 @@ int stages_forward_impl(const asr_stages_config* c, const SLayout& L, const floa
                         bool training, unsigned char* b, hipStream_t s, const void** xL) {
   const float inv_std = c->use_norm ? 1.f / c->divide_by_stddev : 1.f;
   const int wdt = L.bf ? ASR_BF16 : ASR_F32;
+  // every stage's W first, in one launch for the bf16 stages (the balanced pack of asr_theta_to_w,
+  // k_theta_to_w_pack_bal: a workgroup per layer, the stages' packs side by side)
+  PackJob jobs[kMaxPackJobs];
+  int nj = 0;
+  for (int si = 0; si < L.ns; ++si) {
+    const StageL& g = L.st[si];
+    if (g.L == 0) continue;
+    const bool pack = L.bf && nj + 2 <= kMaxPackJobs && (g.C == 16 || g.C == 32 || g.C == 64);
+    if (pack)
+      jobs[nj++] = {params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src), c->gamma, b + g.wbuf,
+                    g.wstride, c->param_kind != ASR_PARAM_REGULAR ? (const int32_t*)(b + g.theta_dst) : nullptr,
+                    g.ntheta};
+    else
+      ASR_TRY(asr_theta_to_w(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src), c->gamma,
+                             b + g.wbuf, g.wstride, wdt, s));
+    if (training && L.sep_bwd) {
+      if (pack)
+        jobs[nj++] = {params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src_bwd), 0.f,
+                      b + g.wbuf_bwd, g.wstride, nullptr, 0};
+      else
+        ASR_TRY(asr_theta_to_w(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src_bwd), 0.f,
+                               b + g.wbuf_bwd, g.wstride, wdt, s));
+    }
+  }
+  if (nj) ASR_TRY(theta_to_w_bf16_jobs(jobs, nj, s));
   ASR_TRY(stem_forward(images, c->input_u8, params + L.off_c1k, params + L.off_c1b, c->N, c->H, c->W, c->Cin,
                        c->C[0], c->subtract_mean, inv_std, c->use_norm, b + L.act0, L.bf ? 1 : 0, s));
   const void* x = b + L.act0;
@@ -1249,15 +1270,6 @@ int stages_forward_impl(const asr_stages_config* c, const SLayout& L, const floa
       }
     }
     if (g.L == 0) continue;
-    if (g.deep)
-      ASR_TRY(theta_to_w_pack_hilo(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src),
-                                   c->gamma, b + g.wbuf, b + g.wbuf_lo, g.wstride, s));
-    else
-      ASR_TRY(asr_theta_to_w(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src), c->gamma,
-                             b + g.wbuf, g.wstride, wdt, s));
-    if (training && L.sep_bwd)
-      ASR_TRY(asr_theta_to_w(params + g.off_blk, g.blk_stride, g.L, g.C, (const int32_t*)(b + g.w_src_bwd), 0.f,
-                             b + g.wbuf_bwd, g.wstride, wdt, s));
     if (g.img32) {  // fp32: all L blocks in one launch, a workgroup per image
       if (x != b + g.x0)
         ASR_TRY(hip_check(hipMemcpyAsync(b + g.x0, x, (size_t)g.P * 4, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync"));
@@ -1279,7 +1291,7 @@ int stages_forward_impl(const asr_stages_config* c, const SLayout& L, const floa
       if (x != b + g.x0)
         ASR_TRY(hip_check(hipMemcpyAsync(b + g.x0, x, (size_t)g.P * 2, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync"));
       ASR_TRY(deep16_forward(b + g.x0, b + g.acts, g.P, (uint8_t*)(b + g.masks), g.mask_bytes, b + g.wbuf,
-                             params + g.off_blk + g.ntheta, g.blk_stride, c->h, c->N, g.L, true, s, b + g.wbuf_lo));
+                             params + g.off_blk + g.ntheta, g.blk_stride, c->h, c->N, g.L, true, s));
       x = b + g.acts + (size_t)(g.L - 1) * g.P * 2;
       continue;
     }

@@ -120,7 +120,15 @@ long asr_wpack_elems(int C);
  *   theta:  layer l's theta at theta + l*theta_stride (float32)
  *   w_src:  device copy of asr_param_map's w_src
  *   dtype == ASR_BF16: w_out (bf16) gets the MFMA fragment-packed layout,
- *                      layer l at l*w_stride elements;
+ *                      layer l at l*w_stride elements.  Balanced rounding
+ *                      (C <= 64, maps that pair every off-diagonal entry with
+ *                      its antisymmetric partner: the 3by3 and general kinds):
+ *                      each pair takes the bf16 neighbour that keeps every
+ *                      output channel's sum of rounding errors near zero, so
+ *                      W stays exactly antisymmetric and no channel carries a
+ *                      fixed offset through a deep stack; otherwise round to
+ *                      nearest.  Deterministic; restated bit-exactly by
+ *                      tests/helpers.py w_bf16_balanced;
  *   dtype == ASR_F32:  w_out (float) gets plain HWIO [3][3][C][C]. */
 int asr_theta_to_w(const float* theta, long theta_stride, int L, int C, const int32_t* w_src,
                    float gamma, void* w_out, long w_stride, int dtype, asr_stream_t stream);
@@ -316,15 +324,15 @@ typedef struct asr_net_config {
                                       workgroup slab) instead of the pair-local
                                       D = dW - dW*^T (74 tiles) the projection
                                       needs (cross-check and A/B arm)           */
-#define ASR_VARIANT_W_BF16 512    /* C=16 bf16 networks (the fused deep16 stack):
-                                     the forward conv takes W in bf16 alone
-                                     instead of bf16 hi + lo (~16 mantissa bits,
-                                     the default).  Faster (C3 +15 % images/s),
-                                     but rounding W perturbs every pixel of every
-                                     layer the same way, and over 108 blocks that
-                                     systematic error reaches 2.7e-2 relative L2
-                                     of a block's gradient vs the fp32 reference
-                                     (tests/test_gpu_depth.py)       */
+#define ASR_VARIANT_W_BF16 512    /* bf16 networks: W rounded to nearest bf16
+                                     instead of asr_theta_to_w's balanced
+                                     rounding.  Same speed; the nearest
+                                     rounding offsets every output channel by
+                                     a fixed sum that every pixel of every
+                                     layer sees, and over C3's 108 blocks that
+                                     reaches 2.7e-2 relative L2 of a block's
+                                     gradient vs the fp32 reference
+                                     (tests/test_gpu_depth.py)    */
 
 long asr_net_param_count(const asr_net_config* cfg);
 size_t asr_net_workspace_bytes(const asr_net_config* cfg);

@@ -747,21 +747,23 @@ def stages_init_params(spec: StagesSpec, rng, dtype=np.float64, bias_std=0.0):
 
 
 def _block_W(spec: StagesSpec, C, theta):
+    """(W, src, sign) of one block (src, sign None for the regular kind)."""
     if spec.kind == "regular":
-        return np.asarray(theta[0])
+        return np.asarray(theta[0]), None, None
     src, sign = _cached_map(C, spec.kind, spec.antisymmetric)
-    return assemble_from_map(flatten(theta), C, src, sign, spec.gamma)
+    return assemble_from_map(flatten(theta), C, src, sign, spec.gamma), src, sign
 
 
-def stages_forward(spec: StagesSpec, params, images, dtype=np.float64, rnd=None, w_hilo_stages=()):
+def stages_forward(spec: StagesSpec, params, images, dtype=np.float64, rnd=None, rnd_w=None):
     """rnd (optional): a rounding applied where a bf16 net (asr_stages_config
     dtype ASR_BF16) stores in bf16 -- the stem's output, every transition's and
     block's output, the blocks' assembled W -- so the restatement follows the
     bf16 executor's storage; everything else stays in `dtype`.
-    w_hilo_stages: indices of stages whose forward conv takes W as bf16 hi + lo
-    (the fused C=16 forward, k_fwd16_fused<.., LO>): their forward uses the
-    unrounded W, their backward (cached W) the rounded one."""
+    rnd_w (optional): the blocks' W rounding instead of rnd, called as
+    rnd_w(W, src, sign) with the block's parameter map (None, None for the
+    regular kind): the executor's balanced bf16 pack (tests/helpers.py)."""
     r = rnd if rnd is not None else (lambda a: a)
+    rw = rnd_w if rnd_w is not None else (lambda W, src, sign: r(W))
     ns = NetSpec(subtract_mean=spec.subtract_mean, divide_by_stddev=spec.divide_by_stddev)
     x0 = normalize_input(images, ns, dtype)
     z1 = conv2d_same(x0, params[0]) + params[1]
@@ -779,9 +781,9 @@ def stages_forward(spec: StagesSpec, params, images, dtype=np.float64, rnd=None,
         for _ in range(L):
             theta, b = params[i:i + nt], params[i + nt]
             i += nt + 1
-            W0 = _block_W(spec, C, theta)
-            W = r(W0)
-            y, z = euler_fwd(x, W0 if si in w_hilo_stages else W, b, spec.h)
+            W0, src, sign = _block_W(spec, C, theta)
+            W = np.asarray(rw(W0, src, sign), np.float64) if (rnd is not None or rnd_w is not None) else W0
+            y, z = euler_fwd(x, W, b, spec.h)
             ops.append(("b", x, z, W, C))
             x = r(y)
     fc_k, fc_b = params[i], params[i + 1]

@@ -10,6 +10,69 @@ def bf16_round(x):
     return r.astype(np.uint32).view(np.float32).reshape(a.shape)
 
 
+def _pairs_antisymmetric(src, sign, C):
+    """Every off-diagonal W[t][i][o] (i > o) and W[8-t][o][i] read the same
+    theta with opposite signs (the 3by3 and general maps, either
+    `antisymmetric` flag; not the regular kind)."""
+    s = np.asarray(src).reshape(9, C, C)
+    g = np.asarray(sign).reshape(9, C, C)
+    i, o = np.triu_indices(C, 1)[::-1]  # i > o
+    a, b = s[:, i, o], s[::-1][:, o, i]
+    return bool(np.all(a >= 0) and np.all(a == b) and np.all(g[:, i, o] == -g[::-1][:, o, i]))
+
+
+def w_bf16_balanced(W, src=None, sign=None):
+    """The bf16 W of the executor's weight pack (asr_theta.hip,
+    k_theta_to_w_pack_bal), bit-exact.  Maps whose off-diagonal entries come
+    in antisymmetric pairs (W[t][i][o] = -W[8-t][o][i]) round each pair to one
+    of its two bf16 neighbours, chosen so that every output channel's sum of
+    rounding errors stays near zero: round-to-nearest perturbs each output
+    channel by a fixed sum that every pixel of every image sees, and over a
+    deep stack that coherent error dominates (tools/bf16_depth_emulate.py,
+    DESIGN §3g).  Diagonal entries round to nearest and their errors (taps
+    0..8, float32) start each channel's error sum e; the pairs are then
+    visited in the round-robin order of the kernel (C-1 rounds of C/2 disjoint
+    channel pairs); within a pair (o, i), D = e_o - e_i, and per tap 0..8 the
+    upper neighbour iff D + (d_lo + d_hi) < 0, else the lower (a bf16 value
+    stays), D += 2d; then e_o += S, e_i -= S for the pair's S = sum d, all in
+    float32.  A map without the pairing (or src=None) rounds to nearest."""
+    W32 = np.asarray(W, np.float32).reshape(3, 3, W.shape[2], W.shape[3])
+    C = W32.shape[2]
+    Q = bf16_round(W32).reshape(9, C, C).copy()
+    if src is None or C % 2 or not _pairs_antisymmetric(src, sign, C):
+        return Q.reshape(W32.shape)
+    X = W32.reshape(9, C, C)
+    err = np.zeros(C, np.float32)
+    dg = np.arange(C)
+    for t in range(9):  # the error sums start from the diagonal entries' (nearest) rounding
+        err = err + (Q[t, dg, dg] - X[t, dg, dg])
+    q = np.arange(1, C // 2)
+    for r in range(C - 1):
+        a = np.concatenate([[C - 1], (r + q) % (C - 1)])
+        b = np.concatenate([[r], (r - q) % (C - 1)])
+        o, i = np.minimum(a, b), np.maximum(a, b)
+        eo, ei = err[o].copy(), err[i].copy()
+        D, S = eo - ei, np.zeros_like(eo)
+        for t in range(9):
+            x = X[t, i, o]
+            bits = x.view(np.uint32)
+            exact = (bits & np.uint32(0xFFFF)) == 0
+            dtz = (bits & np.uint32(0xFFFF0000)).view(np.float32) - x
+            daw = ((bits & np.uint32(0xFFFF0000)) + np.uint32(0x10000)).view(np.float32) - x
+            zero = np.float32(0)
+            d_lo = np.where(exact, zero, np.where(x > 0, dtz, daw)).astype(np.float32)
+            d_hi = np.where(exact, zero, np.where(x > 0, daw, dtz)).astype(np.float32)
+            sd = np.where(exact, zero, dtz + daw).astype(np.float32)
+            d = np.where(D + sd < 0, d_hi, d_lo).astype(np.float32)
+            D = (D + np.float32(2) * d).astype(np.float32)
+            S = (S + d).astype(np.float32)
+            qv = (x + d).astype(np.float32)
+            Q[t, i, o] = qv
+            Q[8 - t, o, i] = -qv
+        err[o], err[i] = eo + S, ei - S
+    return Q.reshape(W32.shape)
+
+
 def decode_mask(mask_bytes, N, H, W, C):
     """Inverse of the relu-mask layout (include/asr.h): bit (pixel*C + o),
     LSB first, pixel = (n*H + y)*W + x.  Returns bool [N,H,W,C]."""

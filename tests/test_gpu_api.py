@@ -13,7 +13,7 @@ import os
 import numpy as np
 import pytest
 
-from helpers import assert_close, bf16_round
+from helpers import assert_close, bf16_round, w_bf16_balanced
 from oracle import asr_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -42,14 +42,15 @@ def _layer_case(layer, shape, dtype, seed):
     xo = bf16_round(x_np).astype(np.float64) if bf else x_np.astype(np.float64)
     ro = bf16_round(r_np).astype(np.float64) if bf else r_np.astype(np.float64)
     Wk = layer.get_kernel().astype(np.float64)
-    Wo = bf16_round(Wk).astype(np.float64) if bf else Wk
+    src = layer.param_map().w_src
+    sign = np.where(src & 1, -1, 1)
+    osrc = np.where(src >= 0, src >> 1, -1)
+    Wo = w_bf16_balanced(Wk, osrc, sign).astype(np.float64) if bf else Wk
     bias = layer.bias.value.astype(np.float64) if layer.bias is not None else 0.0
     want_y = O.conv2d_same(xo, Wo) + bias
     want_dx = O.conv2d_backprop_input(ro, Wo, xo.shape)
     dW = O.conv2d_backprop_filter(xo, ro)
-    src = layer.param_map().w_src
-    sign = np.where(src & 1, -1, 1)
-    dth = O.project_dW(dW, np.where(src >= 0, src >> 1, -1), sign, layer.theta_flat().size)
+    dth = O.project_dW(dW, osrc, sign, layer.theta_flat().size)
     return y, x.grad, th.grad, b.grad if b is not None else None, want_y, want_dx, dth, ro.sum(axis=(0, 1, 2)), bf
 
 

@@ -16,7 +16,7 @@ Checks:
 import numpy as np
 import pytest
 
-from helpers import assert_close, bf16_round, decode_mask, rel_l2
+from helpers import assert_close, bf16_round, decode_mask, rel_l2, w_bf16_balanced
 from oracle import asr_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -60,7 +60,8 @@ def test_stack_equals_sequential_blocks_and_oracle(rt, N, L, gamma, with_bias):
     src, sign = O.param_map(16)
     xin = x0
     for l in range(L):
-        Wl = bf16_round(O.assemble_from_map(th[l].astype(np.float64), 16, src, sign, gamma)).astype(np.float64)
+        Wl = w_bf16_balanced(O.assemble_from_map(th[l].astype(np.float64), 16, src, sign, gamma), src,
+                             sign).astype(np.float64)
         xo = xin.float().cpu().numpy().astype(np.float64)
         z = O.conv2d_same(xo, Wl) + (b[l] if with_bias else 0.0)
         want = xo + h * np.maximum(z, 0)

@@ -36,7 +36,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 GROUP_TOL = 2e-2
-TENSOR_TOL = 5e-2   # per tensor, of the group's max |ref| (see helpers.assert_grad_tensors_max)
+TENSOR_TOL = 1e-2   # per tensor, of the group's max |ref| (see helpers.assert_grad_tensors_max; measured <= 7.9e-3)
 
 
 def _params(spec, init, seed):
@@ -110,18 +110,21 @@ def test_c3_full_depth_vs_oracle(N, init, seed):
     _check(*_run(16, 108, N, "euler", init, seed), tag=f"C3 L=108 N={N} {init}")
 
 
-def test_c3_bf16_weights_variant_is_the_systematic_error():
-    """ASR_VARIANT_W_BF16 (the fused C=16 forward with W in bf16 alone instead
-    of bf16 hi + lo): on the reference-init case above the 108-block net's
-    worst block gradient leaves the 2e-2 bar (measured 2.7e-2 at block 92; the
-    CPU emulation, tools/bf16_depth_emulate.py, puts 2.6e-2 of it on the W
-    rounding alone), while the default hi/lo forward measures 7e-3.  Both stay
-    within 1 % on the loss; the hi/lo error is the smaller."""
+def test_c3_nearest_rounded_weights_are_the_systematic_error():
+    """ASR_VARIANT_W_BF16 (W rounded to nearest bf16 instead of the balanced
+    pack, asr_theta.hip k_theta_to_w_pack_bal): on the reference-init case
+    above the 108-block net's worst block gradient leaves the 2e-2 bar
+    (measured 2.7e-2 at block 92; the CPU emulation, tools/bf16_depth_emulate.py,
+    puts 2.6e-2 of it on the W rounding alone: every output channel carries the
+    fixed sum of its row's rounding errors through every pixel and layer),
+    while the balanced pack, the same bf16 W with each channel's error sum
+    kept near zero, stays under it (emulated 6.8e-3).  Both within 1 % on the
+    loss; the balanced error is the smaller."""
     from differential_equations_resnet_amd.runtime import ASR_VARIANT_W_BF16
     worst = {}
     for v in (0, ASR_VARIANT_W_BF16):
         spec, loss, want_loss, probs_gpu, probs, g_got, g_want = _run(16, 108, 4, "euler", "ref", 6, variant=v)
         assert abs(loss - want_loss) <= 1e-2 * abs(want_loss)
         worst[v] = max(rel_l2(a, b) for (_, a), (_, b) in zip(grad_groups(spec, g_got), grad_groups(spec, g_want)))
-    print(f"\nC3 ref init, worst group rel-L2: hi/lo {worst[0]:.3e}, W in bf16 {worst[ASR_VARIANT_W_BF16]:.3e}")
+    print(f"\nC3 ref init, worst group rel-L2: balanced {worst[0]:.3e}, nearest {worst[ASR_VARIANT_W_BF16]:.3e}")
     assert worst[0] <= GROUP_TOL and worst[0] < worst[ASR_VARIANT_W_BF16]

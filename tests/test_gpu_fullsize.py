@@ -22,7 +22,7 @@ is checked through properties that do not depend on the size:
 import numpy as np
 import pytest
 
-from helpers import assert_close, bf16_round, decode_mask
+from helpers import assert_close, bf16_round, decode_mask, w_bf16_balanced
 from oracle import asr_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -75,7 +75,7 @@ def test_block_fullsize(rt, N, C, integrator):
         assert np.abs(f - s).max() <= 1e-5 * np.abs(f).max(), what
     # per-image spot checks against the oracle (same bf16-rounded inputs)
     src, sign = O.param_map(C)
-    Wo = bf16_round(O.assemble_from_map(th.astype(np.float64), C, src, sign, gamma)).astype(np.float64)
+    Wo = w_bf16_balanced(O.assemble_from_map(th.astype(np.float64), C, src, sign, gamma), src, sign).astype(np.float64)
     for n in (0, N - 1):
         xo = x[n:n + 1].float().cpu().numpy().astype(np.float64)
         dyo = dy[n:n + 1].float().cpu().numpy().astype(np.float64)
@@ -297,13 +297,15 @@ def test_stem_fwd_mfma_matches_fp32_path(rt, N, u8, C):
 
 def _bf16_emulated_probs(spec, params, img):
     """The notebooks' network on ONE image in float64 with the bf16 path's
-    roundings (W_l, the stem output and every x_{l+1} rounded to bf16; fp32
+    roundings (W_l in the balanced bf16 pack, the stem output and every x_{l+1}
+    rounded to bf16; fp32
     parameters otherwise): oracle.net_forward's composition, step by step."""
     conv1_k, conv1_b, blocks, fc_k, fc_b = O.split_params(spec, params)
     x = bf16_round(np.maximum(O.conv2d_same(O.normalize_input(img[None], spec), conv1_k) + conv1_b, 0))
     src, sign = O.param_map(spec.C)
     for theta, b in blocks:
-        W = bf16_round(O.assemble_from_map(O.flatten(theta), spec.C, src, sign, spec.gamma)).astype(np.float64)
+        W = w_bf16_balanced(O.assemble_from_map(O.flatten(theta), spec.C, src, sign, spec.gamma), src,
+                            sign).astype(np.float64)
         z = O.conv2d_same(x.astype(np.float64), W) + b
         x = bf16_round(x + spec.h * np.maximum(z, 0)).astype(np.float64)
     return O.softmax(x.mean(axis=(1, 2)) @ fc_k + fc_b)[0]

@@ -12,7 +12,7 @@ Masks must agree exactly wherever |z| > 1e-4 * max|z| (fp32) / 2e-2 * max|z| (bf
 import numpy as np
 import pytest
 
-from helpers import assert_close, bf16_round, decode_mask
+from helpers import assert_close, bf16_round, decode_mask, w_bf16_balanced
 from oracle import asr_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -58,6 +58,40 @@ def test_theta_to_w_multi_layer(rt):
         np.testing.assert_array_equal(W[l], want.astype(np.float32))
 
 
+def _unpack_bf16(pack, C):
+    """The MFMA W pack (include/asr.h) back to HWIO [3, 3, C, C] float32."""
+    KS = (9 * C + 31) // 32
+    o, kappa = np.meshgrid(np.arange(C), np.arange(9 * C), indexing="ij")
+    idx = (((o // 16) * KS + kappa // 32) * 64 + (o % 16) + 16 * ((kappa % 32) // 8)) * 8 + kappa % 8
+    Wt = pack[idx]  # [o, kappa = tap * C + i]
+    return Wt.reshape(C, 9, C).transpose(1, 2, 0).reshape(3, 3, C, C)
+
+
+@pytest.mark.parametrize("C,kind,anti,gamma,L", [(16, 0, True, 0.0, 3), (32, 0, True, -0.1, 2), (64, 0, True, 0.0, 2),
+                                                 (64, 1, False, 0.05, 1), (32, 1, True, 0.0, 1), (16, 2, False, 0.0, 1),
+                                                 (80, 0, True, 0.0, 1)])
+def test_theta_to_w_bf16_pack_exact(rt, C, kind, anti, gamma, L):
+    """asr_theta_to_w's bf16 pack bit for bit against helpers.w_bf16_balanced
+    (the balanced rounding of the antisymmetric pairs: 3by3 and general maps,
+    C <= 64), round-to-nearest for the regular kind and for C = 80 (above the
+    balanced kernel's LDS)."""
+    pm = rt.param_map(C, kind, anti)
+    n = pm.n_theta
+    stride = n + 8
+    flat = (np.random.default_rng(C + kind).standard_normal(L * stride) * 0.2).astype(np.float32)
+    w = rt.theta_to_w(torch.from_numpy(flat).cuda(), C, pm, gamma, rt.ASR_BF16, layers=L, theta_stride=stride)
+    packs = w.view(torch.int16).cpu().numpy().reshape(L, -1)
+    ws = pm.w_src.astype(np.int64)
+    src, sign = np.where(ws >= 0, ws >> 1, -1), np.where(ws & 1, -1, 1)
+    for l in range(L):
+        W = O.assemble_from_map(flat[l * stride:l * stride + n].astype(np.float64), C, src, sign, gamma)
+        want = w_bf16_balanced(W, src, sign) if C <= 64 else bf16_round(W)
+        got = (packs[l].astype(np.uint16).astype(np.uint32) << 16).view(np.float32)
+        np.testing.assert_array_equal(_unpack_bf16(got, C).view(np.uint32), want.view(np.uint32))
+        if kind != 2 and C <= 64:  # balanced: differs from nearest somewhere, exactly antisymmetric off the diagonal
+            assert not np.array_equal(want, bf16_round(W))
+
+
 def _run_forward(rt, mode, x_np, th, b, C, gamma, h, dtype):
     dev = torch.device("cuda")
     pm = rt.param_map(C)
@@ -74,7 +108,7 @@ def _run_forward(rt, mode, x_np, th, b, C, gamma, h, dtype):
 def _oracle_W(th, C, gamma, bf):
     src, sign = O.param_map(C)
     W = O.assemble_from_map(th.astype(np.float64), C, src, sign, gamma)
-    return bf16_round(W).astype(np.float64) if bf else W
+    return w_bf16_balanced(W, src, sign).astype(np.float64) if bf else W
 
 
 SHAPES_BF16 = [(2, 32, 32, 16), (2, 32, 32, 32), (2, 32, 32, 64), (1, 11, 32, 64), (3, 5, 32, 16)]

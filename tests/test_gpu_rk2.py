@@ -15,7 +15,7 @@ Tolerances (as test_gpu_kernels.py / test_gpu_network.py):
 import numpy as np
 import pytest
 
-from helpers import assert_close, assert_grad_groups_rel_l2, bf16_round, decode_mask
+from helpers import assert_close, assert_grad_groups_rel_l2, bf16_round, decode_mask, w_bf16_balanced
 from oracle import asr_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -61,7 +61,7 @@ def test_rk2_block_parity(rt, dtype_name, shape, gamma, h):
     src, sign = O.param_map(C)
     Wo = O.assemble_from_map(th.astype(np.float64), C, src, sign, gamma)
     q = (lambda a: bf16_round(a).astype(np.float64)) if bf else (lambda a: np.asarray(a, np.float64))
-    Wo = q(Wo)
+    Wo = w_bf16_balanced(Wo, src, sign).astype(np.float64) if bf else Wo
     xo, dyo = q(x_np), q(dy_np)
     # forward, stage by stage (stage 2 fed the GPU's midpoint)
     z1 = O.conv2d_same(xo, Wo) + b
@@ -193,7 +193,7 @@ def test_rk2_forward_multiband(rt):
     x = torch.from_numpy(x_np).to(dev).to(torch.bfloat16).contiguous()
     y, xm, m1, m2 = rt.rk2_forward(x, w, torch.from_numpy(b).to(dev), h)
     src, sign = O.param_map(C)
-    Wo = bf16_round(O.assemble_from_map(th.astype(np.float64), C, src, sign, gamma)).astype(np.float64)
+    Wo = w_bf16_balanced(O.assemble_from_map(th.astype(np.float64), C, src, sign, gamma), src, sign).astype(np.float64)
     xo = bf16_round(x_np).astype(np.float64)
     xm_want = xo + 0.5 * h * np.maximum(O.conv2d_same(xo, Wo) + b, 0)
     xm_gpu = xm.float().cpu().numpy().astype(np.float64)

@@ -17,7 +17,7 @@ Checks:
 import numpy as np
 import pytest
 
-from helpers import assert_close, bf16_round
+from helpers import assert_close, bf16_round, w_bf16_balanced
 from oracle import asr_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -57,7 +57,8 @@ def test_stack64_equals_single_blocks(rt, N, L, with_bias):
     pick = np.arange(N) if N <= 5 else np.array([0, N // 2, N - 1])
     xin = x0[pick].float().cpu().numpy().astype(np.float64)
     for l in range(L):
-        Wl = bf16_round(O.assemble_from_map(th[l].astype(np.float64), C, src, sign, 0.0)).astype(np.float64)
+        Wl = w_bf16_balanced(O.assemble_from_map(th[l].astype(np.float64), C, src, sign, 0.0), src,
+                             sign).astype(np.float64)
         z = O.conv2d_same(xin, Wl) + (b[l] if with_bias else 0.0)
         want = xin + h * np.maximum(z, 0)
         got = ys[l][pick].float().cpu().numpy()

@@ -20,7 +20,7 @@ bf16 storage rounding, and the bf16 network bar against the plain oracle.
 import numpy as np
 import pytest
 
-from helpers import assert_close, assert_grad_tensors_max, bf16_round, rel_l2
+from helpers import assert_close, assert_grad_tensors_max, bf16_round, rel_l2, w_bf16_balanced
 from oracle import asr_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -221,18 +221,6 @@ def _stage_groups(spec, g):
     return [(name, np.concatenate([np.ravel(g[j]) for j in idx])) for name, idx in _stage_group_indices(spec)]
 
 
-def _hilo_stages(spec):
-    """Stages the executor runs on the fused C=16 kernels (asr_stages.hip: a bf16 stage at C=16,
-    32 x 32 with blocks), whose forward takes W as bf16 hi + lo (k_fwd16_fused<.., LO>)."""
-    out, H = set(), spec.H
-    for si, (C, L, S) in enumerate(spec.stages):
-        if S:
-            H = -(-H // S)
-        if C == 16 and H == 32 and spec.W == 32 and L > 0:
-            out.add(si)
-    return out
-
-
 def _bf16_net_errors(ex, spec, params, imgs, onehot, rnd=None):
     """(max |probs - oracle|, |loss - oracle| / oracle, {layer: grad rel-L2})
     of the bf16 executor vs the fp64 oracle (rnd: the oracle's bf16 storage
@@ -240,7 +228,7 @@ def _bf16_net_errors(ex, spec, params, imgs, onehot, rnd=None):
     flat = _t(O.flatten(params))
     assert flat.numel() == ex.n_params == spec.n_params()
     probs_gpu = ex.forward(flat, torch.from_numpy(imgs).cuda()).cpu().numpy()
-    probs, cache = O.stages_forward(spec, params, imgs, rnd=rnd, w_hilo_stages=_hilo_stages(spec) if rnd else ())
+    probs, cache = O.stages_forward(spec, params, imgs, rnd=rnd, rnd_w=w_bf16_balanced if rnd else None)
     loss, grads = ex.forward_backward(flat, torch.from_numpy(imgs).cuda(), _t(onehot), want_probs=True)
     assert np.array_equal(ex.probs.cpu().numpy(), probs_gpu)  # the training call's forward is the same kernels
     want_loss = O.net_loss(probs, onehot)
@@ -253,10 +241,10 @@ def _bf16_net_errors(ex, spec, params, imgs, onehot, rnd=None):
 
 def _assert_bf16_net(ex, spec, params, imgs, onehot):
     """Two bars.  (1) Against the oracle with the executor's bf16 storage
-    rounding (helpers.bf16_round at every stored activation, chain gradient
-    and block W; the C=16 32x32 stage's forward with the unrounded W, as its
-    hi/lo kernel): what remains is fp32 accumulation order and the bf16
-    roundings it flips -- probabilities within 2e-3, loss within 1e-3
+    rounding (helpers.bf16_round at every stored activation and chain
+    gradient, helpers.w_bf16_balanced for the blocks' W): what remains is
+    fp32 accumulation order and the bf16 roundings it flips -- probabilities
+    within 2e-3, loss within 1e-3
     relative, every layer's gradient within 2e-2 relative L2.
     (2) Against the plain fp64 oracle (the reference's math): probabilities
     within 2e-2, loss within 1e-2 relative, and every layer's gradient within

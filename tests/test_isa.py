@@ -65,10 +65,7 @@ SPILL_ALLOW = {
     r"k_bwd16_fusedILb1E": (12, 36, "its gamma != 0 instantiation (+ the dz tile term)"),
     r"k_bwd3ILi64ELi32ELi4ELi2ELb0ELb1E": (4, 20, "per-block backward, first RK2 stage (extra dx term in registers)"),
     r"k_fwd3_stack": (0, 0, "forward stack: no spills"),
-    r"k_fwd16_fusedILb[01]ELb[01]ELb0E|k_fwd16_fusedILb0ELb0ELb1E": (0, 0, "fused C=16 forward: no spills"),
-    r"k_fwd16_fusedILb1ELb1ELb1E": (8, 36, "its hi/lo-weight training instantiation (2 x 5 more A fragments): two "
-                                          "16-B spills of per-image set-up, reloaded once per image outside the "
-                                          "layer loop"),
+    r"k_fwd16_fused": (0, 0, "fused C=16 forward: no spills"),
     r"k_fwd3I": (0, 0, "per-block forward: no spills"),
     r"k_bwd3ILi64ELi32ELi4ELi[23]ELb[01]ELb0E": (0, 0, "per-block backward (Euler, conv, relu'): no spills"),
 }

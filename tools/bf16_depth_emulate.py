@@ -8,7 +8,8 @@ precision fix for the C3 (L=108, C=16) failure in tests/test_gpu_depth.py.
 Rounding points (each switchable):
   xs  the residual stream x_{l+1} = x_l + h relu(z) rounded to bf16 every block
   xc  the conv operand (bf16 copy of x_l fed to the MFMA)
-  w   the assembled W in bf16
+  w   the assembled W in bf16: to nearest (w=1) or the executor's balanced
+      pack (w='bal', helpers.w_bf16_balanced, asr_theta.hip)
   dz  the MFMA operand dz = h dy [z>0] in bf16
   dx  the chain gradient rounded to bf16 every `seg` blocks (deep16: 8)
 
@@ -20,18 +21,20 @@ import numpy as np
 
 sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
 sys.path.insert(0, __file__.rsplit("/tools/", 1)[0] + "/tests")
-from helpers import bf16_round, grad_groups, rel_l2  # noqa: E402
+from helpers import bf16_round, grad_groups, rel_l2, w_bf16_balanced  # noqa: E402
 from oracle import asr_oracle as O  # noqa: E402
 
 
 def run(spec, params, imgs, onehot, xs=False, xc=False, w=False, dz=False, dx=False, seg=8):
     R = lambda on: (lambda a: bf16_round(a).astype(np.float64)) if on else (lambda a: a)  # noqa: E731
     rxs, rxc, rw, rdz, rdx = R(xs), R(xc), R(w), R(dz), R(dx)
+    src, sign = O.param_map(spec.C)
+    if w == "bal":
+        rw = lambda a: w_bf16_balanced(a, src, sign).astype(np.float64)  # noqa: E731
     conv1_k, conv1_b, blocks, fc_k, fc_b = O.split_params(spec, params)
     x0 = O.normalize_input(imgs, spec)
     z1 = O.conv2d_same(x0, conv1_k) + conv1_b
     x = rxs(np.maximum(z1, 0))
-    src, sign = O.param_map(spec.C)
     cache = []
     for theta, b in blocks:
         W = rw(O.assemble_from_map(O.flatten(theta), spec.C, src, sign, spec.gamma))
@@ -74,6 +77,8 @@ def main():
     onehot = np.eye(10)[rng.integers(0, 10, N)]
     p0, g0 = run(spec, params, imgs, onehot)
     for name, kw in [("all (xs xc w dz dx/8)", dict(xs=1, xc=1, w=1, dz=1, dx=1)),
+                     ("all, W balanced (the executor)", dict(xs=1, xc=1, w="bal", dz=1, dx=1)),
+                     ("W balanced only", dict(w="bal")),
                      ("fp32 residual stream (xc w dz dx/8)", dict(xc=1, w=1, dz=1, dx=1)),
                      ("residual only (xs)", dict(xs=1)), ("conv operand only (xc)", dict(xc=1)),
                      ("W only", dict(w=1)), ("dz only", dict(dz=1)), ("dx/8 only", dict(dx=1)),
