@@ -44,6 +44,9 @@ probs, cache = O.stages_forward(spec, params, imgs)
 g_plain = O.stages_backward(spec, params, cache, onehot)
 probs_s, cache_s = O.stages_forward(spec, params, imgs, rnd=bf16_round, rnd_w=w_bf16_balanced)
 g_store = O.stages_backward(spec, params, cache_s, onehot)
+# round 5's executor rounded W to nearest (r05k ran that)
+probs_n, cache_n = O.stages_forward(spec, params, imgs, rnd=bf16_round)
+g_near = O.stages_backward(spec, params, cache_n, onehot)
 
 # which block / output channel owns each tensor index (general kind, O.theta_shapes_general: per
 # output o its diagonal-block scalars, then its [3,3,C-o-1,1] kernel; then the block's bias)
@@ -64,10 +67,12 @@ for si, (C, L, S) in enumerate(spec.stages):
         bi += 1
 ops = [op for op in cache["ops"] if op[0] == "b"]
 ops_s = [op for op in cache_s["ops"] if op[0] == "b"]
+ops_n = [op for op in cache_n["ops"] if op[0] == "b"]
 for k in a.idx:
     si, b, bi, o, shp = owner[k]
-    z, zs = ops[bi][2][..., o], ops_s[bi][2][..., o]
+    z, zs, zn = ops[bi][2][..., o], ops_s[bi][2][..., o], ops_n[bi][2][..., o]
     print(f"grad[{k}] {shp}: stage {si} block {b}, output channel {o}: GPU {float(np.ravel(g_got[k])[0]):+.3e}  "
-          f"fp64 {float(np.ravel(g_plain[k])[0]):+.3e}  bf16-storage {float(np.ravel(g_store[k])[0]):+.3e}  |  "
-          f"channel z: fp64 max {z.max():+.3e} ({int((z > 0).sum())} px > 0), bf16-storage max {zs.max():+.3e} "
-          f"({int((zs > 0).sum())} px > 0)")
+          f"fp64 {float(np.ravel(g_plain[k])[0]):+.3e}  bf16-storage {float(np.ravel(g_store[k])[0]):+.3e}  "
+          f"bf16-storage with W to nearest (round 5) {float(np.ravel(g_near[k])[0]):+.3e}  |  channel z max "
+          f"(px > 0): fp64 {z.max():+.3e} ({int((z > 0).sum())}), bf16-storage {zs.max():+.3e} ({int((zs > 0).sum())}), "
+          f"W to nearest {zn.max():+.3e} ({int((zn > 0).sum())})")

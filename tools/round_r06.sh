@@ -1,12 +1,16 @@
 #!/bin/bash
-# Round-6 evidence in one GPU call: GPU suite, smoke, the default bench line,
-# rocprofv3 kernel stats + per-step breakdown of the same command, the other
-# configs' bench lines, one PMC clock pass, PMC HBM traffic and counters of the
-# stacked C=64 kernels.  Stops at the first failing step.  usage: tools/round_r06.sh TAG
+# Round-6 evidence in two GPU calls (each under gpurun's 20-minute limit).
+# Part a: GPU suite, smoke, the default bench line, rocprofv3 kernel stats +
+# per-step breakdowns (C2, he32_bf16, C3), the full-depth parity log, the r05k
+# reproduction.  Part b: the other configs' bench lines, one PMC clock pass,
+# PMC HBM traffic and counters of the stacked C=64 kernels.  Stops at the
+# first failing step.  usage: tools/round_r06.sh TAG a|b
 set -o pipefail
 TAG=$1
+PART=$2
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+if [ "$PART" = a ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 180 --timeout-method thread -p no:cacheprovider -rfEs > gpurun_out/test_$TAG.log 2>&1; rc=$?; tail -3 gpurun_out/test_$TAG.log; [ $rc -le 1 ] || exit $rc
 grep -E "FAILED|ERROR" gpurun_out/test_$TAG.log | head -10
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { echo SMOKE FAILED; tail -5 gpurun_out/smoke_$TAG.log; exit 1; }
@@ -24,6 +28,9 @@ timeout -k 10 300 python -u -m pytest -q -s --timeout 250 --timeout-method threa
 grep -E "^C[235]|balanced" gpurun_out/depth_$TAG.log
 timeout -k 10 200 python tools/r05k_dead_channel.py > gpurun_out/r05k_$TAG.txt 2>&1 || { echo R05K FAILED; tail -5 gpurun_out/r05k_$TAG.txt; exit 1; }
 cat gpurun_out/r05k_$TAG.txt
+fi
+if [ "$PART" = b ]; then
+timeout -k 10 200 python tools/r05k_dead_channel.py > gpurun_out/r05k_${TAG}b.txt 2>&1 || { echo R05K FAILED; tail -5 gpurun_out/r05k_${TAG}b.txt; exit 1; }
 for cfg in he32_bf16 he32 c2_eval c5 c3 c1 c2_f32 v6 v7_predict; do
   timeout -k 10 600 python3 bench.py --config $cfg --no-cpu-baseline > gpurun_out/bench_${TAG}_$cfg.json 2> gpurun_out/bench_${TAG}_$cfg.err || { echo "BENCH $cfg FAILED"; tail -5 gpurun_out/bench_${TAG}_$cfg.err; exit 1; }
   python3 -c "import json; d=json.load(open('gpurun_out/bench_${TAG}_$cfg.json')); r=d['roofline']; print('$cfg', d['value'], d['ms_per_step'], r['frac'], {k: v.get('avg_us') for k, v in r.get('kernels', {}).items()})"
@@ -31,3 +38,4 @@ done
 bash tools/clock_pass.sh $TAG c2 || exit 1
 TRAFFIC_BLOCKS=30 bash tools/traffic.sh $TAG c2 --reps 3 --stack 30 || exit 1
 bash tools/pmc.sh $TAG --reps 3 --stack 30 || exit 1
+fi
