@@ -2129,8 +2129,10 @@ __global__ __launch_bounds__(768, 1) void k_bwd3(const bf16* __restrict__ dy, co
       unsigned mwv = 0u;
       // the next band's DMA pieces of this wave: own dy row (waves 0-3, or 0-5 when
       // the next band starts an image), x rows (waves 4-7; rows 2.. when it
-      // continues this band's image); issued kBwd3Dma0 at once, the rest one
-      // after each of the first rows' MFMAs (a piece among MFMAs issues cheaper)
+      // continues this band's image); the first kBwd3Dma0 pieces issued here, the
+      // rest after the band's MFMAs (below; the per-row interleave among the MFMAs
+      // went with the round-5 cleanup d41213d, and this per-block path's speed was
+      // not re-measured: the networks run the stacked kernels)
       if constexpr (EULER) {
         if (orow >= 0) mwv = bwd2_mask_word<C, W>(mask, nxt.n, nxt.b * BR, orow, H, lane);
       }
