@@ -289,6 +289,7 @@ __global__ __launch_bounds__(256) void k_sum_chunks(const float* __restrict__ pa
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (e < E) {
     int c = sl;
+#pragma unroll 4  // (unrolled, the later iterations' loads issue before the earlier adds: same sums)
     for (; c + 12 < chunks; c += 16) {
       a0 += part[(long)c * E + e];
       a1 += part[(long)(c + 4) * E + e];

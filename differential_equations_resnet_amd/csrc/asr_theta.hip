@@ -531,22 +531,43 @@ int theta_to_w_bf16_jobs(const PackJob* jobs, int njobs, hipStream_t s) {
 // device: split-K reduction of fp32 slabs and the theta projection
 // ---------------------------------------------------------------------------
 
+// The sum of rows [p0, p1) of a slab column (stride E): four accumulators taking rows
+// p0 + 4k + j in turn, the remainder into the first, (a0 + a1) + (a2 + a3): a fixed order
+// (deterministic).  A full group of 32 rows issues all its loads before the first add
+// (a rolled loop kept four in flight: latency-bound at C3's 27648 slab rows).
+__device__ __forceinline__ float sum_slab_rows(const float* __restrict__ src, long E, long e, int p0, int p1) {
+  float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+  if (p1 - p0 == 32) {
+    float v[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) v[k] = src[(long)(p0 + k) * E + e];
+#pragma unroll
+    for (int k = 0; k < 32; k += 4) {
+      acc0 += v[k];
+      acc1 += v[k + 1];
+      acc2 += v[k + 2];
+      acc3 += v[k + 3];
+    }
+    return (acc0 + acc1) + (acc2 + acc3);
+  }
+  int p = p0;
+  for (; p + 3 < p1; p += 4) {
+    acc0 += src[(long)p * E + e];
+    acc1 += src[(long)(p + 1) * E + e];
+    acc2 += src[(long)(p + 2) * E + e];
+    acc3 += src[(long)(p + 3) * E + e];
+  }
+  for (; p < p1; ++p) acc0 += src[(long)p * E + e];
+  return (acc0 + acc1) + (acc2 + acc3);
+}
+
 // out[g][e] = sum_{p in [g*per, min((g+1)*per, P))} in[p][e]   (deterministic)
 __global__ void k_reduce_slabs(const float* __restrict__ in, long E, int P, int per, float* __restrict__ out) {
   const long e = blockIdx.x * (long)blockDim.x + threadIdx.x;
   const int g = blockIdx.y;
   if (e >= E) return;
   const int p0 = g * per, p1 = min(P, p0 + per);
-  float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-  int p = p0;
-  for (; p + 3 < p1; p += 4) {
-    acc0 += in[(long)p * E + e];
-    acc1 += in[(long)(p + 1) * E + e];
-    acc2 += in[(long)(p + 2) * E + e];
-    acc3 += in[(long)(p + 3) * E + e];
-  }
-  for (; p < p1; ++p) acc0 += in[(long)p * E + e];
-  out[(long)g * E + e] = (acc0 + acc1) + (acc2 + acc3);
+  out[(long)g * E + e] = sum_slab_rows(in, E, e, p0, p1);
 }
 
 // dtheta[j] = sum over the (<=2) W entries theta j feeds of sign * dW[e],
@@ -724,16 +745,7 @@ __global__ void k_reduce_slabs_layers(const float* __restrict__ in, long slab_st
   if (e >= E) return;
   const float* src = in + blockIdx.z * slab_stride;
   const int p0 = g * per, p1 = min(P, p0 + per);
-  float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-  int p = p0;
-  for (; p + 3 < p1; p += 4) {
-    acc0 += src[(long)p * E + e];
-    acc1 += src[(long)(p + 1) * E + e];
-    acc2 += src[(long)(p + 2) * E + e];
-    acc3 += src[(long)(p + 3) * E + e];
-  }
-  for (; p < p1; ++p) acc0 += src[(long)p * E + e];
-  out[blockIdx.z * out_stride + (long)g * E + e] = (acc0 + acc1) + (acc2 + acc3);
+  out[blockIdx.z * out_stride + (long)g * E + e] = sum_slab_rows(src, E, e, p0, p1);
 }
 
 int reduce_slab_layers(const float* slabs, long slab_stride, int P, long ES, float* grp, long grp_stride, int L,
