@@ -324,9 +324,34 @@ __device__ __forceinline__ void st4(float* p, f32x4 v) { *(f32x4*)p = v; }
 __device__ __forceinline__ void st4(bf16* p, f32x4 v) {
   *(uint2*)p = make_uint2(pk_bf16_rn(v[0], v[1]), pk_bf16_rn(v[2], v[3]));
 }
-__device__ __forceinline__ f32x4 mask4(const uint8_t* m) {
-  const unsigned u = *(const unsigned*)m;
+__device__ __forceinline__ f32x4 mask4u(unsigned u) {
   return f32x4{(float)(u & 0xff), (float)((u >> 8) & 0xff), (float)((u >> 16) & 0xff), (float)(u >> 24)};
+}
+__device__ __forceinline__ f32x4 mask4(const uint8_t* m) { return mask4u(*(const unsigned*)m); }
+
+// Stage TOTAL 16-B elements with NT threads into LDS, BS at a time: load(i, v, m) fills an
+// element (v and m zero unless it loads), store(i, v, m) writes it.  All BS loads issue
+// before the first store (a rolled load-then-store loop waits for each load in turn).
+template <int TOTAL, int NT, typename LoadF, typename StoreF>
+__device__ __forceinline__ void stage_batched(int tid, LoadF load, StoreF store) {
+  constexpr int NI = (TOTAL + NT - 1) / NT, BS = 4;
+#pragma unroll
+  for (int k0 = 0; k0 < NI; k0 += BS) {
+    f32x4 v[BS];
+    unsigned m[BS];
+#pragma unroll
+    for (int k = 0; k < BS; ++k) {
+      v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      m[k] = 0u;
+      const int i = tid + (k0 + k) * NT;
+      if (k0 + k < NI && i < TOTAL) load(i, v[k], m[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < BS; ++k) {
+      const int i = tid + (k0 + k) * NT;
+      if (k0 + k < NI && i < TOTAL) store(i, v[k], m[k]);
+    }
+  }
 }
 
 // forward: D[o][xo] over (tap, i) + the 1x1 shortcut; wave = (n, yo, 16 xo, 16 o)
@@ -544,24 +569,27 @@ __global__ __launch_bounds__(512) void k_trans_wgrad_lds(const T* __restrict__ d
     const int n = (int)(item / nb), yo0 = (int)(item % nb) * BRO;
     const int rows = min(BRO, Ho - yo0);
     __syncthreads();  // the previous band's operands consumed
-    for (int i = tid; i < G::XR * TW * (CI / 4); i += 512) {
+    // (staged BS elements at a time, all loads before their stores: a rolled loop waited for each)
+    stage_batched<G::XR * TW * (CI / 4), 512>(tid, [&](int i, f32x4& v, unsigned&) {
       const int j = i / (TW * (CI / 4)), rem = i % (TW * (CI / 4)), col = rem / (CI / 4), c4 = rem % (CI / 4);
       const int gy = 2 * yo0 + j;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (gy < H && col < W) v = ld4(x + (((long)n * H + gy) * W + col) * CI + 4 * c4);
+    }, [&](int i, const f32x4& v, unsigned) {
+      const int j = i / (TW * (CI / 4)), rem = i % (TW * (CI / 4)), col = rem / (CI / 4), c4 = rem % (CI / 4);
       *(f32x4*)(xt + (j * TW + col) * XS + 4 * c4) = v;
-    }
-    for (int i = tid; i < G::NPX * (CO / 4); i += 512) {
+    });
+    stage_batched<G::NPX * (CO / 4), 512>(tid, [&](int i, f32x4& v, unsigned& m) {
       const int k = i / (CO / 4), c4 = i % (CO / 4);
-      f32x4 v = {0.f, 0.f, 0.f, 0.f}, z = {0.f, 0.f, 0.f, 0.f};
       if (k / WO < rows) {
         const long e = (((long)n * Ho + yo0) * WO + k) * CO + 4 * c4;
         v = ld4(dy + e);
-        z = v * mask4(mask + e);
+        m = *(const unsigned*)(mask + e);
       }
+    }, [&](int i, const f32x4& v, unsigned m) {
+      const int k = i / (CO / 4), c4 = i % (CO / 4);
       *(f32x4*)(dyt + k * DS + 4 * c4) = v;
-      *(f32x4*)(dzt + k * DS + 4 * c4) = z;
-    }
+      *(f32x4*)(dzt + k * DS + 4 * c4) = v * mask4u(m);
+    });
     __syncthreads();
     const int steps = rows * WO / 4;
     for (int st = rs; st < steps; st += G::RS) {
@@ -662,13 +690,14 @@ __global__ __launch_bounds__((64 * TFw<CI, CO, WO>::NW)) void k_trans_fwd_lds(
   for (long item = i0; item < i1; ++item) {
     const int n = (int)(item / nb), yo0 = (int)(item % nb) * BRO;
     __syncthreads();  // the previous band's rows consumed
-    for (int e = tid; e < G::XR * TW * (CI / 4); e += 64 * G::NW) {
+    stage_batched<G::XR * TW * (CI / 4), 64 * G::NW>(tid, [&](int e, f32x4& v, unsigned&) {
       const int j = e / (TW * (CI / 4)), rem = e % (TW * (CI / 4)), col = rem / (CI / 4), c4 = rem % (CI / 4);
       const int gy = 2 * yo0 + j;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (gy < H && col < W) v = ld4(x + (((long)n * H + gy) * W + col) * CI + 4 * c4);
+    }, [&](int e, const f32x4& v, unsigned) {
+      const int j = e / (TW * (CI / 4)), rem = e % (TW * (CI / 4)), col = rem / (CI / 4), c4 = rem % (CI / 4);
       *(f32x4*)(lds_tf + (j * TW + col) * PX + 4 * c4) = v;
-    }
+    });
     __syncthreads();
     f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accs = {0.f, 0.f, 0.f, 0.f};
     const float* xb = lds_tf + ((2 * r) * TW + 2 * xo) * PX + 4 * g;
@@ -789,18 +818,19 @@ __global__ __launch_bounds__(512) void k_trans_dgrad_lds(const T* __restrict__ d
   for (long item = i0; item < i1; ++item) {
     const int n = (int)(item / nb), gy0 = (int)(item % nb) * BR, yb = gy0 / 2 - 1;  // staged source row 0 = yo yb
     __syncthreads();  // the previous band's operands consumed
-    for (int e = tid; e < G::SR * SC * (CO / 4); e += 512) {
+    stage_batched<G::SR * SC * (CO / 4), 512>(tid, [&](int e, f32x4& v, unsigned& m) {
       const int j = e / (SC * (CO / 4)), rem = e % (SC * (CO / 4)), c = rem / (CO / 4), c4 = rem % (CO / 4);
       const int yo = yb + j, xo = c - 1;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f}, z = {0.f, 0.f, 0.f, 0.f};
       if (yo >= 0 && yo < Ho && xo >= 0) {
         const long off = (((long)n * Ho + yo) * WO + xo) * CO + 4 * c4;
         v = ld4(dy + off);
-        z = v * mask4(mask + off);
+        m = *(const unsigned*)(mask + off);
       }
+    }, [&](int e, const f32x4& v, unsigned m) {
+      const int j = e / (SC * (CO / 4)), rem = e % (SC * (CO / 4)), c = rem / (CO / 4), c4 = rem % (CO / 4);
       *(f32x4*)(dyt + (j * SC + c) * PS + 4 * c4) = v;
-      *(f32x4*)(dzt + (j * SC + c) * PS + 4 * c4) = z;
-    }
+      *(f32x4*)(dzt + (j * SC + c) * PS + 4 * c4) = v * mask4u(m);
+    });
     __syncthreads();
     for (int tk = wi; tk < G::TPB; tk += G::WPI) {  // (wave-uniform)
       const int pxp = tk & 1, rg = tk >> 1;          // column parity, row group
