@@ -1296,15 +1296,29 @@ __global__ __launch_bounds__((StImg<C, W>::NTH)) void k_stageb(const bf16* __res
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
         A[ks] = *(const bf16x8*)(wpack + (long)l * w_stride + (((long)ot * KS + ks) * 64 + lane) * 8);
-      st_barrier();  // dy of layer l complete (loaded, or the previous layer's dx); dz free
+      // layer l's relu bits, loaded before the barrier (a byte load per chunk inside the loop below
+      // waited for each in turn)
       const uint8_t* ml = masks + (long)l * mask_stride;
+      constexpr int NPT = (G::NCH + G::NTH - 1) / G::NTH;
+      unsigned mb[IPW][NPT];
+#pragma unroll
+      for (int im = 0; im < IPW; ++im)
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+          const int i = tid + k * G::NTH;
+          mb[im][k] = (im < nimg && i < G::NCH) ? ml[((long)(n0 + im) * G::H * W * C + 8L * i) >> 3] : 0u;
+        }
+      st_barrier();  // dy of layer l complete (loaded, or the previous layer's dx); dz free
       for (int im = 0; im < nimg; ++im) {
         const long ib = (long)(n0 + im) * G::H * W * C;
-        for (int i = tid; i < G::NCH; i += G::NTH) {
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+          const int i = tid + k * G::NTH;
+          if (i >= G::NCH) break;
           const int px = i / G::C8, c8 = i % G::C8;
           const uint4 v = *(const uint4*)(dyb(im) + px * G::PS + 8 * c8);
           *(uint4*)(dys + (long)l * d_stride + ib + 8L * i) = v;  // the gradient entering layer l (its wgrad's dy)
-          *(uint4*)(dzb(im) + st_off<C, W>(px / W, px % W) + 8 * c8) = mask8_bf16(v, ml[(ib + 8L * i) >> 3]);
+          *(uint4*)(dzb(im) + st_off<C, W>(px / W, px % W) + 8 * c8) = mask8_bf16(v, mb[im][k]);
         }
       }
       st_barrier();  // dz complete
@@ -1482,13 +1496,29 @@ __global__ __launch_bounds__((StImg32<C, W>::NTH)) void k_stageb32(const float* 
     for (int i = tid; i < G::NCH; i += G::NTH)
       *(f32x4*)(dyt + (i / (C / 4)) * PS + 4 * (i % (C / 4))) = *(const f32x4*)(dyL + ib + 4L * i);
     for (int l = L - 1; l >= 0; --l) {
-      st_barrier();  // dy of layer l complete; dz free
+      // layer l's relu bytes, loaded before the barrier (a byte load per chunk inside the loop below
+      // waited for each in turn)
       const uint8_t* ml = masks + (long)l * mask_stride;
-      for (int i = tid; i < G::NCH; i += G::NTH) {
+      constexpr int NPT = (G::NCH + G::NTH - 1) / G::NTH;
+      unsigned mb[NPT];
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const int i = tid + k * G::NTH;
+        mb[k] = i < G::NCH ? ml[(ib + 4L * i) >> 3] : 0u;
+      }
+      st_barrier();  // dy of layer l complete; dz free
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const int i = tid + k * G::NTH;
+        if (i >= G::NCH) break;
         const int px = i / (C / 4), c4 = i % (C / 4);
         const f32x4 v = *(const f32x4*)(dyt + px * PS + 4 * c4);
         *(f32x4*)(dys + (long)l * d_stride + ib + 4L * i) = v;  // the gradient entering layer l (its wgrad's dy)
-        *(f32x4*)(dzt + st32_off<C, W>(px / W, px % W) + 4 * c4) = masked_dz4(v, ml, ib + 4L * i, h);
+        const unsigned nib = mb[k] >> ((ib + 4L * i) & 7);  // (masked_dz4's bits: pixel * C + channel)
+        f32x4 z;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) z[j] = ((nib >> j) & 1u) ? h * v[j] : 0.f;
+        *(f32x4*)(dzt + st32_off<C, W>(px / W, px % W) + 4 * c4) = z;
       }
       const float* wl = w + (long)l * w_stride;
       float A[9][OQ][4];
