@@ -225,6 +225,7 @@ __device__ __forceinline__ void f32_stage_rows(const Ts* __restrict__ src, float
   for (int k0 = 0; k0 < NIT; k0 += B) {
     f32x4 v[B];
     long ev[B];
+    unsigned mb[B];  // the relu byte of each element (with dmask), loaded beside its values
 #pragma unroll
     for (int k = 0; k < B; ++k) {
       const int i = tid + (k0 + k) * NT;
@@ -232,9 +233,11 @@ __device__ __forceinline__ void f32_stage_rows(const Ts* __restrict__ src, float
       const int gy = y0 - 1 + r, gx = col - 1;
       v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
       ev[k] = -1;
+      mb[k] = 0u;
       if (k0 + k < NIT && i < NCH && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)G::W) {
         ev[k] = (((long)n * H + gy) * G::W + gx) * C + 4 * c4;
         v[k] = load4f(src + ev[k]);
+        if (dmask) mb[k] = dmask[ev[k] >> 3];
       }
     }
 #pragma unroll
@@ -242,7 +245,11 @@ __device__ __forceinline__ void f32_stage_rows(const Ts* __restrict__ src, float
       const int i = tid + (k0 + k) * NT;
       if (k0 + k < NIT && i < NCH) {
         const int r = i / (G::TW * C4), rem = i % (G::TW * C4), col = rem / C4, c4 = rem % C4;
-        if (dmask && ev[k] >= 0) v[k] = masked_dz4(v[k], dmask, ev[k], dh);
+        if (dmask && ev[k] >= 0) {  // (masked_dz4 on the preloaded byte: dz = dh dy [relu bit])
+          const unsigned nib = mb[k] >> (ev[k] & 7);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[k][j] = ((nib >> j) & 1u) ? dh * v[k][j] : 0.f;
+        }
         *(f32x4*)(tile + (r * G::TW + col) * PS + 4 * c4) = v[k];
       }
     }
