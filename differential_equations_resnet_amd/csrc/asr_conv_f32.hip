@@ -726,26 +726,6 @@ __device__ __forceinline__ uint4 mask8_bf16(uint4 v, unsigned bits) {
   return v;
 }
 
-// rows y0-1 .. y0+BR of image n into the bf16 tile (zeros outside the image and in the halo
-// columns), 16 B (8 channels) per thread and step; with dmask, src is dy and the tile gets dz = dy & mask
-template <int C, int W>
-__device__ __forceinline__ void bf_stage_rows(const bf16* __restrict__ src, bf16* tile, int n, int y0, int H, int tid,
-                                              const uint8_t* __restrict__ dmask) {
-  using G = BfBand<C, W>;
-  constexpr int C8 = C / 8, NCH = (G::BR + 2) * G::TW * C8;
-  for (int i = tid; i < NCH; i += 256) {
-    const int r = i / (G::TW * C8), rem = i % (G::TW * C8), col = rem / C8, c8 = rem % C8;
-    const int gy = y0 - 1 + r, gx = col - 1;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W) {
-      const long e = (((long)n * H + gy) * W + gx) * C + 8 * c8;
-      v = *(const uint4*)(src + e);
-      if (dmask) v = mask8_bf16(v, dmask[e >> 3]);  // (bit index pixel*C + channel: a byte per 8 channels)
-    }
-    *(uint4*)(tile + (r * G::TW + col) * C + 8 * c8) = v;
-  }
-}
-
 template <int C, int W, int MODE>
 __global__ __launch_bounds__(256) void k_convb(const bf16* __restrict__ xin, bf16* __restrict__ out,
                                                uint8_t* __restrict__ mask, const bf16* __restrict__ wpack,
@@ -1079,7 +1059,9 @@ static int launch_wgradb(const bf16* x, const bf16* dy, const uint8_t* mask, int
   using G = WgB<C, W>;
   const long items = (long)N * ((H + G::BR - 1) / G::BR);
   // at most the fp32 wgrad's grid: the rows the workspaces size per block (f32_block_slab_rows)
-  constexpr int minb = C == 16 ? 1 : C == 32 ? 8 : 32;  // bands per workgroup (profiles/r05_he32_bf16_ab.txt)
+  // bands per workgroup (profiles/r05_he32_bf16_ab.txt; re-measured after this round's reductions:
+  // profiles/r06ai_wgradb_grid_ab.txt)
+  constexpr int minb = C == 16 ? 1 : C == 32 ? 8 : 32;
   const int grid = (int)std::max<long>(1, std::min<long>((items + minb - 1) / minb, wgrad32_grid<C, W>(N, H)));
   hipLaunchKernelGGL((k_wgradb<C, W, MASKED>), dim3(grid, layers), dim3(G::NTH), G::LDS, s, x, dy, mask, N, H, h, slabs,
                      x_stride, dy_stride, m_stride, s_stride);
@@ -1182,6 +1164,24 @@ __device__ __forceinline__ void st_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// an image's NCH 16-B chunks from global into LDS, put(i, v) storing chunk i: every load of a thread
+// issued before its first store (a load-store loop waited for each load in turn)
+template <int NCH, int NTH, typename V, typename T, typename Put>
+__device__ __forceinline__ void st_fetch_image(const T* __restrict__ src, int tid, Put put) {
+  constexpr int NPT = (NCH + NTH - 1) / NTH, EPC = 16 / (int)sizeof(T);
+  V v[NPT];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int i = tid + k * NTH;
+    if (i < NCH) v[k] = *(const V*)(src + (long)EPC * i);
+  }
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int i = tid + k * NTH;
+    if (i < NCH) put(i, v[k]);
+  }
+}
+
 constexpr int kStIpw = 1;
 // IPW images per workgroup: 1 (a wave's two MFMA chains are two tiles of the image); 2 (the chains are
 // one tile of each image, the layer's A fragments shared) measured -7 % (r05ar: half the workgroups)
@@ -1203,10 +1203,11 @@ __global__ __launch_bounds__((StImg<C, W>::NTH)) void k_stagef(const bf16* __res
     const int nimg = min(IPW, N - n0);  // (uniform)
     for (int im = 0; im < nimg; ++im) {
       const long ib = (long)(n0 + im) * G::H * W * C;
-      for (int i = tid; i < G::NCH; i += G::NTH) {
+      bf16* dst = imgb(im, 0);
+      st_fetch_image<G::NCH, G::NTH, uint4>(x0 + ib, tid, [&](int i, const uint4& v) {
         const int px = i / G::C8, c8 = i % G::C8;
-        *(uint4*)(imgb(im, 0) + st_off<C, W>(px / W, px % W) + 8 * c8) = *(const uint4*)(x0 + ib + 8L * i);
-      }
+        *(uint4*)(dst + st_off<C, W>(px / W, px % W) + 8 * c8) = v;
+      });
     }
     st_barrier();
     for (int l = 0; l < L; ++l) {
@@ -1295,8 +1296,10 @@ __global__ __launch_bounds__((StImg<C, W>::NTH)) void k_stageb(const bf16* __res
     st_barrier();  // (the previous images' dx read out)
     for (int im = 0; im < nimg; ++im) {
       const long ib = (long)(n0 + im) * G::H * W * C;
-      for (int i = tid; i < G::NCH; i += G::NTH)
-        *(uint4*)(dyb(im) + (i / G::C8) * G::PS + 8 * (i % G::C8)) = *(const uint4*)(dyL + ib + 8L * i);
+      bf16* dst = dyb(im);
+      st_fetch_image<G::NCH, G::NTH, uint4>(dyL + ib, tid, [&](int i, const uint4& v) {
+        *(uint4*)(dst + (i / G::C8) * G::PS + 8 * (i % G::C8)) = v;
+      });
     }
     for (int l = L - 1; l >= 0; --l) {
       bf16x8 A[KS];
@@ -1421,10 +1424,10 @@ __global__ __launch_bounds__((StImg32<C, W>::NTH)) void k_stagef32(const float* 
   __syncthreads();
   for (int n = blockIdx.x; n < N; n += gridDim.x) {
     const long ib = (long)n * G::H * W * C;
-    for (int i = tid; i < G::NCH; i += G::NTH) {
+    st_fetch_image<G::NCH, G::NTH, f32x4>(x0 + ib, tid, [&](int i, const f32x4& v) {
       const int px = i / (C / 4), c4 = i % (C / 4);
-      *(f32x4*)(img0 + st32_off<C, W>(px / W, px % W) + 4 * c4) = *(const f32x4*)(x0 + ib + 4L * i);
-    }
+      *(f32x4*)(img0 + st32_off<C, W>(px / W, px % W) + 4 * c4) = v;
+    });
     __syncthreads();
     for (int l = 0; l < L; ++l) {
       const float* cur = (l & 1) ? img1 : img0;
@@ -1500,8 +1503,9 @@ __global__ __launch_bounds__((StImg32<C, W>::NTH)) void k_stageb32(const float* 
   for (int i = tid; i < G::IMGF / 4; i += G::NTH) ((f32x4*)dzt)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int n = blockIdx.x; n < N; n += gridDim.x) {
     const long ib = (long)n * G::H * W * C;
-    for (int i = tid; i < G::NCH; i += G::NTH)
-      *(f32x4*)(dyt + (i / (C / 4)) * PS + 4 * (i % (C / 4))) = *(const f32x4*)(dyL + ib + 4L * i);
+    st_fetch_image<G::NCH, G::NTH, f32x4>(dyL + ib, tid, [&](int i, const f32x4& v) {
+      *(f32x4*)(dyt + (i / (C / 4)) * PS + 4 * (i % (C / 4))) = v;
+    });
     for (int l = L - 1; l >= 0; --l) {
       // layer l's relu bytes, loaded before the barrier (a byte load per chunk inside the loop below
       // waited for each in turn)
